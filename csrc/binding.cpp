@@ -1,0 +1,381 @@
+// Python bindings for the MNIST HIP kernels (torch extension `_kernels`).
+//
+// Every entry point validates device, dtype, contiguity and that each buffer is
+// large enough for the indices the kernel will form, BEFORE launching: a
+// mis-sized operand must raise here, never fault on the GPU.  Launches go to
+// the caller's current HIP stream (so they are hipGraph-capturable and honour
+// torch.cuda.stream contexts).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include "kernels/launchers.h"
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check(const Tensor& t, at::ScalarType dt, int64_t need, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, ": must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, ": expected dtype ", dt, ", got ", t.scalar_type());
+  TORCH_CHECK(t.is_contiguous(), name, ": must be contiguous");
+  TORCH_CHECK(need >= 0 && t.numel() >= need, name, ": needs ", need, " elements, has ", t.numel());
+}
+
+int64_t span(int64_t rows, int64_t ld, int64_t cols) { return rows <= 0 ? 0 : (rows - 1) * ld + cols; }
+
+template <class T>
+T* P(const Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+const mnistx::bf16_t* BF(const Tensor& t) { return reinterpret_cast<const mnistx::bf16_t*>(t.data_ptr()); }
+mnistx::bf16_t* BFm(const Tensor& t) { return reinterpret_cast<mnistx::bf16_t*>(t.data_ptr()); }
+
+void hip_ok(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, what, " launch failed: ", hipGetErrorString(e));
+}
+
+mnistx::GemmEpi make_epi(const Tensor& out, int64_t M, int64_t N, int64_t ldc, const optional<Tensor>& bias,
+                         int64_t bias_n, bool relu, const optional<Tensor>& mask, int64_t ldm) {
+  TORCH_CHECK(ldc >= N, "ldc < N");
+  mnistx::GemmEpi ep{};
+  if (out.scalar_type() == at::kBFloat16) {
+    check(out, at::kBFloat16, span(M, ldc, N), "out");
+    ep.mode = mnistx::EPI_BF16;
+  } else {
+    check(out, at::kFloat, span(M, ldc, N), "out");
+    ep.mode = mnistx::EPI_F32;
+  }
+  ep.out = out.data_ptr();
+  ep.ldc = (int)ldc;
+  ep.bias = nullptr;
+  ep.bias_n = 0;
+  if (bias.has_value() && bias->defined()) {
+    check(*bias, at::kFloat, bias_n, "bias");
+    ep.bias = P<const float>(*bias);
+    ep.bias_n = (int)bias_n;
+  }
+  ep.relu = relu ? 1 : 0;
+  ep.mask = nullptr;
+  ep.ldm = 0;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(ldm >= N, "ldm < N");
+    check(*mask, at::kBFloat16, span(M, ldm, N), "mask");
+    ep.mask = BF(*mask);
+    ep.ldm = (int)ldm;
+  }
+  ep.slab_stride = 0;
+  return ep;
+}
+
+mnistx::GemmEpi make_slab(const Tensor& slab, int64_t splits, int64_t M, int64_t N) {
+  check(slab, at::kFloat, splits * M * N, "slab");
+  mnistx::GemmEpi ep{};
+  ep.out = slab.data_ptr();
+  ep.ldc = (int)N;
+  ep.mode = mnistx::EPI_SLAB;
+  ep.slab_stride = M * N;
+  return ep;
+}
+
+// Effective split count the launcher will use (kchunk rounded to BK=32).
+int64_t eff_splits(int64_t K, int64_t splits) {
+  if (splits < 1) splits = 1;
+  int64_t kchunk = (K + splits - 1) / splits;
+  kchunk = ((kchunk + 31) / 32) * 32;
+  if (kchunk < 32) kchunk = 32;
+  return (K + kchunk - 1) / kchunk;
+}
+
+void dense_fwd(Tensor x, Tensor w, Tensor out, int64_t M, int64_t N, int64_t K, int64_t ldx, int64_t ldw,
+               int64_t ldc, optional<Tensor> bias, int64_t bias_n, bool relu, optional<Tensor> mask, int64_t ldm) {
+  check(x, at::kBFloat16, span(M, ldx, K), "x");
+  check(w, at::kBFloat16, span(K, ldw, N), "w");
+  TORCH_CHECK(ldx >= K && ldw >= N, "bad leading dims");
+  auto ep = make_epi(out, M, N, ldc, bias, bias_n, relu, mask, ldm);
+  hip_ok(mnistx::dense_fwd(BF(x), BF(w), (int)M, (int)N, (int)K, (int)ldx, (int)ldw, ep, cur_stream()), "dense_fwd");
+}
+
+void dense_dgrad(Tensor dy, Tensor w, Tensor out, int64_t M, int64_t N, int64_t K, int64_t lddy, int64_t ldw,
+                 int64_t ldc, optional<Tensor> mask, int64_t ldm) {
+  // out[M, N=Din] = dy[M, K=Dout] . W[Din, Dout]^T
+  check(dy, at::kBFloat16, span(M, lddy, K), "dy");
+  check(w, at::kBFloat16, span(N, ldw, K), "w");
+  TORCH_CHECK(lddy >= K && ldw >= K, "bad leading dims");
+  auto ep = make_epi(out, M, N, ldc, c10::nullopt, 0, false, mask, ldm);
+  hip_ok(mnistx::dense_dgrad(BF(dy), BF(w), (int)M, (int)N, (int)K, (int)lddy, (int)ldw, ep, cur_stream()),
+         "dense_dgrad");
+}
+
+int64_t dense_wgrad(Tensor x, Tensor dy, Tensor slab, int64_t Din, int64_t Dout, int64_t B, int64_t ldx, int64_t lddy,
+                    bool with_bias, int64_t splits) {
+  check(x, at::kBFloat16, span(B, ldx, Din), "x");
+  check(dy, at::kBFloat16, span(B, lddy, Dout), "dy");
+  TORCH_CHECK(ldx >= Din && lddy >= Dout, "bad leading dims");
+  const int64_t M = Din + (with_bias ? 1 : 0);
+  const int64_t S = eff_splits(B, splits);
+  auto ep = make_slab(slab, S, M, Dout);
+  hip_ok(mnistx::dense_wgrad(BF(x), BF(dy), (int)Din, (int)Dout, (int)B, (int)ldx, (int)lddy, with_bias ? 1 : 0,
+                             (int)S, ep, cur_stream()),
+         "dense_wgrad");
+  return S;
+}
+
+void conv_fwd(Tensor x, Tensor w, Tensor out, int64_t Nb, int64_t H, int64_t W, int64_t C, int64_t OH, int64_t OW,
+              int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t Cout, optional<Tensor> bias, int64_t bias_n,
+              bool relu) {
+  check(x, at::kBFloat16, Nb * H * W * C, "x");
+  check(w, at::kBFloat16, KH * KW * C * Cout, "w");
+  TORCH_CHECK(Cout % 8 == 0, "Cout must be padded to a multiple of 8");
+  auto ep = make_epi(out, Nb * OH * OW, Cout, Cout, bias, bias_n, relu, c10::nullopt, 0);
+  hip_ok(mnistx::conv_fwd(BF(x), BF(w), (int)Nb, (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)KH, (int)KW, (int)ph,
+                          (int)pw, (int)Cout, ep, cur_stream()),
+         "conv_fwd");
+}
+
+void conv_dgrad(Tensor dy, Tensor w, Tensor out, int64_t Nb, int64_t OH, int64_t OW, int64_t Cout, int64_t H,
+                int64_t W, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t Cin, optional<Tensor> mask) {
+  check(dy, at::kBFloat16, Nb * OH * OW * Cout, "dy");
+  check(w, at::kBFloat16, KH * KW * Cin * Cout, "w");
+  TORCH_CHECK(Cout % 8 == 0 && Cin % 8 == 0, "channels must be padded to multiples of 8");
+  auto ep = make_epi(out, Nb * H * W, Cin, Cin, c10::nullopt, 0, false, mask, Cin);
+  hip_ok(mnistx::conv_dgrad(BF(dy), BF(w), (int)Nb, (int)OH, (int)OW, (int)Cout, (int)H, (int)W, (int)KH, (int)KW,
+                            (int)ph, (int)pw, (int)Cin, ep, cur_stream()),
+         "conv_dgrad");
+}
+
+int64_t conv_wgrad(Tensor x, Tensor dy, Tensor slab, int64_t Nb, int64_t H, int64_t W, int64_t C, int64_t OH,
+                   int64_t OW, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t Cout, bool with_bias,
+                   int64_t splits) {
+  check(x, at::kBFloat16, Nb * H * W * C, "x");
+  check(dy, at::kBFloat16, Nb * OH * OW * Cout, "dy");
+  TORCH_CHECK(Cout % 8 == 0, "Cout must be padded to a multiple of 8");
+  const int64_t M = KH * KW * C + (with_bias ? 1 : 0);
+  const int64_t S = eff_splits(Nb * OH * OW, splits);
+  auto ep = make_slab(slab, S, M, Cout);
+  hip_ok(mnistx::conv_wgrad(BF(x), BF(dy), (int)Nb, (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)KH, (int)KW,
+                            (int)ph, (int)pw, (int)Cout, with_bias ? 1 : 0, (int)S, ep, cur_stream()),
+         "conv_wgrad");
+  return S;
+}
+
+void prep_images(Tensor src, Tensor idx, Tensor lab_src, Tensor out, Tensor lab_out, int64_t HW, int64_t Csrc,
+                 int64_t Cdst) {
+  const int64_t B = idx.numel();
+  TORCH_CHECK((HW * Cdst) % 8 == 0, "HW*C must be a multiple of 8");
+  check(idx, at::kLong, B, "idx");
+  TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kByte && src.is_contiguous(), "src: uint8 GPU tensor");
+  TORCH_CHECK(src.numel() % (HW * Csrc) == 0, "src size");
+  check(lab_src, at::kInt, src.numel() / (HW * Csrc), "lab_src");
+  check(out, at::kBFloat16, B * HW * Cdst, "out");
+  check(lab_out, at::kInt, B, "lab_out");
+  hip_ok(mnistx::prep_images(P<const uint8_t>(src), P<const int64_t>(idx), P<const int32_t>(lab_src), (int)B,
+                             (int)HW, (int)Csrc, (int)Cdst, BFm(out), P<int32_t>(lab_out), cur_stream()),
+         "prep_images");
+}
+
+void maxpool_fwd(Tensor x, Tensor y, Tensor arg, int64_t Nb, int64_t H, int64_t W, int64_t C, int64_t OH,
+                 int64_t OW) {
+  TORCH_CHECK(C % 8 == 0, "C must be a multiple of 8");
+  TORCH_CHECK(OH == (H + 1) / 2 && OW == (W + 1) / 2, "2x2/2 SAME pooling shape");
+  check(x, at::kBFloat16, Nb * H * W * C, "x");
+  check(y, at::kBFloat16, Nb * OH * OW * C, "y");
+  check(arg, at::kByte, Nb * OH * OW * C, "arg");
+  hip_ok(mnistx::maxpool_fwd(BF(x), (int)Nb, (int)H, (int)W, (int)C, (int)OH, (int)OW, BFm(y), P<uint8_t>(arg),
+                             cur_stream()),
+         "maxpool_fwd");
+}
+
+void maxpool_bwd(Tensor dy, Tensor arg, Tensor y, bool relu_mask, Tensor dx, int64_t Nb, int64_t H, int64_t W,
+                 int64_t C, int64_t OH, int64_t OW) {
+  TORCH_CHECK(C % 8 == 0, "C must be a multiple of 8");
+  TORCH_CHECK(OH == (H + 1) / 2 && OW == (W + 1) / 2, "2x2/2 SAME pooling shape");
+  check(dy, at::kBFloat16, Nb * OH * OW * C, "dy");
+  check(arg, at::kByte, Nb * OH * OW * C, "arg");
+  check(y, at::kBFloat16, Nb * OH * OW * C, "y");
+  check(dx, at::kBFloat16, Nb * H * W * C, "dx");
+  hip_ok(mnistx::maxpool_bwd(BF(dy), P<const uint8_t>(arg), BF(y), relu_mask ? 1 : 0, (int)Nb, (int)H, (int)W,
+                             (int)C, (int)OH, (int)OW, BFm(dx), cur_stream()),
+         "maxpool_bwd");
+}
+
+void lrn_fwd(Tensor x, Tensor y, int64_t P_, int64_t C, int64_t r, double bias, double alpha, double beta) {
+  check(x, at::kBFloat16, P_ * C, "x");
+  check(y, at::kBFloat16, P_ * C, "y");
+  hip_ok(mnistx::lrn_fwd(BF(x), (int)P_, (int)C, (int)r, (float)bias, (float)alpha, (float)beta, BFm(y),
+                         cur_stream()),
+         "lrn_fwd");
+}
+
+void lrn_bwd(Tensor x, Tensor dy, Tensor dx, int64_t P_, int64_t C, int64_t r, double bias, double alpha,
+             double beta, bool relu_mask) {
+  check(x, at::kBFloat16, P_ * C, "x");
+  check(dy, at::kBFloat16, P_ * C, "dy");
+  check(dx, at::kBFloat16, P_ * C, "dx");
+  hip_ok(mnistx::lrn_bwd(BF(x), BF(dy), (int)P_, (int)C, (int)r, (float)bias, (float)alpha, (float)beta,
+                         relu_mask ? 1 : 0, BFm(dx), cur_stream()),
+         "lrn_bwd");
+}
+
+void softmax_ce(Tensor logits, int64_t ldl, optional<Tensor> labels, int64_t B, int64_t NC, double scale,
+                optional<Tensor> dlogits, int64_t ldd, optional<Tensor> stats, optional<Tensor> probs) {
+  TORCH_CHECK(ldl >= NC, "ldl < NC");
+  check(logits, at::kFloat, span(B, ldl, NC), "logits");
+  const int32_t* lab = nullptr;
+  if (labels.has_value() && labels->defined()) {
+    check(*labels, at::kInt, B, "labels");
+    lab = P<const int32_t>(*labels);
+  }
+  mnistx::bf16_t* dl = nullptr;
+  if (dlogits.has_value() && dlogits->defined()) {
+    TORCH_CHECK(lab != nullptr, "dlogits needs labels");
+    TORCH_CHECK(ldd >= NC, "ldd < NC");
+    check(*dlogits, at::kBFloat16, B * ldd, "dlogits");
+    dl = BFm(*dlogits);
+  }
+  float* st = nullptr;
+  if (stats.has_value() && stats->defined()) {
+    check(*stats, at::kFloat, 8, "stats");
+    st = P<float>(*stats);
+  }
+  float* pr = nullptr;
+  if (probs.has_value() && probs->defined()) {
+    check(*probs, at::kFloat, B * NC, "probs");
+    pr = P<float>(*probs);
+  }
+  hip_ok(mnistx::softmax_ce(P<const float>(logits), (int)ldl, lab, (int)B, (int)NC, (float)scale, dl, (int)ldd, st, pr,
+                            cur_stream()),
+         "softmax_ce");
+}
+
+void splitk_reduce(Tensor slab, int64_t splits, int64_t M, int64_t N, int64_t G, int64_t Ipad, int64_t I, int64_t J,
+                   int64_t bias_row, Tensor wdst, optional<Tensor> bdst, double scale) {
+  check(slab, at::kFloat, splits * M * N, "slab");
+  TORCH_CHECK(I <= Ipad && J <= N && G * Ipad <= M, "reduce geometry");
+  check(wdst, at::kFloat, G * I * J, "wdst");
+  float* b = nullptr;
+  if (bdst.has_value() && bdst->defined()) {
+    TORCH_CHECK(bias_row >= 0 && bias_row < M, "bias_row");
+    check(*bdst, at::kFloat, J, "bdst");
+    b = P<float>(*bdst);
+  }
+  hip_ok(mnistx::splitk_reduce(P<const float>(slab), (int)splits, (int)M, (int)N, (int)G, (int)Ipad, (int)I, (int)J,
+                               (int)bias_row, P<float>(wdst), b, (float)scale, cur_stream()),
+         "splitk_reduce");
+}
+
+// segs: int64 tensor [nseg, 12] on CPU:
+//   off, n, G, I, J, Ip, Jp, bf_off, wd_bits(float32 as int), track_l2, 0, 0
+void fused_optimizer(Tensor params, Tensor grads, Tensor mom, Tensor ema, Tensor bf, Tensor segs, Tensor step,
+                     double lr0, double decay_rate, int64_t decay_steps, double momentum, bool nesterov,
+                     bool use_momentum, double grad_scale, double ema_max, optional<Tensor> l2) {
+  const int64_t total = params.numel();
+  check(params, at::kFloat, total, "params");
+  check(grads, at::kFloat, total, "grads");
+  if (use_momentum) check(mom, at::kFloat, total, "mom");
+  if (ema_max >= 0) check(ema, at::kFloat, total, "ema");
+  check(step, at::kLong, 1, "step");
+  TORCH_CHECK(!segs.is_cuda() && segs.scalar_type() == at::kLong && segs.dim() == 2 && segs.size(1) == 12,
+              "segs: CPU int64 [n,12]");
+  const int nseg = (int)segs.size(0);
+  std::vector<mnistx::OptSeg> sv(nseg);
+  auto a = segs.accessor<int64_t, 2>();
+  int64_t expect_off = 0;
+  int max_l2 = 0;
+  for (int i = 0; i < nseg; ++i) {
+    auto& s = sv[i];
+    s.off = a[i][0];
+    s.n = a[i][1];
+    s.G = (int)a[i][2];
+    s.I = (int)a[i][3];
+    s.J = (int)a[i][4];
+    s.Ip = (int)a[i][5];
+    s.Jp = (int)a[i][6];
+    s.bf_off = a[i][7];
+    int32_t wb = (int32_t)a[i][8];
+    std::memcpy(&s.wd, &wb, 4);
+    s.track_l2 = (int)a[i][9];
+    TORCH_CHECK(s.off == expect_off, "segments must tile the flat buffer in order");
+    TORCH_CHECK(s.n == (int64_t)s.G * s.I * s.J, "segment size mismatch");
+    TORCH_CHECK(s.Ip >= s.I && s.Jp >= s.J, "padding");
+    if (s.bf_off >= 0)
+      TORCH_CHECK(s.bf_off + (int64_t)s.G * s.Ip * s.Jp <= bf.numel(), "bf16 copy out of range");
+    if (s.track_l2 > max_l2) max_l2 = s.track_l2;
+    expect_off += s.n;
+  }
+  TORCH_CHECK(expect_off == total, "segments do not cover the parameters");
+  check(bf, at::kBFloat16, 0, "bf");
+  float* l2p = nullptr;
+  if (l2.has_value() && l2->defined()) {
+    check(*l2, at::kFloat, max_l2, "l2");
+    l2p = P<float>(*l2);
+  }
+  mnistx::OptParams op{};
+  op.lr0 = (float)lr0;
+  op.decay_rate = (float)decay_rate;
+  op.decay_steps = decay_steps;
+  op.momentum = (float)momentum;
+  op.nesterov = nesterov ? 1 : 0;
+  op.use_momentum = use_momentum ? 1 : 0;
+  op.grad_scale = (float)grad_scale;
+  op.ema_max = (float)ema_max;
+  hip_ok(mnistx::fused_optimizer(P<float>(params), P<const float>(grads), use_momentum ? P<float>(mom) : nullptr,
+                                 ema_max >= 0 ? P<float>(ema) : nullptr, BFm(bf), sv.data(), nseg, total,
+                                 P<const int64_t>(step), op, l2p, cur_stream()),
+         "fused_optimizer");
+}
+
+void finalize_step(Tensor step, Tensor stats, optional<Tensor> l2, optional<Tensor> wds, int64_t nw,
+                   optional<Tensor> loss_ema, int64_t n_ema, int64_t batch, bool increment) {
+  check(step, at::kLong, 1, "step");
+  check(stats, at::kFloat, 8, "stats");
+  const float* l2p = nullptr;
+  const float* wp = nullptr;
+  if (nw > 0) {
+    TORCH_CHECK(l2.has_value() && wds.has_value(), "l2/wds needed when nw > 0");
+    check(*l2, at::kFloat, nw, "l2");
+    check(*wds, at::kFloat, nw, "wds");
+    l2p = P<const float>(*l2);
+    wp = P<const float>(*wds);
+  }
+  float* le = nullptr;
+  if (loss_ema.has_value() && loss_ema->defined()) {
+    check(*loss_ema, at::kFloat, 3 * n_ema, "loss_ema");
+    le = P<float>(*loss_ema);
+  }
+  hip_ok(mnistx::finalize_step(P<int64_t>(step), P<float>(stats), l2p, wp, (int)nw, le, le ? (int)n_ema : 0,
+                               (int)batch, increment ? 1 : 0, cur_stream()),
+         "finalize_step");
+}
+
+void cast_f32_bf16_padded(Tensor src, Tensor dst, int64_t G, int64_t I, int64_t J, int64_t Ip, int64_t Jp) {
+  check(src, at::kFloat, G * I * J, "src");
+  check(dst, at::kBFloat16, G * Ip * Jp, "dst");
+  TORCH_CHECK(Ip >= I && Jp >= J, "padding");
+  hip_ok(mnistx::cast_f32_bf16_padded(P<const float>(src), BFm(dst), (int)G, (int)I, (int)J, (int)Ip, (int)Jp,
+                                      cur_stream()),
+         "cast_f32_bf16_padded");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_kernels, m) {
+  m.doc() = "MI355X (gfx950) HIP kernels for the MNIST trainer";
+  m.def("dense_fwd", &dense_fwd);
+  m.def("dense_dgrad", &dense_dgrad);
+  m.def("dense_wgrad", &dense_wgrad);
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("prep_images", &prep_images);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("lrn_fwd", &lrn_fwd);
+  m.def("lrn_bwd", &lrn_bwd);
+  m.def("softmax_ce", &softmax_ce);
+  m.def("splitk_reduce", &splitk_reduce);
+  m.def("fused_optimizer", &fused_optimizer);
+  m.def("finalize_step", &finalize_step);
+  m.def("cast_f32_bf16_padded", &cast_f32_bf16_padded);
+  m.attr("ARCH") = "gfx950";
+}

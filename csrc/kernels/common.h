@@ -1,0 +1,61 @@
+// Common CDNA4 (gfx950) helpers for the MNIST kernels.
+// Wave = 64 lanes; MFMA operands are bf16x8 fragments, fp32 accumulators.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DEV __device__ __forceinline__
+
+typedef uint16_t bf16_t;  // raw bf16 storage in global memory / LDS
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+DEV float bf2f(uint32_t v) { return __uint_as_float(v << 16); }
+
+// Round-to-nearest-even f32 -> bf16 (NaN stays NaN: hipcc emits v_cvt_pk_bf16_f32).
+DEV bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+DEV uint32_t pack2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// 8 bf16 in a 16-byte vector: element j lives in word j/2, half j%2.
+DEV float u4_get(const u32x4& v, int j) {
+  uint32_t w = v[j >> 1];
+  return (j & 1) ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(w << 16);
+}
+
+DEV void u4_set(u32x4& v, int j, bf16_t x) {
+  uint32_t w = v[j >> 1];
+  w = (j & 1) ? ((w & 0x0000ffffu) | ((uint32_t)x << 16)) : ((w & 0xffff0000u) | x);
+  v[j >> 1] = w;
+}
+
+DEV float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+DEV int warp_sum_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Bijective XCD-aware block-id remap (guide §5 "XCD swizzle must be bijective"):
+// consecutive *logical* tiles land on one XCD so they share its L2.
+DEV int xcd_remap(int bid, int nwg) {
+  const int NX = 8;
+  if (nwg <= NX) return bid;
+  int xcd = bid % NX, loc = bid / NX;
+  int q = nwg / NX, r = nwg % NX;
+  int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + loc;
+}

@@ -1,0 +1,429 @@
+// MFMA GEMM engine for gfx950 (CDNA4) — dense layers and implicit-GEMM convolutions.
+//
+// One templated kernel computes C[M,N] = sum_k A(m,k) B(k,n) with bf16 operands
+// on v_mfma_f32_16x16x32_bf16 (fp32 accumulate).  Operands come through
+// "loaders" that produce 16-byte (8 x bf16) vectors along the operand's
+// contiguous memory direction, so the same engine serves
+//   * dense fwd / dgrad / wgrad      (MatLoader in either orientation)
+//   * conv fwd / dgrad (implicit im2col along K, Im2colK, WFlipK)
+//   * conv wgrad (im2col transposed: pixels are the reduction dim, Im2colMN)
+// without materialising im2col or transposes in HBM.
+//
+// LDS images keep the operand in its *memory* orientation:
+//   K-contiguous image  [rows = m|n][BK]   -> fragment by 2 x ds_read_b64
+//   MN-contiguous image [BK][cols = m|n]   -> fragment by 2 x ds_read_b64_tr_b16
+// The fragment k-slot order is permuted identically for A and B
+// (lane group g, element j -> k = 4g + (j&3) + 16(j>>2)), which makes the
+// transposed reads bank-conflict-free with an odd-multiple-of-32B row stride
+// (a plain 8g+j order puts rows r and r+8 of one 32-lane half on the same banks).
+//
+// Staging: register double-buffered (global -> VGPR for tile t+1 while the MFMAs
+// of tile t run from LDS), one barrier per K step; split-K over blockIdx.y for
+// the huge-K weight-gradient reductions (deterministic fp32 slabs, reduced by
+// splitk_reduce in misc.hip).  Tiles are mapped XCD-aware (common.h).
+//
+// Replaces the reference's TF Conv2D / Conv2DBackprop* / MatMul kernels
+// (call sites mnist_input.py:142,161,184,192,205).
+#include "common.h"
+#include "launchers.h"
+
+namespace mnistx {
+namespace {
+
+constexpr int BK = 32;
+
+// Row stride (elements) of an LDS image whose contiguous extent is COLS.
+template <int COLS, bool KC>
+struct ImgStride {
+  static constexpr int value = KC ? (COLS + 8) : (((COLS / 16) % 2 == 0) ? COLS + 16 : COLS);
+};
+
+// ---------------------------------------------------------------- loaders
+// load(r, c): 8 bf16 at memory coordinates (row r, cols c..c+7); zero outside.
+
+struct MatLoader {
+  const bf16_t* p;
+  int R, C, ld;
+  int ones_col;  // virtual column holding 1.0 (bias-gradient row), -1 = none
+  DEV u32x4 load(int r, int c) const {
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (r >= R) return v;
+    const bf16_t* row = p + (int64_t)r * ld;
+    if (c + 8 <= C && (ld & 7) == 0) {
+      v = *(const u32x4*)(row + c);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (c + j < C) u4_set(v, j, row[c + j]);
+    }
+    if (ones_col >= c && ones_col < c + 8) u4_set(v, ones_col - c, (bf16_t)0x3f80);
+    return v;
+  }
+};
+
+// Implicit im2col, K-contiguous: row m = output pixel (n, oh, ow), col k = (kh, kw, ci).
+struct Im2colK {
+  const bf16_t* x;
+  int H, W, C;          // input NHWC (C = channel stride)
+  int OH, OW;           // output spatial
+  int KH, KW, ph, pw;   // stride 1
+  int M, K;
+  DEV u32x4 load(int m, int k) const {
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (m >= M || k >= K) return v;
+    const int ohw = OH * OW;
+    const int n = m / ohw;
+    const int rem = m - n * ohw;
+    const int oh = rem / OW;
+    const int ow = rem - oh * OW;
+    if ((C & 7) == 0) {
+      const int tap = k / C;
+      const int ci = k - tap * C;
+      const int kh = tap / KW;
+      const int kw = tap - kh * KW;
+      const int ih = oh - ph + kh, iw = ow - pw + kw;
+      if (ih < 0 || ih >= H || iw < 0 || iw >= W) return v;
+      return *(const u32x4*)(x + (((int64_t)n * H + ih) * W + iw) * C + ci);
+    }
+    const bf16_t* img = x + (int64_t)n * H * W * C;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kk = k + j;
+      if (kk < K) {
+        const int tap = kk / C;
+        const int ci = kk - tap * C;
+        const int kh = tap / KW;
+        const int kw = tap - kh * KW;
+        const int ih = oh - ph + kh, iw = ow - pw + kw;
+        if (ih >= 0 && ih < H && iw >= 0 && iw < W) u4_set(v, j, img[((int64_t)ih * W + iw) * C + ci]);
+      }
+    }
+    return v;
+  }
+};
+
+// Implicit im2col, MN-contiguous (conv weight gradient): row = pixel p (reduction),
+// col = m = (kh, kw, ci); column Mreal is a virtual 1.0 (bias gradient).
+struct Im2colMN {
+  const bf16_t* x;
+  int H, W, C;
+  int OH, OW;
+  int KH, KW, ph, pw;
+  int P, Mreal;
+  int ones;  // 1: append the ones column at Mreal
+  DEV u32x4 load(int p, int m) const {
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (p >= P) return v;
+    const int ohw = OH * OW;
+    const int n = p / ohw;
+    const int rem = p - n * ohw;
+    const int oh = rem / OW;
+    const int ow = rem - oh * OW;
+    if ((C & 7) == 0 && m + 8 <= Mreal) {
+      const int tap = m / C;
+      const int ci = m - tap * C;
+      const int kh = tap / KW;
+      const int kw = tap - kh * KW;
+      const int ih = oh - ph + kh, iw = ow - pw + kw;
+      if (ih >= 0 && ih < H && iw >= 0 && iw < W)
+        v = *(const u32x4*)(x + (((int64_t)n * H + ih) * W + iw) * C + ci);
+    } else {
+      const bf16_t* img = x + (int64_t)n * H * W * C;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int mm = m + j;
+        if (mm < Mreal) {
+          const int tap = mm / C;
+          const int ci = mm - tap * C;
+          const int kh = tap / KW;
+          const int kw = tap - kh * KW;
+          const int ih = oh - ph + kh, iw = ow - pw + kw;
+          if (ih >= 0 && ih < H && iw >= 0 && iw < W) u4_set(v, j, img[((int64_t)ih * W + iw) * C + ci]);
+        }
+      }
+    }
+    if (ones && Mreal >= m && Mreal < m + 8) u4_set(v, Mreal - m, (bf16_t)0x3f80);
+    return v;
+  }
+};
+
+// Conv data-gradient B operand, K-contiguous: row = ci (fwd input channel),
+// col k = (tap', co); value W[KH*KW-1-tap'][ci][co]  (180-degree filter flip).
+struct WFlipK {
+  const bf16_t* w;  // [T][Cin_p][Cout_p]
+  int T, Cin, Cout;
+  DEV u32x4 load(int ci, int k) const {
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (ci >= Cin || k >= T * Cout) return v;
+    const int tp = k / Cout;
+    const int co = k - tp * Cout;
+    const int tap = T - 1 - tp;
+    return *(const u32x4*)(w + ((int64_t)tap * Cin + ci) * Cout + co);
+  }
+};
+
+// ---------------------------------------------------------------- fragment reads
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+DEV bf16x8 join(s16x4 lo, s16x4 hi) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+// K-contiguous image [rows][S]: lane i=l&15 row r0+i, k = kb + 4g + {0..3} and +16.
+template <int S>
+DEV bf16x8 frag_kc(const bf16_t* img, int r0, int kb, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const bf16_t* p = img + (r0 + i) * S + kb + 4 * g;
+  s16x4 lo = *(const s16x4*)p;
+  s16x4 hi = *(const s16x4*)(p + 16);
+  return join(lo, hi);
+}
+
+// MN-contiguous image [BK][S]: transposed read of 4-row x 16-col blocks.
+template <int S>
+DEV bf16x8 frag_tr(const bf16_t* img, int c0, int kb, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const bf16_t* a0 = img + (kb + 4 * g + q) * S + c0 + 4 * p;
+  const bf16_t* a1 = a0 + 16 * S;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+  return join(lo, hi);
+}
+
+// ---------------------------------------------------------------- kernel
+template <int BM, int BN, int WM, int WN, class LA, bool AKC, class LB, bool BKC>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEpi ep, int M, int N, int K,
+                                                            int kchunk, int tiles_n) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  static_assert(FM >= 1 && FN >= 1, "wave tile too small");
+  constexpr int SA = ImgStride<AKC ? BK : BM, AKC>::value;
+  constexpr int SB = ImgStride<BKC ? BK : BN, BKC>::value;
+  constexpr int A_ELEMS = AKC ? BM * SA : BK * SA;
+  constexpr int B_ELEMS = BKC ? BN * SB : BK * SB;
+  constexpr int A_VEC = BM * BK / 8, B_VEC = BN * BK / 8;
+  constexpr int A_VPT = (A_VEC + NT - 1) / NT, B_VPT = (B_VEC + NT - 1) / NT;
+
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (A_ELEMS + B_ELEMS)];
+  // buffer b of A / B (computed, not a pointer table: a local array of LDS
+  // addresses is lowered as a static initializer hipcc cannot emit)
+#define As(b) (smem + (b) * A_ELEMS)
+#define Bs(b) (smem + 2 * A_ELEMS + (b) * B_ELEMS)
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  const int tiles_mn = gridDim.x;
+  const int t = xcd_remap(blockIdx.x, tiles_mn);
+  const int m0 = (t / tiles_n) * BM;
+  const int n0 = (t % tiles_n) * BN;
+  const int kbeg = blockIdx.y * kchunk;
+  const int kend = min(K, kbeg + kchunk);
+  const int nsteps = (kend - kbeg + BK - 1) / BK;
+
+  u32x4 ra[A_VPT], rb[B_VPT];
+
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < A_VPT; ++u) {
+      const int v = tid + u * NT;
+      if (v < A_VEC) {
+        if (AKC) {
+          const int r = v / (BK / 8), c = (v % (BK / 8)) * 8;
+          ra[u] = (k0 + c < kend) ? la.load(m0 + r, k0 + c) : u32x4{0u, 0u, 0u, 0u};
+        } else {
+          const int r = v / (BM / 8), c = (v % (BM / 8)) * 8;
+          ra[u] = (k0 + r < kend) ? la.load(k0 + r, m0 + c) : u32x4{0u, 0u, 0u, 0u};
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < B_VPT; ++u) {
+      const int v = tid + u * NT;
+      if (v < B_VEC) {
+        if (BKC) {
+          const int r = v / (BK / 8), c = (v % (BK / 8)) * 8;
+          rb[u] = (k0 + c < kend) ? lb.load(n0 + r, k0 + c) : u32x4{0u, 0u, 0u, 0u};
+        } else {
+          const int r = v / (BN / 8), c = (v % (BN / 8)) * 8;
+          rb[u] = (k0 + r < kend) ? lb.load(k0 + r, n0 + c) : u32x4{0u, 0u, 0u, 0u};
+        }
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < A_VPT; ++u) {
+      const int v = tid + u * NT;
+      if (v < A_VEC) {
+        int off;
+        if (AKC) off = (v / (BK / 8)) * SA + (v % (BK / 8)) * 8;
+        else off = (v / (BM / 8)) * SA + (v % (BM / 8)) * 8;
+        *(u32x4*)(As(buf) + off) = ra[u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < B_VPT; ++u) {
+      const int v = tid + u * NT;
+      if (v < B_VEC) {
+        int off;
+        if (BKC) off = (v / (BK / 8)) * SB + (v % (BK / 8)) * 8;
+        else off = (v / (BN / 8)) * SB + (v % (BN / 8)) * 8;
+        *(u32x4*)(Bs(buf) + off) = rb[u];
+      }
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nsteps > 0) {
+    gload(kbeg);
+    sstore(0);
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+      const int cur = s & 1;
+      if (s + 1 < nsteps) gload(kbeg + (s + 1) * BK);
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r0 = wm * TM + i * 16;
+        af[i] = AKC ? frag_kc<SA>(As(cur), r0, 0, lane) : frag_tr<SA>(As(cur), r0, 0, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c0 = wn * TN + j * 16;
+        bfr[j] = BKC ? frag_kc<SB>(Bs(cur), c0, 0, lane) : frag_tr<SB>(Bs(cur), c0, 0, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if (s + 1 < nsteps) sstore(cur ^ 1);
+      __syncthreads();
+    }
+  }
+
+#undef As
+#undef Bs
+  // ---- epilogue: lane holds D[4g + r][i] of each 16x16 tile
+  const int g = lane >> 4, li = lane & 15;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * TN + j * 16 + li;
+      if (n >= N) continue;
+      float bias = 0.f;
+      if (ep.bias && n < ep.bias_n) bias = ep.bias[n];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * TM + i * 16 + 4 * g + r;
+        if (m >= M) continue;
+        float v = acc[i][j][r];
+        if (ep.mode == EPI_SLAB) {
+          float* o = (float*)ep.out + (int64_t)blockIdx.y * ep.slab_stride;
+          o[(int64_t)m * ep.ldc + n] = v;
+          continue;
+        }
+        v += bias;
+        if (ep.relu) v = fmaxf(v, 0.f);
+        if (ep.mask && !(bf2f(ep.mask[(int64_t)m * ep.ldm + n]) > 0.f)) v = 0.f;
+        if (ep.mode == EPI_F32) ((float*)ep.out)[(int64_t)m * ep.ldc + n] = v;
+        else ((bf16_t*)ep.out)[(int64_t)m * ep.ldc + n] = f2bf(v);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- dispatch
+template <int BM, int BN, int WM, int WN, class LA, bool AKC, class LB, bool BKC>
+hipError_t launch_cfg(const LA& la, const LB& lb, const GemmEpi& ep, int M, int N, int K, int splits,
+                      hipStream_t st) {
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  if (splits < 1) splits = 1;
+  int kchunk = (K + splits - 1) / splits;
+  kchunk = ((kchunk + BK - 1) / BK) * BK;
+  splits = (K + kchunk - 1) / kchunk;
+  if (splits < 1) splits = 1;
+  dim3 grid(tm * tn, splits);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, LA, AKC, LB, BKC>), grid, dim3(64 * WM * WN), 0, st, la, lb, ep,
+                     M, N, K, kchunk, tn);
+  return hipGetLastError();
+}
+
+// Tile selection by output width N (narrow N = conv channels; wide N = dense).
+template <class LA, bool AKC, class LB, bool BKC>
+hipError_t launch_any(const LA& la, const LB& lb, const GemmEpi& ep, int M, int N, int K, int splits,
+                      hipStream_t st) {
+  if (N <= 16) return launch_cfg<256, 16, 4, 1, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+  if (N <= 32) return launch_cfg<256, 32, 4, 1, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+  if (N <= 64) return launch_cfg<128, 64, 2, 2, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+  if (M <= 64) return launch_cfg<64, 128, 1, 4, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+  return launch_cfg<128, 128, 2, 2, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- public launchers
+hipError_t dense_fwd(const bf16_t* x, const bf16_t* w, int M, int N, int K, int ldx, int ldw,
+                     const GemmEpi& ep, hipStream_t st) {
+  MatLoader a{x, M, K, ldx, -1};
+  MatLoader b{w, K, N, ldw, -1};
+  return launch_any<MatLoader, true, MatLoader, false>(a, b, ep, M, N, K, 1, st);
+}
+
+hipError_t dense_dgrad(const bf16_t* dy, const bf16_t* w, int M, int N, int K, int lddy, int ldw,
+                       const GemmEpi& ep, hipStream_t st) {
+  // dX[M, N=Din] = dY[M, K=Dout] . W[Din, Dout]^T  ; B(k, n) = W[n][k]  (K-contiguous rows n)
+  MatLoader a{dy, M, K, lddy, -1};
+  MatLoader b{w, N, K, ldw, -1};
+  return launch_any<MatLoader, true, MatLoader, true>(a, b, ep, M, N, K, 1, st);
+}
+
+hipError_t dense_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int B, int ldx, int lddy,
+                       int with_bias, int splits, const GemmEpi& ep, hipStream_t st) {
+  // slab[Din(+1), Dout] = X^T dY ; A(m=din, k=b) = X[b][din] ; B(k=b, n) = dY[b][n]
+  MatLoader a{x, B, Din, ldx, with_bias ? Din : -1};
+  MatLoader b{dy, B, Dout, lddy, -1};
+  const int M = Din + (with_bias ? 1 : 0);
+  return launch_any<MatLoader, false, MatLoader, false>(a, b, ep, M, Dout, B, splits, st);
+}
+
+hipError_t conv_fwd(const bf16_t* x, const bf16_t* w, int Nb, int H, int W, int C, int OH, int OW, int KH,
+                    int KW, int ph, int pw, int Cout, const GemmEpi& ep, hipStream_t st) {
+  const int M = Nb * OH * OW, K = KH * KW * C;
+  Im2colK a{x, H, W, C, OH, OW, KH, KW, ph, pw, M, K};
+  MatLoader b{w, K, Cout, Cout, -1};
+  return launch_any<Im2colK, true, MatLoader, false>(a, b, ep, M, Cout, K, 1, st);
+}
+
+hipError_t conv_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int OH, int OW, int Cout, int H, int W,
+                      int KH, int KW, int ph, int pw, int Cin, const GemmEpi& ep, hipStream_t st) {
+  // dX = conv(dY, flip(W)^T) with pad' = K-1-pad, over the dY image.
+  const int M = Nb * H * W, K = KH * KW * Cout;
+  Im2colK a{dy, OH, OW, Cout, H, W, KH, KW, KH - 1 - ph, KW - 1 - pw, M, K};
+  WFlipK b{w, KH * KW, Cin, Cout};
+  return launch_any<Im2colK, true, WFlipK, true>(a, b, ep, M, Cin, K, 1, st);
+}
+
+hipError_t conv_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int H, int W, int C, int OH, int OW, int KH,
+                      int KW, int ph, int pw, int Cout, int with_bias, int splits, const GemmEpi& ep,
+                      hipStream_t st) {
+  const int P = Nb * OH * OW, Mreal = KH * KW * C;
+  Im2colMN a{x, H, W, C, OH, OW, KH, KW, ph, pw, P, Mreal, with_bias};
+  MatLoader b{dy, P, Cout, Cout, -1};
+  return launch_any<Im2colMN, false, MatLoader, false>(a, b, ep, Mreal + (with_bias ? 1 : 0), Cout, P, splits,
+                                                       st);
+}
+
+}  // namespace mnistx

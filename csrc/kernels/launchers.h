@@ -1,0 +1,84 @@
+// Host-callable launchers for the MNIST HIP kernels (no torch dependency).
+// All pointers are device pointers; every launcher is asynchronous on `st`
+// and graph-capturable (no allocation, no synchronisation).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mnistx {
+
+typedef uint16_t bf16_t;
+
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_SLAB = 2 };
+
+struct GemmEpi {
+  void* out;              // bf16 / f32 output, or f32 split-K slab base
+  int ldc;                // output row stride (elements)
+  int mode;               // EPI_*
+  const float* bias;      // fp32 bias (master weights), may be null
+  int bias_n;             // bias valid for n < bias_n (zero-padded columns beyond)
+  int relu;               // apply ReLU after bias
+  const bf16_t* mask;     // ReLU-backward mask source: keep v where mask > 0
+  int ldm;
+  int64_t slab_stride;    // elements between split-K slabs
+};
+
+// ---- gemm.hip
+hipError_t dense_fwd(const bf16_t* x, const bf16_t* w, int M, int N, int K, int ldx, int ldw,
+                     const GemmEpi& ep, hipStream_t st);
+hipError_t dense_dgrad(const bf16_t* dy, const bf16_t* w, int M, int N, int K, int lddy, int ldw,
+                       const GemmEpi& ep, hipStream_t st);
+hipError_t dense_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int B, int ldx, int lddy,
+                       int with_bias, int splits, const GemmEpi& ep, hipStream_t st);
+hipError_t conv_fwd(const bf16_t* x, const bf16_t* w, int Nb, int H, int W, int C, int OH, int OW, int KH,
+                    int KW, int ph, int pw, int Cout, const GemmEpi& ep, hipStream_t st);
+hipError_t conv_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int OH, int OW, int Cout, int H, int W,
+                      int KH, int KW, int ph, int pw, int Cin, const GemmEpi& ep, hipStream_t st);
+hipError_t conv_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int H, int W, int C, int OH, int OW, int KH,
+                      int KW, int ph, int pw, int Cout, int with_bias, int splits, const GemmEpi& ep,
+                      hipStream_t st);
+
+// ---- misc.hip
+hipError_t prep_images(const uint8_t* src, const int64_t* idx, const int32_t* lab_src, int B, int HW, int Csrc,
+                       int Cdst, bf16_t* out, int32_t* lab_out, hipStream_t st);
+hipError_t maxpool_fwd(const bf16_t* x, int Nb, int H, int W, int C, int OH, int OW, bf16_t* y, uint8_t* arg,
+                       hipStream_t st);
+hipError_t maxpool_bwd(const bf16_t* dy, const uint8_t* arg, const bf16_t* y, int relu_mask, int Nb, int H,
+                       int W, int C, int OH, int OW, bf16_t* dx, hipStream_t st);
+hipError_t lrn_fwd(const bf16_t* x, int P, int C, int r, float bias, float alpha, float beta, bf16_t* y,
+                   hipStream_t st);
+hipError_t lrn_bwd(const bf16_t* x, const bf16_t* dy, int P, int C, int r, float bias, float alpha, float beta,
+                   int relu_mask, bf16_t* dx, hipStream_t st);
+hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B, int NC, float scale,
+                      bf16_t* dlogits, int ldd, float* stats, float* probs, hipStream_t st);
+hipError_t splitk_reduce(const float* slab, int splits, int M, int N, int G, int Ipad, int I, int J,
+                         int bias_row, float* wdst, float* bdst, float scale, hipStream_t st);
+
+struct OptSeg {          // one trainable tensor inside the flat buffers
+  int64_t off;           // offset in the flat fp32 buffers
+  int64_t n;             // elements
+  int G, I, J;           // master shape [G][I][J]
+  int Ip, Jp;            // padded bf16 copy shape [G][Ip][Jp]
+  int64_t bf_off;        // offset of the bf16 copy (-1: none)
+  float wd;              // L2 weight decay (0: none)
+  int track_l2;          // accumulate sum(w^2) into l2[seg]
+};
+
+struct OptParams {
+  float lr0, decay_rate;
+  int64_t decay_steps;   // staircase exponential_decay; <=0: constant
+  float momentum;
+  int nesterov;          // 0/1
+  int use_momentum;
+  float grad_scale;      // e.g. 1/world_size
+  float ema_max;         // 0.9999 ; <0 disables EMA
+};
+
+hipError_t fused_optimizer(float* params, const float* grads, float* mom, float* ema, bf16_t* bf, const OptSeg* segs,
+                           int nseg, int64_t total, const int64_t* step, OptParams op, float* l2, hipStream_t st);
+hipError_t finalize_step(int64_t* step, float* stats, const float* l2, const float* wds, int nw, float* loss_ema,
+                         int n_ema, int batch, int increment, hipStream_t st);
+hipError_t cast_f32_bf16_padded(const float* src, bf16_t* dst, int G, int I, int J, int Ip, int Jp,
+                                hipStream_t st);
+
+}  // namespace mnistx

@@ -1,0 +1,500 @@
+// Bandwidth-bound kernels of the MNIST step on gfx950:
+//   input prep (K10), max-pool fwd/bwd (K6), LRN fwd/bwd (K7), softmax-CE (K8),
+//   split-K slab reduce (K3 tail), fused optimizer + EMA + LR schedule (K9),
+//   step finalisation (loss EMAs, global_step, NaN flag).
+// All 16-byte vectorised over 8 bf16 channels (NHWC with channels padded to 8).
+// Reference ops replaced: SURVEY.md §2.3 N6-N14 (mnist_input.py:37-39,149-172,
+// 224-231,252-267,288-290).
+#include "common.h"
+#include "launchers.h"
+
+namespace mnistx {
+namespace {
+
+constexpr int TPB = 256;
+
+inline int nblocks(int64_t n, int per_block = TPB, int cap = 1 << 20) {
+  int64_t b = (n + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  if (b > cap) b = cap;
+  return (int)b;
+}
+
+// ------------------------------------------------------------------ K10 input prep
+// out[b, p, c] = src[idx[b], p, c_src] / 255 - 0.5   (mnist_input.py:39)
+__global__ void prep_images_k(const uint8_t* __restrict__ src, const int64_t* __restrict__ idx,
+                              const int32_t* __restrict__ lab_src, int B, int HW, int Csrc, int Cdst,
+                              bf16_t* __restrict__ out, int32_t* __restrict__ lab_out) {
+  const int64_t per_img = (int64_t)HW * Cdst;  // multiple of 8 (HW = 784)
+  const int64_t nvec = (int64_t)B * per_img / 8;
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = v * 8;
+    const int64_t b = e / per_img;
+    const int64_t w = e - b * per_img;
+    const uint8_t* img = src + idx[b] * (int64_t)HW * Csrc;
+    u32x4 o;
+    if (Csrc == Cdst) {
+      const uint8_t* s = img + w;
+      uint32_t lo = *(const uint32_t*)s, hi = *(const uint32_t*)(s + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float a = (float)((lo >> (8 * j)) & 0xff) * (1.f / 255.f) - 0.5f;
+        float c = (float)((hi >> (8 * j)) & 0xff) * (1.f / 255.f) - 0.5f;
+        u4_set(o, j, f2bf(a));
+        u4_set(o, j + 4, f2bf(c));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t ww = w + j;
+        const int64_t p = ww / Cdst;
+        const int c = (int)(ww - p * Cdst);
+        const int cs = c < Csrc ? c : 0;  // 1 -> 3 channel replication
+        u4_set(o, j, f2bf((float)img[p * Csrc + cs] * (1.f / 255.f) - 0.5f));
+      }
+    }
+    *(u32x4*)(out + e) = o;
+  }
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (lab_out && t < B) lab_out[t] = lab_src[idx[t]];
+}
+
+// ------------------------------------------------------------------ K6 max-pool 2x2/2 SAME
+__global__ void maxpool_fwd_k(const bf16_t* __restrict__ x, int Nb, int H, int W, int C, int OH, int OW,
+                              bf16_t* __restrict__ y, uint8_t* __restrict__ arg) {
+  const int CV = C / 8;
+  const int64_t total = (int64_t)Nb * OH * OW * CV;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int cv = (int)(t % CV);
+    int64_t r = t / CV;
+    const int ow = (int)(r % OW);
+    r /= OW;
+    const int oh = (int)(r % OH);
+    const int n = (int)(r / OH);
+    float best[8];
+    uint32_t bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int ih = 2 * oh + (d >> 1), iw = 2 * ow + (d & 1);
+      if (ih < H && iw < W) {
+        const u32x4 v = *(const u32x4*)(x + (((int64_t)n * H + ih) * W + iw) * C + cv * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = u4_get(v, j);
+          if (f > best[j]) { best[j] = f; bi[j] = d; }
+        }
+      }
+    }
+    u32x4 o;
+    uint32_t a0 = 0, a1 = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      u4_set(o, j, f2bf(best[j]));
+      if (j < 4) a0 |= bi[j] << (8 * j);
+      else a1 |= bi[j] << (8 * (j - 4));
+    }
+    const int64_t off = (((int64_t)n * OH + oh) * OW + ow) * C + cv * 8;
+    *(u32x4*)(y + off) = o;
+    *(u32x2*)(arg + off) = u32x2{a0, a1};
+  }
+}
+
+__global__ void maxpool_bwd_k(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                              const bf16_t* __restrict__ y, int relu_mask, int Nb, int H, int W, int C, int OH,
+                              int OW, bf16_t* __restrict__ dx) {
+  const int CV = C / 8;
+  const int64_t total = (int64_t)Nb * OH * OW * CV;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int cv = (int)(t % CV);
+    int64_t r = t / CV;
+    const int ow = (int)(r % OW);
+    r /= OW;
+    const int oh = (int)(r % OH);
+    const int n = (int)(r / OH);
+    const int64_t off = (((int64_t)n * OH + oh) * OW + ow) * C + cv * 8;
+    u32x4 g = *(const u32x4*)(dy + off);
+    const u32x2 a = *(const u32x2*)(arg + off);
+    if (relu_mask) {
+      const u32x4 yv = *(const u32x4*)(y + off);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (!(u4_get(yv, j) > 0.f)) u4_set(g, j, 0);
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int ih = 2 * oh + (d >> 1), iw = 2 * ow + (d & 1);
+      if (ih < H && iw < W) {
+        u32x4 o = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t aj = ((j < 4 ? a[0] : a[1]) >> (8 * (j & 3))) & 0xff;
+          if (aj == (uint32_t)d) u4_set(o, j, (bf16_t)((g[j >> 1] >> (16 * (j & 1))) & 0xffff));
+        }
+        *(u32x4*)(dx + (((int64_t)n * H + ih) * W + iw) * C + cv * 8) = o;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ K7 LRN (TF semantics)
+// y[c] = x[c] * (bias + alpha * sum_{|c'-c|<=r} x[c']^2)^-beta
+template <int C>
+__global__ void lrn_fwd_k(const bf16_t* __restrict__ x, int64_t P, int r, float bias, float alpha, float beta,
+                          bf16_t* __restrict__ y) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < P; p += (int64_t)gridDim.x * blockDim.x) {
+    float v[C], sq[C];
+#pragma unroll
+    for (int c8 = 0; c8 < C / 8; ++c8) {
+      const u32x4 u = *(const u32x4*)(x + p * C + c8 * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { v[c8 * 8 + j] = u4_get(u, j); sq[c8 * 8 + j] = v[c8 * 8 + j] * v[c8 * 8 + j]; }
+    }
+#pragma unroll
+    for (int c8 = 0; c8 < C / 8; ++c8) {
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c8 * 8 + j;
+        float s = 0.f;
+#pragma unroll
+        for (int d = -8; d <= 8; ++d)
+          if (d >= -r && d <= r && c + d >= 0 && c + d < C) s += sq[c + d];
+        const float sc = bias + alpha * s;
+        u4_set(o, j, f2bf(v[c] * __expf(-beta * __logf(sc))));
+      }
+      *(u32x4*)(y + p * C + c8 * 8) = o;
+    }
+  }
+}
+
+// dx[c] = dy[c] s[c]^-b - 2ab x[c] sum_{|c'-c|<=r} dy[c'] x[c'] s[c']^(-b-1)
+template <int C>
+__global__ void lrn_bwd_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, int64_t P, int r, float bias,
+                          float alpha, float beta, int relu_mask, bf16_t* __restrict__ dx) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < P; p += (int64_t)gridDim.x * blockDim.x) {
+    float v[C], sq[C], t[C], pb[C];
+#pragma unroll
+    for (int c8 = 0; c8 < C / 8; ++c8) {
+      const u32x4 u = *(const u32x4*)(x + p * C + c8 * 8);
+      const u32x4 g = *(const u32x4*)(dy + p * C + c8 * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[c8 * 8 + j] = u4_get(u, j);
+        sq[c8 * 8 + j] = v[c8 * 8 + j] * v[c8 * 8 + j];
+        t[c8 * 8 + j] = u4_get(g, j);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      float s = 0.f;
+#pragma unroll
+      for (int d = -8; d <= 8; ++d)
+        if (d >= -r && d <= r && c + d >= 0 && c + d < C) s += sq[c + d];
+      const float sc = bias + alpha * s;
+      const float pw = __expf(-beta * __logf(sc));  // s^-b
+      pb[c] = pw;
+      sq[c] = t[c] * v[c] * pw / sc;  // reuse: dy*x*s^(-b-1)
+    }
+#pragma unroll
+    for (int c8 = 0; c8 < C / 8; ++c8) {
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c8 * 8 + j;
+        float s = 0.f;
+#pragma unroll
+        for (int d = -8; d <= 8; ++d)
+          if (d >= -r && d <= r && c + d >= 0 && c + d < C) s += sq[c + d];
+        float g = t[c] * pb[c] - 2.f * alpha * beta * v[c] * s;
+        if (relu_mask && !(v[c] > 0.f)) g = 0.f;
+        u4_set(o, j, f2bf(g));
+      }
+      *(u32x4*)(dx + p * C + c8 * 8) = o;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ K8 softmax cross-entropy
+// stats[0] += sum(-log p[label]) ; stats[1] += #(logit[label] == max) ; stats[2] = 1 if non-finite.
+__global__ void softmax_ce_k(const float* __restrict__ logits, int ldl, const int32_t* __restrict__ labels, int B,
+                             int NC, float scale, bf16_t* __restrict__ dl, int ldd, float* __restrict__ stats,
+                             float* __restrict__ probs) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  float loss = 0.f, corr = 0.f;
+  int bad = 0;
+  if (row < B) {
+    const float* l = logits + (int64_t)row * ldl;
+    float mx = -INFINITY;
+    for (int c = 0; c < NC; ++c) mx = fmaxf(mx, l[c]);
+    float se = 0.f;
+    for (int c = 0; c < NC; ++c) se += __expf(l[c] - mx);
+    const float inv = 1.f / se;
+    const int lab = labels ? labels[row] : -1;
+    if (labels) {
+      const float ll = l[lab];
+      loss = -(ll - mx - __logf(se));
+      corr = (ll >= mx) ? 1.f : 0.f;
+      if (!isfinite(loss)) bad = 1;
+    }
+    if (dl) {
+      bf16_t* d = dl + (int64_t)row * ldd;
+      for (int c = 0; c < ldd; ++c) {
+        float g = 0.f;
+        if (c < NC) g = (__expf(l[c] - mx) * inv - (c == lab ? 1.f : 0.f)) * scale;
+        d[c] = f2bf(g);
+      }
+    }
+    if (probs)
+      for (int c = 0; c < NC; ++c) probs[(int64_t)row * NC + c] = __expf(l[c] - mx) * inv;
+  }
+  if (stats) {
+    loss = warp_sum(loss);
+    corr = warp_sum(corr);
+    bad = warp_sum_i(bad);
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&stats[0], loss);
+      atomicAdd(&stats[1], corr);
+      if (bad) stats[2] = 1.f;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ split-K reduce
+// dst weights [G][I][J] <- sum_s slab[s][g*Ipad + i][j] ; bias[j] <- sum_s slab[s][bias_row][j]
+__global__ void splitk_reduce_k(const float* __restrict__ slab, int S, int M, int N, int G, int Ipad, int I, int J,
+                                int bias_row, float* __restrict__ wdst, float* __restrict__ bdst, float scale) {
+  const int64_t nw = (int64_t)G * I * J;
+  const int64_t total = nw + (bdst ? J : 0);
+  const int64_t ss = (int64_t)M * N;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t row;
+    int j;
+    if (t < nw) {
+      j = (int)(t % J);
+      const int64_t gi = t / J;
+      const int i = (int)(gi % I);
+      const int g = (int)(gi / I);
+      row = (int64_t)g * Ipad + i;
+    } else {
+      j = (int)(t - nw);
+      row = bias_row;
+    }
+    float s = 0.f;
+    const float* p = slab + row * N + j;
+    for (int z = 0; z < S; ++z) s += p[z * ss];
+    if (t < nw) wdst[t] = s * scale;
+    else bdst[j] = s * scale;
+  }
+}
+
+// ------------------------------------------------------------------ K9 fused optimizer
+constexpr int MAXSEG = 16;
+struct SegTable {
+  OptSeg s[MAXSEG];
+  int n;
+};
+
+__global__ void fused_opt_k(float* __restrict__ params, const float* __restrict__ grads, float* __restrict__ mom,
+                            float* __restrict__ ema, bf16_t* __restrict__ bf, SegTable tab, int64_t total,
+                            const int64_t* __restrict__ step_p, OptParams op, float* __restrict__ l2) {
+  const int64_t step = *step_p;
+  float lr = op.lr0;
+  if (op.decay_steps > 0) lr *= powf(op.decay_rate, (float)(step / op.decay_steps));  // staircase
+  float ema_d = 0.f;
+  if (op.ema_max >= 0.f) ema_d = fminf(op.ema_max, (1.f + (float)step) / (10.f + (float)step));
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e - threadIdx.x < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    int si = -1;
+    float sq = 0.f;
+    if (e < total) {
+      si = 0;
+      while (si + 1 < tab.n && e >= tab.s[si + 1].off) ++si;
+      const OptSeg sg = tab.s[si];
+      float p = params[e];
+      sq = p * p;
+      float g = grads[e] * op.grad_scale + sg.wd * p;
+      float upd = g;
+      if (op.use_momentum) {
+        const float v = mom[e] * op.momentum + g;
+        mom[e] = v;
+        upd = op.nesterov ? g + op.momentum * v : v;
+      }
+      p -= lr * upd;
+      params[e] = p;
+      if (op.ema_max >= 0.f) {
+        const float s = ema[e];
+        ema[e] = s - (1.f - ema_d) * (s - p);
+      }
+      if (sg.bf_off >= 0) {
+        const int64_t li = e - sg.off;
+        const int64_t ij = (int64_t)sg.I * sg.J;
+        const int gg = (int)(li / ij);
+        const int64_t rem = li - gg * ij;
+        const int ii = (int)(rem / sg.J), jj = (int)(rem - (int64_t)ii * sg.J);
+        bf[sg.bf_off + ((int64_t)gg * sg.Ip + ii) * sg.Jp + jj] = f2bf(p);
+      }
+      if (!sg.track_l2) si = -1;
+      else si = sg.track_l2 - 1;
+    }
+    if (l2) {
+      const int s0 = __shfl(si, 0, 64);
+      if (__all(si == s0)) {
+        const float t = warp_sum(sq);
+        if ((threadIdx.x & 63) == 0 && s0 >= 0) atomicAdd(&l2[s0], t);
+      } else if (si >= 0) {
+        atomicAdd(&l2[si], sq);
+      }
+    }
+  }
+}
+
+// stats: [0] ce_sum acc [1] correct acc [2] nan flag [3] -
+//        [4] ce_mean [5] accuracy [6] total_loss [7] steps done (float)
+// loss_ema: n_ema x {biased, local_step, avg}  (TF zero-debiased EMA, decay 0.9:
+//           mnist_input.py:288-290); order = weight losses..., cross_entropy, total_loss
+__global__ void finalize_k(int64_t* step, float* stats, float* l2, const float* wds, int nw, float* loss_ema,
+                           int n_ema, int batch, int increment) {
+  if (threadIdx.x != 0) return;
+  const float ce = stats[0] / (float)batch;
+  const float acc = stats[1] / (float)batch;
+  float total = ce;
+  for (int i = 0; i < nw; ++i) {
+    const float wl = wds[i] * 0.5f * (l2 ? l2[i] : 0.f);
+    total += wl;
+    if (loss_ema && i < n_ema) {
+      float* e = loss_ema + 3 * i;
+      e[0] = 0.9f * e[0] + 0.1f * wl;
+      e[1] += 1.f;
+      e[2] = e[0] / (1.f - powf(0.9f, e[1]));
+    }
+    if (l2) l2[i] = 0.f;
+  }
+  if (loss_ema && n_ema >= nw + 2) {
+    float* e = loss_ema + 3 * nw;
+    e[0] = 0.9f * e[0] + 0.1f * ce;
+    e[1] += 1.f;
+    e[2] = e[0] / (1.f - powf(0.9f, e[1]));
+    e += 3;
+    e[0] = 0.9f * e[0] + 0.1f * total;
+    e[1] += 1.f;
+    e[2] = e[0] / (1.f - powf(0.9f, e[1]));
+  }
+  stats[4] = ce;
+  stats[5] = acc;
+  stats[6] = total;
+  stats[7] += 1.f;
+  if (!isfinite(total)) stats[2] = 1.f;
+  stats[0] = 0.f;
+  stats[1] = 0.f;
+  if (increment) *step += 1;
+}
+
+__global__ void cast_pad_k(const float* __restrict__ src, bf16_t* __restrict__ dst, int G, int I, int J, int Ip,
+                           int Jp) {
+  const int64_t total = (int64_t)G * Ip * Jp;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int jj = (int)(t % Jp);
+    const int64_t r = t / Jp;
+    const int ii = (int)(r % Ip);
+    const int gg = (int)(r / Ip);
+    float v = 0.f;
+    if (ii < I && jj < J) v = src[((int64_t)gg * I + ii) * J + jj];
+    dst[t] = f2bf(v);
+  }
+}
+
+}  // namespace
+
+hipError_t prep_images(const uint8_t* src, const int64_t* idx, const int32_t* lab_src, int B, int HW, int Csrc,
+                       int Cdst, bf16_t* out, int32_t* lab_out, hipStream_t st) {
+  const int64_t nvec = (int64_t)B * HW * Cdst / 8;
+  int nb = nblocks(nvec, TPB, 8192);
+  const int need = (B + TPB - 1) / TPB;
+  if (nb < need) nb = need;
+  hipLaunchKernelGGL(prep_images_k, dim3(nb), dim3(TPB), 0, st, src, idx, lab_src, B, HW, Csrc, Cdst, out, lab_out);
+  return hipGetLastError();
+}
+
+hipError_t maxpool_fwd(const bf16_t* x, int Nb, int H, int W, int C, int OH, int OW, bf16_t* y, uint8_t* arg,
+                       hipStream_t st) {
+  const int64_t total = (int64_t)Nb * OH * OW * (C / 8);
+  hipLaunchKernelGGL(maxpool_fwd_k, dim3(nblocks(total, TPB, 16384)), dim3(TPB), 0, st, x, Nb, H, W, C, OH, OW, y,
+                     arg);
+  return hipGetLastError();
+}
+
+hipError_t maxpool_bwd(const bf16_t* dy, const uint8_t* arg, const bf16_t* y, int relu_mask, int Nb, int H, int W,
+                       int C, int OH, int OW, bf16_t* dx, hipStream_t st) {
+  const int64_t total = (int64_t)Nb * OH * OW * (C / 8);
+  hipLaunchKernelGGL(maxpool_bwd_k, dim3(nblocks(total, TPB, 16384)), dim3(TPB), 0, st, dy, arg, y, relu_mask, Nb,
+                     H, W, C, OH, OW, dx);
+  return hipGetLastError();
+}
+
+#define LRN_DISPATCH(KER, ...)                                                                   \
+  switch (C) {                                                                                   \
+    case 8: hipLaunchKernelGGL(KER<8>, grid, dim3(TPB), 0, st, __VA_ARGS__); break;               \
+    case 16: hipLaunchKernelGGL(KER<16>, grid, dim3(TPB), 0, st, __VA_ARGS__); break;             \
+    case 32: hipLaunchKernelGGL(KER<32>, grid, dim3(TPB), 0, st, __VA_ARGS__); break;             \
+    case 64: hipLaunchKernelGGL(KER<64>, grid, dim3(TPB), 0, st, __VA_ARGS__); break;             \
+    default: return hipErrorInvalidValue;                                                        \
+  }
+
+hipError_t lrn_fwd(const bf16_t* x, int P, int C, int r, float bias, float alpha, float beta, bf16_t* y,
+                   hipStream_t st) {
+  if (r > 8) return hipErrorInvalidValue;
+  dim3 grid(nblocks(P, TPB, 16384));
+  LRN_DISPATCH(lrn_fwd_k, x, (int64_t)P, r, bias, alpha, beta, y);
+  return hipGetLastError();
+}
+
+hipError_t lrn_bwd(const bf16_t* x, const bf16_t* dy, int P, int C, int r, float bias, float alpha, float beta,
+                   int relu_mask, bf16_t* dx, hipStream_t st) {
+  if (r > 8) return hipErrorInvalidValue;
+  dim3 grid(nblocks(P, TPB, 16384));
+  LRN_DISPATCH(lrn_bwd_k, x, dy, (int64_t)P, r, bias, alpha, beta, relu_mask, dx);
+  return hipGetLastError();
+}
+
+hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B, int NC, float scale,
+                      bf16_t* dlogits, int ldd, float* stats, float* probs, hipStream_t st) {
+  hipLaunchKernelGGL(softmax_ce_k, dim3((B + TPB - 1) / TPB), dim3(TPB), 0, st, logits, ldl, labels, B, NC, scale,
+                     dlogits, ldd, stats, probs);
+  return hipGetLastError();
+}
+
+hipError_t splitk_reduce(const float* slab, int splits, int M, int N, int G, int Ipad, int I, int J, int bias_row,
+                         float* wdst, float* bdst, float scale, hipStream_t st) {
+  const int64_t total = (int64_t)G * I * J + (bdst ? J : 0);
+  hipLaunchKernelGGL(splitk_reduce_k, dim3(nblocks(total, TPB, 8192)), dim3(TPB), 0, st, slab, splits, M, N, G, Ipad,
+                     I, J, bias_row, wdst, bdst, scale);
+  return hipGetLastError();
+}
+
+hipError_t fused_optimizer(float* params, const float* grads, float* mom, float* ema, bf16_t* bf, const OptSeg* segs,
+                           int nseg, int64_t total, const int64_t* step, OptParams op, float* l2, hipStream_t st) {
+  if (nseg > MAXSEG || nseg < 1) return hipErrorInvalidValue;
+  SegTable tab;
+  for (int i = 0; i < nseg; ++i) tab.s[i] = segs[i];
+  tab.n = nseg;
+  hipLaunchKernelGGL(fused_opt_k, dim3(nblocks(total, TPB, 4096)), dim3(TPB), 0, st, params, grads, mom, ema, bf, tab,
+                     total, step, op, l2);
+  return hipGetLastError();
+}
+
+hipError_t finalize_step(int64_t* step, float* stats, const float* l2, const float* wds, int nw, float* loss_ema,
+                         int n_ema, int batch, int increment, hipStream_t st) {
+  hipLaunchKernelGGL(finalize_k, dim3(1), dim3(64), 0, st, step, stats, (float*)l2, wds, nw, loss_ema, n_ema, batch,
+                     increment);
+  return hipGetLastError();
+}
+
+hipError_t cast_f32_bf16_padded(const float* src, bf16_t* dst, int G, int I, int J, int Ip, int Jp, hipStream_t st) {
+  const int64_t total = (int64_t)G * Ip * Jp;
+  hipLaunchKernelGGL(cast_pad_k, dim3(nblocks(total, TPB, 8192)), dim3(TPB), 0, st, src, dst, G, I, J, Ip, Jp);
+  return hipGetLastError();
+}
+
+}  // namespace mnistx

@@ -1,0 +1,266 @@
+"""T3: every HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+Inputs are bf16-representable so the only differences are fp32 accumulation
+order and the final bf16 rounding of the output.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_tensorflow_ibm_mnist_amd.ops import functional as Fk
+from distributed_tensorflow_ibm_mnist_amd.models.torch_ref import lrn_tf
+
+pytestmark = pytest.mark.gpu
+
+
+def rnd(*shape, dev, scale=1.0, dtype=torch.bfloat16):
+    return (torch.randn(*shape, device=dev) * scale).to(dtype)
+
+
+def close(out, ref, rel=2e-2):
+    out = out.float()
+    ref = ref.float()
+    tol = rel * ref.abs().max().item() + 1e-6
+    err = (out - ref).abs().max().item()
+    assert err <= tol, f"max err {err:.3e} > tol {tol:.3e}"
+
+
+# ---------------------------------------------------------------- dense
+@pytest.mark.parametrize("M,N,Kd", [(128, 1024, 3136), (37, 120, 400), (5, 16, 88), (300, 192, 1024),
+                                    (64, 64, 64), (1000, 88, 120), (3, 1024, 3136)])
+@pytest.mark.parametrize("relu", [False, True])
+def test_dense_forward(dev, K, M, N, Kd, relu):
+    torch.manual_seed(0)
+    x = rnd(M, Kd, dev=dev)
+    w = rnd(Kd, N, dev=dev, scale=1 / math.sqrt(Kd))
+    b = torch.randn(N, device=dev)
+    out = Fk.dense(x, w, b, relu)
+    ref = x.float() @ w.float() + b
+    if relu:
+        ref = ref.relu()
+    close(out, ref)
+    out32 = Fk.dense(x, w, b, relu, out_dtype=torch.float32)
+    close(out32, ref, rel=1e-4)
+
+
+def test_dense_bias_padding(dev, K):
+    # bias only for the first 10 of 16 columns; padded columns must be exactly 0
+    x = rnd(50, 84, dev=dev)
+    w = torch.zeros(84, 16, device=dev)
+    w[:, :10] = torch.randn(84, 10, device=dev) * 0.1
+    w = w.to(torch.bfloat16)
+    b = torch.randn(10, device=dev)
+    out = Fk.dense(x, w, b, False, out_dtype=torch.float32, bias_n=10)
+    ref = x.float() @ w.float()
+    ref[:, :10] += b
+    close(out, ref, rel=1e-4)
+    assert out[:, 10:].abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("M,Din,Dout", [(128, 3136, 1024), (37, 400, 120), (300, 1024, 192), (50, 88, 16)])
+def test_dense_dgrad(dev, K, M, Din, Dout):
+    torch.manual_seed(1)
+    dy = rnd(M, Dout, dev=dev)
+    w = rnd(Din, Dout, dev=dev, scale=0.05)
+    mask = rnd(M, Din, dev=dev).relu().to(torch.bfloat16)
+    out = Fk.dense_dgrad(dy, w)
+    ref = dy.float() @ w.float().t()
+    close(out, ref)
+    outm = Fk.dense_dgrad(dy, w, mask=mask)
+    close(outm, ref * (mask.float() > 0))
+
+
+@pytest.mark.parametrize("B,Din,Dout,splits", [(128, 3136, 1024, None), (1000, 400, 120, None),
+                                               (777, 120, 88, 3), (64, 88, 16, 1), (4096, 1024, 192, None)])
+def test_dense_wgrad(dev, K, B, Din, Dout, splits):
+    torch.manual_seed(2)
+    x = rnd(B, Din, dev=dev)
+    dy = rnd(B, Dout, dev=dev)
+    din, dout = Din - (Din % 8 == 0 and Din > 100) * 4, Dout - 6 * (Dout == 16)  # exercise unpadding
+    dw, db = Fk.dense_wgrad(x, dy, din, dout, True, splits)
+    ref = x.float().t() @ dy.float()
+    close(dw, ref[:din, :dout], rel=1e-3)
+    close(db, dy.float().sum(0)[:dout], rel=1e-3)
+
+
+# ---------------------------------------------------------------- conv
+def conv_ref(x, w, b, padding, relu):
+    xn = x.float().permute(0, 3, 1, 2)
+    wt = w.float().permute(3, 2, 0, 1)
+    kh, kw = w.shape[:2]
+    if padding == "SAME":
+        xn = F.pad(xn, ((kw - 1) // 2, kw // 2, (kh - 1) // 2, kh // 2))
+    y = F.conv2d(xn, wt)
+    if b is not None:
+        y = y + b.view(1, -1, 1, 1)
+    if relu:
+        y = y.relu()
+    return y.permute(0, 2, 3, 1)
+
+
+CONV_CASES = [
+    # N, H, W, Cin, Cout, k, padding
+    (4, 28, 28, 1, 8, 5, "SAME"),
+    (3, 28, 28, 3, 32, 5, "SAME"),
+    (2, 14, 14, 32, 64, 5, "SAME"),
+    (5, 14, 14, 8, 16, 5, "VALID"),
+    (1, 7, 9, 16, 32, 3, "SAME"),
+]
+
+
+@pytest.mark.parametrize("N,H,W,Ci,Co,k,pad", CONV_CASES)
+def test_conv_fwd(dev, K, N, H, W, Ci, Co, k, pad):
+    torch.manual_seed(3)
+    x = rnd(N, H, W, Ci, dev=dev)
+    w = rnd(k, k, Ci, Co, dev=dev, scale=1 / math.sqrt(k * k * Ci))
+    b = torch.randn(Co, device=dev)
+    y = Fk.conv2d(x, w, b, pad, relu=True)
+    close(y, conv_ref(x, w, b, pad, True))
+
+
+@pytest.mark.parametrize("N,H,W,Ci,Co,k,pad", [c for c in CONV_CASES if c[3] % 8 == 0])
+def test_conv_dgrad(dev, K, N, H, W, Ci, Co, k, pad):
+    torch.manual_seed(4)
+    x = rnd(N, H, W, Ci, dev=dev).float().requires_grad_(True)
+    w = rnd(k, k, Ci, Co, dev=dev, scale=1 / math.sqrt(k * k * Ci))
+    y = conv_ref(x, w, None, pad, False)
+    dy = rnd(*y.shape, dev=dev)
+    y.backward(dy.float())
+    dx = Fk.conv2d_dgrad(dy, w, (H, W), pad)
+    close(dx, x.grad)
+    mask = rnd(N, H, W, Ci, dev=dev).relu().to(torch.bfloat16)
+    dxm = Fk.conv2d_dgrad(dy, w, (H, W), pad, mask=mask)
+    close(dxm, x.grad * (mask.float() > 0))
+
+
+@pytest.mark.parametrize("N,H,W,Ci,Co,k,pad", CONV_CASES)
+@pytest.mark.parametrize("splits", [None, 1])
+def test_conv_wgrad(dev, K, N, H, W, Ci, Co, k, pad, splits):
+    torch.manual_seed(5)
+    x = rnd(N, H, W, Ci, dev=dev)
+    w = rnd(k, k, Ci, Co, dev=dev).float().requires_grad_(True)
+    b = torch.zeros(Co, device=dev, requires_grad=True)
+    y = conv_ref(x, w, b, pad, False)
+    dy = rnd(*y.shape, dev=dev)
+    y.backward(dy.float())
+    ci_real = Ci - 2 if Ci == 8 else Ci   # padded-channel unpadding
+    co_real = Co - 2 if Co == 8 else Co
+    dw, db = Fk.conv2d_wgrad(x, dy, k, k, pad, ci_real, co_real, True, splits)
+    close(dw, w.grad[:, :, :ci_real, :co_real], rel=1e-3)
+    close(db, b.grad[:co_real], rel=1e-3)
+
+
+# ---------------------------------------------------------------- pool / lrn / loss
+@pytest.mark.parametrize("N,H,W,C", [(4, 28, 28, 8), (3, 14, 14, 64), (2, 7, 7, 16), (5, 10, 10, 16)])
+def test_maxpool(dev, K, N, H, W, C):
+    torch.manual_seed(6)
+    x = rnd(N, H, W, C, dev=dev).relu().to(torch.bfloat16)
+    y, arg = Fk.maxpool2x2(x)
+    xn = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    ref = F.max_pool2d(xn, 2, 2, ceil_mode=True)
+    close(y, ref.permute(0, 2, 3, 1), rel=0)
+    dy = rnd(*y.shape, dev=dev)
+    ref.backward(dy.float().permute(0, 3, 1, 2))
+    dx = Fk.maxpool2x2_bwd(dy, arg, y, (H, W), relu_mask=True)
+    g = xn.grad.permute(0, 2, 3, 1) * (x.float() > 0)
+    # ties (relu zeros) may route to a different window element; only nonzero inputs are defined
+    close(dx.float() * (x.float() > 0), g, rel=0)
+
+
+@pytest.mark.parametrize("C", [32, 64])
+def test_lrn(dev, K, C):
+    torch.manual_seed(7)
+    r, bias, alpha, beta = 4, 1.0, 0.001 / 9.0, 0.75
+    x = (rnd(6, 14, 14, C, dev=dev, scale=3.0)).relu().to(torch.bfloat16)
+    y = Fk.lrn(x, r, bias, alpha, beta)
+    xn = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    ref = lrn_tf(xn, r, bias, alpha, beta)
+    close(y, ref.permute(0, 2, 3, 1))
+    dy = rnd(*y.shape, dev=dev)
+    ref.backward(dy.float().permute(0, 3, 1, 2))
+    dx = Fk.lrn_bwd(x, dy, r, bias, alpha, beta, relu_mask=False)
+    close(dx, xn.grad.permute(0, 2, 3, 1))
+    dxm = Fk.lrn_bwd(x, dy, r, bias, alpha, beta, relu_mask=True)
+    close(dxm, xn.grad.permute(0, 2, 3, 1) * (x.float() > 0))
+
+
+@pytest.mark.parametrize("B", [1, 3, 127, 128, 4099])
+def test_softmax_ce(dev, K, B):
+    torch.manual_seed(8)
+    logits = torch.randn(B, 16, device=dev) * 3
+    logits[:, 10:] = 0
+    labels = torch.randint(0, 10, (B,), device=dev, dtype=torch.int32)
+    dl, stats = Fk.softmax_ce(logits, labels, 10)
+    l = logits[:, :10].clone().requires_grad_(True)
+    loss = F.cross_entropy(l, labels.long())
+    loss.backward()
+    torch.cuda.synchronize()
+    assert abs(stats[0].item() / B - loss.item()) < 1e-4 * max(1, loss.item())
+    acc = (l.argmax(1) == labels.long()).float().sum().item()
+    assert stats[1].item() == acc
+    close(dl[:, :10], l.grad)
+    assert dl[:, 10:].float().abs().max().item() == 0
+    pr = Fk.softmax_probs(logits, 10)
+    close(pr, torch.softmax(logits[:, :10], 1), rel=1e-5)
+
+
+def test_softmax_nan_flag(dev, K):
+    logits = torch.zeros(64, 16, device=dev)
+    logits[5, 3] = float("nan")
+    labels = torch.zeros(64, device=dev, dtype=torch.int32)
+    _, stats = Fk.softmax_ce(logits, labels, 10)
+    assert stats[2].item() == 1.0
+
+
+def test_prep_images(dev, K):
+    torch.manual_seed(9)
+    src = torch.randint(0, 256, (100, 784), dtype=torch.uint8, device=dev)
+    lab = torch.randint(0, 10, (100,), dtype=torch.int32, device=dev)
+    idx = torch.randperm(100, device=dev)[:37]
+    out = torch.empty(37, 28, 28, 1, dtype=torch.bfloat16, device=dev)
+    lo = torch.empty(37, dtype=torch.int32, device=dev)
+    K.prep_images(src, idx, lab, out, lo, 784, 1, 1)
+    ref = src[idx].float() / 255.0 - 0.5
+    close(out.view(37, 784), ref, rel=1e-2)
+    assert torch.equal(lo, lab[idx])
+    out3 = torch.empty(37, 28, 28, 3, dtype=torch.bfloat16, device=dev)
+    K.prep_images(src, idx, lab, out3, lo, 784, 1, 3)
+    close(out3, ref.view(37, 28, 28, 1).expand(37, 28, 28, 3), rel=1e-2)
+
+
+def test_fused_optimizer(dev, K):
+    from distributed_tensorflow_ibm_mnist_amd.runtime.params import FlatParams, OptConfig
+    torch.manual_seed(10)
+    shapes = [("a/weights", (5, 5, 3, 32), 0.0), ("a/biases", (32,), None), ("b/weights", (40, 10), 0.004),
+              ("b/biases", (10,), None)]
+    init = {n: torch.randn(*s) for n, s, _ in shapes}
+    fp = FlatParams.build([(n, s, wd) for n, s, wd in shapes], init, dev, pads={"a/weights": (8 - 3 + 3, 32),
+                                                                              "b/weights": (40, 16)})
+    cfg = OptConfig(lr0=0.1, decay_rate=0.5, decay_steps=2, momentum=0.9, nesterov=True, use_momentum=True,
+                    ema_max=0.9999)
+    ref = {n: init[n].clone().to(dev) for n in init}
+    mom = {n: torch.zeros_like(ref[n]) for n in ref}
+    ema = {n: ref[n].clone() for n in ref}
+    for step in range(5):
+        g = {n: torch.randn_like(ref[n]) for n in ref}
+        for n in ref:
+            fp.grad_view(n).copy_(g[n])
+        fp.apply(cfg, grad_scale=0.5)
+        lr = 0.1 * 0.5 ** (step // 2)
+        d = min(0.9999, (1 + step) / (10 + step))
+        for n, s, wd in shapes:
+            gg = g[n] * 0.5 + (wd or 0.0) * ref[n]
+            mom[n] = mom[n] * 0.9 + gg
+            ref[n] = ref[n] - lr * (gg + 0.9 * mom[n])
+            ema[n] = ema[n] - (1 - d) * (ema[n] - ref[n])
+        fp.step.add_(1)
+    torch.cuda.synchronize()
+    for n in ref:
+        close(fp.param_view(n), ref[n], rel=1e-5)
+        close(fp.ema_view(n), ema[n], rel=1e-5)
+    wbf = fp.bf16_view("b/weights")
+    assert wbf.shape == (40, 16)
+    close(wbf[:, :10], ref["b/weights"], rel=1e-2)
+    assert wbf[:, 10:].float().abs().max().item() == 0

@@ -1,0 +1,164 @@
+#!/usr/bin/env python3
+"""Headline benchmark: training images/sec (whole node), MNIST LeNet-5, bf16.
+
+BASELINE.json metric: "images/sec (whole node) MNIST LeNet-5 at 1/2/4/8 MI355X"
+on synthetic 28x28x1 data with random-init weights; the per-GPU batch defaults
+to the BASELINE stress config (65536 / GPU, weak scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model lenet5]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Each timed step is the complete training step: on-device batch gather +
+normalise (K10), forward, softmax-CE, backward, RCCL all-reduce of the gradient
+buckets (N > 1), fused SGD + weight-EMA update, loss-EMA/step finalisation.
+K steps are bracketed by barrier + device synchronize on both sides; the
+reported time is the MAX over ranks; rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MODEL_LABEL = {"lenet5": "LeNet-5", "reference_cnn": "reference CNN (mnist_input.inference)", "mlp": "MLP 784-128-10"}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="lenet5", choices=sorted(MODEL_LABEL))
+    ap.add_argument("--batch", type=int, default=65536, help="per-GPU batch (BASELINE stress config: 65536)")
+    ap.add_argument("--in_channels", type=int, default=1)
+    ap.add_argument("--impl", default="hip", choices=["hip", "torch"],
+                    help="hip = our CDNA4 kernels; torch = PyTorch-ROCm baseline (MIOpen/hipBLASLt, bf16 autocast)")
+    ap.add_argument("--bucket_mb", type=float, default=4.0)
+    ap.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph (hip impl, N=1)")
+    ap.add_argument("--optimizer", default="momentum", choices=["sgd", "momentum", "nesterov"])
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--dataset_size", type=int, default=60000)
+    return ap.parse_args()
+
+
+def main() -> int:
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from distributed_tensorflow_ibm_mnist_amd.models import get_model
+    from distributed_tensorflow_ibm_mnist_amd.models.torch_ref import init_params
+    from distributed_tensorflow_ibm_mnist_amd.runtime.params import OptConfig
+    from distributed_tensorflow_ibm_mnist_amd.parallel.dp import DataParallel
+    from distributed_tensorflow_ibm_mnist_amd.data.synthetic import make_synthetic
+    from distributed_tensorflow_ibm_mnist_amd.data.device_loader import DeviceDataset, DeviceLoader
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    spec = get_model(args.model, args.in_channels)
+    init = init_params(spec, seed=args.seed)
+    opt = OptConfig(lr0=args.lr, decay_rate=0.1, decay_steps=0, momentum=0.9 if args.optimizer != "sgd" else 0.0,
+                    nesterov=args.optimizer == "nesterov", use_momentum=args.optimizer != "sgd", ema_max=0.9999)
+    if args.impl == "hip":
+        from distributed_tensorflow_ibm_mnist_amd.runtime.executor import HipNet
+        net = HipNet(spec, args.batch, dev, init, opt)
+    else:
+        from distributed_tensorflow_ibm_mnist_amd.runtime.torchnet import TorchNet
+        net = TorchNet(spec, args.batch, dev, init, opt)
+    dp = DataParallel(net, bucket_cap_mb=args.bucket_mb)
+    dp.broadcast_state()
+
+    imgs, labs = make_synthetic(args.dataset_size, seed=args.seed, channels=1, device=dev)
+    ds = DeviceDataset(imgs, labs, dev, hw=784, channels=1)
+    loader = DeviceLoader(ds, net.x0, net.labels, rank=rank, world=world, seed=args.seed)
+
+    use_graph = bool(args.graph) and args.impl == "hip" and world == 1
+    graph = None
+
+    def step_body():
+        dp.train_step()
+
+    if use_graph:
+        from distributed_tensorflow_ibm_mnist_amd.runtime.graph import StepGraph
+        graph = StepGraph(step_body)
+
+    def step():
+        loader.next()
+        if graph is not None:
+            graph.replay()
+        else:
+            step_body()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    el = float(elapsed.item())
+    stats = net.read_stats()
+    global_batch = args.batch * world
+    ms = el / max(args.steps, 1) * 1e3
+    value = global_batch * args.steps / el
+    if rank == 0:
+        fwd, tot = spec.flops_per_image()
+        out = {
+            "metric": "images/sec (whole node) MNIST LeNet-5" if args.model == "lenet5"
+            else f"images/sec (whole node) MNIST {MODEL_LABEL[args.model]}",
+            "value": round(value, 1),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic 28x28x1 (on-device generated MNIST-like glyphs), random-init weights",
+            "config": {
+                "model": MODEL_LABEL[args.model],
+                "global_batch": global_batch,
+                "per_gpu_batch": args.batch,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "impl": args.impl,
+                "hip_graph": use_graph,
+                "optimizer": args.optimizer,
+            },
+            "tflops_per_s": round(tot * value / 1e12, 2),
+            "final_train_loss": round(stats["cross_entropy"], 5),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

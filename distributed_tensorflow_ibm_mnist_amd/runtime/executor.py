@@ -1,0 +1,297 @@
+"""Static execution plan for a ``ModelSpec`` on the HIP kernels.
+
+This replaces TF's graph executor for the reference model: the
+forward, the *explicit* backward and the fused update of one training step are
+a fixed sequence of kernel launches over buffers allocated once for a given
+batch size (an arena), so the whole step can be captured into a hipGraph
+(``runtime/graph.py``) and replayed with no host work.
+
+Design points (MI355X-first, not a port of the TF graph):
+* activations bf16 NHWC, channels padded to 8 → every operand load is 16 B;
+* ReLU backward is fused into whichever kernel produces the gradient
+  (dgrad epilogue, pool-backward, LRN-backward), never a separate pass;
+* bias gradients ride in the weight-gradient GEMM as a virtual ones column;
+* weight gradients are written straight into the flat gradient buffer, and a
+  per-layer "grads ready" hook lets the data-parallel layer launch RCCL
+  all-reduce of finished buckets while earlier layers are still in backward;
+* loss / accuracy / NaN flag stay on device (``stats``); the host reads them
+  only when it logs (no per-step sync).
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Callable, Dict, List, Optional, Tuple
+
+import torch
+
+from ..models.spec import Conv, Dense, LRN, MaxPool, ModelSpec
+from ..ops import functional as Fk
+from ..ops._ext import kernels
+from .params import FlatParams, OptConfig
+
+
+def _bf16(*shape, device) -> torch.Tensor:
+    return torch.zeros(*shape, dtype=torch.bfloat16, device=device)
+
+
+class _Layer:
+    name: str
+    has_params = False
+    out: torch.Tensor          # output activation buffer [B, ...]
+
+    def fwd(self, nb: int) -> None: ...
+    def bwd(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor]) -> None: ...
+
+
+class ConvLayer(_Layer):
+    has_params = True
+
+    def __init__(self, spec: Conv, x: torch.Tensor, in_relu: bool, first: bool, fp: FlatParams, B: int, dev):
+        self.spec, self.name, self.x, self.in_relu, self.first, self.fp = spec, spec.name, x, in_relu, first, fp
+        _, self.H, self.W, self.C = x.shape
+        self.OH, self.OW = Fk.conv_out_hw(self.H, self.W, spec.kh, spec.kw, spec.padding)
+        self.Cp = Fk.pad8(spec.cout)
+        self.ph, self.pw = Fk.conv_pads(spec.kh, spec.kw, spec.padding)
+        self.out = _bf16(B, self.OH, self.OW, self.Cp, device=dev)
+        self.wname, self.bname = f"{spec.name}/weights", f"{spec.name}/biases"
+        self.M_wg = spec.kh * spec.kw * self.C + 1
+        self.splits = Fk.pick_splits(self.M_wg, self.Cp, B * self.OH * self.OW)
+        self.slab_elems = self.splits * self.M_wg * self.Cp
+
+    def fwd(self, nb: int) -> None:
+        s = self.spec
+        kernels().conv_fwd(self.x, self.fp.bf16_view(self.wname), self.out, nb, self.H, self.W, self.C, self.OH,
+                           self.OW, s.kh, s.kw, self.ph, self.pw, self.Cp, self.fp.param_view(self.bname), s.cout,
+                           s.relu)
+
+    def bwd(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor], slab: torch.Tensor) -> None:
+        s = self.spec
+        K = kernels()
+        S = K.conv_wgrad(self.x, dy, slab, nb, self.H, self.W, self.C, self.OH, self.OW, s.kh, s.kw, self.ph, self.pw,
+                         self.Cp, True, Fk.pick_splits(self.M_wg, self.Cp, nb * self.OH * self.OW))
+        K.splitk_reduce(slab, S, self.M_wg, self.Cp, s.kh * s.kw, self.C, s.cin, s.cout, s.kh * s.kw * self.C,
+                        self.fp.grad_view(self.wname), self.fp.grad_view(self.bname), 1.0)
+        if dx is not None:
+            K.conv_dgrad(dy, self.fp.bf16_view(self.wname), dx, nb, self.OH, self.OW, self.Cp, self.H, self.W, s.kh,
+                         s.kw, self.ph, self.pw, self.C, self.x if self.in_relu else None)
+
+
+class PoolLayer(_Layer):
+    def __init__(self, spec: MaxPool, x: torch.Tensor, in_relu: bool, B: int, dev):
+        assert spec.k == 2 and spec.s == 2 and spec.padding == "SAME", "2x2/2 SAME pooling only"
+        self.spec, self.name, self.x, self.in_relu = spec, spec.name, x, in_relu
+        _, self.H, self.W, self.C = x.shape
+        self.OH, self.OW = (self.H + 1) // 2, (self.W + 1) // 2
+        self.out = _bf16(B, self.OH, self.OW, self.C, device=dev)
+        self.arg = torch.zeros(B, self.OH, self.OW, self.C, dtype=torch.uint8, device=dev)
+
+    def fwd(self, nb: int) -> None:
+        kernels().maxpool_fwd(self.x, self.out, self.arg, nb, self.H, self.W, self.C, self.OH, self.OW)
+
+    def bwd(self, nb: int, dy, dx, slab=None) -> None:
+        if dx is not None:
+            kernels().maxpool_bwd(dy, self.arg, self.out, self.in_relu, dx, nb, self.H, self.W, self.C, self.OH,
+                                  self.OW)
+
+
+class LRNLayer(_Layer):
+    def __init__(self, spec: LRN, x: torch.Tensor, in_relu: bool, B: int, dev):
+        self.spec, self.name, self.x, self.in_relu = spec, spec.name, x, in_relu
+        self.C = x.shape[-1]
+        self.out = torch.zeros_like(x)
+
+    def _p(self, nb):
+        return nb * (self.x[0].numel() // self.C)
+
+    def fwd(self, nb: int) -> None:
+        s = self.spec
+        kernels().lrn_fwd(self.x, self.out, self._p(nb), self.C, s.depth_radius, s.bias, s.alpha, s.beta)
+
+    def bwd(self, nb: int, dy, dx, slab=None) -> None:
+        if dx is not None:
+            s = self.spec
+            kernels().lrn_bwd(self.x, dy, dx, self._p(nb), self.C, s.depth_radius, s.bias, s.alpha, s.beta,
+                              self.in_relu)
+
+
+class DenseLayer(_Layer):
+    has_params = True
+
+    def __init__(self, spec: Dense, x: torch.Tensor, in_relu: bool, first: bool, last: bool, fp: FlatParams, B: int,
+                 dev):
+        self.spec, self.name, self.in_relu, self.first, self.last, self.fp = spec, spec.name, in_relu, first, last, fp
+        self.x = x.view(B, -1)
+        self.Dp = self.x.shape[1]
+        self.Np = Fk.pad8(spec.dout) if not last else max(16, Fk.pad8(spec.dout))
+        self.out = torch.zeros(B, self.Np, dtype=torch.float32 if last else torch.bfloat16, device=dev)
+        self.wname, self.bname = f"{spec.name}/weights", f"{spec.name}/biases"
+        self.M_wg = self.Dp + 1
+        self.splits = Fk.pick_splits(self.M_wg, self.Np, B)
+        self.slab_elems = self.splits * self.M_wg * self.Np
+
+    def fwd(self, nb: int) -> None:
+        s = self.spec
+        kernels().dense_fwd(self.x, self.fp.bf16_view(self.wname), self.out, nb, self.Np, self.Dp, self.Dp, self.Np,
+                            self.Np, self.fp.param_view(self.bname), s.dout, s.relu, None, 0)
+
+    def bwd(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor], slab: torch.Tensor) -> None:
+        s = self.spec
+        K = kernels()
+        dy2 = dy.view(-1, self.Np)
+        S = K.dense_wgrad(self.x, dy2, slab, self.Dp, self.Np, nb, self.Dp, self.Np, True,
+                          Fk.pick_splits(self.M_wg, self.Np, nb))
+        K.splitk_reduce(slab, S, self.M_wg, self.Np, 1, self.Dp, s.din, s.dout, self.Dp,
+                        self.fp.grad_view(self.wname), self.fp.grad_view(self.bname), 1.0)
+        if dx is not None:
+            K.dense_dgrad(dy2, self.fp.bf16_view(self.wname), dx.view(-1, self.Dp), nb, self.Dp, self.Np, self.Np,
+                          self.Np, self.Dp, self.x if self.in_relu else None, self.Dp)
+
+
+def _weight_pads(spec: ModelSpec) -> Dict[str, Tuple[int, int]]:
+    """(I_pad, J_pad) of every weight's bf16 copy, following activation padding."""
+    pads: Dict[str, Tuple[int, int]] = {}
+    c = spec.in_channels
+    flat: Optional[int] = None
+    layers = spec.layers
+    for i, L in enumerate(layers):
+        if isinstance(L, Conv):
+            cout_p = Fk.pad8(L.cout)
+            pads[f"{L.name}/weights"] = (c, cout_p)
+            c = cout_p
+        elif isinstance(L, Dense):
+            din_p = flat if flat is not None else None
+            if din_p is None:
+                din_p = L.din  # flatten of a spatial map (channels must be unpadded)
+            last = i == len(layers) - 1
+            dout_p = max(16, Fk.pad8(L.dout)) if last else Fk.pad8(L.dout)
+            pads[f"{L.name}/weights"] = (din_p, dout_p)
+            flat = dout_p
+    return pads
+
+
+class HipNet:
+    """One model replica on one GPU: buffers + kernels for fwd / bwd / update."""
+
+    def __init__(self, spec: ModelSpec, batch: int, device, init: Dict[str, torch.Tensor],
+                 opt: Optional[OptConfig] = None):
+        dev = torch.device(device)
+        self.spec, self.B, self.device = spec, batch, dev
+        self.opt = opt or OptConfig()
+        pads = _weight_pads(spec)
+        specs = []
+        for L in spec.weights():
+            shp = (L.kh, L.kw, L.cin, L.cout) if isinstance(L, Conv) else (L.din, L.dout)
+            specs.append((f"{L.name}/weights", shp, L.wd))
+            specs.append((f"{L.name}/biases", (L.cout if isinstance(L, Conv) else L.dout,), None))
+        self.fp = FlatParams.build(specs, init, dev, pads)
+        H, W = spec.input_hw
+        self.x0 = _bf16(batch, H, W, spec.in_channels, device=dev)
+        self.labels = torch.zeros(batch, dtype=torch.int32, device=dev)
+        self.layers: List[_Layer] = []
+        x, in_relu = self.x0, False
+        n = len(spec.layers)
+        for i, L in enumerate(spec.layers):
+            if isinstance(L, Conv):
+                lay = ConvLayer(L, x, in_relu, i == 0, self.fp, batch, dev)
+                in_relu = L.relu
+            elif isinstance(L, MaxPool):
+                lay = PoolLayer(L, x, in_relu, batch, dev)
+                in_relu = False
+            elif isinstance(L, LRN):
+                lay = LRNLayer(L, x, in_relu, batch, dev)
+                in_relu = False
+            elif isinstance(L, Dense):
+                if x.dim() == 4:  # NHWC flatten (mnist_input.py:177-180); padded channels would break it
+                    assert x[0].numel() == L.din, f"{L.name}: flatten {x[0].numel()} != din {L.din}"
+                lay = DenseLayer(L, x, in_relu, i == 0, i == n - 1, self.fp, batch, dev)
+                in_relu = L.relu
+            else:
+                raise TypeError(L)
+            self.layers.append(lay)
+            x = lay.out
+        assert isinstance(self.layers[-1], DenseLayer) and self.layers[-1].last, "model must end in a Dense"
+        self.logits = self.layers[-1].out
+        self.n_classes = spec.num_classes
+        # gradient ping-pong buffers (largest activation) + split-K slab workspace
+        gmax = max(int(l.out.numel()) for l in self.layers[:-1]) if len(self.layers) > 1 else 1
+        self.gbuf = [_bf16(gmax, device=dev), _bf16(gmax, device=dev)]
+        self.dlogits = _bf16(batch, self.logits.shape[1], device=dev)
+        slab = max(getattr(l, "slab_elems", 0) for l in self.layers)
+        self.slab = torch.zeros(max(slab, 1), dtype=torch.float32, device=dev)
+        self.stats = torch.zeros(8, dtype=torch.float32, device=dev)
+        self.eval_stats = torch.zeros(8, dtype=torch.float32, device=dev)
+        names = [e.name for e in self.fp.wd_entries]
+        self.loss_names = [n.replace("/weights", "/weight_loss") for n in names] + ["cross_entropy", "total_loss"]
+        self.loss_ema = torch.zeros(3 * len(self.loss_names), dtype=torch.float32, device=dev)
+        self.grad_ready_hooks: List[Callable[[int], None]] = []
+
+    # ------------------------------------------------------------------ step parts
+    def forward(self, nb: Optional[int] = None) -> torch.Tensor:
+        nb = self.B if nb is None else nb
+        for lay in self.layers:
+            lay.fwd(nb)
+        return self.logits
+
+    def loss_and_grad(self, nb: Optional[int] = None, scale: Optional[float] = None) -> None:
+        nb = self.B if nb is None else nb
+        kernels().softmax_ce(self.logits, self.logits.shape[1], self.labels, nb, self.n_classes,
+                             (1.0 / nb) if scale is None else scale, self.dlogits, self.logits.shape[1], self.stats,
+                             None)
+
+    def backward(self, nb: Optional[int] = None) -> None:
+        nb = self.B if nb is None else nb
+        dy = self.dlogits
+        k = 0
+        for i in range(len(self.layers) - 1, -1, -1):
+            lay = self.layers[i]
+            if i > 0:
+                nel = self.layers[i - 1].out.numel()
+                dx = self.gbuf[k][:nel].view(self.layers[i - 1].out.shape)
+                k ^= 1
+            else:
+                dx = None
+            lay.bwd(nb, dy, dx, self.slab)
+            if lay.has_params:
+                for h in self.grad_ready_hooks:
+                    h(i)
+            dy = dx
+
+    def update(self, grad_scale: float = 1.0, increment: bool = True, batch_for_stats: Optional[int] = None) -> None:
+        self.fp.apply(self.opt, grad_scale)
+        self.finalize(batch_for_stats or self.B, increment)
+
+    def finalize(self, batch: int, increment: bool = True) -> None:
+        fp = self.fp
+        nw = len(fp.wd_entries)
+        kernels().finalize_step(fp.step, self.stats, fp.l2 if nw else None, fp.wds if nw else None, nw,
+                                self.loss_ema, len(self.loss_names), batch, increment)
+
+    def train_step(self, grad_scale: float = 1.0) -> None:
+        self.forward()
+        self.loss_and_grad()
+        self.backward()
+        self.update(grad_scale)
+
+    # ------------------------------------------------------------------ eval
+    def eval_batch(self, nb: int, stats: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Forward only on x0[:nb] / labels[:nb]; accumulates loss/correct into stats."""
+        self.forward(nb)
+        st = self.eval_stats if stats is None else stats
+        kernels().softmax_ce(self.logits, self.logits.shape[1], self.labels, nb, self.n_classes, 1.0, None,
+                             self.logits.shape[1], st, None)
+        return st
+
+    def probs(self, nb: int) -> torch.Tensor:
+        self.forward(nb)
+        return Fk.softmax_probs(self.logits[:nb], self.n_classes)
+
+    # ------------------------------------------------------------------ introspection
+    def activation(self, layer_name: str) -> torch.Tensor:
+        for lay in self.layers:
+            if lay.name == layer_name:
+                return lay.out
+        raise KeyError(layer_name)
+
+    def read_stats(self) -> Dict[str, float]:
+        s = self.stats.detach().cpu().tolist()
+        return {"cross_entropy": s[4], "accuracy": s[5], "total_loss": s[6], "nan": s[2]}

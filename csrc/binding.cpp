@@ -357,6 +357,73 @@ void cast_f32_bf16_padded(Tensor src, Tensor dst, int64_t G, int64_t I, int64_t 
          "cast_f32_bf16_padded");
 }
 
+struct CPGeo {
+  int cfg, OH, OW, PH, PW, KM;
+};
+
+CPGeo cp_geo(int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t w) {
+  CPGeo g{};
+  g.cfg = mnistx::convpool_config((int)cin, (int)cout, (int)ks, (int)pad, (int)h, (int)w);
+  TORCH_CHECK(g.cfg >= 0, "convpool: unsupported geometry cin=", cin, " cout=", cout, " k=", ks, " pad=", pad,
+              " ", h, "x", w);
+  g.OH = (int)(h + 2 * pad - ks + 1);
+  g.OW = (int)(w + 2 * pad - ks + 1);
+  g.PH = g.OH / 2;
+  g.PW = g.OW / 2;
+  g.KM = mnistx::convpool_wgrad_rows(g.cfg);
+  return g;
+}
+
+int64_t convpool_supported(int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t w) {
+  return mnistx::convpool_config((int)cin, (int)cout, (int)ks, (int)pad, (int)h, (int)w);
+}
+
+int64_t convpool_rows(int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t w) {
+  return cp_geo(cin, cout, ks, pad, h, w).KM;
+}
+
+void convpool_fwd(Tensor x, Tensor w, Tensor bias, int64_t bias_n, Tensor pooled, Tensor arg, int64_t B, int64_t cin,
+                  int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t wd) {
+  auto g = cp_geo(cin, cout, ks, pad, h, wd);
+  check(x, at::kBFloat16, B * h * wd * cin, "x");
+  check(w, at::kBFloat16, ks * ks * cin * cout, "w");
+  check(bias, at::kFloat, bias_n, "bias");
+  check(pooled, at::kBFloat16, B * g.PH * g.PW * cout, "pooled");
+  check(arg, at::kByte, B * g.PH * g.PW * cout, "arg");
+  hip_ok(mnistx::convpool_fwd(g.cfg, BF(x), BF(w), P<const float>(bias), (int)bias_n, (int)B, BFm(pooled),
+                              P<uint8_t>(arg), cur_stream()),
+         "convpool_fwd");
+}
+
+void convpool_wgrad(Tensor x, Tensor dP, Tensor arg, Tensor pooled, Tensor slab, int64_t grid, int64_t B, int64_t cin,
+                    int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t wd) {
+  auto g = cp_geo(cin, cout, ks, pad, h, wd);
+  TORCH_CHECK(grid >= 1 && grid <= 65535, "grid");
+  const int64_t np = B * g.PH * g.PW * cout;
+  check(x, at::kBFloat16, B * h * wd * cin, "x");
+  check(dP, at::kBFloat16, np, "dP");
+  check(arg, at::kByte, np, "arg");
+  check(pooled, at::kBFloat16, np, "pooled");
+  check(slab, at::kFloat, grid * g.KM * cout, "slab");
+  hip_ok(mnistx::convpool_wgrad(g.cfg, BF(x), BF(dP), P<const uint8_t>(arg), BF(pooled), (int)B, P<float>(slab),
+                                (int)grid, cur_stream()),
+         "convpool_wgrad");
+}
+
+void convpool_dgrad(Tensor dP, Tensor arg, Tensor pooled, Tensor w, Tensor dx, int64_t B, int64_t cin, int64_t cout,
+                    int64_t ks, int64_t pad, int64_t h, int64_t wd) {
+  auto g = cp_geo(cin, cout, ks, pad, h, wd);
+  const int64_t np = B * g.PH * g.PW * cout;
+  check(dP, at::kBFloat16, np, "dP");
+  check(arg, at::kByte, np, "arg");
+  check(pooled, at::kBFloat16, np, "pooled");
+  check(w, at::kBFloat16, ks * ks * cin * cout, "w");
+  check(dx, at::kBFloat16, B * h * wd * cin, "dx");
+  hip_ok(mnistx::convpool_dgrad(g.cfg, BF(dP), P<const uint8_t>(arg), BF(pooled), BF(w), (int)B, BFm(dx),
+                                cur_stream()),
+         "convpool_dgrad");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_kernels, m) {
@@ -377,5 +444,10 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("fused_optimizer", &fused_optimizer);
   m.def("finalize_step", &finalize_step);
   m.def("cast_f32_bf16_padded", &cast_f32_bf16_padded);
+  m.def("convpool_supported", &convpool_supported);
+  m.def("convpool_rows", &convpool_rows);
+  m.def("convpool_fwd", &convpool_fwd);
+  m.def("convpool_wgrad", &convpool_wgrad);
+  m.def("convpool_dgrad", &convpool_dgrad);
   m.attr("ARCH") = "gfx950";
 }

@@ -38,6 +38,16 @@ hipError_t conv_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int H, int W, i
                       int KW, int ph, int pw, int Cout, int with_bias, int splits, const GemmEpi& ep,
                       hipStream_t st);
 
+// ---- convpool.hip (fused small-channel conv + bias + ReLU + 2x2 max-pool)
+int convpool_config(int cin, int cout, int ks, int pad, int h, int w);  // -1: unsupported
+int convpool_wgrad_rows(int cfg);                                      // KM (slab rows incl. bias row)
+hipError_t convpool_fwd(int cfg, const bf16_t* x, const bf16_t* w, const float* bias, int bias_n, int B,
+                        bf16_t* pooled, uint8_t* arg, hipStream_t st);
+hipError_t convpool_wgrad(int cfg, const bf16_t* x, const bf16_t* dP, const uint8_t* arg, const bf16_t* P, int B,
+                          float* slab, int grid, hipStream_t st);
+hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const bf16_t* P, const bf16_t* w, int B,
+                          bf16_t* dx, hipStream_t st);
+
 // ---- misc.hip
 hipError_t prep_images(const uint8_t* src, const int64_t* idx, const int32_t* lab_src, int B, int HW, int Csrc,
                        int Cdst, bf16_t* out, int32_t* lab_out, hipStream_t st);

@@ -263,29 +263,56 @@ __global__ void softmax_ce_k(const float* __restrict__ logits, int ldl, const in
 
 // ------------------------------------------------------------------ split-K reduce
 // dst weights [G][I][J] <- sum_s slab[s][g*Ipad + i][j] ; bias[j] <- sum_s slab[s][bias_row][j]
+// Fixed summation order (deterministic).  Few slabs: one thread per output;
+// many slabs (per-block partials of the fused conv kernels): one wave per
+// output, lanes stride the slabs, then a wave reduction.
+DEV int64_t reduce_row(int64_t t, int64_t nw, int G, int Ipad, int I, int J, int bias_row, int& j) {
+  if (t < nw) {
+    j = (int)(t % J);
+    const int64_t gi = t / J;
+    const int i = (int)(gi % I);
+    const int g = (int)(gi / I);
+    return (int64_t)g * Ipad + i;
+  }
+  j = (int)(t - nw);
+  return bias_row;
+}
+
 __global__ void splitk_reduce_k(const float* __restrict__ slab, int S, int M, int N, int G, int Ipad, int I, int J,
                                 int bias_row, float* __restrict__ wdst, float* __restrict__ bdst, float scale) {
   const int64_t nw = (int64_t)G * I * J;
   const int64_t total = nw + (bdst ? J : 0);
   const int64_t ss = (int64_t)M * N;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    int64_t row;
     int j;
-    if (t < nw) {
-      j = (int)(t % J);
-      const int64_t gi = t / J;
-      const int i = (int)(gi % I);
-      const int g = (int)(gi / I);
-      row = (int64_t)g * Ipad + i;
-    } else {
-      j = (int)(t - nw);
-      row = bias_row;
-    }
+    const int64_t row = reduce_row(t, nw, G, Ipad, I, J, bias_row, j);
     float s = 0.f;
     const float* p = slab + row * N + j;
     for (int z = 0; z < S; ++z) s += p[z * ss];
     if (t < nw) wdst[t] = s * scale;
     else bdst[j] = s * scale;
+  }
+}
+
+__global__ void splitk_reduce_wave_k(const float* __restrict__ slab, int S, int M, int N, int G, int Ipad, int I,
+                                     int J, int bias_row, float* __restrict__ wdst, float* __restrict__ bdst,
+                                     float scale) {
+  const int64_t nw = (int64_t)G * I * J;
+  const int64_t total = nw + (bdst ? J : 0);
+  const int64_t ss = (int64_t)M * N;
+  const int lane = threadIdx.x & 63;
+  const int64_t wpb = blockDim.x / 64;
+  for (int64_t t = blockIdx.x * wpb + (threadIdx.x >> 6); t < total; t += (int64_t)gridDim.x * wpb) {
+    int j;
+    const int64_t row = reduce_row(t, nw, G, Ipad, I, J, bias_row, j);
+    const float* p = slab + row * N + j;
+    float s = 0.f;
+    for (int z = lane; z < S; z += 64) s += p[z * ss];
+    s = warp_sum(s);
+    if (lane == 0) {
+      if (t < nw) wdst[t] = s * scale;
+      else bdst[j] = s * scale;
+    }
   }
 }
 
@@ -468,8 +495,12 @@ hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B
 hipError_t splitk_reduce(const float* slab, int splits, int M, int N, int G, int Ipad, int I, int J, int bias_row,
                          float* wdst, float* bdst, float scale, hipStream_t st) {
   const int64_t total = (int64_t)G * I * J + (bdst ? J : 0);
-  hipLaunchKernelGGL(splitk_reduce_k, dim3(nblocks(total, TPB, 8192)), dim3(TPB), 0, st, slab, splits, M, N, G, Ipad,
-                     I, J, bias_row, wdst, bdst, scale);
+  if (splits >= 32)
+    hipLaunchKernelGGL(splitk_reduce_wave_k, dim3(nblocks(total, TPB / 64, 8192)), dim3(TPB), 0, st, slab, splits, M,
+                       N, G, Ipad, I, J, bias_row, wdst, bdst, scale);
+  else
+    hipLaunchKernelGGL(splitk_reduce_k, dim3(nblocks(total, TPB, 8192)), dim3(TPB), 0, st, slab, splits, M, N, G,
+                       Ipad, I, J, bias_row, wdst, bdst, scale);
   return hipGetLastError();
 }
 

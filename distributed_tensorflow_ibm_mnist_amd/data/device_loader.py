@@ -57,11 +57,10 @@ class DeviceLoader:
         self.B = int(out_labels.shape[0])
         self.rank, self.world, self.shard, self.shuffle = rank, world, shard, shuffle
         self.global_batch = self.B * world if shard else self.B
-        if self.global_batch > len(ds):
-            # tiny datasets: sample with replacement-by-repetition so big batches still work
-            self.reps = (self.global_batch + len(ds) - 1) // len(ds)
-        else:
-            self.reps = 1
+        # One device permutation covers >= 16 global batches (several passes over
+        # small datasets), so the sort behind randperm is amortised instead of
+        # running every step when the global batch approaches the dataset size.
+        self.reps = max(1, -(-16 * self.global_batch // len(ds))) if self.global_batch * 4 > len(ds) else 1
         self.cdst = int(out_images.shape[-1])
         self.gen = torch.Generator(device=ds.device)
         self.gen.manual_seed(seed if shard else seed + 7919 * rank)

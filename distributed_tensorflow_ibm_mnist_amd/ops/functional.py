@@ -42,11 +42,16 @@ def gemm_tile(M: int, N: int) -> Tuple[int, int]:
     return 128, 128
 
 
-def pick_splits(M: int, N: int, K: int, target: int = TARGET_BLOCKS, min_k: int = 8 * BK) -> int:
+SLAB_CAP = 8 << 20    # fp32 elements of split-K partials (32 MB)
+
+
+def pick_splits(M: int, N: int, K: int, target: int = TARGET_BLOCKS, min_k: int = 1024) -> int:
+    """Split-K factor for a weight-gradient GEMM: fill ~4 WGs/CU, but keep every
+    split >= min_k reduction elements and the fp32 slab under SLAB_CAP."""
     bm, bn = gemm_tile(M, N)
     tiles = math.ceil(M / bm) * math.ceil(N / bn)
     s = max(1, math.ceil(target / tiles))
-    s = min(s, max(1, K // min_k))
+    s = min(s, max(1, K // min_k), max(1, SLAB_CAP // max(1, M * N)))
     return eff_splits(K, s)
 
 

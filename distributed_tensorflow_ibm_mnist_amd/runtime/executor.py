@@ -76,6 +76,62 @@ class ConvLayer(_Layer):
                          s.kw, self.ph, self.pw, self.C, self.x if self.in_relu else None)
 
 
+class ConvPoolLayer(_Layer):
+    """conv + bias + ReLU + 2x2 max-pool as ONE fused kernel (csrc/kernels/convpool.hip).
+
+    Used when a ReLU conv is directly followed by a 2x2/2 pool and the geometry
+    has a compile-time specialisation (LeNet-5 conv1/conv2, reference conv1).
+    The full-resolution conv output is never materialised; backward rebuilds
+    dY from the pooled gradient, argmax byte and ReLU mask inside the wgrad
+    (and, when needed, dgrad) kernels.
+    """
+    has_params = True
+
+    @staticmethod
+    def supported(spec: Conv, pool: MaxPool, x_shape) -> bool:
+        _, H, W, C = x_shape
+        if not (spec.relu and spec.kh == spec.kw == 5 and pool.k == 2 and pool.s == 2 and pool.padding == "SAME"):
+            return False
+        pad = 2 if spec.padding == "SAME" else 0
+        return kernels().convpool_supported(C, Fk.pad8(spec.cout), 5, pad, H, W) >= 0
+
+    def __init__(self, spec: Conv, pool: MaxPool, x: torch.Tensor, first: bool, fp: FlatParams, B: int, dev,
+                 need_dx: bool):
+        self.spec, self.pool, self.name, self.x, self.first, self.fp = spec, pool, spec.name, x, first, fp
+        _, self.H, self.W, self.C = x.shape
+        self.pad = 2 if spec.padding == "SAME" else 0
+        self.Cp = Fk.pad8(spec.cout)
+        self.cfg = kernels().convpool_supported(self.C, self.Cp, 5, self.pad, self.H, self.W)
+        OH, OW = Fk.conv_out_hw(self.H, self.W, 5, 5, spec.padding)
+        self.PH, self.PW = OH // 2, OW // 2
+        self.out = _bf16(B, self.PH, self.PW, self.Cp, device=dev)
+        self.arg = torch.zeros(B, self.PH, self.PW, self.Cp, dtype=torch.uint8, device=dev)
+        self.wname, self.bname = f"{spec.name}/weights", f"{spec.name}/biases"
+        self.KM = kernels().convpool_rows(self.C, self.Cp, 5, self.pad, self.H, self.W)
+        self.grid = 1024
+        self.slab_elems = self.grid * self.KM * self.Cp
+        self.can_dgrad = self.cfg == 1
+        if need_dx and not self.can_dgrad:
+            raise ValueError(f"{spec.name}: fused dgrad not available for this geometry")
+
+    def _geo(self):
+        return (self.C, self.Cp, 5, self.pad, self.H, self.W)
+
+    def fwd(self, nb: int) -> None:
+        kernels().convpool_fwd(self.x, self.fp.bf16_view(self.wname), self.fp.param_view(self.bname),
+                               self.spec.cout, self.out, self.arg, nb, *self._geo())
+
+    def bwd(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor], slab: torch.Tensor) -> None:
+        s = self.spec
+        K = kernels()
+        grid = min(self.grid, max(1, (nb + 3) // 4))
+        K.convpool_wgrad(self.x, dy, self.arg, self.out, slab, grid, nb, *self._geo())
+        K.splitk_reduce(slab, grid, self.KM, self.Cp, 25, self.C, s.cin, s.cout, 25 * self.C,
+                        self.fp.grad_view(self.wname), self.fp.grad_view(self.bname), 1.0)
+        if dx is not None:
+            K.convpool_dgrad(dy, self.arg, self.out, self.fp.bf16_view(self.wname), dx, nb, *self._geo())
+
+
 class PoolLayer(_Layer):
     def __init__(self, spec: MaxPool, x: torch.Tensor, in_relu: bool, B: int, dev):
         assert spec.k == 2 and spec.s == 2 and spec.padding == "SAME", "2x2/2 SAME pooling only"
@@ -173,7 +229,7 @@ class HipNet:
     """One model replica on one GPU: buffers + kernels for fwd / bwd / update."""
 
     def __init__(self, spec: ModelSpec, batch: int, device, init: Dict[str, torch.Tensor],
-                 opt: Optional[OptConfig] = None):
+                 opt: Optional[OptConfig] = None, fuse_convpool: bool = True):
         dev = torch.device(device)
         self.spec, self.B, self.device = spec, batch, dev
         self.opt = opt or OptConfig()
@@ -190,7 +246,22 @@ class HipNet:
         self.layers: List[_Layer] = []
         x, in_relu = self.x0, False
         n = len(spec.layers)
-        for i, L in enumerate(spec.layers):
+        i = 0
+        while i < n:
+            L = spec.layers[i]
+            nxt = spec.layers[i + 1] if i + 1 < n else None
+            if (fuse_convpool and isinstance(L, Conv) and isinstance(nxt, MaxPool) and not in_relu
+                    and ConvPoolLayer.supported(L, nxt, x.shape)):
+                # the fused dgrad exists only for interior layers whose geometry has it
+                lay = ConvPoolLayer(L, nxt, x, i == 0, self.fp, batch, dev, need_dx=False)
+                if i > 0 and not lay.can_dgrad:
+                    lay = None
+                if lay is not None:
+                    lay.idx = i
+                    self.layers.append(lay)
+                    x, in_relu = lay.out, False
+                    i += 2
+                    continue
             if isinstance(L, Conv):
                 lay = ConvLayer(L, x, in_relu, i == 0, self.fp, batch, dev)
                 in_relu = L.relu
@@ -207,8 +278,10 @@ class HipNet:
                 in_relu = L.relu
             else:
                 raise TypeError(L)
+            lay.idx = i
             self.layers.append(lay)
             x = lay.out
+            i += 1
         assert isinstance(self.layers[-1], DenseLayer) and self.layers[-1].last, "model must end in a Dense"
         self.logits = self.layers[-1].out
         self.n_classes = spec.num_classes
@@ -253,7 +326,7 @@ class HipNet:
             lay.bwd(nb, dy, dx, self.slab)
             if lay.has_params:
                 for h in self.grad_ready_hooks:
-                    h(i)
+                    h(lay.idx)
             dy = dx
 
     def update(self, grad_scale: float = 1.0, increment: bool = True, batch_for_stats: Optional[int] = None) -> None:

@@ -94,8 +94,8 @@ def test_graph_replay_matches_eager(dev, K):
         net.x0.copy_(x)
         net.labels.copy_(y)
         if use_graph:
-            g = StepGraph(net.train_step, warmup=2)   # 2 warmup steps + 1 captured execution
-            for _ in range(3):
+            g = StepGraph(net.train_step, warmup=2)   # 2 eager warmup steps; capture does not execute
+            for _ in range(4):
                 g.replay()
         else:
             for _ in range(6):

@@ -264,3 +264,57 @@ def test_fused_optimizer(dev, K):
     assert wbf.shape == (40, 16)
     close(wbf[:, :10], ref["b/weights"], rel=1e-2)
     assert wbf[:, 10:].float().abs().max().item() == 0
+
+
+# ---------------------------------------------------------------- fused conv + ReLU + max-pool blocks
+CP_CASES = [
+    # N, H, W, Cin(stride), cin_real, Cout(pad), cout_real, pad
+    (7, 28, 28, 1, 1, 8, 6, 2),      # LeNet-5 conv1
+    (6, 14, 14, 8, 6, 16, 16, 0),    # LeNet-5 conv2 (VALID)
+    (5, 28, 28, 1, 1, 32, 32, 2),    # reference conv1, 1-channel input
+    (5, 28, 28, 3, 3, 32, 32, 2),    # reference conv1, 3-channel (DLI) input
+]
+
+
+@pytest.mark.parametrize("N,H,W,Ci,ci,Co,co,pad", CP_CASES)
+def test_convpool(dev, K, N, H, W, Ci, ci, Co, co, pad):
+    torch.manual_seed(11)
+    padding = "SAME" if pad else "VALID"
+    x = rnd(N, H, W, Ci, dev=dev)
+    x[..., ci:] = 0
+    w = torch.zeros(5, 5, Ci, Co, device=dev)
+    w[:, :, :ci, :co] = torch.randn(5, 5, ci, co, device=dev) / math.sqrt(25 * ci)
+    w = w.to(torch.bfloat16)
+    b = torch.randn(co, device=dev) * 0.1
+    OH, OW = (H, W) if pad else (H - 4, W - 4)
+    PH, PW = OH // 2, OW // 2
+    pooled = torch.empty(N, PH, PW, Co, dtype=torch.bfloat16, device=dev)
+    arg = torch.empty(N, PH, PW, Co, dtype=torch.uint8, device=dev)
+    K.convpool_fwd(x, w, b, co, pooled, arg, N, Ci, Co, 5, pad, H, W)
+    # oracle: conv -> bias -> relu -> pool (fp32)
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    br = torch.zeros(Co, device=dev)
+    br[:co] = b
+    br.requires_grad_(True)
+    y = conv_ref(xr, wr, br, padding, True)                       # [N, OH, OW, Co]
+    yp = F.max_pool2d(y.permute(0, 3, 1, 2), 2, 2).permute(0, 2, 3, 1)
+    close(pooled, yp)
+    if co < Co:
+        assert pooled[..., co:].float().abs().max().item() == 0
+    # backward: wgrad (+ bias via ones row) and, for LeNet conv2, dgrad
+    dP = rnd(N, PH, PW, Co, dev=dev)
+    yp.backward(dP.float())
+    KM = K.convpool_rows(Ci, Co, 5, pad, H, W)
+    grid = 37
+    slab = torch.empty(grid * KM * Co, dtype=torch.float32, device=dev)
+    K.convpool_wgrad(x, dP, arg, pooled, slab, grid, N, Ci, Co, 5, pad, H, W)
+    dw = torch.empty(5, 5, ci, co, device=dev)
+    db = torch.empty(co, device=dev)
+    K.splitk_reduce(slab, grid, KM, Co, 25, Ci, ci, co, 25 * Ci, dw, db, 1.0)
+    close(dw, wr.grad[:, :, :ci, :co], rel=3e-2)
+    close(db, br.grad[:co], rel=3e-2)
+    if K.convpool_supported(Ci, Co, 5, pad, H, W) == 1:
+        dx = torch.empty(N, H, W, Ci, dtype=torch.bfloat16, device=dev)
+        K.convpool_dgrad(dP, arg, pooled, w, dx, N, Ci, Co, 5, pad, H, W)
+        close(dx[..., :ci], xr.grad[..., :ci])

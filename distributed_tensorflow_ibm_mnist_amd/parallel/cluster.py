@@ -1,0 +1,136 @@
+"""Cluster setup — the equivalent of ``setup_distribute()`` (``main.py:42-68``).
+
+Modes:
+
+* **local** — no ``--worker_hosts`` and no torchrun environment: one process,
+  the reference's ``create_local_server`` path (``main.py:63-66``; task_id forced 0);
+* **dp** — torchrun env (``WORLD_SIZE`` > 1), or ``--worker_hosts`` without
+  ``--ps_hosts`` (the reference would silently train unshared per-worker copies,
+  Q10; we treat it as synchronous data parallel);
+* **ps** — ``--ps_hosts`` + ``--worker_hosts`` + ``--job_name`` + ``--task_id``:
+  1..k parameter-server ranks followed by the workers
+  (rank(ps k) = k, rank(worker i) = num_ps + i), rendezvous at the first PS
+  ``host:port`` (TCPStore), RCCL (``nccl``) between GPU processes, gloo on CPU.
+
+Device: one process per GPU; ``LOCAL_RANK`` if set, else rank modulo the
+visible device count.
+"""
+from __future__ import annotations
+
+import dataclasses
+import datetime
+import os
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclasses.dataclass
+class Cluster:
+    mode: str                       # local | dp | ps
+    job_name: str
+    task_id: int
+    ps_hosts: List[str]
+    worker_hosts: List[str]
+    rank: int = 0
+    world: int = 1
+    num_ps: int = 0
+    num_workers: int = 1
+    master: str = ""
+    device: Optional[torch.device] = None
+    backend: str = ""
+
+    @property
+    def is_chief(self) -> bool:
+        """main.py:73: the chief is worker task 0."""
+        return self.job_name != "ps" and self.task_id == 0
+
+    @property
+    def spec(self) -> Dict[str, List[str]]:
+        d: Dict[str, List[str]] = {}
+        if self.worker_hosts:
+            d["worker"] = self.worker_hosts
+        if self.ps_hosts:
+            d["ps"] = self.ps_hosts
+        return d
+
+
+def _split(s: Optional[str]) -> List[str]:
+    return [h.strip() for h in (s or "").split(",") if h.strip()]
+
+
+def _norm_host(hp: str) -> str:
+    host, _, port = hp.rpartition(":")
+    if host in ("localhost", "", "0.0.0.0"):
+        host = "127.0.0.1"
+    return f"{host}:{port}"
+
+
+def pick_device(rank: int, want_gpu: bool) -> torch.device:
+    if not want_gpu or not torch.cuda.is_available():
+        return torch.device("cpu")
+    lr = os.environ.get("LOCAL_RANK")
+    n = torch.cuda.device_count()
+    idx = int(lr) if lr is not None else rank % max(n, 1)
+    return torch.device("cuda", idx)
+
+
+def setup_distribute(job_name: str = "", ps_hosts: str = "", worker_hosts: str = "", task_id: int = 0,
+                     want_gpu: bool = True, timeout_s: float = 600.0, log=print,
+                     ps_backend: str = "") -> Cluster:
+    ps, workers = _split(ps_hosts), _split(worker_hosts)
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    to = datetime.timedelta(seconds=timeout_s)
+    if workers:
+        cl = Cluster("ps" if ps else "dp", job_name or "worker", int(task_id), ps, workers)
+        log("Cluster spec: ", cl.spec)                               # main.py:57
+        if cl.mode == "ps":
+            if cl.job_name not in ("ps", "worker"):
+                raise ValueError('job_name must be "ps" or "worker"')
+            cl.num_ps, cl.num_workers = len(ps), len(workers)
+            n = len(ps) if cl.job_name == "ps" else len(workers)
+            if not 0 <= cl.task_id < n:
+                raise ValueError(f"task_id {cl.task_id} out of range for job {cl.job_name} ({n} tasks)")
+            cl.rank = cl.task_id if cl.job_name == "ps" else len(ps) + cl.task_id
+            cl.world = len(ps) + len(workers)
+            cl.master = _norm_host(ps[0])
+        else:
+            if cl.job_name == "ps":
+                raise ValueError("job_name=ps without --ps_hosts")
+            cl.num_workers = len(workers)
+            cl.rank, cl.world = cl.task_id, len(workers)
+            cl.master = _norm_host(workers[0])
+        cl.device = pick_device(cl.rank, want_gpu)
+        cl.backend = "nccl" if cl.device.type == "cuda" else "gloo"
+        if cl.mode == "ps" and ps_backend:
+            # gloo stages GPU tensors through host memory: lets several PS-mode
+            # processes share one GPU (RCCL needs one rank per GPU)
+            cl.backend = ps_backend
+        if cl.device.type == "cuda":
+            torch.cuda.set_device(cl.device)
+        kw = {"device_id": cl.device} if cl.backend == "nccl" else {}
+        dist.init_process_group(cl.backend, init_method=f"tcp://{cl.master}", rank=cl.rank, world_size=cl.world,
+                                timeout=to, **kw)
+        return cl
+    if env_world > 1:
+        rank = int(os.environ.get("RANK", "0"))
+        cl = Cluster("dp", "worker", rank, [], [], rank=rank, world=env_world, num_workers=env_world)
+        cl.device = pick_device(rank, want_gpu)
+        cl.backend = "nccl" if cl.device.type == "cuda" else "gloo"
+        if cl.device.type == "cuda":
+            torch.cuda.set_device(cl.device)
+        kw = {"device_id": cl.device} if cl.backend == "nccl" else {}
+        dist.init_process_group(cl.backend, timeout=to, **kw)
+        return cl
+    # local server (main.py:63-66): single process, task 0
+    cl = Cluster("local", job_name or "worker", 0, [], [])
+    cl.device = pick_device(0, want_gpu)
+    if cl.device.type == "cuda":
+        torch.cuda.set_device(cl.device)
+    return cl
+
+
+def shutdown() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()

@@ -67,10 +67,13 @@ def plan_buckets(net, cap_bytes: int) -> List[Bucket]:
 
 
 class DataParallel:
-    def __init__(self, net, group=None, bucket_cap_mb: float = 1.0, overlap: bool = True):
+    def __init__(self, net, group=None, bucket_cap_mb: float = 1.0, overlap: bool = True,
+                 world: Optional[int] = None):
         self.net = net
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        if world is None:
+            world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.world = world
         self.buckets = plan_buckets(net, int(bucket_cap_mb * (1 << 20)))
         self.trigger = {b.layers[-1]: b for b in self.buckets}
         self.pending: list = []

@@ -1,0 +1,152 @@
+"""One training replica: model executor + on-device input pipeline + DP wiring.
+
+Bridges the session/hook layer (host-side, step-count driven) and the device
+(`HipNet` on the HIP kernels, or `TorchNet` for CPU / the PyTorch baseline).
+The host keeps a mirror of the global step so hooks never read device memory
+on the hot path; device state (loss, accuracy, NaN flag) is read only when a
+hook asks for it.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..data.device_loader import DeviceDataset, DeviceLoader, eval_batches
+from ..models import torch_ref
+from ..models.spec import ModelSpec
+from ..parallel.dp import DataParallel
+from ..runtime.params import FlatParams, OptConfig
+
+
+def build_net(impl: str, spec: ModelSpec, batch: int, device, init, opt: OptConfig):
+    if impl == "hip":
+        from ..runtime.executor import HipNet
+        return HipNet(spec, batch, device, init, opt)
+    from ..runtime.torchnet import TorchNet
+    return TorchNet(spec, batch, device, init, opt)
+
+
+def state_tensors(net, include_momentum: bool = True) -> Dict[str, np.ndarray]:
+    """Device state -> checkpoint dict with the reference's variable names."""
+    fp: FlatParams = net.fp
+    out: Dict[str, np.ndarray] = {}
+    params = fp.params.detach().cpu().numpy()
+    ema = fp.ema.detach().cpu().numpy()
+    mom = fp.mom.detach().cpu().numpy()
+    for e in fp.entries:
+        sl = slice(e.off, e.off + e.n)
+        out[e.name] = params[sl].reshape(e.shape).copy()
+        if net.opt.ema_max >= 0:
+            out[f"{e.name}/ExponentialMovingAverage"] = ema[sl].reshape(e.shape).copy()
+        if include_momentum and net.opt.use_momentum:
+            out[f"{e.name}/Momentum"] = mom[sl].reshape(e.shape).copy()
+    out["global_step"] = np.asarray(int(fp.step.item()), dtype=np.int64)
+    le = net.loss_ema.detach().cpu().numpy().reshape(-1, 3)
+    for i, name in enumerate(net.loss_names):
+        out[f"{name}/avg"] = np.asarray(le[i, 2], dtype=np.float32)
+        out[f"{name}/avg/biased"] = np.asarray(le[i, 0], dtype=np.float32)
+        out[f"{name}/avg/local_step"] = np.asarray(le[i, 1], dtype=np.float32)
+    return out
+
+
+def load_state(net, tensors: Dict[str, np.ndarray], strict: bool = True) -> int:
+    fp: FlatParams = net.fp
+    missing = [e.name for e in fp.entries if e.name not in tensors]
+    if missing and strict:
+        raise KeyError(f"checkpoint lacks {missing}")
+    vals = {n: torch.from_numpy(np.asarray(tensors[n])) for n in fp.names() if n in tensors}
+    emas = {n: torch.from_numpy(np.asarray(tensors[f"{n}/ExponentialMovingAverage"])) for n in fp.names()
+            if f"{n}/ExponentialMovingAverage" in tensors}
+    moms = {n: torch.from_numpy(np.asarray(tensors[f"{n}/Momentum"])) for n in fp.names()
+            if f"{n}/Momentum" in tensors}
+    fp.load_state(vals, ema_too=not emas, ema_values=emas, mom_values=moms)
+    step = int(np.asarray(tensors.get("global_step", 0)))
+    fp.step.fill_(step)
+    le = net.loss_ema.view(-1, 3)
+    for i, name in enumerate(net.loss_names):
+        if f"{name}/avg/biased" in tensors:
+            le[i, 0] = float(tensors[f"{name}/avg/biased"])
+            le[i, 1] = float(tensors[f"{name}/avg/local_step"])
+            le[i, 2] = float(tensors[f"{name}/avg"])
+    return step
+
+
+class Replica:
+    def __init__(self, spec: ModelSpec, impl: str, batch: int, device, init: Dict[str, torch.Tensor], opt: OptConfig,
+                 train_images: torch.Tensor, train_labels: torch.Tensor, src_channels: int,
+                 eval_images: Optional[torch.Tensor] = None, eval_labels: Optional[torch.Tensor] = None,
+                 seed: int = 0, shard: bool = True, use_graph: bool = True, bucket_mb: float = 4.0,
+                 group=None, standalone: bool = False):
+        self.spec, self.impl, self.B, self.device = spec, impl, batch, torch.device(device)
+        self.net = build_net(impl, spec, batch, self.device, init, opt)
+        # standalone: a parameter-server worker (no data-parallel group of its own)
+        dp_on = dist.is_initialized() and not standalone
+        self.world = dist.get_world_size(group) if dp_on else 1
+        self.rank = dist.get_rank(group) if dp_on else 0
+        self.dp = DataParallel(self.net, group=group, bucket_cap_mb=bucket_mb, world=self.world)
+        self.train_ds = DeviceDataset(train_images, train_labels, self.device, hw=784, channels=src_channels)
+        self.eval_ds = (DeviceDataset(eval_images, eval_labels, self.device, hw=784, channels=src_channels)
+                        if eval_images is not None else None)
+        self.loader = DeviceLoader(self.train_ds, self.net.x0, self.net.labels, rank=self.rank, world=self.world,
+                                   seed=seed, shard=shard)
+        self.use_graph = use_graph and impl == "hip" and self.world == 1 and self.device.type == "cuda"
+        self._graph = None
+        self.global_step = 0
+        self.examples_per_step = batch * self.world
+
+    # ------------------------------------------------------------------ steps
+    def _body(self) -> None:
+        self.dp.train_step()
+
+    def step(self) -> None:
+        self.loader.next()
+        if self.use_graph:
+            if self._graph is None:
+                from ..runtime.graph import StepGraph
+                self._graph = StepGraph(self._body, warmup=1)
+                # warm-up ran one real step; account for it (and reload a batch for the replay)
+                self.global_step += 1
+                self.loader.next()
+            self._graph.replay()
+        else:
+            self._body()
+        self.global_step += 1
+
+    def sync_step_from_device(self) -> None:
+        self.global_step = int(self.net.fp.step.item())
+
+    def learning_rate(self) -> float:
+        return self.net.opt.lr_at(self.global_step)
+
+    def read_stats(self) -> Dict[str, float]:
+        # local replica's last step (no collective: hooks run on the chief only)
+        return self.net.read_stats()
+
+    def evaluate(self, max_examples: Optional[int] = None) -> Dict[str, float]:
+        """Full (or capped) pass over the eval split; returns loss / accuracy."""
+        if self.eval_ds is None:
+            return {"loss": float("nan"), "accuracy": float("nan")}
+        st = self.net.eval_stats
+        st.zero_()
+        n = 0
+        for nb in eval_batches(self.eval_ds, self.net.x0, self.net.labels):
+            self.net.eval_batch(nb, st)
+            n += nb
+            if max_examples and n >= max_examples:
+                break
+        # local pass (no collective, so chief-only hooks can call it safely)
+        v = (st[:2] / max(n, 1)).tolist()
+        return {"loss": v[0], "accuracy": v[1]}
+
+    def inject_nan(self) -> None:
+        with torch.no_grad():
+            self.net.fp.params[0] = float("nan")
+        self.net.fp.refresh_bf16()
+
+    def synchronize(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)

@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Distributed MNIST training — CLI-compatible with the reference ``main.py``.
+
+    python main.py [--train_dir=/tmp/mnist_train] [--config=params.yaml]
+    # data parallel (RCCL all-reduce over xGMI), one process per GPU:
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 main.py
+    # parameter-server mode (reference semantics), e.g. 1 PS + 2 workers on one node:
+    python main.py --job_name=ps     --task_id=0 --ps_hosts=localhost:2222 --worker_hosts=localhost:2223,localhost:2224
+    python main.py --job_name=worker --task_id=0 --ps_hosts=localhost:2222 --worker_hosts=localhost:2223,localhost:2224
+    python main.py --job_name=worker --task_id=1 --ps_hosts=localhost:2222 --worker_hosts=localhost:2223,localhost:2224
+
+Reference flags (main.py:12-32): job_name, ps_hosts, worker_hosts, task_id,
+train_dir, log_device_placement.  Hyper-parameters come from the parameter
+manager (``--config`` YAML/JSON or ``MNISTX_PARAMS``), as DLI's
+tf_parameter_mgr provided them; the extra flags below override it.
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from distributed_tensorflow_ibm_mnist_amd.utils import flags  # noqa: E402
+
+FLAGS = flags.FLAGS
+
+# ---- reference flags (main.py:12-32)
+flags.DEFINE_string("job_name", "", 'One of "ps", "worker"')
+flags.DEFINE_string("ps_hosts", "", "Comma-separated list of hostname:port for the parameter server jobs.")
+flags.DEFINE_string("worker_hosts", "", "Comma-separated list of hostname:port for the worker jobs.")
+flags.DEFINE_integer("task_id", 0, "Task ID of the worker/replica running the training.")
+flags.DEFINE_string("train_dir", "/tmp/mnist_train", "Directory where to write event logs and checkpoint.")
+flags.DEFINE_boolean("log_device_placement", False, "Whether to log device placement.")
+
+# ---- parameter manager (tf_parameter_mgr) source + overrides
+flags.DEFINE_string("config", "", "YAML/JSON hyper-parameter file (the DLI job config replacement)")
+flags.DEFINE_integer("max_steps", -1, "override getMaxSteps()")
+flags.DEFINE_integer("test_interval", -1, "override getTestInterval()")
+flags.DEFINE_integer("batch_size", -1, "override getTrainBatchSize() (per replica)")
+flags.DEFINE_float("base_lr", -1, "override getBaseLearningRate()")
+flags.DEFINE_float("lr_decay", -1, "override getLearningRateDecay()")
+flags.DEFINE_string("optimizer", "", "override getOptimizer(): sgd | momentum | nesterov")
+flags.DEFINE_float("momentum", -1, "momentum for --optimizer=momentum|nesterov")
+flags.DEFINE_string("train_data", "", "override getTrainData() (comma list: TFRecords, synthetic://, idx://, png://)")
+flags.DEFINE_string("test_data", "", "override getTestData()")
+flags.DEFINE_string("val_data", "", "override getValData()")
+
+# ---- framework flags
+flags.DEFINE_string("model", "reference_cnn", "reference_cnn | lenet5 | mlp")
+flags.DEFINE_integer("in_channels", 3, "model input channels: 3 = DLI RGB records (reference), 1 = grayscale")
+flags.DEFINE_string("impl", "hip", "hip = MI355X HIP kernels; torch = plain PyTorch (CPU path / baseline)")
+flags.DEFINE_boolean("cpu", False, "force the CPU (torch impl, gloo)")
+flags.DEFINE_integer("seed", 0, "random seed (weights, shuffling)")
+flags.DEFINE_boolean("train_on_eval_split", False, "parity with the reference, which trains on getTestData() (Q1)")
+flags.DEFINE_boolean("no_shard", False, "every DP rank reads the whole dataset in its own order (reference P3)")
+flags.DEFINE_boolean("verbose_steps", False, "print 'training' + step on every step like the reference (Q11)")
+flags.DEFINE_boolean("hip_graph", True, "capture the training step in a hipGraph (single GPU)")
+flags.DEFINE_float("bucket_mb", 4.0, "gradient all-reduce bucket cap (MB)")
+flags.DEFINE_float("save_checkpoint_secs", 600, "checkpoint every N seconds (TF default 600)")
+flags.DEFINE_integer("save_checkpoint_steps", 0, "checkpoint every N steps (0: off)")
+flags.DEFINE_integer("save_summaries_steps", 100, "loss/accuracy scalars every N steps")
+flags.DEFINE_integer("log_step_count_steps", 100, "global_step/sec every N steps")
+flags.DEFINE_integer("max_to_keep", 5, "checkpoints to keep")
+flags.DEFINE_integer("eval_examples", 10000, "examples per test-summary evaluation (0: whole split)")
+flags.DEFINE_string("ps_backend", "", "PS-mode transport override: '' (RCCL on GPU) | gloo (host-staged)")
+flags.DEFINE_float("collective_timeout", 600.0, "process-group timeout (s): a hung peer fails the job")
+
+
+def main(argv=None):
+    from distributed_tensorflow_ibm_mnist_amd.train.trainer import train
+    res = train(FLAGS)
+    if res:
+        print("result: " + " ".join(f"{k}={v:.6g}" if isinstance(v, float) else f"{k}={v}" for k, v in res.items()))
+    return 0
+
+
+if __name__ == "__main__":
+    flags.run(main)

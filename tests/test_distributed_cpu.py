@@ -1,0 +1,153 @@
+"""T5: distributed correctness on the CPU (gloo backend, same code paths as RCCL).
+
+* data parallel: world 2/4 replicas with bucketed, hook-launched all-reduce give
+  the same parameters as one process on the concatenated global batch;
+* bucket plan: the reference CNN's local3 gradient closes an early bucket;
+* parameter-server mode: 1 PS + 2 workers and 2 PS + 1 worker via the real CLI —
+  async apply, exact global-step total, PS shutdown, chief-only sharded checkpoint.
+"""
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dp_worker(rank, world, port, steps, B, out_q):
+    torch.set_num_threads(1)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from distributed_tensorflow_ibm_mnist_amd.models import get_model, torch_ref
+    from distributed_tensorflow_ibm_mnist_amd.parallel.dp import DataParallel
+    from distributed_tensorflow_ibm_mnist_amd.runtime.params import OptConfig
+    from distributed_tensorflow_ibm_mnist_amd.runtime.torchnet import TorchNet
+    spec = get_model("lenet5", 1)
+    init = torch_ref.init_params(spec, seed=0)
+    opt = OptConfig(lr0=0.05, use_momentum=True, momentum=0.9, nesterov=True, ema_max=0.9999)
+    net = TorchNet(spec, B, "cpu", init, opt)
+    dp = DataParallel(net, bucket_cap_mb=0.05)          # several buckets on LeNet's 247 KB
+    assert len(dp.buckets) > 1
+    g = torch.Generator().manual_seed(123)
+    for _ in range(steps):
+        x = torch.rand(world * B, 28, 28, 1, generator=g) - 0.5
+        y = torch.randint(0, 10, (world * B,), generator=g, dtype=torch.int32)
+        net.x0.copy_(x[rank * B:(rank + 1) * B])
+        net.labels.copy_(y[rank * B:(rank + 1) * B])
+        dp.train_step()
+    if rank == 0:
+        out_q.put((net.fp.params.clone(), net.fp.ema.clone(), int(net.fp.step.item())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _single(steps, B_global):
+    from distributed_tensorflow_ibm_mnist_amd.models import get_model, torch_ref
+    from distributed_tensorflow_ibm_mnist_amd.runtime.params import OptConfig
+    from distributed_tensorflow_ibm_mnist_amd.runtime.torchnet import TorchNet
+    spec = get_model("lenet5", 1)
+    init = torch_ref.init_params(spec, seed=0)
+    opt = OptConfig(lr0=0.05, use_momentum=True, momentum=0.9, nesterov=True, ema_max=0.9999)
+    net = TorchNet(spec, B_global, "cpu", init, opt)
+    g = torch.Generator().manual_seed(123)
+    for _ in range(steps):
+        x = torch.rand(B_global, 28, 28, 1, generator=g) - 0.5
+        y = torch.randint(0, 10, (B_global,), generator=g, dtype=torch.int32)
+        net.x0.copy_(x)
+        net.labels.copy_(y)
+        net.train_step()
+    return net.fp.params.clone(), net.fp.ema.clone()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_matches_single_process_large_batch(world):
+    B, steps = 8, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, steps, B, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    params, ema, step = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref_p, ref_e = _single(steps, B * world)
+    assert step == steps
+    # mean over ranks of per-rank mean gradients == mean over the global batch
+    assert torch.allclose(params, ref_p, rtol=1e-5, atol=1e-6), (params - ref_p).abs().max()
+    assert torch.allclose(ema, ref_e, rtol=1e-5, atol=1e-6)
+
+
+def test_bucket_plan_reference_cnn():
+    from distributed_tensorflow_ibm_mnist_amd.models import get_model, torch_ref
+    from distributed_tensorflow_ibm_mnist_amd.parallel.dp import plan_buckets
+    from distributed_tensorflow_ibm_mnist_amd.runtime.params import OptConfig
+    from distributed_tensorflow_ibm_mnist_amd.runtime.torchnet import TorchNet
+    spec = get_model("reference_cnn", 3)
+    net = TorchNet(spec, 2, "cpu", torch_ref.init_params(spec), OptConfig())
+    b = plan_buckets(net, 4 << 20)
+    names = [[spec.layers[i].name for i in bk.layers] for bk in b]
+    assert names == [["softmax_linear", "local4", "local3"], ["conv2", "conv1"]]
+    assert b[0].end == net.fp.total and b[1].start == 0 and b[0].start == b[1].end
+    assert b[0].nbytes > 12.8e6                      # the local3 gradient goes out early
+
+
+def _spawn_main(args, log):
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONUNBUFFERED="1")
+    return subprocess.Popen([sys.executable, os.path.join(ROOT, "main.py")] + args, cwd=ROOT, env=env,
+                            stdout=open(log, "w"), stderr=subprocess.STDOUT)
+
+
+@pytest.mark.parametrize("num_ps,num_workers", [(1, 2), (2, 1)])
+def test_ps_mode_cli(tmp_path, num_ps, num_workers):
+    base = free_port()
+    ps_hosts = ",".join(f"localhost:{base + i}" for i in range(num_ps))
+    wk_hosts = ",".join(f"localhost:{base + 100 + i}" for i in range(num_workers))
+    d = str(tmp_path / "train")
+    common = ["--impl=torch", "--cpu", "--model=mlp", "--in_channels=1", "--batch_size=32", "--max_steps=40",
+              "--test_interval=20", "--log_step_count_steps=0", "--train_data=synthetic://1500",
+              "--test_data=synthetic://300?seed=1", f"--train_dir={d}", f"--ps_hosts={ps_hosts}",
+              f"--worker_hosts={wk_hosts}", "--optimizer=momentum"]
+    procs = []
+    for j in range(num_ps):
+        procs.append(("ps", j, _spawn_main(common + ["--job_name=ps", f"--task_id={j}"], tmp_path / f"ps{j}.log")))
+    for i in range(num_workers):
+        procs.append(("w", i, _spawn_main(common + ["--job_name=worker", f"--task_id={i}"],
+                                          tmp_path / f"w{i}.log")))
+    t0 = time.time()
+    for kind, i, p in procs:
+        try:
+            p.wait(timeout=max(5, 240 - (time.time() - t0)))
+        except subprocess.TimeoutExpired:
+            for _, _, q in procs:
+                q.kill()
+            pytest.fail(f"{kind}{i} hung:\n" + open(tmp_path / f"{'ps' if kind == 'ps' else 'w'}{i}.log").read())
+    logs = {f"{k}{i}": open(tmp_path / f"{'ps' if k == 'ps' else 'w'}{i}.log").read() for k, i, _ in procs}
+    for (k, i, p) in procs:
+        assert p.returncode == 0, logs[f"{k}{i}"][-3000:]
+    assert "applied 40 update(s)" in logs["ps0"]                   # exactly max_steps pushes applied
+    assert "global_step 40" in logs["ps0"]
+    assert "result: global_step=40" in logs["w0"]
+    from distributed_tensorflow_ibm_mnist_amd.ckpt.bundle import read_index
+    from distributed_tensorflow_ibm_mnist_amd.ckpt.saver import Saver, latest_checkpoint
+    prefix = latest_checkpoint(d)
+    assert prefix.endswith("model.ckpt-40")
+    n, idx = read_index(prefix)
+    assert n == num_ps                                              # one data shard per PS
+    t = Saver.restore(prefix)
+    assert int(t["global_step"]) == 40 and "hidden/weights/Momentum" in t

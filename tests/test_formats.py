@@ -1,0 +1,141 @@
+"""T1: native formats — crc32c, TFRecord, tf.Example, IDX/PNG, tensor bundle,
+checkpoint state, event files."""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from distributed_tensorflow_ibm_mnist_amd.ops._ext import host
+
+
+def test_crc32c_known_values():
+    H = host()
+    assert H.crc32c(b"123456789") == 0xE3069283          # CRC-32C check value
+    assert H.crc32c(b"") == 0
+    assert H.crc32c(b"\x00" * 32) == 0x8A9136AA          # RFC 3720 test vector
+    assert H.crc32c(bytes(range(32))) == 0x46DD794E
+    # masked form used by TFRecord / tensor bundles
+    c = H.crc32c(b"abc")
+    assert H.masked_crc32c(b"abc") == ((((c >> 15) | (c << 17)) & 0xFFFFFFFF) + 0xA282EAD8) & 0xFFFFFFFF
+
+
+def test_tfrecord_roundtrip_and_corruption(tmp_path):
+    from distributed_tensorflow_ibm_mnist_amd.data.tfrecord import TFRecordWriter, read_records
+    p = str(tmp_path / "x.tfrecords")
+    recs = [b"", b"a", os.urandom(1000), b"z" * 70000]
+    with TFRecordWriter(p) as w:
+        for r in recs:
+            w.write(r)
+    assert read_records(p) == recs
+    raw = bytearray(open(p, "rb").read())
+    # frame layout: u64 len | u32 masked crc(len) | data | u32 masked crc(data)
+    assert struct.unpack("<Q", raw[:8])[0] == 0
+    raw[28] ^= 0xFF   # payload byte of record #1 (record #0 is a 16-byte empty frame)
+    open(p, "wb").write(bytes(raw))
+    with pytest.raises(RuntimeError):
+        read_records(p)
+
+
+def test_example_codec_and_native_decode(tmp_path):
+    from distributed_tensorflow_ibm_mnist_amd.data.tfrecord import (decode_example, encode_example,
+                                                                    load_mnist_tfrecords, write_mnist_tfrecords)
+    ex = encode_example({"image_raw": b"\x01\x02\x03", "label": 7, "f": [1.5, 2.0]})
+    d = decode_example(ex)
+    assert d["image_raw"] == b"\x01\x02\x03" and d["label"] == [7] and d["f"] == [1.5, 2.0]
+    imgs = np.random.randint(0, 256, (37, 2352), dtype=np.uint8)
+    labs = np.random.randint(0, 10, 37)
+    p = str(tmp_path / "m.tfrecords")
+    write_mnist_tfrecords(p, imgs, labs)
+    x, y, c = load_mnist_tfrecords([p])
+    assert c == 3 and np.array_equal(x, imgs) and np.array_equal(y, labs)
+    with pytest.raises(ValueError):
+        load_mnist_tfrecords([str(tmp_path / "missing-*.tfrecords")])
+
+
+def test_idx_png_roundtrip(tmp_path):
+    from distributed_tensorflow_ibm_mnist_amd.data import idx
+    imgs = np.random.randint(0, 256, (12, 28, 28), dtype=np.uint8)
+    labs = np.arange(12) % 10
+    idx.write_idx(str(tmp_path / "train"), imgs, labs)
+    lab, pix, n, r, c = idx.read("training", str(tmp_path))
+    assert (n, r, c) == (12, 28, 28) and np.array_equal(pix.reshape(n, r, c), imgs) and np.array_equal(lab, labs)
+    idx.write_dataset(lab, pix, n, r, c, str(tmp_path / "png"))
+    assert sorted(os.listdir(tmp_path / "png")) == [str(i) for i in range(10)]
+    back, bl = idx.load_png_tree(str(tmp_path / "png"))
+    order = np.lexsort((np.arange(len(bl)), bl))
+    # PIL decodes our PNG encoder's output bit-exactly
+    from PIL import Image
+    im = np.asarray(Image.open(tmp_path / "png" / "3" / "3.png"))
+    assert np.array_equal(im, imgs[3])
+    assert back.shape == (12, 784) and sorted(bl.tolist()) == sorted(labs.tolist())
+
+
+def test_crop_or_pad_tf_semantics():
+    from distributed_tensorflow_ibm_mnist_amd.data.idx import crop_or_pad
+    a = np.arange(30 * 32).reshape(30, 32, 1)
+    c = crop_or_pad(a, 28, 28)
+    assert np.array_equal(c[..., 0], a[1:29, 2:30, 0])
+    b = np.ones((20, 26, 1))
+    p = crop_or_pad(b, 28, 28)
+    assert p[4:24, 1:27].all() and p.sum() == 20 * 26
+
+
+def test_bundle_roundtrip_sharded(tmp_path):
+    from distributed_tensorflow_ibm_mnist_amd.ckpt.bundle import read_bundle, read_index, write_bundle
+    t = {"conv1/weights": np.random.randn(5, 5, 3, 32).astype(np.float32),
+         "conv1/biases": np.zeros(32, np.float32),
+         "global_step": np.asarray(1234, dtype=np.int64),
+         "local3/weights": np.random.randn(300, 40).astype(np.float32)}
+    prefix = str(tmp_path / "model.ckpt-1234")
+    write_bundle(prefix, t, num_shards=2, shard_of={"local3/weights": 1})
+    assert os.path.exists(prefix + ".data-00000-of-00002") and os.path.exists(prefix + ".data-00001-of-00002")
+    n, idx = read_index(prefix)
+    assert n == 2 and idx["local3/weights"]["shard"] == 1 and idx["global_step"]["shape"] == ()
+    assert idx["conv1/weights"]["dtype"] == 1 and idx["global_step"]["dtype"] == 9
+    back = read_bundle(prefix)
+    for k in t:
+        assert np.array_equal(back[k], t[k]) and back[k].dtype == t[k].dtype
+    # corrupt a data byte -> checksum error
+    d = bytearray(open(prefix + ".data-00001-of-00002", "rb").read())
+    d[10] ^= 1
+    open(prefix + ".data-00001-of-00002", "wb").write(bytes(d))
+    with pytest.raises(IOError):
+        read_bundle(prefix)
+
+
+def test_sstable_many_entries_multiblock():
+    H = host()
+    ents = [(f"var/{i:06d}".encode(), os.urandom(900)) for i in range(1000)]   # > one 256 KiB block
+    blob = H.sstable_build(ents)
+    assert H.sstable_parse(blob) == ents
+    with pytest.raises(RuntimeError):
+        H.sstable_build([(b"b", b""), (b"a", b"")])
+
+
+def test_saver_max_to_keep_and_state_file(tmp_path):
+    from distributed_tensorflow_ibm_mnist_amd.ckpt.saver import Saver, get_checkpoint_state, latest_checkpoint
+    s = Saver(max_to_keep=3)
+    for step in (0, 10, 20, 30, 40):
+        s.save(str(tmp_path), step, {"w": np.full(4, step, np.float32), "global_step": np.int64(step)})
+    st = get_checkpoint_state(str(tmp_path))
+    assert st.model_checkpoint_path.endswith("model.ckpt-40")
+    assert [os.path.basename(p) for p in st.all_model_checkpoint_paths] == [
+        "model.ckpt-20", "model.ckpt-30", "model.ckpt-40"]
+    assert not os.path.exists(tmp_path / "model.ckpt-0.index")
+    txt = open(tmp_path / "checkpoint").read()
+    assert txt.startswith('model_checkpoint_path: "model.ckpt-40"')
+    assert Saver.restore(latest_checkpoint(str(tmp_path)))["w"][0] == 40
+
+
+def test_event_file_roundtrip(tmp_path):
+    from distributed_tensorflow_ibm_mnist_amd.obs.events import EventFileWriter, find_event_files, read_events
+    w = EventFileWriter(str(tmp_path))
+    w.add_scalars({"train loss": 1.25, "train accuracy": 0.5}, 10)
+    w.add_histograms({"conv1/weight": np.random.randn(1000)}, 10)
+    w.close()
+    evs = list(read_events(find_event_files(str(tmp_path))[0]))
+    assert evs[0]["file_version"] == "brain.Event:2"
+    assert evs[1]["step"] == 10 and evs[1]["values"]["train loss"] == 1.25
+    h = evs[2]["values"]["conv1/weight"]
+    assert h["num"] == 1000 and sum(h["bucket"]) == 1000

@@ -160,7 +160,6 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_k(const bf16_t* __restrict
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   for (int e = tid; e < IMGS * G::TILE; e += NTH) tile[e] = 0;
-  for (int e = tid; e < G::KM * G::NCOL; e += NTH) red[e] = 0.f;
 
   int dk[G::MFW];
   int kind[G::MFW];  // 0: im2col column, 1: bias ones-row, 2: zero pad
@@ -242,14 +241,22 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_k(const bf16_t* __restrict
       }
     }
   }
-  // cross-wave reduction in LDS, then one fp32 slab per block
-  __syncthreads();
+  // cross-wave reduction in LDS in a FIXED wave order (bitwise reproducible:
+  // no float atomics), then one fp32 slab per block
+  for (int wv = 0; wv < NTH / 64; ++wv) {
+    __syncthreads();
+    if (wave == wv) {
 #pragma unroll
-  for (int mf = 0; mf < G::MFW; ++mf)
+      for (int mf = 0; mf < G::MFW; ++mf)
 #pragma unroll
-    for (int nf = 0; nf < G::NF; ++nf)
+        for (int nf = 0; nf < G::NF; ++nf)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) atomicAdd(&red[(mf * 16 + 4 * g + r) * G::NCOL + nf * 16 + li], acc[mf][nf][r]);
+          for (int r = 0; r < 4; ++r) {
+            float& dst = red[(mf * 16 + 4 * g + r) * G::NCOL + nf * 16 + li];
+            dst = (wv == 0) ? acc[mf][nf][r] : dst + acc[mf][nf][r];
+          }
+    }
+  }
   __syncthreads();
   float* out = slab + (int64_t)blockIdx.x * G::KM * G::COUT;
   for (int e = tid; e < G::KM * G::COUT; e += NTH) {

@@ -59,3 +59,20 @@ DEV int xcd_remap(int bid, int nwg) {
   int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
   return base + loc;
 }
+
+// Exact division by a runtime-invariant divisor for 0 <= n < 2^31
+// (round-up multiplier, Granlund-Montgomery): q = mulhi(n, m) >> (l - 1),
+// l = ceil(log2 d).  Replaces ~40-instruction integer divides in index math.
+struct FastDiv {
+  uint32_t d, m, sh;
+  __host__ __device__ FastDiv() : d(1), m(0), sh(0) {}
+  __host__ explicit FastDiv(uint32_t div) : d(div), m(0), sh(0) {
+    if (div <= 1) return;
+    uint32_t l = 0;
+    while ((1ull << l) < div) ++l;
+    m = (uint32_t)(((1ull << (31 + l)) + div - 1) / div);
+    sh = l - 1;
+  }
+  DEV int div(int n) const { return m ? (int)(__umulhi((uint32_t)n, m) >> sh) : n; }
+  DEV int mod(int n, int q) const { return n - q * (int)d; }
+};

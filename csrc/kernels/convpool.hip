@@ -30,11 +30,24 @@
 namespace mnistx {
 namespace {
 
+// smallest column count >= c whose byte width (c * cin * 2) is a multiple of 16
+constexpr int align_cols(int c, int cin) {
+  while ((c * cin * 2) % 16 != 0) ++c;
+  return c;
+}
+
 template <int CIN_, int COUT_, int KS_, int PAD_, int H_, int W_>
 struct Geo {
   static constexpr int CIN = CIN_, COUT = COUT_, KS = KS_, PAD = PAD_, H = H_, W = W_;
   static constexpr int HP = H + 2 * PAD, WP = W + 2 * PAD;
   static constexpr int OH = HP - KS + 1, OW = WP - KS + 1;
+  // LDS tile rows: the interior starts at column X0 >= PAD and every row is a
+  // multiple of 16 bytes, so the interior rows are filled with 8-byte vectors.
+  static constexpr int X0 = align_cols(PAD, CIN);
+  static constexpr int WS = align_cols(X0 + W + PAD, CIN);
+  static constexpr int XOFF = X0 - PAD;
+  static constexpr int ROWV = W * CIN / 4;            // 8-byte vectors per interior row
+  static_assert((W * CIN) % 4 == 0, "interior rows must be whole 8-byte vectors");
   static constexpr int PH = OH / 2, PW = OW / 2;
   static constexpr int NWIN = PH * PW;
   static constexpr int NPIX = OH * OW;
@@ -43,7 +56,7 @@ struct Geo {
   static constexpr int KSTEPS = (KC + 31) / 32;
   static constexpr int NF = (COUT + 15) / 16;
   static constexpr int NCOL = NF * 16;
-  static constexpr int TILE = HP * WP * CIN;
+  static constexpr int TILE = HP * WS * CIN;
   static constexpr int INTERIOR = H * W * CIN;
   static constexpr int KM = ((KC + 1) + 15) / 16 * 16;  // wgrad rows incl. the bias (ones) row
   static constexpr int MFW = KM / 16;
@@ -55,19 +68,33 @@ struct Geo {
   static DEV int kdelta(int k) {
     const int tap = k / CIN, ci = k - (k / CIN) * CIN;
     const int kh = tap / KS, kw = tap - (tap / KS) * KS;
-    return (kh * WP + kw) * CIN + ci;
+    return (kh * WS + kw) * CIN + ci;
   }
   // LDS offset of the top-left input pixel feeding pool window w
   static DEV int wbase(int w) {
     const int ph = w / PW, pw = w - (w / PW) * PW;
-    return ((2 * ph) * WP + 2 * pw) * CIN;
+    return ((2 * ph) * WS + 2 * pw + XOFF) * CIN;
   }
-  static DEV int doff(int d) { return ((d >> 1) * WP + (d & 1)) * CIN; }
+  static DEV int doff(int d) { return ((d >> 1) * WS + (d & 1)) * CIN; }
 };
 
 DEV __bf16 as_bf(bf16_t v) { return __builtin_bit_cast(__bf16, v); }
 
 constexpr int NTH = 256;
+
+// Copy IMGS input images (NHWC, interior only) into their LDS tiles with
+// 8-byte vectors; the zero border written once at kernel start is untouched.
+template <class G, int IMGS>
+DEV void fill_tiles(bf16_t* tile, const bf16_t* __restrict__ x, int img0, int B, int tid) {
+  constexpr int NV = IMGS * G::H * G::ROWV;
+  for (int e = tid; e < NV; e += NTH) {
+    const int im = e / (G::H * G::ROWV), rem = e - im * (G::H * G::ROWV);
+    const int hh = rem / G::ROWV, vv = rem - hh * G::ROWV;
+    u32x2 v = {0u, 0u};
+    if (img0 + im < B) v = *(const u32x2*)(x + (int64_t)(img0 + im) * G::INTERIOR + hh * G::W * G::CIN + 4 * vv);
+    *(u32x2*)(tile + im * G::TILE + ((hh + G::PAD) * G::WS + G::X0) * G::CIN + 4 * vv) = v;
+  }
+}
 
 // ------------------------------------------------------------------ forward
 template <class G, int IMGS>
@@ -102,12 +129,7 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_k(const bf16_t* __restrict__
 
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += gridDim.x * IMGS) {
     __syncthreads();
-    for (int e = tid; e < IMGS * G::INTERIOR; e += NTH) {
-      const int im = e / G::INTERIOR, rem = e - im * G::INTERIOR;
-      const int hh = rem / (G::W * G::CIN), r2 = rem - hh * (G::W * G::CIN);
-      bf16_t v = (img0 + im < B) ? x[(int64_t)(img0 + im) * G::INTERIOR + rem] : (bf16_t)0;
-      tile[im * G::TILE + (hh + G::PAD) * G::WP * G::CIN + G::PAD * G::CIN + r2] = v;
-    }
+    fill_tiles<G, IMGS>(tile, x, img0, B, tid);
     __syncthreads();
     for (int f = wave; f < IMGS * G::MF; f += NTH / 64) {
       const int im = f / G::MF, fm = f - im * G::MF;
@@ -155,7 +177,7 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_k(const bf16_t* __restrict
                                                         float* __restrict__ slab) {
   __shared__ __attribute__((aligned(16))) bf16_t tile[IMGS * G::TILE];
   __shared__ __attribute__((aligned(16))) bf16_t dys[IMGS * G::NWIN * G::COUT];
-  __shared__ uint8_t args[IMGS * G::NWIN * G::COUT];
+  __shared__ __attribute__((aligned(16))) uint8_t args[IMGS * G::NWIN * G::COUT];
   __shared__ float red[G::KM * G::NCOL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -178,24 +200,24 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_k(const bf16_t* __restrict
   constexpr int DEL = IMGS * G::NWIN * G::COUT;
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += gridDim.x * IMGS) {
     __syncthreads();
-    for (int e = tid; e < IMGS * G::INTERIOR; e += NTH) {
-      const int im = e / G::INTERIOR, rem = e - im * G::INTERIOR;
-      const int hh = rem / (G::W * G::CIN), r2 = rem - hh * (G::W * G::CIN);
-      bf16_t v = (img0 + im < B) ? x[(int64_t)(img0 + im) * G::INTERIOR + rem] : (bf16_t)0;
-      tile[im * G::TILE + (hh + G::PAD) * G::WP * G::CIN + G::PAD * G::CIN + r2] = v;
-    }
-    for (int e = tid; e < DEL; e += NTH) {
+    fill_tiles<G, IMGS>(tile, x, img0, B, tid);
+    static_assert(DEL % 8 == 0, "");
+    for (int e8 = tid; e8 < DEL / 8; e8 += NTH) {
+      const int e = 8 * e8;
       const int im = e / (G::NWIN * G::COUT);
-      bf16_t v = 0;
-      uint8_t a = 0xff;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      u32x2 a = {0xffffffffu, 0xffffffffu};
       if (img0 + im < B) {
         const int64_t o = (int64_t)img0 * G::NWIN * G::COUT + e;
-        const bf16_t p = P[o];
-        v = (bf2f(p) > 0.f) ? dP[o] : (bf16_t)0;  // ReLU mask: pooled value > 0
-        a = arg[o];
+        const u32x4 pv = *(const u32x4*)(P + o);
+        v = *(const u32x4*)(dP + o);
+        a = *(const u32x2*)(arg + o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (!(u4_get(pv, j) > 0.f)) u4_set(v, j, 0);   // ReLU mask: pooled value > 0
       }
-      dys[e] = v;
-      args[e] = a;
+      *(u32x4*)(dys + e) = v;
+      *(u32x2*)(args + e) = a;
     }
     __syncthreads();
     for (int it = wave; it < IMGS * G::RSTEPS; it += NTH / 64) {
@@ -310,21 +332,32 @@ __global__ __launch_bounds__(NTH) void convpool_dgrad_k(const bf16_t* __restrict
   constexpr int NWC = G::NWIN * G::COUT;
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += gridDim.x * IMGS) {
     __syncthreads();
-    for (int e = tid; e < IMGS * NWC; e += NTH) {
+    for (int e8 = tid; e8 < IMGS * NWC / 8; e8 += NTH) {
+      const int e = 8 * e8;
       const int im = e / NWC, rem = e - im * NWC;
       const int win = rem / G::COUT, co = rem - win * G::COUT;
-      bf16_t v = 0;
-      int a = 0xff;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      u32x2 a = {0xffffffffu, 0xffffffffu};
       if (img0 + im < B) {
         const int64_t o = (int64_t)img0 * NWC + e;
-        v = (bf2f(P[o]) > 0.f) ? dP[o] : (bf16_t)0;
-        a = arg[o];
+        const u32x4 pv = *(const u32x4*)(P + o);
+        v = *(const u32x4*)(dP + o);
+        a = *(const u32x2*)(arg + o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (!(u4_get(pv, j) > 0.f)) u4_set(v, j, 0);
       }
       const int ph = win / G::PW, pw = win - ph * G::PW;
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         const int oh = 2 * ph + (d >> 1) + Q, ow = 2 * pw + (d & 1) + Q;
-        dyt[im * DT + (oh * OWQ + ow) * G::COUT + co] = (a == d) ? v : (bf16_t)0;
+        u32x4 o = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t aj = ((j < 4 ? a[0] : a[1]) >> (8 * (j & 3))) & 0xff;
+          if (aj == (uint32_t)d) u4_set(o, j, (bf16_t)((v[j >> 1] >> (16 * (j & 1))) & 0xffff));
+        }
+        *(u32x4*)(dyt + im * DT + (oh * OWQ + ow) * G::COUT + co) = o;
       }
     }
     __syncthreads();

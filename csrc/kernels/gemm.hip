@@ -68,19 +68,19 @@ struct Im2colK {
   int OH, OW;           // output spatial
   int KH, KW, ph, pw;   // stride 1
   int M, K;
+  FastDiv fOHW, fOW, fC, fKW;
   DEV u32x4 load(int m, int k) const {
     u32x4 v = {0u, 0u, 0u, 0u};
     if (m >= M || k >= K) return v;
-    const int ohw = OH * OW;
-    const int n = m / ohw;
-    const int rem = m - n * ohw;
-    const int oh = rem / OW;
-    const int ow = rem - oh * OW;
+    const int n = fOHW.div(m);
+    const int rem = fOHW.mod(m, n);
+    const int oh = fOW.div(rem);
+    const int ow = fOW.mod(rem, oh);
     if ((C & 7) == 0) {
-      const int tap = k / C;
-      const int ci = k - tap * C;
-      const int kh = tap / KW;
-      const int kw = tap - kh * KW;
+      const int tap = fC.div(k);
+      const int ci = fC.mod(k, tap);
+      const int kh = fKW.div(tap);
+      const int kw = fKW.mod(tap, kh);
       const int ih = oh - ph + kh, iw = ow - pw + kw;
       if (ih < 0 || ih >= H || iw < 0 || iw >= W) return v;
       return *(const u32x4*)(x + (((int64_t)n * H + ih) * W + iw) * C + ci);
@@ -111,19 +111,19 @@ struct Im2colMN {
   int KH, KW, ph, pw;
   int P, Mreal;
   int ones;  // 1: append the ones column at Mreal
+  FastDiv fOHW, fOW, fC, fKW;
   DEV u32x4 load(int p, int m) const {
     u32x4 v = {0u, 0u, 0u, 0u};
     if (p >= P) return v;
-    const int ohw = OH * OW;
-    const int n = p / ohw;
-    const int rem = p - n * ohw;
-    const int oh = rem / OW;
-    const int ow = rem - oh * OW;
+    const int n = fOHW.div(p);
+    const int rem = fOHW.mod(p, n);
+    const int oh = fOW.div(rem);
+    const int ow = fOW.mod(rem, oh);
     if ((C & 7) == 0 && m + 8 <= Mreal) {
-      const int tap = m / C;
-      const int ci = m - tap * C;
-      const int kh = tap / KW;
-      const int kw = tap - kh * KW;
+      const int tap = fC.div(m);
+      const int ci = fC.mod(m, tap);
+      const int kh = fKW.div(tap);
+      const int kw = fKW.mod(tap, kh);
       const int ih = oh - ph + kh, iw = ow - pw + kw;
       if (ih >= 0 && ih < H && iw >= 0 && iw < W)
         v = *(const u32x4*)(x + (((int64_t)n * H + ih) * W + iw) * C + ci);
@@ -152,11 +152,12 @@ struct Im2colMN {
 struct WFlipK {
   const bf16_t* w;  // [T][Cin_p][Cout_p]
   int T, Cin, Cout;
+  FastDiv fCout;
   DEV u32x4 load(int ci, int k) const {
     u32x4 v = {0u, 0u, 0u, 0u};
     if (ci >= Cin || k >= T * Cout) return v;
-    const int tp = k / Cout;
-    const int co = k - tp * Cout;
+    const int tp = fCout.div(k);
+    const int co = fCout.mod(k, tp);
     const int tap = T - 1 - tp;
     return *(const u32x4*)(w + ((int64_t)tap * Cin + ci) * Cout + co);
   }
@@ -402,7 +403,8 @@ hipError_t dense_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int
 hipError_t conv_fwd(const bf16_t* x, const bf16_t* w, int Nb, int H, int W, int C, int OH, int OW, int KH,
                     int KW, int ph, int pw, int Cout, const GemmEpi& ep, hipStream_t st) {
   const int M = Nb * OH * OW, K = KH * KW * C;
-  Im2colK a{x, H, W, C, OH, OW, KH, KW, ph, pw, M, K};
+  Im2colK a{x, H, W, C, OH, OW, KH, KW, ph, pw, M, K,
+            FastDiv(OH * OW), FastDiv(OW), FastDiv(C), FastDiv(KW)};
   MatLoader b{w, K, Cout, Cout, -1};
   return launch_any<Im2colK, true, MatLoader, false>(a, b, ep, M, Cout, K, 1, st);
 }
@@ -411,8 +413,9 @@ hipError_t conv_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int OH, int OW,
                       int KH, int KW, int ph, int pw, int Cin, const GemmEpi& ep, hipStream_t st) {
   // dX = conv(dY, flip(W)^T) with pad' = K-1-pad, over the dY image.
   const int M = Nb * H * W, K = KH * KW * Cout;
-  Im2colK a{dy, OH, OW, Cout, H, W, KH, KW, KH - 1 - ph, KW - 1 - pw, M, K};
-  WFlipK b{w, KH * KW, Cin, Cout};
+  Im2colK a{dy, OH, OW, Cout, H, W, KH, KW, KH - 1 - ph, KW - 1 - pw, M, K,
+            FastDiv(H * W), FastDiv(W), FastDiv(Cout), FastDiv(KW)};
+  WFlipK b{w, KH * KW, Cin, Cout, FastDiv(Cout)};
   return launch_any<Im2colK, true, WFlipK, true>(a, b, ep, M, Cin, K, 1, st);
 }
 
@@ -420,7 +423,8 @@ hipError_t conv_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int H, int W, i
                       int KW, int ph, int pw, int Cout, int with_bias, int splits, const GemmEpi& ep,
                       hipStream_t st) {
   const int P = Nb * OH * OW, Mreal = KH * KW * C;
-  Im2colMN a{x, H, W, C, OH, OW, KH, KW, ph, pw, P, Mreal, with_bias};
+  Im2colMN a{x, H, W, C, OH, OW, KH, KW, ph, pw, P, Mreal, with_bias,
+             FastDiv(OH * OW), FastDiv(OW), FastDiv(C), FastDiv(KW)};
   MatLoader b{dy, P, Cout, Cout, -1};
   return launch_any<Im2colMN, false, MatLoader, false>(a, b, ep, Mreal + (with_bias ? 1 : 0), Cout, P, splits,
                                                        st);

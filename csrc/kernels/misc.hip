@@ -139,77 +139,107 @@ __global__ void maxpool_bwd_k(const bf16_t* __restrict__ dy, const uint8_t* __re
 }
 
 // ------------------------------------------------------------------ K7 LRN (TF semantics)
-// y[c] = x[c] * (bias + alpha * sum_{|c'-c|<=r} x[c']^2)^-beta
+// y[c] = x[c] * (bias + alpha * sum_{|c'-c|<=R} x[c']^2)^-beta
+// One thread per pixel, all C channels in registers; R is a compile-time
+// constant so the window sums are fully unrolled with static indices (no
+// runtime-guarded adds, no scratch).  Inputs stay bf16-packed in VGPRs.
 template <int C>
-__global__ void lrn_fwd_k(const bf16_t* __restrict__ x, int64_t P, int r, float bias, float alpha, float beta,
-                          bf16_t* __restrict__ y) {
+DEV void load_row(const bf16_t* p, uint32_t (&w)[C / 2]) {
+#pragma unroll
+  for (int c8 = 0; c8 < C / 8; ++c8) {
+    const u32x4 u = *(const u32x4*)(p + c8 * 8);
+    w[4 * c8 + 0] = u[0];
+    w[4 * c8 + 1] = u[1];
+    w[4 * c8 + 2] = u[2];
+    w[4 * c8 + 3] = u[3];
+  }
+}
+
+template <int C>
+DEV float unpk(const uint32_t (&w)[C / 2], int c) {
+  return (c & 1) ? __uint_as_float(w[c >> 1] & 0xffff0000u) : __uint_as_float(w[c >> 1] << 16);
+}
+
+template <int C, int R>
+DEV void window_sums(const float (&v)[C], float (&s)[C]) {
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    float a = 0.f;
+#pragma unroll
+    for (int d = -R; d <= R; ++d)
+      if (c + d >= 0 && c + d < C) a += v[c + d];
+    s[c] = a;
+  }
+}
+
+template <int C, int R>
+__global__ __launch_bounds__(TPB) void lrn_fwd_k(const bf16_t* __restrict__ x, int64_t P, float bias, float alpha,
+                                                 float beta, bf16_t* __restrict__ y) {
   for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < P; p += (int64_t)gridDim.x * blockDim.x) {
-    float v[C], sq[C];
+    uint32_t xw[C / 2];
+    load_row<C>(x + p * C, xw);
+    float sq[C], s[C];
 #pragma unroll
-    for (int c8 = 0; c8 < C / 8; ++c8) {
-      const u32x4 u = *(const u32x4*)(x + p * C + c8 * 8);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { v[c8 * 8 + j] = u4_get(u, j); sq[c8 * 8 + j] = v[c8 * 8 + j] * v[c8 * 8 + j]; }
+    for (int c = 0; c < C; ++c) {
+      const float v = unpk<C>(xw, c);
+      sq[c] = v * v;
     }
+    window_sums<C, R>(sq, s);
 #pragma unroll
     for (int c8 = 0; c8 < C / 8; ++c8) {
       u32x4 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = c8 * 8 + j;
-        float s = 0.f;
-#pragma unroll
-        for (int d = -8; d <= 8; ++d)
-          if (d >= -r && d <= r && c + d >= 0 && c + d < C) s += sq[c + d];
-        const float sc = bias + alpha * s;
-        u4_set(o, j, f2bf(v[c] * __expf(-beta * __logf(sc))));
+      for (int j = 0; j < 4; ++j) {
+        const int c = c8 * 8 + 2 * j;
+        const float a = unpk<C>(xw, c) * __expf(-beta * __logf(bias + alpha * s[c]));
+        const float b = unpk<C>(xw, c + 1) * __expf(-beta * __logf(bias + alpha * s[c + 1]));
+        o[j] = pack2(a, b);
       }
       *(u32x4*)(y + p * C + c8 * 8) = o;
     }
   }
 }
 
-// dx[c] = dy[c] s[c]^-b - 2ab x[c] sum_{|c'-c|<=r} dy[c'] x[c'] s[c']^(-b-1)
-template <int C>
-__global__ void lrn_bwd_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, int64_t P, int r, float bias,
-                          float alpha, float beta, int relu_mask, bf16_t* __restrict__ dx) {
+// dx[c] = dy[c] s[c]^-b - 2ab x[c] sum_{|c'-c|<=R} dy[c'] x[c'] s[c']^(-b-1)
+template <int C, int R>
+__global__ __launch_bounds__(TPB) void lrn_bwd_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                                 int64_t P, float bias, float alpha, float beta, int relu_mask,
+                                                 bf16_t* __restrict__ dx) {
   for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < P; p += (int64_t)gridDim.x * blockDim.x) {
-    float v[C], sq[C], t[C], pb[C];
-#pragma unroll
-    for (int c8 = 0; c8 < C / 8; ++c8) {
-      const u32x4 u = *(const u32x4*)(x + p * C + c8 * 8);
-      const u32x4 g = *(const u32x4*)(dy + p * C + c8 * 8);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        v[c8 * 8 + j] = u4_get(u, j);
-        sq[c8 * 8 + j] = v[c8 * 8 + j] * v[c8 * 8 + j];
-        t[c8 * 8 + j] = u4_get(g, j);
-      }
-    }
+    uint32_t xw[C / 2], gw[C / 2];
+    load_row<C>(x + p * C, xw);
+    load_row<C>(dy + p * C, gw);
+    float t[C], s[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      float s = 0.f;
-#pragma unroll
-      for (int d = -8; d <= 8; ++d)
-        if (d >= -r && d <= r && c + d >= 0 && c + d < C) s += sq[c + d];
-      const float sc = bias + alpha * s;
-      const float pw = __expf(-beta * __logf(sc));  // s^-b
-      pb[c] = pw;
-      sq[c] = t[c] * v[c] * pw / sc;  // reuse: dy*x*s^(-b-1)
+      const float v = unpk<C>(xw, c);
+      t[c] = v * v;
     }
+    window_sums<C, R>(t, s);                       // s = window sum of x^2
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float sc = bias + alpha * s[c];
+      const float pw = __expf(-beta * __logf(sc));  // sc^-beta
+      s[c] = pw;                                     // keep sc^-beta
+      t[c] = unpk<C>(gw, c) * unpk<C>(xw, c) * pw / sc;
+    }
+    float u[C];
+    window_sums<C, R>(t, u);
 #pragma unroll
     for (int c8 = 0; c8 < C / 8; ++c8) {
       u32x4 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = c8 * 8 + j;
-        float s = 0.f;
+      for (int j = 0; j < 4; ++j) {
+        float r2[2];
 #pragma unroll
-        for (int d = -8; d <= 8; ++d)
-          if (d >= -r && d <= r && c + d >= 0 && c + d < C) s += sq[c + d];
-        float g = t[c] * pb[c] - 2.f * alpha * beta * v[c] * s;
-        if (relu_mask && !(v[c] > 0.f)) g = 0.f;
-        u4_set(o, j, f2bf(g));
+        for (int h = 0; h < 2; ++h) {
+          const int c = c8 * 8 + 2 * j + h;
+          const float xv = unpk<C>(xw, c);
+          float g = unpk<C>(gw, c) * s[c] - 2.f * alpha * beta * xv * u[c];
+          if (relu_mask && !(xv > 0.f)) g = 0.f;
+          r2[h] = g;
+        }
+        o[j] = pack2(r2[0], r2[1]);
       }
       *(u32x4*)(dx + p * C + c8 * 8) = o;
     }
@@ -317,62 +347,71 @@ __global__ void splitk_reduce_wave_k(const float* __restrict__ slab, int S, int 
 }
 
 // ------------------------------------------------------------------ K9 fused optimizer
+// Each workgroup owns one contiguous chunk of ONE segment (block -> segment
+// table built on the host), so there is no per-element segment search and the
+// L2 norm needed for the weight-decay loss is reduced in the workgroup and added
+// with a single atomic per workgroup.
 constexpr int MAXSEG = 16;
+constexpr int OPT_EPT = 8;                       // elements per thread
+constexpr int OPT_CHUNK = TPB * OPT_EPT;         // elements per workgroup
 struct SegTable {
   OptSeg s[MAXSEG];
+  int blk0[MAXSEG + 1];
   int n;
 };
 
-__global__ void fused_opt_k(float* __restrict__ params, const float* __restrict__ grads, float* __restrict__ mom,
-                            float* __restrict__ ema, bf16_t* __restrict__ bf, SegTable tab, int64_t total,
-                            const int64_t* __restrict__ step_p, OptParams op, float* __restrict__ l2) {
+__global__ __launch_bounds__(TPB) void fused_opt_k(float* __restrict__ params, const float* __restrict__ grads,
+                                                   float* __restrict__ mom, float* __restrict__ ema,
+                                                   bf16_t* __restrict__ bf, SegTable tab,
+                                                   const int64_t* __restrict__ step_p, OptParams op,
+                                                   float* __restrict__ l2) {
+  __shared__ float red[TPB / 64];
+  int si = 0;
+  while (si + 1 < tab.n && (int)blockIdx.x >= tab.blk0[si + 1]) ++si;
+  const OptSeg sg = tab.s[si];
   const int64_t step = *step_p;
   float lr = op.lr0;
   if (op.decay_steps > 0) lr *= powf(op.decay_rate, (float)(step / op.decay_steps));  // staircase
   float ema_d = 0.f;
   if (op.ema_max >= 0.f) ema_d = fminf(op.ema_max, (1.f + (float)step) / (10.f + (float)step));
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e - threadIdx.x < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    int si = -1;
-    float sq = 0.f;
-    if (e < total) {
-      si = 0;
-      while (si + 1 < tab.n && e >= tab.s[si + 1].off) ++si;
-      const OptSeg sg = tab.s[si];
-      float p = params[e];
-      sq = p * p;
-      float g = grads[e] * op.grad_scale + sg.wd * p;
-      float upd = g;
-      if (op.use_momentum) {
-        const float v = mom[e] * op.momentum + g;
-        mom[e] = v;
-        upd = op.nesterov ? g + op.momentum * v : v;
-      }
-      p -= lr * upd;
-      params[e] = p;
-      if (op.ema_max >= 0.f) {
-        const float s = ema[e];
-        ema[e] = s - (1.f - ema_d) * (s - p);
-      }
-      if (sg.bf_off >= 0) {
-        const int64_t li = e - sg.off;
-        const int64_t ij = (int64_t)sg.I * sg.J;
-        const int gg = (int)(li / ij);
-        const int64_t rem = li - gg * ij;
-        const int ii = (int)(rem / sg.J), jj = (int)(rem - (int64_t)ii * sg.J);
-        bf[sg.bf_off + ((int64_t)gg * sg.Ip + ii) * sg.Jp + jj] = f2bf(p);
-      }
-      if (!sg.track_l2) si = -1;
-      else si = sg.track_l2 - 1;
+  const int64_t lo = (int64_t)(blockIdx.x - tab.blk0[si]) * OPT_CHUNK;
+  const int64_t ij = (int64_t)sg.I * sg.J;
+  float sq = 0.f;
+#pragma unroll
+  for (int u = 0; u < OPT_EPT; ++u) {
+    const int64_t li = lo + u * TPB + threadIdx.x;
+    if (li >= sg.n) continue;
+    const int64_t e = sg.off + li;
+    float p = params[e];
+    sq += p * p;
+    const float g = grads[e] * op.grad_scale + sg.wd * p;
+    float upd = g;
+    if (op.use_momentum) {
+      const float v = mom[e] * op.momentum + g;
+      mom[e] = v;
+      upd = op.nesterov ? g + op.momentum * v : v;
     }
-    if (l2) {
-      const int s0 = __shfl(si, 0, 64);
-      if (__all(si == s0)) {
-        const float t = warp_sum(sq);
-        if ((threadIdx.x & 63) == 0 && s0 >= 0) atomicAdd(&l2[s0], t);
-      } else if (si >= 0) {
-        atomicAdd(&l2[si], sq);
-      }
+    p -= lr * upd;
+    params[e] = p;
+    if (op.ema_max >= 0.f) {
+      const float s = ema[e];
+      ema[e] = s - (1.f - ema_d) * (s - p);
+    }
+    if (sg.bf_off >= 0) {
+      const int gg = (int)(li / ij);
+      const int64_t rem = li - gg * ij;
+      const int ii = (int)(rem / sg.J), jj = (int)(rem - (int64_t)ii * sg.J);
+      bf[sg.bf_off + ((int64_t)gg * sg.Ip + ii) * sg.Jp + jj] = f2bf(p);
+    }
+  }
+  if (l2 && sg.track_l2) {
+    sq = warp_sum(sq);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.f;
+      for (int w = 0; w < TPB / 64; ++w) t += red[w];
+      atomicAdd(&l2[sg.track_l2 - 1], t);
     }
   }
 }
@@ -460,29 +499,25 @@ hipError_t maxpool_bwd(const bf16_t* dy, const uint8_t* arg, const bf16_t* y, in
   return hipGetLastError();
 }
 
-#define LRN_DISPATCH(KER, ...)                                                                   \
-  switch (C) {                                                                                   \
-    case 8: hipLaunchKernelGGL(KER<8>, grid, dim3(TPB), 0, st, __VA_ARGS__); break;               \
-    case 16: hipLaunchKernelGGL(KER<16>, grid, dim3(TPB), 0, st, __VA_ARGS__); break;             \
-    case 32: hipLaunchKernelGGL(KER<32>, grid, dim3(TPB), 0, st, __VA_ARGS__); break;             \
-    case 64: hipLaunchKernelGGL(KER<64>, grid, dim3(TPB), 0, st, __VA_ARGS__); break;             \
-    default: return hipErrorInvalidValue;                                                        \
-  }
+#define LRN_CASE(KER, CC, RR, ...) \
+  if (C == CC && r == RR) { hipLaunchKernelGGL((KER<CC, RR>), grid, dim3(TPB), 0, st, __VA_ARGS__); return hipGetLastError(); }
+#define LRN_ALL(KER, ...)                                                                                     \
+  LRN_CASE(KER, 8, 4, __VA_ARGS__) LRN_CASE(KER, 16, 4, __VA_ARGS__) LRN_CASE(KER, 32, 4, __VA_ARGS__)         \
+  LRN_CASE(KER, 64, 4, __VA_ARGS__) LRN_CASE(KER, 32, 2, __VA_ARGS__) LRN_CASE(KER, 64, 2, __VA_ARGS__)        \
+  LRN_CASE(KER, 32, 5, __VA_ARGS__) LRN_CASE(KER, 64, 5, __VA_ARGS__)
 
 hipError_t lrn_fwd(const bf16_t* x, int P, int C, int r, float bias, float alpha, float beta, bf16_t* y,
                    hipStream_t st) {
-  if (r > 8) return hipErrorInvalidValue;
   dim3 grid(nblocks(P, TPB, 16384));
-  LRN_DISPATCH(lrn_fwd_k, x, (int64_t)P, r, bias, alpha, beta, y);
-  return hipGetLastError();
+  LRN_ALL(lrn_fwd_k, x, (int64_t)P, bias, alpha, beta, y)
+  return hipErrorInvalidValue;  // (C, depth_radius) combination not instantiated
 }
 
 hipError_t lrn_bwd(const bf16_t* x, const bf16_t* dy, int P, int C, int r, float bias, float alpha, float beta,
                    int relu_mask, bf16_t* dx, hipStream_t st) {
-  if (r > 8) return hipErrorInvalidValue;
   dim3 grid(nblocks(P, TPB, 16384));
-  LRN_DISPATCH(lrn_bwd_k, x, dy, (int64_t)P, r, bias, alpha, beta, relu_mask, dx);
-  return hipGetLastError();
+  LRN_ALL(lrn_bwd_k, x, dy, (int64_t)P, bias, alpha, beta, relu_mask, dx)
+  return hipErrorInvalidValue;
 }
 
 hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B, int NC, float scale,
@@ -508,10 +543,16 @@ hipError_t fused_optimizer(float* params, const float* grads, float* mom, float*
                            int nseg, int64_t total, const int64_t* step, OptParams op, float* l2, hipStream_t st) {
   if (nseg > MAXSEG || nseg < 1) return hipErrorInvalidValue;
   SegTable tab;
-  for (int i = 0; i < nseg; ++i) tab.s[i] = segs[i];
+  int nb = 0;
+  for (int i = 0; i < nseg; ++i) {
+    tab.s[i] = segs[i];
+    tab.blk0[i] = nb;
+    nb += (int)((segs[i].n + OPT_CHUNK - 1) / OPT_CHUNK);
+  }
+  tab.blk0[nseg] = nb;
   tab.n = nseg;
-  hipLaunchKernelGGL(fused_opt_k, dim3(nblocks(total, TPB, 4096)), dim3(TPB), 0, st, params, grads, mom, ema, bf, tab,
-                     total, step, op, l2);
+  (void)total;
+  hipLaunchKernelGGL(fused_opt_k, dim3(nb), dim3(TPB), 0, st, params, grads, mom, ema, bf, tab, step, op, l2);
   return hipGetLastError();
 }
 

@@ -382,6 +382,15 @@ int64_t convpool_rows(int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64_
   return cp_geo(cin, cout, ks, pad, h, w).KM;
 }
 
+// (G, Ipad, I, bias_row) arguments of splitk_reduce for this geometry's wgrad slab
+std::vector<int64_t> convpool_reduce_args(int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t w,
+                                          int64_t cin_real) {
+  auto g = cp_geo(cin, cout, ks, pad, h, w);
+  int o[4];
+  TORCH_CHECK(mnistx::convpool_reduce_layout(g.cfg, o) == 0, "convpool_reduce_args");
+  return {o[0], o[1], o[2] < 0 ? cin_real : (int64_t)o[2], o[3]};
+}
+
 void convpool_fwd(Tensor x, Tensor w, Tensor bias, int64_t bias_n, Tensor pooled, Tensor arg, int64_t B, int64_t cin,
                   int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t wd) {
   auto g = cp_geo(cin, cout, ks, pad, h, wd);
@@ -446,6 +455,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("cast_f32_bf16_padded", &cast_f32_bf16_padded);
   m.def("convpool_supported", &convpool_supported);
   m.def("convpool_rows", &convpool_rows);
+  m.def("convpool_reduce_args", &convpool_reduce_args);
   m.def("convpool_fwd", &convpool_fwd);
   m.def("convpool_wgrad", &convpool_wgrad);
   m.def("convpool_dgrad", &convpool_dgrad);

@@ -76,3 +76,16 @@ struct FastDiv {
   DEV int div(int n) const { return m ? (int)(__umulhi((uint32_t)n, m) >> sh) : n; }
   DEV int mod(int n, int q) const { return n - q * (int)d; }
 };
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+DEV bf16x8 join(s16x4 lo, s16x4 hi) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+// Transposed LDS read (ds_read_b64_tr_b16): in each 16-lane group, lane 4q+p
+// supplies the address of 4 consecutive bf16 (row q, columns 4p..4p+3); lane i
+// of the group receives column i of the 4 rows.  Addresses must be 8-byte aligned.
+DEV s16x4 lds_tr4(const bf16_t* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p); }

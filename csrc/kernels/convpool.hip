@@ -36,6 +36,16 @@ constexpr int align_cols(int c, int cin) {
   return c;
 }
 
+// Row width (columns) for tiles read with ds_read_b64 by 16 pixels spanning two
+// image rows (pool-window-major): a row of 128 bytes mod 256 puts the second row
+// in the other half of the 64 banks.
+constexpr int bank_cols(int c, int cin) {
+  c = align_cols(c, cin);
+  if (cin % 4 != 0) return c;
+  while ((c * cin * 2) % 256 != 128) c += align_cols(1, cin);
+  return c;
+}
+
 template <int CIN_, int COUT_, int KS_, int PAD_, int H_, int W_>
 struct Geo {
   static constexpr int CIN = CIN_, COUT = COUT_, KS = KS_, PAD = PAD_, H = H_, W = W_;
@@ -44,7 +54,7 @@ struct Geo {
   // LDS tile rows: the interior starts at column X0 >= PAD and every row is a
   // multiple of 16 bytes, so the interior rows are filled with 8-byte vectors.
   static constexpr int X0 = align_cols(PAD, CIN);
-  static constexpr int WS = align_cols(X0 + W + PAD, CIN);
+  static constexpr int WS = bank_cols(X0 + W + PAD, CIN);
   static constexpr int XOFF = X0 - PAD;
   static constexpr int ROWV = W * CIN / 4;            // 8-byte vectors per interior row
   static_assert((W * CIN) % 4 == 0, "interior rows must be whole 8-byte vectors");
@@ -52,23 +62,50 @@ struct Geo {
   static constexpr int NWIN = PH * PW;
   static constexpr int NPIX = OH * OW;
   static constexpr int MF = (NPIX + 15) / 16;
-  static constexpr int KC = KS * KS * CIN;
-  static constexpr int KSTEPS = (KC + 31) / 32;
+  // im2col column order (K):
+  //  MODE 0 (Cin == 1):     k = kh*8 + kw, kw padded to 8.  Four consecutive k are
+  //                         four consecutive pixels of one input row; the image is
+  //                         kept in LDS 4 times, shifted by 0..3 elements, so every
+  //                         such run is ONE aligned 8-byte LDS read.
+  //  MODE 1 (Cin % 4 == 0): k = (kh*KS + kw)*Cin + ci; four consecutive k are four
+  //                         channels of one pixel (aligned 8-byte read).
+  //  MODE 2 (other Cin):    MODE 1 order with scalar 2-byte gathers.
+  static constexpr int MODE = CIN == 1 ? 0 : (CIN % 4 == 0 ? 1 : 2);
+  static constexpr int KC = KS * KS * CIN;             // real im2col columns
+  static constexpr int KE = MODE == 0 ? KS * 8 : KC;   // im2col columns incl. kw padding
+  static constexpr int KSTEPS = (KE + 31) / 32;
   static constexpr int NF = (COUT + 15) / 16;
   static constexpr int NCOL = NF * 16;
   static constexpr int TILE = HP * WS * CIN;
+  static constexpr int NCOPY = MODE == 0 ? 4 : 1;
+  static constexpr int TSTR = (TILE + 16 + 7) / 8 * 8;  // per-copy stride: zero slack for padded-k over-reads
+  static constexpr int IMG_LDS = NCOPY * TSTR;
   static constexpr int INTERIOR = H * W * CIN;
-  static constexpr int KM = ((KC + 1) + 15) / 16 * 16;  // wgrad rows incl. the bias (ones) row
+  static constexpr int KM = ((KE + 1) + 15) / 16 * 16;  // wgrad rows incl. the bias (ones) row at KE
   static constexpr int MFW = KM / 16;
   static constexpr int RSTEPS = (NPIX + 31) / 32;
+  // slab row layout for splitk_reduce: row = g * RED_IP + i, bias row KE
+  static constexpr int RED_G = MODE == 0 ? KS : KS * KS;
+  static constexpr int RED_IP = MODE == 0 ? 8 : CIN;
   static_assert(OH % 2 == 0 && OW % 2 == 0, "pool-window-major order needs an even conv output");
   static_assert(NPIX == 4 * NWIN, "");
+  static_assert(MODE == 2 || KE % 4 == 0, "bias row must start a 4-column chunk");
+  static_assert(MODE != 0 || WS % 4 == 0, "MODE 0 chunk deltas must keep the shifted-copy alignment");
+  // Cout == 8 with Cin == 1: MFMA columns 8..15 compute the right-hand pixel of
+  // each 2x2 pool window (weights shifted by one kw), see convpool_*_pair_k.
+  static constexpr bool PAIR = MODE == 0 && COUT == 8;
+  static_assert(MODE != 0 || ((OH - 1 + KS - 1) * WS + OW - 1 + XOFF + 7) < TSTR, "padded-kw over-read inside the copy");
 
-  // LDS offset of im2col column k = (kh, kw, ci) relative to the pixel base
+  // LDS offset of im2col column k (MODE 1/2 order) relative to the pixel base
   static DEV int kdelta(int k) {
     const int tap = k / CIN, ci = k - (k / CIN) * CIN;
     const int kh = tap / KS, kw = tap - (tap / KS) * KS;
     return (kh * WS + kw) * CIN + ci;
+  }
+  // LDS offset of the 4-column chunk starting at k (k % 4 == 0, k < KE)
+  static DEV int chunk_delta(int k) {
+    if constexpr (MODE == 0) return (k >> 3) * WS + (k & 7);
+    else return kdelta(k);
   }
   // LDS offset of the top-left input pixel feeding pool window w
   static DEV int wbase(int w) {
@@ -76,14 +113,27 @@ struct Geo {
     return ((2 * ph) * WS + 2 * pw + XOFF) * CIN;
   }
   static DEV int doff(int d) { return ((d >> 1) * WS + (d & 1)) * CIN; }
+  // LDS element offset (within one image's region) of the 4 columns starting at
+  // copy-0 offset a: MODE 0 picks the shifted copy that makes the read aligned.
+  static DEV int aligned_off(int a) {
+    if constexpr (MODE == 0) return a + (a & 3) * (TSTR - 1);
+    else return a;
+  }
 };
 
 DEV __bf16 as_bf(bf16_t v) { return __builtin_bit_cast(__bf16, v); }
 
 constexpr int NTH = 256;
 
-// Copy IMGS input images (NHWC, interior only) into their LDS tiles with
-// 8-byte vectors; the zero border written once at kernel start is untouched.
+template <int N>
+DEV void lds_zero(bf16_t* p, int tid) {
+  static_assert(N % 8 == 0, "");
+  for (int e = tid; e < N / 8; e += NTH) *(u32x4*)(p + 8 * e) = u32x4{0u, 0u, 0u, 0u};
+}
+
+// Copy IMGS input images (NHWC, interior only) into copy 0 of their LDS tiles
+// with 8-byte vectors; the zero border written once at kernel start is untouched.
+// MODE 0 then derives the three shifted copies (copy_s[j] = copy_0[j + s]).
 template <class G, int IMGS>
 DEV void fill_tiles(bf16_t* tile, const bf16_t* __restrict__ x, int img0, int B, int tid) {
   constexpr int NV = IMGS * G::H * G::ROWV;
@@ -92,7 +142,23 @@ DEV void fill_tiles(bf16_t* tile, const bf16_t* __restrict__ x, int img0, int B,
     const int hh = rem / G::ROWV, vv = rem - hh * G::ROWV;
     u32x2 v = {0u, 0u};
     if (img0 + im < B) v = *(const u32x2*)(x + (int64_t)(img0 + im) * G::INTERIOR + hh * G::W * G::CIN + 4 * vv);
-    *(u32x2*)(tile + im * G::TILE + ((hh + G::PAD) * G::WS + G::X0) * G::CIN + 4 * vv) = v;
+    *(u32x2*)(tile + im * G::IMG_LDS + ((hh + G::PAD) * G::WS + G::X0) * G::CIN + 4 * vv) = v;
+  }
+  if constexpr (G::MODE == 0) {
+    __syncthreads();
+    constexpr int NG = G::TSTR / 4;
+    for (int e = tid; e < IMGS * NG; e += NTH) {
+      const int im = e / NG, v = e - im * NG;
+      bf16_t* src = tile + im * G::IMG_LDS;
+      const u32x2 lo = *(const u32x2*)(src + 4 * v);
+      const u32x2 hi = (v + 1 < NG) ? *(const u32x2*)(src + 4 * v + 4) : u32x2{0u, 0u};
+      const uint32_t w0 = lo[0], w1 = lo[1], w2 = hi[0], w3 = hi[1];
+      *(u32x2*)(src + 1 * G::TSTR + 4 * v) = u32x2{__builtin_amdgcn_alignbit(w1, w0, 16),
+                                                   __builtin_amdgcn_alignbit(w2, w1, 16)};
+      *(u32x2*)(src + 2 * G::TSTR + 4 * v) = u32x2{w1, w2};
+      *(u32x2*)(src + 3 * G::TSTR + 4 * v) = u32x2{__builtin_amdgcn_alignbit(w2, w1, 16),
+                                                   __builtin_amdgcn_alignbit(w3, w2, 16)};
+    }
   }
 }
 
@@ -101,25 +167,43 @@ template <class G, int IMGS>
 __global__ __launch_bounds__(NTH) void convpool_fwd_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                       const float* __restrict__ bias, int bias_n, int B,
                                                       bf16_t* __restrict__ pooled, uint8_t* __restrict__ arg) {
-  __shared__ __attribute__((aligned(16))) bf16_t tile[IMGS * G::TILE];
+  constexpr int LDS = (IMGS * G::IMG_LDS + 7) / 8 * 8;
+  __shared__ __attribute__((aligned(16))) bf16_t tile[LDS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  for (int e = tid; e < IMGS * G::TILE; e += NTH) tile[e] = 0;
+  lds_zero<LDS>(tile, tid);
 
-  int dl[G::KSTEPS][8];
+  // per-lane A-operand offsets: dd = 4-column chunk deltas (MODE 0/1), dl = scalar deltas (MODE 2)
+  int dd[G::KSTEPS][2];
+  int dl[G::MODE == 2 ? G::KSTEPS : 1][8];
   bf16x8 bfr[G::KSTEPS][G::NF];
 #pragma unroll
-  for (int s = 0; s < G::KSTEPS; ++s)
+  for (int s = 0; s < G::KSTEPS; ++s) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k0 = 32 * s + 16 * h + 4 * g;
+      dd[s][h] = k0 < G::KE ? G::chunk_delta(k0) : 0;   // padded k: any finite pixel (zero weight)
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int k = 32 * s + 4 * g + (j & 3) + 16 * (j >> 2);
-      dl[s][j] = k < G::KC ? G::kdelta(k) : 0;
+      if constexpr (G::MODE == 2) dl[s][j] = k < G::KC ? G::kdelta(k) : 0;
+      bool valid;
+      int wrow;
+      if constexpr (G::MODE == 0) {
+        valid = (k >> 3) < G::KS && (k & 7) < G::KS;
+        wrow = (k >> 3) * G::KS + (k & 7);
+      } else {
+        valid = k < G::KC;
+        wrow = k;
+      }
 #pragma unroll
       for (int nf = 0; nf < G::NF; ++nf) {
         const int n = nf * 16 + li;
-        bfr[s][nf][j] = as_bf((k < G::KC && n < G::COUT) ? w[k * G::COUT + n] : (bf16_t)0);
+        bfr[s][nf][j] = as_bf((valid && n < G::COUT) ? w[wrow * G::COUT + n] : (bf16_t)0);
       }
     }
+  }
   float bs[G::NF];
 #pragma unroll
   for (int nf = 0; nf < G::NF; ++nf) {
@@ -134,34 +218,39 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_k(const bf16_t* __restrict__
     for (int f = wave; f < IMGS * G::MF; f += NTH / 64) {
       const int im = f / G::MF, fm = f - im * G::MF;
       const int r = min(fm * 16 + li, G::NPIX - 1);
-      const bf16_t* tb = tile + im * G::TILE + G::wbase(r >> 2) + G::doff(r & 3);
+      const bf16_t* tb = tile + im * G::IMG_LDS;
+      const int pb = G::wbase(r >> 2) + G::doff(r & 3);
       f32x4 acc[G::NF];
 #pragma unroll
       for (int nf = 0; nf < G::NF; ++nf) acc[nf] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < G::KSTEPS; ++s) {
         bf16x8 a;
+        if constexpr (G::MODE == 2) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = as_bf(tb[dl[s][j]]);
+          for (int j = 0; j < 8; ++j) a[j] = as_bf(tb[pb + dl[s][j]]);
+        } else {
+          const s16x4 lo = *(const s16x4*)(tb + G::aligned_off(pb + dd[s][0]));
+          const s16x4 hi = *(const s16x4*)(tb + G::aligned_off(pb + dd[s][1]));
+          a = join(lo, hi);
+        }
 #pragma unroll
         for (int nf = 0; nf < G::NF; ++nf) acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[s][nf], acc[nf], 0, 0, 0);
       }
       const int win = fm * 4 + g;
       if (win < G::NWIN && img0 + im < B) {
+        bf16_t* pimg = pooled + (int64_t)(img0 + im) * (G::NWIN * G::COUT);
+        uint8_t* aimg = arg + (int64_t)(img0 + im) * (G::NWIN * G::COUT);
 #pragma unroll
         for (int nf = 0; nf < G::NF; ++nf) {
           const int n = nf * 16 + li;
           if (n < G::COUT) {
-            float best = -INFINITY;
-            int bi = 0;
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-              const float v = fmaxf(acc[nf][d] + bs[nf], 0.f);
-              if (v > best) { best = v; bi = d; }
-            }
-            const int64_t off = ((int64_t)(img0 + im) * G::NWIN + win) * G::COUT + n;
-            pooled[off] = f2bf(best);
-            arg[off] = (uint8_t)bi;
+            // relu(. + b) is monotone: pool the raw sums, then bias + ReLU once
+            const f32x4 v = acc[nf];
+            const float m = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+            const int bi = v[0] == m ? 0 : (v[1] == m ? 1 : (v[2] == m ? 2 : 3));
+            pimg[win * G::COUT + n] = f2bf(fmaxf(m + bs[nf], 0.f));
+            aimg[win * G::COUT + n] = (uint8_t)bi;
           }
         }
       }
@@ -169,27 +258,126 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_k(const bf16_t* __restrict__
   }
 }
 
+DEV float swap_half_row(float v) {  // lane i <-> lane i^8 within each 16-lane row (DPP row_ror:8)
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xf, 0xf, false));
+}
+DEV int swap_half_row(int v) { return __builtin_amdgcn_mov_dpp(v, 0x128, 0xf, 0xf, false); }
+
+// ------------------------------------------------------------------ forward, Cin 1 / Cout 8 pair layout
+// MFMA row i of a fragment = (pool window fm*8 + i/2, window row dy = i&1) at the
+// window's LEFT column; column n = (channel c = n&7, side sx = n>>3).  Side 1 uses
+// the weights shifted by one kw, i.e. it convolves the RIGHT-hand pixel, so one
+// 16x16x32 MFMA chain produces a whole 2x2 window per (row pair, channel).  The
+// pool max over dy stays in the lane, the max over dx is one DPP half-row swap,
+// and every lane stores one (window, channel): 16 contiguous bf16 per row group.
+template <class G, int IMGS>
+__global__ __launch_bounds__(NTH) void convpool_fwd_pair_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                           const float* __restrict__ bias, int bias_n, int B,
+                                                           bf16_t* __restrict__ pooled, uint8_t* __restrict__ arg) {
+  static_assert(G::PAIR, "");
+  constexpr int LDS = (IMGS * G::IMG_LDS + 7) / 8 * 8;
+  constexpr int MFP = (G::NWIN + 7) / 8;  // fragments per image (8 windows each)
+  __shared__ __attribute__((aligned(16))) bf16_t tile[LDS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int c = li & 7, sx = li >> 3;
+  lds_zero<LDS>(tile, tid);
+
+  int dd[G::KSTEPS][2];
+  bf16x8 bfr[G::KSTEPS];
+#pragma unroll
+  for (int s = 0; s < G::KSTEPS; ++s) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k0 = 32 * s + 16 * h + 4 * g;
+      dd[s][h] = k0 < G::KE ? G::chunk_delta(k0) : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 32 * s + 4 * g + (j & 3) + 16 * (j >> 2);
+      const int kh = k >> 3, kw = (k & 7) - sx;
+      const bool valid = kh < G::KS && kw >= 0 && kw < G::KS;
+      bfr[s][j] = as_bf(valid ? w[(kh * G::KS + kw) * 8 + c] : (bf16_t)0);
+    }
+  }
+  const float bs = c < bias_n ? bias[c] : 0.f;
+
+  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += gridDim.x * IMGS) {
+    __syncthreads();
+    fill_tiles<G, IMGS>(tile, x, img0, B, tid);
+    __syncthreads();
+#pragma unroll 1
+    for (int im = 0; im < IMGS; ++im) {
+      const bf16_t* timg = tile + im * G::IMG_LDS;
+      const bool img_ok = img0 + im < B;
+      bf16_t* pimg = pooled + (int64_t)(img0 + im) * (G::NWIN * 8);
+      uint8_t* aimg = arg + (int64_t)(img0 + im) * (G::NWIN * 8);
+      for (int fm = wave; fm < MFP; fm += NTH / 64) {
+        const int wa = min(fm * 8 + (li >> 1), G::NWIN - 1);
+        const bf16_t* tb = timg + G::aligned_off(G::wbase(wa) + (li & 1) * G::WS);
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < G::KSTEPS; ++s) {
+          const bf16x8 a = join(*(const s16x4*)(tb + dd[s][0]), *(const s16x4*)(tb + dd[s][1]));
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[s], acc, 0, 0, 0);
+        }
+        // rows 4g+r: r=0,1 -> window 2g (dy 0,1); r=2,3 -> window 2g+1
+        const float m0 = fmaxf(acc[0], acc[1]), m1 = fmaxf(acc[2], acc[3]);
+        const int d0 = acc[1] > acc[0] ? 2 : 0, d1 = acc[3] > acc[2] ? 2 : 0;
+        // side 0 owns window 2g, side 1 owns window 2g+1: trade the other window's column max
+        const float oth = swap_half_row(sx ? m0 : m1);
+        const int doth = swap_half_row(sx ? d0 : d1);
+        const float L = sx ? oth : m0, R = sx ? m1 : oth;
+        const int dL = sx ? doth : d0, dR = sx ? d1 : doth;
+        const bool right = R > L;
+        const int wo = fm * 8 + 2 * g + sx;
+        if (wo < G::NWIN && img_ok) {
+          pimg[wo * 8 + c] = f2bf(fmaxf((right ? R : L) + bs, 0.f));
+          aimg[wo * 8 + c] = (uint8_t)(right ? dR + 1 : dL);
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ weight gradient
+// dW[k][n] = sum over pixels of im2col[pixel][k] * dY[pixel][n]: M = k, N = Cout,
+// reduction = pixels (pool-window-major).  MODE 0/1 read the im2col^T operand
+// with ds_read_b64_tr_b16: each lane supplies one pixel row and one 4-column
+// chunk; the bias row (k = KE) reads a constant [1,0,0,0] LDS cell.
 template <class G, int IMGS>
 __global__ __launch_bounds__(NTH) void convpool_wgrad_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dP,
                                                         const uint8_t* __restrict__ arg,
                                                         const bf16_t* __restrict__ P, int B,
                                                         float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) bf16_t tile[IMGS * G::TILE];
+  constexpr int CELL = IMGS * G::IMG_LDS;             // [1,0,0,0] then [0,0,0,0]
+  constexpr int LDS = (CELL + 8 + 7) / 8 * 8;
+  __shared__ __attribute__((aligned(16))) bf16_t tile[LDS];
   __shared__ __attribute__((aligned(16))) bf16_t dys[IMGS * G::NWIN * G::COUT];
   __shared__ __attribute__((aligned(16))) uint8_t args[IMGS * G::NWIN * G::COUT];
   __shared__ float red[G::KM * G::NCOL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  for (int e = tid; e < IMGS * G::TILE; e += NTH) tile[e] = 0;
+  lds_zero<LDS>(tile, tid);
+  __syncthreads();
+  if (tid == 0) tile[CELL] = (bf16_t)0x3f80;
 
-  int dk[G::MFW];
-  int kind[G::MFW];  // 0: im2col column, 1: bias ones-row, 2: zero pad
+  // MODE 0/1: per-lane chunk delta of the tr-read column chunk (-1: bias cell, -2: zero cell)
+  // MODE 2: per-lane scalar delta of im2col column k = mf*16 + li
+  const int q = (lane >> 2) & 3, p = lane & 3;
+  int cd[G::MFW];
+  int kind[G::MFW];  // MODE 2: 0 im2col column, 1 bias ones-row, 2 zero pad
 #pragma unroll
   for (int mf = 0; mf < G::MFW; ++mf) {
-    const int k = mf * 16 + li;
-    dk[mf] = k < G::KC ? G::kdelta(k) : 0;
-    kind[mf] = k < G::KC ? 0 : (k == G::KC ? 1 : 2);
+    if constexpr (G::MODE != 2) {
+      const int k0 = mf * 16 + 4 * p;
+      cd[mf] = k0 < G::KE ? G::chunk_delta(k0) : (k0 == G::KE ? -1 : -2);
+      kind[mf] = 0;
+    } else {
+      const int k = mf * 16 + li;
+      cd[mf] = k < G::KC ? G::kdelta(k) : 0;
+      kind[mf] = k < G::KC ? 0 : (k == G::KC ? 1 : 2);
+    }
   }
   f32x4 acc[G::MFW][G::NF];
 #pragma unroll
@@ -200,7 +388,6 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_k(const bf16_t* __restrict
   constexpr int DEL = IMGS * G::NWIN * G::COUT;
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += gridDim.x * IMGS) {
     __syncthreads();
-    fill_tiles<G, IMGS>(tile, x, img0, B, tid);
     static_assert(DEL % 8 == 0, "");
     for (int e8 = tid; e8 < DEL / 8; e8 += NTH) {
       const int e = 8 * e8;
@@ -219,14 +406,14 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_k(const bf16_t* __restrict
       *(u32x4*)(dys + e) = v;
       *(u32x2*)(args + e) = a;
     }
+    fill_tiles<G, IMGS>(tile, x, img0, B, tid);
     __syncthreads();
     for (int it = wave; it < IMGS * G::RSTEPS; it += NTH / 64) {
       const int im = it / G::RSTEPS, s = it - im * G::RSTEPS;
       // this lane's two pool windows for the 8 reduction slots
       const int w0 = 8 * s + g, w1 = w0 + 4;
       const bool v0 = w0 < G::NWIN, v1 = w1 < G::NWIN;
-      const bf16_t* tb = tile + im * G::TILE;
-      const int b0 = v0 ? G::wbase(w0) : 0, b1 = v1 ? G::wbase(w1) : 0;
+      const bf16_t* tb = tile + im * G::IMG_LDS;
       bf16x8 bfr[G::NF];
 #pragma unroll
       for (int nf = 0; nf < G::NF; ++nf) {
@@ -241,25 +428,43 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_k(const bf16_t* __restrict
           bfr[nf][4 + d] = as_bf(a1 == d ? y1 : (bf16_t)0);
         }
       }
+      if constexpr (G::MODE != 2) {
+        // rows supplied by this lane: pixel q of windows w0 / w1 (clamped; dY is zero there)
+        const int pb0 = G::wbase(min(w0, G::NWIN - 1)) + G::doff(q);
+        const int pb1 = G::wbase(min(w1, G::NWIN - 1)) + G::doff(q);
 #pragma unroll
-      for (int mf = 0; mf < G::MFW; ++mf) {
-        bf16x8 a;
+        for (int mf = 0; mf < G::MFW; ++mf) {
+          const int c = cd[mf];
+          const int cell = CELL + (c == -1 ? 0 : 4);
+          const int o0 = c >= 0 ? im * G::IMG_LDS + G::aligned_off(pb0 + c) : cell;
+          const int o1 = c >= 0 ? im * G::IMG_LDS + G::aligned_off(pb1 + c) : cell;
+          const bf16x8 a = join(lds_tr4(tile + o0), lds_tr4(tile + o1));
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          bf16_t e0 = 0, e1 = 0;
-          if (kind[mf] == 0) {
-            e0 = v0 ? tb[b0 + G::doff(d) + dk[mf]] : (bf16_t)0;
-            e1 = v1 ? tb[b1 + G::doff(d) + dk[mf]] : (bf16_t)0;
-          } else if (kind[mf] == 1) {
-            e0 = v0 ? (bf16_t)0x3f80 : (bf16_t)0;
-            e1 = v1 ? (bf16_t)0x3f80 : (bf16_t)0;
-          }
-          a[d] = as_bf(e0);
-          a[4 + d] = as_bf(e1);
+          for (int nf = 0; nf < G::NF; ++nf)
+            acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[nf], acc[mf][nf], 0, 0, 0);
         }
+      } else {
+        const int b0 = v0 ? G::wbase(w0) : 0, b1 = v1 ? G::wbase(w1) : 0;
 #pragma unroll
-        for (int nf = 0; nf < G::NF; ++nf)
-          acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[nf], acc[mf][nf], 0, 0, 0);
+        for (int mf = 0; mf < G::MFW; ++mf) {
+          bf16x8 a;
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            bf16_t e0 = 0, e1 = 0;
+            if (kind[mf] == 0) {
+              e0 = v0 ? tb[b0 + G::doff(d) + cd[mf]] : (bf16_t)0;
+              e1 = v1 ? tb[b1 + G::doff(d) + cd[mf]] : (bf16_t)0;
+            } else if (kind[mf] == 1) {
+              e0 = v0 ? (bf16_t)0x3f80 : (bf16_t)0;
+              e1 = v1 ? (bf16_t)0x3f80 : (bf16_t)0;
+            }
+            a[d] = as_bf(e0);
+            a[4 + d] = as_bf(e1);
+          }
+#pragma unroll
+          for (int nf = 0; nf < G::NF; ++nf)
+            acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[nf], acc[mf][nf], 0, 0, 0);
+        }
       }
     }
   }
@@ -287,24 +492,140 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_k(const bf16_t* __restrict
   }
 }
 
+// ------------------------------------------------------------------ weight gradient, Cin 1 / Cout 8 pair layout
+// Reduction slot t of a 32-slot step = (window 16*s + t/2, window row dy = t&1) at
+// the window's LEFT column; output column (c, sx) pairs that left-pixel patch with
+// the dY of pixel (dy, sx).  The right pixel's patch is the left one shifted by one
+// kw, so R[kh*8+kw'][8+c] accumulates dW[kh][kw'-1][c]: the fold
+// dW[m][c] = R[m][c] + R[m+1][8+c] (bias row: both sides) is applied to the block
+// partials, and the slab has the plain MODE 0 layout [KM][8].
+template <class G, int IMGS>
+__global__ __launch_bounds__(NTH) void convpool_wgrad_pair_k(const bf16_t* __restrict__ x,
+                                                             const bf16_t* __restrict__ dP,
+                                                             const uint8_t* __restrict__ arg,
+                                                             const bf16_t* __restrict__ P, int B,
+                                                             float* __restrict__ slab) {
+  static_assert(G::PAIR, "");
+  constexpr int CELL = IMGS * G::IMG_LDS;
+  constexpr int LDS = (CELL + 8 + 7) / 8 * 8;
+  constexpr int RS = (2 * G::NWIN + 31) / 32;        // reduction steps per image
+  constexpr int NWC = G::NWIN * 8;
+  __shared__ __attribute__((aligned(16))) bf16_t tile[LDS];
+  __shared__ __attribute__((aligned(16))) bf16_t dys[IMGS * NWC];
+  __shared__ __attribute__((aligned(16))) uint8_t args[IMGS * NWC];
+  __shared__ float red[G::KM * 16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int c = li & 7, sx = li >> 3;
+  lds_zero<LDS>(tile, tid);
+  __syncthreads();
+  if (tid == 0) tile[CELL] = (bf16_t)0x3f80;
+
+  const int q = (lane >> 2) & 3, p = lane & 3;
+  int cd[G::MFW];
+#pragma unroll
+  for (int mf = 0; mf < G::MFW; ++mf) {
+    const int k0 = mf * 16 + 4 * p;
+    cd[mf] = k0 < G::KE ? G::chunk_delta(k0) : (k0 == G::KE ? -1 : -2);
+  }
+  f32x4 acc[G::MFW];
+#pragma unroll
+  for (int mf = 0; mf < G::MFW; ++mf) acc[mf] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += gridDim.x * IMGS) {
+    __syncthreads();
+    static_assert((IMGS * NWC) % 8 == 0, "");
+    for (int e8 = tid; e8 < IMGS * NWC / 8; e8 += NTH) {
+      const int e = 8 * e8;
+      const int im = e / NWC;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      u32x2 a = {0xffffffffu, 0xffffffffu};
+      if (img0 + im < B) {
+        const int64_t o = (int64_t)img0 * NWC + e;
+        const u32x4 pv = *(const u32x4*)(P + o);
+        v = *(const u32x4*)(dP + o);
+        a = *(const u32x2*)(arg + o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (!(u4_get(pv, j) > 0.f)) u4_set(v, j, 0);   // ReLU mask: pooled value > 0
+      }
+      *(u32x4*)(dys + e) = v;
+      *(u32x2*)(args + e) = a;
+    }
+    fill_tiles<G, IMGS>(tile, x, img0, B, tid);
+    __syncthreads();
+    for (int it = wave; it < IMGS * RS; it += NTH / 64) {
+      const int im = it / RS, s = it - im * RS;
+      // dY operand: element j <-> slot 4g + (j&3) + 16(j>>2) = window 16s + 2g + ((j>>1)&1) + 8(j>>2), dy = j&1
+      bf16x8 bfr;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int wj = 16 * s + 2 * g + (jj & 1) + 8 * (jj >> 1);
+        const bool ok = wj < G::NWIN;
+        const int i = (im * G::NWIN + wj) * 8 + c;
+        const bf16_t y = ok ? dys[i] : (bf16_t)0;
+        const int a = ok ? args[i] : 0xff;
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy) bfr[4 * (jj >> 1) + 2 * (jj & 1) + dy] = as_bf(a == 2 * dy + sx ? y : (bf16_t)0);
+      }
+      // im2col^T operand rows supplied by this lane: slot 4g+q (+16): window 16s + 2g + q/2 (+8), dy = q&1
+      const int wq = 16 * s + 2 * g + (q >> 1);
+      const int pb0 = G::wbase(min(wq, G::NWIN - 1)) + (q & 1) * G::WS;
+      const int pb1 = G::wbase(min(wq + 8, G::NWIN - 1)) + (q & 1) * G::WS;
+#pragma unroll
+      for (int mf = 0; mf < G::MFW; ++mf) {
+        const int cc = cd[mf];
+        const int cell = CELL + (cc == -1 ? 0 : 4);
+        const int o0 = cc >= 0 ? im * G::IMG_LDS + G::aligned_off(pb0 + cc) : cell;
+        const int o1 = cc >= 0 ? im * G::IMG_LDS + G::aligned_off(pb1 + cc) : cell;
+        const bf16x8 a = join(lds_tr4(tile + o0), lds_tr4(tile + o1));
+        acc[mf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr, acc[mf], 0, 0, 0);
+      }
+    }
+  }
+  for (int wv = 0; wv < NTH / 64; ++wv) {
+    __syncthreads();
+    if (wave == wv) {
+#pragma unroll
+      for (int mf = 0; mf < G::MFW; ++mf)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float& dst = red[(mf * 16 + 4 * g + r) * 16 + li];
+          dst = (wv == 0) ? acc[mf][r] : dst + acc[mf][r];
+        }
+    }
+  }
+  __syncthreads();
+  float* out = slab + (int64_t)blockIdx.x * G::KM * 8;
+  for (int e = tid; e < G::KM * 8; e += NTH) {
+    const int m = e >> 3, cc = e & 7;
+    const int m2 = m == G::KE ? m : m + 1;            // bias row: both sides of the same row
+    out[e] = red[m * 16 + cc] + (m2 < G::KM ? red[m2 * 16 + 8 + cc] : 0.f);
+  }
+}
+
 // ------------------------------------------------------------------ data gradient (pooled dY -> dX)
+// The unpooled dY image lives in LDS with a KS-1-PAD halo; pixels are DPS = Cout+8
+// elements apart so the 16 pixel rows of a ds_read_b64 fragment fall in distinct banks.
 template <class G, int IMGS>
 __global__ __launch_bounds__(NTH) void convpool_dgrad_k(const bf16_t* __restrict__ dP, const uint8_t* __restrict__ arg,
                                                         const bf16_t* __restrict__ P, const bf16_t* __restrict__ w,
                                                         int B, bf16_t* __restrict__ dx) {
   constexpr int Q = G::KS - 1 - G::PAD;
   constexpr int OHQ = G::OH + 2 * Q, OWQ = G::OW + 2 * Q;
-  constexpr int DT = OHQ * OWQ * G::COUT;
+  constexpr int DPS = G::COUT + 8;
+  constexpr int DT = OHQ * OWQ * DPS;
   constexpr int KD = G::KS * G::KS * G::COUT;
   constexpr int KSD = (KD + 31) / 32;
   constexpr int NPX = G::H * G::W;
   constexpr int MFD = (NPX + 15) / 16;
   constexpr int NFD = (G::CIN + 15) / 16;
   static_assert(G::COUT % 16 == 0, "dgrad operand reads need Cout % 16 == 0");
+  static_assert((IMGS * DT) % 8 == 0, "");
   __shared__ __attribute__((aligned(16))) bf16_t dyt[IMGS * DT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  for (int e = tid; e < IMGS * DT; e += NTH) dyt[e] = 0;
+  lds_zero<IMGS * DT>(dyt, tid);
 
   int dd[KSD][2];
   bf16x8 bw[KSD][NFD];
@@ -315,7 +636,7 @@ __global__ __launch_bounds__(NTH) void convpool_dgrad_k(const bf16_t* __restrict
       const int k = 32 * s + 4 * g + 16 * h;  // 4 consecutive co at one flipped tap
       const int tp = k / G::COUT, co = k - tp * G::COUT;
       const int kh = tp / G::KS, kw = tp - kh * G::KS;
-      dd[s][h] = k < KD ? (kh * OWQ + kw) * G::COUT + co : 0;
+      dd[s][h] = k < KD ? (kh * OWQ + kw) * DPS + co : 0;
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -357,7 +678,7 @@ __global__ __launch_bounds__(NTH) void convpool_dgrad_k(const bf16_t* __restrict
           const uint32_t aj = ((j < 4 ? a[0] : a[1]) >> (8 * (j & 3))) & 0xff;
           if (aj == (uint32_t)d) u4_set(o, j, (bf16_t)((v[j >> 1] >> (16 * (j & 1))) & 0xffff));
         }
-        *(u32x4*)(dyt + im * DT + (oh * OWQ + ow) * G::COUT + co) = o;
+        *(u32x4*)(dyt + im * DT + (oh * OWQ + ow) * DPS + co) = o;
       }
     }
     __syncthreads();
@@ -365,16 +686,13 @@ __global__ __launch_bounds__(NTH) void convpool_dgrad_k(const bf16_t* __restrict
       const int im = f / MFD, mf = f - im * MFD;
       const int m = min(mf * 16 + li, NPX - 1);
       const int ih = m / G::W, iw = m - ih * G::W;
-      const bf16_t* tb = dyt + im * DT + (ih * OWQ + iw) * G::COUT;
+      const bf16_t* tb = dyt + im * DT + (ih * OWQ + iw) * DPS;
       f32x4 acc[NFD];
 #pragma unroll
       for (int nf = 0; nf < NFD; ++nf) acc[nf] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KSD; ++s) {
-        const s16x4 lo = *(const s16x4*)(tb + dd[s][0]);
-        const s16x4 hi = *(const s16x4*)(tb + dd[s][1]);
-        typedef short s16x8 __attribute__((ext_vector_type(8)));
-        const bf16x8 a = __builtin_bit_cast(bf16x8, (s16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        const bf16x8 a = join(*(const s16x4*)(tb + dd[s][0]), *(const s16x4*)(tb + dd[s][1]));
 #pragma unroll
         for (int nf = 0; nf < NFD; ++nf) acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[s][nf], acc[nf], 0, 0, 0);
       }
@@ -395,6 +713,119 @@ __global__ __launch_bounds__(NTH) void convpool_dgrad_k(const bf16_t* __restrict
   }
 }
 
+// ------------------------------------------------------------------ data gradient, Cin 8 pair layout
+// Row m of the implicit GEMM = input-pixel PAIR (ih, 2*jw); column n = (ci = n&7,
+// side sx = n>>3).  The dY patch row spans kw' = 0..KS (one extra tap) and side 1
+// uses the flipped filter shifted by one kw, so it produces dx at (ih, 2*jw + 1):
+// 7 x 15 MFMAs per 14x14 image instead of 13 x 13, and 16 lanes store 32
+// contiguous bytes.
+template <class G, int IMGS>
+__global__ __launch_bounds__(NTH) void convpool_dgrad_pair_k(const bf16_t* __restrict__ dP,
+                                                             const uint8_t* __restrict__ arg,
+                                                             const bf16_t* __restrict__ P,
+                                                             const bf16_t* __restrict__ w, int B,
+                                                             bf16_t* __restrict__ dx) {
+  static_assert(G::CIN == 8 && G::COUT == 16 && G::W % 2 == 0, "pair dgrad layout");
+  constexpr int Q = G::KS - 1 - G::PAD;
+  constexpr int OHQ = G::OH + 2 * Q, OWQ = G::OW + 2 * Q;
+  constexpr int DPS = G::COUT + 8;                    // 48-byte pixels: a pixel pair is 6 x 16 B
+  // row stride: an odd number of 16-byte units, = 5 mod 8, so the 16 pixel pairs of
+  // a fragment (2-3 image rows) fall in distinct 16-byte bank groups
+  constexpr int RSE = [] { int u = (OWQ * DPS * 2 + 15) / 16; while (u % 8 != 5) ++u; return u * 8; }();
+  constexpr int DT = OHQ * RSE;
+  constexpr int KWQ = G::KS + 1;
+  constexpr int KD = G::KS * KWQ * G::COUT;
+  constexpr int KSD = (KD + 31) / 32;
+  constexpr int JW = G::W / 2;
+  constexpr int NPR = G::H * JW;                      // pixel pairs per image
+  constexpr int MFD = (NPR + 15) / 16;
+  static_assert((IMGS * DT) % 8 == 0, "");
+  static_assert(G::W - 2 + KWQ - 1 < OWQ, "patch row stays inside the haloed tile");
+  __shared__ __attribute__((aligned(16))) bf16_t dyt[IMGS * DT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int ci = li & 7, sx = li >> 3;
+  lds_zero<IMGS * DT>(dyt, tid);
+
+  int dd[KSD][2];
+  bf16x8 bw[KSD];
+#pragma unroll
+  for (int s = 0; s < KSD; ++s) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = 32 * s + 4 * g + 16 * h;  // 4 consecutive co at one (kh, kw') tap
+      const int tp = k / G::COUT, co = k - tp * G::COUT;
+      const int kh = tp / KWQ, kw = tp - kh * KWQ;
+      dd[s][h] = k < KD ? kh * RSE + kw * DPS + co : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 32 * s + 4 * g + (j & 3) + 16 * (j >> 2);
+      const int tp = k / G::COUT, co = k - tp * G::COUT;
+      const int kh = tp / KWQ, kw = tp - kh * KWQ - sx;
+      const bool valid = k < KD && kw >= 0 && kw < G::KS;
+      const int tap = (G::KS - 1 - kh) * G::KS + (G::KS - 1 - kw);
+      bw[s][j] = as_bf(valid ? w[(tap * G::CIN + ci) * G::COUT + co] : (bf16_t)0);
+    }
+  }
+  constexpr int NWC = G::NWIN * G::COUT;
+  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += gridDim.x * IMGS) {
+    __syncthreads();
+    for (int e8 = tid; e8 < IMGS * NWC / 8; e8 += NTH) {
+      const int e = 8 * e8;
+      const int im = e / NWC, rem = e - im * NWC;
+      const int win = rem / G::COUT, co = rem - win * G::COUT;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      u32x2 a = {0xffffffffu, 0xffffffffu};
+      if (img0 + im < B) {
+        const int64_t o = (int64_t)img0 * NWC + e;
+        const u32x4 pv = *(const u32x4*)(P + o);
+        v = *(const u32x4*)(dP + o);
+        a = *(const u32x2*)(arg + o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (!(u4_get(pv, j) > 0.f)) u4_set(v, j, 0);
+      }
+      const int ph = win / G::PW, pw = win - ph * G::PW;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int oh = 2 * ph + (d >> 1) + Q, ow = 2 * pw + (d & 1) + Q;
+        u32x4 o = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t aj = ((j < 4 ? a[0] : a[1]) >> (8 * (j & 3))) & 0xff;
+          if (aj == (uint32_t)d) u4_set(o, j, (bf16_t)((v[j >> 1] >> (16 * (j & 1))) & 0xffff));
+        }
+        *(u32x4*)(dyt + im * DT + oh * RSE + ow * DPS + co) = o;
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int im = 0; im < IMGS; ++im) {
+      const bool img_ok = img0 + im < B;
+      bf16_t* dimg = dx + (int64_t)(img0 + im) * (G::H * G::W * 8);
+      for (int mf = wave; mf < MFD; mf += NTH / 64) {
+        const int m = min(mf * 16 + li, NPR - 1);
+        const int ih = m / JW, iw = 2 * (m - ih * JW);
+        const bf16_t* tb = dyt + im * DT + ih * RSE + iw * DPS;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KSD; ++s) {
+          const bf16x8 a = join(*(const s16x4*)(tb + dd[s][0]), *(const s16x4*)(tb + dd[s][1]));
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[s], acc, 0, 0, 0);
+        }
+        if (img_ok) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int mm = mf * 16 + 4 * g + r;    // pair index: pixel 2*mm + sx in row-major order
+            if (mm < NPR) dimg[(2 * mm + sx) * 8 + ci] = f2bf(acc[r]);
+          }
+        }
+      }
+    }
+  }
+}
+
 int grid_for(int B, int imgs, int cap) {
   int n = (B + imgs - 1) / imgs;
   return n < cap ? (n < 1 ? 1 : n) : cap;
@@ -403,23 +834,36 @@ int grid_for(int B, int imgs, int cap) {
 template <class G, int IMGS>
 hipError_t run_fwd(const bf16_t* x, const bf16_t* w, const float* bias, int bias_n, int B, bf16_t* pooled, uint8_t* arg,
                    hipStream_t st) {
-  hipLaunchKernelGGL((convpool_fwd_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, x, w, bias, bias_n, B,
-                     pooled, arg);
+  if constexpr (G::PAIR) {
+    hipLaunchKernelGGL((convpool_fwd_pair_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, x, w, bias,
+                       bias_n, B, pooled, arg);
+  } else {
+    hipLaunchKernelGGL((convpool_fwd_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, x, w, bias, bias_n,
+                       B, pooled, arg);
+  }
   return hipGetLastError();
 }
 
 template <class G, int IMGS>
 hipError_t run_wgrad(const bf16_t* x, const bf16_t* dP, const uint8_t* arg, const bf16_t* P, int B, float* slab,
                      int grid, hipStream_t st) {
-  hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, P, B, slab);
+  if constexpr (G::PAIR) {
+    hipLaunchKernelGGL((convpool_wgrad_pair_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, P, B, slab);
+  } else {
+    hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, P, B, slab);
+  }
   return hipGetLastError();
 }
 
 template <class G, int IMGS>
 hipError_t run_dgrad(const bf16_t* dP, const uint8_t* arg, const bf16_t* P, const bf16_t* w, int B, bf16_t* dx,
                      hipStream_t st) {
-  hipLaunchKernelGGL((convpool_dgrad_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, dP, arg, P, w, B,
-                     dx);
+  if constexpr (G::CIN == 8 && G::COUT == 16)
+    hipLaunchKernelGGL((convpool_dgrad_pair_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, dP, arg, P,
+                       w, B, dx);
+  else
+    hipLaunchKernelGGL((convpool_dgrad_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, dP, arg, P, w,
+                       B, dx);
   return hipGetLastError();
 }
 
@@ -449,12 +893,30 @@ int convpool_wgrad_rows(int cfg) {
   return -1;
 }
 
+template <class G>
+void reduce_layout(int* out) {
+  out[0] = G::RED_G;
+  out[1] = G::RED_IP;
+  out[2] = G::MODE == 0 ? G::KS : -1;  // real inner count (-1: the layer's real Cin)
+  out[3] = G::KE;
+}
+
+int convpool_reduce_layout(int cfg, int* out) {
+  switch (cfg) {
+    case 0: reduce_layout<LeNetC1>(out); return 0;
+    case 1: reduce_layout<LeNetC2>(out); return 0;
+    case 2: reduce_layout<RefC1g>(out); return 0;
+    case 3: reduce_layout<RefC1c>(out); return 0;
+  }
+  return -1;
+}
+
 hipError_t convpool_fwd(int cfg, const bf16_t* x, const bf16_t* w, const float* bias, int bias_n, int B,
                         bf16_t* pooled, uint8_t* arg, hipStream_t st) {
   switch (cfg) {
-    case 0: return run_fwd<LeNetC1, 4>(x, w, bias, bias_n, B, pooled, arg, st);
+    case 0: return run_fwd<LeNetC1, 2>(x, w, bias, bias_n, B, pooled, arg, st);
     case 1: return run_fwd<LeNetC2, 4>(x, w, bias, bias_n, B, pooled, arg, st);
-    case 2: return run_fwd<RefC1g, 4>(x, w, bias, bias_n, B, pooled, arg, st);
+    case 2: return run_fwd<RefC1g, 2>(x, w, bias, bias_n, B, pooled, arg, st);
     case 3: return run_fwd<RefC1c, 4>(x, w, bias, bias_n, B, pooled, arg, st);
   }
   return hipErrorInvalidValue;
@@ -463,7 +925,7 @@ hipError_t convpool_fwd(int cfg, const bf16_t* x, const bf16_t* w, const float* 
 hipError_t convpool_wgrad(int cfg, const bf16_t* x, const bf16_t* dP, const uint8_t* arg, const bf16_t* P, int B,
                           float* slab, int grid, hipStream_t st) {
   switch (cfg) {
-    case 0: return run_wgrad<LeNetC1, 4>(x, dP, arg, P, B, slab, grid, st);
+    case 0: return run_wgrad<LeNetC1, 2>(x, dP, arg, P, B, slab, grid, st);
     case 1: return run_wgrad<LeNetC2, 4>(x, dP, arg, P, B, slab, grid, st);
     case 2: return run_wgrad<RefC1g, 2>(x, dP, arg, P, B, slab, grid, st);
     case 3: return run_wgrad<RefC1c, 2>(x, dP, arg, P, B, slab, grid, st);
@@ -474,7 +936,7 @@ hipError_t convpool_wgrad(int cfg, const bf16_t* x, const bf16_t* dP, const uint
 hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const bf16_t* P, const bf16_t* w, int B,
                           bf16_t* dx, hipStream_t st) {
   switch (cfg) {
-    case 1: return run_dgrad<LeNetC2, 4>(dP, arg, P, w, B, dx, st);
+    case 1: return run_dgrad<LeNetC2, 2>(dP, arg, P, w, B, dx, st);
   }
   return hipErrorInvalidValue;
 }

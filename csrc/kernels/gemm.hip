@@ -164,13 +164,6 @@ struct WFlipK {
 };
 
 // ---------------------------------------------------------------- fragment reads
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-
-DEV bf16x8 join(s16x4 lo, s16x4 hi) {
-  typedef short s16x8 __attribute__((ext_vector_type(8)));
-  s16x8 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(bf16x8, r);
-}
 
 // K-contiguous image [rows][S]: lane i=l&15 row r0+i, k = kb + 4g + {0..3} and +16.
 template <int S>

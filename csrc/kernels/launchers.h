@@ -41,6 +41,8 @@ hipError_t conv_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int H, int W, i
 // ---- convpool.hip (fused small-channel conv + bias + ReLU + 2x2 max-pool)
 int convpool_config(int cin, int cout, int ks, int pad, int h, int w);  // -1: unsupported
 int convpool_wgrad_rows(int cfg);                                      // KM (slab rows incl. bias row)
+// slab -> dW layout for splitk_reduce: {G, Ipad, I (-1: real Cin), bias_row}
+int convpool_reduce_layout(int cfg, int* out);
 hipError_t convpool_fwd(int cfg, const bf16_t* x, const bf16_t* w, const float* bias, int bias_n, int B,
                         bf16_t* pooled, uint8_t* arg, hipStream_t st);
 hipError_t convpool_wgrad(int cfg, const bf16_t* x, const bf16_t* dP, const uint8_t* arg, const bf16_t* P, int B,

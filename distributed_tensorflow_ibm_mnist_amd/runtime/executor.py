@@ -108,6 +108,7 @@ class ConvPoolLayer(_Layer):
         self.arg = torch.zeros(B, self.PH, self.PW, self.Cp, dtype=torch.uint8, device=dev)
         self.wname, self.bname = f"{spec.name}/weights", f"{spec.name}/biases"
         self.KM = kernels().convpool_rows(self.C, self.Cp, 5, self.pad, self.H, self.W)
+        self.red = kernels().convpool_reduce_args(*self._geo(), spec.cin)   # (G, Ipad, I, bias_row)
         self.grid = 1024
         self.slab_elems = self.grid * self.KM * self.Cp
         self.can_dgrad = self.cfg == 1
@@ -126,7 +127,8 @@ class ConvPoolLayer(_Layer):
         K = kernels()
         grid = min(self.grid, max(1, (nb + 3) // 4))
         K.convpool_wgrad(self.x, dy, self.arg, self.out, slab, grid, nb, *self._geo())
-        K.splitk_reduce(slab, grid, self.KM, self.Cp, 25, self.C, s.cin, s.cout, 25 * self.C,
+        G, Ip, I, brow = self.red
+        K.splitk_reduce(slab, grid, self.KM, self.Cp, G, Ip, I, s.cout, brow,
                         self.fp.grad_view(self.wname), self.fp.grad_view(self.bname), 1.0)
         if dx is not None:
             K.convpool_dgrad(dy, self.arg, self.out, self.fp.bf16_view(self.wname), dx, nb, *self._geo())

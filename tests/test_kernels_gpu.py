@@ -311,7 +311,8 @@ def test_convpool(dev, K, N, H, W, Ci, ci, Co, co, pad):
     K.convpool_wgrad(x, dP, arg, pooled, slab, grid, N, Ci, Co, 5, pad, H, W)
     dw = torch.empty(5, 5, ci, co, device=dev)
     db = torch.empty(co, device=dev)
-    K.splitk_reduce(slab, grid, KM, Co, 25, Ci, ci, co, 25 * Ci, dw, db, 1.0)
+    G, Ip, I, brow = K.convpool_reduce_args(Ci, Co, 5, pad, H, W, ci)
+    K.splitk_reduce(slab, grid, KM, Co, G, Ip, I, co, brow, dw, db, 1.0)
     close(dw, wr.grad[:, :, :ci, :co], rel=3e-2)
     close(db, br.grad[:co], rel=3e-2)
     if K.convpool_supported(Ci, Co, 5, pad, H, W) == 1:

@@ -252,6 +252,7 @@ void splitk_reduce(Tensor slab, int64_t splits, int64_t M, int64_t N, int64_t G,
                    int64_t bias_row, Tensor wdst, optional<Tensor> bdst, double scale) {
   check(slab, at::kFloat, splits * M * N, "slab");
   TORCH_CHECK(I <= Ipad && J <= N && G * Ipad <= M, "reduce geometry");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(slab.data_ptr()) % 16 == 0, "slab must be 16-byte aligned");
   check(wdst, at::kFloat, G * I * J, "wdst");
   float* b = nullptr;
   if (bdst.has_value() && bdst->defined()) {
@@ -259,7 +260,7 @@ void splitk_reduce(Tensor slab, int64_t splits, int64_t M, int64_t N, int64_t G,
     check(*bdst, at::kFloat, J, "bdst");
     b = P<float>(*bdst);
   }
-  hip_ok(mnistx::splitk_reduce(P<const float>(slab), (int)splits, (int)M, (int)N, (int)G, (int)Ipad, (int)I, (int)J,
+  hip_ok(mnistx::splitk_reduce(P<float>(slab), (int)splits, (int)M, (int)N, (int)G, (int)Ipad, (int)I, (int)J,
                                (int)bias_row, P<float>(wdst), b, (float)scale, cur_stream()),
          "splitk_reduce");
 }
@@ -382,6 +383,12 @@ int64_t convpool_rows(int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64_
   return cp_geo(cin, cout, ks, pad, h, w).KM;
 }
 
+std::vector<int64_t> gemm_tile(int64_t M, int64_t N, bool wgrad) {
+  int bm, bn;
+  mnistx::gemm_tile((int)M, (int)N, wgrad ? 1 : 0, &bm, &bn);
+  return {bm, bn};
+}
+
 // (G, Ipad, I, bias_row) arguments of splitk_reduce for this geometry's wgrad slab
 std::vector<int64_t> convpool_reduce_args(int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t w,
                                           int64_t cin_real) {
@@ -455,6 +462,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("cast_f32_bf16_padded", &cast_f32_bf16_padded);
   m.def("convpool_supported", &convpool_supported);
   m.def("convpool_rows", &convpool_rows);
+  m.def("gemm_tile", &gemm_tile);
   m.def("convpool_reduce_args", &convpool_reduce_args);
   m.def("convpool_fwd", &convpool_fwd);
   m.def("convpool_wgrad", &convpool_wgrad);

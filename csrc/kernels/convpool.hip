@@ -714,57 +714,51 @@ __global__ __launch_bounds__(NTH) void convpool_dgrad_k(const bf16_t* __restrict
 }
 
 // ------------------------------------------------------------------ data gradient, Cin 8 pair layout
-// Row m of the implicit GEMM = input-pixel PAIR (ih, 2*jw); column n = (ci = n&7,
-// side sx = n>>3).  The dY patch row spans kw' = 0..KS (one extra tap) and side 1
-// uses the flipped filter shifted by one kw, so it produces dx at (ih, 2*jw + 1):
-// 7 x 15 MFMAs per 14x14 image instead of 13 x 13, and 16 lanes store 32
-// contiguous bytes.
+// Row i of a fragment = input-pixel PAIR (ih = 2*mf + i/8, iw = 2*(i&7)): two
+// image rows of 8 pairs (the 8th pair is padding for a 14-wide image), so with
+// 48-byte pixels (a pair = 6 x 16 B) and an odd row stride in 16-byte units the
+// 16 rows of every fragment read 16 distinct 16-byte bank groups.  Column n =
+// (ci = n&7, side sx = n>>3): the dY patch row spans kw' = 0..KS (one extra tap)
+// and side 1 uses the flipped filter shifted by one kw, i.e. it produces dx at
+// (ih, iw + 1).  K-slot order: lane group g, element j -> tap 2s + g/2, co 8(g&1)+j,
+// so each A fragment is ONE ds_read_b128.
 template <class G, int IMGS>
 __global__ __launch_bounds__(NTH) void convpool_dgrad_pair_k(const bf16_t* __restrict__ dP,
                                                              const uint8_t* __restrict__ arg,
                                                              const bf16_t* __restrict__ P,
                                                              const bf16_t* __restrict__ w, int B,
                                                              bf16_t* __restrict__ dx) {
-  static_assert(G::CIN == 8 && G::COUT == 16 && G::W % 2 == 0, "pair dgrad layout");
+  static_assert(G::CIN == 8 && G::COUT == 16 && G::W % 2 == 0 && G::H % 2 == 0 && G::W <= 16, "pair dgrad layout");
   constexpr int Q = G::KS - 1 - G::PAD;
   constexpr int OHQ = G::OH + 2 * Q, OWQ = G::OW + 2 * Q;
   constexpr int DPS = G::COUT + 8;                    // 48-byte pixels: a pixel pair is 6 x 16 B
-  // row stride: an odd number of 16-byte units, = 5 mod 8, so the 16 pixel pairs of
-  // a fragment (2-3 image rows) fall in distinct 16-byte bank groups
   constexpr int RSE = [] { int u = (OWQ * DPS * 2 + 15) / 16; while (u % 8 != 5) ++u; return u * 8; }();
   constexpr int DT = OHQ * RSE;
   constexpr int KWQ = G::KS + 1;
-  constexpr int KD = G::KS * KWQ * G::COUT;
-  constexpr int KSD = (KD + 31) / 32;
-  constexpr int JW = G::W / 2;
-  constexpr int NPR = G::H * JW;                      // pixel pairs per image
-  constexpr int MFD = (NPR + 15) / 16;
+  constexpr int NTAP = G::KS * KWQ;
+  constexpr int KSD = (NTAP + 1) / 2;                 // 2 taps x 16 co per 32-wide k-step
+  constexpr int MFD = G::H / 2;                       // 2 image rows per fragment
   static_assert((IMGS * DT) % 8 == 0, "");
-  static_assert(G::W - 2 + KWQ - 1 < OWQ, "patch row stays inside the haloed tile");
+  static_assert(14 + KWQ - 1 < RSE / DPS, "padding pair's patch row stays inside the row stride");
   __shared__ __attribute__((aligned(16))) bf16_t dyt[IMGS * DT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int ci = li & 7, sx = li >> 3;
   lds_zero<IMGS * DT>(dyt, tid);
 
-  int dd[KSD][2];
+  int dtap[KSD];
   bf16x8 bw[KSD];
 #pragma unroll
   for (int s = 0; s < KSD; ++s) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int k = 32 * s + 4 * g + 16 * h;  // 4 consecutive co at one (kh, kw') tap
-      const int tp = k / G::COUT, co = k - tp * G::COUT;
-      const int kh = tp / KWQ, kw = tp - kh * KWQ;
-      dd[s][h] = k < KD ? kh * RSE + kw * DPS + co : 0;
-    }
+    const int tp = 2 * s + (g >> 1);
+    const int kh = tp / KWQ, kwq = tp - kh * KWQ;
+    dtap[s] = tp < NTAP ? kh * RSE + kwq * DPS + 8 * (g & 1) : 0;
+    const int kw = kwq - sx;
+    const bool valid = tp < NTAP && kw >= 0 && kw < G::KS;
+    const int tap = (G::KS - 1 - kh) * G::KS + (G::KS - 1 - kw);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int k = 32 * s + 4 * g + (j & 3) + 16 * (j >> 2);
-      const int tp = k / G::COUT, co = k - tp * G::COUT;
-      const int kh = tp / KWQ, kw = tp - kh * KWQ - sx;
-      const bool valid = k < KD && kw >= 0 && kw < G::KS;
-      const int tap = (G::KS - 1 - kh) * G::KS + (G::KS - 1 - kw);
+      const int co = 8 * (g & 1) + j;
       bw[s][j] = as_bf(valid ? w[(tap * G::CIN + ci) * G::COUT + co] : (bf16_t)0);
     }
   }
@@ -805,20 +799,20 @@ __global__ __launch_bounds__(NTH) void convpool_dgrad_pair_k(const bf16_t* __res
       const bool img_ok = img0 + im < B;
       bf16_t* dimg = dx + (int64_t)(img0 + im) * (G::H * G::W * 8);
       for (int mf = wave; mf < MFD; mf += NTH / 64) {
-        const int m = min(mf * 16 + li, NPR - 1);
-        const int ih = m / JW, iw = 2 * (m - ih * JW);
-        const bf16_t* tb = dyt + im * DT + ih * RSE + iw * DPS;
+        const bf16_t* tb = dyt + im * DT + (2 * mf + (li >> 3)) * RSE + 2 * (li & 7) * DPS;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < KSD; ++s) {
-          const bf16x8 a = join(*(const s16x4*)(tb + dd[s][0]), *(const s16x4*)(tb + dd[s][1]));
+          const bf16x8 a = __builtin_bit_cast(bf16x8, *(const u32x4*)(tb + dtap[s]));
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[s], acc, 0, 0, 0);
         }
+        // accumulator rows 4g + r: image row 2mf + g/2, pair jr = 4(g&1) + r
         if (img_ok) {
+          const int ih = 2 * mf + (g >> 1);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int mm = mf * 16 + 4 * g + r;    // pair index: pixel 2*mm + sx in row-major order
-            if (mm < NPR) dimg[(2 * mm + sx) * 8 + ci] = f2bf(acc[r]);
+            const int jr = 4 * (g & 1) + r;
+            if (2 * jr < G::W) dimg[(ih * G::W + 2 * jr + sx) * 8 + ci] = f2bf(acc[r]);
           }
         }
       }

@@ -309,8 +309,63 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEp
 
 #undef As
 #undef Bs
-  // ---- epilogue: lane holds D[4g + r][i] of each 16x16 tile
+  // ---- epilogue.  Vector path (N, ldc, ldm multiples of 8): each wave stages a
+  // 16 x TN block of its accumulators in LDS, then every lane owns 8 consecutive
+  // columns of one row: bias / ReLU / mask on 8 values, one 16-byte bf16 store
+  // (or 2 x 16-byte fp32 stores) instead of eight 2-byte stores.
   const int g = lane >> 4, li = lane & 15;
+  const bool vec = (N % 8 == 0) && (ep.ldc % 8 == 0) && ((uintptr_t)ep.out % 16 == 0) &&
+                   (ep.mask == nullptr || (ep.ldm % 8 == 0 && (uintptr_t)ep.mask % 16 == 0));
+  if (vec) {
+    constexpr int EP_LD = TN + 4;
+    static_assert((NT / 64) * 16 * EP_LD * 4 <= 2 * (A_ELEMS + B_ELEMS) * 2, "epilogue staging must fit in smem");
+    float* eb = (float*)smem + wave * 16 * EP_LD;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) eb[(4 * g + r) * EP_LD + j * 16 + li] = acc[i][j][r];
+      __syncthreads();
+      for (int v = lane; v < 16 * (TN / 8); v += 64) {
+        const int rr = v / (TN / 8), cv = (v - rr * (TN / 8)) * 8;
+        const int m = m0 + wm * TM + i * 16 + rr, n = n0 + wn * TN + cv;
+        if (m < M && n < N) {
+          f32x4 lo = *(const f32x4*)(eb + rr * EP_LD + cv), hi = *(const f32x4*)(eb + rr * EP_LD + cv + 4);
+          if (ep.mode == EPI_SLAB) {
+            float* o = (float*)ep.out + (int64_t)blockIdx.y * ep.slab_stride + (int64_t)m * ep.ldc + n;
+            *(f32x4*)o = lo;
+            *(f32x4*)(o + 4) = hi;
+            continue;
+          }
+          float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          if (ep.bias)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] += (n + e < ep.bias_n) ? ep.bias[n + e] : 0.f;
+          if (ep.relu)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] = fmaxf(x[e], 0.f);
+          if (ep.mask) {
+            const u32x4 mk = *(const u32x4*)(ep.mask + (int64_t)m * ep.ldm + n);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (!(u4_get(mk, e) > 0.f)) x[e] = 0.f;
+          }
+          if (ep.mode == EPI_F32) {
+            float* o = (float*)ep.out + (int64_t)m * ep.ldc + n;
+            *(f32x4*)o = f32x4{x[0], x[1], x[2], x[3]};
+            *(f32x4*)(o + 4) = f32x4{x[4], x[5], x[6], x[7]};
+          } else {
+            *(u32x4*)((bf16_t*)ep.out + (int64_t)m * ep.ldc + n) =
+                u32x4{pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(x[4], x[5]), pack2(x[6], x[7])};
+          }
+        }
+      }
+      __syncthreads();
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
 #pragma unroll
@@ -355,20 +410,63 @@ hipError_t launch_cfg(const LA& la, const LB& lb, const GemmEpi& ep, int M, int 
   return hipGetLastError();
 }
 
-// Tile selection by output width N (narrow N = conv channels; wide N = dense).
+// Tile choice (ops/functional.py::gemm_tile mirrors the weight-gradient rule).
+//  * Weight gradients (A and B both MN-contiguous, K = batch or pixels) have a
+//    small output and a huge K: small tiles give every split many workgroups,
+//    so the deterministic fp32 split-K slab (splits x M x N) stays small.
+//  * Everything else drops to 64-row tiles whenever the large tile would leave
+//    the 256 CUs with fewer than 4 workgroups each.
+enum TileCode { T256x16, T256x32, T128x64, T64x128, T128x128, T64x16, T64x32, T64x64 };
+
+int tile_code(int M, int N, bool wgrad) {
+  auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+  if (wgrad) {
+    if (N <= 16) return T64x16;
+    if (N <= 32) return T64x32;
+    if (N <= 64 || tiles(128, 128) < 256) return T64x64;
+    return T128x128;
+  }
+  if (N <= 16) return tiles(256, 16) >= 1024 ? T256x16 : T64x16;
+  if (N <= 32) return tiles(256, 32) >= 1024 ? T256x32 : T64x32;
+  if (N <= 64) return tiles(128, 64) >= 1024 ? T128x64 : T64x64;
+  if (M <= 64 || tiles(128, 128) < 1024) return T64x128;
+  return T128x128;
+}
+
 template <class LA, bool AKC, class LB, bool BKC>
 hipError_t launch_any(const LA& la, const LB& lb, const GemmEpi& ep, int M, int N, int K, int splits,
                       hipStream_t st) {
-  if (N <= 16) return launch_cfg<256, 16, 4, 1, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
-  if (N <= 32) return launch_cfg<256, 32, 4, 1, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
-  if (N <= 64) return launch_cfg<128, 64, 2, 2, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
-  if (M <= 64) return launch_cfg<64, 128, 1, 4, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
-  return launch_cfg<128, 128, 2, 2, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+  constexpr bool WG = !AKC && !BKC;
+  switch (tile_code(M, N, WG)) {
+    case T64x16: return launch_cfg<64, 16, 4, 1, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+    case T64x32: return launch_cfg<64, 32, 4, 1, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+    case T64x64: return launch_cfg<64, 64, 2, 2, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+    case T128x128: return launch_cfg<128, 128, 2, 2, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+    default: break;
+  }
+  if constexpr (!WG) {
+    switch (tile_code(M, N, false)) {
+      case T256x16: return launch_cfg<256, 16, 4, 1, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+      case T256x32: return launch_cfg<256, 32, 4, 1, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+      case T128x64: return launch_cfg<128, 64, 2, 2, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+      case T64x128: return launch_cfg<64, 128, 1, 4, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+      default: break;
+    }
+  }
+  return hipErrorInvalidValue;
 }
 
 }  // namespace
 
 // ---------------------------------------------------------------- public launchers
+void gemm_tile(int M, int N, int wgrad, int* bm, int* bn) {
+  static const int BMS[] = {256, 256, 128, 64, 128, 64, 64, 64};
+  static const int BNS[] = {16, 32, 64, 128, 128, 16, 32, 64};
+  const int c = tile_code(M, N, wgrad != 0);
+  *bm = BMS[c];
+  *bn = BNS[c];
+}
+
 hipError_t dense_fwd(const bf16_t* x, const bf16_t* w, int M, int N, int K, int ldx, int ldw,
                      const GemmEpi& ep, hipStream_t st) {
   MatLoader a{x, M, K, ldx, -1};

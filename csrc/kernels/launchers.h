@@ -24,6 +24,8 @@ struct GemmEpi {
 };
 
 // ---- gemm.hip
+// tile (BM, BN) launch_any picks for an M x N output (wgrad: both operands MN-contiguous)
+void gemm_tile(int M, int N, int wgrad, int* bm, int* bn);
 hipError_t dense_fwd(const bf16_t* x, const bf16_t* w, int M, int N, int K, int ldx, int ldw,
                      const GemmEpi& ep, hipStream_t st);
 hipError_t dense_dgrad(const bf16_t* dy, const bf16_t* w, int M, int N, int K, int lddy, int ldw,
@@ -63,7 +65,8 @@ hipError_t lrn_bwd(const bf16_t* x, const bf16_t* dy, int P, int C, int r, float
                    int relu_mask, bf16_t* dx, hipStream_t st);
 hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B, int NC, float scale,
                       bf16_t* dlogits, int ldd, float* stats, float* probs, hipStream_t st);
-hipError_t splitk_reduce(const float* slab, int splits, int M, int N, int G, int Ipad, int I, int J,
+// NOTE: many splits over a small output are pre-summed IN PLACE (the slab is scratch).
+hipError_t splitk_reduce(float* slab, int splits, int M, int N, int G, int Ipad, int I, int J,
                          int bias_row, float* wdst, float* bdst, float scale, hipStream_t st);
 
 struct OptSeg {          // one trainable tensor inside the flat buffers

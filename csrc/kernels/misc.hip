@@ -324,26 +324,52 @@ __global__ void splitk_reduce_k(const float* __restrict__ slab, int S, int M, in
   }
 }
 
-__global__ void splitk_reduce_wave_k(const float* __restrict__ slab, int S, int M, int N, int G, int Ipad, int I,
-                                     int J, int bias_row, float* __restrict__ wdst, float* __restrict__ bdst,
-                                     float scale) {
-  const int64_t nw = (int64_t)G * I * J;
-  const int64_t total = nw + (bdst ? J : 0);
-  const int64_t ss = (int64_t)M * N;
-  const int lane = threadIdx.x & 63;
-  const int64_t wpb = blockDim.x / 64;
-  for (int64_t t = blockIdx.x * wpb + (threadIdx.x >> 6); t < total; t += (int64_t)gridDim.x * wpb) {
-    int j;
-    const int64_t row = reduce_row(t, nw, G, Ipad, I, J, bias_row, j);
-    const float* p = slab + row * N + j;
-    float s = 0.f;
-    for (int z = lane; z < S; z += 64) s += p[z * ss];
-    s = warp_sum(s);
-    if (lane == 0) {
-      if (t < nw) wdst[t] = s * scale;
-      else bdst[j] = s * scale;
+// Coalesced variant (N % 4 == 0): each lane owns 4 consecutive slab columns of one
+// row (one 16-byte load per split), the 4 waves of a block take every 4th split,
+// and the 4 partial sums are combined in a fixed order (deterministic).
+// Splits z*zstride, z < S, are summed (zstride > 1 after splitk_partial4_k).
+__global__ __launch_bounds__(256) void splitk_reduce4_k(const float* __restrict__ slab, int S, int zstride, int M,
+                                                        int N, int G, int Ipad, int I, int J, int bias_row,
+                                                        float* __restrict__ wdst, float* __restrict__ bdst,
+                                                        float scale) {
+  __shared__ f32x4 part[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int NQ = N >> 2;
+  const int64_t nq = (int64_t)M * NQ;
+  const int64_t qd = (int64_t)blockIdx.x * 64 + lane;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (qd < nq) {
+    const f32x4* p = (const f32x4*)slab + qd;
+    const int64_t zs = (int64_t)zstride * nq;
+    int z = wave;
+    for (; z + 12 < S; z += 16) {
+      const f32x4 a = p[z * zs], b = p[(z + 4) * zs];
+      const f32x4 c = p[(z + 8) * zs], d = p[(z + 12) * zs];
+      acc += a;
+      acc += b;
+      acc += c;
+      acc += d;
     }
+    for (; z < S; z += 4) acc += p[z * zs];
   }
+  part[wave][lane] = acc;
+  __syncthreads();
+  if (wave != 0 || qd >= nq) return;
+  const f32x4 t = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+  const int row = (int)(qd / NQ), j0 = (int)(qd - (int64_t)row * NQ) * 4;
+  if (row == bias_row) {
+    if (bdst)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        if (j0 + jj < J) bdst[j0 + jj] = t[jj] * scale;
+    return;
+  }
+  const int g = row / Ipad, i = row - g * Ipad;
+  if (g >= G || i >= I) return;
+  float* d = wdst + ((int64_t)g * I + i) * J;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj)
+    if (j0 + jj < J) d[j0 + jj] = t[jj] * scale;
 }
 
 // ------------------------------------------------------------------ K9 fused optimizer
@@ -527,15 +553,43 @@ hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B
   return hipGetLastError();
 }
 
-hipError_t splitk_reduce(const float* slab, int splits, int M, int N, int G, int Ipad, int I, int J, int bias_row,
+// First pass for many splits over a small output: block (qb, sb) sums splits
+// [64 sb, 64 sb + 64) of its 64 quads and stores the sum IN PLACE in split 64 sb
+// (only this block reads or writes that range), so pass 2 has S/64 splits.
+constexpr int RED_CHUNK = 64;
+__global__ __launch_bounds__(256) void splitk_partial4_k(float* __restrict__ slab, int S, int64_t nq) {
+  __shared__ f32x4 part[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t qd = (int64_t)blockIdx.x * 64 + lane;
+  const int z0 = blockIdx.y * RED_CHUNK, z1 = min(S, z0 + RED_CHUNK);
+  f32x4* p = (f32x4*)slab + qd;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (qd < nq)
+    for (int z = z0 + wave; z < z1; z += 4) acc += p[(int64_t)z * nq];
+  part[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && qd < nq) p[(int64_t)z0 * nq] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+}
+
+hipError_t splitk_reduce(float* slab, int splits, int M, int N, int G, int Ipad, int I, int J, int bias_row,
                          float* wdst, float* bdst, float scale, hipStream_t st) {
   const int64_t total = (int64_t)G * I * J + (bdst ? J : 0);
-  if (splits >= 32)
-    hipLaunchKernelGGL(splitk_reduce_wave_k, dim3(nblocks(total, TPB / 64, 8192)), dim3(TPB), 0, st, slab, splits, M,
-                       N, G, Ipad, I, J, bias_row, wdst, bdst, scale);
-  else
+  if (N % 4 == 0 && splits > 1) {
+    const int64_t nq = (int64_t)M * (N / 4);
+    const unsigned qb = (unsigned)((nq + 63) / 64);
+    int S = splits, zstride = 1;
+    if (S > RED_CHUNK && qb < 512) {
+      const int sb = (S + RED_CHUNK - 1) / RED_CHUNK;
+      hipLaunchKernelGGL(splitk_partial4_k, dim3(qb, sb), dim3(256), 0, st, slab, S, nq);
+      S = sb;
+      zstride = RED_CHUNK;
+    }
+    hipLaunchKernelGGL(splitk_reduce4_k, dim3(qb), dim3(256), 0, st, slab, S, zstride, M, N, G, Ipad, I, J,
+                       bias_row, wdst, bdst, scale);
+  } else {
     hipLaunchKernelGGL(splitk_reduce_k, dim3(nblocks(total, TPB, 8192)), dim3(TPB), 0, st, slab, splits, M, N, G,
                        Ipad, I, J, bias_row, wdst, bdst, scale);
+  }
   return hipGetLastError();
 }
 

@@ -22,7 +22,7 @@ import torch
 from ._ext import kernels
 
 BK = 32
-TARGET_BLOCKS = 1024   # ~4 workgroups per CU on 256 CUs
+TARGET_BLOCKS = 2048   # ~8 workgroups per CU on 256 CUs
 
 
 def pad8(c: int) -> int:
@@ -30,23 +30,24 @@ def pad8(c: int) -> int:
 
 
 def gemm_tile(M: int, N: int) -> Tuple[int, int]:
-    """Mirror of ``launch_any`` tile selection in gemm.hip."""
+    """Tile of a weight-gradient GEMM: mirror of ``tile_code(M, N, wgrad=true)``
+    in gemm.hip (checked against ``kernels().gemm_tile`` by the GPU tests).
+    Small tiles give every K-split many workgroups, which keeps the
+    deterministic split-K slab (splits x M x N fp32) small."""
     if N <= 16:
-        return 256, 16
+        return 64, 16
     if N <= 32:
-        return 256, 32
-    if N <= 64:
-        return 128, 64
-    if M <= 64:
-        return 64, 128
+        return 64, 32
+    if N <= 64 or math.ceil(M / 128) * math.ceil(N / 128) < 256:
+        return 64, 64
     return 128, 128
 
 
-SLAB_CAP = 8 << 20    # fp32 elements of split-K partials (32 MB)
+SLAB_CAP = 16 << 20   # fp32 elements of split-K partials (64 MB)
 
 
-def pick_splits(M: int, N: int, K: int, target: int = TARGET_BLOCKS, min_k: int = 1024) -> int:
-    """Split-K factor for a weight-gradient GEMM: fill ~4 WGs/CU, but keep every
+def pick_splits(M: int, N: int, K: int, target: int = TARGET_BLOCKS, min_k: int = 256) -> int:
+    """Split-K factor for a weight-gradient GEMM: fill ~8 WGs/CU, but keep every
     split >= min_k reduction elements and the fp32 slab under SLAB_CAP."""
     bm, bn = gemm_tile(M, N)
     tiles = math.ceil(M / bm) * math.ceil(N / bn)

@@ -73,7 +73,9 @@ def test_dense_dgrad(dev, K, M, Din, Dout):
 
 
 @pytest.mark.parametrize("B,Din,Dout,splits", [(128, 3136, 1024, None), (1000, 400, 120, None),
-                                               (777, 120, 88, 3), (64, 88, 16, 1), (4096, 1024, 192, None)])
+                                               (777, 120, 88, 3), (64, 88, 16, 1), (4096, 1024, 192, None),
+                                               (96, 4096, 1024, None), (3000, 200, 32, None),
+                                               (8192, 88, 16, 100), (20000, 120, 88, 300)])
 def test_dense_wgrad(dev, K, B, Din, Dout, splits):
     torch.manual_seed(2)
     x = rnd(B, Din, dev=dev)
@@ -83,6 +85,28 @@ def test_dense_wgrad(dev, K, B, Din, Dout, splits):
     ref = x.float().t() @ dy.float()
     close(dw, ref[:din, :dout], rel=1e-3)
     close(db, dy.float().sum(0)[:dout], rel=1e-3)
+
+
+# every tile code of launch_any (large M reaches the 128/256-row tiles)
+@pytest.mark.parametrize("M,N,Kd,tile", [(262144, 16, 88, (256, 16)), (262144, 32, 40, (256, 32)),
+                                         (131072, 64, 64, (128, 64)), (131072, 128, 64, (128, 128)),
+                                         (65536, 128, 400, (64, 128)), (4000, 64, 72, (64, 64)),
+                                         (9000, 24, 48, (64, 32)), (1000, 10, 40, (64, 16))])
+def test_gemm_tile_codes(dev, K, M, N, Kd, tile):
+    assert tuple(K.gemm_tile(M, N, False)) == tile
+    torch.manual_seed(5)
+    x = rnd(M, Kd, dev=dev)
+    w = rnd(Kd, N, dev=dev, scale=1 / math.sqrt(Kd))
+    out = Fk.dense(x, w, None, False, out_dtype=torch.float32)
+    close(out, x.float() @ w.float(), rel=1e-4)
+    dx = Fk.dense_dgrad(out.to(torch.bfloat16)[:, :N], w)
+    close(dx, out.to(torch.bfloat16).float() @ w.float().t())
+
+
+@pytest.mark.parametrize("M,N", [(401, 120), (121, 88), (89, 16), (801, 64), (3137, 384), (4097, 1024),
+                                 (201, 32), (26, 8), (49, 32)])
+def test_wgrad_tile_mirror(K, M, N):
+    assert tuple(K.gemm_tile(M, N, True)) == Fk.gemm_tile(M, N)
 
 
 # ---------------------------------------------------------------- conv

@@ -411,32 +411,34 @@ void convpool_fwd(Tensor x, Tensor w, Tensor bias, int64_t bias_n, Tensor pooled
          "convpool_fwd");
 }
 
-void convpool_wgrad(Tensor x, Tensor dP, Tensor arg, Tensor pooled, Tensor slab, int64_t grid, int64_t B, int64_t cin,
-                    int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t wd) {
+void convpool_wgrad(Tensor x, Tensor dP, Tensor arg, Tensor slab, int64_t grid, int64_t B, int64_t cin, int64_t cout,
+                    int64_t ks, int64_t pad, int64_t h, int64_t wd) {
   auto g = cp_geo(cin, cout, ks, pad, h, wd);
   TORCH_CHECK(grid >= 1 && grid <= 65535, "grid");
   const int64_t np = B * g.PH * g.PW * cout;
   check(x, at::kBFloat16, B * h * wd * cin, "x");
   check(dP, at::kBFloat16, np, "dP");
   check(arg, at::kByte, np, "arg");
-  check(pooled, at::kBFloat16, np, "pooled");
   check(slab, at::kFloat, grid * g.KM * cout, "slab");
-  hip_ok(mnistx::convpool_wgrad(g.cfg, BF(x), BF(dP), P<const uint8_t>(arg), BF(pooled), (int)B, P<float>(slab),
-                                (int)grid, cur_stream()),
+  hip_ok(mnistx::convpool_wgrad(g.cfg, BF(x), BF(dP), P<const uint8_t>(arg), (int)B, P<float>(slab), (int)grid,
+                                cur_stream()),
          "convpool_wgrad");
 }
 
-void convpool_dgrad(Tensor dP, Tensor arg, Tensor pooled, Tensor w, Tensor dx, int64_t B, int64_t cin, int64_t cout,
-                    int64_t ks, int64_t pad, int64_t h, int64_t wd) {
+bool convpool_has_dgrad(int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t w) {
+  return mnistx::convpool_has_dgrad(cp_geo(cin, cout, ks, pad, h, w).cfg) != 0;
+}
+
+void convpool_dgrad(Tensor dP, Tensor arg, Tensor w, Tensor dx, int64_t B, int64_t cin, int64_t cout, int64_t ks,
+                    int64_t pad, int64_t h, int64_t wd) {
   auto g = cp_geo(cin, cout, ks, pad, h, wd);
+  TORCH_CHECK(mnistx::convpool_has_dgrad(g.cfg), "convpool_dgrad: no fused dgrad for this geometry");
   const int64_t np = B * g.PH * g.PW * cout;
   check(dP, at::kBFloat16, np, "dP");
   check(arg, at::kByte, np, "arg");
-  check(pooled, at::kBFloat16, np, "pooled");
   check(w, at::kBFloat16, ks * ks * cin * cout, "w");
   check(dx, at::kBFloat16, B * h * wd * cin, "dx");
-  hip_ok(mnistx::convpool_dgrad(g.cfg, BF(dP), P<const uint8_t>(arg), BF(pooled), BF(w), (int)B, BFm(dx),
-                                cur_stream()),
+  hip_ok(mnistx::convpool_dgrad(g.cfg, BF(dP), P<const uint8_t>(arg), BF(w), (int)B, BFm(dx), cur_stream()),
          "convpool_dgrad");
 }
 
@@ -467,5 +469,6 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("convpool_fwd", &convpool_fwd);
   m.def("convpool_wgrad", &convpool_wgrad);
   m.def("convpool_dgrad", &convpool_dgrad);
+  m.def("convpool_has_dgrad", &convpool_has_dgrad);
   m.attr("ARCH") = "gfx950";
 }

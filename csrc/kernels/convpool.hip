@@ -3,23 +3,26 @@
 // The first conv layers of MNIST nets have tiny channel counts (Cin 1/3/8, Cout
 // 8/16/32), so a generic implicit GEMM wastes its tiles and spends its time in
 // index arithmetic.  These kernels are specialised at compile time on the
-// layer geometry and keep one padded input image per LDS tile:
+// layer geometry and keep whole padded input images as LDS tiles:
 //
 // * Pool-window-major GEMM rows: output pixel row r = 4*window + d with
 //   d = (dy, dx) inside the 2x2 pooling window.  A v_mfma_f32_16x16x32_bf16
 //   accumulator gives each lane rows 4g..4g+3 of one column, i.e. exactly one
-//   pooling window of one channel — so bias + ReLU + max-pool + argmax happen
-//   in registers and the full-resolution conv output never touches HBM.
-// * im2col fragments are gathered straight from the LDS tile with per-lane
-//   offsets precomputed once per kernel (no division in the inner loop);
-//   weight fragments stay in VGPRs for the whole persistent grid-stride loop.
-// * Backward (wgrad): the max-unpool + ReLU mask is applied while building the
-//   dY operand from the pooled gradient (argmax byte + pooled value > 0), the
-//   bias gradient is a virtual ones-row of the im2col operand, per-block fp32
+//   pooling window of one channel -- bias + ReLU + max-pool + argmax happen in
+//   registers and the full-resolution conv output never touches HBM.
+// * im2col fragments are aligned vector LDS reads: Cin 8 -> one ds_read_b128 of
+//   8 channels; Cin 1 -> K ordered (kh, kw padded to 8) and the image kept 4x in
+//   LDS shifted by 0..3 elements, so every run of 4 pixels is one aligned
+//   ds_read_b64.  Weight gradients read im2col^T with ds_read_b64_tr_b16.
+// * Idle MFMA columns: with Cout 8 (LeNet conv1) / Cin 8 (LeNet conv2 dgrad) the
+//   16-wide MFMA N dimension is half empty; the "pair" kernels fill columns
+//   8..15 with the kw-shifted filter, i.e. the horizontally adjacent pixel.
+// * Backward rebuilds dY from the pooled gradient and the argmax byte; the ReLU
+//   mask is folded into the byte (ARG_OFF), so the pooled activations are never
+//   re-read.  wgrad's bias gradient is a virtual ones-row; per-block fp32
 //   partials go to a slab reduced deterministically by splitk_reduce.
-// * Backward (dgrad, LeNet conv2): the unpooled dY image is staged in LDS with
-//   a KS-1-PAD halo; the flipped-filter implicit GEMM reads its K-contiguous
-//   operand with ds_read_b64.
+// * Staging is software-pipelined: the next image group's global data is
+//   loaded into VGPRs while the current group computes.
 //
 // Replaces: Conv2D + BiasAdd + Relu + MaxPool and
 // their gradients at mnist_input.py:142-150 (conv1 -> pool1) and the LeNet-5
@@ -67,10 +70,10 @@ struct Geo {
   //                         four consecutive pixels of one input row; the image is
   //                         kept in LDS 4 times, shifted by 0..3 elements, so every
   //                         such run is ONE aligned 8-byte LDS read.
-  //  MODE 1 (Cin % 4 == 0): k = (kh*KS + kw)*Cin + ci; four consecutive k are four
-  //                         channels of one pixel (aligned 8-byte read).
+  //  MODE 1 (Cin % 8 == 0): k = (kh*KS + kw)*Cin + ci; a lane's 8 k-slots are the 8
+  //                         consecutive channels of one tap (one ds_read_b128).
   //  MODE 2 (other Cin):    MODE 1 order with scalar 2-byte gathers.
-  static constexpr int MODE = CIN == 1 ? 0 : (CIN % 4 == 0 ? 1 : 2);
+  static constexpr int MODE = CIN == 1 ? 0 : (CIN % 8 == 0 ? 1 : 2);
   static constexpr int KC = KS * KS * CIN;             // real im2col columns
   static constexpr int KE = MODE == 0 ? KS * 8 : KC;   // im2col columns incl. kw padding
   static constexpr int KSTEPS = (KE + 31) / 32;
@@ -119,11 +122,22 @@ struct Geo {
     if constexpr (MODE == 0) return a + (a & 3) * (TSTR - 1);
     else return a;
   }
+  // im2col column of A/B fragment element j of lane group g in k-step s.
+  // MODE 0: two runs of 4 (4g.., 16+4g..) = two aligned 8-byte reads;
+  // MODE 1/2: one run of 8 (8g..) = one 16-byte read (MODE 1).
+  static DEV int kslot(int s, int g, int j) {
+    if constexpr (MODE == 0) return 32 * s + 4 * g + (j & 3) + 16 * (j >> 2);
+    else return 32 * s + 8 * g + j;
+  }
 };
 
 DEV __bf16 as_bf(bf16_t v) { return __builtin_bit_cast(__bf16, v); }
 
 constexpr int NTH = 256;
+// Argmax byte of a pool window whose ReLU output is 0: matches no position, so
+// the backward kernels need only (dP, arg) -- the ReLU mask is folded in here
+// and the pooled activations are never re-read.
+constexpr uint32_t ARG_OFF = 4;
 
 template <int N>
 DEV void lds_zero(bf16_t* p, int tid) {
@@ -131,36 +145,91 @@ DEV void lds_zero(bf16_t* p, int tid) {
   for (int e = tid; e < N / 8; e += NTH) *(u32x4*)(p + 8 * e) = u32x4{0u, 0u, 0u, 0u};
 }
 
-// Copy IMGS input images (NHWC, interior only) into copy 0 of their LDS tiles
-// with 8-byte vectors; the zero border written once at kernel start is untouched.
-// MODE 0 then derives the three shifted copies (copy_s[j] = copy_0[j + s]).
+// ------------------------------------------------------------------ staging
+// Global data of the NEXT image group is loaded into VGPRs while the current
+// group computes (software pipelining); store() moves it to LDS after the barrier.
+
+// Input interiors (NHWC rows) -> copy 0 of the LDS image tiles, 8-byte vectors.
 template <class G, int IMGS>
-DEV void fill_tiles(bf16_t* tile, const bf16_t* __restrict__ x, int img0, int B, int tid) {
-  constexpr int NV = IMGS * G::H * G::ROWV;
-  for (int e = tid; e < NV; e += NTH) {
-    const int im = e / (G::H * G::ROWV), rem = e - im * (G::H * G::ROWV);
-    const int hh = rem / G::ROWV, vv = rem - hh * G::ROWV;
-    u32x2 v = {0u, 0u};
-    if (img0 + im < B) v = *(const u32x2*)(x + (int64_t)(img0 + im) * G::INTERIOR + hh * G::W * G::CIN + 4 * vv);
-    *(u32x2*)(tile + im * G::IMG_LDS + ((hh + G::PAD) * G::WS + G::X0) * G::CIN + 4 * vv) = v;
-  }
-  if constexpr (G::MODE == 0) {
-    __syncthreads();
-    constexpr int NG = G::TSTR / 4;
-    for (int e = tid; e < IMGS * NG; e += NTH) {
-      const int im = e / NG, v = e - im * NG;
-      bf16_t* src = tile + im * G::IMG_LDS;
-      const u32x2 lo = *(const u32x2*)(src + 4 * v);
-      const u32x2 hi = (v + 1 < NG) ? *(const u32x2*)(src + 4 * v + 4) : u32x2{0u, 0u};
-      const uint32_t w0 = lo[0], w1 = lo[1], w2 = hi[0], w3 = hi[1];
-      *(u32x2*)(src + 1 * G::TSTR + 4 * v) = u32x2{__builtin_amdgcn_alignbit(w1, w0, 16),
-                                                   __builtin_amdgcn_alignbit(w2, w1, 16)};
-      *(u32x2*)(src + 2 * G::TSTR + 4 * v) = u32x2{w1, w2};
-      *(u32x2*)(src + 3 * G::TSTR + 4 * v) = u32x2{__builtin_amdgcn_alignbit(w2, w1, 16),
-                                                   __builtin_amdgcn_alignbit(w3, w2, 16)};
+struct XStage {
+  static constexpr int NV = IMGS * G::H * G::ROWV;
+  static constexpr int PER = (NV + NTH - 1) / NTH;
+  u32x2 v[PER];
+  DEV void load(const bf16_t* __restrict__ x, int img0, int B, int tid) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = tid + u * NTH;
+      v[u] = u32x2{0u, 0u};
+      if (e < NV) {
+        const int im = e / (G::H * G::ROWV), rem = e - im * (G::H * G::ROWV);
+        if (img0 + im < B) v[u] = *(const u32x2*)(x + (int64_t)(img0 + im) * G::INTERIOR + rem * 4);
+      }
     }
   }
+  DEV void store(bf16_t* tile, int tid) const {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = tid + u * NTH;
+      if (e < NV) {
+        const int im = e / (G::H * G::ROWV), rem = e - im * (G::H * G::ROWV);
+        const int hh = rem / G::ROWV, vv = rem - hh * G::ROWV;
+        *(u32x2*)(tile + im * G::IMG_LDS + ((hh + G::PAD) * G::WS + G::X0) * G::CIN + 4 * vv) = v[u];
+      }
+    }
+  }
+};
+
+// MODE 0: derive the three shifted copies (copy_s[j] = copy_0[j + s]) of every image.
+template <class G, int IMGS>
+DEV void make_shifted(bf16_t* tile, int tid) {
+  constexpr int NG = G::TSTR / 4;
+  for (int e = tid; e < IMGS * NG; e += NTH) {
+    const int im = e / NG, v = e - im * NG;
+    bf16_t* src = tile + im * G::IMG_LDS;
+    const u32x2 lo = *(const u32x2*)(src + 4 * v);
+    const u32x2 hi = (v + 1 < NG) ? *(const u32x2*)(src + 4 * v + 4) : u32x2{0u, 0u};
+    const uint32_t w0 = lo[0], w1 = lo[1], w2 = hi[0], w3 = hi[1];
+    *(u32x2*)(src + 1 * G::TSTR + 4 * v) = u32x2{__builtin_amdgcn_alignbit(w1, w0, 16),
+                                                 __builtin_amdgcn_alignbit(w2, w1, 16)};
+    *(u32x2*)(src + 2 * G::TSTR + 4 * v) = u32x2{w1, w2};
+    *(u32x2*)(src + 3 * G::TSTR + 4 * v) = u32x2{__builtin_amdgcn_alignbit(w2, w1, 16),
+                                                 __builtin_amdgcn_alignbit(w3, w2, 16)};
+  }
 }
+
+// Pooled gradient + argmax bytes ([img][window][Cout]), 8 channels per vector.
+template <class G, int IMGS>
+struct DYStage {
+  static constexpr int NWC = G::NWIN * G::COUT;
+  static constexpr int NV = IMGS * NWC / 8;
+  static constexpr int PER = (NV + NTH - 1) / NTH;
+  static_assert(NWC % 8 == 0, "");
+  u32x4 y[PER];
+  u32x2 a[PER];
+  DEV void load(const bf16_t* __restrict__ dP, const uint8_t* __restrict__ arg, int img0, int B, int tid) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = 8 * (tid + u * NTH);
+      y[u] = u32x4{0u, 0u, 0u, 0u};
+      a[u] = u32x2{0x04040404u, 0x04040404u};
+      if (e < IMGS * NWC && img0 + e / NWC < B) {
+        const int64_t o = (int64_t)img0 * NWC + e;
+        y[u] = *(const u32x4*)(dP + o);
+        a[u] = *(const u32x2*)(arg + o);
+      }
+    }
+  }
+  DEV void store(bf16_t* dys, uint8_t* args, int tid) const {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = 8 * (tid + u * NTH);
+      if (e < IMGS * NWC) {
+        *(u32x4*)(dys + e) = y[u];
+        *(u32x2*)(args + e) = a[u];
+      }
+    }
+  }
+};
 
 // ------------------------------------------------------------------ forward
 template <class G, int IMGS>
@@ -173,7 +242,8 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_k(const bf16_t* __restrict__
   const int g = lane >> 4, li = lane & 15;
   lds_zero<LDS>(tile, tid);
 
-  // per-lane A-operand offsets: dd = 4-column chunk deltas (MODE 0/1), dl = scalar deltas (MODE 2)
+  // per-lane A-operand offsets: dd = run deltas (MODE 0: two 4-runs; MODE 1: one 8-run),
+  // dl = scalar deltas (MODE 2)
   int dd[G::KSTEPS][2];
   int dl[G::MODE == 2 ? G::KSTEPS : 1][8];
   bf16x8 bfr[G::KSTEPS][G::NF];
@@ -181,12 +251,12 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_k(const bf16_t* __restrict__
   for (int s = 0; s < G::KSTEPS; ++s) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int k0 = 32 * s + 16 * h + 4 * g;
-      dd[s][h] = k0 < G::KE ? G::chunk_delta(k0) : 0;   // padded k: any finite pixel (zero weight)
+      const int k0 = G::kslot(s, g, 4 * h);
+      dd[s][h] = (G::MODE != 2 && k0 < G::KE) ? G::chunk_delta(k0) : 0;  // padded k: finite pixel, zero weight
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int k = 32 * s + 4 * g + (j & 3) + 16 * (j >> 2);
+      const int k = G::kslot(s, g, j);
       if constexpr (G::MODE == 2) dl[s][j] = k < G::KC ? G::kdelta(k) : 0;
       bool valid;
       int wrow;
@@ -211,10 +281,18 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_k(const bf16_t* __restrict__
     bs[nf] = n < bias_n ? bias[n] : 0.f;
   }
 
-  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += gridDim.x * IMGS) {
+  const int stride = gridDim.x * IMGS;
+  XStage<G, IMGS> xs;
+  xs.load(x, blockIdx.x * IMGS, B, tid);
+  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
     __syncthreads();
-    fill_tiles<G, IMGS>(tile, x, img0, B, tid);
+    xs.store(tile, tid);
     __syncthreads();
+    if constexpr (G::MODE == 0) {
+      make_shifted<G, IMGS>(tile, tid);
+      __syncthreads();
+    }
+    if (img0 + stride < B) xs.load(x, img0 + stride, B, tid);
     for (int f = wave; f < IMGS * G::MF; f += NTH / 64) {
       const int im = f / G::MF, fm = f - im * G::MF;
       const int r = min(fm * 16 + li, G::NPIX - 1);
@@ -229,6 +307,8 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_k(const bf16_t* __restrict__
         if constexpr (G::MODE == 2) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) a[j] = as_bf(tb[pb + dl[s][j]]);
+        } else if constexpr (G::MODE == 1) {
+          a = __builtin_bit_cast(bf16x8, *(const u32x4*)(tb + pb + dd[s][0]));
         } else {
           const s16x4 lo = *(const s16x4*)(tb + G::aligned_off(pb + dd[s][0]));
           const s16x4 hi = *(const s16x4*)(tb + G::aligned_off(pb + dd[s][1]));
@@ -249,8 +329,9 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_k(const bf16_t* __restrict__
             const f32x4 v = acc[nf];
             const float m = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
             const int bi = v[0] == m ? 0 : (v[1] == m ? 1 : (v[2] == m ? 2 : 3));
-            pimg[win * G::COUT + n] = f2bf(fmaxf(m + bs[nf], 0.f));
-            aimg[win * G::COUT + n] = (uint8_t)bi;
+            const float o = m + bs[nf];
+            pimg[win * G::COUT + n] = f2bf(fmaxf(o, 0.f));
+            aimg[win * G::COUT + n] = (uint8_t)(o > 0.f ? bi : ARG_OFF);
           }
         }
       }
@@ -302,10 +383,16 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_pair_k(const bf16_t* __restr
   }
   const float bs = c < bias_n ? bias[c] : 0.f;
 
-  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += gridDim.x * IMGS) {
+  const int stride = gridDim.x * IMGS;
+  XStage<G, IMGS> xs;
+  xs.load(x, blockIdx.x * IMGS, B, tid);
+  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
     __syncthreads();
-    fill_tiles<G, IMGS>(tile, x, img0, B, tid);
+    xs.store(tile, tid);
     __syncthreads();
+    make_shifted<G, IMGS>(tile, tid);
+    __syncthreads();
+    if (img0 + stride < B) xs.load(x, img0 + stride, B, tid);
 #pragma unroll 1
     for (int im = 0; im < IMGS; ++im) {
       const bf16_t* timg = tile + im * G::IMG_LDS;
@@ -332,8 +419,9 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_pair_k(const bf16_t* __restr
         const bool right = R > L;
         const int wo = fm * 8 + 2 * g + sx;
         if (wo < G::NWIN && img_ok) {
-          pimg[wo * 8 + c] = f2bf(fmaxf((right ? R : L) + bs, 0.f));
-          aimg[wo * 8 + c] = (uint8_t)(right ? dR + 1 : dL);
+          const float o = (right ? R : L) + bs;
+          pimg[wo * 8 + c] = f2bf(fmaxf(o, 0.f));
+          aimg[wo * 8 + c] = (uint8_t)(o > 0.f ? (right ? dR + 1 : dL) : (int)ARG_OFF);
         }
       }
     }
@@ -344,11 +432,11 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_pair_k(const bf16_t* __restr
 // dW[k][n] = sum over pixels of im2col[pixel][k] * dY[pixel][n]: M = k, N = Cout,
 // reduction = pixels (pool-window-major).  MODE 0/1 read the im2col^T operand
 // with ds_read_b64_tr_b16: each lane supplies one pixel row and one 4-column
-// chunk; the bias row (k = KE) reads a constant [1,0,0,0] LDS cell.
+// chunk; the bias row (k = KE) reads a constant [1,0,0,0] LDS cell.  dY is
+// rebuilt from (dP, arg): position d of a window gets dP iff arg == d.
 template <class G, int IMGS>
 __global__ __launch_bounds__(NTH) void convpool_wgrad_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dP,
-                                                        const uint8_t* __restrict__ arg,
-                                                        const bf16_t* __restrict__ P, int B,
+                                                        const uint8_t* __restrict__ arg, int B,
                                                         float* __restrict__ slab) {
   constexpr int CELL = IMGS * G::IMG_LDS;             // [1,0,0,0] then [0,0,0,0]
   constexpr int LDS = (CELL + 8 + 7) / 8 * 8;
@@ -385,29 +473,24 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_k(const bf16_t* __restrict
 #pragma unroll
     for (int nf = 0; nf < G::NF; ++nf) acc[mf][nf] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  constexpr int DEL = IMGS * G::NWIN * G::COUT;
-  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += gridDim.x * IMGS) {
+  const int stride = gridDim.x * IMGS;
+  XStage<G, IMGS> xs;
+  DYStage<G, IMGS> ys;
+  xs.load(x, blockIdx.x * IMGS, B, tid);
+  ys.load(dP, arg, blockIdx.x * IMGS, B, tid);
+  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
     __syncthreads();
-    static_assert(DEL % 8 == 0, "");
-    for (int e8 = tid; e8 < DEL / 8; e8 += NTH) {
-      const int e = 8 * e8;
-      const int im = e / (G::NWIN * G::COUT);
-      u32x4 v = {0u, 0u, 0u, 0u};
-      u32x2 a = {0xffffffffu, 0xffffffffu};
-      if (img0 + im < B) {
-        const int64_t o = (int64_t)img0 * G::NWIN * G::COUT + e;
-        const u32x4 pv = *(const u32x4*)(P + o);
-        v = *(const u32x4*)(dP + o);
-        a = *(const u32x2*)(arg + o);
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (!(u4_get(pv, j) > 0.f)) u4_set(v, j, 0);   // ReLU mask: pooled value > 0
-      }
-      *(u32x4*)(dys + e) = v;
-      *(u32x2*)(args + e) = a;
+    xs.store(tile, tid);
+    ys.store(dys, args, tid);
+    __syncthreads();
+    if constexpr (G::MODE == 0) {
+      make_shifted<G, IMGS>(tile, tid);
+      __syncthreads();
     }
-    fill_tiles<G, IMGS>(tile, x, img0, B, tid);
-    __syncthreads();
+    if (img0 + stride < B) {
+      xs.load(x, img0 + stride, B, tid);
+      ys.load(dP, arg, img0 + stride, B, tid);
+    }
     for (int it = wave; it < IMGS * G::RSTEPS; it += NTH / 64) {
       const int im = it / G::RSTEPS, s = it - im * G::RSTEPS;
       // this lane's two pool windows for the 8 reduction slots
@@ -421,7 +504,7 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_k(const bf16_t* __restrict
         const bool nv = n < G::COUT;
         const int i0 = (im * G::NWIN + w0) * G::COUT + n, i1 = (im * G::NWIN + w1) * G::COUT + n;
         const bf16_t y0 = (nv && v0) ? dys[i0] : (bf16_t)0, y1 = (nv && v1) ? dys[i1] : (bf16_t)0;
-        const int a0 = (nv && v0) ? args[i0] : 0xff, a1 = (nv && v1) ? args[i1] : 0xff;
+        const int a0 = (nv && v0) ? args[i0] : (int)ARG_OFF, a1 = (nv && v1) ? args[i1] : (int)ARG_OFF;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
           bfr[nf][d] = as_bf(a0 == d ? y0 : (bf16_t)0);
@@ -502,8 +585,7 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_k(const bf16_t* __restrict
 template <class G, int IMGS>
 __global__ __launch_bounds__(NTH) void convpool_wgrad_pair_k(const bf16_t* __restrict__ x,
                                                              const bf16_t* __restrict__ dP,
-                                                             const uint8_t* __restrict__ arg,
-                                                             const bf16_t* __restrict__ P, int B,
+                                                             const uint8_t* __restrict__ arg, int B,
                                                              float* __restrict__ slab) {
   static_assert(G::PAIR, "");
   constexpr int CELL = IMGS * G::IMG_LDS;
@@ -532,28 +614,22 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_pair_k(const bf16_t* __res
 #pragma unroll
   for (int mf = 0; mf < G::MFW; ++mf) acc[mf] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += gridDim.x * IMGS) {
+  const int stride = gridDim.x * IMGS;
+  XStage<G, IMGS> xs;
+  DYStage<G, IMGS> ys;
+  xs.load(x, blockIdx.x * IMGS, B, tid);
+  ys.load(dP, arg, blockIdx.x * IMGS, B, tid);
+  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
     __syncthreads();
-    static_assert((IMGS * NWC) % 8 == 0, "");
-    for (int e8 = tid; e8 < IMGS * NWC / 8; e8 += NTH) {
-      const int e = 8 * e8;
-      const int im = e / NWC;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      u32x2 a = {0xffffffffu, 0xffffffffu};
-      if (img0 + im < B) {
-        const int64_t o = (int64_t)img0 * NWC + e;
-        const u32x4 pv = *(const u32x4*)(P + o);
-        v = *(const u32x4*)(dP + o);
-        a = *(const u32x2*)(arg + o);
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (!(u4_get(pv, j) > 0.f)) u4_set(v, j, 0);   // ReLU mask: pooled value > 0
-      }
-      *(u32x4*)(dys + e) = v;
-      *(u32x2*)(args + e) = a;
+    xs.store(tile, tid);
+    ys.store(dys, args, tid);
+    __syncthreads();
+    make_shifted<G, IMGS>(tile, tid);
+    __syncthreads();
+    if (img0 + stride < B) {
+      xs.load(x, img0 + stride, B, tid);
+      ys.load(dP, arg, img0 + stride, B, tid);
     }
-    fill_tiles<G, IMGS>(tile, x, img0, B, tid);
-    __syncthreads();
     for (int it = wave; it < IMGS * RS; it += NTH / 64) {
       const int im = it / RS, s = it - im * RS;
       // dY operand: element j <-> slot 4g + (j&3) + 16(j>>2) = window 16s + 2g + ((j>>1)&1) + 8(j>>2), dy = j&1
@@ -564,7 +640,7 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_pair_k(const bf16_t* __res
         const bool ok = wj < G::NWIN;
         const int i = (im * G::NWIN + wj) * 8 + c;
         const bf16_t y = ok ? dys[i] : (bf16_t)0;
-        const int a = ok ? args[i] : 0xff;
+        const int a = ok ? args[i] : (int)ARG_OFF;
 #pragma unroll
         for (int dy = 0; dy < 2; ++dy) bfr[4 * (jj >> 1) + 2 * (jj & 1) + dy] = as_bf(a == 2 * dy + sx ? y : (bf16_t)0);
       }
@@ -604,115 +680,6 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_pair_k(const bf16_t* __res
   }
 }
 
-// ------------------------------------------------------------------ data gradient (pooled dY -> dX)
-// The unpooled dY image lives in LDS with a KS-1-PAD halo; pixels are DPS = Cout+8
-// elements apart so the 16 pixel rows of a ds_read_b64 fragment fall in distinct banks.
-template <class G, int IMGS>
-__global__ __launch_bounds__(NTH) void convpool_dgrad_k(const bf16_t* __restrict__ dP, const uint8_t* __restrict__ arg,
-                                                        const bf16_t* __restrict__ P, const bf16_t* __restrict__ w,
-                                                        int B, bf16_t* __restrict__ dx) {
-  constexpr int Q = G::KS - 1 - G::PAD;
-  constexpr int OHQ = G::OH + 2 * Q, OWQ = G::OW + 2 * Q;
-  constexpr int DPS = G::COUT + 8;
-  constexpr int DT = OHQ * OWQ * DPS;
-  constexpr int KD = G::KS * G::KS * G::COUT;
-  constexpr int KSD = (KD + 31) / 32;
-  constexpr int NPX = G::H * G::W;
-  constexpr int MFD = (NPX + 15) / 16;
-  constexpr int NFD = (G::CIN + 15) / 16;
-  static_assert(G::COUT % 16 == 0, "dgrad operand reads need Cout % 16 == 0");
-  static_assert((IMGS * DT) % 8 == 0, "");
-  __shared__ __attribute__((aligned(16))) bf16_t dyt[IMGS * DT];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  lds_zero<IMGS * DT>(dyt, tid);
-
-  int dd[KSD][2];
-  bf16x8 bw[KSD][NFD];
-#pragma unroll
-  for (int s = 0; s < KSD; ++s) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int k = 32 * s + 4 * g + 16 * h;  // 4 consecutive co at one flipped tap
-      const int tp = k / G::COUT, co = k - tp * G::COUT;
-      const int kh = tp / G::KS, kw = tp - kh * G::KS;
-      dd[s][h] = k < KD ? (kh * OWQ + kw) * DPS + co : 0;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 32 * s + 4 * g + (j & 3) + 16 * (j >> 2);
-      const int tp = k / G::COUT, co = k - tp * G::COUT;
-      const int tap = G::KS * G::KS - 1 - tp;
-#pragma unroll
-      for (int nf = 0; nf < NFD; ++nf) {
-        const int ci = nf * 16 + li;
-        bw[s][nf][j] = as_bf((k < KD && ci < G::CIN) ? w[(tap * G::CIN + ci) * G::COUT + co] : (bf16_t)0);
-      }
-    }
-  }
-  constexpr int NWC = G::NWIN * G::COUT;
-  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += gridDim.x * IMGS) {
-    __syncthreads();
-    for (int e8 = tid; e8 < IMGS * NWC / 8; e8 += NTH) {
-      const int e = 8 * e8;
-      const int im = e / NWC, rem = e - im * NWC;
-      const int win = rem / G::COUT, co = rem - win * G::COUT;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      u32x2 a = {0xffffffffu, 0xffffffffu};
-      if (img0 + im < B) {
-        const int64_t o = (int64_t)img0 * NWC + e;
-        const u32x4 pv = *(const u32x4*)(P + o);
-        v = *(const u32x4*)(dP + o);
-        a = *(const u32x2*)(arg + o);
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (!(u4_get(pv, j) > 0.f)) u4_set(v, j, 0);
-      }
-      const int ph = win / G::PW, pw = win - ph * G::PW;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const int oh = 2 * ph + (d >> 1) + Q, ow = 2 * pw + (d & 1) + Q;
-        u32x4 o = {0u, 0u, 0u, 0u};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint32_t aj = ((j < 4 ? a[0] : a[1]) >> (8 * (j & 3))) & 0xff;
-          if (aj == (uint32_t)d) u4_set(o, j, (bf16_t)((v[j >> 1] >> (16 * (j & 1))) & 0xffff));
-        }
-        *(u32x4*)(dyt + im * DT + (oh * OWQ + ow) * DPS + co) = o;
-      }
-    }
-    __syncthreads();
-    for (int f = wave; f < IMGS * MFD; f += NTH / 64) {
-      const int im = f / MFD, mf = f - im * MFD;
-      const int m = min(mf * 16 + li, NPX - 1);
-      const int ih = m / G::W, iw = m - ih * G::W;
-      const bf16_t* tb = dyt + im * DT + (ih * OWQ + iw) * DPS;
-      f32x4 acc[NFD];
-#pragma unroll
-      for (int nf = 0; nf < NFD; ++nf) acc[nf] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < KSD; ++s) {
-        const bf16x8 a = join(*(const s16x4*)(tb + dd[s][0]), *(const s16x4*)(tb + dd[s][1]));
-#pragma unroll
-        for (int nf = 0; nf < NFD; ++nf) acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[s][nf], acc[nf], 0, 0, 0);
-      }
-      if (img0 + im < B) {
-#pragma unroll
-        for (int nf = 0; nf < NFD; ++nf) {
-          const int ci = nf * 16 + li;
-          if (ci < G::CIN) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int mm = mf * 16 + 4 * g + r;
-              if (mm < NPX) dx[((int64_t)(img0 + im) * NPX + mm) * G::CIN + ci] = f2bf(acc[nf][r]);
-            }
-          }
-        }
-      }
-    }
-  }
-}
-
 // ------------------------------------------------------------------ data gradient, Cin 8 pair layout
 // Row i of a fragment = input-pixel PAIR (ih = 2*mf + i/8, iw = 2*(i&7)): two
 // image rows of 8 pairs (the 8th pair is padding for a 14-wide image), so with
@@ -721,11 +688,11 @@ __global__ __launch_bounds__(NTH) void convpool_dgrad_k(const bf16_t* __restrict
 // (ci = n&7, side sx = n>>3): the dY patch row spans kw' = 0..KS (one extra tap)
 // and side 1 uses the flipped filter shifted by one kw, i.e. it produces dx at
 // (ih, iw + 1).  K-slot order: lane group g, element j -> tap 2s + g/2, co 8(g&1)+j,
-// so each A fragment is ONE ds_read_b128.
+// so each A fragment is ONE ds_read_b128.  The unpooled dY image lives in LDS
+// with a KS-1-PAD halo.
 template <class G, int IMGS>
 __global__ __launch_bounds__(NTH) void convpool_dgrad_pair_k(const bf16_t* __restrict__ dP,
                                                              const uint8_t* __restrict__ arg,
-                                                             const bf16_t* __restrict__ P,
                                                              const bf16_t* __restrict__ w, int B,
                                                              bf16_t* __restrict__ dx) {
   static_assert(G::CIN == 8 && G::COUT == 16 && G::W % 2 == 0 && G::H % 2 == 0 && G::W <= 16, "pair dgrad layout");
@@ -738,8 +705,9 @@ __global__ __launch_bounds__(NTH) void convpool_dgrad_pair_k(const bf16_t* __res
   constexpr int NTAP = G::KS * KWQ;
   constexpr int KSD = (NTAP + 1) / 2;                 // 2 taps x 16 co per 32-wide k-step
   constexpr int MFD = G::H / 2;                       // 2 image rows per fragment
+  constexpr int NWC = G::NWIN * G::COUT;
   static_assert((IMGS * DT) % 8 == 0, "");
-  static_assert(14 + KWQ - 1 < RSE / DPS, "padding pair's patch row stays inside the row stride");
+  static_assert(2 * 7 + KWQ - 1 < RSE / DPS, "padding pair's patch row stays inside the row stride");
   __shared__ __attribute__((aligned(16))) bf16_t dyt[IMGS * DT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -762,38 +730,34 @@ __global__ __launch_bounds__(NTH) void convpool_dgrad_pair_k(const bf16_t* __res
       bw[s][j] = as_bf(valid ? w[(tap * G::CIN + ci) * G::COUT + co] : (bf16_t)0);
     }
   }
-  constexpr int NWC = G::NWIN * G::COUT;
-  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += gridDim.x * IMGS) {
+  const int stride = gridDim.x * IMGS;
+  DYStage<G, IMGS> ys;
+  ys.load(dP, arg, blockIdx.x * IMGS, B, tid);
+  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
     __syncthreads();
-    for (int e8 = tid; e8 < IMGS * NWC / 8; e8 += NTH) {
-      const int e = 8 * e8;
-      const int im = e / NWC, rem = e - im * NWC;
-      const int win = rem / G::COUT, co = rem - win * G::COUT;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      u32x2 a = {0xffffffffu, 0xffffffffu};
-      if (img0 + im < B) {
-        const int64_t o = (int64_t)img0 * NWC + e;
-        const u32x4 pv = *(const u32x4*)(P + o);
-        v = *(const u32x4*)(dP + o);
-        a = *(const u32x2*)(arg + o);
+    // max-unpool: position d of a window receives dP where arg == d (arg 4: ReLU off)
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (!(u4_get(pv, j) > 0.f)) u4_set(v, j, 0);
-      }
-      const int ph = win / G::PW, pw = win - ph * G::PW;
+    for (int u = 0; u < DYStage<G, IMGS>::PER; ++u) {
+      const int e = 8 * (tid + u * NTH);
+      if (e < IMGS * NWC) {
+        const int im = e / NWC, rem = e - im * NWC;
+        const int win = rem / G::COUT, co = rem - win * G::COUT;
+        const int ph = win / G::PW, pw = win - ph * G::PW;
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const int oh = 2 * ph + (d >> 1) + Q, ow = 2 * pw + (d & 1) + Q;
-        u32x4 o = {0u, 0u, 0u, 0u};
+        for (int d = 0; d < 4; ++d) {
+          const int oh = 2 * ph + (d >> 1) + Q, ow = 2 * pw + (d & 1) + Q;
+          u32x4 o = {0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint32_t aj = ((j < 4 ? a[0] : a[1]) >> (8 * (j & 3))) & 0xff;
-          if (aj == (uint32_t)d) u4_set(o, j, (bf16_t)((v[j >> 1] >> (16 * (j & 1))) & 0xffff));
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t aj = ((j < 4 ? ys.a[u][0] : ys.a[u][1]) >> (8 * (j & 3))) & 0xff;
+            if (aj == (uint32_t)d) u4_set(o, j, (bf16_t)((ys.y[u][j >> 1] >> (16 * (j & 1))) & 0xffff));
+          }
+          *(u32x4*)(dyt + im * DT + oh * RSE + ow * DPS + co) = o;
         }
-        *(u32x4*)(dyt + im * DT + oh * RSE + ow * DPS + co) = o;
       }
     }
     __syncthreads();
+    if (img0 + stride < B) ys.load(dP, arg, img0 + stride, B, tid);
 #pragma unroll 1
     for (int im = 0; im < IMGS; ++im) {
       const bool img_ok = img0 + im < B;
@@ -839,25 +803,20 @@ hipError_t run_fwd(const bf16_t* x, const bf16_t* w, const float* bias, int bias
 }
 
 template <class G, int IMGS>
-hipError_t run_wgrad(const bf16_t* x, const bf16_t* dP, const uint8_t* arg, const bf16_t* P, int B, float* slab,
-                     int grid, hipStream_t st) {
+hipError_t run_wgrad(const bf16_t* x, const bf16_t* dP, const uint8_t* arg, int B, float* slab, int grid,
+                     hipStream_t st) {
   if constexpr (G::PAIR) {
-    hipLaunchKernelGGL((convpool_wgrad_pair_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, P, B, slab);
+    hipLaunchKernelGGL((convpool_wgrad_pair_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab);
   } else {
-    hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, P, B, slab);
+    hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab);
   }
   return hipGetLastError();
 }
 
 template <class G, int IMGS>
-hipError_t run_dgrad(const bf16_t* dP, const uint8_t* arg, const bf16_t* P, const bf16_t* w, int B, bf16_t* dx,
-                     hipStream_t st) {
-  if constexpr (G::CIN == 8 && G::COUT == 16)
-    hipLaunchKernelGGL((convpool_dgrad_pair_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, dP, arg, P,
-                       w, B, dx);
-  else
-    hipLaunchKernelGGL((convpool_dgrad_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, dP, arg, P, w,
-                       B, dx);
+hipError_t run_dgrad(const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int B, bf16_t* dx, hipStream_t st) {
+  hipLaunchKernelGGL((convpool_dgrad_pair_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, dP, arg, w,
+                     B, dx);
   return hipGetLastError();
 }
 
@@ -916,21 +875,23 @@ hipError_t convpool_fwd(int cfg, const bf16_t* x, const bf16_t* w, const float* 
   return hipErrorInvalidValue;
 }
 
-hipError_t convpool_wgrad(int cfg, const bf16_t* x, const bf16_t* dP, const uint8_t* arg, const bf16_t* P, int B,
-                          float* slab, int grid, hipStream_t st) {
+hipError_t convpool_wgrad(int cfg, const bf16_t* x, const bf16_t* dP, const uint8_t* arg, int B, float* slab,
+                          int grid, hipStream_t st) {
   switch (cfg) {
-    case 0: return run_wgrad<LeNetC1, 2>(x, dP, arg, P, B, slab, grid, st);
-    case 1: return run_wgrad<LeNetC2, 4>(x, dP, arg, P, B, slab, grid, st);
-    case 2: return run_wgrad<RefC1g, 2>(x, dP, arg, P, B, slab, grid, st);
-    case 3: return run_wgrad<RefC1c, 2>(x, dP, arg, P, B, slab, grid, st);
+    case 0: return run_wgrad<LeNetC1, 2>(x, dP, arg, B, slab, grid, st);
+    case 1: return run_wgrad<LeNetC2, 4>(x, dP, arg, B, slab, grid, st);
+    case 2: return run_wgrad<RefC1g, 2>(x, dP, arg, B, slab, grid, st);
+    case 3: return run_wgrad<RefC1c, 2>(x, dP, arg, B, slab, grid, st);
   }
   return hipErrorInvalidValue;
 }
 
-hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const bf16_t* P, const bf16_t* w, int B,
-                          bf16_t* dx, hipStream_t st) {
+int convpool_has_dgrad(int cfg) { return cfg == 1 ? 1 : 0; }
+
+hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int B, bf16_t* dx,
+                          hipStream_t st) {
   switch (cfg) {
-    case 1: return run_dgrad<LeNetC2, 2>(dP, arg, P, w, B, dx, st);
+    case 1: return run_dgrad<LeNetC2, 2>(dP, arg, w, B, dx, st);
   }
   return hipErrorInvalidValue;
 }

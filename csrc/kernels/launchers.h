@@ -47,10 +47,12 @@ int convpool_wgrad_rows(int cfg);                                      // KM (sl
 int convpool_reduce_layout(int cfg, int* out);
 hipError_t convpool_fwd(int cfg, const bf16_t* x, const bf16_t* w, const float* bias, int bias_n, int B,
                         bf16_t* pooled, uint8_t* arg, hipStream_t st);
-hipError_t convpool_wgrad(int cfg, const bf16_t* x, const bf16_t* dP, const uint8_t* arg, const bf16_t* P, int B,
-                          float* slab, int grid, hipStream_t st);
-hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const bf16_t* P, const bf16_t* w, int B,
-                          bf16_t* dx, hipStream_t st);
+// backward needs only (dP, arg): arg == 4 marks a window whose ReLU output is 0
+hipError_t convpool_wgrad(int cfg, const bf16_t* x, const bf16_t* dP, const uint8_t* arg, int B, float* slab,
+                          int grid, hipStream_t st);
+int convpool_has_dgrad(int cfg);
+hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int B, bf16_t* dx,
+                          hipStream_t st);
 
 // ---- misc.hip
 hipError_t prep_images(const uint8_t* src, const int64_t* idx, const int32_t* lab_src, int B, int HW, int Csrc,

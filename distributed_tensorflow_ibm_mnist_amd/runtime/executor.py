@@ -111,7 +111,7 @@ class ConvPoolLayer(_Layer):
         self.red = kernels().convpool_reduce_args(*self._geo(), spec.cin)   # (G, Ipad, I, bias_row)
         self.grid = 1024
         self.slab_elems = self.grid * self.KM * self.Cp
-        self.can_dgrad = self.cfg == 1
+        self.can_dgrad = kernels().convpool_has_dgrad(*self._geo())
         if need_dx and not self.can_dgrad:
             raise ValueError(f"{spec.name}: fused dgrad not available for this geometry")
 
@@ -126,12 +126,12 @@ class ConvPoolLayer(_Layer):
         s = self.spec
         K = kernels()
         grid = min(self.grid, max(1, (nb + 3) // 4))
-        K.convpool_wgrad(self.x, dy, self.arg, self.out, slab, grid, nb, *self._geo())
+        K.convpool_wgrad(self.x, dy, self.arg, slab, grid, nb, *self._geo())
         G, Ip, I, brow = self.red
         K.splitk_reduce(slab, grid, self.KM, self.Cp, G, Ip, I, s.cout, brow,
                         self.fp.grad_view(self.wname), self.fp.grad_view(self.bname), 1.0)
         if dx is not None:
-            K.convpool_dgrad(dy, self.arg, self.out, self.fp.bf16_view(self.wname), dx, nb, *self._geo())
+            K.convpool_dgrad(dy, self.arg, self.fp.bf16_view(self.wname), dx, nb, *self._geo())
 
 
 class PoolLayer(_Layer):

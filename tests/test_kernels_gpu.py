@@ -332,14 +332,16 @@ def test_convpool(dev, K, N, H, W, Ci, ci, Co, co, pad):
     KM = K.convpool_rows(Ci, Co, 5, pad, H, W)
     grid = 37
     slab = torch.empty(grid * KM * Co, dtype=torch.float32, device=dev)
-    K.convpool_wgrad(x, dP, arg, pooled, slab, grid, N, Ci, Co, 5, pad, H, W)
+    K.convpool_wgrad(x, dP, arg, slab, grid, N, Ci, Co, 5, pad, H, W)
     dw = torch.empty(5, 5, ci, co, device=dev)
     db = torch.empty(co, device=dev)
     G, Ip, I, brow = K.convpool_reduce_args(Ci, Co, 5, pad, H, W, ci)
     K.splitk_reduce(slab, grid, KM, Co, G, Ip, I, co, brow, dw, db, 1.0)
     close(dw, wr.grad[:, :, :ci, :co], rel=3e-2)
     close(db, br.grad[:co], rel=3e-2)
-    if K.convpool_supported(Ci, Co, 5, pad, H, W) == 1:
+    # the ReLU mask lives in the argmax byte: 4 exactly where the pooled output is 0
+    assert torch.equal(arg == 4, pooled == 0)
+    if K.convpool_has_dgrad(Ci, Co, 5, pad, H, W):
         dx = torch.empty(N, H, W, Ci, dtype=torch.bfloat16, device=dev)
-        K.convpool_dgrad(dP, arg, pooled, w, dx, N, Ci, Co, 5, pad, H, W)
+        K.convpool_dgrad(dP, arg, w, dx, N, Ci, Co, 5, pad, H, W)
         close(dx[..., :ci], xr.grad[..., :ci])

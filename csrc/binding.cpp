@@ -218,9 +218,10 @@ void lrn_bwd(Tensor x, Tensor dy, Tensor dx, int64_t P_, int64_t C, int64_t r, d
 }
 
 void softmax_ce(Tensor logits, int64_t ldl, optional<Tensor> labels, int64_t B, int64_t NC, double scale,
-                optional<Tensor> dlogits, int64_t ldd, optional<Tensor> stats, optional<Tensor> probs) {
+                optional<Tensor> dlogits, int64_t ldd, optional<Tensor> stats, optional<Tensor> probs,
+                optional<Tensor> work) {
   TORCH_CHECK(ldl >= NC, "ldl < NC");
-  check(logits, at::kFloat, span(B, ldl, NC), "logits");
+  check(logits, at::kFloat, B * ldl, "logits");   // whole padded rows (vector loads)
   const int32_t* lab = nullptr;
   if (labels.has_value() && labels->defined()) {
     check(*labels, at::kInt, B, "labels");
@@ -231,6 +232,7 @@ void softmax_ce(Tensor logits, int64_t ldl, optional<Tensor> labels, int64_t B, 
     TORCH_CHECK(lab != nullptr, "dlogits needs labels");
     TORCH_CHECK(ldd >= NC, "ldd < NC");
     check(*dlogits, at::kBFloat16, B * ldd, "dlogits");
+    TORCH_CHECK(ldd == ldl || ldd >= NC, "ldd");
     dl = BFm(*dlogits);
   }
   float* st = nullptr;
@@ -243,8 +245,13 @@ void softmax_ce(Tensor logits, int64_t ldl, optional<Tensor> labels, int64_t B, 
     check(*probs, at::kFloat, B * NC, "probs");
     pr = P<float>(*probs);
   }
+  float* wk = nullptr;
+  if (work.has_value() && work->defined()) {
+    check(*work, at::kFloat, 4 * 1024 + 1, "work");
+    wk = P<float>(*work);
+  }
   hip_ok(mnistx::softmax_ce(P<const float>(logits), (int)ldl, lab, (int)B, (int)NC, (float)scale, dl, (int)ldd, st, pr,
-                            cur_stream()),
+                            wk, cur_stream()),
          "softmax_ce");
 }
 
@@ -457,7 +464,9 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("lrn_fwd", &lrn_fwd);
   m.def("lrn_bwd", &lrn_bwd);
-  m.def("softmax_ce", &softmax_ce);
+  m.def("softmax_ce", &softmax_ce, py::arg("logits"), py::arg("ldl"), py::arg("labels"), py::arg("B"), py::arg("NC"),
+        py::arg("scale"), py::arg("dlogits"), py::arg("ldd"), py::arg("stats"), py::arg("probs"),
+        py::arg("work") = py::none());
   m.def("splitk_reduce", &splitk_reduce);
   m.def("fused_optimizer", &fused_optimizer);
   m.def("finalize_step", &finalize_step);

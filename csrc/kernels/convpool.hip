@@ -327,8 +327,11 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_k(const bf16_t* __restrict__
           if (n < G::COUT) {
             // relu(. + b) is monotone: pool the raw sums, then bias + ReLU once
             const f32x4 v = acc[nf];
-            const float m = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
-            const int bi = v[0] == m ? 0 : (v[1] == m ? 1 : (v[2] == m ? 2 : 3));
+            const bool t01 = v[1] > v[0], t23 = v[3] > v[2];
+            const float m01 = t01 ? v[1] : v[0], m23 = t23 ? v[3] : v[2];
+            const bool hi = m23 > m01;
+            const float m = hi ? m23 : m01;
+            const int bi = hi ? (t23 ? 3 : 2) : (t01 ? 1 : 0);
             const float o = m + bs[nf];
             pimg[win * G::COUT + n] = f2bf(fmaxf(o, 0.f));
             aimg[win * G::COUT + n] = (uint8_t)(o > 0.f ? bi : ARG_OFF);
@@ -359,10 +362,12 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_pair_k(const bf16_t* __restr
   constexpr int LDS = (IMGS * G::IMG_LDS + 7) / 8 * 8;
   constexpr int MFP = (G::NWIN + 7) / 8;  // fragments per image (8 windows each)
   __shared__ __attribute__((aligned(16))) bf16_t tile[LDS];
+  __shared__ int wtab[G::NWIN];            // window -> aligned LDS offset of its top-left pixel
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int c = li & 7, sx = li >> 3;
   lds_zero<LDS>(tile, tid);
+  for (int w = tid; w < G::NWIN; w += NTH) wtab[w] = G::aligned_off(G::wbase(w));
 
   int dd[G::KSTEPS][2];
   bf16x8 bfr[G::KSTEPS];
@@ -400,8 +405,8 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_pair_k(const bf16_t* __restr
       bf16_t* pimg = pooled + (int64_t)(img0 + im) * (G::NWIN * 8);
       uint8_t* aimg = arg + (int64_t)(img0 + im) * (G::NWIN * 8);
       for (int fm = wave; fm < MFP; fm += NTH / 64) {
-        const int wa = min(fm * 8 + (li >> 1), G::NWIN - 1);
-        const bf16_t* tb = timg + G::aligned_off(G::wbase(wa) + (li & 1) * G::WS);
+        // dy = li&1 adds WS (a multiple of 4): same shifted copy as the window base
+        const bf16_t* tb = timg + wtab[min(fm * 8 + (li >> 1), G::NWIN - 1)] + (li & 1) * G::WS;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < G::KSTEPS; ++s) {
@@ -409,8 +414,10 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_pair_k(const bf16_t* __restr
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[s], acc, 0, 0, 0);
         }
         // rows 4g+r: r=0,1 -> window 2g (dy 0,1); r=2,3 -> window 2g+1
-        const float m0 = fmaxf(acc[0], acc[1]), m1 = fmaxf(acc[2], acc[3]);
-        const int d0 = acc[1] > acc[0] ? 2 : 0, d1 = acc[3] > acc[2] ? 2 : 0;
+        // one compare per pair feeds both the max and the argmax (no NaN-canonicalising fmaxf)
+        const bool t0 = acc[1] > acc[0], t1 = acc[3] > acc[2];
+        const float m0 = t0 ? acc[1] : acc[0], m1 = t1 ? acc[3] : acc[2];
+        const int d0 = t0 ? 2 : 0, d1 = t1 ? 2 : 0;
         // side 0 owns window 2g, side 1 owns window 2g+1: trade the other window's column max
         const float oth = swap_half_row(sx ? m0 : m1);
         const int doth = swap_half_row(sx ? d0 : d1);
@@ -596,10 +603,12 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_pair_k(const bf16_t* __res
   __shared__ __attribute__((aligned(16))) bf16_t dys[IMGS * NWC];
   __shared__ __attribute__((aligned(16))) uint8_t args[IMGS * NWC];
   __shared__ float red[G::KM * 16];
+  __shared__ int wtab[G::NWIN];            // window -> aligned LDS offset of its top-left pixel
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int c = li & 7, sx = li >> 3;
   lds_zero<LDS>(tile, tid);
+  for (int w = tid; w < G::NWIN; w += NTH) wtab[w] = G::aligned_off(G::wbase(w));
   __syncthreads();
   if (tid == 0) tile[CELL] = (bf16_t)0x3f80;
 
@@ -645,15 +654,16 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_pair_k(const bf16_t* __res
         for (int dy = 0; dy < 2; ++dy) bfr[4 * (jj >> 1) + 2 * (jj & 1) + dy] = as_bf(a == 2 * dy + sx ? y : (bf16_t)0);
       }
       // im2col^T operand rows supplied by this lane: slot 4g+q (+16): window 16s + 2g + q/2 (+8), dy = q&1
+      // (dy adds WS and the chunk deltas are multiples of 4: the copy is the window's)
       const int wq = 16 * s + 2 * g + (q >> 1);
-      const int pb0 = G::wbase(min(wq, G::NWIN - 1)) + (q & 1) * G::WS;
-      const int pb1 = G::wbase(min(wq + 8, G::NWIN - 1)) + (q & 1) * G::WS;
+      const int pb0 = im * G::IMG_LDS + wtab[min(wq, G::NWIN - 1)] + (q & 1) * G::WS;
+      const int pb1 = im * G::IMG_LDS + wtab[min(wq + 8, G::NWIN - 1)] + (q & 1) * G::WS;
 #pragma unroll
       for (int mf = 0; mf < G::MFW; ++mf) {
         const int cc = cd[mf];
         const int cell = CELL + (cc == -1 ? 0 : 4);
-        const int o0 = cc >= 0 ? im * G::IMG_LDS + G::aligned_off(pb0 + cc) : cell;
-        const int o1 = cc >= 0 ? im * G::IMG_LDS + G::aligned_off(pb1 + cc) : cell;
+        const int o0 = cc >= 0 ? pb0 + cc : cell;
+        const int o1 = cc >= 0 ? pb1 + cc : cell;
         const bf16x8 a = join(lds_tr4(tile + o0), lds_tr4(tile + o1));
         acc[mf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr, acc[mf], 0, 0, 0);
       }

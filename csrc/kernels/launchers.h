@@ -65,8 +65,10 @@ hipError_t lrn_fwd(const bf16_t* x, int P, int C, int r, float bias, float alpha
                    hipStream_t st);
 hipError_t lrn_bwd(const bf16_t* x, const bf16_t* dy, int P, int C, int r, float bias, float alpha, float beta,
                    int relu_mask, bf16_t* dx, hipStream_t st);
+// work (optional): >= 4*1024+1 floats, zero-initialised once; makes the loss /
+// accuracy sums deterministic (per-block partials combined in block order)
 hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B, int NC, float scale,
-                      bf16_t* dlogits, int ldd, float* stats, float* probs, hipStream_t st);
+                      bf16_t* dlogits, int ldd, float* stats, float* probs, float* work, hipStream_t st);
 // NOTE: many splits over a small output are pre-summed IN PLACE (the slab is scratch).
 hipError_t splitk_reduce(float* slab, int splits, int M, int N, int G, int Ipad, int I, int J,
                          int bias_row, float* wdst, float* bdst, float scale, hipStream_t st);

@@ -8,6 +8,8 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <algorithm>
+
 namespace mnistx {
 namespace {
 
@@ -291,6 +293,123 @@ __global__ void softmax_ce_k(const float* __restrict__ logits, int ldl, const in
   }
 }
 
+// Row-vectorized variant for padded logit rows of LD = 16 / 32 floats (the
+// classifier output is padded to >= 16 columns): one thread per row, f32x4 loads,
+// 16-byte bf16 stores.  Statistics: warp + block reduction, then either one
+// atomic per block or -- with a workspace -- per-block partials combined by the
+// last block to finish (ticket counter) in block order: bitwise deterministic.
+constexpr int CE_MAXB = 1024;
+template <int LD>
+__global__ __launch_bounds__(256) void softmax_ce_rows_k(const float* __restrict__ logits,
+                                                         const int32_t* __restrict__ labels, int B, int NC,
+                                                         float scale, bf16_t* __restrict__ dl,
+                                                         float* __restrict__ stats, float* __restrict__ probs,
+                                                         float* __restrict__ work) {
+  __shared__ float red[3][4];
+  __shared__ int last;
+  float loss = 0.f, corr = 0.f, bad = 0.f;
+  for (int row = blockIdx.x * 256 + threadIdx.x; row < B; row += gridDim.x * 256) {
+    float l[LD];
+#pragma unroll
+    for (int v = 0; v < LD / 4; ++v) {
+      const f32x4 t = *(const f32x4*)(logits + (int64_t)row * LD + 4 * v);
+      l[4 * v] = t[0];
+      l[4 * v + 1] = t[1];
+      l[4 * v + 2] = t[2];
+      l[4 * v + 3] = t[3];
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < LD; ++c)
+      if (c < NC) mx = fmaxf(mx, l[c]);
+    float e[LD], se = 0.f;
+#pragma unroll
+    for (int c = 0; c < LD; ++c) {
+      e[c] = c < NC ? __expf(l[c] - mx) : 0.f;
+      se += e[c];
+    }
+    const float inv = 1.f / se;
+    const int lab = labels ? labels[row] : -1;
+    if (labels) {
+      float ll = 0.f;
+#pragma unroll
+      for (int c = 0; c < LD; ++c) ll = (c == lab) ? l[c] : ll;
+      const float lo = -(ll - mx - __logf(se));
+      loss += lo;
+      corr += (ll >= mx) ? 1.f : 0.f;
+      if (!isfinite(lo)) bad = 1.f;
+    }
+    if (dl) {
+#pragma unroll
+      for (int v = 0; v < LD / 8; ++v) {
+        u32x4 o;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const int c0 = 8 * v + 2 * h;
+          const float g0 = (e[c0] * inv - (c0 == lab ? 1.f : 0.f)) * scale;
+          const float g1 = (e[c0 + 1] * inv - (c0 + 1 == lab ? 1.f : 0.f)) * scale;
+          o[h] = pack2(c0 < NC ? g0 : 0.f, c0 + 1 < NC ? g1 : 0.f);
+        }
+        *(u32x4*)(dl + (int64_t)row * LD + 8 * v) = o;
+      }
+    }
+    if (probs)
+#pragma unroll
+      for (int c = 0; c < LD; ++c)
+        if (c < NC) probs[(int64_t)row * NC + c] = e[c] * inv;
+  }
+  if (!stats) return;
+  loss = warp_sum(loss);
+  corr = warp_sum(corr);
+  bad = warp_sum(bad);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wave] = loss;
+    red[1][wave] = corr;
+    red[2][wave] = bad;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    loss = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+    corr = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+    bad = red[2][0] + red[2][1] + red[2][2] + red[2][3];
+    if (!work) {
+      atomicAdd(&stats[0], loss);
+      atomicAdd(&stats[1], corr);
+      if (bad > 0.f) stats[2] = 1.f;
+    } else {
+      work[4 * blockIdx.x] = loss;
+      work[4 * blockIdx.x + 1] = corr;
+      work[4 * blockIdx.x + 2] = bad;
+      __threadfence();
+      unsigned* ticket = (unsigned*)(work + 4 * CE_MAXB);
+      last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+  }
+  if (!work) return;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  // last block: combine the partials in block order (64 lanes of wave 0, fixed tree)
+  if (wave != 0) return;
+  const volatile float* wv = work;
+  float a = 0.f, b = 0.f, c = 0.f;
+  for (int i = lane; i < (int)gridDim.x; i += 64) {
+    a += wv[4 * i];
+    b += wv[4 * i + 1];
+    c += wv[4 * i + 2];
+  }
+  a = warp_sum(a);
+  b = warp_sum(b);
+  c = warp_sum(c);
+  if (lane == 0) {
+    stats[0] += a;
+    stats[1] += b;
+    if (c > 0.f) stats[2] = 1.f;
+    *(unsigned*)(work + 4 * CE_MAXB) = 0u;
+  }
+}
+
 // ------------------------------------------------------------------ split-K reduce
 // dst weights [G][I][J] <- sum_s slab[s][g*Ipad + i][j] ; bias[j] <- sum_s slab[s][bias_row][j]
 // Fixed summation order (deterministic).  Few slabs: one thread per output;
@@ -547,7 +666,19 @@ hipError_t lrn_bwd(const bf16_t* x, const bf16_t* dy, int P, int C, int r, float
 }
 
 hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B, int NC, float scale,
-                      bf16_t* dlogits, int ldd, float* stats, float* probs, hipStream_t st) {
+                      bf16_t* dlogits, int ldd, float* stats, float* probs, float* work, hipStream_t st) {
+  const int nb = (int)std::min<int64_t>(CE_MAXB, ((int64_t)B + 255) / 256);
+  const bool rows_ok = (ldl == 16 || ldl == 32) && NC <= ldl && (!dlogits || ldd == ldl) &&
+                       ((uintptr_t)logits % 16 == 0) && (!dlogits || (uintptr_t)dlogits % 16 == 0);
+  if (rows_ok && B > 0) {
+    if (ldl == 16)
+      hipLaunchKernelGGL(softmax_ce_rows_k<16>, dim3(nb), dim3(256), 0, st, logits, labels, B, NC, scale, dlogits,
+                         stats, probs, work);
+    else
+      hipLaunchKernelGGL(softmax_ce_rows_k<32>, dim3(nb), dim3(256), 0, st, logits, labels, B, NC, scale, dlogits,
+                         stats, probs, work);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(softmax_ce_k, dim3((B + TPB - 1) / TPB), dim3(TPB), 0, st, logits, ldl, labels, B, NC, scale,
                      dlogits, ldd, stats, probs);
   return hipGetLastError();

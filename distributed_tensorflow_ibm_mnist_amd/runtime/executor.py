@@ -295,6 +295,8 @@ class HipNet:
         self.slab = torch.zeros(max(slab, 1), dtype=torch.float32, device=dev)
         self.stats = torch.zeros(8, dtype=torch.float32, device=dev)
         self.eval_stats = torch.zeros(8, dtype=torch.float32, device=dev)
+        # softmax-CE per-block partials + ticket: deterministic loss / accuracy sums
+        self.ce_work = torch.zeros(4 * 1024 + 1, dtype=torch.float32, device=dev)
         names = [e.name for e in self.fp.wd_entries]
         self.loss_names = [n.replace("/weights", "/weight_loss") for n in names] + ["cross_entropy", "total_loss"]
         self.loss_ema = torch.zeros(3 * len(self.loss_names), dtype=torch.float32, device=dev)
@@ -311,7 +313,7 @@ class HipNet:
         nb = self.B if nb is None else nb
         kernels().softmax_ce(self.logits, self.logits.shape[1], self.labels, nb, self.n_classes,
                              (1.0 / nb) if scale is None else scale, self.dlogits, self.logits.shape[1], self.stats,
-                             None)
+                             None, self.ce_work)
 
     def backward(self, nb: Optional[int] = None) -> None:
         nb = self.B if nb is None else nb
@@ -353,7 +355,7 @@ class HipNet:
         self.forward(nb)
         st = self.eval_stats if stats is None else stats
         kernels().softmax_ce(self.logits, self.logits.shape[1], self.labels, nb, self.n_classes, 1.0, None,
-                             self.logits.shape[1], st, None)
+                             self.logits.shape[1], st, None, self.ce_work)
         return st
 
     def probs(self, nb: int) -> torch.Tensor:

@@ -1,10 +1,15 @@
 """Synthetic MNIST-shaped data (no network in this environment: SURVEY.md §4).
 
-``synthetic://N[?seed=S&noise=F]`` yields N 28×28 uint8 images with labels 0-9.
-Each class has a fixed random "stroke" template (a smooth blob path, like a
-pen-drawn glyph); every sample is its class template shifted by up to ±2 px,
-intensity-jittered, with additive noise.  The task is learnable (so
-steps-to-99%-train-accuracy is meaningful) but not trivially separable at init.
+``synthetic://N[?seed=S&noise=F&style=glyph|hand]`` yields N 28×28 uint8 images
+with labels 0-9.  Each class has a fixed random "stroke" template (a smooth path
+of 6 control points, like a pen-drawn glyph).
+
+* ``glyph`` (default): every sample is its class template shifted by up to
+  ±2 px, intensity-jittered, with additive noise -- fast, and easy.
+* ``hand``: every sample re-draws its class path from control points jittered
+  per sample (σ 1.6 px), rotated (±15°), scaled (0.85-1.15), with a random pen
+  width and shift -- intra-class variability like handwriting, so
+  steps-to-99%-train-accuracy (BASELINE.json) measures real learning.
 
 Generation is vectorised torch (CPU or GPU) and deterministic in the seed.
 """
@@ -37,10 +42,53 @@ def _templates(seed: int, classes: int = 10, size: int = 28) -> torch.Tensor:
     return out
 
 
+def _control_points(seed: int = 0, classes: int = 10) -> torch.Tensor:
+    g = torch.Generator().manual_seed(1000 + seed)
+    return torch.stack([4 + torch.rand(6, 2, generator=g) * 20 for _ in range(classes)])  # [10, 6, 2]
+
+
+def _hand(labels: torch.Tensor, g: torch.Generator, dev: torch.device, chunk: int = 1024) -> torch.Tensor:
+    n = labels.numel()
+    cp = _control_points().to(dev)[labels]                                       # [n, 6, 2]
+    cp = cp + 1.6 * torch.randn(cp.shape, generator=g, device=dev)
+    ang = (torch.rand(n, generator=g, device=dev) - 0.5) * (torch.pi / 6)
+    sc = 0.85 + 0.3 * torch.rand(n, generator=g, device=dev)
+    c, s_ = torch.cos(ang) * sc, torch.sin(ang) * sc
+    ctr = cp - 14.0
+    cp = torch.stack([c[:, None] * ctr[..., 0] - s_[:, None] * ctr[..., 1],
+                      s_[:, None] * ctr[..., 0] + c[:, None] * ctr[..., 1]], -1) + 14.0
+    cp = cp + (torch.rand(n, 1, 2, generator=g, device=dev) - 0.5) * 4.0        # shift ±2 px
+    width = 0.9 + 0.9 * torch.rand(n, generator=g, device=dev)
+    t = torch.linspace(0, 1, 12, device=dev)
+    path = (cp[:, :-1, None] * (1 - t[None, None, :, None]) + cp[:, 1:, None] * t[None, None, :, None])
+    path = path.reshape(n, -1, 2)                                                # [n, 60, 2]
+    ar = torch.arange(28, dtype=torch.float32, device=dev)
+    out = torch.empty(n, 28, 28, device=dev)
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        py, px = path[a:b, :, 0], path[a:b, :, 1]
+        d2 = (ar[None, None, :, None] - py[:, :, None, None]) ** 2 + (ar[None, None, None, :] - px[:, :, None, None]) ** 2
+        img = torch.exp(-d2.amin(1) / (2 * width[a:b, None, None] ** 2))
+        out[a:b] = img / img.amax((1, 2), keepdim=True).clamp_min(1e-6)
+    return out
+
+
 def make_synthetic(n: int, seed: int = 0, channels: int = 1, noise: float = 0.25,
-                   device: str | torch.device = "cpu") -> Tuple[torch.Tensor, torch.Tensor]:
+                   device: str | torch.device = "cpu", style: str = "glyph") -> Tuple[torch.Tensor, torch.Tensor]:
     """Returns (images uint8 [n, 28*28*channels] HWC-flattened, labels int32 [n])."""
     dev = torch.device(device)
+    if style == "hand":
+        g = torch.Generator(device=dev).manual_seed(seed)
+        labels = torch.randint(0, 10, (n,), generator=g, device=dev)
+        imgs = _hand(labels, g, dev)
+        scale = 0.6 + 0.4 * torch.rand(n, 1, 1, generator=g, device=dev)
+        imgs = imgs * scale + noise * torch.rand(n, 28, 28, generator=g, device=dev)
+        u8 = (imgs.clamp(0, 1) * 255).round().to(torch.uint8)
+        if channels > 1:
+            u8 = u8[..., None].expand(n, 28, 28, channels)
+        return u8.reshape(n, -1).contiguous(), labels.to(torch.int32)
+    if style != "glyph":
+        raise ValueError(f"unknown synthetic style {style!r}")
     tmpl = _templates(0).to(dev)  # class templates are shared by every split (train/test/val)
     g = torch.Generator(device=dev).manual_seed(seed)
     labels = torch.randint(0, 10, (n,), generator=g, device=dev)
@@ -72,6 +120,8 @@ def parse_uri(uri: str) -> Tuple[int, dict]:
         opts["seed"] = int(q["seed"])
     if "noise" in q:
         opts["noise"] = float(q["noise"])
+    if "style" in q:
+        opts["style"] = q["style"]
     return n, opts
 
 

@@ -29,6 +29,8 @@ slice, then (STATE) EMA and momentum slices.
 from __future__ import annotations
 
 import os
+import signal
+import sys
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -95,6 +97,9 @@ class ParameterServer:
         self.opt = opt
         self.max_steps = max_steps
         self.log = log
+        # T6 fault injection: MNIST_FI_KILL_RANK_AT_STEP=r:k SIGKILLs this PS (rank r) at global step k
+        kr = os.environ.get("MNIST_FI_KILL_RANK_AT_STEP", "")
+        self._kill = tuple(int(v) for v in kr.split(":")) if ":" in kr else (-1, -1)
         self.global_step = 0
         if restore is not None:
             from ..train.replica import load_state  # noqa: F401  (names match)
@@ -153,6 +158,10 @@ class ParameterServer:
             if self.j == 0:
                 self.global_step += 1
                 self.fp.step.fill_(self.global_step)
+            if self._kill[0] == dist.get_rank() and self.global_step >= self._kill[1]:
+                self.log(f"[ps {self.j}] fault injection: SIGKILL at global step {self.global_step}")
+                sys.stdout.flush()
+                os.kill(os.getpid(), signal.SIGKILL)
         self._reply(r, want_state=ctrl[1] > 0)
         return True
 

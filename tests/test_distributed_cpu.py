@@ -151,3 +151,51 @@ def test_ps_mode_cli(tmp_path, num_ps, num_workers):
     assert n == num_ps                                              # one data shard per PS
     t = Saver.restore(prefix)
     assert int(t["global_step"]) == 40 and "hidden/weights/Momentum" in t
+
+
+def test_ps_kill_fails_workers_then_resume(tmp_path):
+    """T6: the PS is SIGKILLed mid-run -> every worker exits non-zero (no hang);
+    a restarted cluster resumes from the last checkpoint and finishes."""
+    d = str(tmp_path / "train")
+
+    def launch(tag, env_extra):
+        base = free_port()
+        ps_hosts = f"localhost:{base}"
+        wk_hosts = ",".join(f"localhost:{base + 100 + i}" for i in range(2))
+        common = ["--impl=torch", "--cpu", "--model=mlp", "--in_channels=1", "--batch_size=32", "--max_steps=40",
+                  "--test_interval=100", "--log_step_count_steps=0", "--train_data=synthetic://1500",
+                  "--test_data=synthetic://300?seed=1", f"--train_dir={d}", f"--ps_hosts={ps_hosts}",
+                  f"--worker_hosts={wk_hosts}", "--save_checkpoint_steps=5", "--collective_timeout=120"]
+        env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONUNBUFFERED="1", **env_extra)
+        procs = []
+        for job, i in [("ps", 0), ("worker", 0), ("worker", 1)]:
+            log = tmp_path / f"{tag}_{job}{i}.log"
+            procs.append((f"{job}{i}", log, subprocess.Popen(
+                [sys.executable, os.path.join(ROOT, "main.py")] + common + [f"--job_name={job}", f"--task_id={i}"],
+                cwd=ROOT, env=env, stdout=open(log, "w"), stderr=subprocess.STDOUT)))
+        t0 = time.time()
+        for name, log, p in procs:
+            try:
+                p.wait(timeout=max(5, 240 - (time.time() - t0)))
+            except subprocess.TimeoutExpired:
+                for _, _, q in procs:
+                    q.kill()
+                pytest.fail(f"{tag} {name} hung:\n" + open(log).read()[-3000:])
+        return {name: (p.returncode, open(log).read()) for name, log, p in procs}
+
+    r1 = launch("kill", {"MNIST_FI_KILL_RANK_AT_STEP": "0:17"})
+    assert r1["ps0"][0] == -9, r1["ps0"][1][-2000:]
+    assert "fault injection: SIGKILL" in r1["ps0"][1]
+    for w in ("worker0", "worker1"):
+        assert r1[w][0] != 0, r1[w][1][-2000:]
+    from distributed_tensorflow_ibm_mnist_amd.ckpt.saver import latest_checkpoint
+    lc = latest_checkpoint(d)
+    assert lc is not None and 5 <= int(lc.rsplit("-", 1)[1]) <= 17     # async: saves at the first step >= 5k
+    r2 = launch("resume", {})
+    for name, (rc, out) in r2.items():
+        assert rc == 0, (name, out[-2000:])
+    assert "restored shard from" in r2["ps0"][1] and os.path.basename(lc) in r2["ps0"][1]   # the PS owns the state
+    res = [l for l in r2["worker0"][1].splitlines() if l.startswith("result:")][-1]
+    assert "global_step=40" in res
+    # continues from the checkpoint, not from scratch: exactly the missing updates are applied
+    assert f"applied {40 - int(lc.rsplit('-', 1)[1])} update(s)" in r2["ps0"][1]

@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--dataset_size", type=int, default=60000)
+    ap.add_argument("--phases", type=int, default=3,
+                    help="extra eager steps AFTER the timed region, timed per phase with HIP events (0 = off)")
     return ap.parse_args()
 
 
@@ -122,6 +124,14 @@ def main() -> int:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     el = float(elapsed.item())
     stats = net.read_stats()
+    phases = None
+    if args.phases > 0:                     # outside the timed region: per-phase breakdown of an eager step
+        from distributed_tensorflow_ibm_mnist_amd.runtime.timers import PhaseTimer
+        timer = PhaseTimer(dev)
+        for _ in range(args.phases):
+            loader.next()
+            dp.train_step(timer)
+        phases = timer.summary()
     global_batch = args.batch * world
     ms = el / max(args.steps, 1) * 1e3
     value = global_batch * args.steps / el
@@ -153,6 +163,8 @@ def main() -> int:
             },
             "tflops_per_s": round(tot * value / 1e12, 2),
             "final_train_loss": round(stats["cross_entropy"], 5),
+            "phase_ms_eager": phases,
+            "grad_bucket_mb": [round(b.nbytes / 2 ** 20, 3) for b in dp.buckets] if world > 1 else None,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

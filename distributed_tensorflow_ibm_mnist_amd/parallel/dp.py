@@ -99,13 +99,28 @@ class DataParallel:
             w.wait()
         self.pending.clear()
 
-    def train_step(self) -> None:
+    def train_step(self, timer=None) -> None:
+        """One DP step; ``timer`` (runtime/timers.PhaseTimer) records phase boundaries."""
         net = self.net
+        if timer is None:
+            net.forward()
+            net.loss_and_grad()
+            net.backward()
+            self.sync_grads()
+            net.update(grad_scale=1.0 / self.world)
+            return
+        timer.mark("start")
         net.forward()
+        timer.mark("forward")
         net.loss_and_grad()
+        timer.mark("loss")
         net.backward()
+        timer.mark("backward")
         self.sync_grads()
+        timer.mark("allreduce_wait")
         net.update(grad_scale=1.0 / self.world)
+        timer.mark("update")
+        timer.close()
 
     def broadcast_state(self, src: int = 0) -> None:
         """Make every replica start from the chief's parameters / slots / step."""

@@ -34,3 +34,20 @@ def test_steps_to_accuracy_cli():
     assert r["unit"] == "steps" and r["higher_is_better"] is False
     assert r["value"] is not None and r["value"] % 25 == 0 and r["final_probe_accuracy"] >= 0.95
     assert r["images_seen"] == r["value"] * 64
+
+
+def test_phase_timer_dp_step():
+    from distributed_tensorflow_ibm_mnist_amd.models import get_model, torch_ref
+    from distributed_tensorflow_ibm_mnist_amd.parallel.dp import DataParallel
+    from distributed_tensorflow_ibm_mnist_amd.runtime.params import OptConfig
+    from distributed_tensorflow_ibm_mnist_amd.runtime.timers import PhaseTimer
+    from distributed_tensorflow_ibm_mnist_amd.runtime.torchnet import TorchNet
+    spec = get_model("mlp", 1)
+    net = TorchNet(spec, 16, "cpu", torch_ref.init_params(spec), OptConfig())
+    dp = DataParallel(net)
+    t = PhaseTimer("cpu")
+    for _ in range(3):
+        dp.train_step(t)
+    s = t.summary()
+    assert list(s) == ["forward", "loss", "backward", "allreduce_wait", "update"] and t.steps == 3
+    assert all(v >= 0 for v in s.values()) and int(net.fp.step.item()) == 3

@@ -10,12 +10,16 @@
 // without materialising im2col or transposes in HBM.
 //
 // LDS images keep the operand in its *memory* orientation:
-//   K-contiguous image  [rows = m|n][BK]   -> fragment by 2 x ds_read_b64
+//   K-contiguous image  [rows = m|n][48]   -> fragment by ONE ds_read_b128
 //   MN-contiguous image [BK][cols = m|n]   -> fragment by 2 x ds_read_b64_tr_b16
 // The fragment k-slot order is permuted identically for A and B
 // (lane group g, element j -> k = 4g + (j&3) + 16(j>>2)), which makes the
 // transposed reads bank-conflict-free with an odd-multiple-of-32B row stride
 // (a plain 8g+j order puts rows r and r+8 of one 32-lane half on the same banks).
+// K-contiguous images are stored in that permuted order (column c' = 8g + j), so a
+// lane's 8 k-slots are 16 contiguous bytes; the staging store splits each 16-byte
+// global vector into two 8-byte halves.  Row stride 48 elements (6 x 16 B): every
+// ds_read_b128 lane group hits 16 distinct 16-byte bank groups (bench/lds_sim.py).
 //
 // Staging: register double-buffered (global -> VGPR for tile t+1 while the MFMAs
 // of tile t run from LDS), one barrier per K step; split-K over blockIdx.y for
@@ -27,16 +31,24 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <type_traits>
+
 namespace mnistx {
 namespace {
 
 constexpr int BK = 32;
 
 // Row stride (elements) of an LDS image whose contiguous extent is COLS.
-template <int COLS, bool KC>
+template <int COLS, bool KC, bool PAD48 = true>
 struct ImgStride {
-  static constexpr int value = KC ? (COLS + 8) : (((COLS / 16) % 2 == 0) ? COLS + 16 : COLS);
+  static_assert(!KC || COLS == 32, "K-contiguous images assume BK = 32");
+  // K-contiguous: 48 = conflict-free ds_read_b128.  Implicit-im2col tiles are bound
+  // by their loader's index math and need the occupancy more: 40 (2-way reads).
+  static constexpr int value = KC ? (PAD48 ? 48 : 40) : (((COLS / 16) % 2 == 0) ? COLS + 16 : COLS);
 };
+
+// permuted column of k (0 <= k < 32) inside a K-contiguous image row
+constexpr int kc_col(int k) { return 8 * ((k & 15) >> 2) + (k & 3) + 4 * (k >> 4); }
 
 // ---------------------------------------------------------------- loaders
 // load(r, c): 8 bf16 at memory coordinates (row r, cols c..c+7); zero outside.
@@ -165,14 +177,13 @@ struct WFlipK {
 
 // ---------------------------------------------------------------- fragment reads
 
-// K-contiguous image [rows][S]: lane i=l&15 row r0+i, k = kb + 4g + {0..3} and +16.
+// K-contiguous image [rows][S] in permuted column order: lane i=l&15 row r0+i,
+// k-slots 4g..4g+3 and 16+4g..16+4g+3 = columns 8g..8g+7 (one 16-byte read).
 template <int S>
 DEV bf16x8 frag_kc(const bf16_t* img, int r0, int kb, int lane) {
   const int i = lane & 15, g = lane >> 4;
-  const bf16_t* p = img + (r0 + i) * S + kb + 4 * g;
-  s16x4 lo = *(const s16x4*)p;
-  s16x4 hi = *(const s16x4*)(p + 16);
-  return join(lo, hi);
+  (void)kb;
+  return __builtin_bit_cast(bf16x8, *(const u32x4*)(img + (r0 + i) * S + 8 * g));
 }
 
 // MN-contiguous image [BK][S]: transposed read of 4-row x 16-col blocks.
@@ -194,8 +205,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEp
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   static_assert(FM >= 1 && FN >= 1, "wave tile too small");
-  constexpr int SA = ImgStride<AKC ? BK : BM, AKC>::value;
-  constexpr int SB = ImgStride<BKC ? BK : BN, BKC>::value;
+  constexpr bool DENSE = std::is_same<LA, MatLoader>::value && std::is_same<LB, MatLoader>::value;
+  constexpr int SA = ImgStride<AKC ? BK : BM, AKC, DENSE>::value;
+  constexpr int SB = ImgStride<BKC ? BK : BN, BKC, DENSE>::value;
   constexpr int A_ELEMS = AKC ? BM * SA : BK * SA;
   constexpr int B_ELEMS = BKC ? BN * SB : BK * SB;
   constexpr int A_VEC = BM * BK / 8, B_VEC = BN * BK / 8;
@@ -250,25 +262,28 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEp
       }
     }
   };
+  // K-contiguous: the 8 k of a vector land in two 4-column runs of the permuted order
+  auto kc_store = [&](bf16_t* img, int S, int v, const u32x4& x) {
+    const int r = v / (BK / 8), vq = v % (BK / 8);
+    bf16_t* row = img + r * S;
+    *(u32x2*)(row + kc_col(8 * vq)) = u32x2{x[0], x[1]};
+    *(u32x2*)(row + kc_col(8 * vq + 4)) = u32x2{x[2], x[3]};
+  };
   auto sstore = [&](int buf) {
 #pragma unroll
     for (int u = 0; u < A_VPT; ++u) {
       const int v = tid + u * NT;
       if (v < A_VEC) {
-        int off;
-        if (AKC) off = (v / (BK / 8)) * SA + (v % (BK / 8)) * 8;
-        else off = (v / (BM / 8)) * SA + (v % (BM / 8)) * 8;
-        *(u32x4*)(As(buf) + off) = ra[u];
+        if (AKC) kc_store(As(buf), SA, v, ra[u]);
+        else *(u32x4*)(As(buf) + (v / (BM / 8)) * SA + (v % (BM / 8)) * 8) = ra[u];
       }
     }
 #pragma unroll
     for (int u = 0; u < B_VPT; ++u) {
       const int v = tid + u * NT;
       if (v < B_VEC) {
-        int off;
-        if (BKC) off = (v / (BK / 8)) * SB + (v % (BK / 8)) * 8;
-        else off = (v / (BN / 8)) * SB + (v % (BN / 8)) * 8;
-        *(u32x4*)(Bs(buf) + off) = rb[u];
+        if (BKC) kc_store(Bs(buf), SB, v, rb[u]);
+        else *(u32x4*)(Bs(buf) + (v / (BN / 8)) * SB + (v % (BN / 8)) * 8) = rb[u];
       }
     }
   };

@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--optimizer", default="momentum", choices=["sgd", "momentum", "nesterov"])
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--fused_input", type=int, default=0, help="first conv reads the uint8 dataset directly")
     ap.add_argument("--dataset_size", type=int, default=60000)
     ap.add_argument("--phases", type=int, default=3,
                     help="extra eager steps AFTER the timed region, timed per phase with HIP events (0 = off)")
@@ -87,7 +88,12 @@ def main() -> int:
 
     imgs, labs = make_synthetic(args.dataset_size, seed=args.seed, channels=1, device=dev)
     ds = DeviceDataset(imgs, labs, dev, hw=784, channels=1)
-    loader = DeviceLoader(ds, net.x0, net.labels, rank=rank, world=world, seed=args.seed)
+    # --fused_input: the first fused conv reads the uint8 dataset through the batch index
+    # (K10 fused).  Off by default: measured ~25 us/step slower on LeNet-5 at 65536 than
+    # prep_images + bf16 (profiles/r1_u8_input/).
+    fused_in = args.impl == "hip" and args.fused_input and net.bind_u8_input(ds.images)
+    loader = DeviceLoader(ds, net.x0, net.labels, rank=rank, world=world, seed=args.seed,
+                          idx_out=net.idx_buf if fused_in else None)
 
     use_graph = bool(args.graph) and args.impl == "hip" and world == 1
     graph = None

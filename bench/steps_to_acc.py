@@ -49,6 +49,7 @@ def parse(argv=None):
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--graph", type=int, default=1)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--fused_input", type=int, default=0, help="first conv reads the uint8 dataset directly")
     return ap.parse_args(argv)
 
 
@@ -93,7 +94,12 @@ def run(args) -> dict:
     ds = DeviceDataset(imgs, labs, dev, hw=784, channels=args.in_channels)
     n_probe = min(args.probe, args.dataset_size)
     probe = DeviceDataset(imgs[:n_probe], labs[:n_probe], dev, hw=784, channels=args.in_channels)
-    loader = DeviceLoader(ds, net.x0, net.labels, rank=rank, world=world, seed=args.seed)
+    # --fused_input: the first fused conv reads the uint8 dataset through the batch index
+    # (K10 fused).  Off by default: measured ~25 us/step slower on LeNet-5 at 65536 than
+    # prep_images + bf16 (profiles/r1_u8_input/).
+    fused_in = args.impl == "hip" and args.fused_input and net.bind_u8_input(ds.images)
+    loader = DeviceLoader(ds, net.x0, net.labels, rank=rank, world=world, seed=args.seed,
+                          idx_out=net.idx_buf if fused_in else None)
 
     graph = None
     if args.graph and args.impl == "hip" and world == 1 and dev.type == "cuda":

@@ -405,31 +405,57 @@ std::vector<int64_t> convpool_reduce_args(int64_t cin, int64_t cout, int64_t ks,
   return {o[0], o[1], o[2] < 0 ? cin_real : (int64_t)o[2], o[3]};
 }
 
+// Input of a fused conv: bf16 x, or the uint8 dataset + per-sample index (Cin == 1 geometries)
+mnistx::XSrc cp_src(const Tensor& x, const optional<Tensor>& u8, const optional<Tensor>& idx, int cfg, int64_t B,
+                    int64_t hwc) {
+  mnistx::XSrc src{nullptr, nullptr, nullptr, 0};
+  if (u8.has_value() && u8->defined()) {
+    TORCH_CHECK(mnistx::convpool_u8_input(cfg), "convpool: uint8 input only for 1-channel first layers");
+    TORCH_CHECK(idx.has_value() && idx->defined(), "convpool: uint8 input needs idx");
+    check(*u8, at::kByte, hwc, "u8");
+    TORCH_CHECK(u8->numel() % hwc == 0 && u8->numel() / hwc < (int64_t)INT32_MAX, "u8: [n, H*W*C] images");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(u8->data_ptr()) % 4 == 0, "u8 must be 4-byte aligned");
+    check(*idx, at::kLong, B, "idx");
+    src.u8 = P<const uint8_t>(*u8);
+    src.idx = P<const int64_t>(*idx);
+    src.n = (int)(u8->numel() / hwc);       // the kernel clamps every index into [0, n)
+  } else {
+    check(x, at::kBFloat16, B * hwc, "x");
+    src.x = BF(x);
+  }
+  return src;
+}
+
 void convpool_fwd(Tensor x, Tensor w, Tensor bias, int64_t bias_n, Tensor pooled, Tensor arg, int64_t B, int64_t cin,
-                  int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t wd) {
+                  int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t wd, optional<Tensor> u8,
+                  optional<Tensor> idx) {
   auto g = cp_geo(cin, cout, ks, pad, h, wd);
-  check(x, at::kBFloat16, B * h * wd * cin, "x");
+  const auto src = cp_src(x, u8, idx, g.cfg, B, h * wd * cin);
   check(w, at::kBFloat16, ks * ks * cin * cout, "w");
   check(bias, at::kFloat, bias_n, "bias");
   check(pooled, at::kBFloat16, B * g.PH * g.PW * cout, "pooled");
   check(arg, at::kByte, B * g.PH * g.PW * cout, "arg");
-  hip_ok(mnistx::convpool_fwd(g.cfg, BF(x), BF(w), P<const float>(bias), (int)bias_n, (int)B, BFm(pooled),
+  hip_ok(mnistx::convpool_fwd(g.cfg, src, BF(w), P<const float>(bias), (int)bias_n, (int)B, BFm(pooled),
                               P<uint8_t>(arg), cur_stream()),
          "convpool_fwd");
 }
 
 void convpool_wgrad(Tensor x, Tensor dP, Tensor arg, Tensor slab, int64_t grid, int64_t B, int64_t cin, int64_t cout,
-                    int64_t ks, int64_t pad, int64_t h, int64_t wd) {
+                    int64_t ks, int64_t pad, int64_t h, int64_t wd, optional<Tensor> u8, optional<Tensor> idx) {
   auto g = cp_geo(cin, cout, ks, pad, h, wd);
   TORCH_CHECK(grid >= 1 && grid <= 65535, "grid");
   const int64_t np = B * g.PH * g.PW * cout;
-  check(x, at::kBFloat16, B * h * wd * cin, "x");
+  const auto src = cp_src(x, u8, idx, g.cfg, B, h * wd * cin);
   check(dP, at::kBFloat16, np, "dP");
   check(arg, at::kByte, np, "arg");
   check(slab, at::kFloat, grid * g.KM * cout, "slab");
-  hip_ok(mnistx::convpool_wgrad(g.cfg, BF(x), BF(dP), P<const uint8_t>(arg), (int)B, P<float>(slab), (int)grid,
+  hip_ok(mnistx::convpool_wgrad(g.cfg, src, BF(dP), P<const uint8_t>(arg), (int)B, P<float>(slab), (int)grid,
                                 cur_stream()),
          "convpool_wgrad");
+}
+
+bool convpool_u8_input(int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t w) {
+  return mnistx::convpool_u8_input(cp_geo(cin, cout, ks, pad, h, w).cfg) != 0;
 }
 
 bool convpool_has_dgrad(int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t w) {
@@ -475,8 +501,13 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("convpool_rows", &convpool_rows);
   m.def("gemm_tile", &gemm_tile);
   m.def("convpool_reduce_args", &convpool_reduce_args);
-  m.def("convpool_fwd", &convpool_fwd);
-  m.def("convpool_wgrad", &convpool_wgrad);
+  m.def("convpool_fwd", &convpool_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("bias_n"),
+        py::arg("pooled"), py::arg("arg"), py::arg("B"), py::arg("cin"), py::arg("cout"), py::arg("ks"),
+        py::arg("pad"), py::arg("h"), py::arg("w_"), py::arg("u8") = py::none(), py::arg("idx") = py::none());
+  m.def("convpool_wgrad", &convpool_wgrad, py::arg("x"), py::arg("dP"), py::arg("arg"), py::arg("slab"),
+        py::arg("grid"), py::arg("B"), py::arg("cin"), py::arg("cout"), py::arg("ks"), py::arg("pad"), py::arg("h"),
+        py::arg("w_"), py::arg("u8") = py::none(), py::arg("idx") = py::none());
+  m.def("convpool_u8_input", &convpool_u8_input);
   m.def("convpool_dgrad", &convpool_dgrad);
   m.def("convpool_has_dgrad", &convpool_has_dgrad);
   m.attr("ARCH") = "gfx950";

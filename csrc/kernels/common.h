@@ -21,6 +21,9 @@ DEV bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
+// uint8 pixel -> x/255 - 0.5 (mnist_input.py:37-39); fmaf so every kernel rounds identically
+DEV float u8_norm(uint32_t b) { return fmaf((float)b, 1.f / 255.f, -0.5f); }
+
 DEV uint32_t pack2(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
 }

@@ -164,14 +164,40 @@ struct XStage {
   static constexpr int NV = IMGS * G::H * G::ROWV;
   static constexpr int PER = (NV + NTH - 1) / NTH;
   u32x2 v[PER];
-  DEV void load(const bf16_t* __restrict__ x, int img0, int B, int tid) {
+  // uint8 source: dataset rows of the group to load next, fetched one group ahead
+  // so the (uniform) index load never stalls the data prefetch behind it
+  int rows[IMGS];
+  static constexpr bool U8 = G::CIN == 1;   // uint8 input only for 1-channel first layers
+  DEV void fetch_rows(const XSrc& src, int img0, int B) {
+    if (!U8 || !src.u8) return;
+#pragma unroll
+    for (int im = 0; im < IMGS; ++im) {
+      const int64_t r = img0 + im < B ? src.idx[img0 + im] : 0;
+      rows[im] = (int)min(max(r, (int64_t)0), (int64_t)src.n - 1);
+    }
+  }
+  // bf16 activations, or (first layer) the uint8 dataset gathered through the
+  // batch index and normalised x/255 - 0.5 exactly like prep_images (K10 fused).
+  // uint8: rows[] must hold the rows of this group (fetch_rows one group earlier).
+  DEV void load(const XSrc& src, int img0, int B, int tid) {
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int e = tid + u * NTH;
       v[u] = u32x2{0u, 0u};
       if (e < NV) {
         const int im = e / (G::H * G::ROWV), rem = e - im * (G::H * G::ROWV);
-        if (img0 + im < B) v[u] = *(const u32x2*)(x + (int64_t)(img0 + im) * G::INTERIOR + rem * 4);
+        if (img0 + im < B) {
+          if (U8 && src.u8) {
+            int row = rows[0];
+#pragma unroll
+            for (int k = 1; k < IMGS; ++k) row = im == k ? rows[k] : row;
+            const uint32_t b4 = *(const uint32_t*)(src.u8 + (int64_t)row * G::INTERIOR + rem * 4);
+            v[u] = u32x2{pack2(u8_norm(b4 & 0xff), u8_norm((b4 >> 8) & 0xff)),
+                         pack2(u8_norm((b4 >> 16) & 0xff), u8_norm(b4 >> 24))};
+          } else {
+            v[u] = *(const u32x2*)(src.x + (int64_t)(img0 + im) * G::INTERIOR + rem * 4);
+          }
+        }
       }
     }
   }
@@ -242,7 +268,7 @@ struct DYStage {
 
 // ------------------------------------------------------------------ forward
 template <class G, int IMGS>
-__global__ __launch_bounds__(NTH) void convpool_fwd_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+__global__ __launch_bounds__(NTH) void convpool_fwd_k(const XSrc x, const bf16_t* __restrict__ w,
                                                       const float* __restrict__ bias, int bias_n, int B,
                                                       bf16_t* __restrict__ pooled, uint8_t* __restrict__ arg) {
   constexpr int LDS = (IMGS * G::IMG_LDS + 7) / 8 * 8;
@@ -292,7 +318,9 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_k(const bf16_t* __restrict__
 
   const int stride = gridDim.x * IMGS;
   XStage<G, IMGS> xs;
+  xs.fetch_rows(x, blockIdx.x * IMGS, B);
   xs.load(x, blockIdx.x * IMGS, B, tid);
+  xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
     __syncthreads();
     xs.store(tile, tid);
@@ -301,7 +329,10 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_k(const bf16_t* __restrict__
       make_shifted<G, IMGS>(tile, tid);
       __syncthreads();
     }
-    if (img0 + stride < B) xs.load(x, img0 + stride, B, tid);
+    if (img0 + stride < B) {
+      xs.load(x, img0 + stride, B, tid);
+      xs.fetch_rows(x, img0 + 2 * stride, B);
+    }
     for (int f = wave; f < IMGS * G::MF; f += NTH / 64) {
       const int im = f / G::MF, fm = f - im * G::MF;
       const int r = min(fm * 16 + li, G::NPIX - 1);
@@ -364,7 +395,7 @@ DEV int swap_half_row(int v) { return __builtin_amdgcn_mov_dpp(v, 0x128, 0xf, 0x
 // pool max over dy stays in the lane, the max over dx is one DPP half-row swap,
 // and every lane stores one (window, channel): 16 contiguous bf16 per row group.
 template <class G, int IMGS>
-__global__ __launch_bounds__(NTH) void convpool_fwd_pair_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+__global__ __launch_bounds__(NTH) void convpool_fwd_pair_k(const XSrc x, const bf16_t* __restrict__ w,
                                                            const float* __restrict__ bias, int bias_n, int B,
                                                            bf16_t* __restrict__ pooled, uint8_t* __restrict__ arg) {
   static_assert(G::PAIR, "");
@@ -399,14 +430,19 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_pair_k(const bf16_t* __restr
 
   const int stride = gridDim.x * IMGS;
   XStage<G, IMGS> xs;
+  xs.fetch_rows(x, blockIdx.x * IMGS, B);
   xs.load(x, blockIdx.x * IMGS, B, tid);
+  xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
     __syncthreads();
     xs.store(tile, tid);
     __syncthreads();
     make_shifted<G, IMGS>(tile, tid);
     __syncthreads();
-    if (img0 + stride < B) xs.load(x, img0 + stride, B, tid);
+    if (img0 + stride < B) {
+      xs.load(x, img0 + stride, B, tid);
+      xs.fetch_rows(x, img0 + 2 * stride, B);
+    }
 #pragma unroll 1
     for (int im = 0; im < IMGS; ++im) {
       const bf16_t* timg = tile + im * G::IMG_LDS;
@@ -451,7 +487,7 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_pair_k(const bf16_t* __restr
 // chunk; the bias row (k = KE) reads a constant [1,0,0,0] LDS cell.  dY is
 // rebuilt from (dP, arg): position d of a window gets dP iff arg == d.
 template <class G, int IMGS>
-__global__ __launch_bounds__(NTH) void convpool_wgrad_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dP,
+__global__ __launch_bounds__(NTH) void convpool_wgrad_k(const XSrc x, const bf16_t* __restrict__ dP,
                                                         const uint8_t* __restrict__ arg, int B,
                                                         float* __restrict__ slab) {
   constexpr int CELL = IMGS * G::IMG_LDS;             // [1,0,0,0] then [0,0,0,0]
@@ -492,7 +528,9 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_k(const bf16_t* __restrict
   const int stride = gridDim.x * IMGS;
   XStage<G, IMGS> xs;
   DYStage<G, IMGS> ys;
+  xs.fetch_rows(x, blockIdx.x * IMGS, B);
   xs.load(x, blockIdx.x * IMGS, B, tid);
+  xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
   ys.load(dP, arg, blockIdx.x * IMGS, B, tid);
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
     __syncthreads();
@@ -505,6 +543,7 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_k(const bf16_t* __restrict
     }
     if (img0 + stride < B) {
       xs.load(x, img0 + stride, B, tid);
+      xs.fetch_rows(x, img0 + 2 * stride, B);
       ys.load(dP, arg, img0 + stride, B, tid);
     }
     for (int it = wave; it < IMGS * G::RSTEPS; it += NTH / 64) {
@@ -599,7 +638,7 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_k(const bf16_t* __restrict
 // dW[m][c] = R[m][c] + R[m+1][8+c] (bias row: both sides) is applied to the block
 // partials, and the slab has the plain MODE 0 layout [KM][8].
 template <class G, int IMGS>
-__global__ __launch_bounds__(NTH) void convpool_wgrad_pair_k(const bf16_t* __restrict__ x,
+__global__ __launch_bounds__(NTH) void convpool_wgrad_pair_k(const XSrc x,
                                                              const bf16_t* __restrict__ dP,
                                                              const uint8_t* __restrict__ arg, int B,
                                                              float* __restrict__ slab) {
@@ -635,7 +674,9 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_pair_k(const bf16_t* __res
   const int stride = gridDim.x * IMGS;
   XStage<G, IMGS> xs;
   DYStage<G, IMGS> ys;
+  xs.fetch_rows(x, blockIdx.x * IMGS, B);
   xs.load(x, blockIdx.x * IMGS, B, tid);
+  xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
   ys.load(dP, arg, blockIdx.x * IMGS, B, tid);
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
     __syncthreads();
@@ -646,6 +687,7 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_pair_k(const bf16_t* __res
     __syncthreads();
     if (img0 + stride < B) {
       xs.load(x, img0 + stride, B, tid);
+      xs.fetch_rows(x, img0 + 2 * stride, B);
       ys.load(dP, arg, img0 + stride, B, tid);
     }
     for (int it = wave; it < IMGS * RS; it += NTH / 64) {
@@ -812,7 +854,7 @@ int grid_for(int B, int imgs, int cap) {
 }
 
 template <class G, int IMGS>
-hipError_t run_fwd(const bf16_t* x, const bf16_t* w, const float* bias, int bias_n, int B, bf16_t* pooled, uint8_t* arg,
+hipError_t run_fwd(const XSrc& x, const bf16_t* w, const float* bias, int bias_n, int B, bf16_t* pooled, uint8_t* arg,
                    hipStream_t st) {
   if constexpr (G::PAIR) {
     hipLaunchKernelGGL((convpool_fwd_pair_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, x, w, bias,
@@ -825,7 +867,7 @@ hipError_t run_fwd(const bf16_t* x, const bf16_t* w, const float* bias, int bias
 }
 
 template <class G, int IMGS>
-hipError_t run_wgrad(const bf16_t* x, const bf16_t* dP, const uint8_t* arg, int B, float* slab, int grid,
+hipError_t run_wgrad(const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B, float* slab, int grid,
                      hipStream_t st) {
   if constexpr (G::PAIR) {
     hipLaunchKernelGGL((convpool_wgrad_pair_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab);
@@ -886,7 +928,7 @@ int convpool_reduce_layout(int cfg, int* out) {
   return -1;
 }
 
-hipError_t convpool_fwd(int cfg, const bf16_t* x, const bf16_t* w, const float* bias, int bias_n, int B,
+hipError_t convpool_fwd(int cfg, const XSrc& x, const bf16_t* w, const float* bias, int bias_n, int B,
                         bf16_t* pooled, uint8_t* arg, hipStream_t st) {
   switch (cfg) {
     case 0: return run_fwd<LeNetC1, 2>(x, w, bias, bias_n, B, pooled, arg, st);
@@ -897,7 +939,7 @@ hipError_t convpool_fwd(int cfg, const bf16_t* x, const bf16_t* w, const float* 
   return hipErrorInvalidValue;
 }
 
-hipError_t convpool_wgrad(int cfg, const bf16_t* x, const bf16_t* dP, const uint8_t* arg, int B, float* slab,
+hipError_t convpool_wgrad(int cfg, const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B, float* slab,
                           int grid, hipStream_t st) {
   switch (cfg) {
     case 0: return run_wgrad<LeNetC1, 2>(x, dP, arg, B, slab, grid, st);
@@ -909,6 +951,8 @@ hipError_t convpool_wgrad(int cfg, const bf16_t* x, const bf16_t* dP, const uint
 }
 
 int convpool_has_dgrad(int cfg) { return cfg == 1 ? 1 : 0; }
+
+int convpool_u8_input(int cfg) { return (cfg == 0 || cfg == 2) ? 1 : 0; }  // Cin == 1 first layers
 
 hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int B, bf16_t* dx,
                           hipStream_t st) {

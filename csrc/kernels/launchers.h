@@ -41,14 +41,23 @@ hipError_t conv_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int H, int W, i
                       hipStream_t st);
 
 // ---- convpool.hip (fused small-channel conv + bias + ReLU + 2x2 max-pool)
+// Input of a fused conv: bf16 NHWC activations, or (Cin == 1 first layer) the
+// uint8 dataset [n][H*W] gathered through the per-sample index idx[B].
+struct XSrc {
+  const bf16_t* x;
+  const uint8_t* u8;
+  const int64_t* idx;
+  int n;
+};
+int convpool_u8_input(int cfg);
 int convpool_config(int cin, int cout, int ks, int pad, int h, int w);  // -1: unsupported
 int convpool_wgrad_rows(int cfg);                                      // KM (slab rows incl. bias row)
 // slab -> dW layout for splitk_reduce: {G, Ipad, I (-1: real Cin), bias_row}
 int convpool_reduce_layout(int cfg, int* out);
-hipError_t convpool_fwd(int cfg, const bf16_t* x, const bf16_t* w, const float* bias, int bias_n, int B,
+hipError_t convpool_fwd(int cfg, const XSrc& x, const bf16_t* w, const float* bias, int bias_n, int B,
                         bf16_t* pooled, uint8_t* arg, hipStream_t st);
 // backward needs only (dP, arg): arg == 4 marks a window whose ReLU output is 0
-hipError_t convpool_wgrad(int cfg, const bf16_t* x, const bf16_t* dP, const uint8_t* arg, int B, float* slab,
+hipError_t convpool_wgrad(int cfg, const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B, float* slab,
                           int grid, hipStream_t st);
 int convpool_has_dgrad(int cfg);
 hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int B, bf16_t* dx,

@@ -40,8 +40,8 @@ __global__ void prep_images_k(const uint8_t* __restrict__ src, const int64_t* __
       uint32_t lo = *(const uint32_t*)s, hi = *(const uint32_t*)(s + 4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float a = (float)((lo >> (8 * j)) & 0xff) * (1.f / 255.f) - 0.5f;
-        float c = (float)((hi >> (8 * j)) & 0xff) * (1.f / 255.f) - 0.5f;
+        float a = u8_norm((lo >> (8 * j)) & 0xff);
+        float c = u8_norm((hi >> (8 * j)) & 0xff);
         u4_set(o, j, f2bf(a));
         u4_set(o, j + 4, f2bf(c));
       }
@@ -52,7 +52,7 @@ __global__ void prep_images_k(const uint8_t* __restrict__ src, const int64_t* __
         const int64_t p = ww / Cdst;
         const int c = (int)(ww - p * Cdst);
         const int cs = c < Csrc ? c : 0;  // 1 -> 3 channel replication
-        u4_set(o, j, f2bf((float)img[p * Csrc + cs] * (1.f / 255.f) - 0.5f));
+        u4_set(o, j, f2bf(u8_norm(img[p * Csrc + cs])));
       }
     }
     *(u32x4*)(out + e) = o;

@@ -52,8 +52,13 @@ class DeviceDataset:
 
 class DeviceLoader:
     def __init__(self, ds: DeviceDataset, out_images: torch.Tensor, out_labels: torch.Tensor, rank: int = 0,
-                 world: int = 1, seed: int = 0, shard: bool = True, shuffle: bool = True):
+                 world: int = 1, seed: int = 0, shard: bool = True, shuffle: bool = True,
+                 idx_out: Optional[torch.Tensor] = None):
+        """``idx_out``: instead of gathering + normalising images into ``out_images``,
+        write the batch's dataset indices there (the first fused conv reads the
+        uint8 dataset itself: HipNet.bind_u8_input); labels are still gathered."""
         self.ds, self.out_images, self.out_labels = ds, out_images, out_labels
+        self.idx_out = idx_out
         self.B = int(out_labels.shape[0])
         self.rank, self.world, self.shard, self.shuffle = rank, world, shard, shuffle
         self.global_batch = self.B * world if shard else self.B
@@ -84,7 +89,12 @@ class DeviceLoader:
             self.epoch += 1
             self._new_epoch()
         start = self.cursor + (self.rank * self.B if self.shard else 0)
-        gather_into(self.ds, self.perm[start:start + nb], self.out_images, self.out_labels)
+        idx = self.perm[start:start + nb]
+        if self.idx_out is not None:
+            self.idx_out[:nb].copy_(idx)
+            torch.index_select(self.ds.labels, 0, idx, out=self.out_labels[:nb])
+        else:
+            gather_into(self.ds, idx, self.out_images, self.out_labels)
         self.cursor += self.global_batch
         return nb
 

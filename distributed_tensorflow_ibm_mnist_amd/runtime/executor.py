@@ -118,15 +118,22 @@ class ConvPoolLayer(_Layer):
     def _geo(self):
         return (self.C, self.Cp, 5, self.pad, self.H, self.W)
 
+    # first layer only: read the uint8 dataset through the batch index (fused K10)
+    u8: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+    use_u8 = False
+
+    def _src(self) -> dict:
+        return {"u8": self.u8[0], "idx": self.u8[1]} if (self.u8 is not None and self.use_u8) else {}
+
     def fwd(self, nb: int) -> None:
         kernels().convpool_fwd(self.x, self.fp.bf16_view(self.wname), self.fp.param_view(self.bname),
-                               self.spec.cout, self.out, self.arg, nb, *self._geo())
+                               self.spec.cout, self.out, self.arg, nb, *self._geo(), **self._src())
 
     def bwd(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor], slab: torch.Tensor) -> None:
         s = self.spec
         K = kernels()
         grid = min(self.grid, max(1, (nb + 3) // 4))
-        K.convpool_wgrad(self.x, dy, self.arg, slab, grid, nb, *self._geo())
+        K.convpool_wgrad(self.x, dy, self.arg, slab, grid, nb, *self._geo(), **self._src())
         G, Ip, I, brow = self.red
         K.splitk_reduce(slab, grid, self.KM, self.Cp, G, Ip, I, s.cout, brow,
                         self.fp.grad_view(self.wname), self.fp.grad_view(self.bname), 1.0)
@@ -301,10 +308,31 @@ class HipNet:
         self.loss_names = [n.replace("/weights", "/weight_loss") for n in names] + ["cross_entropy", "total_loss"]
         self.loss_ema = torch.zeros(3 * len(self.loss_names), dtype=torch.float32, device=dev)
         self.grad_ready_hooks: List[Callable[[int], None]] = []
+        self.idx_buf: Optional[torch.Tensor] = None
+
+    def bind_u8_input(self, images_u8: torch.Tensor) -> bool:
+        """Training steps read the uint8 dataset [n, H*W] directly through ``idx_buf``
+        (filled by DeviceLoader(idx_out=...)), fusing the normalise/gather (K10,
+        mnist_input.py:37-39) into the first fused conv.  Eval / inference keep
+        using ``x0``.  Returns False when the first layer cannot (Cin != 1 etc.)."""
+        first = self.layers[0]
+        H, W = self.spec.input_hw
+        if not (isinstance(first, ConvPoolLayer) and self.spec.in_channels == 1
+                and images_u8.dtype == torch.uint8 and images_u8.dim() == 2 and images_u8.shape[1] == H * W
+                and images_u8.device == self.device and kernels().convpool_u8_input(*first._geo())):
+            return False
+        self.idx_buf = torch.zeros(self.B, dtype=torch.int64, device=self.device)
+        first.u8 = (images_u8.contiguous(), self.idx_buf)
+        return True
 
     # ------------------------------------------------------------------ step parts
-    def forward(self, nb: Optional[int] = None) -> torch.Tensor:
+    def forward(self, nb: Optional[int] = None, from_x0: bool = False) -> torch.Tensor:
+        """Training forward reads the bound uint8 source when there is one;
+        ``from_x0`` forces the bf16 ``x0`` buffer (eval / inference / tests)."""
         nb = self.B if nb is None else nb
+        first = self.layers[0]
+        if isinstance(first, ConvPoolLayer):
+            first.use_u8 = first.u8 is not None and not from_x0
         for lay in self.layers:
             lay.fwd(nb)
         return self.logits
@@ -352,14 +380,14 @@ class HipNet:
     # ------------------------------------------------------------------ eval
     def eval_batch(self, nb: int, stats: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Forward only on x0[:nb] / labels[:nb]; accumulates loss/correct into stats."""
-        self.forward(nb)
+        self.forward(nb, from_x0=True)
         st = self.eval_stats if stats is None else stats
         kernels().softmax_ce(self.logits, self.logits.shape[1], self.labels, nb, self.n_classes, 1.0, None,
                              self.logits.shape[1], st, None, self.ce_work)
         return st
 
     def probs(self, nb: int) -> torch.Tensor:
-        self.forward(nb)
+        self.forward(nb, from_x0=True)
         return Fk.softmax_probs(self.logits[:nb], self.n_classes)
 
     # ------------------------------------------------------------------ introspection

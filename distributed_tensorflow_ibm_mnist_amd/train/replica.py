@@ -80,7 +80,7 @@ class Replica:
                  train_images: torch.Tensor, train_labels: torch.Tensor, src_channels: int,
                  eval_images: Optional[torch.Tensor] = None, eval_labels: Optional[torch.Tensor] = None,
                  seed: int = 0, shard: bool = True, use_graph: bool = True, bucket_mb: float = 4.0,
-                 group=None, standalone: bool = False):
+                 group=None, standalone: bool = False, fused_input: bool = False):
         self.spec, self.impl, self.B, self.device = spec, impl, batch, torch.device(device)
         self.net = build_net(impl, spec, batch, self.device, init, opt)
         # standalone: a parameter-server worker (no data-parallel group of its own)
@@ -91,8 +91,10 @@ class Replica:
         self.train_ds = DeviceDataset(train_images, train_labels, self.device, hw=784, channels=src_channels)
         self.eval_ds = (DeviceDataset(eval_images, eval_labels, self.device, hw=784, channels=src_channels)
                         if eval_images is not None else None)
+        # --fused_input (HIP): the first fused conv reads the uint8 training set through the batch index
+        fused_in = fused_input and impl == "hip" and self.net.bind_u8_input(self.train_ds.images)
         self.loader = DeviceLoader(self.train_ds, self.net.x0, self.net.labels, rank=self.rank, world=self.world,
-                                   seed=seed, shard=shard)
+                                   seed=seed, shard=shard, idx_out=self.net.idx_buf if fused_in else None)
         self.use_graph = use_graph and impl == "hip" and self.world == 1 and self.device.type == "cuda"
         self._graph = None
         self.global_step = 0

@@ -119,7 +119,8 @@ def _train(FLAGS, cl: Cluster, max_steps, test_interval, batch_size, impl, log) 
     dp_group = None
     base = Replica(spec, impl, batch_size, cl.device, init, opt, x_tr, y_tr, c_tr, x_ev, y_ev,
                    seed=FLAGS.seed, shard=not FLAGS.no_shard, use_graph=FLAGS.hip_graph,
-                   bucket_mb=FLAGS.bucket_mb, group=dp_group if cl.mode == "dp" else None) \
+                   bucket_mb=FLAGS.bucket_mb, group=dp_group if cl.mode == "dp" else None,
+                   fused_input=FLAGS.fused_input) \
         if cl.mode != "ps" else _ps_base(spec, impl, batch_size, cl, init, opt, x_tr, y_tr, c_tr, x_ev, y_ev, FLAGS)
     replica = base
     if cl.mode == "ps":

@@ -133,3 +133,17 @@ def test_synthetic_data_deterministic_and_learnable():
     means = torch.stack([x[la == c].mean(0) for c in range(10)])
     pred = torch.cdist(x, means).argmin(1)
     assert (pred == la).float().mean().item() > 0.5
+
+
+def test_shipped_configs_load():
+    import glob
+    from distributed_tensorflow_ibm_mnist_amd.utils import parameter_mgr as pm
+    from distributed_tensorflow_ibm_mnist_amd.data.synthetic import parse_uri
+    files = sorted(glob.glob(os.path.join(ROOT, "configs", "*.yaml")))
+    assert len(files) >= 3
+    for f in files:
+        pm.configure(f)
+        assert pm.getMaxSteps() > 0 and pm.getTrainBatchSize() > 0
+        for uri in pm.getTrainData() + pm.getTestData():
+            parse_uri(uri)
+    pm.configure({})

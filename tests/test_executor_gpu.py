@@ -104,3 +104,32 @@ def test_graph_replay_matches_eager(dev, K):
     torch.cuda.synchronize()
     assert int(nets[0].fp.step.item()) == int(nets[1].fp.step.item()) == 6
     assert torch.equal(nets[0].fp.params, nets[1].fp.params)
+
+
+@pytest.mark.parametrize("model", ["lenet5", "reference_cnn"])
+def test_u8_input_path_bitwise_equal(dev, K, model):
+    """First fused conv reading the uint8 dataset through the batch index (fused K10)
+    must equal prep_images + bf16 x0, bitwise, through a full train step."""
+    from distributed_tensorflow_ibm_mnist_amd.data.synthetic import make_synthetic
+    from distributed_tensorflow_ibm_mnist_amd.data.device_loader import DeviceDataset, DeviceLoader
+    spec = get_model(model, 1)
+    init = torch_ref.init_params(spec, seed=3)
+    opt = OptConfig(lr0=0.05, use_momentum=True, momentum=0.9, ema_max=0.9999)
+    imgs, labs = make_synthetic(3000, seed=4, device=dev)
+    ds = DeviceDataset(imgs, labs, dev)
+    a = HipNet(spec, 200, dev, init, opt)
+    b = HipNet(spec, 200, dev, init, opt)
+    assert b.bind_u8_input(ds.images)
+    la = DeviceLoader(ds, a.x0, a.labels, seed=9)
+    lb = DeviceLoader(ds, b.x0, b.labels, seed=9, idx_out=b.idx_buf)
+    for _ in range(3):
+        la.next()
+        lb.next()
+        a.train_step()
+        b.train_step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.labels, b.labels)
+    assert torch.equal(a.fp.params, b.fp.params)
+    # eval keeps reading x0
+    b.x0.copy_(a.x0)
+    assert torch.equal(a.eval_batch(200, torch.zeros(8, device=dev)), b.eval_batch(200, torch.zeros(8, device=dev)))

@@ -142,6 +142,20 @@ DEV int opaque(int v) {
   return v;
 }
 
+// Max-pool with the argmax riding in the value: the 2-bit window position d is
+// written into the two low mantissa bits of the fp32 conv sum (a <= 3-ulp
+// perturbation, far below bf16 resolution), so pooling is plain v_max_f32 and the
+// winner's position is bits & 3.  ReLU(. + b) is monotone, so pooling the raw sums
+// and applying bias + ReLU once is exact.
+DEV float pos_embed(float v, uint32_t d) { return __uint_as_float((__float_as_uint(v) & ~3u) | d); }
+DEV float vmax(float a, float b) {  // bare v_max_f32 (fmaxf adds NaN-canonicalising moves)
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+DEV uint32_t pos_of(float v) { return __float_as_uint(v) & 3u; }
+DEV float pos_clear(float v) { return __uint_as_float(__float_as_uint(v) & ~3u); }
+
 constexpr int NTH = 256;
 // Argmax byte of a pool window whose ReLU output is 0: matches no position, so
 // the backward kernels need only (dP, arg) -- the ReLU mask is folded in here
@@ -367,14 +381,11 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_k(const XSrc x, const bf16_t
           if (n < G::COUT) {
             // relu(. + b) is monotone: pool the raw sums, then bias + ReLU once
             const f32x4 v = acc[nf];
-            const bool t01 = v[1] > v[0], t23 = v[3] > v[2];
-            const float m01 = t01 ? v[1] : v[0], m23 = t23 ? v[3] : v[2];
-            const bool hi = m23 > m01;
-            const float m = hi ? m23 : m01;
-            const int bi = hi ? (t23 ? 3 : 2) : (t01 ? 1 : 0);
-            const float o = m + bs[nf];
-            pimg[win * G::COUT + n] = f2bf(fmaxf(o, 0.f));
-            aimg[win * G::COUT + n] = (uint8_t)(o > 0.f ? bi : ARG_OFF);
+            const float best = vmax(vmax(pos_embed(v[0], 0u), pos_embed(v[1], 1u)),
+                                    vmax(pos_embed(v[2], 2u), pos_embed(v[3], 3u)));
+            const float o = pos_clear(best) + bs[nf];
+            pimg[win * G::COUT + n] = f2bf(vmax(o, 0.f));
+            aimg[win * G::COUT + n] = (uint8_t)(o > 0.f ? pos_of(best) : ARG_OFF);
           }
         }
       }
@@ -477,6 +488,135 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_pair_k(const XSrc x, const b
         }
       }
     }
+  }
+}
+
+// ------------------------------------------------------------------ forward, Cin 1 / Cout 8 quad layout (32x32x16)
+// v_mfma_f32_32x32x16_bf16 with column n = (shift s = n>>3 in 0..3, channel c = n&7):
+// one A row = 8 consecutive input pixels per kernel row (K = kh*8 + kw', kw' 0..7),
+// and shift s convolves output column ow0 + s, so a row produces 4 horizontally
+// adjacent outputs = 2 pool windows.  Row r = (quad qw = r/2, window row dy = r&1),
+// quad = (pooled row ph, column pair pq): output columns 4pq..4pq+3.  The image sits
+// in LDS ONCE with its interior at column X0 = 10, so every A run (input column
+// 4pq - 2 + 10) is 8-byte aligned: two ds_read_b64, no shifted copies.
+// Epilogue: dy max in-lane (accumulator rows 2m, 2m+1), dx max across lanes n, n^8
+// (DPP half-row swap); each lane finalises 4 (window, channel) outputs.
+struct QuadGeo {
+  static constexpr int CIN = 1, H = 28, W = 28, PAD = 2, KS = 5, COUT = 8;
+  static constexpr int HP = 32, X0 = 10, WS = 40;
+  static constexpr int ROWV = W * CIN / 4;          // 4-pixel vectors per interior row
+  static constexpr int INTERIOR = H * W;
+  static constexpr int IMG_LDS = HP * WS;
+  static constexpr int PW = 14, NWIN = 196, PQ = 7, NQUAD = 14 * 7;
+  static_assert(PW == 2 * PQ, "window = 2 * quad + side");
+  static constexpr int MFQ = (NQUAD + 15) / 16;     // 32-row fragments per image
+  static_assert(4 * (PQ - 1) - PAD + X0 + 7 < WS, "A runs stay inside the row");
+  static_assert((X0 - PAD) % 4 == 0 && WS % 4 == 0, "A runs are 8-byte aligned");
+};
+
+template <int IMGS>
+__global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const bf16_t* __restrict__ w,
+                                                           const float* __restrict__ bias, int bias_n, int B,
+                                                           bf16_t* __restrict__ pooled, uint8_t* __restrict__ arg) {
+  using Q = QuadGeo;
+  constexpr int LDS = IMGS * Q::IMG_LDS;
+  constexpr int OUTE = Q::NWIN * 8;                 // pooled elements per image (16-byte multiple)
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  __shared__ __attribute__((aligned(16))) bf16_t tile[LDS];
+  // outputs of the block's image group are staged here and written as 16-byte vectors
+  __shared__ __attribute__((aligned(16))) bf16_t pout[IMGS * OUTE];
+  __shared__ __attribute__((aligned(16))) uint8_t aout[IMGS * OUTE];
+  static_assert((OUTE * 2) % 16 == 0 && OUTE % 16 == 0, "");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = lane & 31, h = lane >> 5;
+  const int s = n >> 3, c = n & 7, sp = s & 1, wp = s >> 1;
+  lds_zero<LDS>(tile, tid);
+
+  // B operand: k = 16q + 8h + j -> (kh = 2q + h, kw' = j); shift s uses tap kw = kw' - s
+  bf16x8 bfr[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kh = 2 * q + h, kw = j - s;
+      const bool valid = kh < Q::KS && kw >= 0 && kw < Q::KS;
+      bfr[q][j] = as_bf(valid ? w[(kh * Q::KS + kw) * Q::COUT + c] : (bf16_t)0);
+    }
+  const float bs = c < bias_n ? bias[c] : 0.f;
+  // this lane's A row: r = lane & 31 -> quad qw = r >> 1, dy = r & 1
+  const int r = lane & 31, qw = r >> 1, dyr = r & 1;
+
+  const int stride = gridDim.x * IMGS;
+  XStage<Q, IMGS> xs;
+  xs.fetch_rows(x, blockIdx.x * IMGS, B);
+  xs.load(x, blockIdx.x * IMGS, B, tid);
+  xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
+  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
+    __syncthreads();
+    // interior rows at column X0 = 10 (4-byte aligned): two 4-byte stores per vector
+#pragma unroll
+    for (int u = 0; u < XStage<Q, IMGS>::PER; ++u) {
+      const int e = tid + u * NTH;
+      if (e < XStage<Q, IMGS>::NV) {
+        const int im = e / (Q::H * Q::ROWV), rem = e - im * (Q::H * Q::ROWV);
+        const int hh = rem / Q::ROWV, vv = rem - hh * Q::ROWV;
+        bf16_t* dst = tile + im * Q::IMG_LDS + (hh + Q::PAD) * Q::WS + Q::X0 + 4 * vv;
+        *(uint32_t*)dst = xs.v[u][0];
+        *(uint32_t*)(dst + 2) = xs.v[u][1];
+      }
+    }
+    __syncthreads();
+    if (img0 + stride < B) {
+      xs.load(x, img0 + stride, B, tid);
+      xs.fetch_rows(x, img0 + 2 * stride, B);
+    }
+#pragma unroll 1
+    for (int im = 0; im < IMGS; ++im) {
+      const bf16_t* timg = tile + im * Q::IMG_LDS;
+      bf16_t* pimg = pout + im * OUTE;
+      uint8_t* aimg = aout + im * OUTE;
+      for (int fm = wave; fm < Q::MFQ; fm += NTH / 64) {
+        const int quad = min(fm * 16 + qw, Q::NQUAD - 1);
+        const int ph = quad / Q::PQ, pq = quad - ph * Q::PQ;
+        // tile row of (oh + kh) for kh = h (+2q): oh = 2ph + dy; column 4pq - PAD + X0
+        const bf16_t* tb = timg + (2 * ph + dyr + h) * Q::WS + 4 * pq - Q::PAD + Q::X0;
+        f32x16 acc = {};
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const int rowoff = min(2 * q, 4 - h) * Q::WS;   // kh = 2q + h; the padded kh = 5 reads row 4 (zero weight)
+          const bf16x8 a = join(*(const s16x4*)(tb + rowoff), *(const s16x4*)(tb + opaque(rowoff + 4)));
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[q], acc, 0, 0, 0);
+        }
+        // acc[i]: row (i&3) + 8(i>>2) + 4h -> quad t-slot t = i/2 (qw = (t&1) + 4(t>>1) + 2h),
+        // dy = i&1; this lane's pixel column within the window is sp: position 2dy + sp
+        float m[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+          m[t] = vmax(pos_embed(acc[2 * t], (uint32_t)sp), pos_embed(acc[2 * t + 1], 2u + sp));
+        // lanes n and n^8 hold the left / right pixel of the same window; the even-s lane
+        // finalises even t-slots, the odd-s lane odd ones
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float oth = swap_half_row(sp ? m[2 * u] : m[2 * u + 1]);
+          const int t = 2 * u + sp;
+          const float best = vmax(sp ? m[2 * u + 1] : m[2 * u], oth);
+          const int qt = fm * 16 + (t & 1) + 4 * (t >> 1) + 2 * h;
+          if (qt < Q::NQUAD) {
+            const int win = 2 * qt + wp;   // ph*14 + 2pq + wp with qt = ph*7 + pq (PW == 2*PQ)
+            const float o = pos_clear(best) + bs;
+            pimg[win * 8 + c] = f2bf(vmax(o, 0.f));
+            aimg[win * 8 + c] = (uint8_t)(o > 0.f ? pos_of(best) : ARG_OFF);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // the group's outputs are contiguous in HBM: full 16-byte stores
+    const int nimg = min(IMGS, B - img0);
+    bf16_t* pg = pooled + (int64_t)img0 * OUTE;
+    uint8_t* ag = arg + (int64_t)img0 * OUTE;
+    for (int e = tid; e < nimg * OUTE / 8; e += NTH) *(u32x4*)(pg + 8 * e) = *(const u32x4*)(pout + 8 * e);
+    for (int e = tid; e < nimg * OUTE / 16; e += NTH) *(u32x4*)(ag + 16 * e) = *(const u32x4*)(aout + 16 * e);
   }
 }
 
@@ -856,7 +996,11 @@ int grid_for(int B, int imgs, int cap) {
 template <class G, int IMGS>
 hipError_t run_fwd(const XSrc& x, const bf16_t* w, const float* bias, int bias_n, int B, bf16_t* pooled, uint8_t* arg,
                    hipStream_t st) {
-  if constexpr (G::PAIR) {
+  if constexpr (G::PAIR && G::H == 28 && G::W == 28 && G::PAD == 2) {
+    constexpr int QI = 4;
+    hipLaunchKernelGGL((convpool_fwd_quad_k<QI>), dim3(grid_for(B, QI, 2048)), dim3(NTH), 0, st, x, w, bias, bias_n,
+                       B, pooled, arg);
+  } else if constexpr (G::PAIR) {
     hipLaunchKernelGGL((convpool_fwd_pair_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, x, w, bias,
                        bias_n, B, pooled, arg);
   } else {

@@ -40,7 +40,18 @@ class _Layer:
     out: torch.Tensor          # output activation buffer [B, ...]
 
     def fwd(self, nb: int) -> None: ...
-    def bwd(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor]) -> None: ...
+
+    # backward = weight gradient (off the critical path: side stream) + data gradient
+    def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor) -> None:
+        pass
+
+    def bwd_data(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor]) -> None:
+        pass
+
+    def bwd(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor], slab=None) -> None:
+        if self.has_params:
+            self.bwd_weight(nb, dy, slab)
+        self.bwd_data(nb, dy, dx)
 
 
 class ConvLayer(_Layer):
@@ -64,16 +75,19 @@ class ConvLayer(_Layer):
                            self.OW, s.kh, s.kw, self.ph, self.pw, self.Cp, self.fp.param_view(self.bname), s.cout,
                            s.relu)
 
-    def bwd(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor], slab: torch.Tensor) -> None:
+    def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor) -> None:
         s = self.spec
         K = kernels()
         S = K.conv_wgrad(self.x, dy, slab, nb, self.H, self.W, self.C, self.OH, self.OW, s.kh, s.kw, self.ph, self.pw,
                          self.Cp, True, Fk.pick_splits(self.M_wg, self.Cp, nb * self.OH * self.OW))
         K.splitk_reduce(slab, S, self.M_wg, self.Cp, s.kh * s.kw, self.C, s.cin, s.cout, s.kh * s.kw * self.C,
                         self.fp.grad_view(self.wname), self.fp.grad_view(self.bname), 1.0)
+
+    def bwd_data(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor]) -> None:
         if dx is not None:
-            K.conv_dgrad(dy, self.fp.bf16_view(self.wname), dx, nb, self.OH, self.OW, self.Cp, self.H, self.W, s.kh,
-                         s.kw, self.ph, self.pw, self.C, self.x if self.in_relu else None)
+            s = self.spec
+            kernels().conv_dgrad(dy, self.fp.bf16_view(self.wname), dx, nb, self.OH, self.OW, self.Cp, self.H, self.W,
+                                 s.kh, s.kw, self.ph, self.pw, self.C, self.x if self.in_relu else None)
 
 
 class ConvPoolLayer(_Layer):
@@ -129,16 +143,17 @@ class ConvPoolLayer(_Layer):
         kernels().convpool_fwd(self.x, self.fp.bf16_view(self.wname), self.fp.param_view(self.bname),
                                self.spec.cout, self.out, self.arg, nb, *self._geo(), **self._src())
 
-    def bwd(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor], slab: torch.Tensor) -> None:
-        s = self.spec
+    def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor) -> None:
         K = kernels()
         grid = min(self.grid, max(1, (nb + 3) // 4))
         K.convpool_wgrad(self.x, dy, self.arg, slab, grid, nb, *self._geo(), **self._src())
         G, Ip, I, brow = self.red
-        K.splitk_reduce(slab, grid, self.KM, self.Cp, G, Ip, I, s.cout, brow,
+        K.splitk_reduce(slab, grid, self.KM, self.Cp, G, Ip, I, self.spec.cout, brow,
                         self.fp.grad_view(self.wname), self.fp.grad_view(self.bname), 1.0)
+
+    def bwd_data(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor]) -> None:
         if dx is not None:
-            K.convpool_dgrad(dy, self.arg, self.fp.bf16_view(self.wname), dx, nb, *self._geo())
+            kernels().convpool_dgrad(dy, self.arg, self.fp.bf16_view(self.wname), dx, nb, *self._geo())
 
 
 class PoolLayer(_Layer):
@@ -153,7 +168,7 @@ class PoolLayer(_Layer):
     def fwd(self, nb: int) -> None:
         kernels().maxpool_fwd(self.x, self.out, self.arg, nb, self.H, self.W, self.C, self.OH, self.OW)
 
-    def bwd(self, nb: int, dy, dx, slab=None) -> None:
+    def bwd_data(self, nb: int, dy, dx) -> None:
         if dx is not None:
             kernels().maxpool_bwd(dy, self.arg, self.out, self.in_relu, dx, nb, self.H, self.W, self.C, self.OH,
                                   self.OW)
@@ -172,7 +187,7 @@ class LRNLayer(_Layer):
         s = self.spec
         kernels().lrn_fwd(self.x, self.out, self._p(nb), self.C, s.depth_radius, s.bias, s.alpha, s.beta)
 
-    def bwd(self, nb: int, dy, dx, slab=None) -> None:
+    def bwd_data(self, nb: int, dy, dx) -> None:
         if dx is not None:
             s = self.spec
             kernels().lrn_bwd(self.x, dy, dx, self._p(nb), self.C, s.depth_radius, s.bias, s.alpha, s.beta,
@@ -199,7 +214,7 @@ class DenseLayer(_Layer):
         kernels().dense_fwd(self.x, self.fp.bf16_view(self.wname), self.out, nb, self.Np, self.Dp, self.Dp, self.Np,
                             self.Np, self.fp.param_view(self.bname), s.dout, s.relu, None, 0)
 
-    def bwd(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor], slab: torch.Tensor) -> None:
+    def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor) -> None:
         s = self.spec
         K = kernels()
         dy2 = dy.view(-1, self.Np)
@@ -207,9 +222,12 @@ class DenseLayer(_Layer):
                           Fk.pick_splits(self.M_wg, self.Np, nb))
         K.splitk_reduce(slab, S, self.M_wg, self.Np, 1, self.Dp, s.din, s.dout, self.Dp,
                         self.fp.grad_view(self.wname), self.fp.grad_view(self.bname), 1.0)
+
+    def bwd_data(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor]) -> None:
         if dx is not None:
-            K.dense_dgrad(dy2, self.fp.bf16_view(self.wname), dx.view(-1, self.Dp), nb, self.Dp, self.Np, self.Np,
-                          self.Np, self.Dp, self.x if self.in_relu else None, self.Dp)
+            dy2 = dy.view(-1, self.Np)
+            kernels().dense_dgrad(dy2, self.fp.bf16_view(self.wname), dx.view(-1, self.Dp), nb, self.Dp, self.Np,
+                                  self.Np, self.Np, self.Dp, self.x if self.in_relu else None, self.Dp)
 
 
 def _weight_pads(spec: ModelSpec) -> Dict[str, Tuple[int, int]]:
@@ -238,7 +256,7 @@ class HipNet:
     """One model replica on one GPU: buffers + kernels for fwd / bwd / update."""
 
     def __init__(self, spec: ModelSpec, batch: int, device, init: Dict[str, torch.Tensor],
-                 opt: Optional[OptConfig] = None, fuse_convpool: bool = True):
+                 opt: Optional[OptConfig] = None, fuse_convpool: bool = True, overlap_backward: bool = False):
         dev = torch.device(device)
         self.spec, self.B, self.device = spec, batch, dev
         self.opt = opt or OptConfig()
@@ -294,12 +312,25 @@ class HipNet:
         assert isinstance(self.layers[-1], DenseLayer) and self.layers[-1].last, "model must end in a Dense"
         self.logits = self.layers[-1].out
         self.n_classes = spec.num_classes
-        # gradient ping-pong buffers (largest activation) + split-K slab workspace
-        gmax = max(int(l.out.numel()) for l in self.layers[:-1]) if len(self.layers) > 1 else 1
-        self.gbuf = [_bf16(gmax, device=dev), _bf16(gmax, device=dev)]
         self.dlogits = _bf16(batch, self.logits.shape[1], device=dev)
-        slab = max(getattr(l, "slab_elems", 0) for l in self.layers)
-        self.slab = torch.zeros(max(slab, 1), dtype=torch.float32, device=dev)
+        # overlap_backward: every weight gradient (+ its split-K reduce) runs on a side
+        # stream, concurrently with the data-gradient chain on the main stream (one
+        # input-gradient buffer and one slab region per layer, so the streams never share
+        # scratch).  Off by default: at B=65536 every kernel already fills the 256 CUs and
+        # concurrent kernels only time-slice (profiles/r1_overlap/); the serial plan is the
+        # same code with one slab.
+        self.overlap = overlap_backward and dev.type == "cuda"
+        self.dbuf: List[Optional[torch.Tensor]] = [None] + [torch.zeros_like(l.out, dtype=torch.bfloat16)
+                                                           for l in self.layers[:-1]]
+        sizes = [(getattr(l, "slab_elems", 0) + 3) // 4 * 4 for l in self.layers]
+        self.slab = torch.zeros(max(1, sum(sizes) if self.overlap else max(sizes)), dtype=torch.float32, device=dev)
+        self.slabs, off = [], 0
+        for n in sizes:
+            self.slabs.append(self.slab[off:off + n] if n else self.slab[:1])
+            off += n if self.overlap else 0
+        if self.overlap:
+            self.side = torch.cuda.Stream(device=dev)
+            self.ev_dy = [torch.cuda.Event() for _ in self.layers]
         self.stats = torch.zeros(8, dtype=torch.float32, device=dev)
         self.eval_stats = torch.zeros(8, dtype=torch.float32, device=dev)
         # softmax-CE per-block partials + ticket: deterministic loss / accuracy sums
@@ -344,22 +375,36 @@ class HipNet:
                              None, self.ce_work)
 
     def backward(self, nb: Optional[int] = None) -> None:
+        """Data-gradient chain on the current stream; each layer's weight gradient
+        forks to the side stream as soon as its dY exists (event), and grad-ready
+        hooks (DP all-reduce launches) are issued from the side stream so RCCL
+        waits on exactly that work.  Joins before returning."""
         nb = self.B if nb is None else nb
         dy = self.dlogits
-        k = 0
+        main = torch.cuda.current_stream(self.device) if self.overlap else None
+        if self.overlap:
+            self.side.wait_stream(main)
         for i in range(len(self.layers) - 1, -1, -1):
             lay = self.layers[i]
-            if i > 0:
-                nel = self.layers[i - 1].out.numel()
-                dx = self.gbuf[k][:nel].view(self.layers[i - 1].out.shape)
-                k ^= 1
-            else:
-                dx = None
-            lay.bwd(nb, dy, dx, self.slab)
+            dx = self.dbuf[i]
             if lay.has_params:
-                for h in self.grad_ready_hooks:
-                    h(lay.idx)
+                # the first layer has no data gradient: its weight gradient IS the tail of
+                # the critical path, so it runs on the main stream while the side drains
+                if self.overlap and i > 0:
+                    self.ev_dy[i].record(main)
+                    self.side.wait_event(self.ev_dy[i])
+                    with torch.cuda.stream(self.side):
+                        lay.bwd_weight(nb, dy, self.slabs[i])
+                        for h in self.grad_ready_hooks:
+                            h(lay.idx)
+                else:
+                    lay.bwd_weight(nb, dy, self.slabs[i])
+                    for h in self.grad_ready_hooks:
+                        h(lay.idx)
+            lay.bwd_data(nb, dy, dx)
             dy = dx
+        if self.overlap:
+            main.wait_stream(self.side)
 
     def update(self, grad_scale: float = 1.0, increment: bool = True, batch_for_stats: Optional[int] = None) -> None:
         self.fp.apply(self.opt, grad_scale)

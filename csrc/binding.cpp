@@ -255,6 +255,56 @@ void softmax_ce(Tensor logits, int64_t ldl, optional<Tensor> labels, int64_t B, 
          "softmax_ce");
 }
 
+bool mlp_head_supported(int64_t d0, int64_t ld1, int64_t ld2, int64_t ld3, int64_t n1, int64_t n2, int64_t nc,
+                        int64_t B) {
+  return mnistx::mlp_head_supported((int)d0, (int)ld1, (int)ld2, (int)ld3, (int)n1, (int)n2, (int)nc, (int)B);
+}
+
+// Fused LeNet-5 dense head.  x [>=nb, 400] bf16; w3t [128,416], w4t [96,128], w5t [16,96]
+// zero-padded transposed bf16 weights (FlatParams.bf16t_view); outputs h3 [nb,120], h4 [nb,88] bf16, logits [nb,16] fp32;
+// with dl: dl [nb,16], dh4 [nb,88], dh3 [nb,120], dx [nb,400] bf16.
+void mlp_head(Tensor x, Tensor w3t, Tensor b3, int64_t n1, Tensor w4t, Tensor b4, int64_t n2, Tensor w5t, Tensor b5,
+              int64_t nc, Tensor labels, int64_t nb, double scale, Tensor h3, Tensor h4, Tensor logits,
+              optional<Tensor> dl, optional<Tensor> dh4, optional<Tensor> dh3, optional<Tensor> dx, Tensor stats,
+              Tensor work) {
+  TORCH_CHECK(mnistx::mlp_head_supported(400, 120, 88, 16, (int)n1, (int)n2, (int)nc, (int)std::max<int64_t>(nb, 1)),
+              "mlp_head: unsupported geometry");
+  check(x, at::kBFloat16, nb * 400, "x");
+  check(w3t, at::kBFloat16, 128 * 416, "w3t");
+  check(w4t, at::kBFloat16, 96 * 128, "w4t");
+  check(w5t, at::kBFloat16, 16 * 96, "w5t");
+  check(b3, at::kFloat, n1, "b3");
+  check(b4, at::kFloat, n2, "b4");
+  check(b5, at::kFloat, nc, "b5");
+  check(labels, at::kInt, nb, "labels");
+  check(h3, at::kBFloat16, nb * 120, "h3");
+  check(h4, at::kBFloat16, nb * 88, "h4");
+  check(logits, at::kFloat, nb * 16, "logits");
+  check(stats, at::kFloat, 8, "stats");
+  check(work, at::kFloat, 4 * 1024 + 1, "work");
+  for (const Tensor* t : {&x, &w3t, &w4t, &w5t, &h3, &h4, &logits})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "mlp_head: operands must be 16-byte aligned");
+  mnistx::bf16_t *pdl = nullptr, *pdh4 = nullptr, *pdh3 = nullptr, *pdx = nullptr;
+  if (dl.has_value() && dl->defined()) {
+    TORCH_CHECK(dh4.has_value() && dh3.has_value() && dx.has_value(), "mlp_head: dl needs dh4, dh3, dx");
+    check(*dl, at::kBFloat16, nb * 16, "dl");
+    check(*dh4, at::kBFloat16, nb * 88, "dh4");
+    check(*dh3, at::kBFloat16, nb * 120, "dh3");
+    check(*dx, at::kBFloat16, nb * 400, "dx");
+    for (const Tensor* t : {&*dl, &*dh4, &*dh3, &*dx})
+      TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 8 == 0, "mlp_head: gradients must be 8-byte aligned");
+    pdl = BFm(*dl);
+    pdh4 = BFm(*dh4);
+    pdh3 = BFm(*dh3);
+    pdx = BFm(*dx);
+  }
+  hip_ok(mnistx::mlp_head(BF(x), BF(w3t), P<const float>(b3), (int)n1, BF(w4t), P<const float>(b4), (int)n2, BF(w5t),
+                          P<const float>(b5), (int)nc, P<const int32_t>(labels), (int)nb, (float)scale, BFm(h3),
+                          BFm(h4), P<float>(logits), pdl, pdh4, pdh3, pdx, P<float>(stats), P<float>(work),
+                          cur_stream()),
+         "mlp_head");
+}
+
 void splitk_reduce(Tensor slab, int64_t splits, int64_t M, int64_t N, int64_t G, int64_t Ipad, int64_t I, int64_t J,
                    int64_t bias_row, Tensor wdst, optional<Tensor> bdst, double scale) {
   check(slab, at::kFloat, splits * M * N, "slab");
@@ -272,8 +322,8 @@ void splitk_reduce(Tensor slab, int64_t splits, int64_t M, int64_t N, int64_t G,
          "splitk_reduce");
 }
 
-// segs: int64 tensor [nseg, 12] on CPU:
-//   off, n, G, I, J, Ip, Jp, bf_off, wd_bits(float32 as int), track_l2, 0, 0
+// segs: int64 tensor [nseg, 14] on CPU:
+//   off, n, G, I, J, Ip, Jp, bf_off, wd_bits(float32 as int), track_l2, bft_off, Jt, It, 0
 void fused_optimizer(Tensor params, Tensor grads, Tensor mom, Tensor ema, Tensor bf, Tensor segs, Tensor step,
                      double lr0, double decay_rate, int64_t decay_steps, double momentum, bool nesterov,
                      bool use_momentum, double grad_scale, double ema_max, optional<Tensor> l2) {
@@ -283,8 +333,8 @@ void fused_optimizer(Tensor params, Tensor grads, Tensor mom, Tensor ema, Tensor
   if (use_momentum) check(mom, at::kFloat, total, "mom");
   if (ema_max >= 0) check(ema, at::kFloat, total, "ema");
   check(step, at::kLong, 1, "step");
-  TORCH_CHECK(!segs.is_cuda() && segs.scalar_type() == at::kLong && segs.dim() == 2 && segs.size(1) == 12,
-              "segs: CPU int64 [n,12]");
+  TORCH_CHECK(!segs.is_cuda() && segs.scalar_type() == at::kLong && segs.dim() == 2 && segs.size(1) == 14,
+              "segs: CPU int64 [n,14]");
   const int nseg = (int)segs.size(0);
   std::vector<mnistx::OptSeg> sv(nseg);
   auto a = segs.accessor<int64_t, 2>();
@@ -303,11 +353,18 @@ void fused_optimizer(Tensor params, Tensor grads, Tensor mom, Tensor ema, Tensor
     int32_t wb = (int32_t)a[i][8];
     std::memcpy(&s.wd, &wb, 4);
     s.track_l2 = (int)a[i][9];
+    s.bft_off = a[i][10];
+    s.Jt = (int)a[i][11];
+    s.It = (int)a[i][12];
     TORCH_CHECK(s.off == expect_off, "segments must tile the flat buffer in order");
     TORCH_CHECK(s.n == (int64_t)s.G * s.I * s.J, "segment size mismatch");
     TORCH_CHECK(s.Ip >= s.I && s.Jp >= s.J, "padding");
     if (s.bf_off >= 0)
       TORCH_CHECK(s.bf_off + (int64_t)s.G * s.Ip * s.Jp <= bf.numel(), "bf16 copy out of range");
+    if (s.bft_off >= 0) {
+      TORCH_CHECK(s.bf_off >= 0 && s.G == 1 && s.Jt >= s.J && s.It >= s.I, "transposed copy geometry");
+      TORCH_CHECK(s.bft_off + (int64_t)s.Jt * s.It <= bf.numel(), "transposed bf16 copy out of range");
+    }
     if (s.track_l2 > max_l2) max_l2 = s.track_l2;
     expect_off += s.n;
   }
@@ -494,6 +551,12 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("scale"), py::arg("dlogits"), py::arg("ldd"), py::arg("stats"), py::arg("probs"),
         py::arg("work") = py::none());
   m.def("splitk_reduce", &splitk_reduce);
+  m.def("mlp_head_supported", &mlp_head_supported);
+  m.def("mlp_head", &mlp_head, py::arg("x"), py::arg("w3t"), py::arg("b3"), py::arg("n1"), py::arg("w4t"),
+        py::arg("b4"), py::arg("n2"), py::arg("w5t"), py::arg("b5"), py::arg("nc"), py::arg("labels"), py::arg("nb"),
+        py::arg("scale"), py::arg("h3"), py::arg("h4"), py::arg("logits"), py::arg("dl") = py::none(),
+        py::arg("dh4") = py::none(), py::arg("dh3") = py::none(), py::arg("dx") = py::none(), py::arg("stats"),
+        py::arg("work"));
   m.def("fused_optimizer", &fused_optimizer);
   m.def("finalize_step", &finalize_step);
   m.def("cast_f32_bf16_padded", &cast_f32_bf16_padded);

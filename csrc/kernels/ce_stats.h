@@ -1,0 +1,73 @@
+// Deterministic per-step cross-entropy statistics (loss sum, correct count, NaN
+// flag) shared by the softmax-CE kernel (misc.hip) and the fused dense head
+// (mlp_head.hip).  Each block reduces its threads in a fixed tree, writes one
+// partial to `work`, and the last block to finish (ticket counter at
+// work[4 * CE_MAXB]) combines the partials in block order: bitwise identical
+// results across runs and between hipGraph replay and eager execution.
+#pragma once
+#include "common.h"
+
+constexpr int CE_MAXB = 1024;  // max blocks per launch (work holds 4 floats per block + ticket)
+
+// Every thread of the block must call this (it synchronises the block).
+// With work == nullptr each block adds its partial atomically (order-dependent).
+template <int NW>
+DEV void ce_block_stats(float loss, float corr, float bad, float* __restrict__ stats, float* __restrict__ work) {
+  __shared__ float red[3][NW];
+  __shared__ int last;
+  loss = warp_sum(loss);
+  corr = warp_sum(corr);
+  bad = warp_sum(bad);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wave] = loss;
+    red[1][wave] = corr;
+    red[2][wave] = bad;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    loss = red[0][0];
+    corr = red[1][0];
+    bad = red[2][0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      loss += red[0][w];
+      corr += red[1][w];
+      bad += red[2][w];
+    }
+    if (!work) {
+      atomicAdd(&stats[0], loss);
+      atomicAdd(&stats[1], corr);
+      if (bad > 0.f) stats[2] = 1.f;
+    } else {
+      work[4 * blockIdx.x] = loss;
+      work[4 * blockIdx.x + 1] = corr;
+      work[4 * blockIdx.x + 2] = bad;
+      __threadfence();
+      unsigned* ticket = (unsigned*)(work + 4 * CE_MAXB);
+      last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    }
+  }
+  if (!work) return;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  // last block: combine the partials in block order (64 lanes of wave 0, fixed tree)
+  if (wave != 0) return;
+  const volatile float* wv = work;
+  float a = 0.f, b = 0.f, c = 0.f;
+  for (int i = lane; i < (int)gridDim.x; i += 64) {
+    a += wv[4 * i];
+    b += wv[4 * i + 1];
+    c += wv[4 * i + 2];
+  }
+  a = warp_sum(a);
+  b = warp_sum(b);
+  c = warp_sum(c);
+  if (lane == 0) {
+    stats[0] += a;
+    stats[1] += b;
+    if (c > 0.f) stats[2] = 1.f;
+    *(unsigned*)(work + 4 * CE_MAXB) = 0u;
+  }
+}

@@ -523,9 +523,11 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
   constexpr int OUTE = Q::NWIN * 8;                 // pooled elements per image (16-byte multiple)
   typedef float f32x16 __attribute__((ext_vector_type(16)));
   __shared__ __attribute__((aligned(16))) bf16_t tile[LDS];
-  // outputs of the block's image group are staged here and written as 16-byte vectors
-  __shared__ __attribute__((aligned(16))) bf16_t pout[IMGS * OUTE];
-  __shared__ __attribute__((aligned(16))) uint8_t aout[IMGS * OUTE];
+  // STAGE_OUT: outputs of the block's image group are staged in LDS and written as
+  // 16-byte vectors; otherwise each lane stores its (window, channel) directly
+  constexpr bool STAGE_OUT = true;
+  __shared__ __attribute__((aligned(16))) bf16_t pout[STAGE_OUT ? IMGS * OUTE : 8];
+  __shared__ __attribute__((aligned(16))) uint8_t aout[STAGE_OUT ? IMGS * OUTE : 16];
   static_assert((OUTE * 2) % 16 == 0 && OUTE % 16 == 0, "");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 31, h = lane >> 5;
@@ -573,8 +575,9 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
 #pragma unroll 1
     for (int im = 0; im < IMGS; ++im) {
       const bf16_t* timg = tile + im * Q::IMG_LDS;
-      bf16_t* pimg = pout + im * OUTE;
-      uint8_t* aimg = aout + im * OUTE;
+      if (!STAGE_OUT && img0 + im >= B) break;
+      bf16_t* pimg = STAGE_OUT ? pout + im * OUTE : pooled + (int64_t)(img0 + im) * OUTE;
+      uint8_t* aimg = STAGE_OUT ? aout + im * OUTE : arg + (int64_t)(img0 + im) * OUTE;
       for (int fm = wave; fm < Q::MFQ; fm += NTH / 64) {
         const int quad = min(fm * 16 + qw, Q::NQUAD - 1);
         const int ph = quad / Q::PQ, pq = quad - ph * Q::PQ;
@@ -610,13 +613,15 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
         }
       }
     }
-    __syncthreads();
-    // the group's outputs are contiguous in HBM: full 16-byte stores
-    const int nimg = min(IMGS, B - img0);
-    bf16_t* pg = pooled + (int64_t)img0 * OUTE;
-    uint8_t* ag = arg + (int64_t)img0 * OUTE;
-    for (int e = tid; e < nimg * OUTE / 8; e += NTH) *(u32x4*)(pg + 8 * e) = *(const u32x4*)(pout + 8 * e);
-    for (int e = tid; e < nimg * OUTE / 16; e += NTH) *(u32x4*)(ag + 16 * e) = *(const u32x4*)(aout + 16 * e);
+    if constexpr (STAGE_OUT) {
+      __syncthreads();
+      // the group's outputs are contiguous in HBM: full 16-byte stores
+      const int nimg = min(IMGS, B - img0);
+      bf16_t* pg = pooled + (int64_t)img0 * OUTE;
+      uint8_t* ag = arg + (int64_t)img0 * OUTE;
+      for (int e = tid; e < nimg * OUTE / 8; e += NTH) *(u32x4*)(pg + 8 * e) = *(const u32x4*)(pout + 8 * e);
+      for (int e = tid; e < nimg * OUTE / 16; e += NTH) *(u32x4*)(ag + 16 * e) = *(const u32x4*)(aout + 16 * e);
+    }
   }
 }
 

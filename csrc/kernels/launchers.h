@@ -78,6 +78,15 @@ hipError_t lrn_bwd(const bf16_t* x, const bf16_t* dy, int P, int C, int r, float
 // accuracy sums deterministic (per-block partials combined in block order)
 hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B, int NC, float scale,
                       bf16_t* dlogits, int ldd, float* stats, float* probs, float* work, hipStream_t st);
+// Fused LeNet-5 dense head (mlp_head.hip): fc3/fc4/fc5 + softmax-CE (+ with dl:
+// the data-gradient chain dlogits -> dh4 -> dh3 -> dx).  Writes h3, h4, logits
+// always; dl, dh4, dh3, dx when dl != nullptr.  Same work-buffer contract as softmax_ce.
+bool mlp_head_supported(int d0, int ld1, int ld2, int ld3, int n1, int n2, int nc, int B);
+// w3t / w4t / w5t: zero-padded W^T copies [128][416], [96][128], [16][96].
+hipError_t mlp_head(const bf16_t* x, const bf16_t* w3t, const float* b3, int n1, const bf16_t* w4t, const float* b4,
+                    int n2, const bf16_t* w5t, const float* b5, int nc, const int32_t* labels, int nb, float scale,
+                    bf16_t* h3, bf16_t* h4, float* logits, bf16_t* dl, bf16_t* dh4, bf16_t* dh3, bf16_t* dx,
+                    float* stats, float* work, hipStream_t st);
 // NOTE: many splits over a small output are pre-summed IN PLACE (the slab is scratch).
 hipError_t splitk_reduce(float* slab, int splits, int M, int N, int G, int Ipad, int I, int J,
                          int bias_row, float* wdst, float* bdst, float scale, hipStream_t st);
@@ -90,6 +99,8 @@ struct OptSeg {          // one trainable tensor inside the flat buffers
   int64_t bf_off;        // offset of the bf16 copy (-1: none)
   float wd;              // L2 weight decay (0: none)
   int track_l2;          // accumulate sum(w^2) into l2[seg]
+  int64_t bft_off;       // offset of a transposed bf16 copy [Jt][It] (G == 1; -1: none)
+  int Jt, It;
 };
 
 struct OptParams {

@@ -6,6 +6,7 @@
 // Reference ops replaced: SURVEY.md §2.3 N6-N14 (mnist_input.py:37-39,149-172,
 // 224-231,252-267,288-290).
 #include "common.h"
+#include "ce_stats.h"
 #include "launchers.h"
 
 #include <algorithm>
@@ -298,15 +299,12 @@ __global__ void softmax_ce_k(const float* __restrict__ logits, int ldl, const in
 // 16-byte bf16 stores.  Statistics: warp + block reduction, then either one
 // atomic per block or -- with a workspace -- per-block partials combined by the
 // last block to finish (ticket counter) in block order: bitwise deterministic.
-constexpr int CE_MAXB = 1024;
 template <int LD>
 __global__ __launch_bounds__(256) void softmax_ce_rows_k(const float* __restrict__ logits,
                                                          const int32_t* __restrict__ labels, int B, int NC,
                                                          float scale, bf16_t* __restrict__ dl,
                                                          float* __restrict__ stats, float* __restrict__ probs,
                                                          float* __restrict__ work) {
-  __shared__ float red[3][4];
-  __shared__ int last;
   float loss = 0.f, corr = 0.f, bad = 0.f;
   for (int row = blockIdx.x * 256 + threadIdx.x; row < B; row += gridDim.x * 256) {
     float l[LD];
@@ -358,56 +356,7 @@ __global__ __launch_bounds__(256) void softmax_ce_rows_k(const float* __restrict
       for (int c = 0; c < LD; ++c)
         if (c < NC) probs[(int64_t)row * NC + c] = e[c] * inv;
   }
-  if (!stats) return;
-  loss = warp_sum(loss);
-  corr = warp_sum(corr);
-  bad = warp_sum(bad);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) {
-    red[0][wave] = loss;
-    red[1][wave] = corr;
-    red[2][wave] = bad;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    loss = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
-    corr = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
-    bad = red[2][0] + red[2][1] + red[2][2] + red[2][3];
-    if (!work) {
-      atomicAdd(&stats[0], loss);
-      atomicAdd(&stats[1], corr);
-      if (bad > 0.f) stats[2] = 1.f;
-    } else {
-      work[4 * blockIdx.x] = loss;
-      work[4 * blockIdx.x + 1] = corr;
-      work[4 * blockIdx.x + 2] = bad;
-      __threadfence();
-      unsigned* ticket = (unsigned*)(work + 4 * CE_MAXB);
-      last = atomicAdd(ticket, 1u) == gridDim.x - 1;
-    }
-  }
-  if (!work) return;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  // last block: combine the partials in block order (64 lanes of wave 0, fixed tree)
-  if (wave != 0) return;
-  const volatile float* wv = work;
-  float a = 0.f, b = 0.f, c = 0.f;
-  for (int i = lane; i < (int)gridDim.x; i += 64) {
-    a += wv[4 * i];
-    b += wv[4 * i + 1];
-    c += wv[4 * i + 2];
-  }
-  a = warp_sum(a);
-  b = warp_sum(b);
-  c = warp_sum(c);
-  if (lane == 0) {
-    stats[0] += a;
-    stats[1] += b;
-    if (c > 0.f) stats[2] = 1.f;
-    *(unsigned*)(work + 4 * CE_MAXB) = 0u;
-  }
+  if (stats) ce_block_stats<4>(loss, corr, bad, stats, work);
 }
 
 // ------------------------------------------------------------------ split-K reduce
@@ -546,7 +495,9 @@ __global__ __launch_bounds__(TPB) void fused_opt_k(float* __restrict__ params, c
       const int gg = (int)(li / ij);
       const int64_t rem = li - gg * ij;
       const int ii = (int)(rem / sg.J), jj = (int)(rem - (int64_t)ii * sg.J);
-      bf[sg.bf_off + ((int64_t)gg * sg.Ip + ii) * sg.Jp + jj] = f2bf(p);
+      const bf16_t pb = f2bf(p);
+      bf[sg.bf_off + ((int64_t)gg * sg.Ip + ii) * sg.Jp + jj] = pb;
+      if (sg.bft_off >= 0) bf[sg.bft_off + (int64_t)jj * sg.It + ii] = pb;  // W^T copy (fused dense head)
     }
   }
   if (l2 && sg.track_l2) {

@@ -103,14 +103,14 @@ class DataParallel:
         """One DP step; ``timer`` (runtime/timers.PhaseTimer) records phase boundaries."""
         net = self.net
         if timer is None:
-            net.forward()
+            net.forward(defer_head=True)
             net.loss_and_grad()
             net.backward()
             self.sync_grads()
             net.update(grad_scale=1.0 / self.world)
             return
         timer.mark("start")
-        net.forward()
+        net.forward(defer_head=True)
         timer.mark("forward")
         net.loss_and_grad()
         timer.mark("loss")

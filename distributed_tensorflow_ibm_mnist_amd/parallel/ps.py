@@ -294,7 +294,7 @@ class PSWorkerReplica:
     def step(self) -> None:
         net = self.net
         self.loader.next()
-        net.forward()
+        net.forward(defer_head=True)
         net.loss_and_grad()
         net.backward()
         net.finalize(net.B, increment=False)

@@ -256,7 +256,8 @@ class HipNet:
     """One model replica on one GPU: buffers + kernels for fwd / bwd / update."""
 
     def __init__(self, spec: ModelSpec, batch: int, device, init: Dict[str, torch.Tensor],
-                 opt: Optional[OptConfig] = None, fuse_convpool: bool = True, overlap_backward: bool = False):
+                 opt: Optional[OptConfig] = None, fuse_convpool: bool = True, overlap_backward: bool = False,
+                 fuse_head: bool = True):
         dev = torch.device(device)
         self.spec, self.B, self.device = spec, batch, dev
         self.opt = opt or OptConfig()
@@ -340,6 +341,40 @@ class HipNet:
         self.loss_ema = torch.zeros(3 * len(self.loss_names), dtype=torch.float32, device=dev)
         self.grad_ready_hooks: List[Callable[[int], None]] = []
         self.idx_buf: Optional[torch.Tensor] = None
+        # fused dense head (mlp_head.hip): index of its first layer, or None
+        self.head: Optional[int] = self._find_head() if (fuse_head and dev.type == "cuda") else None
+        self._head_pending: Optional[int] = None   # nb of a deferred head (forward(defer_head=True))
+        self._head_grads = False                   # loss_and_grad already produced the head's dgrads
+
+    def _find_head(self) -> Optional[int]:
+        """LeNet-5's fc3 -> fc4 -> fc5 tail (400 -> 120 -> 84 -> 10 with ReLUs on the
+        hidden layers) runs as ONE kernel with softmax-CE and its data gradients."""
+        if len(self.layers) < 4:
+            return None
+        i = len(self.layers) - 3
+        l3, l4, l5 = self.layers[i:]
+        if not all(isinstance(l, DenseLayer) for l in (l3, l4, l5)):
+            return None
+        dims = (l3.Dp, l3.Np, l4.Dp, l4.Np, l5.Dp, l5.Np)
+        if dims != (400, 120, 120, 88, 88, 16) or l3.in_relu or not (l3.spec.relu and l4.spec.relu) or l5.spec.relu:
+            return None
+        if not kernels().mlp_head_supported(400, 120, 88, 16, l3.spec.dout, l4.spec.dout, l5.spec.dout, self.B):
+            return None
+        # the kernel stages transposed, tile-padded weight copies (W^T rows = output units)
+        self.fp.enable_transposed({l3.wname: (128, 416), l4.wname: (96, 128), l5.wname: (16, 96)})
+        return i
+
+    def _run_head(self, nb: int, scale: float, grads: bool, stats: torch.Tensor) -> None:
+        i = self.head
+        l3, l4, l5 = self.layers[i:]
+        fp = self.fp
+        kernels().mlp_head(l3.x, fp.bf16t_view(l3.wname), fp.param_view(l3.bname), l3.spec.dout,
+                           fp.bf16t_view(l4.wname), fp.param_view(l4.bname), l4.spec.dout,
+                           fp.bf16t_view(l5.wname), fp.param_view(l5.bname), l5.spec.dout,
+                           self.labels, nb, scale, l3.out, l4.out, l5.out,
+                           dl=self.dlogits if grads else None, dh4=self.dbuf[i + 2] if grads else None,
+                           dh3=self.dbuf[i + 1] if grads else None, dx=self.dbuf[i] if grads else None,
+                           stats=stats, work=self.ce_work)
 
     def bind_u8_input(self, images_u8: torch.Tensor) -> bool:
         """Training steps read the uint8 dataset [n, H*W] directly through ``idx_buf``
@@ -357,19 +392,29 @@ class HipNet:
         return True
 
     # ------------------------------------------------------------------ step parts
-    def forward(self, nb: Optional[int] = None, from_x0: bool = False) -> torch.Tensor:
+    def forward(self, nb: Optional[int] = None, from_x0: bool = False, defer_head: bool = False) -> torch.Tensor:
         """Training forward reads the bound uint8 source when there is one;
-        ``from_x0`` forces the bf16 ``x0`` buffer (eval / inference / tests)."""
+        ``from_x0`` forces the bf16 ``x0`` buffer (eval / inference / tests).
+        ``defer_head``: a fused dense head is left to ``loss_and_grad`` (which then
+        runs head forward + softmax-CE + head data gradients as one kernel), so the
+        logits are only valid after it."""
         nb = self.B if nb is None else nb
         first = self.layers[0]
         if isinstance(first, ConvPoolLayer):
             first.use_u8 = first.u8 is not None and not from_x0
-        for lay in self.layers:
+        stop = self.head if (defer_head and self.head is not None) else len(self.layers)
+        for lay in self.layers[:stop]:
             lay.fwd(nb)
+        self._head_pending = nb if stop < len(self.layers) else None
         return self.logits
 
     def loss_and_grad(self, nb: Optional[int] = None, scale: Optional[float] = None) -> None:
         nb = self.B if nb is None else nb
+        if self._head_pending is not None:
+            assert self._head_pending == nb, "loss_and_grad batch differs from the deferred forward"
+            self._run_head(nb, (1.0 / nb) if scale is None else scale, True, self.stats)
+            self._head_pending, self._head_grads = None, True
+            return
         kernels().softmax_ce(self.logits, self.logits.shape[1], self.labels, nb, self.n_classes,
                              (1.0 / nb) if scale is None else scale, self.dlogits, self.logits.shape[1], self.stats,
                              None, self.ce_work)
@@ -401,8 +446,10 @@ class HipNet:
                     lay.bwd_weight(nb, dy, self.slabs[i])
                     for h in self.grad_ready_hooks:
                         h(lay.idx)
-            lay.bwd_data(nb, dy, dx)
+            if not (self._head_grads and i >= self.head):   # the fused head wrote these already
+                lay.bwd_data(nb, dy, dx)
             dy = dx
+        self._head_grads = False
         if self.overlap:
             main.wait_stream(self.side)
 
@@ -417,7 +464,7 @@ class HipNet:
                                 self.loss_ema, len(self.loss_names), batch, increment)
 
     def train_step(self, grad_scale: float = 1.0) -> None:
-        self.forward()
+        self.forward(defer_head=True)
         self.loss_and_grad()
         self.backward()
         self.update(grad_scale)
@@ -425,8 +472,12 @@ class HipNet:
     # ------------------------------------------------------------------ eval
     def eval_batch(self, nb: int, stats: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Forward only on x0[:nb] / labels[:nb]; accumulates loss/correct into stats."""
-        self.forward(nb, from_x0=True)
         st = self.eval_stats if stats is None else stats
+        self.forward(nb, from_x0=True, defer_head=True)
+        if self._head_pending is not None:
+            self._run_head(nb, 1.0, False, st)
+            self._head_pending = None
+            return st
         kernels().softmax_ce(self.logits, self.logits.shape[1], self.labels, nb, self.n_classes, 1.0, None,
                              self.logits.shape[1], st, None, self.ce_work)
         return st

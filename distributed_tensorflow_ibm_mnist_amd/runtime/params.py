@@ -83,11 +83,37 @@ class FlatParams:
         self.l2 = torch.zeros(max(len(self.wd_entries), 1), dtype=torch.float32, device=device)
         self.wds = torch.tensor([float(e.wd) for e in self.wd_entries] or [0.0], dtype=torch.float32,
                                 device=device)
+        # name -> (offset in bf16, Jt, It): optional transposed bf16 copies W^T [Jt][It]
+        self.bft: Dict[str, Tuple[int, int, int]] = {}
+        self._build_segs()
+
+    def _build_segs(self) -> None:
         rows = []
-        for e in entries:
+        for e in self.entries:
+            t = self.bft.get(e.name)
             rows.append([e.off, e.n, e.G, e.I, e.J, e.Ip, e.Jp, e.bf_off, _f32_bits(e.wd or 0.0),
-                         e.l2_index + 1, 0, 0])
+                         e.l2_index + 1, t[0] if t else -1, t[1] if t else 0, t[2] if t else 0, 0])
         self.segs = torch.tensor(rows, dtype=torch.int64)
+
+    def enable_transposed(self, tdims: Dict[str, Tuple[int, int]]) -> None:
+        """Also keep a transposed, zero-padded bf16 copy W^T [Jt][It] of these 2-D
+        weights, rewritten by every optimizer step (the fused dense head stages
+        them into LDS with straight 16-byte copies instead of transposing)."""
+        off = (self.bf16.numel() + 7) // 8 * 8
+        for name, (Jt, It) in tdims.items():
+            e = self.by_name[name]
+            assert e.G == 1 and Jt >= e.J and It >= e.I, name
+            self.bft[name] = (off, int(Jt), int(It))
+            off = (off + Jt * It + 7) // 8 * 8
+        grown = torch.zeros(off, dtype=torch.bfloat16, device=self.device)
+        grown[:self.bf16.numel()].copy_(self.bf16)
+        self.bf16 = grown
+        self._build_segs()
+        self.refresh_bf16()
+
+    def bf16t_view(self, name: str) -> torch.Tensor:
+        off, Jt, It = self.bft[name]
+        return self.bf16[off:off + Jt * It].view(Jt, It)
 
     # -- construction -----------------------------------------------------
     @classmethod
@@ -179,6 +205,10 @@ class FlatParams:
             if e.bf_off >= 0:
                 K.cast_f32_bf16_padded(self.param_view(e.name).contiguous(), self.bf16[e.bf_off:], e.G, e.I, e.J,
                                        e.Ip, e.Jp)
+        with torch.no_grad():
+            for name in self.bft:
+                e = self.by_name[name]
+                self.bf16t_view(name)[:e.J, :e.I].copy_(self.param_view(name).reshape(e.I, e.J).t())
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
         return {e.name: self.param_view(e.name).detach().cpu().clone() for e in self.entries}

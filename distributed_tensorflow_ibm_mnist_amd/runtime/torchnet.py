@@ -76,7 +76,7 @@ class TorchNet:
     def _params(self, leaf: torch.Tensor) -> Dict[str, torch.Tensor]:
         return {e.name: leaf[e.off:e.off + e.n].view(e.shape) for e in self.fp.entries}
 
-    def forward(self, nb: Optional[int] = None, grad: bool = True) -> torch.Tensor:
+    def forward(self, nb: Optional[int] = None, grad: bool = True, defer_head: bool = False) -> torch.Tensor:
         nb = self.B if nb is None else nb
         leaf = self.fp.params.detach().requires_grad_(grad)
         self._leaf = leaf

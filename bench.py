@@ -39,7 +39,8 @@ def parse():
     ap.add_argument("--in_channels", type=int, default=1)
     ap.add_argument("--impl", default="hip", choices=["hip", "torch"],
                     help="hip = our CDNA4 kernels; torch = PyTorch-ROCm baseline (MIOpen/hipBLASLt, bf16 autocast)")
-    ap.add_argument("--bucket_mb", type=float, default=4.0)
+    ap.add_argument("--bucket_mb", type=float, default=0.125,
+                    help="gradient bucket cap (MB); every bucket but the last overlaps backward")
     ap.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph (hip impl, N=1)")
     ap.add_argument("--optimizer", default="momentum", choices=["sgd", "momentum", "nesterov"])
     ap.add_argument("--lr", type=float, default=0.01)

@@ -305,21 +305,47 @@ void mlp_head(Tensor x, Tensor w3t, Tensor b3, int64_t n1, Tensor w4t, Tensor b4
          "mlp_head");
 }
 
-void splitk_reduce(Tensor slab, int64_t splits, int64_t M, int64_t N, int64_t G, int64_t Ipad, int64_t I, int64_t J,
-                   int64_t bias_row, Tensor wdst, optional<Tensor> bdst, double scale) {
+mnistx::RedSpec red_spec(Tensor slab, int64_t splits, int64_t M, int64_t N, int64_t G, int64_t Ipad, int64_t I,
+                         int64_t J, int64_t bias_row, Tensor wdst, const Tensor* bdst, double scale) {
   check(slab, at::kFloat, splits * M * N, "slab");
   TORCH_CHECK(I <= Ipad && J <= N && G * Ipad <= M, "reduce geometry");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(slab.data_ptr()) % 16 == 0, "slab must be 16-byte aligned");
   check(wdst, at::kFloat, G * I * J, "wdst");
   float* b = nullptr;
-  if (bdst.has_value() && bdst->defined()) {
+  if (bdst != nullptr && bdst->defined() && bdst->numel() > 0) {
     TORCH_CHECK(bias_row >= 0 && bias_row < M, "bias_row");
     check(*bdst, at::kFloat, J, "bdst");
     b = P<float>(*bdst);
   }
-  hip_ok(mnistx::splitk_reduce(P<float>(slab), (int)splits, (int)M, (int)N, (int)G, (int)Ipad, (int)I, (int)J,
-                               (int)bias_row, P<float>(wdst), b, (float)scale, cur_stream()),
-         "splitk_reduce");
+  return mnistx::RedSpec{P<float>(slab), P<float>(wdst), b, (int)splits, (int)M, (int)N, (int)G, (int)Ipad, (int)I,
+                         (int)J, (int)bias_row, (float)scale};
+}
+
+void splitk_reduce(Tensor slab, int64_t splits, int64_t M, int64_t N, int64_t G, int64_t Ipad, int64_t I, int64_t J,
+                   int64_t bias_row, Tensor wdst, optional<Tensor> bdst, double scale) {
+  const Tensor* bp = (bdst.has_value() && bdst->defined()) ? &*bdst : nullptr;
+  const mnistx::RedSpec r = red_spec(slab, splits, M, N, G, Ipad, I, J, bias_row, wdst, bp, scale);
+  hip_ok(mnistx::splitk_reduce_multi(&r, 1, cur_stream()), "splitk_reduce");
+}
+
+// Several split-K slabs reduced by one launch per pass.  geo: int64 [n, 8] on CPU =
+// (splits, M, N, G, Ipad, I, J, bias_row) per tensor; bdsts[i] empty = no bias.
+void splitk_reduce_multi(std::vector<Tensor> slabs, std::vector<Tensor> wdsts, std::vector<Tensor> bdsts, Tensor geo,
+                         std::vector<double> scales) {
+  const int64_t n = (int64_t)slabs.size();
+  TORCH_CHECK((int64_t)wdsts.size() == n && (int64_t)bdsts.size() == n && (int64_t)scales.size() == n,
+              "splitk_reduce_multi: list lengths differ");
+  TORCH_CHECK(geo.device().is_cpu() && geo.scalar_type() == at::kLong && geo.dim() == 2 && geo.size(0) == n &&
+                  geo.size(1) == 8 && geo.is_contiguous(),
+              "splitk_reduce_multi: geo must be a contiguous CPU int64 [n, 8] tensor");
+  const int64_t* g = geo.data_ptr<int64_t>();
+  std::vector<mnistx::RedSpec> specs;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t* r = g + 8 * i;
+    specs.push_back(red_spec(slabs[i], r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7], wdsts[i], &bdsts[i],
+                             scales[i]));
+  }
+  hip_ok(mnistx::splitk_reduce_multi(specs.data(), (int)n, cur_stream()), "splitk_reduce_multi");
 }
 
 // segs: int64 tensor [nseg, 14] on CPU:
@@ -551,6 +577,7 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("scale"), py::arg("dlogits"), py::arg("ldd"), py::arg("stats"), py::arg("probs"),
         py::arg("work") = py::none());
   m.def("splitk_reduce", &splitk_reduce);
+  m.def("splitk_reduce_multi", &splitk_reduce_multi);
   m.def("mlp_head_supported", &mlp_head_supported);
   m.def("mlp_head", &mlp_head, py::arg("x"), py::arg("w3t"), py::arg("b3"), py::arg("n1"), py::arg("w4t"),
         py::arg("b4"), py::arg("n2"), py::arg("w5t"), py::arg("b5"), py::arg("nc"), py::arg("labels"), py::arg("nb"),

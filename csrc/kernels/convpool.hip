@@ -286,7 +286,13 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_k(const XSrc x, const bf16_t
                                                       const float* __restrict__ bias, int bias_n, int B,
                                                       bf16_t* __restrict__ pooled, uint8_t* __restrict__ arg) {
   constexpr int LDS = (IMGS * G::IMG_LDS + 7) / 8 * 8;
+  constexpr int OUTE = G::NWIN * G::COUT;              // pooled elements per image
+  // small outputs (LeNet conv2: 400 per image) are staged in LDS and leave as 16-byte
+  // vectors; wide ones (32 channels) keep direct 32-byte-per-row stores (LDS budget)
+  constexpr bool STAGE = IMGS * OUTE * 3 <= 16384 && OUTE % 16 == 0;
   __shared__ __attribute__((aligned(16))) bf16_t tile[LDS];
+  __shared__ __attribute__((aligned(16))) bf16_t pout[STAGE ? IMGS * OUTE : 8];
+  __shared__ __attribute__((aligned(16))) uint8_t aout[STAGE ? IMGS * OUTE : 16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   lds_zero<LDS>(tile, tid);
@@ -372,9 +378,9 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_k(const XSrc x, const bf16_t
         for (int nf = 0; nf < G::NF; ++nf) acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[s][nf], acc[nf], 0, 0, 0);
       }
       const int win = fm * 4 + g;
-      if (win < G::NWIN && img0 + im < B) {
-        bf16_t* pimg = pooled + (int64_t)(img0 + im) * (G::NWIN * G::COUT);
-        uint8_t* aimg = arg + (int64_t)(img0 + im) * (G::NWIN * G::COUT);
+      if (win < G::NWIN && (STAGE || img0 + im < B)) {
+        bf16_t* pimg = STAGE ? pout + im * OUTE : pooled + (int64_t)(img0 + im) * OUTE;
+        uint8_t* aimg = STAGE ? aout + im * OUTE : arg + (int64_t)(img0 + im) * OUTE;
 #pragma unroll
         for (int nf = 0; nf < G::NF; ++nf) {
           const int n = nf * 16 + li;
@@ -389,6 +395,14 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_k(const XSrc x, const bf16_t
           }
         }
       }
+    }
+    if constexpr (STAGE) {
+      __syncthreads();
+      const int nimg = min(IMGS, B - img0);
+      bf16_t* pg = pooled + (int64_t)img0 * OUTE;
+      uint8_t* ag = arg + (int64_t)img0 * OUTE;
+      for (int e = tid; e < nimg * OUTE / 8; e += NTH) *(u32x4*)(pg + 8 * e) = *(const u32x4*)(pout + 8 * e);
+      for (int e = tid; e < nimg * OUTE / 16; e += NTH) *(u32x4*)(ag + 16 * e) = *(const u32x4*)(aout + 16 * e);
     }
   }
 }
@@ -917,7 +931,10 @@ __global__ __launch_bounds__(NTH) void convpool_dgrad_pair_k(const bf16_t* __res
   constexpr int NWC = G::NWIN * G::COUT;
   static_assert((IMGS * DT) % 8 == 0, "");
   static_assert(2 * 7 + KWQ - 1 < RSE / DPS, "padding pair's patch row stays inside the row stride");
+  constexpr int OUTE = G::H * G::W * 8;              // dx elements per image
+  static_assert(OUTE % 8 == 0, "");
   __shared__ __attribute__((aligned(16))) bf16_t dyt[IMGS * DT];
+  __shared__ __attribute__((aligned(16))) bf16_t outs[IMGS * OUTE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int ci = li & 7, sx = li >> 3;
@@ -932,12 +949,10 @@ __global__ __launch_bounds__(NTH) void convpool_dgrad_pair_k(const bf16_t* __res
     dtap[s] = tp < NTAP ? kh * RSE + kwq * DPS + 8 * (g & 1) : 0;
     const int kw = kwq - sx;
     const bool valid = tp < NTAP && kw >= 0 && kw < G::KS;
-    const int tap = (G::KS - 1 - kh) * G::KS + (G::KS - 1 - kw);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int co = 8 * (g & 1) + j;
-      bw[s][j] = as_bf(valid ? w[(tap * G::CIN + ci) * G::COUT + co] : (bf16_t)0);
-    }
+    const int tap = valid ? (G::KS - 1 - kh) * G::KS + (G::KS - 1 - kw) : 0;
+    // the 8 co of one (tap, ci) are contiguous: one 16-byte load, zeroed for padded taps
+    const u32x4 v = *(const u32x4*)(w + (tap * G::CIN + ci) * G::COUT + 8 * (g & 1));
+    bw[s] = __builtin_bit_cast(bf16x8, valid ? v : u32x4{0u, 0u, 0u, 0u});
   }
   const int stride = gridDim.x * IMGS;
   DYStage<G, IMGS> ys;
@@ -967,29 +982,30 @@ __global__ __launch_bounds__(NTH) void convpool_dgrad_pair_k(const bf16_t* __res
     }
     __syncthreads();
     if (img0 + stride < B) ys.load(dP, arg, img0 + stride, B, tid);
-#pragma unroll 1
-    for (int im = 0; im < IMGS; ++im) {
-      const bool img_ok = img0 + im < B;
-      bf16_t* dimg = dx + (int64_t)(img0 + im) * (G::H * G::W * 8);
-      for (int mf = wave; mf < MFD; mf += NTH / 64) {
-        const bf16_t* tb = dyt + im * DT + (2 * mf + (li >> 3)) * RSE + 2 * (li & 7) * DPS;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // the group's 2 x MFD fragments are dealt over the 4 waves together (balance)
+    for (int f = wave; f < IMGS * MFD; f += NTH / 64) {
+      const int im = f / MFD, mf = f - im * MFD;
+      const bf16_t* tb = dyt + im * DT + (2 * mf + (li >> 3)) * RSE + 2 * (li & 7) * DPS;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < KSD; ++s) {
-          const bf16x8 a = __builtin_bit_cast(bf16x8, *(const u32x4*)(tb + dtap[s]));
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[s], acc, 0, 0, 0);
-        }
-        // accumulator rows 4g + r: image row 2mf + g/2, pair jr = 4(g&1) + r
-        if (img_ok) {
-          const int ih = 2 * mf + (g >> 1);
+      for (int s = 0; s < KSD; ++s) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, *(const u32x4*)(tb + dtap[s]));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[s], acc, 0, 0, 0);
+      }
+      // accumulator rows 4g + r: image row 2mf + g/2, pair jr = 4(g&1) + r -> LDS staging
+      const int ih = 2 * mf + (g >> 1);
+      bf16_t* oimg = outs + im * OUTE;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int jr = 4 * (g & 1) + r;
-            if (2 * jr < G::W) dimg[(ih * G::W + 2 * jr + sx) * 8 + ci] = f2bf(acc[r]);
-          }
-        }
+      for (int r = 0; r < 4; ++r) {
+        const int jr = 4 * (g & 1) + r;
+        if (2 * jr < G::W) oimg[(ih * G::W + 2 * jr + sx) * 8 + ci] = f2bf(acc[r]);
       }
     }
+    __syncthreads();
+    // the group's dx images are contiguous in HBM: 16-byte stores
+    const int nimg = min(IMGS, B - img0);
+    bf16_t* dg = dx + (int64_t)img0 * OUTE;
+    for (int e = tid; e < nimg * OUTE / 8; e += NTH) *(u32x4*)(dg + 8 * e) = *(const u32x4*)(outs + 8 * e);
   }
 }
 

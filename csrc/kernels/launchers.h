@@ -90,6 +90,16 @@ hipError_t mlp_head(const bf16_t* x, const bf16_t* w3t, const float* b3, int n1,
 // NOTE: many splits over a small output are pre-summed IN PLACE (the slab is scratch).
 hipError_t splitk_reduce(float* slab, int splits, int M, int N, int G, int Ipad, int I, int J,
                          int bias_row, float* wdst, float* bdst, float scale, hipStream_t st);
+// Several layers' slabs in one launch per pass (descriptors are copied into the
+// kernel arguments, so the call is hipGraph-capturable).
+struct RedSpec {
+  float* slab;
+  float* wdst;
+  float* bdst;           // nullptr: no bias row
+  int splits, M, N, G, Ipad, I, J, bias_row;
+  float scale;
+};
+hipError_t splitk_reduce_multi(const RedSpec* specs, int n, hipStream_t st);
 
 struct OptSeg {          // one trainable tensor inside the flat buffers
   int64_t off;           // offset in the flat fp32 buffers

@@ -392,23 +392,50 @@ __global__ void splitk_reduce_k(const float* __restrict__ slab, int S, int M, in
   }
 }
 
-// Coalesced variant (N % 4 == 0): each lane owns 4 consecutive slab columns of one
-// row (one 16-byte load per split), the 4 waves of a block take every 4th split,
-// and the 4 partial sums are combined in a fixed order (deterministic).
-// Splits z*zstride, z < S, are summed (zstride > 1 after splitk_partial4_k).
-__global__ __launch_bounds__(256) void splitk_reduce4_k(const float* __restrict__ slab, int S, int zstride, int M,
-                                                        int N, int G, int Ipad, int I, int J, int bias_row,
-                                                        float* __restrict__ wdst, float* __restrict__ bdst,
-                                                        float scale) {
+// Coalesced variant (N % 4 == 0), multi-tensor: ONE launch reduces the split-K
+// slabs of several layers (RedTable, block ranges per descriptor), so a backward
+// pass pays one reduce launch per gradient bucket instead of two per layer.
+// Each lane owns 4 consecutive slab columns of one row (one 16-byte load per
+// split), the 4 waves of a block take every 4th split, and the 4 partial sums
+// are combined in a fixed order (deterministic).  Splits z*zstride, z < S, are
+// summed (zstride > 1 after the partial pass).
+constexpr int RED_CHUNK = 64;
+constexpr int MAXRED = 8;
+struct RedDesc {
+  float* slab;
+  float* wdst;
+  float* bdst;
+  int64_t nq;        // M * N / 4 quads per split
+  int S, M, N, G, Ipad, I, J, bias_row;
+  int qb, sb;        // reduce blocks; partial-pass split blocks (0 = no partial pass)
+  float scale;
+};
+struct RedTable {
+  RedDesc d[MAXRED];
+  int pblk0[MAXRED + 1];  // partial-pass block prefix
+  int rblk0[MAXRED + 1];  // reduce-pass block prefix
+  int n;
+};
+
+DEV int red_find(const int* blk0, int n, int b) {
+  int k = 0;
+  for (int i = 1; i < n; ++i) k = b >= blk0[i] ? i : k;
+  return k;
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce4_k(RedTable tab) {
   __shared__ f32x4 part[4][64];
+  const int k = red_find(tab.rblk0, tab.n, blockIdx.x);
+  const RedDesc& D = tab.d[k];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int NQ = N >> 2;
-  const int64_t nq = (int64_t)M * NQ;
-  const int64_t qd = (int64_t)blockIdx.x * 64 + lane;
+  const int NQ = D.N >> 2;
+  const int64_t nq = D.nq;
+  const int64_t qd = (int64_t)(blockIdx.x - tab.rblk0[k]) * 64 + lane;
+  const int S = D.sb ? D.sb : D.S;
+  const int64_t zs = (int64_t)(D.sb ? RED_CHUNK : 1) * nq;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (qd < nq) {
-    const f32x4* p = (const f32x4*)slab + qd;
-    const int64_t zs = (int64_t)zstride * nq;
+    const f32x4* p = (const f32x4*)D.slab + qd;
     int z = wave;
     for (; z + 12 < S; z += 16) {
       const f32x4 a = p[z * zs], b = p[(z + 4) * zs];
@@ -425,19 +452,52 @@ __global__ __launch_bounds__(256) void splitk_reduce4_k(const float* __restrict_
   if (wave != 0 || qd >= nq) return;
   const f32x4 t = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
   const int row = (int)(qd / NQ), j0 = (int)(qd - (int64_t)row * NQ) * 4;
-  if (row == bias_row) {
-    if (bdst)
+  if (row == D.bias_row) {
+    if (D.bdst)
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj)
-        if (j0 + jj < J) bdst[j0 + jj] = t[jj] * scale;
+        if (j0 + jj < D.J) D.bdst[j0 + jj] = t[jj] * D.scale;
     return;
   }
-  const int g = row / Ipad, i = row - g * Ipad;
-  if (g >= G || i >= I) return;
-  float* d = wdst + ((int64_t)g * I + i) * J;
+  const int g = row / D.Ipad, i = row - g * D.Ipad;
+  if (g >= D.G || i >= D.I) return;
+  float* d = D.wdst + ((int64_t)g * D.I + i) * D.J;
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj)
-    if (j0 + jj < J) d[j0 + jj] = t[jj] * scale;
+    if (j0 + jj < D.J) d[j0 + jj] = t[jj] * D.scale;
+}
+
+// First pass for many splits over a small output: block (q, s) of a descriptor
+// sums splits [64 s, 64 s + 64) of its 64 quads and stores the sum IN PLACE in
+// split 64 s (only this block reads or writes that range), so the reduce pass
+// has S/64 splits.
+__global__ __launch_bounds__(256) void splitk_partial4_k(RedTable tab) {
+  __shared__ f32x4 part[4][64];
+  const int k = red_find(tab.pblk0, tab.n, blockIdx.x);
+  const RedDesc& D = tab.d[k];
+  const int local = blockIdx.x - tab.pblk0[k];
+  const int qblk = local % D.qb, sblk = local / D.qb;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t nq = D.nq;
+  const int64_t qd = (int64_t)qblk * 64 + lane;
+  const int z0 = sblk * RED_CHUNK, z1 = min(D.S, z0 + RED_CHUNK);
+  f32x4* p = (f32x4*)D.slab + qd;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (qd < nq) {
+    // all 16 loads in flight at once (a dependent chain was latency-bound), summed in order
+    constexpr int PER = RED_CHUNK / 4;
+    f32x4 v[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int z = z0 + wave + 4 * u;
+      v[u] = z < z1 ? p[(int64_t)z * nq] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) acc += v[u];
+  }
+  part[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && qd < nq) p[(int64_t)z0 * nq] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
 }
 
 // ------------------------------------------------------------------ K9 fused optimizer
@@ -635,44 +695,60 @@ hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B
   return hipGetLastError();
 }
 
-// First pass for many splits over a small output: block (qb, sb) sums splits
-// [64 sb, 64 sb + 64) of its 64 quads and stores the sum IN PLACE in split 64 sb
-// (only this block reads or writes that range), so pass 2 has S/64 splits.
-constexpr int RED_CHUNK = 64;
-__global__ __launch_bounds__(256) void splitk_partial4_k(float* __restrict__ slab, int S, int64_t nq) {
-  __shared__ f32x4 part[4][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t qd = (int64_t)blockIdx.x * 64 + lane;
-  const int z0 = blockIdx.y * RED_CHUNK, z1 = min(S, z0 + RED_CHUNK);
-  f32x4* p = (f32x4*)slab + qd;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  if (qd < nq)
-    for (int z = z0 + wave; z < z1; z += 4) acc += p[(int64_t)z * nq];
-  part[wave][lane] = acc;
-  __syncthreads();
-  if (wave == 0 && qd < nq) p[(int64_t)z0 * nq] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+hipError_t splitk_reduce_multi(const RedSpec* specs, int n, hipStream_t st) {
+  if (n < 1) return hipSuccess;
+  bool vec = true;
+  for (int i = 0; i < n; ++i) vec = vec && specs[i].N % 4 == 0 && specs[i].splits > 1;
+  if (!vec) {  // generic path, one launch per tensor
+    for (int i = 0; i < n; ++i) {
+      const RedSpec& r = specs[i];
+      const int64_t total = (int64_t)r.G * r.I * r.J + (r.bdst ? r.J : 0);
+      hipLaunchKernelGGL(splitk_reduce_k, dim3(nblocks(total, TPB, 8192)), dim3(TPB), 0, st, r.slab, r.splits, r.M,
+                         r.N, r.G, r.Ipad, r.I, r.J, r.bias_row, r.wdst, r.bdst, r.scale);
+    }
+    return hipGetLastError();
+  }
+  for (int i0 = 0; i0 < n; i0 += MAXRED) {
+    RedTable tab;
+    tab.n = std::min(MAXRED, n - i0);
+    int pb = 0, rb = 0;
+    for (int i = 0; i < tab.n; ++i) {
+      const RedSpec& r = specs[i0 + i];
+      RedDesc& D = tab.d[i];
+      D.slab = r.slab;
+      D.wdst = r.wdst;
+      D.bdst = r.bdst;
+      D.nq = (int64_t)r.M * (r.N / 4);
+      D.S = r.splits;
+      D.M = r.M;
+      D.N = r.N;
+      D.G = r.G;
+      D.Ipad = r.Ipad;
+      D.I = r.I;
+      D.J = r.J;
+      D.bias_row = r.bias_row;
+      D.scale = r.scale;
+      D.qb = (int)((D.nq + 63) / 64);
+      D.sb = (D.S > RED_CHUNK && D.qb < 512) ? (D.S + RED_CHUNK - 1) / RED_CHUNK : 0;
+      tab.pblk0[i] = pb;
+      tab.rblk0[i] = rb;
+      pb += D.sb ? D.qb * D.sb : 0;
+      rb += D.qb;
+    }
+    for (int i = tab.n; i <= MAXRED; ++i) {
+      tab.pblk0[i] = pb;
+      tab.rblk0[i] = rb;
+    }
+    if (pb > 0) hipLaunchKernelGGL(splitk_partial4_k, dim3(pb), dim3(256), 0, st, tab);
+    hipLaunchKernelGGL(splitk_reduce4_k, dim3(rb), dim3(256), 0, st, tab);
+  }
+  return hipGetLastError();
 }
 
 hipError_t splitk_reduce(float* slab, int splits, int M, int N, int G, int Ipad, int I, int J, int bias_row,
                          float* wdst, float* bdst, float scale, hipStream_t st) {
-  const int64_t total = (int64_t)G * I * J + (bdst ? J : 0);
-  if (N % 4 == 0 && splits > 1) {
-    const int64_t nq = (int64_t)M * (N / 4);
-    const unsigned qb = (unsigned)((nq + 63) / 64);
-    int S = splits, zstride = 1;
-    if (S > RED_CHUNK && qb < 512) {
-      const int sb = (S + RED_CHUNK - 1) / RED_CHUNK;
-      hipLaunchKernelGGL(splitk_partial4_k, dim3(qb, sb), dim3(256), 0, st, slab, S, nq);
-      S = sb;
-      zstride = RED_CHUNK;
-    }
-    hipLaunchKernelGGL(splitk_reduce4_k, dim3(qb), dim3(256), 0, st, slab, S, zstride, M, N, G, Ipad, I, J,
-                       bias_row, wdst, bdst, scale);
-  } else {
-    hipLaunchKernelGGL(splitk_reduce_k, dim3(nblocks(total, TPB, 8192)), dim3(TPB), 0, st, slab, splits, M, N, G,
-                       Ipad, I, J, bias_row, wdst, bdst, scale);
-  }
-  return hipGetLastError();
+  const RedSpec r{slab, wdst, bdst, splits, M, N, G, Ipad, I, J, bias_row, scale};
+  return splitk_reduce_multi(&r, 1, st);
 }
 
 hipError_t fused_optimizer(float* params, const float* grads, float* mom, float* ema, bf16_t* bf, const OptSeg* segs,

@@ -13,9 +13,14 @@ Design for MI355X:
   finished bucket overlaps the backward of the layers below it.  For the
   reference CNN the 12.85 MB ``local3/weights`` gradient (92.7 % of the bytes)
   is ready after local3's wgrad and overlaps the whole conv backward;
-* the cap is sized for xGMI (7 links × ~153 GB/s, ring per-link bound): a few
-  MB per bucket keeps RCCL at bandwidth while leaving few launches; LeNet-5
-  (247 KB of gradients) is one latency-bound bucket;
+* every bucket except the last overlaps the backward still to run, so the cap is
+  small (bench/main default 0.125 MB): LeNet-5's 236 KB fc bucket is reduced
+  while conv2/conv1 backward (~80 % of backward time) runs, leaving a 10 KB
+  latency-bound conv bucket at the end; the reference CNN gets [softmax+local4]
+  0.8 MB, [local3] 12.85 MB (ring per-link bound on xGMI: ~2·7/8·S / 153 GB/s
+  ≈ 150 µs, hidden behind ~3 ms of conv backward), [conv2], [conv1];
+* split-K weight-gradient reduces of a bucket's layers are flushed as ONE
+  multi-tensor launch just before its all-reduce (``HipNet.hook_layers``);
 * ``work.wait()`` only makes the compute stream wait (no host block); the
   gradient average is folded into the fused optimizer (grad_scale = 1/world).
 """
@@ -80,6 +85,8 @@ class DataParallel:
         self.overlap = overlap
         if self.world > 1:
             net.grad_ready_hooks.append(self._hook)
+            if hasattr(net, "hook_layers"):       # reduced gradients are needed only at bucket triggers
+                net.hook_layers = set(self.trigger)
 
     def _hook(self, layer_index: int) -> None:
         if not self.overlap:

@@ -34,6 +34,16 @@ def _bf16(*shape, device) -> torch.Tensor:
     return torch.zeros(*shape, dtype=torch.bfloat16, device=device)
 
 
+def _reduce(red: Optional[list], slab: torch.Tensor, geo: Tuple[int, ...], wdst: torch.Tensor,
+            bdst: torch.Tensor) -> None:
+    """Split-K reduce of one weight gradient: now, or queued on ``red``.
+    geo = (splits, M, N, G, Ipad, I, J, bias_row) of splitk_reduce."""
+    if red is None:
+        kernels().splitk_reduce(slab, *geo, wdst, bdst, 1.0)
+    else:
+        red.append((slab, geo, wdst, bdst))
+
+
 class _Layer:
     name: str
     has_params = False
@@ -41,8 +51,10 @@ class _Layer:
 
     def fwd(self, nb: int) -> None: ...
 
-    # backward = weight gradient (off the critical path: side stream) + data gradient
-    def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor) -> None:
+    # backward = weight gradient (off the critical path: side stream) + data gradient.
+    # ``red``: a list collecting this layer's split-K reduce (see HipNet._flush_reduce)
+    # instead of launching it right away.
+    def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor, red: Optional[list] = None) -> None:
         pass
 
     def bwd_data(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor]) -> None:
@@ -75,13 +87,13 @@ class ConvLayer(_Layer):
                            self.OW, s.kh, s.kw, self.ph, self.pw, self.Cp, self.fp.param_view(self.bname), s.cout,
                            s.relu)
 
-    def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor) -> None:
+    def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor, red: Optional[list] = None) -> None:
         s = self.spec
         K = kernels()
         S = K.conv_wgrad(self.x, dy, slab, nb, self.H, self.W, self.C, self.OH, self.OW, s.kh, s.kw, self.ph, self.pw,
                          self.Cp, True, Fk.pick_splits(self.M_wg, self.Cp, nb * self.OH * self.OW))
-        K.splitk_reduce(slab, S, self.M_wg, self.Cp, s.kh * s.kw, self.C, s.cin, s.cout, s.kh * s.kw * self.C,
-                        self.fp.grad_view(self.wname), self.fp.grad_view(self.bname), 1.0)
+        _reduce(red, slab, (S, self.M_wg, self.Cp, s.kh * s.kw, self.C, s.cin, s.cout, s.kh * s.kw * self.C),
+                self.fp.grad_view(self.wname), self.fp.grad_view(self.bname))
 
     def bwd_data(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor]) -> None:
         if dx is not None:
@@ -143,13 +155,13 @@ class ConvPoolLayer(_Layer):
         kernels().convpool_fwd(self.x, self.fp.bf16_view(self.wname), self.fp.param_view(self.bname),
                                self.spec.cout, self.out, self.arg, nb, *self._geo(), **self._src())
 
-    def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor) -> None:
+    def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor, red: Optional[list] = None) -> None:
         K = kernels()
         grid = min(self.grid, max(1, (nb + 3) // 4))
         K.convpool_wgrad(self.x, dy, self.arg, slab, grid, nb, *self._geo(), **self._src())
         G, Ip, I, brow = self.red
-        K.splitk_reduce(slab, grid, self.KM, self.Cp, G, Ip, I, self.spec.cout, brow,
-                        self.fp.grad_view(self.wname), self.fp.grad_view(self.bname), 1.0)
+        _reduce(red, slab, (grid, self.KM, self.Cp, G, Ip, I, self.spec.cout, brow),
+                self.fp.grad_view(self.wname), self.fp.grad_view(self.bname))
 
     def bwd_data(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor]) -> None:
         if dx is not None:
@@ -214,14 +226,14 @@ class DenseLayer(_Layer):
         kernels().dense_fwd(self.x, self.fp.bf16_view(self.wname), self.out, nb, self.Np, self.Dp, self.Dp, self.Np,
                             self.Np, self.fp.param_view(self.bname), s.dout, s.relu, None, 0)
 
-    def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor) -> None:
+    def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor, red: Optional[list] = None) -> None:
         s = self.spec
         K = kernels()
         dy2 = dy.view(-1, self.Np)
         S = K.dense_wgrad(self.x, dy2, slab, self.Dp, self.Np, nb, self.Dp, self.Np, True,
                           Fk.pick_splits(self.M_wg, self.Np, nb))
-        K.splitk_reduce(slab, S, self.M_wg, self.Np, 1, self.Dp, s.din, s.dout, self.Dp,
-                        self.fp.grad_view(self.wname), self.fp.grad_view(self.bname), 1.0)
+        _reduce(red, slab, (S, self.M_wg, self.Np, 1, self.Dp, s.din, s.dout, self.Dp),
+                self.fp.grad_view(self.wname), self.fp.grad_view(self.bname))
 
     def bwd_data(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor]) -> None:
         if dx is not None:
@@ -321,14 +333,19 @@ class HipNet:
         # concurrent kernels only time-slice (profiles/r1_overlap/); the serial plan is the
         # same code with one slab.
         self.overlap = overlap_backward and dev.type == "cuda"
+        # serial plan: every layer's split-K reduce is queued and flushed as ONE
+        # multi-tensor launch per gradient bucket (``hook_layers``), so the layers
+        # need disjoint slab regions, as with overlap
+        self.defer_reduce = not self.overlap
         self.dbuf: List[Optional[torch.Tensor]] = [None] + [torch.zeros_like(l.out, dtype=torch.bfloat16)
                                                            for l in self.layers[:-1]]
         sizes = [(getattr(l, "slab_elems", 0) + 3) // 4 * 4 for l in self.layers]
-        self.slab = torch.zeros(max(1, sum(sizes) if self.overlap else max(sizes)), dtype=torch.float32, device=dev)
+        disjoint = self.overlap or self.defer_reduce
+        self.slab = torch.zeros(max(1, sum(sizes) if disjoint else max(sizes)), dtype=torch.float32, device=dev)
         self.slabs, off = [], 0
         for n in sizes:
             self.slabs.append(self.slab[off:off + n] if n else self.slab[:1])
-            off += n if self.overlap else 0
+            off += n if disjoint else 0
         if self.overlap:
             self.side = torch.cuda.Stream(device=dev)
             self.ev_dy = [torch.cuda.Event() for _ in self.layers]
@@ -340,6 +357,9 @@ class HipNet:
         self.loss_names = [n.replace("/weights", "/weight_loss") for n in names] + ["cross_entropy", "total_loss"]
         self.loss_ema = torch.zeros(3 * len(self.loss_names), dtype=torch.float32, device=dev)
         self.grad_ready_hooks: List[Callable[[int], None]] = []
+        # layers after whose weight gradient the hooks need reduced gradients (e.g. the
+        # DP bucket triggers); None = every layer
+        self.hook_layers: Optional[set] = None
         self.idx_buf: Optional[torch.Tensor] = None
         # fused dense head (mlp_head.hip): index of its first layer, or None
         self.head: Optional[int] = self._find_head() if (fuse_head and dev.type == "cuda") else None
@@ -426,6 +446,7 @@ class HipNet:
         waits on exactly that work.  Joins before returning."""
         nb = self.B if nb is None else nb
         dy = self.dlogits
+        pending: list = []
         main = torch.cuda.current_stream(self.device) if self.overlap else None
         if self.overlap:
             self.side.wait_stream(main)
@@ -442,6 +463,12 @@ class HipNet:
                         lay.bwd_weight(nb, dy, self.slabs[i])
                         for h in self.grad_ready_hooks:
                             h(lay.idx)
+                elif self.defer_reduce:
+                    lay.bwd_weight(nb, dy, self.slabs[i], pending)
+                    if self.grad_ready_hooks and (self.hook_layers is None or lay.idx in self.hook_layers):
+                        self._flush_reduce(pending)
+                        for h in self.grad_ready_hooks:
+                            h(lay.idx)
                 else:
                     lay.bwd_weight(nb, dy, self.slabs[i])
                     for h in self.grad_ready_hooks:
@@ -450,8 +477,19 @@ class HipNet:
                 lay.bwd_data(nb, dy, dx)
             dy = dx
         self._head_grads = False
+        self._flush_reduce(pending)
         if self.overlap:
             main.wait_stream(self.side)
+
+    @staticmethod
+    def _flush_reduce(pending: list) -> None:
+        """One multi-tensor split-K reduce (one launch per pass) for the queued layers."""
+        if not pending:
+            return
+        geo = torch.tensor([g for _, g, _, _ in pending], dtype=torch.int64)
+        kernels().splitk_reduce_multi([p[0] for p in pending], [p[2] for p in pending],
+                                      [p[3] for p in pending], geo, [1.0] * len(pending))
+        pending.clear()
 
     def update(self, grad_scale: float = 1.0, increment: bool = True, batch_for_stats: Optional[int] = None) -> None:
         self.fp.apply(self.opt, grad_scale)

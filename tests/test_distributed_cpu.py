@@ -107,6 +107,25 @@ def test_bucket_plan_reference_cnn():
     assert b[0].nbytes > 12.8e6                      # the local3 gradient goes out early
 
 
+def test_bucket_plan_default_cap():
+    """The default 0.125 MB cap leaves only a small bucket that cannot overlap backward."""
+    from distributed_tensorflow_ibm_mnist_amd.models import get_model, torch_ref
+    from distributed_tensorflow_ibm_mnist_amd.parallel.dp import plan_buckets
+    from distributed_tensorflow_ibm_mnist_amd.runtime.params import OptConfig
+    from distributed_tensorflow_ibm_mnist_amd.runtime.torchnet import TorchNet
+    cap = int(0.125 * (1 << 20))
+    spec = get_model("lenet5", 1)
+    net = TorchNet(spec, 2, "cpu", torch_ref.init_params(spec), OptConfig())
+    b = plan_buckets(net, cap)
+    assert [[spec.layers[i].name for i in bk.layers] for bk in b] == [["softmax_linear", "fc4", "fc3"], ["conv2", "conv1"]]
+    assert b[1].nbytes < 16 << 10                    # the tail bucket: conv params only
+    spec = get_model("reference_cnn", 3)
+    net = TorchNet(spec, 2, "cpu", torch_ref.init_params(spec), OptConfig())
+    b = plan_buckets(net, cap)
+    assert [[spec.layers[i].name for i in bk.layers] for bk in b] == [
+        ["softmax_linear", "local4"], ["local3"], ["conv2"], ["conv1"]]
+
+
 def _spawn_main(args, log):
     env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONUNBUFFERED="1")
     return subprocess.Popen([sys.executable, os.path.join(ROOT, "main.py")] + args, cwd=ROOT, env=env,

@@ -345,3 +345,42 @@ def test_convpool(dev, K, N, H, W, Ci, ci, Co, co, pad):
         dx = torch.empty(N, H, W, Ci, dtype=torch.bfloat16, device=dev)
         K.convpool_dgrad(dP, arg, w, dx, N, Ci, Co, 5, pad, H, W)
         close(dx[..., :ci], xr.grad[..., :ci])
+
+
+# ---------------------------------------------------------------- split-K reduce
+def test_splitk_reduce_multi_matches_single(dev, K):
+    """One multi-tensor launch == per-slab reduces (bitwise) == fp64 sums, across the
+    partial-pass (S > 64) and direct cases, with and without a bias row."""
+    torch.manual_seed(0)
+    cases = [  # (splits, M, N, G, Ipad, I, J, bias_row)
+        (1024, 208, 16, 25, 8, 6, 16, 200),   # LeNet conv2 wgrad slab (partial pass)
+        (48, 401, 120, 1, 400, 400, 120, 400),
+        (7, 89, 16, 1, 88, 84, 10, 88),
+        (300, 48, 8, 5, 8, 5, 6, 40),
+    ]
+    slabs, slabs2, w1, w2, b1, b2 = [], [], [], [], [], []
+    for (S, M, N, G, Ip, I, J, br) in cases:
+        s = torch.randn(S * M * N, device=dev)
+        slabs.append(s)
+        slabs2.append(s.clone())
+        w1.append(torch.empty(G * I * J, device=dev))
+        w2.append(torch.empty(G * I * J, device=dev))
+        b1.append(torch.empty(J, device=dev))
+        b2.append(torch.empty(J, device=dev))
+    for i, c in enumerate(cases):
+        K.splitk_reduce(slabs[i], *c, w1[i], b1[i], 0.5)
+    geo = torch.tensor(cases, dtype=torch.int64)
+    K.splitk_reduce_multi(slabs2, w2, b2, geo, [0.5] * len(cases))
+    torch.cuda.synchronize()
+    for i, (S, M, N, G, Ip, I, J, br) in enumerate(cases):
+        assert torch.equal(w1[i], w2[i]) and torch.equal(b1[i], b2[i])
+    # oracle on fresh data (the reduce pre-sums in place)
+    S, M, N, G, Ip, I, J, br = cases[0]
+    s = torch.randn(S * M * N, device=dev)
+    ref = s.double().view(S, M, N).sum(0) * 0.5
+    w = torch.empty(G * I * J, device=dev)
+    b = torch.empty(J, device=dev)
+    K.splitk_reduce_multi([s], [w], [b], torch.tensor([cases[0]]), [0.5])
+    wr = ref[:G * Ip].view(G, Ip, N)[:, :I, :J].reshape(-1)
+    assert torch.allclose(w.double(), wr, rtol=1e-5, atol=1e-4)
+    assert torch.allclose(b.double(), ref[br, :J], rtol=1e-5, atol=1e-4)

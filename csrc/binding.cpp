@@ -541,6 +541,12 @@ bool convpool_u8_input(int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64
   return mnistx::convpool_u8_input(cp_geo(cin, cout, ks, pad, h, w).cfg) != 0;
 }
 
+int64_t convpool_wgrad_grid(int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t w) {
+  const int n = mnistx::convpool_wgrad_grid(cp_geo(cin, cout, ks, pad, h, w).cfg);
+  TORCH_CHECK(n > 0, "convpool_wgrad_grid: occupancy query failed");
+  return n;
+}
+
 bool convpool_has_dgrad(int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t w) {
   return mnistx::convpool_has_dgrad(cp_geo(cin, cout, ks, pad, h, w).cfg) != 0;
 }
@@ -600,5 +606,6 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("convpool_u8_input", &convpool_u8_input);
   m.def("convpool_dgrad", &convpool_dgrad);
   m.def("convpool_has_dgrad", &convpool_has_dgrad);
+  m.def("convpool_wgrad_grid", &convpool_wgrad_grid);
   m.attr("ARCH") = "gfx950";
 }

@@ -30,6 +30,8 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <cstdlib>
+
 namespace mnistx {
 namespace {
 
@@ -157,6 +159,12 @@ DEV uint32_t pos_of(float v) { return __float_as_uint(v) & 3u; }
 DEV float pos_clear(float v) { return __uint_as_float(__float_as_uint(v) & ~3u); }
 
 constexpr int NTH = 256;
+// Minimum waves per SIMD the register allocator must leave room for (the
+// __launch_bounds__ second argument).  LeNet conv2 fwd fits 93 VGPRs (5 waves, was
+// 4 at 106) and its wgrad 167 (3 waves, was 2 at 172) without spills; the
+// reference conv1 variants spill under a bound, so they keep the default.
+template <class G> constexpr int fwd_minw() { return (G::CIN == 8 && G::COUT == 16) ? 5 : 1; }
+template <class G> constexpr int wgrad_minw() { return (G::CIN == 8 && G::COUT == 16) ? 3 : 1; }
 // Argmax byte of a pool window whose ReLU output is 0: matches no position, so
 // the backward kernels need only (dP, arg) -- the ReLU mask is folded in here
 // and the pooled activations are never re-read.
@@ -282,7 +290,7 @@ struct DYStage {
 
 // ------------------------------------------------------------------ forward
 template <class G, int IMGS>
-__global__ __launch_bounds__(NTH) void convpool_fwd_k(const XSrc x, const bf16_t* __restrict__ w,
+__global__ __launch_bounds__(NTH, fwd_minw<G>()) void convpool_fwd_k(const XSrc x, const bf16_t* __restrict__ w,
                                                       const float* __restrict__ bias, int bias_n, int B,
                                                       bf16_t* __restrict__ pooled, uint8_t* __restrict__ arg) {
   constexpr int LDS = (IMGS * G::IMG_LDS + 7) / 8 * 8;
@@ -646,7 +654,7 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
 // chunk; the bias row (k = KE) reads a constant [1,0,0,0] LDS cell.  dY is
 // rebuilt from (dP, arg): position d of a window gets dP iff arg == d.
 template <class G, int IMGS>
-__global__ __launch_bounds__(NTH) void convpool_wgrad_k(const XSrc x, const bf16_t* __restrict__ dP,
+__global__ __launch_bounds__(NTH, wgrad_minw<G>()) void convpool_wgrad_k(const XSrc x, const bf16_t* __restrict__ dP,
                                                         const uint8_t* __restrict__ arg, int B,
                                                         float* __restrict__ slab) {
   constexpr int CELL = IMGS * G::IMG_LDS;             // [1,0,0,0] then [0,0,0,0]
@@ -794,41 +802,54 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_k(const XSrc x, const bf16
 // the window's LEFT column; output column (c, sx) pairs that left-pixel patch with
 // the dY of pixel (dy, sx).  The right pixel's patch is the left one shifted by one
 // kw, so R[kh*8+kw'][8+c] accumulates dW[kh][kw'-1][c]: the fold
-// dW[m][c] = R[m][c] + R[m+1][8+c] (bias row: both sides) is applied to the block
-// partials, and the slab has the plain MODE 0 layout [KM][8].
+// dW[m][c] = R[m][c] + R[m+1][8+c] is applied to the block partials, and the slab
+// has the plain MODE 0 layout [KM][8].
+//
+// The unpooled dY lives in LDS as U[sx*8 + c][window][dy] (one dword per window),
+// built once per image group from the (dP, arg) vectors, so the MFMA B operand of a
+// step is two aligned ds_read_b64 (windows 16s+2g.. and +8) with no per-step unpool
+// arithmetic.  Row stride 212 dwords (4 x odd): the 16 rows x 2 lane groups of a
+// ds_read_b64 half-wave hit 64 distinct banks.  The bias gradient (sum of dP over
+// ReLU-active windows) is accumulated while staging, in a fixed per-thread window
+// order, and combined in a fixed thread order: deterministic, and im2col rows
+// KE..KM-1 carry no bias/zero cells (their accumulators are never read).
 template <class G, int IMGS>
-__global__ __launch_bounds__(NTH) void convpool_wgrad_pair_k(const XSrc x,
+__global__ __launch_bounds__(NTH, 5) void convpool_wgrad_pair_k(const XSrc x,
                                                              const bf16_t* __restrict__ dP,
                                                              const uint8_t* __restrict__ arg, int B,
                                                              float* __restrict__ slab) {
   static_assert(G::PAIR, "");
-  constexpr int CELL = IMGS * G::IMG_LDS;
-  constexpr int LDS = (CELL + 8 + 7) / 8 * 8;
   constexpr int RS = (2 * G::NWIN + 31) / 32;        // reduction steps per image
+  constexpr int NWP = RS * 16;                        // windows incl. the zero tail of the last step
+  constexpr int URS = 212;                            // U row stride in dwords (4 x odd, >= NWP)
+  static_assert(URS >= NWP && URS % 8 == 4, "U row stride");
+  constexpr int UIMG = 16 * URS;                      // dwords per image
   constexpr int NWC = G::NWIN * 8;
-  __shared__ __attribute__((aligned(16))) bf16_t tile[LDS];
-  __shared__ __attribute__((aligned(16))) bf16_t dys[IMGS * NWC];
-  __shared__ __attribute__((aligned(16))) uint8_t args[IMGS * NWC];
+  constexpr int TILE_E = (IMGS * G::IMG_LDS + 7) / 8 * 8;
+  __shared__ __attribute__((aligned(16))) bf16_t tile[TILE_E];
+  __shared__ __attribute__((aligned(16))) uint32_t U[IMGS * UIMG];   // also the bias combine at the end
   __shared__ float red[G::KM * 16];
   __shared__ int wtab[G::NWIN];            // window -> aligned LDS offset of its top-left pixel
+  static_assert(IMGS * UIMG >= NTH * 8 + 256, "bias combine reuses U");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  const int c = li & 7, sx = li >> 3;
-  lds_zero<LDS>(tile, tid);
+  lds_zero<TILE_E>(tile, tid);
+  lds_zero<IMGS * UIMG * 2>((bf16_t*)U, tid);          // windows >= NWIN stay zero
   for (int w = tid; w < G::NWIN; w += NTH) wtab[w] = G::aligned_off(G::wbase(w));
-  __syncthreads();
-  if (tid == 0) tile[CELL] = (bf16_t)0x3f80;
 
   const int q = (lane >> 2) & 3, p = lane & 3;
   int cd[G::MFW];
 #pragma unroll
   for (int mf = 0; mf < G::MFW; ++mf) {
     const int k0 = mf * 16 + 4 * p;
-    cd[mf] = k0 < G::KE ? G::chunk_delta(k0) : (k0 == G::KE ? -1 : -2);
+    cd[mf] = k0 < G::KE ? G::chunk_delta(k0) : 0;   // rows >= KE: any valid pixel (never read back)
   }
   f32x4 acc[G::MFW];
 #pragma unroll
   for (int mf = 0; mf < G::MFW; ++mf) acc[mf] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) bacc[c] = 0.f;
 
   const int stride = gridDim.x * IMGS;
   XStage<G, IMGS> xs;
@@ -840,7 +861,24 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_pair_k(const XSrc x,
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
     __syncthreads();
     xs.store(tile, tid);
-    ys.store(dys, args, tid);
+    // max-unpool into U: U[sx*8+c][w] = (dy0: arg==sx ? dP : 0, dy1: arg==2+sx ? dP : 0)
+#pragma unroll
+    for (int u = 0; u < DYStage<G, IMGS>::PER; ++u) {
+      const int e = 8 * (tid + u * NTH);
+      if (e < IMGS * NWC) {
+        const int im = e / NWC, win = (e - im * NWC) >> 3;
+        uint32_t* urow = U + im * UIMG + win;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const uint32_t yc = (ys.y[u][c >> 1] >> (16 * (c & 1))) & 0xffffu;
+          const uint32_t ac = (ys.a[u][c >> 2] >> (8 * (c & 3))) & 0xffu;
+          bacc[c] += ac < 4u ? __uint_as_float(yc << 16) : 0.f;
+#pragma unroll
+          for (int sx = 0; sx < 2; ++sx)
+            urow[(sx * 8 + c) * URS] = (ac == (uint32_t)sx ? yc : 0u) | (ac == (uint32_t)(2 + sx) ? yc << 16 : 0u);
+        }
+      }
+    }
     __syncthreads();
     make_shifted<G, IMGS>(tile, tid);
     __syncthreads();
@@ -851,18 +889,9 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_pair_k(const XSrc x,
     }
     for (int it = wave; it < IMGS * RS; it += NTH / 64) {
       const int im = it / RS, s = it - im * RS;
-      // dY operand: element j <-> slot 4g + (j&3) + 16(j>>2) = window 16s + 2g + ((j>>1)&1) + 8(j>>2), dy = j&1
-      bf16x8 bfr;
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int wj = 16 * s + 2 * g + (jj & 1) + 8 * (jj >> 1);
-        const bool ok = wj < G::NWIN;
-        const int i = (im * G::NWIN + wj) * 8 + c;
-        const bf16_t y = ok ? dys[i] : (bf16_t)0;
-        const int a = ok ? args[i] : (int)ARG_OFF;
-#pragma unroll
-        for (int dy = 0; dy < 2; ++dy) bfr[4 * (jj >> 1) + 2 * (jj & 1) + dy] = as_bf(a == 2 * dy + sx ? y : (bf16_t)0);
-      }
+      // dY operand: element j <-> window 16s + 2g + ((j>>1)&1) + 8(j>>2), dy = j&1
+      const uint32_t* ub = U + im * UIMG + li * URS + 16 * s + 2 * g;
+      const bf16x8 bfr = join(*(const s16x4*)ub, *(const s16x4*)(ub + opaque(8)));
       // im2col^T operand rows supplied by this lane: slot 4g+q (+16): window 16s + 2g + q/2 (+8), dy = q&1
       // (dy adds WS and the chunk deltas are multiples of 4: the copy is the window's)
       const int wq = 16 * s + 2 * g + (q >> 1);
@@ -870,11 +899,7 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_pair_k(const XSrc x,
       const int pb1 = im * G::IMG_LDS + wtab[min(wq + 8, G::NWIN - 1)] + (q & 1) * G::WS;
 #pragma unroll
       for (int mf = 0; mf < G::MFW; ++mf) {
-        const int cc = cd[mf];
-        const int cell = CELL + (cc == -1 ? 0 : 4);
-        const int o0 = cc >= 0 ? pb0 + cc : cell;
-        const int o1 = cc >= 0 ? pb1 + cc : cell;
-        const bf16x8 a = join(lds_tr4(tile + o0), lds_tr4(tile + o1));
+        const bf16x8 a = join(lds_tr4(tile + pb0 + cd[mf]), lds_tr4(tile + pb1 + cd[mf]));
         acc[mf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr, acc[mf], 0, 0, 0);
       }
     }
@@ -891,12 +916,30 @@ __global__ __launch_bounds__(NTH) void convpool_wgrad_pair_k(const XSrc x,
         }
     }
   }
+  float* bred = (float*)U;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) bred[c * NTH + tid] = bacc[c];
+  __syncthreads();
+  // bias: 8 x 256 per-thread sums -> 8 x 32 (8 consecutive threads each) -> 8, fixed order
+  float* bred2 = bred + 8 * NTH;
+  if (tid < 8 * 32) {
+    const float* src = bred + (tid >> 5) * NTH + (tid & 31) * 8;
+    float v = src[0];
+#pragma unroll
+    for (int t = 1; t < 8; ++t) v += src[t];
+    bred2[tid] = v;
+  }
   __syncthreads();
   float* out = slab + (int64_t)blockIdx.x * G::KM * 8;
   for (int e = tid; e < G::KM * 8; e += NTH) {
     const int m = e >> 3, cc = e & 7;
-    const int m2 = m == G::KE ? m : m + 1;            // bias row: both sides of the same row
-    out[e] = red[m * 16 + cc] + (m2 < G::KM ? red[m2 * 16 + 8 + cc] : 0.f);
+    float v = 0.f;
+    if (m == G::KE) {
+      for (int t = 0; t < 32; ++t) v += bred2[cc * 32 + t];
+    } else if (m < G::KE) {
+      v = red[m * 16 + cc] + red[(m + 1) * 16 + 8 + cc];
+    }
+    out[e] = v;
   }
 }
 
@@ -1014,18 +1057,39 @@ int grid_for(int B, int imgs, int cap) {
   return n < cap ? (n < 1 ? 1 : n) : cap;
 }
 
+// Workgroups that fill every CU exactly once (occupancy API, cached per kernel):
+// the persistent grid-stride kernels get one resident wave and no partial last round.
+template <auto KER>   // the kernel itself is the key: kernels with one signature share a type
+int resident_grid() {
+  static int n = 0;
+  if (n == 0) {
+    int per_cu = 0, dev = 0, cus = 0;
+    const char* env = getenv("MNISTX_RESIDENT_GRID");   // "0": legacy 2048-block grids (A/B runs)
+    if (env && env[0] == '0') return n = 2048;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, KER, NTH, 0) == hipSuccess &&
+        hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && per_cu > 0)
+      n = per_cu * cus;
+    else
+      n = 2048;
+  }
+  return n;
+}
+
 template <class G, int IMGS>
 hipError_t run_fwd(const XSrc& x, const bf16_t* w, const float* bias, int bias_n, int B, bf16_t* pooled, uint8_t* arg,
                    hipStream_t st) {
   if constexpr (G::PAIR && G::H == 28 && G::W == 28 && G::PAD == 2) {
     constexpr int QI = 4;
+    // two resident rounds (2048) measured 5 % faster than one for this kernel (same-box A/B)
     hipLaunchKernelGGL((convpool_fwd_quad_k<QI>), dim3(grid_for(B, QI, 2048)), dim3(NTH), 0, st, x, w, bias, bias_n,
                        B, pooled, arg);
   } else if constexpr (G::PAIR) {
     hipLaunchKernelGGL((convpool_fwd_pair_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, x, w, bias,
                        bias_n, B, pooled, arg);
   } else {
-    hipLaunchKernelGGL((convpool_fwd_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, x, w, bias, bias_n,
+    hipLaunchKernelGGL((convpool_fwd_k<G, IMGS>), dim3(grid_for(B, IMGS, resident_grid<convpool_fwd_k<G, IMGS>>())),
+                       dim3(NTH), 0, st, x, w, bias, bias_n,
                        B, pooled, arg);
   }
   return hipGetLastError();
@@ -1044,12 +1108,14 @@ hipError_t run_wgrad(const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B,
 
 template <class G, int IMGS>
 hipError_t run_dgrad(const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int B, bf16_t* dx, hipStream_t st) {
-  hipLaunchKernelGGL((convpool_dgrad_pair_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, dP, arg, w,
+  hipLaunchKernelGGL((convpool_dgrad_pair_k<G, IMGS>),
+                     dim3(grid_for(B, IMGS, resident_grid<convpool_dgrad_pair_k<G, IMGS>>())), dim3(NTH), 0, st, dP, arg, w,
                      B, dx);
   return hipGetLastError();
 }
 
 using LeNetC1 = Geo<1, 8, 5, 2, 28, 28>;
+constexpr int WG_IMGS_C1 = 1;   // conv1 wgrad: one image per group (LDS 28 KB -> 5 workgroups / CU)
 using LeNetC2 = Geo<8, 16, 5, 0, 14, 14>;
 using RefC1g = Geo<1, 32, 5, 2, 28, 28>;
 using RefC1c = Geo<3, 32, 5, 2, 28, 28>;
@@ -1107,12 +1173,41 @@ hipError_t convpool_fwd(int cfg, const XSrc& x, const bf16_t* w, const float* bi
 hipError_t convpool_wgrad(int cfg, const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B, float* slab,
                           int grid, hipStream_t st) {
   switch (cfg) {
-    case 0: return run_wgrad<LeNetC1, 2>(x, dP, arg, B, slab, grid, st);
+    case 0: return run_wgrad<LeNetC1, WG_IMGS_C1>(x, dP, arg, B, slab, grid, st);
     case 1: return run_wgrad<LeNetC2, 4>(x, dP, arg, B, slab, grid, st);
     case 2: return run_wgrad<RefC1g, 2>(x, dP, arg, B, slab, grid, st);
     case 3: return run_wgrad<RefC1c, 2>(x, dP, arg, B, slab, grid, st);
   }
   return hipErrorInvalidValue;
+}
+
+template <class G, int IMGS>
+int wgrad_grid_for() {
+  int per_cu = 0, dev = 0, cus = 0;
+  if constexpr (G::PAIR) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, convpool_wgrad_pair_k<G, IMGS>, NTH, 0) != hipSuccess)
+      return -1;
+  } else {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, convpool_wgrad_k<G, IMGS>, NTH, 0) != hipSuccess)
+      return -1;
+  }
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return -1;
+  return per_cu * cus;
+}
+
+// One resident wave of wgrad workgroups (every CU full, nothing queued): the
+// persistent grid-stride loop then gives every block the same image count, and
+// the slab has exactly one partial per resident block.
+int convpool_wgrad_grid(int cfg) {
+  switch (cfg) {
+    case 0: return wgrad_grid_for<LeNetC1, WG_IMGS_C1>();
+    case 1: return wgrad_grid_for<LeNetC2, 4>();
+    case 2: return wgrad_grid_for<RefC1g, 2>();
+    case 3: return wgrad_grid_for<RefC1c, 2>();
+  }
+  return -1;
 }
 
 int convpool_has_dgrad(int cfg) { return cfg == 1 ? 1 : 0; }

@@ -57,6 +57,8 @@ int convpool_reduce_layout(int cfg, int* out);
 hipError_t convpool_fwd(int cfg, const XSrc& x, const bf16_t* w, const float* bias, int bias_n, int B,
                         bf16_t* pooled, uint8_t* arg, hipStream_t st);
 // backward needs only (dP, arg): arg == 4 marks a window whose ReLU output is 0
+// workgroups that fill every CU once for this geometry's wgrad kernel (occupancy API)
+int convpool_wgrad_grid(int cfg);
 hipError_t convpool_wgrad(int cfg, const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B, float* slab,
                           int grid, hipStream_t st);
 int convpool_has_dgrad(int cfg);

@@ -93,7 +93,10 @@ def build_kernels(force: bool = False, verbose: bool = True, jobs: int = 8) -> s
         o = os.path.join(BUILD, os.path.basename(s) + ".o")
         objs.append(o)
         if force or _newer(o, [s] + hdrs):
+            # MFMA accumulators in the VGPR form: the AGPR form made the register allocator
+            # shuffle loop-carried accumulators with v_accvgpr moves (up to 12 per step)
             jobs_list.append([HIPCC, "-std=c++17", "-O3", f"--offload-arch={ARCH}", "-fno-gpu-rdc", "-fPIC",
+                              "-mllvm", "-amdgpu-mfma-vgpr-form",
                               "-D__HIP_PLATFORM_AMD__=1", f"-I{CSRC}", "-c", s, "-o", o])
     bsrc = os.path.join(CSRC, "binding.cpp")
     bobj = os.path.join(BUILD, "binding.o")

@@ -135,7 +135,8 @@ class ConvPoolLayer(_Layer):
         self.wname, self.bname = f"{spec.name}/weights", f"{spec.name}/biases"
         self.KM = kernels().convpool_rows(self.C, self.Cp, 5, self.pad, self.H, self.W)
         self.red = kernels().convpool_reduce_args(*self._geo(), spec.cin)   # (G, Ipad, I, bias_row)
-        self.grid = 1024
+        # one resident wave of wgrad workgroups (occupancy query; 1024 without a GPU)
+        self.grid = kernels().convpool_wgrad_grid(*self._geo()) if dev.type == "cuda" else 1024
         self.slab_elems = self.grid * self.KM * self.Cp
         self.can_dgrad = kernels().convpool_has_dgrad(*self._geo())
         if need_dx and not self.can_dgrad:

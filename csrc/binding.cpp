@@ -79,6 +79,8 @@ mnistx::GemmEpi make_slab(const Tensor& slab, int64_t splits, int64_t M, int64_t
 }
 
 // Effective split count the launcher will use (kchunk rounded to BK=32).
+// split-K count the weight-gradient launch really uses: chunks round up to its
+// K step (gemm.hip BK_WG = 32)
 int64_t eff_splits(int64_t K, int64_t splits) {
   if (splits < 1) splits = 1;
   int64_t kchunk = (K + splits - 1) / splits;
@@ -108,7 +110,7 @@ void dense_dgrad(Tensor dy, Tensor w, Tensor out, int64_t M, int64_t N, int64_t 
 }
 
 int64_t dense_wgrad(Tensor x, Tensor dy, Tensor slab, int64_t Din, int64_t Dout, int64_t B, int64_t ldx, int64_t lddy,
-                    bool with_bias, int64_t splits) {
+                    bool with_bias, int64_t splits, int64_t tile) {
   check(x, at::kBFloat16, span(B, ldx, Din), "x");
   check(dy, at::kBFloat16, span(B, lddy, Dout), "dy");
   TORCH_CHECK(ldx >= Din && lddy >= Dout, "bad leading dims");
@@ -116,7 +118,7 @@ int64_t dense_wgrad(Tensor x, Tensor dy, Tensor slab, int64_t Din, int64_t Dout,
   const int64_t S = eff_splits(B, splits);
   auto ep = make_slab(slab, S, M, Dout);
   hip_ok(mnistx::dense_wgrad(BF(x), BF(dy), (int)Din, (int)Dout, (int)B, (int)ldx, (int)lddy, with_bias ? 1 : 0,
-                             (int)S, ep, cur_stream()),
+                             (int)S, ep, cur_stream(), (int)tile),
          "dense_wgrad");
   return S;
 }
@@ -570,7 +572,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for the MNIST trainer";
   m.def("dense_fwd", &dense_fwd);
   m.def("dense_dgrad", &dense_dgrad);
-  m.def("dense_wgrad", &dense_wgrad);
+  m.def("dense_wgrad", &dense_wgrad, py::arg("x"), py::arg("dy"), py::arg("slab"), py::arg("Din"), py::arg("Dout"),
+        py::arg("B"), py::arg("ldx"), py::arg("lddy"), py::arg("with_bias"), py::arg("splits"), py::arg("tile") = -1);
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);

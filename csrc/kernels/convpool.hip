@@ -163,7 +163,7 @@ constexpr int NTH = 256;
 // __launch_bounds__ second argument).  LeNet conv2 fwd fits 93 VGPRs (5 waves, was
 // 4 at 106) and its wgrad 167 (3 waves, was 2 at 172) without spills; the
 // reference conv1 variants spill under a bound, so they keep the default.
-template <class G> constexpr int fwd_minw() { return (G::CIN == 8 && G::COUT == 16) ? 5 : 1; }
+template <class G> constexpr int fwd_minw() { return (G::CIN == 8 && G::COUT == 16) ? 4 : 1; }
 template <class G> constexpr int wgrad_minw() { return (G::CIN == 8 && G::COUT == 16) ? 3 : 1; }
 // Argmax byte of a pool window whose ReLU output is 0: matches no position, so
 // the backward kernels need only (dP, arg) -- the ReLU mask is folded in here
@@ -369,22 +369,28 @@ __global__ __launch_bounds__(NTH, fwd_minw<G>()) void convpool_fwd_k(const XSrc 
       f32x4 acc[G::NF];
 #pragma unroll
       for (int nf = 0; nf < G::NF; ++nf) acc[nf] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // every A fragment of the chain is read before the first MFMA (a read-then-wait per
+      // MFMA serialised the chain on LDS latency)
+      bf16x8 a[G::KSTEPS];
 #pragma unroll
       for (int s = 0; s < G::KSTEPS; ++s) {
-        bf16x8 a;
         if constexpr (G::MODE == 2) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) a[j] = as_bf(tb[pb + dl[s][j]]);
+          for (int j = 0; j < 8; ++j) a[s][j] = as_bf(tb[pb + dl[s][j]]);
         } else if constexpr (G::MODE == 1) {
-          a = __builtin_bit_cast(bf16x8, *(const u32x4*)(tb + pb + dd[s][0]));
+          a[s] = __builtin_bit_cast(bf16x8, *(const u32x4*)(tb + pb + dd[s][0]));
         } else {
           const s16x4 lo = *(const s16x4*)(tb + G::aligned_off(pb + dd[s][0]));
           const s16x4 hi = *(const s16x4*)(tb + G::aligned_off(pb + opaque(dd[s][1])));
-          a = join(lo, hi);
+          a[s] = join(lo, hi);
         }
-#pragma unroll
-        for (int nf = 0; nf < G::NF; ++nf) acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[s][nf], acc[nf], 0, 0, 0);
       }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < G::KSTEPS; ++s)
+#pragma unroll
+        for (int nf = 0; nf < G::NF; ++nf)
+          acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], bfr[s][nf], acc[nf], 0, 0, 0);
       const int win = fm * 4 + g;
       if (win < G::NWIN && (STAGE || img0 + im < B)) {
         bf16_t* pimg = STAGE ? pout + im * OUTE : pooled + (int64_t)(img0 + im) * OUTE;
@@ -1030,11 +1036,14 @@ __global__ __launch_bounds__(NTH) void convpool_dgrad_pair_k(const bf16_t* __res
       const int im = f / MFD, mf = f - im * MFD;
       const bf16_t* tb = dyt + im * DT + (2 * mf + (li >> 3)) * RSE + 2 * (li & 7) * DPS;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      // all A fragments in flight before the MFMA chain: one read ahead left every
+      // MFMA waiting out a full LDS latency (wait_any 57 %, MFMA busy 38 %)
+      bf16x8 a[KSD];
 #pragma unroll
-      for (int s = 0; s < KSD; ++s) {
-        const bf16x8 a = __builtin_bit_cast(bf16x8, *(const u32x4*)(tb + dtap[s]));
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[s], acc, 0, 0, 0);
-      }
+      for (int s = 0; s < KSD; ++s) a[s] = __builtin_bit_cast(bf16x8, *(const u32x4*)(tb + dtap[s]));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < KSD; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], bw[s], acc, 0, 0, 0);
       // accumulator rows 4g + r: image row 2mf + g/2, pair jr = 4(g&1) + r -> LDS staging
       const int ih = 2 * mf + (g >> 1);
       bf16_t* oimg = outs + im * OUTE;

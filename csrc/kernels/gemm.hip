@@ -37,6 +37,13 @@ namespace mnistx {
 namespace {
 
 constexpr int BK = 32;
+// K rows staged per step by the weight-gradient GEMMs (both operands MN-contiguous,
+// split-K).  128 was measured SLOWER on every wgrad shape (LeNet fc3/fc4/fc5 at
+// B=65536: bench/micro_wgrad.py; reference conv2 wgrad 1.50 -> 1.74 ms): the 80 KB+
+// LDS images halve the resident blocks.  The knob stays for future tiles.
+constexpr int BK_WG = 32;
+template <bool AKC, bool BKC>
+constexpr int kstep() { return (!AKC && !BKC) ? BK_WG : BK; }
 
 // Row stride (elements) of an LDS image whose contiguous extent is COLS.
 template <int COLS, bool KC, bool PAD48 = true>
@@ -206,11 +213,12 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEp
   constexpr int FM = TM / 16, FN = TN / 16;
   static_assert(FM >= 1 && FN >= 1, "wave tile too small");
   constexpr bool DENSE = std::is_same<LA, MatLoader>::value && std::is_same<LB, MatLoader>::value;
+  constexpr int KB = kstep<AKC, BKC>();                 // rows of K staged per step
   constexpr int SA = ImgStride<AKC ? BK : BM, AKC, DENSE>::value;
   constexpr int SB = ImgStride<BKC ? BK : BN, BKC, DENSE>::value;
-  constexpr int A_ELEMS = AKC ? BM * SA : BK * SA;
-  constexpr int B_ELEMS = BKC ? BN * SB : BK * SB;
-  constexpr int A_VEC = BM * BK / 8, B_VEC = BN * BK / 8;
+  constexpr int A_ELEMS = AKC ? BM * SA : KB * SA;
+  constexpr int B_ELEMS = BKC ? BN * SB : KB * SB;
+  constexpr int A_VEC = BM * KB / 8, B_VEC = BN * KB / 8;
   constexpr int A_VPT = (A_VEC + NT - 1) / NT, B_VPT = (B_VEC + NT - 1) / NT;
 
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (A_ELEMS + B_ELEMS)];
@@ -230,7 +238,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEp
   const int n0 = (t % tiles_n) * BN;
   const int kbeg = blockIdx.y * kchunk;
   const int kend = min(K, kbeg + kchunk);
-  const int nsteps = (kend - kbeg + BK - 1) / BK;
+  const int nsteps = (kend - kbeg + KB - 1) / KB;
 
   u32x4 ra[A_VPT], rb[B_VPT];
 
@@ -300,23 +308,26 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEp
     __syncthreads();
     for (int s = 0; s < nsteps; ++s) {
       const int cur = s & 1;
-      if (s + 1 < nsteps) gload(kbeg + (s + 1) * BK);
-      bf16x8 af[FM], bfr[FN];
+      if (s + 1 < nsteps) gload(kbeg + (s + 1) * KB);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int r0 = wm * TM + i * 16;
-        af[i] = AKC ? frag_kc<SA>(As(cur), r0, 0, lane) : frag_tr<SA>(As(cur), r0, 0, lane);
+      for (int kb = 0; kb < KB; kb += BK) {
+        bf16x8 af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int r0 = wm * TM + i * 16;
+          af[i] = AKC ? frag_kc<SA>(As(cur), r0, kb, lane) : frag_tr<SA>(As(cur), r0, kb, lane);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int c0 = wn * TN + j * 16;
+          bfr[j] = BKC ? frag_kc<SB>(Bs(cur), c0, kb, lane) : frag_tr<SB>(Bs(cur), c0, kb, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int c0 = wn * TN + j * 16;
-        bfr[j] = BKC ? frag_kc<SB>(Bs(cur), c0, 0, lane) : frag_tr<SB>(Bs(cur), c0, 0, lane);
-      }
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       if (s + 1 < nsteps) sstore(cur ^ 1);
       __syncthreads();
     }
@@ -416,7 +427,8 @@ hipError_t launch_cfg(const LA& la, const LB& lb, const GemmEpi& ep, int M, int 
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   if (splits < 1) splits = 1;
   int kchunk = (K + splits - 1) / splits;
-  kchunk = ((kchunk + BK - 1) / BK) * BK;
+  constexpr int KB = kstep<AKC, BKC>();
+  kchunk = ((kchunk + KB - 1) / KB) * KB;
   splits = (K + kchunk - 1) / kchunk;
   if (splits < 1) splits = 1;
   dim3 grid(tm * tn, splits);
@@ -450,21 +462,22 @@ int tile_code(int M, int N, bool wgrad) {
 
 template <class LA, bool AKC, class LB, bool BKC>
 hipError_t launch_any(const LA& la, const LB& lb, const GemmEpi& ep, int M, int N, int K, int splits,
-                      hipStream_t st) {
+                      hipStream_t st, int code = -1) {
   constexpr bool WG = !AKC && !BKC;
-  switch (tile_code(M, N, WG)) {
+  const int c = code >= 0 ? code : tile_code(M, N, WG);
+  switch (c) {
     case T64x16: return launch_cfg<64, 16, 4, 1, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
     case T64x32: return launch_cfg<64, 32, 4, 1, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
     case T64x64: return launch_cfg<64, 64, 2, 2, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
     case T128x128: return launch_cfg<128, 128, 2, 2, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+    case T128x64: return launch_cfg<128, 64, 2, 2, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+    case T64x128: return launch_cfg<64, 128, 1, 4, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
     default: break;
   }
   if constexpr (!WG) {
-    switch (tile_code(M, N, false)) {
+    switch (c) {
       case T256x16: return launch_cfg<256, 16, 4, 1, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
       case T256x32: return launch_cfg<256, 32, 4, 1, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
-      case T128x64: return launch_cfg<128, 64, 2, 2, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
-      case T64x128: return launch_cfg<64, 128, 1, 4, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
       default: break;
     }
   }
@@ -498,12 +511,12 @@ hipError_t dense_dgrad(const bf16_t* dy, const bf16_t* w, int M, int N, int K, i
 }
 
 hipError_t dense_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int B, int ldx, int lddy,
-                       int with_bias, int splits, const GemmEpi& ep, hipStream_t st) {
+                       int with_bias, int splits, const GemmEpi& ep, hipStream_t st, int tile) {
   // slab[Din(+1), Dout] = X^T dY ; A(m=din, k=b) = X[b][din] ; B(k=b, n) = dY[b][n]
   MatLoader a{x, B, Din, ldx, with_bias ? Din : -1};
   MatLoader b{dy, B, Dout, lddy, -1};
   const int M = Din + (with_bias ? 1 : 0);
-  return launch_any<MatLoader, false, MatLoader, false>(a, b, ep, M, Dout, B, splits, st);
+  return launch_any<MatLoader, false, MatLoader, false>(a, b, ep, M, Dout, B, splits, st, tile);
 }
 
 hipError_t conv_fwd(const bf16_t* x, const bf16_t* w, int Nb, int H, int W, int C, int OH, int OW, int KH,

@@ -506,7 +506,7 @@ __global__ __launch_bounds__(256) void splitk_partial4_k(RedTable tab) {
 // L2 norm needed for the weight-decay loss is reduced in the workgroup and added
 // with a single atomic per workgroup.
 constexpr int MAXSEG = 16;
-constexpr int OPT_EPT = 8;                       // elements per thread
+constexpr int OPT_EPT = 2;                       // elements per thread (more, shorter blocks: latency)
 constexpr int OPT_CHUNK = TPB * OPT_EPT;         // elements per workgroup
 struct SegTable {
   OptSeg s[MAXSEG];
@@ -578,31 +578,24 @@ __global__ __launch_bounds__(TPB) void fused_opt_k(float* __restrict__ params, c
 //           mnist_input.py:288-290); order = weight losses..., cross_entropy, total_loss
 __global__ void finalize_k(int64_t* step, float* stats, float* l2, const float* wds, int nw, float* loss_ema,
                            int n_ema, int batch, int increment) {
-  if (threadIdx.x != 0) return;
+  // one wave; lane i owns loss entry i (weight losses..., cross_entropy, total_loss), so the
+  // EMA read-modify-writes run in parallel instead of as one dependent chain
+  const int t = threadIdx.x;
   const float ce = stats[0] / (float)batch;
   const float acc = stats[1] / (float)batch;
+  const float wl = t < nw ? wds[t] * 0.5f * (l2 ? l2[t] : 0.f) : 0.f;
   float total = ce;
-  for (int i = 0; i < nw; ++i) {
-    const float wl = wds[i] * 0.5f * (l2 ? l2[i] : 0.f);
-    total += wl;
-    if (loss_ema && i < n_ema) {
-      float* e = loss_ema + 3 * i;
-      e[0] = 0.9f * e[0] + 0.1f * wl;
-      e[1] += 1.f;
-      e[2] = e[0] / (1.f - powf(0.9f, e[1]));
-    }
-    if (l2) l2[i] = 0.f;
+  for (int i = 0; i < nw; ++i) total += __shfl(wl, i, 64);   // fixed order (bitwise as before)
+  if (loss_ema && t < n_ema && t < nw + 2) {
+    const float v = t < nw ? wl : (t == nw ? ce : total);
+    float* e = loss_ema + 3 * t;
+    const float b = 0.9f * e[0] + 0.1f * v, n = e[1] + 1.f;
+    e[0] = b;
+    e[1] = n;
+    e[2] = b / (1.f - powf(0.9f, n));
   }
-  if (loss_ema && n_ema >= nw + 2) {
-    float* e = loss_ema + 3 * nw;
-    e[0] = 0.9f * e[0] + 0.1f * ce;
-    e[1] += 1.f;
-    e[2] = e[0] / (1.f - powf(0.9f, e[1]));
-    e += 3;
-    e[0] = 0.9f * e[0] + 0.1f * total;
-    e[1] += 1.f;
-    e[2] = e[0] / (1.f - powf(0.9f, e[1]));
-  }
+  if (l2 && t < nw) l2[t] = 0.f;
+  if (t != 0) return;
   stats[4] = ce;
   stats[5] = acc;
   stats[6] = total;

@@ -22,6 +22,7 @@ import torch
 from ._ext import kernels
 
 BK = 32
+BK_WG = 32           # K rows per step of the split-K weight-gradient GEMMs (gemm.hip BK_WG)
 TARGET_BLOCKS = 2048   # ~8 workgroups per CU on 256 CUs
 
 
@@ -58,7 +59,7 @@ def pick_splits(M: int, N: int, K: int, target: int = TARGET_BLOCKS, min_k: int 
 
 def eff_splits(K: int, s: int) -> int:
     s = max(1, s)
-    kchunk = max(BK, (math.ceil(K / s) + BK - 1) // BK * BK)
+    kchunk = max(BK_WG, (math.ceil(K / s) + BK_WG - 1) // BK_WG * BK_WG)
     return math.ceil(K / kchunk)
 
 

@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--fused_input", type=int, default=0, help="first conv reads the uint8 dataset directly")
+    ap.add_argument("--overlap", default="none", choices=["none", "dense", "all"],
+                    help="weight gradients on a side stream: none / dense layers only / every layer")
     ap.add_argument("--dataset_size", type=int, default=60000)
     ap.add_argument("--phases", type=int, default=3,
                     help="extra eager steps AFTER the timed region, timed per phase with HIP events (0 = off)")
@@ -80,7 +82,8 @@ def main() -> int:
                     nesterov=args.optimizer == "nesterov", use_momentum=args.optimizer != "sgd", ema_max=0.9999)
     if args.impl == "hip":
         from distributed_tensorflow_ibm_mnist_amd.runtime.executor import HipNet
-        net = HipNet(spec, args.batch, dev, init, opt)
+        net = HipNet(spec, args.batch, dev, init, opt,
+                     overlap_backward={"none": False, "dense": "dense", "all": True}[args.overlap])
     else:
         from distributed_tensorflow_ibm_mnist_amd.runtime.torchnet import TorchNet
         net = TorchNet(spec, args.batch, dev, init, opt)

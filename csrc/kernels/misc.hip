@@ -143,63 +143,82 @@ __global__ void maxpool_bwd_k(const bf16_t* __restrict__ dy, const uint8_t* __re
 
 // ------------------------------------------------------------------ K7 LRN (TF semantics)
 // y[c] = x[c] * (bias + alpha * sum_{|c'-c|<=R} x[c']^2)^-beta
-// One thread per pixel, all C channels in registers; R is a compile-time
-// constant so the window sums are fully unrolled with static indices (no
-// runtime-guarded adds, no scratch).  Inputs stay bf16-packed in VGPRs.
-template <int C>
-DEV void load_row(const bf16_t* p, uint32_t (&w)[C / 2]) {
+// Channel-parallel: each lane owns 8 channels (one 16-byte vector) of a pixel, the
+// C/8 lanes of a pixel sit side by side inside one 16-lane DPP row, and the R
+// channels a window needs from the neighbouring vectors come over DPP row shifts
+// (zeroed at the pixel's first / last vector).  Loads and stores are fully
+// coalesced 16-byte vectors and a lane needs ~40 VGPRs (the one-pixel-per-lane form
+// held all C channels three times over: 2 waves/SIMD, 2-3x the HBM floor).
+DEV float dpp_from_left(float v) {   // lane i <- lane i-1 within its 16-lane row (0 at the row start)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, true));
+}
+DEV float dpp_from_right(float v) {  // lane i <- lane i+1 within its 16-lane row (0 at the row end)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x101, 0xf, 0xf, true));
+}
+
+// window sums over channels of the 8 values of this lane, with the R neighbours on
+// either side taken from the adjacent lanes of the same pixel (G lanes per pixel)
+template <int G, int R>
+DEV void lane_window_sums(const float (&v)[8], int c8, float (&s)[8]) {
+  static_assert(R <= 8 && 16 % G == 0, "neighbours must come from the adjacent lane of one DPP row");
+  float e[8 + 2 * R];
 #pragma unroll
-  for (int c8 = 0; c8 < C / 8; ++c8) {
-    const u32x4 u = *(const u32x4*)(p + c8 * 8);
-    w[4 * c8 + 0] = u[0];
-    w[4 * c8 + 1] = u[1];
-    w[4 * c8 + 2] = u[2];
-    w[4 * c8 + 3] = u[3];
+  for (int j = 0; j < 8; ++j) e[R + j] = v[j];
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    float l = dpp_from_left(v[8 - R + k]), r = dpp_from_right(v[k]);
+    if constexpr (G == 1) {
+      l = 0.f;
+      r = 0.f;
+    }
+    e[k] = c8 == 0 ? 0.f : l;
+    e[R + 8 + k] = c8 == G - 1 ? 0.f : r;
+  }
+  // sliding window: one full sum, then +entering -leaving (inputs are non-negative
+  // squares or same-scale products, so the running form loses nothing at bf16 output)
+  float a = 0.f;
+#pragma unroll
+  for (int d = 0; d <= 2 * R; ++d) a += e[d];
+  s[0] = a;
+#pragma unroll
+  for (int j = 1; j < 8; ++j) {
+    a += e[j + 2 * R] - e[j - 1];
+    s[j] = a;
   }
 }
 
-template <int C>
-DEV float unpk(const uint32_t (&w)[C / 2], int c) {
-  return (c & 1) ? __uint_as_float(w[c >> 1] & 0xffff0000u) : __uint_as_float(w[c >> 1] << 16);
-}
+// x^p for x > 0 as exp2(p log2 x): two transcendental ops, no ln/log2e rescaling
+DEV float powp(float x, float p) { return __builtin_amdgcn_exp2f(p * __builtin_amdgcn_logf(x)); }
 
-template <int C, int R>
-DEV void window_sums(const float (&v)[C], float (&s)[C]) {
+DEV void unpack8(const u32x4& u, float (&v)[8]) {
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
-    float a = 0.f;
-#pragma unroll
-    for (int d = -R; d <= R; ++d)
-      if (c + d >= 0 && c + d < C) a += v[c + d];
-    s[c] = a;
-  }
+  for (int j = 0; j < 8; ++j) v[j] = u4_get(u, j);
 }
 
 template <int C, int R>
 __global__ __launch_bounds__(TPB) void lrn_fwd_k(const bf16_t* __restrict__ x, int64_t P, float bias, float alpha,
                                                  float beta, bf16_t* __restrict__ y) {
-  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < P; p += (int64_t)gridDim.x * blockDim.x) {
-    uint32_t xw[C / 2];
-    load_row<C>(x + p * C, xw);
-    float sq[C], s[C];
+  constexpr int G = C / 8;
+  const int64_t total = P * G;   // one 8-channel vector per lane; whole pixels per wave
+  const int c8 = threadIdx.x % G;
+  // uniform trip count: every lane takes part in the DPP exchanges
+  for (int64_t base = (int64_t)blockIdx.x * TPB; base < total; base += (int64_t)gridDim.x * TPB) {
+    const int64_t t = base + threadIdx.x;
+    const bool ok = t < total;
+    const u32x4 xv = ok ? *(const u32x4*)(x + t * 8) : u32x4{0u, 0u, 0u, 0u};
+    float v[8], sq[8], s[8];
+    unpack8(xv, v);
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const float v = unpk<C>(xw, c);
-      sq[c] = v * v;
+    for (int j = 0; j < 8; ++j) sq[j] = v[j] * v[j];
+    lane_window_sums<G, R>(sq, c8, s);
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float a = v[2 * j] * powp(bias + alpha * s[2 * j], -beta);
+      const float b = v[2 * j + 1] * powp(bias + alpha * s[2 * j + 1], -beta);
+      o[j] = pack2(a, b);
     }
-    window_sums<C, R>(sq, s);
-#pragma unroll
-    for (int c8 = 0; c8 < C / 8; ++c8) {
-      u32x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = c8 * 8 + 2 * j;
-        const float a = unpk<C>(xw, c) * __expf(-beta * __logf(bias + alpha * s[c]));
-        const float b = unpk<C>(xw, c + 1) * __expf(-beta * __logf(bias + alpha * s[c + 1]));
-        o[j] = pack2(a, b);
-      }
-      *(u32x4*)(y + p * C + c8 * 8) = o;
-    }
+    if (ok) *(u32x4*)(y + t * 8) = o;
   }
 }
 
@@ -208,44 +227,42 @@ template <int C, int R>
 __global__ __launch_bounds__(TPB) void lrn_bwd_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                                                  int64_t P, float bias, float alpha, float beta, int relu_mask,
                                                  bf16_t* __restrict__ dx) {
-  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < P; p += (int64_t)gridDim.x * blockDim.x) {
-    uint32_t xw[C / 2], gw[C / 2];
-    load_row<C>(x + p * C, xw);
-    load_row<C>(dy + p * C, gw);
-    float t[C], s[C];
+  constexpr int G = C / 8;
+  const int64_t total = P * G;
+  const int c8 = threadIdx.x % G;
+  for (int64_t base = (int64_t)blockIdx.x * TPB; base < total; base += (int64_t)gridDim.x * TPB) {
+    const int64_t t = base + threadIdx.x;
+    const bool ok = t < total;
+    const u32x4 xv = ok ? *(const u32x4*)(x + t * 8) : u32x4{0u, 0u, 0u, 0u};
+    const u32x4 gv = ok ? *(const u32x4*)(dy + t * 8) : u32x4{0u, 0u, 0u, 0u};
+    float v[8], g[8], w[8], s[8], u[8];
+    unpack8(xv, v);
+    unpack8(gv, g);
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const float v = unpk<C>(xw, c);
-      t[c] = v * v;
+    for (int j = 0; j < 8; ++j) w[j] = v[j] * v[j];
+    lane_window_sums<G, R>(w, c8, s);             // s = window sum of x^2
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float sc = bias + alpha * s[j];
+      const float pw = powp(sc, -beta);               // sc^-beta
+      s[j] = pw;
+      w[j] = g[j] * v[j] * pw * __builtin_amdgcn_rcpf(sc);
     }
-    window_sums<C, R>(t, s);                       // s = window sum of x^2
+    lane_window_sums<G, R>(w, c8, u);
+    u32x4 o;
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const float sc = bias + alpha * s[c];
-      const float pw = __expf(-beta * __logf(sc));  // sc^-beta
-      s[c] = pw;                                     // keep sc^-beta
-      t[c] = unpk<C>(gw, c) * unpk<C>(xw, c) * pw / sc;
-    }
-    float u[C];
-    window_sums<C, R>(t, u);
+    for (int j = 0; j < 4; ++j) {
+      float r2[2];
 #pragma unroll
-    for (int c8 = 0; c8 < C / 8; ++c8) {
-      u32x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float r2[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int c = c8 * 8 + 2 * j + h;
-          const float xv = unpk<C>(xw, c);
-          float g = unpk<C>(gw, c) * s[c] - 2.f * alpha * beta * xv * u[c];
-          if (relu_mask && !(xv > 0.f)) g = 0.f;
-          r2[h] = g;
-        }
-        o[j] = pack2(r2[0], r2[1]);
+      for (int h = 0; h < 2; ++h) {
+        const int c = 2 * j + h;
+        float d = g[c] * s[c] - 2.f * alpha * beta * v[c] * u[c];
+        if (relu_mask && !(v[c] > 0.f)) d = 0.f;
+        r2[h] = d;
       }
-      *(u32x4*)(dx + p * C + c8 * 8) = o;
+      o[j] = pack2(r2[0], r2[1]);
     }
+    if (ok) *(u32x4*)(dx + t * 8) = o;
   }
 }
 
@@ -657,14 +674,14 @@ hipError_t maxpool_bwd(const bf16_t* dy, const uint8_t* arg, const bf16_t* y, in
 
 hipError_t lrn_fwd(const bf16_t* x, int P, int C, int r, float bias, float alpha, float beta, bf16_t* y,
                    hipStream_t st) {
-  dim3 grid(nblocks(P, TPB, 16384));
+  dim3 grid(nblocks((int64_t)P * (C / 8), TPB, 16384));   // one lane per 8-channel vector
   LRN_ALL(lrn_fwd_k, x, (int64_t)P, bias, alpha, beta, y)
   return hipErrorInvalidValue;  // (C, depth_radius) combination not instantiated
 }
 
 hipError_t lrn_bwd(const bf16_t* x, const bf16_t* dy, int P, int C, int r, float bias, float alpha, float beta,
                    int relu_mask, bf16_t* dx, hipStream_t st) {
-  dim3 grid(nblocks(P, TPB, 16384));
+  dim3 grid(nblocks((int64_t)P * (C / 8), TPB, 16384));
   LRN_ALL(lrn_bwd_k, x, dy, (int64_t)P, bias, alpha, beta, relu_mask, dx)
   return hipErrorInvalidValue;
 }

@@ -333,11 +333,15 @@ class HipNet:
         # scratch).  Off by default: at B=65536 every kernel already fills the 256 CUs and
         # concurrent kernels only time-slice (profiles/r1_overlap/); the serial plan is the
         # same code with one slab.
-        self.overlap = overlap_backward and dev.type == "cuda"
+        # overlap_backward="dense": only the dense weight gradients (latency-bound split-K
+        # GEMMs with little work per CU) fork to the side stream, beside the conv backward
+        # (measured 4 % SLOWER at B=65536 too: profiles/r1s2/ab_overlap_dense.txt).
+        self.overlap_dense_only = overlap_backward == "dense"
+        self.overlap = bool(overlap_backward) and dev.type == "cuda"
         # serial plan: every layer's split-K reduce is queued and flushed as ONE
         # multi-tensor launch per gradient bucket (``hook_layers``), so the layers
         # need disjoint slab regions, as with overlap
-        self.defer_reduce = not self.overlap
+        self.defer_reduce = not self.overlap or self.overlap_dense_only
         self.dbuf: List[Optional[torch.Tensor]] = [None] + [torch.zeros_like(l.out, dtype=torch.bfloat16)
                                                            for l in self.layers[:-1]]
         sizes = [(getattr(l, "slab_elems", 0) + 3) // 4 * 4 for l in self.layers]
@@ -447,7 +451,8 @@ class HipNet:
         waits on exactly that work.  Joins before returning."""
         nb = self.B if nb is None else nb
         dy = self.dlogits
-        pending: list = []
+        pending: list = []          # split-K reduces queued on the main stream
+        side_pending: list = []     # ... and on the side stream
         main = torch.cuda.current_stream(self.device) if self.overlap else None
         if self.overlap:
             self.side.wait_stream(main)
@@ -457,13 +462,15 @@ class HipNet:
             if lay.has_params:
                 # the first layer has no data gradient: its weight gradient IS the tail of
                 # the critical path, so it runs on the main stream while the side drains
-                if self.overlap and i > 0:
+                if self.overlap and i > 0 and (not self.overlap_dense_only or isinstance(lay, DenseLayer)):
                     self.ev_dy[i].record(main)
                     self.side.wait_event(self.ev_dy[i])
                     with torch.cuda.stream(self.side):
-                        lay.bwd_weight(nb, dy, self.slabs[i])
-                        for h in self.grad_ready_hooks:
-                            h(lay.idx)
+                        lay.bwd_weight(nb, dy, self.slabs[i], side_pending)
+                        if self.grad_ready_hooks and (self.hook_layers is None or lay.idx in self.hook_layers):
+                            self._flush_reduce(side_pending)
+                            for h in self.grad_ready_hooks:
+                                h(lay.idx)
                 elif self.defer_reduce:
                     lay.bwd_weight(nb, dy, self.slabs[i], pending)
                     if self.grad_ready_hooks and (self.hook_layers is None or lay.idx in self.hook_layers):
@@ -480,6 +487,8 @@ class HipNet:
         self._head_grads = False
         self._flush_reduce(pending)
         if self.overlap:
+            with torch.cuda.stream(self.side):
+                self._flush_reduce(side_pending)
             main.wait_stream(self.side)
 
     @staticmethod

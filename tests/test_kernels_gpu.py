@@ -193,11 +193,14 @@ def test_maxpool(dev, K, N, H, W, C):
     close(dx.float() * (x.float() > 0), g, rel=0)
 
 
-@pytest.mark.parametrize("C", [32, 64])
-def test_lrn(dev, K, C):
+@pytest.mark.parametrize("C,r,alpha", [(32, 4, 0.001 / 9.0), (64, 4, 0.001 / 9.0), (64, 4, 0.05), (32, 2, 0.05),
+                                       (64, 5, 0.05), (32, 5, 0.05), (16, 4, 0.05), (8, 4, 0.05)])
+def test_lrn(dev, K, C, r, alpha):
+    """Channel windows cross the 8-channel lane vectors (DPP neighbour exchange): a
+    large alpha makes every neighbour term visible; 5x13x13 pixels leave a partial wave."""
     torch.manual_seed(7)
-    r, bias, alpha, beta = 4, 1.0, 0.001 / 9.0, 0.75
-    x = (rnd(6, 14, 14, C, dev=dev, scale=3.0)).relu().to(torch.bfloat16)
+    bias, beta = 1.0, 0.75
+    x = (rnd(5, 13, 13, C, dev=dev, scale=3.0)).relu().to(torch.bfloat16)
     y = Fk.lrn(x, r, bias, alpha, beta)
     xn = x.float().permute(0, 3, 1, 2).requires_grad_(True)
     ref = lrn_tf(xn, r, bias, alpha, beta)

@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--overlap", default="none", choices=["none", "dense", "all"],
                     help="weight gradients on a side stream: none / dense layers only / every layer")
     ap.add_argument("--dataset_size", type=int, default=60000)
+    ap.add_argument("--dist_backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (production); gloo = host-staged rehearsal of the DP "
+                         "path with several ranks sharing one GPU (ranks map to device LOCAL_RANK %% count)")
     ap.add_argument("--phases", type=int, default=3,
                     help="extra eager steps AFTER the timed region, timed per phase with HIP events (0 = off)")
     return ap.parse_args()
@@ -71,10 +74,13 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     spec = get_model(args.model, args.in_channels)
     init = init_params(spec, seed=args.seed)
@@ -134,6 +140,13 @@ def main() -> int:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     el = float(elapsed.item())
     stats = net.read_stats()
+    in_sync = None
+    if world > 1:                           # outside the timed region: replicas must hold identical weights
+        ck = net.fp.params.double().sum().reshape(1)
+        lo, hi = ck.clone(), ck.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        in_sync = bool((hi - lo).abs().item() == 0.0)
     phases = None
     if args.phases > 0:                     # outside the timed region: per-phase breakdown of an eager step
         from distributed_tensorflow_ibm_mnist_amd.runtime.timers import PhaseTimer
@@ -167,6 +180,7 @@ def main() -> int:
                 "per_gpu_batch": args.batch,
                 "seq_len": None,
                 "parallelism": f"dp{world}",
+                "dist_backend": args.dist_backend if world > 1 else None,
                 "impl": args.impl,
                 "hip_graph": use_graph,
                 "optimizer": args.optimizer,
@@ -174,6 +188,7 @@ def main() -> int:
             "tflops_per_s": round(tot * value / 1e12, 2),
             "final_train_loss": round(stats["cross_entropy"], 5),
             "phase_ms_eager": phases,
+            "replicas_in_sync": in_sync,
             "grad_bucket_mb": [round(b.nbytes / 2 ** 20, 3) for b in dp.buckets] if world > 1 else None,
         }
         print(json.dumps(out), flush=True)

@@ -72,13 +72,13 @@ def pick_device(rank: int, want_gpu: bool) -> torch.device:
         return torch.device("cpu")
     lr = os.environ.get("LOCAL_RANK")
     n = torch.cuda.device_count()
-    idx = int(lr) if lr is not None else rank % max(n, 1)
-    return torch.device("cuda", idx)
+    idx = int(lr) if lr is not None else rank
+    return torch.device("cuda", idx % max(n, 1))   # several ranks may share a GPU (gloo rehearsal)
 
 
 def setup_distribute(job_name: str = "", ps_hosts: str = "", worker_hosts: str = "", task_id: int = 0,
                      want_gpu: bool = True, timeout_s: float = 600.0, log=print,
-                     ps_backend: str = "") -> Cluster:
+                     ps_backend: str = "", dp_backend: str = "") -> Cluster:
     ps, workers = _split(ps_hosts), _split(worker_hosts)
     env_world = int(os.environ.get("WORLD_SIZE", "1"))
     to = datetime.timedelta(seconds=timeout_s)
@@ -103,6 +103,8 @@ def setup_distribute(job_name: str = "", ps_hosts: str = "", worker_hosts: str =
             cl.master = _norm_host(workers[0])
         cl.device = pick_device(cl.rank, want_gpu)
         cl.backend = "nccl" if cl.device.type == "cuda" else "gloo"
+        if cl.mode == "dp" and dp_backend:
+            cl.backend = dp_backend
         if cl.mode == "ps" and ps_backend:
             # gloo stages GPU tensors through host memory: lets several PS-mode
             # processes share one GPU (RCCL needs one rank per GPU)
@@ -117,7 +119,7 @@ def setup_distribute(job_name: str = "", ps_hosts: str = "", worker_hosts: str =
         rank = int(os.environ.get("RANK", "0"))
         cl = Cluster("dp", "worker", rank, [], [], rank=rank, world=env_world, num_workers=env_world)
         cl.device = pick_device(rank, want_gpu)
-        cl.backend = "nccl" if cl.device.type == "cuda" else "gloo"
+        cl.backend = dp_backend or ("nccl" if cl.device.type == "cuda" else "gloo")
         if cl.device.type == "cuda":
             torch.cuda.set_device(cl.device)
         kw = {"device_id": cl.device} if cl.backend == "nccl" else {}

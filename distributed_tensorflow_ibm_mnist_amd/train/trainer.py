@@ -85,7 +85,8 @@ def train(FLAGS, log=print) -> Dict[str, float]:
     if impl == "hip" and not torch.cuda.is_available():
         raise RuntimeError("--impl=hip needs an MI355X (HIP device); use --impl=torch for the CPU path")
     cl = setup_distribute(FLAGS.job_name, FLAGS.ps_hosts, FLAGS.worker_hosts, FLAGS.task_id, want_gpu=want_gpu,
-                          timeout_s=FLAGS.collective_timeout, log=log, ps_backend=FLAGS.ps_backend)
+                          timeout_s=FLAGS.collective_timeout, log=log, ps_backend=FLAGS.ps_backend,
+                          dp_backend=FLAGS.dp_backend)
     try:
         return _train(FLAGS, cl, max_steps, test_interval, batch_size, impl, log)
     finally:

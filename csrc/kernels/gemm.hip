@@ -233,10 +233,23 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEp
   const int wm = wave / WN, wn = wave % WN;
 
   const int tiles_mn = gridDim.x;
-  const int t = xcd_remap(blockIdx.x, tiles_mn);
+  // Split-K launches remap the whole 2-D grid: blocks are dealt round-robin over the
+  // 8 XCDs by linear id, so a plain (tile, split) grid scatters the tiles of one split
+  // -- which all read the same K rows of both operands -- over every XCD.  Remapped,
+  // consecutive logical ids (the tiles of a split, then the next split) share one
+  // XCD's L2 and each K slab is fetched from HBM about once instead of once per tile.
+  int t, split;
+  if (gridDim.y > 1) {
+    const int lin = xcd_remap(blockIdx.y * tiles_mn + blockIdx.x, tiles_mn * gridDim.y);
+    split = lin / tiles_mn;
+    t = lin - split * tiles_mn;
+  } else {
+    t = xcd_remap(blockIdx.x, tiles_mn);
+    split = 0;
+  }
   const int m0 = (t / tiles_n) * BM;
   const int n0 = (t % tiles_n) * BN;
-  const int kbeg = blockIdx.y * kchunk;
+  const int kbeg = split * kchunk;
   const int kend = min(K, kbeg + kchunk);
   const int nsteps = (kend - kbeg + KB - 1) / KB;
 
@@ -360,7 +373,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEp
         if (m < M && n < N) {
           f32x4 lo = *(const f32x4*)(eb + rr * EP_LD + cv), hi = *(const f32x4*)(eb + rr * EP_LD + cv + 4);
           if (ep.mode == EPI_SLAB) {
-            float* o = (float*)ep.out + (int64_t)blockIdx.y * ep.slab_stride + (int64_t)m * ep.ldc + n;
+            float* o = (float*)ep.out + (int64_t)split * ep.slab_stride + (int64_t)m * ep.ldc + n;
             *(f32x4*)o = lo;
             *(f32x4*)(o + 4) = hi;
             continue;
@@ -406,7 +419,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEp
         if (m >= M) continue;
         float v = acc[i][j][r];
         if (ep.mode == EPI_SLAB) {
-          float* o = (float*)ep.out + (int64_t)blockIdx.y * ep.slab_stride;
+          float* o = (float*)ep.out + (int64_t)split * ep.slab_stride;
           o[(int64_t)m * ep.ldc + n] = v;
           continue;
         }

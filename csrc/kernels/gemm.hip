@@ -31,6 +31,7 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <cstring>
 #include <type_traits>
 
 namespace mnistx {
@@ -42,6 +43,9 @@ constexpr int BK = 32;
 // B=65536: bench/micro_wgrad.py; reference conv2 wgrad 1.50 -> 1.74 ms): the 80 KB+
 // LDS images halve the resident blocks.  The knob stays for future tiles.
 constexpr int BK_WG = 32;
+// K steps kept in flight (VGPR prefetch slots) by the weight-gradient GEMMs.
+constexpr int WG_PF_DENSE = 4;
+constexpr int WG_PF_IM2COL = 2;
 template <bool AKC, bool BKC>
 constexpr int kstep() { return (!AKC && !BKC) ? BK_WG : BK; }
 
@@ -60,70 +64,122 @@ constexpr int kc_col(int k) { return 8 * ((k & 15) >> 2) + (k & 3) + 4 * (k >> 4
 // ---------------------------------------------------------------- loaders
 // load(r, c): 8 bf16 at memory coordinates (row r, cols c..c+7); zero outside.
 
-struct MatLoader {
+// Branch-free vector loads.  A loader whose result passes through a
+// data-dependent select or a per-lane branch (zero-fill, the bias ones-column)
+// makes the compiler wait for the load right there (s_waitcnt vmcnt(0) at the
+// join), which serialises the K-step prefetch -- every weight-gradient GEMM was
+// latency-bound on exactly that.  The vector loaders (V = true) issue ONE
+// unconditional buffer_load_dwordx4 per vector: an out-of-range element gets a
+// byte offset past the descriptor's num_records and the hardware returns zeros
+// without touching memory (a shared zero vector in HBM would funnel every padded
+// load onto one L2 channel).  The bias ones-column is OR-ed in by fix() at LDS
+// store time, where the value is waited for anyway.
+constexpr uint32_t OOB_OFF = 0x80000000u;   // > every num_records (vec_ok: < 2 GB)
+DEV __amdgpu_buffer_rsrc_t rsrc_of(const void* base, int64_t nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nbytes, 0x00020000);
+}
+DEV u32x4 bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+constexpr int64_t VEC_MAX_BYTES = (int64_t)1 << 31;
+
+template <bool V>
+struct MatLoaderT {
   const bf16_t* p;
   int R, C, ld;
   int ones_col;  // virtual column holding 1.0 (bias-gradient row), -1 = none
+  // whole 16-byte vectors; the ones column (if any) starts the vector past C
+  __host__ __device__ bool vec_ok() const {
+    return ((ld | C) & 7) == 0 && (ones_col < 0 || ones_col == C) && (int64_t)R * ld * 2 < VEC_MAX_BYTES;
+  }
   DEV u32x4 load(int r, int c) const {
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if (r >= R) return v;
-    const bf16_t* row = p + (int64_t)r * ld;
-    if (c + 8 <= C && (ld & 7) == 0) {
-      v = *(const u32x4*)(row + c);
+    if constexpr (V) {
+      const bool in = r < R && c < C;
+      return bload(rsrc_of(p, (int64_t)R * ld * 2), in ? (uint32_t)(r * ld + c) * 2u : OOB_OFF);
     } else {
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (r >= R) return v;
+      const bf16_t* row = p + (int64_t)r * ld;
+      if (c + 8 <= C && (ld & 7) == 0) {
+        v = *(const u32x4*)(row + c);
+      } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (c + j < C) u4_set(v, j, row[c + j]);
+        for (int j = 0; j < 8; ++j)
+          if (c + j < C) u4_set(v, j, row[c + j]);
+      }
+      if (ones_col >= c && ones_col < c + 8) u4_set(v, ones_col - c, (bf16_t)0x3f80);
+      return v;
     }
-    if (ones_col >= c && ones_col < c + 8) u4_set(v, ones_col - c, (bf16_t)0x3f80);
-    return v;
+  }
+  // vector path: the ones column is the first element of the vector at c == C
+  DEV void fix(u32x4& v, int r, int c) const {
+    if constexpr (V) {
+      if (c == ones_col && r < R) v[0] |= 0x3f80u;
+    }
   }
 };
+using MatLoader = MatLoaderT<false>;
+using MatLoaderV = MatLoaderT<true>;
+template <class L> struct IsMat : std::false_type {};
+template <bool V> struct IsMat<MatLoaderT<V>> : std::true_type {};
 
 // Implicit im2col, K-contiguous: row m = output pixel (n, oh, ow), col k = (kh, kw, ci).
-struct Im2colK {
+template <bool V>
+struct Im2colKT {
   const bf16_t* x;
   int H, W, C;          // input NHWC (C = channel stride)
   int OH, OW;           // output spatial
   int KH, KW, ph, pw;   // stride 1
   int M, K;
   FastDiv fOHW, fOW, fC, fKW;
+  __host__ __device__ int64_t nbytes() const { return (int64_t)(M / (OH * OW)) * H * W * C * 2; }
+  __host__ __device__ bool vec_ok() const { return (C & 7) == 0 && nbytes() < VEC_MAX_BYTES; }
   DEV u32x4 load(int m, int k) const {
     u32x4 v = {0u, 0u, 0u, 0u};
-    if (m >= M || k >= K) return v;
-    const int n = fOHW.div(m);
-    const int rem = fOHW.mod(m, n);
-    const int oh = fOW.div(rem);
-    const int ow = fOW.mod(rem, oh);
-    if ((C & 7) == 0) {
+    if constexpr (V) {                     // branch-free buffer load (see bload)
+      const bool ok = m < M && k < K;
+      m = ok ? m : 0;
+      k = ok ? k : 0;
+      const int n = fOHW.div(m);
+      const int rem = fOHW.mod(m, n);
+      const int oh = fOW.div(rem);
+      const int ow = fOW.mod(rem, oh);
       const int tap = fC.div(k);
       const int ci = fC.mod(k, tap);
       const int kh = fKW.div(tap);
       const int kw = fKW.mod(tap, kh);
       const int ih = oh - ph + kh, iw = ow - pw + kw;
-      if (ih < 0 || ih >= H || iw < 0 || iw >= W) return v;
-      return *(const u32x4*)(x + (((int64_t)n * H + ih) * W + iw) * C + ci);
-    }
-    const bf16_t* img = x + (int64_t)n * H * W * C;
+      const bool in = ok && ih >= 0 && ih < H && iw >= 0 && iw < W;
+      return bload(rsrc_of(x, nbytes()), in ? (uint32_t)((((n * H + ih) * W + iw) * C + ci) * 2) : OOB_OFF);
+    } else {
+      if (m >= M || k >= K) return v;
+      const int n = fOHW.div(m);
+      const int rem = fOHW.mod(m, n);
+      const int oh = fOW.div(rem);
+      const int ow = fOW.mod(rem, oh);
+      const bf16_t* img = x + (int64_t)n * H * W * C;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int kk = k + j;
-      if (kk < K) {
-        const int tap = kk / C;
-        const int ci = kk - tap * C;
-        const int kh = tap / KW;
-        const int kw = tap - kh * KW;
-        const int ih = oh - ph + kh, iw = ow - pw + kw;
-        if (ih >= 0 && ih < H && iw >= 0 && iw < W) u4_set(v, j, img[((int64_t)ih * W + iw) * C + ci]);
+      for (int j = 0; j < 8; ++j) {
+        const int kk = k + j;
+        if (kk < K) {
+          const int tap = kk / C;
+          const int ci = kk - tap * C;
+          const int kh = tap / KW;
+          const int kw = tap - kh * KW;
+          const int ih = oh - ph + kh, iw = ow - pw + kw;
+          if (ih >= 0 && ih < H && iw >= 0 && iw < W) u4_set(v, j, img[((int64_t)ih * W + iw) * C + ci]);
+        }
       }
+      return v;
     }
-    return v;
   }
+  DEV void fix(u32x4&, int, int) const {}
 };
 
 // Implicit im2col, MN-contiguous (conv weight gradient): row = pixel p (reduction),
 // col = m = (kh, kw, ci); column Mreal is a virtual 1.0 (bias gradient).
-struct Im2colMN {
+template <bool V>
+struct Im2colMNT {
   const bf16_t* x;
   int H, W, C;
   int OH, OW;
@@ -131,22 +187,30 @@ struct Im2colMN {
   int P, Mreal;
   int ones;  // 1: append the ones column at Mreal
   FastDiv fOHW, fOW, fC, fKW;
+  __host__ __device__ int64_t nbytes() const { return (int64_t)(P / (OH * OW)) * H * W * C * 2; }
+  __host__ __device__ bool vec_ok() const { return ((C | Mreal) & 7) == 0 && nbytes() < VEC_MAX_BYTES; }
   DEV u32x4 load(int p, int m) const {
     u32x4 v = {0u, 0u, 0u, 0u};
-    if (p >= P) return v;
-    const int n = fOHW.div(p);
-    const int rem = fOHW.mod(p, n);
-    const int oh = fOW.div(rem);
-    const int ow = fOW.mod(rem, oh);
-    if ((C & 7) == 0 && m + 8 <= Mreal) {
-      const int tap = fC.div(m);
-      const int ci = fC.mod(m, tap);
+    if constexpr (V) {                     // branch-free buffer load; ones column: fix()
+      const bool pin = p < P, min_ = m < Mreal;
+      const int pp = pin ? p : 0, mm = min_ ? m : 0;
+      const int n = fOHW.div(pp);
+      const int rem = fOHW.mod(pp, n);
+      const int oh = fOW.div(rem);
+      const int ow = fOW.mod(rem, oh);
+      const int tap = fC.div(mm);
+      const int ci = fC.mod(mm, tap);
       const int kh = fKW.div(tap);
       const int kw = fKW.mod(tap, kh);
       const int ih = oh - ph + kh, iw = ow - pw + kw;
-      if (ih >= 0 && ih < H && iw >= 0 && iw < W)
-        v = *(const u32x4*)(x + (((int64_t)n * H + ih) * W + iw) * C + ci);
+      const bool in = pin && min_ && ih >= 0 && ih < H && iw >= 0 && iw < W;
+      return bload(rsrc_of(x, nbytes()), in ? (uint32_t)((((n * H + ih) * W + iw) * C + ci) * 2) : OOB_OFF);
     } else {
+      if (p >= P) return v;
+      const int n = fOHW.div(p);
+      const int rem = fOHW.mod(p, n);
+      const int oh = fOW.div(rem);
+      const int ow = fOW.mod(rem, oh);
       const bf16_t* img = x + (int64_t)n * H * W * C;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -160,9 +224,14 @@ struct Im2colMN {
           if (ih >= 0 && ih < H && iw >= 0 && iw < W) u4_set(v, j, img[((int64_t)ih * W + iw) * C + ci]);
         }
       }
+      if (ones && Mreal >= m && Mreal < m + 8) u4_set(v, Mreal - m, (bf16_t)0x3f80);
+      return v;
     }
-    if (ones && Mreal >= m && Mreal < m + 8) u4_set(v, Mreal - m, (bf16_t)0x3f80);
-    return v;
+  }
+  DEV void fix(u32x4& v, int p, int m) const {
+    if constexpr (V) {
+      if (ones && m == Mreal && p < P) v[0] |= 0x3f80u;
+    }
   }
 };
 
@@ -172,15 +241,21 @@ struct WFlipK {
   const bf16_t* w;  // [T][Cin_p][Cout_p]
   int T, Cin, Cout;
   FastDiv fCout;
-  DEV u32x4 load(int ci, int k) const {
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if (ci >= Cin || k >= T * Cout) return v;
+  __host__ __device__ bool vec_ok() const { return (int64_t)T * Cin * Cout * 2 < VEC_MAX_BYTES; }
+  DEV u32x4 load(int ci, int k) const {   // branch-free buffer load (see bload)
+    const bool in = ci < Cin && k < T * Cout;
+    k = in ? k : 0;
     const int tp = fCout.div(k);
     const int co = fCout.mod(k, tp);
     const int tap = T - 1 - tp;
-    return *(const u32x4*)(w + ((int64_t)tap * Cin + ci) * Cout + co);
+    return bload(rsrc_of(w, (int64_t)T * Cin * Cout * 2), in ? (uint32_t)(((tap * Cin + ci) * Cout + co) * 2) : OOB_OFF);
   }
+  DEV void fix(u32x4&, int, int) const {}
 };
+using Im2colK = Im2colKT<false>;
+using Im2colKV = Im2colKT<true>;
+using Im2colMN = Im2colMNT<false>;
+using Im2colMNV = Im2colMNT<true>;
 
 // ---------------------------------------------------------------- fragment reads
 
@@ -212,7 +287,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEp
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   static_assert(FM >= 1 && FN >= 1, "wave tile too small");
-  constexpr bool DENSE = std::is_same<LA, MatLoader>::value && std::is_same<LB, MatLoader>::value;
+  constexpr bool DENSE = IsMat<LA>::value && IsMat<LB>::value;
   constexpr int KB = kstep<AKC, BKC>();                 // rows of K staged per step
   constexpr int SA = ImgStride<AKC ? BK : BM, AKC, DENSE>::value;
   constexpr int SB = ImgStride<BKC ? BK : BN, BKC, DENSE>::value;
@@ -228,6 +303,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEp
 #define Bs(b) (smem + 2 * A_ELEMS + (b) * B_ELEMS)
 
   const int tid = threadIdx.x;
+  if (tid >= NT) __builtin_unreachable();   // lets hipcc drop the v < A_VEC guards when A_VEC % NT == 0
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -253,33 +329,40 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEp
   const int kend = min(K, kbeg + kchunk);
   const int nsteps = (kend - kbeg + KB - 1) / KB;
 
-  u32x4 ra[A_VPT], rb[B_VPT];
+  // Prefetch depth (K steps in flight in VGPRs).  Weight gradients have a small
+  // output, so few workgroups per CU: with one step in flight a CU keeps only
+  // ~4 x 8 KB of loads outstanding and the split-K GEMMs ran at a fraction of HBM
+  // bandwidth, latency-bound.  PF slots let each block keep PF steps in flight.
+  constexpr int PF = (!AKC && !BKC) ? (DENSE ? WG_PF_DENSE : WG_PF_IM2COL) : 1;
+  u32x4 ra[PF][A_VPT], rb[PF][B_VPT];
 
-  auto gload = [&](int k0) {
+  // K index past the split's end: every loader returns zeros for it (out of range)
+  constexpr int KOOB = 0x3fffffff;
+  // Every load is unconditional (vectors past A_VEC/B_VEC re-load a valid one and
+  // are simply not stored): a load under a per-lane branch leaves the compiler's
+  // vmcnt bookkeeping with two paths to merge, and it falls back to waiting for
+  // everything, which serialises the prefetch.
+  auto gload = [&](int slot, int k0) {
 #pragma unroll
     for (int u = 0; u < A_VPT; ++u) {
-      const int v = tid + u * NT;
-      if (v < A_VEC) {
-        if (AKC) {
-          const int r = v / (BK / 8), c = (v % (BK / 8)) * 8;
-          ra[u] = (k0 + c < kend) ? la.load(m0 + r, k0 + c) : u32x4{0u, 0u, 0u, 0u};
-        } else {
-          const int r = v / (BM / 8), c = (v % (BM / 8)) * 8;
-          ra[u] = (k0 + r < kend) ? la.load(k0 + r, m0 + c) : u32x4{0u, 0u, 0u, 0u};
-        }
+      const int v = (A_VEC % NT == 0) ? tid + u * NT : (tid + u * NT) % A_VEC;
+      if (AKC) {
+        const int r = v / (BK / 8), c = (v % (BK / 8)) * 8;
+        ra[slot][u] = la.load(m0 + r, k0 + c < kend ? k0 + c : KOOB);
+      } else {
+        const int r = v / (BM / 8), c = (v % (BM / 8)) * 8;
+        ra[slot][u] = la.load(k0 + r < kend ? k0 + r : KOOB, m0 + c);
       }
     }
 #pragma unroll
     for (int u = 0; u < B_VPT; ++u) {
-      const int v = tid + u * NT;
-      if (v < B_VEC) {
-        if (BKC) {
-          const int r = v / (BK / 8), c = (v % (BK / 8)) * 8;
-          rb[u] = (k0 + c < kend) ? lb.load(n0 + r, k0 + c) : u32x4{0u, 0u, 0u, 0u};
-        } else {
-          const int r = v / (BN / 8), c = (v % (BN / 8)) * 8;
-          rb[u] = (k0 + r < kend) ? lb.load(k0 + r, n0 + c) : u32x4{0u, 0u, 0u, 0u};
-        }
+      const int v = (B_VEC % NT == 0) ? tid + u * NT : (tid + u * NT) % B_VEC;
+      if (BKC) {
+        const int r = v / (BK / 8), c = (v % (BK / 8)) * 8;
+        rb[slot][u] = lb.load(n0 + r, k0 + c < kend ? k0 + c : KOOB);
+      } else {
+        const int r = v / (BN / 8), c = (v % (BN / 8)) * 8;
+        rb[slot][u] = lb.load(k0 + r < kend ? k0 + r : KOOB, n0 + c);
       }
     }
   };
@@ -290,21 +373,38 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEp
     *(u32x2*)(row + kc_col(8 * vq)) = u32x2{x[0], x[1]};
     *(u32x2*)(row + kc_col(8 * vq + 4)) = u32x2{x[2], x[3]};
   };
-  auto sstore = [&](int buf) {
+  // fix(): loader post-processing of a waited-for vector (the bias ones column)
+  auto sstore = [&](int slot, int buf, int k0) {
 #pragma unroll
     for (int u = 0; u < A_VPT; ++u) {
       const int v = tid + u * NT;
       if (v < A_VEC) {
-        if (AKC) kc_store(As(buf), SA, v, ra[u]);
-        else *(u32x4*)(As(buf) + (v / (BM / 8)) * SA + (v % (BM / 8)) * 8) = ra[u];
+        u32x4 x = ra[slot][u];
+        if (AKC) {
+          const int r = v / (BK / 8), c = (v % (BK / 8)) * 8;
+          la.fix(x, m0 + r, k0 + c < kend ? k0 + c : KOOB);
+          kc_store(As(buf), SA, v, x);
+        } else {
+          const int r = v / (BM / 8), c = (v % (BM / 8)) * 8;
+          la.fix(x, k0 + r < kend ? k0 + r : KOOB, m0 + c);
+          *(u32x4*)(As(buf) + r * SA + c) = x;
+        }
       }
     }
 #pragma unroll
     for (int u = 0; u < B_VPT; ++u) {
       const int v = tid + u * NT;
       if (v < B_VEC) {
-        if (BKC) kc_store(Bs(buf), SB, v, rb[u]);
-        else *(u32x4*)(Bs(buf) + (v / (BN / 8)) * SB + (v % (BN / 8)) * 8) = rb[u];
+        u32x4 x = rb[slot][u];
+        if (BKC) {
+          const int r = v / (BK / 8), c = (v % (BK / 8)) * 8;
+          lb.fix(x, n0 + r, k0 + c < kend ? k0 + c : KOOB);
+          kc_store(Bs(buf), SB, v, x);
+        } else {
+          const int r = v / (BN / 8), c = (v % (BN / 8)) * 8;
+          lb.fix(x, k0 + r < kend ? k0 + r : KOOB, n0 + c);
+          *(u32x4*)(Bs(buf) + r * SB + c) = x;
+        }
       }
     }
   };
@@ -316,33 +416,47 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEp
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (nsteps > 0) {
-    gload(kbeg);
-    sstore(0);
+    // Steps are padded to a multiple of PF (the pad steps read zeros: KOOB) so the
+    // loop body has no data-dependent exits; loads and LDS stores are issued
+    // unconditionally, which keeps hipcc's vmcnt waits counted (it waits only for
+    // the slot it is about to store, not for the loads just issued).
+    const int nsp = (nsteps + PF - 1) / PF * PF;
+    // slots 0..PF-1 <- steps 0..PF-1; step 0 -> LDS buffer 0
+#pragma unroll
+    for (int p = 0; p < PF; ++p) gload(p, kbeg + p * KB);
+    sstore(0, 0, kbeg);
     __syncthreads();
-    for (int s = 0; s < nsteps; ++s) {
-      const int cur = s & 1;
-      if (s + 1 < nsteps) gload(kbeg + (s + 1) * KB);
+    // step s = s0 + p lives in slot p (statically indexed: the loop is unrolled by PF).
+    // Its slot was drained into LDS at the end of step s-1, so the load of step
+    // s + PF reuses it before step s computes.
+    for (int s0 = 0; s0 < nsp; s0 += PF) {
 #pragma unroll
-      for (int kb = 0; kb < KB; kb += BK) {
-        bf16x8 af[FM], bfr[FN];
+      for (int p = 0; p < PF; ++p) {
+        const int s = s0 + p;
+        const int cur = s & 1;
+        gload(p, kbeg + (s + PF) * KB);   // past the end: zeros (KOOB), never stored
 #pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          const int r0 = wm * TM + i * 16;
-          af[i] = AKC ? frag_kc<SA>(As(cur), r0, kb, lane) : frag_tr<SA>(As(cur), r0, kb, lane);
+        for (int kb = 0; kb < KB; kb += BK) {
+          bf16x8 af[FM], bfr[FN];
+#pragma unroll
+          for (int i = 0; i < FM; ++i) {
+            const int r0 = wm * TM + i * 16;
+            af[i] = AKC ? frag_kc<SA>(As(cur), r0, kb, lane) : frag_tr<SA>(As(cur), r0, kb, lane);
+          }
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int c0 = wn * TN + j * 16;
+            bfr[j] = BKC ? frag_kc<SB>(Bs(cur), c0, kb, lane) : frag_tr<SB>(Bs(cur), c0, kb, lane);
+          }
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         }
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int c0 = wn * TN + j * 16;
-          bfr[j] = BKC ? frag_kc<SB>(Bs(cur), c0, kb, lane) : frag_tr<SB>(Bs(cur), c0, kb, lane);
-        }
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        sstore((p + 1) % PF, cur ^ 1, kbeg + (s + 1) * KB);
+        __syncthreads();
       }
-      if (s + 1 < nsteps) sstore(cur ^ 1);
-      __syncthreads();
     }
   }
 
@@ -497,6 +611,22 @@ hipError_t launch_any(const LA& la, const LB& lb, const GemmEpi& ep, int M, int 
   return hipErrorInvalidValue;
 }
 
+// Vector loaders (VA/VB: same fields as LA/LB) when both operands qualify; the
+// general loaders otherwise, with one fixed tile (odd shapes are not hot paths).
+template <class VA, class VB, bool AKC, bool BKC, class LA, class LB>
+hipError_t launch_pick(const LA& la, const LB& lb, const GemmEpi& ep, int M, int N, int K, int splits,
+                       hipStream_t st, int code = -1) {
+  if (la.vec_ok() && lb.vec_ok()) {
+    VA va;
+    VB vb;
+    static_assert(sizeof(VA) == sizeof(LA) && sizeof(VB) == sizeof(LB), "vector loaders mirror the general ones");
+    memcpy((void*)&va, (const void*)&la, sizeof(LA));
+    memcpy((void*)&vb, (const void*)&lb, sizeof(LB));
+    return launch_any<VA, AKC, VB, BKC>(va, vb, ep, M, N, K, splits, st, code);
+  }
+  return launch_cfg<64, 64, 2, 2, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- public launchers
@@ -512,7 +642,7 @@ hipError_t dense_fwd(const bf16_t* x, const bf16_t* w, int M, int N, int K, int 
                      const GemmEpi& ep, hipStream_t st) {
   MatLoader a{x, M, K, ldx, -1};
   MatLoader b{w, K, N, ldw, -1};
-  return launch_any<MatLoader, true, MatLoader, false>(a, b, ep, M, N, K, 1, st);
+  return launch_pick<MatLoaderV, MatLoaderV, true, false>(a, b, ep, M, N, K, 1, st);
 }
 
 hipError_t dense_dgrad(const bf16_t* dy, const bf16_t* w, int M, int N, int K, int lddy, int ldw,
@@ -520,7 +650,7 @@ hipError_t dense_dgrad(const bf16_t* dy, const bf16_t* w, int M, int N, int K, i
   // dX[M, N=Din] = dY[M, K=Dout] . W[Din, Dout]^T  ; B(k, n) = W[n][k]  (K-contiguous rows n)
   MatLoader a{dy, M, K, lddy, -1};
   MatLoader b{w, N, K, ldw, -1};
-  return launch_any<MatLoader, true, MatLoader, true>(a, b, ep, M, N, K, 1, st);
+  return launch_pick<MatLoaderV, MatLoaderV, true, true>(a, b, ep, M, N, K, 1, st);
 }
 
 hipError_t dense_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int B, int ldx, int lddy,
@@ -529,7 +659,7 @@ hipError_t dense_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int
   MatLoader a{x, B, Din, ldx, with_bias ? Din : -1};
   MatLoader b{dy, B, Dout, lddy, -1};
   const int M = Din + (with_bias ? 1 : 0);
-  return launch_any<MatLoader, false, MatLoader, false>(a, b, ep, M, Dout, B, splits, st, tile);
+  return launch_pick<MatLoaderV, MatLoaderV, false, false>(a, b, ep, M, Dout, B, splits, st, tile);
 }
 
 hipError_t conv_fwd(const bf16_t* x, const bf16_t* w, int Nb, int H, int W, int C, int OH, int OW, int KH,
@@ -538,7 +668,7 @@ hipError_t conv_fwd(const bf16_t* x, const bf16_t* w, int Nb, int H, int W, int 
   Im2colK a{x, H, W, C, OH, OW, KH, KW, ph, pw, M, K,
             FastDiv(OH * OW), FastDiv(OW), FastDiv(C), FastDiv(KW)};
   MatLoader b{w, K, Cout, Cout, -1};
-  return launch_any<Im2colK, true, MatLoader, false>(a, b, ep, M, Cout, K, 1, st);
+  return launch_pick<Im2colKV, MatLoaderV, true, false>(a, b, ep, M, Cout, K, 1, st);
 }
 
 hipError_t conv_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int OH, int OW, int Cout, int H, int W,
@@ -548,7 +678,7 @@ hipError_t conv_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int OH, int OW,
   Im2colK a{dy, OH, OW, Cout, H, W, KH, KW, KH - 1 - ph, KW - 1 - pw, M, K,
             FastDiv(H * W), FastDiv(W), FastDiv(Cout), FastDiv(KW)};
   WFlipK b{w, KH * KW, Cin, Cout, FastDiv(Cout)};
-  return launch_any<Im2colK, true, WFlipK, true>(a, b, ep, M, Cin, K, 1, st);
+  return launch_pick<Im2colKV, WFlipK, true, true>(a, b, ep, M, Cin, K, 1, st);
 }
 
 hipError_t conv_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int H, int W, int C, int OH, int OW, int KH,
@@ -558,8 +688,8 @@ hipError_t conv_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int H, int W, i
   Im2colMN a{x, H, W, C, OH, OW, KH, KW, ph, pw, P, Mreal, with_bias,
              FastDiv(OH * OW), FastDiv(OW), FastDiv(C), FastDiv(KW)};
   MatLoader b{dy, P, Cout, Cout, -1};
-  return launch_any<Im2colMN, false, MatLoader, false>(a, b, ep, Mreal + (with_bias ? 1 : 0), Cout, P, splits,
-                                                       st);
+  return launch_pick<Im2colMNV, MatLoaderV, false, false>(a, b, ep, Mreal + (with_bias ? 1 : 0), Cout, P, splits,
+                                                          st);
 }
 
 }  // namespace mnistx

@@ -577,7 +577,9 @@ int tile_code(int M, int N, bool wgrad) {
   if (wgrad) {
     if (N <= 16) return T64x16;
     if (N <= 32) return T64x32;
-    if (N <= 64 || tiles(128, 128) < 256) return T64x64;
+    if (N <= 64) return T64x64;
+    if (N <= 128) return M >= 256 ? T64x128 : T64x64;   // whole N per tile: M operand read once
+    if (tiles(128, 128) < 256) return T64x64;
     return T128x128;
   }
   if (N <= 16) return tiles(256, 16) >= 1024 ? T256x16 : T64x16;

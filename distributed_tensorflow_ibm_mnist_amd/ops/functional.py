@@ -15,6 +15,7 @@ static arena (and under hipGraph capture); tests call them allocation-style.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -23,8 +24,15 @@ from ._ext import kernels
 
 BK = 32
 BK_WG = 32           # K rows per step of the split-K weight-gradient GEMMs (gemm.hip BK_WG)
-TARGET_BLOCKS = 2048   # ~8 workgroups per CU on 256 CUs
-
+# Split-K target for weight-gradient GEMMs (workgroups per launch): ~8 per CU.
+TARGET_BLOCKS = 2048
+# Dense weight gradients with only a few output tiles (LeNet fc3/fc4/fc5) aim for
+# ~2 per CU instead: with the counted-vmcnt 4-deep prefetch (gemm.hip) a block
+# keeps its own loads in flight, and fewer splits mean a smaller fp32 slab to
+# reduce (fc3 at B=65536: S=64 24.9 us vs S=147 ~34 us; LeNet-5 step 0.761 ->
+# 0.744 ms).  Gather-bound im2col weight gradients and many-tile dense ones
+# (reference CNN conv2 / local3) measured faster at 2048 (4.16 vs 4.78 ms/step).
+TARGET_BLOCKS_FEW_TILES = int(os.environ.get("MNISTX_WGRAD_BLOCKS", "512"))
 
 def pad8(c: int) -> int:
     return (c + 7) // 8 * 8
@@ -39,7 +47,11 @@ def gemm_tile(M: int, N: int) -> Tuple[int, int]:
         return 64, 16
     if N <= 32:
         return 64, 32
-    if N <= 64 or math.ceil(M / 128) * math.ceil(N / 128) < 256:
+    if N <= 64:
+        return 64, 64
+    if N <= 128:        # the whole N in one tile: the M operand is read once
+        return (64, 128) if M >= 256 else (64, 64)
+    if math.ceil(M / 128) * math.ceil(N / 128) < 256:
         return 64, 64
     return 128, 128
 
@@ -47,11 +59,15 @@ def gemm_tile(M: int, N: int) -> Tuple[int, int]:
 SLAB_CAP = 16 << 20   # fp32 elements of split-K partials (64 MB)
 
 
-def pick_splits(M: int, N: int, K: int, target: int = TARGET_BLOCKS, min_k: int = 256) -> int:
-    """Split-K factor for a weight-gradient GEMM: fill ~8 WGs/CU, but keep every
-    split >= min_k reduction elements and the fp32 slab under SLAB_CAP."""
+def pick_splits(M: int, N: int, K: int, target: Optional[int] = None, min_k: int = 256,
+                dense: bool = False) -> int:
+    """Split-K factor for a weight-gradient GEMM: fill the CUs (``target``
+    workgroups), but keep every split >= min_k reduction elements and the fp32
+    slab under SLAB_CAP."""
     bm, bn = gemm_tile(M, N)
     tiles = math.ceil(M / bm) * math.ceil(N / bn)
+    if target is None:
+        target = TARGET_BLOCKS_FEW_TILES if (dense and tiles < 64) else TARGET_BLOCKS
     s = max(1, math.ceil(target / tiles))
     s = min(s, max(1, K // min_k), max(1, SLAB_CAP // max(1, M * N)))
     return eff_splits(K, s)
@@ -173,7 +189,7 @@ def dense_wgrad(x: torch.Tensor, dy: torch.Tensor, din: int, dout: int, with_bia
     B, Dp = x.shape
     _, Np = dy.shape
     M = Dp + (1 if with_bias else 0)
-    S = pick_splits(M, Np, B) if splits is None else eff_splits(B, splits)
+    S = pick_splits(M, Np, B, dense=True) if splits is None else eff_splits(B, splits)
     if slab is None:
         slab = torch.empty(S * M * Np, dtype=torch.float32, device=x.device)
     K = kernels()

@@ -219,7 +219,7 @@ class DenseLayer(_Layer):
         self.out = torch.zeros(B, self.Np, dtype=torch.float32 if last else torch.bfloat16, device=dev)
         self.wname, self.bname = f"{spec.name}/weights", f"{spec.name}/biases"
         self.M_wg = self.Dp + 1
-        self.splits = Fk.pick_splits(self.M_wg, self.Np, B)
+        self.splits = Fk.pick_splits(self.M_wg, self.Np, B, dense=True)
         self.slab_elems = self.splits * self.M_wg * self.Np
 
     def fwd(self, nb: int) -> None:
@@ -232,7 +232,7 @@ class DenseLayer(_Layer):
         K = kernels()
         dy2 = dy.view(-1, self.Np)
         S = K.dense_wgrad(self.x, dy2, slab, self.Dp, self.Np, nb, self.Dp, self.Np, True,
-                          Fk.pick_splits(self.M_wg, self.Np, nb))
+                          Fk.pick_splits(self.M_wg, self.Np, nb, dense=True))
         _reduce(red, slab, (S, self.M_wg, self.Np, 1, self.Dp, s.din, s.dout, self.Dp),
                 self.fp.grad_view(self.wname), self.fp.grad_view(self.bname))
 

@@ -387,3 +387,20 @@ def test_splitk_reduce_multi_matches_single(dev, K):
     wr = ref[:G * Ip].view(G, Ip, N)[:, :I, :J].reshape(-1)
     assert torch.allclose(w.double(), wr, rtol=1e-5, atol=1e-4)
     assert torch.allclose(b.double(), ref[br, :J], rtol=1e-5, atol=1e-4)
+
+
+# odd (non multiple-of-8) dense shapes take the general scalar-tail loaders
+@pytest.mark.parametrize("M,Din,Dout", [(77, 37, 13), (300, 101, 9), (5, 9, 3)])
+def test_dense_general_loaders(dev, K, M, Din, Dout):
+    torch.manual_seed(11)
+    x = rnd(M, Din, dev=dev)
+    w = rnd(Din, Dout, dev=dev, scale=1 / math.sqrt(Din))
+    b = torch.randn(Dout, device=dev)
+    out = Fk.dense(x, w, b, False, out_dtype=torch.float32)
+    close(out, x.float() @ w.float() + b, rel=1e-4)
+    dy = rnd(M, Dout, dev=dev)
+    dx = Fk.dense_dgrad(dy, w)
+    close(dx, dy.float() @ w.float().t())
+    dw, db = Fk.dense_wgrad(x, dy, Din, Dout, True, None)
+    close(dw, x.float().t() @ dy.float(), rel=1e-3)
+    close(db, dy.float().sum(0), rel=1e-3)

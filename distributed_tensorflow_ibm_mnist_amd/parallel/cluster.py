@@ -76,6 +76,18 @@ def pick_device(rank: int, want_gpu: bool) -> torch.device:
     return torch.device("cuda", idx % max(n, 1))   # several ranks may share a GPU (gloo rehearsal)
 
 
+def _attempt_store(rank: int, world: int, timeout: datetime.timedelta):
+    """The env:// (torchrun) store, namespaced by the elastic restart attempt.
+
+    torchrun keeps ONE store across ``--max-restarts`` attempts, and a fresh
+    process numbers its process groups from 0 again, so without a namespace the
+    restarted ranks can read the previous attempt's keys -- gloo pair addresses
+    of dead processes ("Connection refused"), or a stale RCCL unique id (a hang)."""
+    store, _, _ = next(dist.rendezvous("env://", rank, world, timeout=timeout))
+    attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+    return dist.PrefixStore(f"mnistx/attempt{attempt}", store)
+
+
 def setup_distribute(job_name: str = "", ps_hosts: str = "", worker_hosts: str = "", task_id: int = 0,
                      want_gpu: bool = True, timeout_s: float = 600.0, log=print,
                      ps_backend: str = "", dp_backend: str = "") -> Cluster:
@@ -123,7 +135,8 @@ def setup_distribute(job_name: str = "", ps_hosts: str = "", worker_hosts: str =
         if cl.device.type == "cuda":
             torch.cuda.set_device(cl.device)
         kw = {"device_id": cl.device} if cl.backend == "nccl" else {}
-        dist.init_process_group(cl.backend, timeout=to, **kw)
+        dist.init_process_group(cl.backend, timeout=to, store=_attempt_store(rank, env_world, to),
+                                rank=rank, world_size=env_world, **kw)
         return cl
     # local server (main.py:63-66): single process, task 0
     cl = Cluster("local", job_name or "worker", 0, [], [])

@@ -200,10 +200,17 @@ class FaultInjectionHook(SessionRunHook):
     MNIST_FI_NAN_AT_STEP=k          poison the loss at global step k (NaN hook must fire)
     MNIST_FI_KILL_RANK_AT_STEP=r:k  SIGKILL rank r at global step k (restart/resume tests)
     MNIST_FI_EXIT_AT_STEP=k         clean sys.exit(17) at global step k
+    MNIST_FI_EVERY_ATTEMPT=1        also inject after a torchrun elastic restart
+                                    (default: only on attempt 0, so --max-restarts
+                                    recovers instead of re-failing at the same step)
     """
 
     def __init__(self, rank: int = 0):
         self.rank = rank
+        attempt = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
+        if attempt > 0 and os.environ.get("MNIST_FI_EVERY_ATTEMPT", "0") != "1":
+            for k in ("MNIST_FI_NAN_AT_STEP", "MNIST_FI_KILL_RANK_AT_STEP", "MNIST_FI_EXIT_AT_STEP"):
+                os.environ.pop(k, None)
         self.nan_at = int(os.environ.get("MNIST_FI_NAN_AT_STEP", "-1"))
         kr = os.environ.get("MNIST_FI_KILL_RANK_AT_STEP", "")
         self.kill_rank, self.kill_at = (int(kr.split(":")[0]), int(kr.split(":")[1])) if ":" in kr else (-1, -1)

@@ -218,3 +218,32 @@ def test_ps_kill_fails_workers_then_resume(tmp_path):
     assert "global_step=40" in res
     # continues from the checkpoint, not from scratch: exactly the missing updates are applied
     assert f"applied {40 - int(lc.rsplit('-', 1)[1])} update(s)" in r2["ps0"][1]
+
+
+def test_dp_rank_kill_elastic_restart_resumes(tmp_path):
+    """T6 (DP): rank 1 is SIGKILLed at step 12 of a 2-rank torchrun job; the elastic
+    agent tears the group down and restarts it (--max-restarts 1), the new attempt
+    resumes from the chief's last checkpoint (step 10) and finishes at 40.  Only the
+    chief writes checkpoints / events."""
+    d = str(tmp_path / "train")
+    # GLOO_SOCKET_IFNAME=lo: the container hostname may not resolve.  The restarted
+    # attempt must not read the dead attempt's store keys (cluster._attempt_store).
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONUNBUFFERED="1", MNIST_FI_KILL_RANK_AT_STEP="1:12",
+               GLOO_SOCKET_IFNAME="lo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--max-restarts=1",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.join(ROOT, "main.py"),
+           "--impl=torch", "--cpu", "--model=mlp", "--in_channels=1", "--batch_size=16", "--max_steps=40",
+           "--test_interval=100", "--log_step_count_steps=0", "--train_data=synthetic://1500",
+           "--test_data=synthetic://300?seed=1", "--eval_examples=300", f"--train_dir={d}",
+           "--save_checkpoint_steps=5", "--collective_timeout=60"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=200)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "restored" in out.lower() and "model.ckpt-10" in out, out[-4000:]
+    results = [l for l in out.splitlines() if l.startswith("result:")]
+    results = [l for l in out.replace("result:", "\nresult:").splitlines() if l.startswith("result:")]
+    assert len(results) == 2 and all("global_step=40" in l for l in results), results
+    from distributed_tensorflow_ibm_mnist_amd.ckpt.saver import latest_checkpoint
+    assert latest_checkpoint(d).endswith("model.ckpt-40")
+    ev = [f for f in os.listdir(d) if f.startswith("events.out.tfevents")]
+    assert len(ev) <= 2, ev          # one per attempt, chief only

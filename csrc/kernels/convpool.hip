@@ -156,6 +156,14 @@ DEV float vmax(float a, float b) {  // bare v_max_f32 (fmaxf adds NaN-canonicali
   return r;
 }
 DEV uint32_t pos_of(float v) { return __float_as_uint(v) & 3u; }
+// 0xffff in each 16-bit half of e that equals d (d < 0x10000), else 0:
+// v_xor + v_pk_min_u16 + v_pk_sub_u16
+DEV uint32_t half_eq_mask(uint32_t e, uint32_t d) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  const u16x2 x = __builtin_bit_cast(u16x2, e ^ (d * 0x00010001u));
+  const u16x2 one = {1, 1};
+  return __builtin_bit_cast(uint32_t, (u16x2)(__builtin_elementwise_min(x, one) - one));
+}
 DEV float pos_clear(float v) { return __uint_as_float(__float_as_uint(v) & ~3u); }
 
 constexpr int NTH = 256;
@@ -1016,15 +1024,20 @@ __global__ __launch_bounds__(NTH) void convpool_dgrad_pair_k(const bf16_t* __res
         const int im = e / NWC, rem = e - im * NWC;
         const int win = rem / G::COUT, co = rem - win * G::COUT;
         const int ph = win / G::PW, pw = win - ph * G::PW;
+        // packed select: arg bytes 2k, 2k+1 spread to the two 16-bit halves of E[k]
+        // (one v_perm), then per position d the halves equal to d become 0xffff
+        // masks with two packed u16 ops -- 4 ops per word instead of a compare and a
+        // select per element
+        uint32_t E[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          E[k] = __builtin_amdgcn_perm(0u, ys.a[u][k >> 1], (k & 1) ? 0x0c030c02u : 0x0c010c00u);
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
           const int oh = 2 * ph + (d >> 1) + Q, ow = 2 * pw + (d & 1) + Q;
-          u32x4 o = {0u, 0u, 0u, 0u};
+          u32x4 o;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const uint32_t aj = ((j < 4 ? ys.a[u][0] : ys.a[u][1]) >> (8 * (j & 3))) & 0xff;
-            if (aj == (uint32_t)d) u4_set(o, j, (bf16_t)((ys.y[u][j >> 1] >> (16 * (j & 1))) & 0xffff));
-          }
+          for (int k = 0; k < 4; ++k) o[k] = ys.y[u][k] & half_eq_mask(E[k], (uint32_t)d);
           *(u32x4*)(dyt + im * DT + oh * RSE + ow * DPS + co) = o;
         }
       }

@@ -62,6 +62,35 @@ __global__ void prep_images_k(const uint8_t* __restrict__ src, const int64_t* __
   if (lab_out && t < B) lab_out[t] = lab_src[idx[t]];
 }
 
+// Hot path of K10 (28x28x1 -> 28x28x1): 16 pixels per thread = one 16-byte gather
+// load and two 16-byte bf16 stores, 49 vectors per image, 32-bit index math with a
+// constant divisor (the generic kernel above does a 64-bit divide per 8 pixels).
+// One thread per image also copies the label.
+constexpr int PREP_V = 784 / 16;
+__global__ __launch_bounds__(256) void prep_images_784_k(const uint8_t* __restrict__ src,
+                                                          const int64_t* __restrict__ idx,
+                                                          const int32_t* __restrict__ lab_src, int B,
+                                                          bf16_t* __restrict__ out, int32_t* __restrict__ lab_out) {
+  const int nvec = B * PREP_V;
+  for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += gridDim.x * blockDim.x) {
+    const int b = v / PREP_V, w = v - b * PREP_V;
+    const int64_t row = idx[b];
+    const u32x4 px = *(const u32x4*)(src + row * 784 + 16 * w);
+    u32x4 o0, o1;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      o0[2 * j] = pack2(u8_norm(px[j] & 0xff), u8_norm((px[j] >> 8) & 0xff));
+      o0[2 * j + 1] = pack2(u8_norm((px[j] >> 16) & 0xff), u8_norm(px[j] >> 24));
+      o1[2 * j] = pack2(u8_norm(px[2 + j] & 0xff), u8_norm((px[2 + j] >> 8) & 0xff));
+      o1[2 * j + 1] = pack2(u8_norm((px[2 + j] >> 16) & 0xff), u8_norm(px[2 + j] >> 24));
+    }
+    bf16_t* dst = out + (int64_t)b * 784 + 16 * w;
+    *(u32x4*)dst = o0;
+    *(u32x4*)(dst + 8) = o1;
+    if (lab_out && w == 0) lab_out[b] = lab_src[row];
+  }
+}
+
 // ------------------------------------------------------------------ K6 max-pool 2x2/2 SAME
 __global__ void maxpool_fwd_k(const bf16_t* __restrict__ x, int Nb, int H, int W, int C, int OH, int OW,
                               bf16_t* __restrict__ y, uint8_t* __restrict__ arg) {
@@ -641,6 +670,13 @@ __global__ void cast_pad_k(const float* __restrict__ src, bf16_t* __restrict__ d
 
 hipError_t prep_images(const uint8_t* src, const int64_t* idx, const int32_t* lab_src, int B, int HW, int Csrc,
                        int Cdst, bf16_t* out, int32_t* lab_out, hipStream_t st) {
+  if (HW == 784 && Csrc == 1 && Cdst == 1 && (uintptr_t)src % 16 == 0 && (uintptr_t)out % 16 == 0 &&
+      (int64_t)B * PREP_V < (1ll << 31)) {
+    const int64_t nvec = (int64_t)B * PREP_V;
+    hipLaunchKernelGGL(prep_images_784_k, dim3(nblocks(nvec, 256, 8192)), dim3(256), 0, st, src, idx, lab_src, B,
+                       out, lab_out);
+    return hipGetLastError();
+  }
   const int64_t nvec = (int64_t)B * HW * Cdst / 8;
   int nb = nblocks(nvec, TPB, 8192);
   const int need = (B + TPB - 1) / TPB;

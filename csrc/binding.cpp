@@ -554,7 +554,7 @@ bool convpool_has_dgrad(int64_t cin, int64_t cout, int64_t ks, int64_t pad, int6
 }
 
 void convpool_dgrad(Tensor dP, Tensor arg, Tensor w, Tensor dx, int64_t B, int64_t cin, int64_t cout, int64_t ks,
-                    int64_t pad, int64_t h, int64_t wd) {
+                    int64_t pad, int64_t h, int64_t wd, int64_t grid_cap) {
   auto g = cp_geo(cin, cout, ks, pad, h, wd);
   TORCH_CHECK(mnistx::convpool_has_dgrad(g.cfg), "convpool_dgrad: no fused dgrad for this geometry");
   const int64_t np = B * g.PH * g.PW * cout;
@@ -562,7 +562,8 @@ void convpool_dgrad(Tensor dP, Tensor arg, Tensor w, Tensor dx, int64_t B, int64
   check(arg, at::kByte, np, "arg");
   check(w, at::kBFloat16, ks * ks * cin * cout, "w");
   check(dx, at::kBFloat16, B * h * wd * cin, "dx");
-  hip_ok(mnistx::convpool_dgrad(g.cfg, BF(dP), P<const uint8_t>(arg), BF(w), (int)B, BFm(dx), cur_stream()),
+  hip_ok(mnistx::convpool_dgrad(g.cfg, BF(dP), P<const uint8_t>(arg), BF(w), (int)B, BFm(dx), (int)grid_cap,
+                                cur_stream()),
          "convpool_dgrad");
 }
 
@@ -607,7 +608,9 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("grid"), py::arg("B"), py::arg("cin"), py::arg("cout"), py::arg("ks"), py::arg("pad"), py::arg("h"),
         py::arg("w_"), py::arg("u8") = py::none(), py::arg("idx") = py::none());
   m.def("convpool_u8_input", &convpool_u8_input);
-  m.def("convpool_dgrad", &convpool_dgrad);
+  m.def("convpool_dgrad", &convpool_dgrad, py::arg("dP"), py::arg("arg"), py::arg("w"), py::arg("dx"), py::arg("B"),
+        py::arg("cin"), py::arg("cout"), py::arg("ks"), py::arg("pad"), py::arg("h"), py::arg("w_"),
+        py::arg("grid_cap") = 0);
   m.def("convpool_has_dgrad", &convpool_has_dgrad);
   m.def("convpool_wgrad_grid", &convpool_wgrad_grid);
   m.attr("ARCH") = "gfx950";

@@ -1129,9 +1129,13 @@ hipError_t run_wgrad(const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B,
 }
 
 template <class G, int IMGS>
-hipError_t run_dgrad(const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int B, bf16_t* dx, hipStream_t st) {
-  hipLaunchKernelGGL((convpool_dgrad_pair_k<G, IMGS>),
-                     dim3(grid_for(B, IMGS, resident_grid<convpool_dgrad_pair_k<G, IMGS>>())), dim3(NTH), 0, st, dP, arg, w,
+hipError_t run_dgrad(const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int B, bf16_t* dx, int grid_cap,
+                     hipStream_t st) {
+  // grid_cap > 0: fewer persistent blocks than one resident wave, leaving CU slots
+  // for a kernel running concurrently on another stream (overlapped backward)
+  int cap = resident_grid<convpool_dgrad_pair_k<G, IMGS>>();
+  if (grid_cap > 0 && grid_cap < cap) cap = grid_cap;
+  hipLaunchKernelGGL((convpool_dgrad_pair_k<G, IMGS>), dim3(grid_for(B, IMGS, cap)), dim3(NTH), 0, st, dP, arg, w,
                      B, dx);
   return hipGetLastError();
 }
@@ -1237,9 +1241,9 @@ int convpool_has_dgrad(int cfg) { return cfg == 1 ? 1 : 0; }
 int convpool_u8_input(int cfg) { return (cfg == 0 || cfg == 2) ? 1 : 0; }  // Cin == 1 first layers
 
 hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int B, bf16_t* dx,
-                          hipStream_t st) {
+                          int grid_cap, hipStream_t st) {
   switch (cfg) {
-    case 1: return run_dgrad<LeNetC2, 2>(dP, arg, w, B, dx, st);
+    case 1: return run_dgrad<LeNetC2, 2>(dP, arg, w, B, dx, grid_cap, st);
   }
   return hipErrorInvalidValue;
 }

@@ -63,7 +63,7 @@ hipError_t convpool_wgrad(int cfg, const XSrc& x, const bf16_t* dP, const uint8_
                           int grid, hipStream_t st);
 int convpool_has_dgrad(int cfg);
 hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int B, bf16_t* dx,
-                          hipStream_t st);
+                          int grid_cap, hipStream_t st);
 
 // ---- misc.hip
 hipError_t prep_images(const uint8_t* src, const int64_t* idx, const int32_t* lab_src, int B, int HW, int Csrc,

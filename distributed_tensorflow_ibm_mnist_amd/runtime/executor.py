@@ -19,6 +19,8 @@ Design points (MI355X-first, not a port of the TF graph):
 """
 from __future__ import annotations
 
+import os
+
 import dataclasses
 from typing import Callable, Dict, List, Optional, Tuple
 
@@ -164,9 +166,12 @@ class ConvPoolLayer(_Layer):
         _reduce(red, slab, (grid, self.KM, self.Cp, G, Ip, I, self.spec.cout, brow),
                 self.fp.grad_view(self.wname), self.fp.grad_view(self.bname))
 
+    dgrad_cap = 0   # persistent dgrad blocks (0: one resident wave); set when backward overlaps
+
     def bwd_data(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor]) -> None:
         if dx is not None:
-            kernels().convpool_dgrad(dy, self.arg, self.fp.bf16_view(self.wname), dx, nb, *self._geo())
+            kernels().convpool_dgrad(dy, self.arg, self.fp.bf16_view(self.wname), dx, nb, *self._geo(),
+                                     grid_cap=self.dgrad_cap)
 
 
 class PoolLayer(_Layer):
@@ -354,6 +359,25 @@ class HipNet:
         if self.overlap:
             self.side = torch.cuda.Stream(device=dev)
             self.ev_dy = [torch.cuda.Event() for _ in self.layers]
+            # Co-residency budget (workgroups per CU) for the persistent conv kernels that
+            # run concurrently: the main-stream dgrad and the side-stream weight gradients
+            # each fill every CU by default, which serialises them.  Measured on LeNet-5 at
+            # B=65536 (profiles/r1s3/overlap_budget.txt): every budget is SLOWER than the
+            # serial plan (0.748 ms): all-default 0.779, "2,2" 0.798, "2,1" 0.842 -- the
+            # conv kernels are LDS/issue-bound on the same units, so sharing a CU does not
+            # add throughput.  Kept as an experiment knob.
+            budget = os.environ.get("MNISTX_OVERLAP_WGS", "")
+            if budget:
+                cus = torch.cuda.get_device_properties(dev).multi_processor_count
+                v = [float(x) for x in budget.split(",")]
+                main_wgs, side_wgs = v[0], v[1]
+                first_wgs = v[2] if len(v) > 2 else 0.0
+                for lay in self.layers:
+                    if isinstance(lay, ConvPoolLayer) and lay.idx > 0:
+                        lay.dgrad_cap = max(1, int(main_wgs * cus))
+                        lay.grid = max(1, min(lay.grid, int(side_wgs * cus)))
+                    elif isinstance(lay, ConvPoolLayer) and first_wgs > 0:
+                        lay.grid = max(1, min(lay.grid, int(first_wgs * cus)))
         self.stats = torch.zeros(8, dtype=torch.float32, device=dev)
         self.eval_stats = torch.zeros(8, dtype=torch.float32, device=dev)
         # softmax-CE per-block partials + ticket: deterministic loss / accuracy sums

@@ -161,6 +161,14 @@ int64_t conv_wgrad(Tensor x, Tensor dy, Tensor slab, int64_t Nb, int64_t H, int6
   return S;
 }
 
+void perm_positions(Tensor out, int64_t start, int64_t N, int64_t seed, int64_t h) {
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kLong && out.is_contiguous(), "perm_positions: out");
+  TORCH_CHECK(N > 0 && h >= 1 && h <= 31 && (1ll << (2 * h)) >= N, "perm_positions: bad domain");
+  hip_ok(mnistx::perm_positions(out.data_ptr<int64_t>(), start, (int)out.numel(), N, (uint32_t)seed, (int)h,
+                                cur_stream()),
+         "perm_positions");
+}
+
 void prep_images(Tensor src, Tensor idx, Tensor lab_src, Tensor out, Tensor lab_out, int64_t HW, int64_t Csrc,
                  int64_t Cdst) {
   const int64_t B = idx.numel();
@@ -579,6 +587,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("prep_images", &prep_images);
+  m.def("perm_positions", &perm_positions);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("lrn_fwd", &lrn_fwd);

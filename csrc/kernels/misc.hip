@@ -23,6 +23,44 @@ inline int nblocks(int64_t n, int per_block = TPB, int cap = 1 << 20) {
   return (int)b;
 }
 
+// ------------------------------------------------------------------ epoch shuffle
+// Stateless per-epoch permutation: position p of the (endless) sample stream maps
+// to dataset row F_e(p mod N), e = p / N, where F_e is a 4-round keyed Feistel
+// bijection on [0, 4^h) >= N restricted to [0, N) by cycle walking.  Replaces a
+// device randperm (a radix sort: 0.23 ms per 1.08M-entry permutation, 0.70 ms at
+// 8 ranks' 8.4M) with ~2 us of integer math per step, and makes the data order a
+// pure function of (seed, position): resume seeks instead of replaying.
+// data/device_loader.py::perm_positions is the bit-identical torch version.
+DEV uint32_t mix32(uint32_t x) {
+  x = (x ^ (x >> 16)) * 0x7feb352du;
+  x = (x ^ (x >> 15)) * 0x846ca68bu;
+  return x ^ (x >> 16);
+}
+DEV uint64_t feistel4(uint64_t x, const uint32_t* key, int h) {
+  const uint64_t mask = (1ull << h) - 1;
+  uint64_t L = x >> h, R = x & mask;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const uint64_t nR = L ^ ((uint64_t)mix32((uint32_t)R ^ key[r]) & mask);
+    L = R;
+    R = nR;
+  }
+  return (L << h) | R;
+}
+__global__ void perm_positions_k(int64_t* __restrict__ out, int64_t start, int n, int64_t N, uint32_t seed, int h) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t p = start + i;
+  const int64_t e = p / N;
+  uint64_t x = (uint64_t)(p - e * N);
+  const uint32_t ek = mix32((uint32_t)e ^ 0x9e3779b9u) ^ seed;
+  uint32_t key[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) key[r] = mix32(ek + 0x85ebca77u * (uint32_t)(r + 1));
+  do { x = feistel4(x, key, h); } while (x >= (uint64_t)N);
+  out[i] = (int64_t)x;
+}
+
 // ------------------------------------------------------------------ K10 input prep
 // out[b, p, c] = src[idx[b], p, c_src] / 255 - 0.5   (mnist_input.py:39)
 __global__ void prep_images_k(const uint8_t* __restrict__ src, const int64_t* __restrict__ idx,
@@ -667,6 +705,12 @@ __global__ void cast_pad_k(const float* __restrict__ src, bf16_t* __restrict__ d
 }
 
 }  // namespace
+
+hipError_t perm_positions(int64_t* out, int64_t start, int n, int64_t N, uint32_t seed, int h, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(perm_positions_k, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, st, out, start, n, N, seed, h);
+  return hipGetLastError();
+}
 
 hipError_t prep_images(const uint8_t* src, const int64_t* idx, const int32_t* lab_src, int B, int HW, int Csrc,
                        int Cdst, bf16_t* out, int32_t* lab_out, hipStream_t st) {

@@ -5,9 +5,11 @@ Replaces the reference's queue-runner pipeline (``string_input_producer`` →
 min_after_dequeue=1000)``, ``mnist_input.py:58-71``).  MNIST is 47 MB as uint8,
 so the whole split lives in HBM; each step is ONE gather+normalise kernel
 (``prep_images``: ``x/255 - 0.5``, optional 1→3 channel replication) writing
-straight into the executor's input buffer.  Shuffling is a device-side
-permutation per epoch (a full-epoch shuffle — stronger than the reference's
-1000-example shuffle buffer).
+straight into the executor's input buffer.  Shuffling is a full-epoch
+permutation (stronger than the reference's 1000-example shuffle buffer),
+computed per batch as a keyed Feistel bijection of the stream position
+(``perm_positions``: no sort, no per-epoch state; the data order is a pure
+function of (seed, position), so ``seek(step)`` resumes it exactly).
 
 Data parallel sharding: with ``shard=True`` every rank walks the
 same global permutation and takes its slice of each global batch
@@ -50,6 +52,62 @@ class DeviceDataset:
         return int(self.images.shape[0])
 
 
+M32 = 0xFFFFFFFF
+
+
+def _mix32(x):
+    """32-bit integer hash (works on Python ints and int64 tensors; wraps like uint32)."""
+    x = ((x ^ (x >> 16)) * 0x7feb352d) & M32
+    x = ((x ^ (x >> 15)) * 0x846ca68b) & M32
+    return x ^ (x >> 16)
+
+
+def _half_bits(n: int) -> int:
+    h = 1
+    while (1 << (2 * h)) < n:
+        h += 1
+    return h
+
+
+def perm_positions(start: int, n: int, N: int, seed: int, device=None, out: Optional[torch.Tensor] = None
+                   ) -> torch.Tensor:
+    """Dataset rows of stream positions start..start+n-1: position p -> F_e(p mod N),
+    e = p // N, F_e a 4-round keyed Feistel bijection on [0, 4^h) restricted to
+    [0, N) by cycle walking.  Every epoch is a full permutation of the dataset.
+    On a GPU this is the ``perm_positions`` HIP kernel (misc.hip), bit-identical."""
+    h = _half_bits(N)
+    seed &= M32
+    dev = torch.device(device) if device is not None else (out.device if out is not None else torch.device("cpu"))
+    if dev.type == "cuda":
+        if out is None:
+            out = torch.empty(n, dtype=torch.int64, device=dev)
+        kernels().perm_positions(out[:n], int(start), int(N), int(seed), int(h))
+        return out[:n]
+    mask = (1 << h) - 1
+    p = torch.arange(start, start + n, dtype=torch.int64)
+    e = p // N
+    x = p - e * N
+    ek = _mix32((e & M32) ^ 0x9E3779B9) ^ seed
+    keys = [_mix32((ek + 0x85EBCA77 * (r + 1)) & M32) for r in range(4)]
+
+    def F(v):
+        L, R = v >> h, v & mask
+        for r in range(4):
+            L, R = R, L ^ (_mix32(R ^ keys[r]) & mask)
+        return (L << h) | R
+
+    x = F(x)
+    while True:
+        bad = x >= N
+        if not bool(bad.any()):
+            break
+        x = torch.where(bad, F(x), x)
+    if out is not None:
+        out[:n].copy_(x)
+        return out[:n]
+    return x
+
+
 class DeviceLoader:
     def __init__(self, ds: DeviceDataset, out_images: torch.Tensor, out_labels: torch.Tensor, rank: int = 0,
                  world: int = 1, seed: int = 0, shard: bool = True, shuffle: bool = True,
@@ -62,40 +120,35 @@ class DeviceLoader:
         self.B = int(out_labels.shape[0])
         self.rank, self.world, self.shard, self.shuffle = rank, world, shard, shuffle
         self.global_batch = self.B * world if shard else self.B
-        # One device permutation covers >= 16 global batches (several passes over
-        # small datasets), so the sort behind randperm is amortised instead of
-        # running every step when the global batch approaches the dataset size.
-        self.reps = max(1, -(-16 * self.global_batch // len(ds))) if self.global_batch * 4 > len(ds) else 1
         self.cdst = int(out_images.shape[-1])
-        self.gen = torch.Generator(device=ds.device)
-        self.gen.manual_seed(seed if shard else seed + 7919 * rank)
-        self.perm: Optional[torch.Tensor] = None
-        self.cursor = 0
-        self.epoch = 0
-        self._new_epoch()
+        # sharded ranks walk ONE global order (same key); unsharded ones each their own
+        self.seed = (seed if shard else seed + 7919 * rank) & M32
+        self.idx = torch.empty(self.B, dtype=torch.int64, device=ds.device)
+        self.pos = 0          # stream position of the next global batch
 
-    def _new_epoch(self) -> None:
-        n = len(self.ds) * self.reps
-        if self.shuffle:
-            self.perm = torch.randperm(n, generator=self.gen, device=self.ds.device) % len(self.ds)
-        else:
-            self.perm = torch.arange(n, device=self.ds.device) % len(self.ds)
-        self.cursor = 0
+    @property
+    def epoch(self) -> int:
+        return self.pos // len(self.ds)
+
+    def seek(self, step: int) -> None:
+        """Position the stream at global step ``step`` (resume from a checkpoint)."""
+        self.pos = int(step) * self.global_batch
 
     def next(self, nb: Optional[int] = None) -> int:
         """Gather the next local batch into the output buffers; returns its size."""
         nb = self.B if nb is None else nb
-        if self.cursor + self.global_batch > self.perm.numel():
-            self.epoch += 1
-            self._new_epoch()
-        start = self.cursor + (self.rank * self.B if self.shard else 0)
-        idx = self.perm[start:start + nb]
+        start = self.pos + (self.rank * self.B if self.shard else 0)
+        N = len(self.ds)
+        if self.shuffle:
+            idx = perm_positions(start, nb, N, self.seed, out=self.idx)
+        else:
+            idx = torch.remainder(torch.arange(start, start + nb, device=self.ds.device), N)
         if self.idx_out is not None:
             self.idx_out[:nb].copy_(idx)
             torch.index_select(self.ds.labels, 0, idx, out=self.out_labels[:nb])
         else:
             gather_into(self.ds, idx, self.out_images, self.out_labels)
-        self.cursor += self.global_batch
+        self.pos += self.global_batch
         return nb
 
 

@@ -100,6 +100,9 @@ class MonitoredTrainingSession:
                 self.log(f"Restored from {prefix}")
         r.dp.broadcast_state(0)
         r.sync_step_from_device()
+        loader = getattr(r, "loader", None)
+        if loader is not None and hasattr(loader, "seek"):
+            loader.seek(r.global_step)     # the data order resumes where the checkpoint left it
 
     # ------------------------------------------------------------------ loop
     def __enter__(self):

@@ -68,7 +68,9 @@ def test_training_reduces_loss(dev, K, model):
     from distributed_tensorflow_ibm_mnist_amd.data.device_loader import DeviceDataset, DeviceLoader
     spec = get_model(model, 1)
     init = torch_ref.init_params(spec, seed=0)
-    net = HipNet(spec, 256, dev, init, OptConfig(lr0=0.05, use_momentum=True, momentum=0.9, ema_max=0.9999))
+    # lr 0.05 + momentum 0.9 sits at the edge of divergence for LeNet-5 here (one of three
+    # data orders diverged); 0.02 converges for every order tried
+    net = HipNet(spec, 256, dev, init, OptConfig(lr0=0.02, use_momentum=True, momentum=0.9, ema_max=0.9999))
     imgs, labs = make_synthetic(8192, seed=0, device=dev)
     ds = DeviceDataset(imgs, labs, dev)
     loader = DeviceLoader(ds, net.x0, net.labels, seed=0)

@@ -139,3 +139,35 @@ def test_event_file_roundtrip(tmp_path):
     assert evs[1]["step"] == 10 and evs[1]["values"]["train loss"] == 1.25
     h = evs[2]["values"]["conv1/weight"]
     assert h["num"] == 1000 and sum(h["bucket"]) == 1000
+
+
+def test_feistel_epoch_permutation_and_sharding():
+    """Stateless loader order: every epoch is a full permutation, epochs differ,
+    sharded ranks partition each global batch, and seek(step) resumes the order."""
+    import torch
+    from distributed_tensorflow_ibm_mnist_amd.data.device_loader import (DeviceDataset, DeviceLoader,
+                                                                         perm_positions)
+    for N in (1, 7, 64, 1000, 60000):
+        x = perm_positions(0, 3 * N, N, 11)
+        for e in range(3):
+            assert torch.equal(torch.sort(x[e * N:(e + 1) * N]).values, torch.arange(N))
+    a, b = perm_positions(0, 1000, 1000, 1), perm_positions(1000, 1000, 1000, 1)
+    assert not torch.equal(a, b) and not torch.equal(a, perm_positions(0, 1000, 1000, 2))
+    assert torch.equal(perm_positions(123, 50, 1000, 5), perm_positions(0, 173, 1000, 5)[123:])
+    imgs = torch.arange(100, dtype=torch.int64).repeat_interleave(784).view(100, 784).to(torch.uint8)
+    ds = DeviceDataset(imgs, torch.arange(100), "cpu")
+    def loader(rank, world):
+        return DeviceLoader(ds, torch.zeros(8, 28, 28, 1), torch.zeros(8, dtype=torch.int32), rank=rank,
+                            world=world, seed=3)
+    l0, l1, ref = loader(0, 2), loader(1, 2), loader(0, 1)
+    ref16 = DeviceLoader(ds, torch.zeros(16, 28, 28, 1), torch.zeros(16, dtype=torch.int32), seed=3)
+    for _ in range(20):            # crosses several epochs of the 100-row dataset
+        l0.next(); l1.next(); ref16.next()
+        assert torch.equal(torch.cat([l0.out_labels, l1.out_labels]), ref16.out_labels)
+    l2 = loader(1, 2)
+    l2.seek(19)
+    l1b = loader(1, 2)
+    for _ in range(19):
+        l1b.next()
+    l2.next(); l1b.next()
+    assert torch.equal(l2.out_labels, l1b.out_labels)

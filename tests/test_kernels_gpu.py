@@ -404,3 +404,12 @@ def test_dense_general_loaders(dev, K, M, Din, Dout):
     dw, db = Fk.dense_wgrad(x, dy, Din, Dout, True, None)
     close(dw, x.float().t() @ dy.float(), rel=1e-3)
     close(db, dy.float().sum(0), rel=1e-3)
+
+
+@pytest.mark.parametrize("N,start,n,seed", [(60000, 0, 65536, 0), (60000, 524288 * 7 + 3, 65536, 9),
+                                            (7, 0, 100, 1), (1, 5, 10, 2)])
+def test_perm_positions_matches_torch(dev, K, N, start, n, seed):
+    from distributed_tensorflow_ibm_mnist_amd.data.device_loader import perm_positions
+    g = perm_positions(start, n, N, seed, device=dev)
+    c = perm_positions(start, n, N, seed)
+    assert torch.equal(g.cpu(), c)

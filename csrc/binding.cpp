@@ -123,6 +123,42 @@ int64_t dense_wgrad(Tensor x, Tensor dy, Tensor slab, int64_t Din, int64_t Dout,
   return S;
 }
 
+// Grouped dense weight gradients (with bias rows) in one launch; returns the
+// effective split counts.  Every problem must take the vector loader path
+// (leading dims and widths multiples of 8): the executor checks dense_wgrad_group_ok.
+std::vector<int64_t> dense_wgrad_group(std::vector<Tensor> x, std::vector<Tensor> dy, std::vector<Tensor> slab,
+                                       std::vector<int64_t> Din, std::vector<int64_t> Dout, int64_t B,
+                                       std::vector<int64_t> splits) {
+  const size_t n = x.size();
+  TORCH_CHECK(n >= 1 && n <= 4 && dy.size() == n && slab.size() == n && Din.size() == n && Dout.size() == n &&
+                  splits.size() == n,
+              "dense_wgrad_group: 1-4 problems, matching lists");
+  const mnistx::bf16_t* xp[4];
+  const mnistx::bf16_t* dp[4];
+  int din[4], dout[4], ldx[4], lddy[4], sp[4];
+  mnistx::GemmEpi ep[4];
+  for (size_t p = 0; p < n; ++p) {
+    TORCH_CHECK(x[p].dim() == 2 && dy[p].dim() == 2, "dense_wgrad_group: 2-D operands");
+    const int64_t lx = x[p].size(1), ly = dy[p].size(1);
+    TORCH_CHECK(Din[p] % 8 == 0 && Dout[p] % 8 == 0 && lx % 8 == 0 && ly % 8 == 0 && lx >= Din[p] && ly >= Dout[p],
+                "dense_wgrad_group: widths must be multiples of 8");
+    check(x[p], at::kBFloat16, span(B, lx, Din[p]), "x");
+    check(dy[p], at::kBFloat16, span(B, ly, Dout[p]), "dy");
+    const int64_t S = eff_splits(B, splits[p]);
+    ep[p] = make_slab(slab[p], S, Din[p] + 1, Dout[p]);
+    xp[p] = BF(x[p]);
+    dp[p] = BF(dy[p]);
+    din[p] = (int)Din[p];
+    dout[p] = (int)Dout[p];
+    ldx[p] = (int)lx;
+    lddy[p] = (int)ly;
+    sp[p] = (int)S;
+  }
+  hip_ok(mnistx::dense_wgrad_group((int)n, xp, dp, din, dout, (int)B, ldx, lddy, sp, ep, cur_stream()),
+         "dense_wgrad_group");
+  return std::vector<int64_t>(sp, sp + n);
+}
+
 void conv_fwd(Tensor x, Tensor w, Tensor out, int64_t Nb, int64_t H, int64_t W, int64_t C, int64_t OH, int64_t OW,
               int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t Cout, optional<Tensor> bias, int64_t bias_n,
               bool relu) {
@@ -587,6 +623,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("prep_images", &prep_images);
+  m.def("dense_wgrad_group", &dense_wgrad_group);
   m.def("perm_positions", &perm_positions);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

@@ -280,9 +280,10 @@ DEV bf16x8 frag_tr(const bf16_t* img, int c0, int kb, int lane) {
 }
 
 // ---------------------------------------------------------------- kernel
+// One (tile t, K split) of C = A.B; the kernels below only choose (t, split).
 template <int BM, int BN, int WM, int WN, class LA, bool AKC, class LB, bool BKC>
-__global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEpi ep, int M, int N, int K,
-                                                            int kchunk, int tiles_n) {
+DEV void gemm_body(const LA& la, const LB& lb, const GemmEpi& ep, int M, int N, int K, int kchunk, int tiles_n,
+                   int t, int split) {
   constexpr int NT = 64 * WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
@@ -308,21 +309,6 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEp
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
 
-  const int tiles_mn = gridDim.x;
-  // Split-K launches remap the whole 2-D grid: blocks are dealt round-robin over the
-  // 8 XCDs by linear id, so a plain (tile, split) grid scatters the tiles of one split
-  // -- which all read the same K rows of both operands -- over every XCD.  Remapped,
-  // consecutive logical ids (the tiles of a split, then the next split) share one
-  // XCD's L2 and each K slab is fetched from HBM about once instead of once per tile.
-  int t, split;
-  if (gridDim.y > 1) {
-    const int lin = xcd_remap(blockIdx.y * tiles_mn + blockIdx.x, tiles_mn * gridDim.y);
-    split = lin / tiles_mn;
-    t = lin - split * tiles_mn;
-  } else {
-    t = xcd_remap(blockIdx.x, tiles_mn);
-    split = 0;
-  }
   const int m0 = (t / tiles_n) * BM;
   const int n0 = (t % tiles_n) * BN;
   const int kbeg = split * kchunk;
@@ -547,6 +533,62 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEp
   }
 }
 
+template <int BM, int BN, int WM, int WN, class LA, bool AKC, class LB, bool BKC>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEpi ep, int M, int N, int K,
+                                                            int kchunk, int tiles_n) {
+  const int tiles_mn = gridDim.x;
+  // Split-K launches remap the whole 2-D grid: blocks are dealt round-robin over the
+  // 8 XCDs by linear id, so a plain (tile, split) grid scatters the tiles of one split
+  // -- which all read the same K rows of both operands -- over every XCD.  Remapped,
+  // consecutive logical ids (the tiles of a split, then the next split) share one
+  // XCD's L2 and each K slab is fetched from HBM about once instead of once per tile.
+  int t, split;
+  if (gridDim.y > 1) {
+    const int lin = xcd_remap(blockIdx.y * tiles_mn + blockIdx.x, tiles_mn * gridDim.y);
+    split = lin / tiles_mn;
+    t = lin - split * tiles_mn;
+  } else {
+    t = xcd_remap(blockIdx.x, tiles_mn);
+    split = 0;
+  }
+  gemm_body<BM, BN, WM, WN, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, kchunk, tiles_n, t, split);
+}
+
+// Grouped weight gradients: up to WG_GROUP_MAX independent split-K problems in ONE
+// launch (LeNet's fc3 / fc4 / fc5 run back to back otherwise, each too small to
+// fill the GPU on its own and each paying a drain / ramp between kernels).  Blocks
+// [start[p], start[p+1]) belong to problem p; the XCD remap keeps a problem's split
+// on one L2.
+constexpr int WG_GROUP_MAX = 4;
+struct WgGroup {
+  MatLoaderV a[WG_GROUP_MAX], b[WG_GROUP_MAX];
+  GemmEpi ep[WG_GROUP_MAX];
+  int M[WG_GROUP_MAX], N[WG_GROUP_MAX], K[WG_GROUP_MAX], kchunk[WG_GROUP_MAX], tiles_n[WG_GROUP_MAX],
+      tiles_mn[WG_GROUP_MAX];
+  int start[WG_GROUP_MAX + 1];
+  int np;
+};
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_wg_group_kernel(const WgGroup g) {
+  // Problem ranges start at multiples of 8 blocks, so block b of problem p sits on
+  // XCD b % 8 like any launch: the remap is applied WITHIN each problem (its splits
+  // group on one L2) while every problem still spreads over all 8 XCDs.  Remapping
+  // the whole grid instead put fc3's (heavy) blocks on 3 XCDs and fc5's on 2.
+  const int b = blockIdx.x;
+  int p = 0;
+#pragma unroll
+  for (int q = 1; q < WG_GROUP_MAX; ++q) p += (q < g.np && b >= g.start[q]) ? 1 : 0;
+  p = __builtin_amdgcn_readfirstlane(p);
+  const int n = g.tiles_mn[p] * ((g.K[p] + g.kchunk[p] - 1) / g.kchunk[p]);
+  // bijective on the padded range: every logical block < n is produced exactly once
+  const int local = xcd_remap(b - g.start[p], (n + 7) / 8 * 8);
+  if (local >= n) return;                     // one of the <= 7 padding blocks
+  const int split = local / g.tiles_mn[p];
+  const int t = local - split * g.tiles_mn[p];
+  gemm_body<BM, BN, WM, WN, MatLoaderV, false, MatLoaderV, false>(g.a[p], g.b[p], g.ep[p], g.M[p], g.N[p], g.K[p],
+                                                                 g.kchunk[p], g.tiles_n[p], t, split);
+}
+
 // ---------------------------------------------------------------- dispatch
 template <int BM, int BN, int WM, int WN, class LA, bool AKC, class LB, bool BKC>
 hipError_t launch_cfg(const LA& la, const LB& lb, const GemmEpi& ep, int M, int N, int K, int splits,
@@ -662,6 +704,39 @@ hipError_t dense_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int
   MatLoader b{dy, B, Dout, lddy, -1};
   const int M = Din + (with_bias ? 1 : 0);
   return launch_pick<MatLoaderV, MatLoaderV, false, false>(a, b, ep, M, Dout, B, splits, st, tile);
+}
+
+hipError_t dense_wgrad_group(int np, const bf16_t* const* x, const bf16_t* const* dy, const int* Din, const int* Dout,
+                             int B, const int* ldx, const int* lddy, int* splits, const GemmEpi* ep, hipStream_t st) {
+  constexpr int BM = 64, BN = 64;
+  if (np < 1 || np > WG_GROUP_MAX) return hipErrorInvalidValue;
+  WgGroup g{};
+  g.np = np;
+  int total = 0;
+  for (int p = 0; p < np; ++p) {
+    MatLoader a{x[p], B, Din[p], ldx[p], Din[p]};
+    MatLoader b{dy[p], B, Dout[p], lddy[p], -1};
+    if (!a.vec_ok() || !b.vec_ok()) return hipErrorInvalidValue;   // callers fall back to dense_wgrad
+    memcpy((void*)&g.a[p], (const void*)&a, sizeof(a));
+    memcpy((void*)&g.b[p], (const void*)&b, sizeof(b));
+    g.ep[p] = ep[p];
+    g.M[p] = Din[p] + 1;
+    g.N[p] = Dout[p];
+    g.K[p] = B;
+    int s = splits[p] < 1 ? 1 : splits[p];
+    int kchunk = (B + s - 1) / s;
+    kchunk = (kchunk + BK_WG - 1) / BK_WG * BK_WG;
+    s = (B + kchunk - 1) / kchunk;
+    splits[p] = s;
+    g.kchunk[p] = kchunk;
+    g.tiles_n[p] = (g.N[p] + BN - 1) / BN;
+    g.tiles_mn[p] = ((g.M[p] + BM - 1) / BM) * g.tiles_n[p];
+    g.start[p] = total;
+    total += (g.tiles_mn[p] * s + 7) / 8 * 8;
+  }
+  g.start[np] = total;
+  hipLaunchKernelGGL((gemm_wg_group_kernel<BM, BN, 2, 2>), dim3(total), dim3(256), 0, st, g);
+  return hipGetLastError();
 }
 
 hipError_t conv_fwd(const bf16_t* x, const bf16_t* w, int Nb, int H, int W, int C, int OH, int OW, int KH,

@@ -32,6 +32,9 @@ hipError_t dense_dgrad(const bf16_t* dy, const bf16_t* w, int M, int N, int K, i
                        const GemmEpi& ep, hipStream_t st);
 hipError_t dense_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int B, int ldx, int lddy,
                        int with_bias, int splits, const GemmEpi& ep, hipStream_t st, int tile = -1);
+// np (<= 4) dense weight gradients in one launch (64x64 tiles; splits[] in: requested, out: effective)
+hipError_t dense_wgrad_group(int np, const bf16_t* const* x, const bf16_t* const* dy, const int* Din, const int* Dout,
+                             int B, const int* ldx, const int* lddy, int* splits, const GemmEpi* ep, hipStream_t st);
 hipError_t conv_fwd(const bf16_t* x, const bf16_t* w, int Nb, int H, int W, int C, int OH, int OW, int KH,
                     int KW, int ph, int pw, int Cout, const GemmEpi& ep, hipStream_t st);
 hipError_t conv_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int OH, int OW, int Cout, int H, int W,

@@ -60,11 +60,12 @@ SLAB_CAP = 16 << 20   # fp32 elements of split-K partials (64 MB)
 
 
 def pick_splits(M: int, N: int, K: int, target: Optional[int] = None, min_k: int = 256,
-                dense: bool = False) -> int:
+                dense: bool = False, grouped: bool = False) -> int:
     """Split-K factor for a weight-gradient GEMM: fill the CUs (``target``
     workgroups), but keep every split >= min_k reduction elements and the fp32
-    slab under SLAB_CAP."""
-    bm, bn = gemm_tile(M, N)
+    slab under SLAB_CAP.  ``grouped``: one problem of a dense_wgrad_group launch
+    (64x64 tiles)."""
+    bm, bn = (64, 64) if grouped else gemm_tile(M, N)
     tiles = math.ceil(M / bm) * math.ceil(N / bn)
     if target is None:
         target = TARGET_BLOCKS_FEW_TILES if (dense and tiles < 64) else TARGET_BLOCKS

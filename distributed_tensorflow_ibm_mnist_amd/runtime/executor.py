@@ -224,7 +224,9 @@ class DenseLayer(_Layer):
         self.out = torch.zeros(B, self.Np, dtype=torch.float32 if last else torch.bfloat16, device=dev)
         self.wname, self.bname = f"{spec.name}/weights", f"{spec.name}/biases"
         self.M_wg = self.Dp + 1
-        self.splits = Fk.pick_splits(self.M_wg, self.Np, B, dense=True)
+        # slab sized for the larger of the standalone and the grouped (64x64-tile) split
+        self.splits = max(Fk.pick_splits(self.M_wg, self.Np, B, dense=True),
+                          Fk.pick_splits(self.M_wg, self.Np, B, dense=True, grouped=True))
         self.slab_elems = self.splits * self.M_wg * self.Np
 
     def fwd(self, nb: int) -> None:
@@ -233,11 +235,15 @@ class DenseLayer(_Layer):
                             self.Np, self.fp.param_view(self.bname), s.dout, s.relu, None, 0)
 
     def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor, red: Optional[list] = None) -> None:
-        s = self.spec
         K = kernels()
         dy2 = dy.view(-1, self.Np)
         S = K.dense_wgrad(self.x, dy2, slab, self.Dp, self.Np, nb, self.Dp, self.Np, True,
                           Fk.pick_splits(self.M_wg, self.Np, nb, dense=True))
+        self.reduce_wgrad(S, slab, red)
+
+    def reduce_wgrad(self, S: int, slab: torch.Tensor, red: Optional[list] = None) -> None:
+        """Queue (or run) the split-K reduce of an S-split weight-gradient slab."""
+        s = self.spec
         _reduce(red, slab, (S, self.M_wg, self.Np, 1, self.Dp, s.din, s.dout, self.Dp),
                 self.fp.grad_view(self.wname), self.fp.grad_view(self.bname))
 
@@ -393,6 +399,11 @@ class HipNet:
         # fused dense head (mlp_head.hip): index of its first layer, or None
         self.head: Optional[int] = self._find_head() if (fuse_head and dev.type == "cuda") else None
         self._head_pending: Optional[int] = None   # nb of a deferred head (forward(defer_head=True))
+        # the head's fc3/fc4/fc5 weight gradients as one grouped launch (gemm.hip
+        # dense_wgrad_group); MNISTX_GROUP_WGRAD=0 launches them one by one
+        self.group_head_wgrad = (self.head is not None and os.environ.get("MNISTX_GROUP_WGRAD", "1") != "0"
+                                 and all(l.Dp % 8 == 0 and l.Np % 8 == 0 for l in self.layers[self.head:]))
+        self._group_S: Optional[list] = None
         self._head_grads = False                   # loss_and_grad already produced the head's dgrads
 
     def _find_head(self) -> Optional[int]:
@@ -480,6 +491,15 @@ class HipNet:
         main = torch.cuda.current_stream(self.device) if self.overlap else None
         if self.overlap:
             self.side.wait_stream(main)
+        # fused head: its three weight gradients run as ONE grouped split-K launch
+        self._group_S = None
+        if self.group_head_wgrad and self._head_grads and self.defer_reduce and not self.overlap:
+            hl = self.layers[self.head:]
+            dys = [self.dbuf[self.head + 1], self.dbuf[self.head + 2], self.dlogits]
+            self._group_S = kernels().dense_wgrad_group(
+                [l.x for l in hl], [d.view(-1, l.Np) for d, l in zip(dys, hl)],
+                [self.slabs[self.head + k] for k in range(3)], [l.Dp for l in hl], [l.Np for l in hl], nb,
+                [Fk.pick_splits(l.M_wg, l.Np, nb, dense=True, grouped=True) for l in hl])
         for i in range(len(self.layers) - 1, -1, -1):
             lay = self.layers[i]
             dx = self.dbuf[i]
@@ -495,6 +515,12 @@ class HipNet:
                             self._flush_reduce(side_pending)
                             for h in self.grad_ready_hooks:
                                 h(lay.idx)
+                elif self.defer_reduce and self._group_S is not None and i >= self.head:
+                    lay.reduce_wgrad(self._group_S[i - self.head], self.slabs[i], pending)
+                    if self.grad_ready_hooks and (self.hook_layers is None or lay.idx in self.hook_layers):
+                        self._flush_reduce(pending)
+                        for h in self.grad_ready_hooks:
+                            h(lay.idx)
                 elif self.defer_reduce:
                     lay.bwd_weight(nb, dy, self.slabs[i], pending)
                     if self.grad_ready_hooks and (self.hook_layers is None or lay.idx in self.hook_layers):

@@ -413,3 +413,23 @@ def test_perm_positions_matches_torch(dev, K, N, start, n, seed):
     g = perm_positions(start, n, N, seed, device=dev)
     c = perm_positions(start, n, N, seed)
     assert torch.equal(g.cpu(), c)
+
+
+def test_dense_wgrad_group_matches_single(dev, K):
+    """Grouped split-K weight gradients (one launch) vs the fp32 reference, with the
+    same effective split counts as the per-layer launches."""
+    torch.manual_seed(21)
+    B = 5000
+    shapes = [(400, 120), (120, 88), (88, 16)]
+    xs = [rnd(B, d, dev=dev) for d, _ in shapes]
+    dys = [rnd(B, n, dev=dev) for _, n in shapes]
+    splits = [37, 20, 9]
+    slabs = [torch.zeros(s * (d + 1) * n, device=dev) for s, (d, n) in zip(splits, shapes)]
+    S = K.dense_wgrad_group(xs, dys, slabs, [d for d, _ in shapes], [n for _, n in shapes], B, splits)
+    for (d, n), x, dy, slab, s, sg in zip(shapes, xs, dys, slabs, splits, S):
+        ref = torch.zeros_like(slab)
+        s1 = K.dense_wgrad(x, dy, ref, d, n, B, d, n, True, s, 7)   # tile code 7 = 64x64
+        assert s1 == sg
+        tot = slab[: sg * (d + 1) * n].view(sg, d + 1, n).sum(0)
+        exp = torch.cat([x.float().t() @ dy.float(), dy.float().sum(0, keepdim=True)])
+        close(tot, exp, rel=1e-3)

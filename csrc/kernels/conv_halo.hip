@@ -1,0 +1,244 @@
+// LDS-halo implicit-GEMM 5x5 convolution for the reference CNN's conv2 geometry
+// (14x14 NHWC images, stride 1, SAME padding, Cin % 32 == 0): forward
+// (conv + bias + ReLU) and data gradient (the same convolution of dY with the
+// 180-degree-flipped, in/out-swapped filter, optional ReLU mask).
+//
+// The generic GEMM path (gemm.hip Im2colK) gathers every im2col element from
+// L2: each input value is fetched 25 times (once per tap), and at Cin = 32..64
+// the 16-byte gathers -- not the MFMAs -- bound it (conv2 dgrad 1.2 ms for
+// 164 GFLOP at B = 16384).  Here a workgroup keeps
+//   * its slice of the filter resident in LDS for the whole (persistent) launch,
+//     as [tap][out channel][in channel] rows (B fragments = one ds_read_b128), and
+//   * one zero-haloed 18x18xCin image at a time (A fragments = one ds_read_b128
+//     of 8 channels of one (pixel, tap)),
+// so HBM/L2 see each input image once per output-channel slice.  16-byte chunks
+// are XOR-swizzled by row so a fragment's 16 rows hit 16 distinct bank groups.
+// A wave computes four 16-pixel M-fragments per pass (B fragments shared), with
+// v_mfma_f32_16x16x32_bf16 and K ordered (tap, channel block).  The next image is
+// prefetched into VGPRs while the current one computes.
+//
+// Replaces: Conv2D / Conv2DBackpropInput of conv2,
+// mnist_input.py:161 (reference CNN); the gemm.hip launchers route to it.
+#include "common.h"
+#include "launchers.h"
+
+#include <cstdlib>
+
+namespace mnistx {
+namespace {
+
+constexpr int HW = 14, KS = 5, HP = HW + 4, NPIX = HW * HW, NTAP = KS * KS;
+constexpr int MFR = (NPIX + 15) / 16;        // 13 M-fragments of 16 pixels
+
+// 16-byte chunk swizzle of row r (CH chunks per row)
+template <int CH>
+DEV int swz(int r, int c) {
+  if constexpr (CH == 4) return c ^ (r & 3);
+  else return c ^ ((r ^ (r >> 3)) & (CH - 1));
+}
+
+// MODE 0 = forward: out[p][n] = relu(sum_{tap,ci} x[p+tap][ci] W[tap][ci][n] + b[n])
+// MODE 1 = data gradient: out[p][n] = mask * sum_{tap,ci} dy[p+tap][ci] W[24-tap][n][ci]
+//   (W is the conv's [kh][kw][cin][cout] filter; here ci runs over the conv's
+//    output channels and n over its input channels)
+template <int CIN, int CW, int NW, int MODE, int FR>
+__global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                        int wcin, int wcout, const float* __restrict__ bias, int bias_n,
+                                                        int relu, const bf16_t* __restrict__ mask, int ldm, int B,
+                                                        bf16_t* __restrict__ out, int ldo) {
+  constexpr int NT = 64 * NW;
+  constexpr int CH = CIN / 8;                 // 16-byte chunks per pixel / filter row
+  constexpr int NF = CW / 16;
+  constexpr int KC = CIN / 32;                // 32-wide k-steps per tap
+  constexpr int XE = HP * HP * CIN;           // image tile elements
+  constexpr int WE = NTAP * CW * CIN;         // filter slice elements
+  constexpr int NV = NPIX * CH;               // 16-byte vectors per input image
+  constexpr int PER = (NV + NT - 1) / NT;
+  constexpr int NGRP = (MFR + FR - 1) / FR;   // fragment groups per image (FR fragments share the B reads)
+  static_assert(CIN % 32 == 0 && CW % 16 == 0 && (CH == 4 || CH == 8), "conv5_halo geometry");
+  __shared__ __attribute__((aligned(16))) bf16_t xs[XE];
+  __shared__ __attribute__((aligned(16))) bf16_t ws[WE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.y * CW;
+
+  for (int e = tid; e < XE / 8; e += NT) *(u32x4*)(xs + 8 * e) = u32x4{0u, 0u, 0u, 0u};   // the halo stays zero
+  // filter slice -> ws[(tap*CW + n)][ci] (swizzled chunks), once per block
+  if constexpr (MODE == 0) {
+    // W[tap][ci][n0 + n .. +7] is contiguous: one vector load, 8 scattered 2-byte LDS stores
+    for (int e = tid; e < NTAP * CIN * (CW / 8); e += NT) {
+      const int nv = e % (CW / 8), rest = e / (CW / 8), ci = rest % CIN, t = rest / CIN;
+      const u32x4 v = *(const u32x4*)(w + ((int64_t)t * wcin + ci) * wcout + n0 + 8 * nv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = t * CW + 8 * nv + j;
+        ws[r * CIN + (swz<CH>(r, ci >> 3) << 3) + (ci & 7)] = (bf16_t)((v[j >> 1] >> (16 * (j & 1))) & 0xffffu);
+      }
+    }
+  } else {
+    // flipped tap, row n = conv input channel n0 + n, columns = conv output channels (contiguous)
+    for (int e = tid; e < NTAP * CW * CH; e += NT) {
+      const int c = e % CH, r = e / CH, n = r % CW, t = r / CW;
+      const u32x4 v = *(const u32x4*)(w + ((int64_t)(NTAP - 1 - t) * wcin + n0 + n) * wcout + 8 * c);
+      *(u32x4*)(ws + r * CIN + (swz<CH>(r, c) << 3)) = v;
+    }
+  }
+
+  u32x4 pre[PER];
+  auto gload = [&](int img) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int v = tid + u * NT;
+      pre[u] = (v < NV && img < B) ? *(const u32x4*)(x + (int64_t)img * NPIX * CIN + 8 * v) : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  gload(blockIdx.x);
+  for (int img = blockIdx.x; img < B; img += gridDim.x) {
+    __syncthreads();                            // previous image's fragments consumed
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int v = tid + u * NT;
+      if (v < NV) {
+        const int p = v / CH, c = v - p * CH;
+        const int P = (p / HW + 2) * HP + (p % HW) + 2;
+        *(u32x4*)(xs + P * CIN + (swz<CH>(P, c) << 3)) = pre[u];
+      }
+    }
+    __syncthreads();
+    gload(img + gridDim.x);                     // next image in flight during the MFMAs
+    for (int gr = wave; gr < NGRP; gr += NW) {
+      // fragments FR*gr .. FR*gr+FR-1 (fragments past the 13th are padding pixels)
+      int P0[FR];
+#pragma unroll
+      for (int h = 0; h < FR; ++h) {
+        const int p = min((FR * gr + h) * 16 + i, NPIX - 1);
+        P0[h] = (p / HW) * HP + (p % HW);       // tile pixel of tap (0,0)
+      }
+      f32x4 acc[FR][NF];
+#pragma unroll
+      for (int h = 0; h < FR; ++h)
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf) acc[h][nf] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int kh = 0; kh < KS; ++kh) {
+#pragma unroll
+        for (int kw = 0; kw < KS; ++kw) {
+          const int t = kh * KS + kw;
+          const int dP = kh * HP + kw;
+#pragma unroll
+          for (int kc = 0; kc < KC; ++kc) {
+            const int c = 4 * kc + g;
+            bf16x8 a[FR], b[NF];
+#pragma unroll
+            for (int h = 0; h < FR; ++h) {
+              const int P = P0[h] + dP;
+              a[h] = __builtin_bit_cast(bf16x8, *(const u32x4*)(xs + P * CIN + (swz<CH>(P, c) << 3)));
+            }
+#pragma unroll
+            for (int nf = 0; nf < NF; ++nf) {
+              const int r = t * CW + nf * 16 + i;
+              b[nf] = __builtin_bit_cast(bf16x8, *(const u32x4*)(ws + r * CIN + (swz<CH>(r, c) << 3)));
+            }
+#pragma unroll
+            for (int h = 0; h < FR; ++h)
+#pragma unroll
+              for (int nf = 0; nf < NF; ++nf)
+                acc[h][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h], b[nf], acc[h][nf], 0, 0, 0);
+          }
+        }
+      }
+      // D rows 4g + r = pixels, column i = output channel n0 + nf*16 + i
+#pragma unroll
+      for (int h = 0; h < FR; ++h)
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf) {
+          const int n = n0 + nf * 16 + i;
+          const float bn = (MODE == 0 && bias != nullptr && n < bias_n) ? bias[n] : 0.f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int q = (FR * gr + h) * 16 + 4 * g + r;
+            if (q < NPIX) {
+              float v = acc[h][nf][r] + bn;
+              if (relu) v = fmaxf(v, 0.f);
+              const int64_t row = (int64_t)img * NPIX + q;
+              if (mask != nullptr && !(bf2f(mask[row * ldm + n]) > 0.f)) v = 0.f;
+              out[row * ldo + n] = f2bf(v);
+            }
+          }
+        }
+    }
+  }
+}
+
+template <int CIN, int CW, int NW, int MODE, int FR>
+int halo_grid(int B) {
+  static int per = -1;
+  if (per < 0) {
+    int dev = 0, cus = 0, pc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, conv5_halo_k<CIN, CW, NW, MODE, FR>, 64 * NW, 0) ==
+            hipSuccess &&
+        hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && pc > 0)
+      per = pc * cus;
+    else
+      per = 256;
+  }
+  return B < per ? B : per;
+}
+
+template <int CIN, int CW, int NW, int MODE, int FR>
+hipError_t run_halo(const bf16_t* x, const bf16_t* w, int wcin, int wcout, const float* bias, int bias_n, int relu,
+                    const bf16_t* mask, int ldm, int B, bf16_t* out, int ncols, int ldo, hipStream_t st) {
+  if (B <= 0) return hipSuccess;
+  dim3 grid(halo_grid<CIN, CW, NW, MODE, FR>(B), ncols / CW);
+  hipLaunchKernelGGL((conv5_halo_k<CIN, CW, NW, MODE, FR>), grid, dim3(64 * NW), 0, st, x, w, wcin, wcout, bias, bias_n,
+                     relu, mask, ldm, B, out, ldo);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// Geometry the halo kernels cover: 14x14, 5x5, pad 2, stride 1; fwd Cin 32 -> Cout % 32,
+// dgrad dY 64 channels -> dX 32.
+bool conv5_halo_fwd_ok(int H, int W, int C, int OH, int OW, int KH, int KW, int ph, int pw, int Cout) {
+  return H == 14 && W == 14 && OH == 14 && OW == 14 && KH == 5 && KW == 5 && ph == 2 && pw == 2 && C == 32 &&
+         Cout % 32 == 0;
+}
+bool conv5_halo_dgrad_ok(int OH, int OW, int Cout, int H, int W, int KH, int KW, int ph, int pw, int Cin) {
+  return H == 14 && W == 14 && OH == 14 && OW == 14 && KH == 5 && KW == 5 && ph == 2 && pw == 2 && Cout == 64 &&
+         Cin % 32 == 0;
+}
+
+// Variant (MNISTX_HALO_FWD / MNISTX_HALO_DGRAD = index; sweep: bench/gpu_halo_sweep.sh)
+static int halo_variant(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return (e && e[0] >= '0' && e[0] <= '9') ? e[0] - '0' : dflt;
+}
+
+hipError_t conv5_halo_fwd(const bf16_t* x, const bf16_t* w, int Nb, int C, int Cout, const float* bias, int bias_n,
+                          int relu, bf16_t* out, hipStream_t st) {
+  static const int v = halo_variant("MNISTX_HALO_FWD", 0);
+  switch (v) {
+    case 1:   // whole Cout per block (NF = 4): 123 KB LDS, 1 block / CU
+      if (Cout == 64) return run_halo<32, 64, 4, 0, 4>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
+      break;
+    case 2:   // 8 waves, fragment pairs
+      return run_halo<32, 32, 8, 0, 2>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
+    default: break;
+  }
+  return run_halo<32, 32, 4, 0, 4>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
+}
+
+hipError_t conv5_halo_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int Cout, int Cin, const bf16_t* mask,
+                            bf16_t* dx, hipStream_t st) {
+  static const int v = halo_variant("MNISTX_HALO_DGRAD", 0);
+  switch (v) {
+    case 1:   // 8 waves, fragment pairs
+      return run_halo<64, 32, 8, 1, 2>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
+    case 2:   // half the input channels of the conv per block (NF = 1)
+      return run_halo<64, 16, 4, 1, 4>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
+    default: break;
+  }
+  return run_halo<64, 32, 4, 1, 4>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
+}
+
+}  // namespace mnistx

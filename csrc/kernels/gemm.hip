@@ -31,6 +31,7 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 
@@ -739,8 +740,17 @@ hipError_t dense_wgrad_group(int np, const bf16_t* const* x, const bf16_t* const
   return hipGetLastError();
 }
 
+// MNISTX_CONV_HALO=0 keeps the im2col GEMM for the geometries conv_halo.hip covers
+static bool halo_enabled() {
+  static const int on = [] { const char* e = getenv("MNISTX_CONV_HALO"); return (e && e[0] == '0') ? 0 : 1; }();
+  return on != 0;
+}
+
 hipError_t conv_fwd(const bf16_t* x, const bf16_t* w, int Nb, int H, int W, int C, int OH, int OW, int KH,
                     int KW, int ph, int pw, int Cout, const GemmEpi& ep, hipStream_t st) {
+  if (halo_enabled() && ep.mode == EPI_BF16 && ep.ldc == Cout && ep.mask == nullptr &&
+      conv5_halo_fwd_ok(H, W, C, OH, OW, KH, KW, ph, pw, Cout))
+    return conv5_halo_fwd(x, w, Nb, C, Cout, ep.bias, ep.bias_n, ep.relu, (bf16_t*)ep.out, st);
   const int M = Nb * OH * OW, K = KH * KW * C;
   Im2colK a{x, H, W, C, OH, OW, KH, KW, ph, pw, M, K,
             FastDiv(OH * OW), FastDiv(OW), FastDiv(C), FastDiv(KW)};
@@ -750,6 +760,9 @@ hipError_t conv_fwd(const bf16_t* x, const bf16_t* w, int Nb, int H, int W, int 
 
 hipError_t conv_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int OH, int OW, int Cout, int H, int W,
                       int KH, int KW, int ph, int pw, int Cin, const GemmEpi& ep, hipStream_t st) {
+  if (halo_enabled() && ep.mode == EPI_BF16 && ep.ldc == Cin && ep.bias == nullptr && !ep.relu &&
+      (ep.mask == nullptr || ep.ldm == Cin) && conv5_halo_dgrad_ok(OH, OW, Cout, H, W, KH, KW, ph, pw, Cin))
+    return conv5_halo_dgrad(dy, w, Nb, Cout, Cin, ep.mask, (bf16_t*)ep.out, st);
   // dX = conv(dY, flip(W)^T) with pad' = K-1-pad, over the dY image.
   const int M = Nb * H * W, K = KH * KW * Cout;
   Im2colK a{dy, OH, OW, Cout, H, W, KH, KW, KH - 1 - ph, KW - 1 - pw, M, K,

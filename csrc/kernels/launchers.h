@@ -35,6 +35,14 @@ hipError_t dense_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int
 // np (<= 4) dense weight gradients in one launch (64x64 tiles; splits[] in: requested, out: effective)
 hipError_t dense_wgrad_group(int np, const bf16_t* const* x, const bf16_t* const* dy, const int* Din, const int* Dout,
                              int B, const int* ldx, const int* lddy, int* splits, const GemmEpi* ep, hipStream_t st);
+// conv_halo.hip: LDS-halo 5x5 convolutions (reference conv2 geometry); conv_fwd /
+// conv_dgrad route there when *_ok() holds
+bool conv5_halo_fwd_ok(int H, int W, int C, int OH, int OW, int KH, int KW, int ph, int pw, int Cout);
+bool conv5_halo_dgrad_ok(int OH, int OW, int Cout, int H, int W, int KH, int KW, int ph, int pw, int Cin);
+hipError_t conv5_halo_fwd(const bf16_t* x, const bf16_t* w, int Nb, int C, int Cout, const float* bias, int bias_n,
+                          int relu, bf16_t* out, hipStream_t st);
+hipError_t conv5_halo_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int Cout, int Cin, const bf16_t* mask,
+                            bf16_t* dx, hipStream_t st);
 hipError_t conv_fwd(const bf16_t* x, const bf16_t* w, int Nb, int H, int W, int C, int OH, int OW, int KH,
                     int KW, int ph, int pw, int Cout, const GemmEpi& ep, hipStream_t st);
 hipError_t conv_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int OH, int OW, int Cout, int H, int W,

@@ -1,3 +1,4 @@
+#include <algorithm>
 // Python bindings for the MNIST HIP kernels (torch extension `_kernels`).
 //
 // Every entry point validates device, dtype, contiguity and that each buffer is
@@ -123,6 +124,17 @@ int64_t dense_wgrad(Tensor x, Tensor dy, Tensor slab, int64_t Din, int64_t Dout,
   return S;
 }
 
+// Split count the conv weight gradient prefers (slab sizing): the halo kernel's
+// persistent grid when it covers the geometry, else -1 (use the GEMM rule).
+int64_t conv_wgrad_pref_splits(int64_t Nb, int64_t H, int64_t W, int64_t C, int64_t OH, int64_t OW, int64_t KH,
+                               int64_t KW, int64_t ph, int64_t pw, int64_t Cout, bool with_bias) {
+  if (mnistx::conv_halo_enabled() &&
+      mnistx::conv5_halo_wgrad_ok((int)H, (int)W, (int)C, (int)OH, (int)OW, (int)KH, (int)KW, (int)ph, (int)pw,
+                                  (int)Cout, with_bias ? 1 : 0))
+    return mnistx::conv5_halo_wgrad_grid((int)Nb);
+  return -1;
+}
+
 // Grouped dense weight gradients (with bias rows) in one launch; returns the
 // effective split counts.  Every problem must take the vector loader path
 // (leading dims and widths multiples of 8): the executor checks dense_wgrad_group_ok.
@@ -189,7 +201,12 @@ int64_t conv_wgrad(Tensor x, Tensor dy, Tensor slab, int64_t Nb, int64_t H, int6
   check(dy, at::kBFloat16, Nb * OH * OW * Cout, "dy");
   TORCH_CHECK(Cout % 8 == 0, "Cout must be padded to a multiple of 8");
   const int64_t M = KH * KW * C + (with_bias ? 1 : 0);
-  const int64_t S = eff_splits(Nb * OH * OW, splits);
+  const bool halo = mnistx::conv_halo_enabled() &&
+                    mnistx::conv5_halo_wgrad_ok((int)H, (int)W, (int)C, (int)OH, (int)OW, (int)KH, (int)KW, (int)ph,
+                                                (int)pw, (int)Cout, with_bias ? 1 : 0);
+  // halo weight gradient: one partial per persistent block (at most `splits`)
+  const int64_t S = halo ? std::max<int64_t>(1, std::min<int64_t>(splits, mnistx::conv5_halo_wgrad_grid((int)Nb)))
+                         : eff_splits(Nb * OH * OW, splits);
   auto ep = make_slab(slab, S, M, Cout);
   hip_ok(mnistx::conv_wgrad(BF(x), BF(dy), (int)Nb, (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)KH, (int)KW,
                             (int)ph, (int)pw, (int)Cout, with_bias ? 1 : 0, (int)S, ep, cur_stream()),
@@ -624,6 +641,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("conv_wgrad", &conv_wgrad);
   m.def("prep_images", &prep_images);
   m.def("dense_wgrad_group", &dense_wgrad_group);
+  m.def("conv_wgrad_pref_splits", &conv_wgrad_pref_splits);
   m.def("perm_positions", &perm_positions);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

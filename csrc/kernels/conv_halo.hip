@@ -169,6 +169,145 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict
   }
 }
 
+// ------------------------------------------------------------------ weight gradient
+// dW[tap][ci][co] = sum_p x[p + tap][ci] dY[p][co]  (+ bias row: sum_p dY[p][co]).
+// M = (tap, ci) rows (25*CIN + the bias row), N = COUT, K = pixels.  A persistent
+// block keeps the whole M x N partial in registers (8 waves, row tiles dealt
+// round-robin, all NFW column tiles each) and streams images: per image the x
+// tile (zero halo) and dY (14 x 16 pixel rows, columns 14/15 zero) are staged in
+// LDS once and every (tap, ci-block) row tile reads its A fragments straight from
+// the x tile with ds_read_b64_tr_b16 (k = 16 consecutive pixels of an image row,
+// +16 = the next row).  The pixel padding (columns 14/15) multiplies zero dY.
+// One fp32 partial per block goes to the split-K slab ([S][25*CIN+1][COUT] rows
+// (tap*CIN + ci), bias row 25*CIN), reduced by splitk_reduce like the GEMM path.
+template <int CIN, int COUT, int NW>
+__global__ __launch_bounds__(64 * NW) void conv5_halo_wgrad_k(const bf16_t* __restrict__ x,
+                                                              const bf16_t* __restrict__ dy, int B,
+                                                              float* __restrict__ slab) {
+  constexpr int NT = 64 * NW;
+  constexpr int SX = CIN + 16, SD = COUT + 16;          // tr-read row strides (gemm.hip ImgStride rule)
+  constexpr int XP = HP * HP + 8;                       // tile pixels + zero over-read slack
+  constexpr int DPIX = HW * 16;                         // dY rows: 14 image rows x 16 columns
+  constexpr int MREAL = NTAP * CIN, MTOT = MREAL + 1;
+  constexpr int RT = NTAP * (CIN / 16) + 1;             // row tiles incl. the bias tile
+  constexpr int NFW = COUT / 16;
+  constexpr int RPW = (RT + NW - 1) / NW;               // row tiles per wave (max)
+  constexpr int KSTEPS = HW / 2;                        // 32 pixels (two image rows) per k-step
+  constexpr int XV = NPIX * CIN / 8, DV = NPIX * COUT / 8;
+  constexpr int PX = (XV + NT - 1) / NT, PD = (DV + NT - 1) / NT;
+  static_assert(CIN % 16 == 0 && COUT % 16 == 0 && HW % 2 == 0, "");
+  __shared__ __attribute__((aligned(16))) bf16_t xs[XP * SX];
+  __shared__ __attribute__((aligned(16))) bf16_t ds[DPIX * SD];
+  __shared__ __attribute__((aligned(16))) bf16_t ones[32 * 16];   // bias A tile: column 0 = 1
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
+  for (int e = tid; e < XP * SX / 8; e += NT) *(u32x4*)(xs + 8 * e) = u32x4{0u, 0u, 0u, 0u};
+  for (int e = tid; e < DPIX * SD / 8; e += NT) *(u32x4*)(ds + 8 * e) = u32x4{0u, 0u, 0u, 0u};
+  for (int e = tid; e < 32 * 16; e += NT) ones[e] = (e & 15) == 0 ? (bf16_t)0x3f80 : (bf16_t)0;
+
+  f32x4 acc[RPW][NFW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int n = 0; n < NFW; ++n) acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 px[PX], pd[PD];
+  auto gload = [&](int img) {
+#pragma unroll
+    for (int u = 0; u < PX; ++u) {
+      const int v = tid + u * NT;
+      px[u] = (v < XV && img < B) ? *(const u32x4*)(x + (int64_t)img * NPIX * CIN + 8 * v) : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      const int v = tid + u * NT;
+      pd[u] = (v < DV && img < B) ? *(const u32x4*)(dy + (int64_t)img * NPIX * COUT + 8 * v) : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  gload(blockIdx.x);
+  for (int img = blockIdx.x; img < B; img += gridDim.x) {
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PX; ++u) {
+      const int v = tid + u * NT;
+      if (v < XV) {
+        const int pix = v / (CIN / 8), c = v - pix * (CIN / 8);
+        const int P = (pix / HW + 2) * HP + (pix % HW) + 2;
+        *(u32x4*)(xs + P * SX + 8 * c) = px[u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      const int v = tid + u * NT;
+      if (v < DV) {
+        const int pix = v / (COUT / 8), c = v - pix * (COUT / 8);
+        const int Q = (pix / HW) * 16 + (pix % HW);
+        *(u32x4*)(ds + Q * SD + 8 * c) = pd[u];
+      }
+    }
+    __syncthreads();
+    gload(img + gridDim.x);
+    for (int ks = 0; ks < KSTEPS; ++ks) {
+      // B fragments: dY rows (2ks, 2ks+1) x 16 columns, all column tiles
+      bf16x8 b[NFW];
+      const bf16_t* db = ds + (2 * ks * 16 + 4 * g + q) * SD + 4 * p4;
+#pragma unroll
+      for (int n = 0; n < NFW; ++n)
+        b[n] = join(lds_tr4(db + 16 * n), lds_tr4(db + 16 * SD + 16 * n));
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) {
+        const int rt = wave + r * NW;
+        if (rt < RT) {                            // wave-uniform
+          bf16x8 a;
+          if (rt < RT - 1) {
+            const int t = rt / (CIN / 16), cb = rt - t * (CIN / 16);
+            const int P = (2 * ks + t / KS) * HP + (t % KS) + 4 * g + q;   // pixel k = 4g+q of row 2ks, tap t
+            const bf16_t* ab = xs + P * SX + 16 * cb + 4 * p4;
+            a = join(lds_tr4(ab), lds_tr4(ab + HP * SX));                  // +16 k = next image row
+          } else {
+            const bf16_t* ob = ones + (4 * g + q) * 16 + 4 * p4;
+            a = join(lds_tr4(ob), lds_tr4(ob + 16 * 16));
+          }
+#pragma unroll
+          for (int n = 0; n < NFW; ++n) acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[n], acc[r][n], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // partial -> slab[blockIdx][m][n]: D rows 4g + r2 of the tile, column (lane & 15)
+  float* out = slab + (int64_t)blockIdx.x * MTOT * COUT;
+  const int li = lane & 15;
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int rt = wave + r * NW;
+    if (rt < RT) {
+#pragma unroll
+      for (int n = 0; n < NFW; ++n)
+#pragma unroll
+        for (int r2 = 0; r2 < 4; ++r2) {
+          const int m = rt * 16 + 4 * g + r2;
+          if (m < MTOT) out[(int64_t)m * COUT + 16 * n + li] = acc[r][n][r2];
+        }
+    }
+  }
+}
+
+template <int CIN, int COUT, int NW>
+int halo_wgrad_resident() {
+  static int per = -1;
+  if (per < 0) {
+    int dev = 0, cus = 0, pc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, conv5_halo_wgrad_k<CIN, COUT, NW>, 64 * NW, 0) ==
+            hipSuccess &&
+        hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && pc > 0)
+      per = pc * cus;
+    else
+      per = 256;
+  }
+  return per;
+}
+
 template <int CIN, int CW, int NW, int MODE, int FR>
 int halo_grid(int B) {
   static int per = -1;
@@ -239,6 +378,21 @@ hipError_t conv5_halo_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int Cout,
     default: break;
   }
   return run_halo<64, 32, 4, 1, 4>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
+}
+
+bool conv5_halo_wgrad_ok(int H, int W, int C, int OH, int OW, int KH, int KW, int ph, int pw, int Cout,
+                         int with_bias) {
+  return with_bias && H == 14 && W == 14 && OH == 14 && OW == 14 && KH == 5 && KW == 5 && ph == 2 && pw == 2 &&
+         C == 32 && Cout == 64;
+}
+int conv5_halo_wgrad_grid(int Nb) {
+  const int r = halo_wgrad_resident<32, 64, 8>();
+  return Nb < r ? (Nb < 1 ? 1 : Nb) : r;
+}
+hipError_t conv5_halo_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int grid, float* slab, hipStream_t st) {
+  if (Nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL((conv5_halo_wgrad_k<32, 64, 8>), dim3(grid), dim3(512), 0, st, x, dy, Nb, slab);
+  return hipGetLastError();
 }
 
 }  // namespace mnistx

@@ -741,10 +741,11 @@ hipError_t dense_wgrad_group(int np, const bf16_t* const* x, const bf16_t* const
 }
 
 // MNISTX_CONV_HALO=0 keeps the im2col GEMM for the geometries conv_halo.hip covers
-static bool halo_enabled() {
+bool conv_halo_enabled() {
   static const int on = [] { const char* e = getenv("MNISTX_CONV_HALO"); return (e && e[0] == '0') ? 0 : 1; }();
   return on != 0;
 }
+static bool halo_enabled() { return conv_halo_enabled(); }
 
 hipError_t conv_fwd(const bf16_t* x, const bf16_t* w, int Nb, int H, int W, int C, int OH, int OW, int KH,
                     int KW, int ph, int pw, int Cout, const GemmEpi& ep, hipStream_t st) {
@@ -774,6 +775,10 @@ hipError_t conv_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int OH, int OW,
 hipError_t conv_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int H, int W, int C, int OH, int OW, int KH,
                       int KW, int ph, int pw, int Cout, int with_bias, int splits, const GemmEpi& ep,
                       hipStream_t st) {
+  // halo path: `splits` persistent blocks, one slab partial each (the binding sizes it)
+  if (halo_enabled() && ep.mode == EPI_SLAB && ep.ldc == Cout &&
+      conv5_halo_wgrad_ok(H, W, C, OH, OW, KH, KW, ph, pw, Cout, with_bias))
+    return conv5_halo_wgrad(x, dy, Nb, splits, (float*)ep.out, st);
   const int P = Nb * OH * OW, Mreal = KH * KW * C;
   Im2colMN a{x, H, W, C, OH, OW, KH, KW, ph, pw, P, Mreal, with_bias,
              FastDiv(OH * OW), FastDiv(OW), FastDiv(C), FastDiv(KW)};

@@ -43,6 +43,11 @@ hipError_t conv5_halo_fwd(const bf16_t* x, const bf16_t* w, int Nb, int C, int C
                           int relu, bf16_t* out, hipStream_t st);
 hipError_t conv5_halo_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int Cout, int Cin, const bf16_t* mask,
                             bf16_t* dx, hipStream_t st);
+bool conv5_halo_wgrad_ok(int H, int W, int C, int OH, int OW, int KH, int KW, int ph, int pw, int Cout,
+                         int with_bias);
+int conv5_halo_wgrad_grid(int Nb);   // persistent blocks (= slab partials) for Nb images
+hipError_t conv5_halo_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int grid, float* slab, hipStream_t st);
+bool conv_halo_enabled();            // MNISTX_CONV_HALO != 0
 hipError_t conv_fwd(const bf16_t* x, const bf16_t* w, int Nb, int H, int W, int C, int OH, int OW, int KH,
                     int KW, int ph, int pw, int Cout, const GemmEpi& ep, hipStream_t st);
 hipError_t conv_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int OH, int OW, int Cout, int H, int W,

@@ -80,7 +80,10 @@ class ConvLayer(_Layer):
         self.out = _bf16(B, self.OH, self.OW, self.Cp, device=dev)
         self.wname, self.bname = f"{spec.name}/weights", f"{spec.name}/biases"
         self.M_wg = spec.kh * spec.kw * self.C + 1
-        self.splits = Fk.pick_splits(self.M_wg, self.Cp, B * self.OH * self.OW)
+        # the LDS-halo weight gradient (conv_halo.hip) wants one partial per resident block
+        self.pref = (kernels().conv_wgrad_pref_splits(B, self.H, self.W, self.C, self.OH, self.OW, spec.kh, spec.kw,
+                                                      self.ph, self.pw, self.Cp, True) if dev.type == "cuda" else -1)
+        self.splits = max(Fk.pick_splits(self.M_wg, self.Cp, B * self.OH * self.OW), self.pref)
         self.slab_elems = self.splits * self.M_wg * self.Cp
 
     def fwd(self, nb: int) -> None:
@@ -92,8 +95,9 @@ class ConvLayer(_Layer):
     def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor, red: Optional[list] = None) -> None:
         s = self.spec
         K = kernels()
+        req = self.pref if self.pref > 0 else Fk.pick_splits(self.M_wg, self.Cp, nb * self.OH * self.OW)
         S = K.conv_wgrad(self.x, dy, slab, nb, self.H, self.W, self.C, self.OH, self.OW, s.kh, s.kw, self.ph, self.pw,
-                         self.Cp, True, Fk.pick_splits(self.M_wg, self.Cp, nb * self.OH * self.OW))
+                         self.Cp, True, req)
         _reduce(red, slab, (S, self.M_wg, self.Cp, s.kh * s.kw, self.C, s.cin, s.cout, s.kh * s.kw * self.C),
                 self.fp.grad_view(self.wname), self.fp.grad_view(self.bname))
 

@@ -41,7 +41,7 @@ DEV int swz(int r, int c) {
 // MODE 1 = data gradient: out[p][n] = mask * sum_{tap,ci} dy[p+tap][ci] W[24-tap][n][ci]
 //   (W is the conv's [kh][kw][cin][cout] filter; here ci runs over the conv's
 //    output channels and n over its input channels)
-template <int CIN, int CW, int NW, int MODE, int FR>
+template <int CIN, int CW, int NW, int MODE, int FR, int IMGS>
 __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                         int wcin, int wcout, const float* __restrict__ bias, int bias_n,
                                                         int relu, const bf16_t* __restrict__ mask, int ldm, int B,
@@ -50,19 +50,19 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict
   constexpr int CH = CIN / 8;                 // 16-byte chunks per pixel / filter row
   constexpr int NF = CW / 16;
   constexpr int KC = CIN / 32;                // 32-wide k-steps per tap
-  constexpr int XE = HP * HP * CIN;           // image tile elements
+  constexpr int XE = HP * HP * CIN;           // image tile elements (one image)
   constexpr int WE = NTAP * CW * CIN;         // filter slice elements
   constexpr int NV = NPIX * CH;               // 16-byte vectors per input image
-  constexpr int PER = (NV + NT - 1) / NT;
-  constexpr int NGRP = (MFR + FR - 1) / FR;   // fragment groups per image (FR fragments share the B reads)
+  constexpr int PER = (IMGS * NV + NT - 1) / NT;
+  constexpr int NGRP = (IMGS * MFR + FR - 1) / FR;   // fragment groups per image group (FR share the B reads)
   static_assert(CIN % 32 == 0 && CW % 16 == 0 && (CH == 4 || CH == 8), "conv5_halo geometry");
-  __shared__ __attribute__((aligned(16))) bf16_t xs[XE];
+  __shared__ __attribute__((aligned(16))) bf16_t xs[IMGS * XE];
   __shared__ __attribute__((aligned(16))) bf16_t ws[WE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.y * CW;
 
-  for (int e = tid; e < XE / 8; e += NT) *(u32x4*)(xs + 8 * e) = u32x4{0u, 0u, 0u, 0u};   // the halo stays zero
+  for (int e = tid; e < IMGS * XE / 8; e += NT) *(u32x4*)(xs + 8 * e) = u32x4{0u, 0u, 0u, 0u};   // halo stays zero
   // filter slice -> ws[(tap*CW + n)][ci] (swizzled chunks), once per block
   if constexpr (MODE == 0) {
     // W[tap][ci][n0 + n .. +7] is contiguous: one vector load, 8 scattered 2-byte LDS stores
@@ -85,34 +85,39 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict
   }
 
   u32x4 pre[PER];
-  auto gload = [&](int img) {
+  auto gload = [&](int img0) {               // images img0 .. img0+IMGS-1 are contiguous in HBM
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int v = tid + u * NT;
-      pre[u] = (v < NV && img < B) ? *(const u32x4*)(x + (int64_t)img * NPIX * CIN + 8 * v) : u32x4{0u, 0u, 0u, 0u};
+      pre[u] = (v < IMGS * NV && img0 + v / NV < B) ? *(const u32x4*)(x + (int64_t)img0 * NPIX * CIN + 8 * v)
+                                                  : u32x4{0u, 0u, 0u, 0u};
     }
   };
-  gload(blockIdx.x);
-  for (int img = blockIdx.x; img < B; img += gridDim.x) {
-    __syncthreads();                            // previous image's fragments consumed
+  const int gstride = gridDim.x * IMGS;
+  gload(blockIdx.x * IMGS);
+  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += gstride) {
+    __syncthreads();                            // previous group's fragments consumed
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int v = tid + u * NT;
-      if (v < NV) {
-        const int p = v / CH, c = v - p * CH;
+      if (v < IMGS * NV) {
+        const int im = v / NV, vv = v - im * NV;
+        const int p = vv / CH, c = vv - p * CH;
         const int P = (p / HW + 2) * HP + (p % HW) + 2;
-        *(u32x4*)(xs + P * CIN + (swz<CH>(P, c) << 3)) = pre[u];
+        const int PI = im * (XE / CIN) + P;      // pixel index across the group's tiles
+        *(u32x4*)(xs + PI * CIN + (swz<CH>(PI, c) << 3)) = pre[u];
       }
     }
     __syncthreads();
-    gload(img + gridDim.x);                     // next image in flight during the MFMAs
+    gload(img0 + gstride);                      // next group in flight during the MFMAs
     for (int gr = wave; gr < NGRP; gr += NW) {
       // fragments FR*gr .. FR*gr+FR-1 (fragments past the 13th are padding pixels)
-      int P0[FR];
+      int P0[FR];                               // element offset of the pixel's tap-(0,0) tile pixel
 #pragma unroll
       for (int h = 0; h < FR; ++h) {
-        const int p = min((FR * gr + h) * 16 + i, NPIX - 1);
-        P0[h] = (p / HW) * HP + (p % HW);       // tile pixel of tap (0,0)
+        const int f = min(FR * gr + h, IMGS * MFR - 1), im = f / MFR;
+        const int p = min((f - im * MFR) * 16 + i, NPIX - 1);
+        P0[h] = im * (XE / CIN) + (p / HW) * HP + (p % HW);
       }
       f32x4 acc[FR][NF];
 #pragma unroll
@@ -155,11 +160,12 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict
           const float bn = (MODE == 0 && bias != nullptr && n < bias_n) ? bias[n] : 0.f;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int q = (FR * gr + h) * 16 + 4 * g + r;
-            if (q < NPIX) {
+            const int f = FR * gr + h, im = f / MFR;
+            const int q = (f - im * MFR) * 16 + 4 * g + r;
+            if (f < IMGS * MFR && q < NPIX && img0 + im < B) {
               float v = acc[h][nf][r] + bn;
               if (relu) v = fmaxf(v, 0.f);
-              const int64_t row = (int64_t)img * NPIX + q;
+              const int64_t row = (int64_t)(img0 + im) * NPIX + q;
               if (mask != nullptr && !(bf2f(mask[row * ldm + n]) > 0.f)) v = 0.f;
               out[row * ldo + n] = f2bf(v);
             }
@@ -308,12 +314,12 @@ int halo_wgrad_resident() {
   return per;
 }
 
-template <int CIN, int CW, int NW, int MODE, int FR>
+template <int CIN, int CW, int NW, int MODE, int FR, int IMGS>
 int halo_grid(int B) {
   static int per = -1;
   if (per < 0) {
     int dev = 0, cus = 0, pc = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, conv5_halo_k<CIN, CW, NW, MODE, FR>, 64 * NW, 0) ==
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, conv5_halo_k<CIN, CW, NW, MODE, FR, IMGS>, 64 * NW, 0) ==
             hipSuccess &&
         hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && pc > 0)
@@ -321,15 +327,16 @@ int halo_grid(int B) {
     else
       per = 256;
   }
-  return B < per ? B : per;
+  const int groups = (B + IMGS - 1) / IMGS;
+  return groups < per ? groups : per;
 }
 
-template <int CIN, int CW, int NW, int MODE, int FR>
+template <int CIN, int CW, int NW, int MODE, int FR, int IMGS = 1>
 hipError_t run_halo(const bf16_t* x, const bf16_t* w, int wcin, int wcout, const float* bias, int bias_n, int relu,
                     const bf16_t* mask, int ldm, int B, bf16_t* out, int ncols, int ldo, hipStream_t st) {
   if (B <= 0) return hipSuccess;
-  dim3 grid(halo_grid<CIN, CW, NW, MODE, FR>(B), ncols / CW);
-  hipLaunchKernelGGL((conv5_halo_k<CIN, CW, NW, MODE, FR>), grid, dim3(64 * NW), 0, st, x, w, wcin, wcout, bias, bias_n,
+  dim3 grid(halo_grid<CIN, CW, NW, MODE, FR, IMGS>(B), ncols / CW);
+  hipLaunchKernelGGL((conv5_halo_k<CIN, CW, NW, MODE, FR, IMGS>), grid, dim3(64 * NW), 0, st, x, w, wcin, wcout, bias, bias_n,
                      relu, mask, ldm, B, out, ldo);
   return hipGetLastError();
 }
@@ -362,6 +369,10 @@ hipError_t conv5_halo_fwd(const bf16_t* x, const bf16_t* w, int Nb, int C, int C
       break;
     case 2:   // 8 waves, fragment pairs
       return run_halo<32, 32, 8, 0, 2>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
+    case 3:   // two images per block, 8 waves x (4 fragments x all 64 channels)
+      if (Cout == 64)
+        return run_halo<32, 64, 8, 0, 4, 2>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
+      break;
     default: break;
   }
   return run_halo<32, 32, 4, 0, 4>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);

@@ -460,8 +460,10 @@ void fused_optimizer(Tensor params, Tensor grads, Tensor mom, Tensor ema, Tensor
   TORCH_CHECK(expect_off == total, "segments do not cover the parameters");
   check(bf, at::kBFloat16, 0, "bf");
   float* l2p = nullptr;
+  const int l2n = max_l2;
   if (l2.has_value() && l2->defined()) {
-    check(*l2, at::kFloat, max_l2, "l2");
+    // [max_l2 per-tensor sums | one partial per optimizer block]
+    check(*l2, at::kFloat, (int64_t)max_l2 + mnistx::fused_optimizer_blocks(sv.data(), nseg), "l2");
     l2p = P<float>(*l2);
   }
   mnistx::OptParams op{};
@@ -475,7 +477,7 @@ void fused_optimizer(Tensor params, Tensor grads, Tensor mom, Tensor ema, Tensor
   op.ema_max = (float)ema_max;
   hip_ok(mnistx::fused_optimizer(P<float>(params), P<const float>(grads), use_momentum ? P<float>(mom) : nullptr,
                                  ema_max >= 0 ? P<float>(ema) : nullptr, BFm(bf), sv.data(), nseg, total,
-                                 P<const int64_t>(step), op, l2p, cur_stream()),
+                                 P<const int64_t>(step), op, l2p, l2n, cur_stream()),
          "fused_optimizer");
 }
 
@@ -659,6 +661,13 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("dh4") = py::none(), py::arg("dh3") = py::none(), py::arg("dx") = py::none(), py::arg("stats"),
         py::arg("work"));
   m.def("fused_optimizer", &fused_optimizer);
+  m.def("fused_optimizer_blocks", [](Tensor segs) {
+    TORCH_CHECK(!segs.is_cuda() && segs.scalar_type() == at::kLong && segs.dim() == 2, "segs: CPU int64 [n,14]");
+    auto a = segs.accessor<int64_t, 2>();
+    std::vector<mnistx::OptSeg> sv(segs.size(0));
+    for (int64_t i = 0; i < segs.size(0); ++i) sv[i].n = a[i][1];
+    return (int64_t)mnistx::fused_optimizer_blocks(sv.data(), (int)sv.size());
+  });
   m.def("finalize_step", &finalize_step);
   m.def("cast_f32_bf16_padded", &cast_f32_bf16_padded);
   m.def("convpool_supported", &convpool_supported);

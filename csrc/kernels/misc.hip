@@ -594,8 +594,10 @@ constexpr int OPT_EPT = 2;                       // elements per thread (more, s
 constexpr int OPT_CHUNK = TPB * OPT_EPT;         // elements per workgroup
 struct SegTable {
   OptSeg s[MAXSEG];
+  FastDiv fij[MAXSEG], fj[MAXSEG];   // I*J and J of each segment (bf16-copy index math)
   int blk0[MAXSEG + 1];
   int n;
+  int l2n;                           // l2[0..l2n): per-tensor sums; l2[l2n + block]: partials
 };
 
 __global__ __launch_bounds__(TPB) void fused_opt_k(float* __restrict__ params, const float* __restrict__ grads,
@@ -636,23 +638,47 @@ __global__ __launch_bounds__(TPB) void fused_opt_k(float* __restrict__ params, c
       ema[e] = s - (1.f - ema_d) * (s - p);
     }
     if (sg.bf_off >= 0) {
-      const int gg = (int)(li / ij);
-      const int64_t rem = li - gg * ij;
-      const int ii = (int)(rem / sg.J), jj = (int)(rem - (int64_t)ii * sg.J);
+      // 32-bit magic-number divisions (segments < 2^31 elements): the 64-bit divides
+      // here were most of this kernel's time on the 3.2M-element local3 weights
+      const int l32 = (int)li;
+      const int gg = tab.fij[si].div(l32);
+      const int rem = l32 - gg * (int)ij;
+      const int ii = tab.fj[si].div(rem), jj = rem - ii * sg.J;
       const bf16_t pb = f2bf(p);
       bf[sg.bf_off + ((int64_t)gg * sg.Ip + ii) * sg.Jp + jj] = pb;
       if (sg.bft_off >= 0) bf[sg.bft_off + (int64_t)jj * sg.It + ii] = pb;  // W^T copy (fused dense head)
     }
   }
   if (l2 && sg.track_l2) {
+    // per-block partial, summed in block order by l2_combine_k: one float atomic per
+    // block on ONE address serialised ~6.8K blocks (96 us of the reference CNN's
+    // update) and made the weight-decay loss order-dependent
     sq = warp_sum(sq);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
     __syncthreads();
     if (threadIdx.x == 0) {
       float t = 0.f;
       for (int w = 0; w < TPB / 64; ++w) t += red[w];
-      atomicAdd(&l2[sg.track_l2 - 1], t);
+      l2[tab.l2n + blockIdx.x] = t;
     }
+  }
+}
+
+// l2[track-1] += sum of the segment's block partials, fixed order (one block per segment)
+__global__ __launch_bounds__(TPB) void l2_combine_k(float* __restrict__ l2, SegTable tab) {
+  __shared__ float red[TPB / 64];
+  const OptSeg sg = tab.s[blockIdx.x];
+  if (!sg.track_l2) return;
+  const int b0 = tab.blk0[blockIdx.x], b1 = tab.blk0[blockIdx.x + 1];
+  float t = 0.f;
+  for (int b = b0 + (int)threadIdx.x; b < b1; b += TPB) t += l2[tab.l2n + b];
+  t = warp_sum(t);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float v = 0.f;
+    for (int w = 0; w < TPB / 64; ++w) v += red[w];
+    l2[sg.track_l2 - 1] += v;
   }
 }
 
@@ -841,20 +867,32 @@ hipError_t splitk_reduce(float* slab, int splits, int M, int N, int G, int Ipad,
   return splitk_reduce_multi(&r, 1, st);
 }
 
+int fused_optimizer_blocks(const OptSeg* segs, int nseg) {
+  int nb = 0;
+  for (int i = 0; i < nseg; ++i) nb += (int)((segs[i].n + OPT_CHUNK - 1) / OPT_CHUNK);
+  return nb;
+}
+
 hipError_t fused_optimizer(float* params, const float* grads, float* mom, float* ema, bf16_t* bf, const OptSeg* segs,
-                           int nseg, int64_t total, const int64_t* step, OptParams op, float* l2, hipStream_t st) {
+                           int nseg, int64_t total, const int64_t* step, OptParams op, float* l2, int l2n,
+                           hipStream_t st) {
   if (nseg > MAXSEG || nseg < 1) return hipErrorInvalidValue;
   SegTable tab;
   int nb = 0;
   for (int i = 0; i < nseg; ++i) {
+    if (segs[i].n >= (1ll << 31) || (int64_t)segs[i].I * segs[i].J >= (1ll << 31)) return hipErrorInvalidValue;
     tab.s[i] = segs[i];
+    tab.fij[i] = FastDiv((uint32_t)(segs[i].I * segs[i].J));
+    tab.fj[i] = FastDiv((uint32_t)segs[i].J);
     tab.blk0[i] = nb;
     nb += (int)((segs[i].n + OPT_CHUNK - 1) / OPT_CHUNK);
   }
   tab.blk0[nseg] = nb;
   tab.n = nseg;
+  tab.l2n = l2n;
   (void)total;
   hipLaunchKernelGGL(fused_opt_k, dim3(nb), dim3(TPB), 0, st, params, grads, mom, ema, bf, tab, step, op, l2);
+  if (l2) hipLaunchKernelGGL(l2_combine_k, dim3(nseg), dim3(TPB), 0, st, l2, tab);
   return hipGetLastError();
 }
 

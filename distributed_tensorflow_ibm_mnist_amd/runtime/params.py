@@ -80,7 +80,10 @@ class FlatParams:
         self.bf16 = torch.zeros(max(bf_total, 1), dtype=torch.bfloat16, device=device)
         self.step = torch.zeros(1, dtype=torch.int64, device=device)
         self.wd_entries = [e for e in entries if e.l2_index >= 0]
-        self.l2 = torch.zeros(max(len(self.wd_entries), 1), dtype=torch.float32, device=device)
+        # [per-tensor sum(w^2) | one partial per fused-optimizer block (misc.hip OPT_CHUNK =
+        # 512 elements)]: the partials are combined in block order (deterministic)
+        n_opt_blocks = sum(-(-e.n // 512) for e in entries)
+        self.l2 = torch.zeros(max(len(self.wd_entries), 1) + n_opt_blocks, dtype=torch.float32, device=device)
         self.wds = torch.tensor([float(e.wd) for e in self.wd_entries] or [0.0], dtype=torch.float32,
                                 device=device)
         # name -> (offset in bf16, Jt, It): optional transposed bf16 copies W^T [Jt][It]

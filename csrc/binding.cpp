@@ -482,7 +482,8 @@ void fused_optimizer(Tensor params, Tensor grads, Tensor mom, Tensor ema, Tensor
 }
 
 void finalize_step(Tensor step, Tensor stats, optional<Tensor> l2, optional<Tensor> wds, int64_t nw,
-                   optional<Tensor> loss_ema, int64_t n_ema, int64_t batch, bool increment) {
+                   optional<Tensor> loss_ema, int64_t n_ema, int64_t batch, bool increment,
+                   optional<Tensor> l2_ranges) {
   check(step, at::kLong, 1, "step");
   check(stats, at::kFloat, 8, "stats");
   const float* l2p = nullptr;
@@ -499,8 +500,14 @@ void finalize_step(Tensor step, Tensor stats, optional<Tensor> l2, optional<Tens
     check(*loss_ema, at::kFloat, 3 * n_ema, "loss_ema");
     le = P<float>(*loss_ema);
   }
-  hip_ok(mnistx::finalize_step(P<int64_t>(step), P<float>(stats), l2p, wp, (int)nw, le, le ? (int)n_ema : 0,
-                               (int)batch, increment ? 1 : 0, cur_stream()),
+  const int* rp = nullptr;
+  if (nw > 0 && l2_ranges.has_value() && l2_ranges->defined()) {
+    check(*l2_ranges, at::kInt, 3 * nw, "l2_ranges");
+    rp = P<const int>(*l2_ranges);
+    // partials follow the nw per-weight slots (binding fused_optimizer: l2n = max track index)
+  }
+  hip_ok(mnistx::finalize_step(P<int64_t>(step), P<float>(stats), l2p, rp, (int)nw, wp, (int)nw, le,
+                               le ? (int)n_ema : 0, (int)batch, increment ? 1 : 0, cur_stream()),
          "finalize_step");
 }
 
@@ -668,7 +675,9 @@ PYBIND11_MODULE(_kernels, m) {
     for (int64_t i = 0; i < segs.size(0); ++i) sv[i].n = a[i][1];
     return (int64_t)mnistx::fused_optimizer_blocks(sv.data(), (int)sv.size());
   });
-  m.def("finalize_step", &finalize_step);
+  m.def("finalize_step", &finalize_step, py::arg("step"), py::arg("stats"), py::arg("l2"), py::arg("wds"),
+        py::arg("nw"), py::arg("loss_ema"), py::arg("n_ema"), py::arg("batch"), py::arg("increment"),
+        py::arg("l2_ranges") = py::none());
   m.def("cast_f32_bf16_padded", &cast_f32_bf16_padded);
   m.def("convpool_supported", &convpool_supported);
   m.def("convpool_rows", &convpool_rows);

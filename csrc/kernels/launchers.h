@@ -146,8 +146,10 @@ struct OptParams {
 int fused_optimizer_blocks(const OptSeg* segs, int nseg);
 hipError_t fused_optimizer(float* params, const float* grads, float* mom, float* ema, bf16_t* bf, const OptSeg* segs,
                            int nseg, int64_t total, const int64_t* step, OptParams op, float* l2, int l2n, hipStream_t st);
-hipError_t finalize_step(int64_t* step, float* stats, const float* l2, const float* wds, int nw, float* loss_ema,
-                         int n_ema, int batch, int increment, hipStream_t st);
+// l2r (optional, device int32 [nw][3] = {weight index, first block, end block}): sum the
+// fused optimizer's per-block partials at l2[l2base + block] for each weight
+hipError_t finalize_step(int64_t* step, float* stats, const float* l2, const int* l2r, int l2base, const float* wds,
+                         int nw, float* loss_ema, int n_ema, int batch, int increment, hipStream_t st);
 hipError_t cast_f32_bf16_padded(const float* src, bf16_t* dst, int G, int I, int J, int Ip, int Jp,
                                 hipStream_t st);
 

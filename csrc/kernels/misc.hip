@@ -650,7 +650,7 @@ __global__ __launch_bounds__(TPB) void fused_opt_k(float* __restrict__ params, c
     }
   }
   if (l2 && sg.track_l2) {
-    // per-block partial, summed in block order by l2_combine_k: one float atomic per
+    // per-block partial, summed in block order by finalize_k: one float atomic per
     // block on ONE address serialised ~6.8K blocks (96 us of the reference CNN's
     // update) and made the weight-decay loss order-dependent
     sq = warp_sum(sq);
@@ -664,36 +664,37 @@ __global__ __launch_bounds__(TPB) void fused_opt_k(float* __restrict__ params, c
   }
 }
 
-// l2[track-1] += sum of the segment's block partials, fixed order (one block per segment)
-__global__ __launch_bounds__(TPB) void l2_combine_k(float* __restrict__ l2, SegTable tab) {
-  __shared__ float red[TPB / 64];
-  const OptSeg sg = tab.s[blockIdx.x];
-  if (!sg.track_l2) return;
-  const int b0 = tab.blk0[blockIdx.x], b1 = tab.blk0[blockIdx.x + 1];
-  float t = 0.f;
-  for (int b = b0 + (int)threadIdx.x; b < b1; b += TPB) t += l2[tab.l2n + b];
-  t = warp_sum(t);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float v = 0.f;
-    for (int w = 0; w < TPB / 64; ++w) v += red[w];
-    l2[sg.track_l2 - 1] += v;
-  }
-}
-
 // stats: [0] ce_sum acc [1] correct acc [2] nan flag [3] -
 //        [4] ce_mean [5] accuracy [6] total_loss [7] steps done (float)
 // loss_ema: n_ema x {biased, local_step, avg}  (TF zero-debiased EMA, decay 0.9:
 //           mnist_input.py:288-290); order = weight losses..., cross_entropy, total_loss
-__global__ void finalize_k(int64_t* step, float* stats, float* l2, const float* wds, int nw, float* loss_ema,
-                           int n_ema, int batch, int increment) {
+__global__ void finalize_k(int64_t* step, float* stats, float* l2, const int* __restrict__ l2r, int l2base,
+                           const float* wds, int nw, float* loss_ema, int n_ema, int batch, int increment) {
   // one wave; lane i owns loss entry i (weight losses..., cross_entropy, total_loss), so the
   // EMA read-modify-writes run in parallel instead of as one dependent chain
   const int t = threadIdx.x;
   const float ce = stats[0] / (float)batch;
   const float acc = stats[1] / (float)batch;
-  const float wl = t < nw ? wds[t] * 0.5f * (l2 ? l2[t] : 0.f) : 0.f;
+  // sum(w^2) of weight t: the fused optimizer's per-block partials l2[l2base + b],
+  // b in [l2r[3w+1], l2r[3w+2]), summed by the whole wave in a fixed order
+  float l2v = (l2 && t < nw) ? l2[t] : 0.f;
+  if (l2 && l2r) {
+    for (int w = 0; w < nw; ++w) {
+      const int idx = l2r[3 * w], b0 = l2r[3 * w + 1], b1 = l2r[3 * w + 2];
+      // 4 independent chains per lane (loads in flight), combined in a fixed order
+      float s4[4] = {0.f, 0.f, 0.f, 0.f};
+      int b = b0 + t;
+      for (; b + 192 < b1; b += 256) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s4[u] += l2[l2base + b + 64 * u];
+      }
+      for (; b < b1; b += 64) s4[0] += l2[l2base + b];
+      float sum = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+      sum = warp_sum(sum);
+      if (t == idx) l2v += sum;
+    }
+  }
+  const float wl = t < nw ? wds[t] * 0.5f * l2v : 0.f;
   float total = ce;
   for (int i = 0; i < nw; ++i) total += __shfl(wl, i, 64);   // fixed order (bitwise as before)
   if (loss_ema && t < n_ema && t < nw + 2) {
@@ -892,14 +893,13 @@ hipError_t fused_optimizer(float* params, const float* grads, float* mom, float*
   tab.l2n = l2n;
   (void)total;
   hipLaunchKernelGGL(fused_opt_k, dim3(nb), dim3(TPB), 0, st, params, grads, mom, ema, bf, tab, step, op, l2);
-  if (l2) hipLaunchKernelGGL(l2_combine_k, dim3(nseg), dim3(TPB), 0, st, l2, tab);
   return hipGetLastError();
 }
 
-hipError_t finalize_step(int64_t* step, float* stats, const float* l2, const float* wds, int nw, float* loss_ema,
-                         int n_ema, int batch, int increment, hipStream_t st) {
-  hipLaunchKernelGGL(finalize_k, dim3(1), dim3(64), 0, st, step, stats, (float*)l2, wds, nw, loss_ema, n_ema, batch,
-                     increment);
+hipError_t finalize_step(int64_t* step, float* stats, const float* l2, const int* l2r, int l2base, const float* wds,
+                         int nw, float* loss_ema, int n_ema, int batch, int increment, hipStream_t st) {
+  hipLaunchKernelGGL(finalize_k, dim3(1), dim3(64), 0, st, step, stats, (float*)l2, l2r, l2base, wds, nw, loss_ema,
+                     n_ema, batch, increment);
   return hipGetLastError();
 }
 

@@ -563,7 +563,8 @@ class HipNet:
         fp = self.fp
         nw = len(fp.wd_entries)
         kernels().finalize_step(fp.step, self.stats, fp.l2 if nw else None, fp.wds if nw else None, nw,
-                                self.loss_ema, len(self.loss_names), batch, increment)
+                                self.loss_ema, len(self.loss_names), batch, increment,
+                                fp.l2_ranges if nw else None)
 
     def train_step(self, grad_scale: float = 1.0) -> None:
         self.forward(defer_head=True)

@@ -89,6 +89,14 @@ class FlatParams:
         # name -> (offset in bf16, Jt, It): optional transposed bf16 copies W^T [Jt][It]
         self.bft: Dict[str, Tuple[int, int, int]] = {}
         self._build_segs()
+        # finalize_step: {weight index, first, end fused-optimizer block} per tracked weight
+        ranges, b = [], 0
+        for e in entries:
+            nb = -(-e.n // 512)
+            if e.l2_index >= 0:
+                ranges.append([e.l2_index, b, b + nb])
+            b += nb
+        self.l2_ranges = torch.tensor(ranges or [[0, 0, 0]], dtype=torch.int32, device=device)
 
     def _build_segs(self) -> None:
         rows = []

@@ -135,3 +135,25 @@ def test_u8_input_path_bitwise_equal(dev, K, model):
     # eval keeps reading x0
     b.x0.copy_(a.x0)
     assert torch.equal(a.eval_batch(200, torch.zeros(8, device=dev)), b.eval_batch(200, torch.zeros(8, device=dev)))
+
+
+def test_weight_decay_total_loss(dev, K):
+    """total_loss = cross-entropy + sum_i wd_i/2 ||W_i||^2 (pre-update weights): the
+    fused optimizer's per-block sum(w^2) partials combined in block order by
+    finalize_k; bitwise identical over two identical runs (no float atomics)."""
+    spec = get_model("reference_cnn", 1)
+    totals = []
+    for _ in range(2):
+        net = HipNet(spec, 64, dev, torch_ref.init_params(spec, seed=3), OptConfig(lr0=0.01))
+        g = torch.Generator(device=dev).manual_seed(1)
+        net.x0.copy_((torch.rand(net.x0.shape, device=dev, generator=g) - 0.5).to(torch.bfloat16))
+        net.labels.copy_(torch.randint(0, 10, (64,), device=dev, generator=g, dtype=torch.int32))
+        wd_term = sum(float(e.wd) * 0.5 * float((net.fp.param_view(e.name).double() ** 2).sum())
+                      for e in net.fp.wd_entries)
+        net.train_step()
+        torch.cuda.synchronize()
+        st = net.read_stats()
+        assert wd_term > 0
+        assert abs(st["total_loss"] - (st["cross_entropy"] + wd_term)) < 1e-4 * max(1.0, wd_term), (st, wd_term)
+        totals.append(net.stats[6].item())
+    assert totals[0] == totals[1]

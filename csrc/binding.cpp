@@ -222,6 +222,20 @@ void perm_positions(Tensor out, int64_t start, int64_t N, int64_t seed, int64_t 
          "perm_positions");
 }
 
+void prep_images_perm(Tensor src, Tensor lab_src, Tensor out, Tensor lab_out, int64_t B, int64_t start, int64_t seed,
+                      int64_t h) {
+  TORCH_CHECK(src.dim() == 2 && src.size(1) == 784, "prep_images_perm: [N, 784] uint8 dataset");
+  const int64_t N = src.size(0);
+  check(src, at::kByte, N * 784, "src");
+  check(lab_src, at::kInt, N, "lab_src");
+  check(out, at::kBFloat16, B * 784, "out");
+  check(lab_out, at::kInt, B, "lab_out");
+  TORCH_CHECK(N > 0 && h >= 1 && h <= 31 && (1ll << (2 * h)) >= N, "prep_images_perm: bad domain");
+  hip_ok(mnistx::prep_images_perm(P<const uint8_t>(src), P<const int32_t>(lab_src), (int)B, start, N, (uint32_t)seed,
+                                  (int)h, BFm(out), P<int32_t>(lab_out), cur_stream()),
+         "prep_images_perm");
+}
+
 void prep_images(Tensor src, Tensor idx, Tensor lab_src, Tensor out, Tensor lab_out, int64_t HW, int64_t Csrc,
                  int64_t Cdst) {
   const int64_t B = idx.numel();
@@ -652,6 +666,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("dense_wgrad_group", &dense_wgrad_group);
   m.def("conv_wgrad_pref_splits", &conv_wgrad_pref_splits);
   m.def("perm_positions", &perm_positions);
+  m.def("prep_images_perm", &prep_images_perm);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("lrn_fwd", &lrn_fwd);

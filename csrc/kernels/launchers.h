@@ -83,6 +83,10 @@ hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const b
 
 // ---- misc.hip
 hipError_t perm_positions(int64_t* out, int64_t start, int n, int64_t N, uint32_t seed, int h, hipStream_t st);
+// 28x28x1 batch gather + normalise with the Feistel epoch shuffle fused in (rows are
+// perm_positions(start + b)): no index array, no separate permutation launch
+hipError_t prep_images_perm(const uint8_t* src, const int32_t* lab_src, int B, int64_t start, int64_t N,
+                            uint32_t seed, int h, bf16_t* out, int32_t* lab_out, hipStream_t st);
 hipError_t prep_images(const uint8_t* src, const int64_t* idx, const int32_t* lab_src, int B, int HW, int Csrc,
                        int Cdst, bf16_t* out, int32_t* lab_out, hipStream_t st);
 hipError_t maxpool_fwd(const bf16_t* x, int Nb, int H, int W, int C, int OH, int OW, bf16_t* y, uint8_t* arg,

@@ -129,6 +129,42 @@ __global__ __launch_bounds__(256) void prep_images_784_k(const uint8_t* __restri
   }
 }
 
+// K10 hot path with the epoch shuffle fused in: the dataset row of batch entry b is
+// the Feistel image of stream position start + b (perm_positions_k), computed by
+// each thread (a few dozen integer ops) instead of by a separate launch + index array.
+__global__ __launch_bounds__(256) void prep_images_784_perm_k(const uint8_t* __restrict__ src,
+                                                               const int32_t* __restrict__ lab_src, int B,
+                                                               int64_t start, int64_t N, uint32_t seed, int h,
+                                                               bf16_t* __restrict__ out,
+                                                               int32_t* __restrict__ lab_out) {
+  const int nvec = B * PREP_V;
+  for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += gridDim.x * blockDim.x) {
+    const int b = v / PREP_V, w = v - b * PREP_V;
+    const int64_t p = start + b;
+    const int64_t e = p / N;
+    uint64_t x = (uint64_t)(p - e * N);
+    const uint32_t ek = mix32((uint32_t)e ^ 0x9e3779b9u) ^ seed;
+    uint32_t key[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) key[r] = mix32(ek + 0x85ebca77u * (uint32_t)(r + 1));
+    do { x = feistel4(x, key, h); } while (x >= (uint64_t)N);
+    const int64_t row = (int64_t)x;
+    const u32x4 px = *(const u32x4*)(src + row * 784 + 16 * w);
+    u32x4 o0, o1;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      o0[2 * j] = pack2(u8_norm(px[j] & 0xff), u8_norm((px[j] >> 8) & 0xff));
+      o0[2 * j + 1] = pack2(u8_norm((px[j] >> 16) & 0xff), u8_norm(px[j] >> 24));
+      o1[2 * j] = pack2(u8_norm(px[2 + j] & 0xff), u8_norm((px[2 + j] >> 8) & 0xff));
+      o1[2 * j + 1] = pack2(u8_norm((px[2 + j] >> 16) & 0xff), u8_norm(px[2 + j] >> 24));
+    }
+    bf16_t* dst = out + (int64_t)b * 784 + 16 * w;
+    *(u32x4*)dst = o0;
+    *(u32x4*)(dst + 8) = o1;
+    if (w == 0) lab_out[b] = lab_src[row];
+  }
+}
+
 // ------------------------------------------------------------------ K6 max-pool 2x2/2 SAME
 __global__ void maxpool_fwd_k(const bf16_t* __restrict__ x, int Nb, int H, int W, int C, int OH, int OW,
                               bf16_t* __restrict__ y, uint8_t* __restrict__ arg) {
@@ -736,6 +772,15 @@ __global__ void cast_pad_k(const float* __restrict__ src, bf16_t* __restrict__ d
 hipError_t perm_positions(int64_t* out, int64_t start, int n, int64_t N, uint32_t seed, int h, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(perm_positions_k, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, st, out, start, n, N, seed, h);
+  return hipGetLastError();
+}
+
+hipError_t prep_images_perm(const uint8_t* src, const int32_t* lab_src, int B, int64_t start, int64_t N,
+                            uint32_t seed, int h, bf16_t* out, int32_t* lab_out, hipStream_t st) {
+  if ((uintptr_t)src % 16 || (uintptr_t)out % 16 || (int64_t)B * PREP_V >= (1ll << 31)) return hipErrorInvalidValue;
+  const int64_t nvec = (int64_t)B * PREP_V;
+  hipLaunchKernelGGL(prep_images_784_perm_k, dim3(nblocks(nvec, 256, 8192)), dim3(256), 0, st, src, lab_src, B, start,
+                     N, seed, h, out, lab_out);
   return hipGetLastError();
 }
 

@@ -139,6 +139,13 @@ class DeviceLoader:
         nb = self.B if nb is None else nb
         start = self.pos + (self.rank * self.B if self.shard else 0)
         N = len(self.ds)
+        if (self.shuffle and self.idx_out is None and self.ds.device.type == "cuda" and self.ds.hw == 784
+                and self.ds.channels == 1 and self.cdst == 1):
+            # one kernel: Feistel row + gather + normalise (+ labels)
+            kernels().prep_images_perm(self.ds.images, self.ds.labels, self.out_images, self.out_labels, nb,
+                                       int(start), int(self.seed), _half_bits(N))
+            self.pos += self.global_batch
+            return nb
         if self.shuffle:
             idx = perm_positions(start, nb, N, self.seed, out=self.idx)
         else:

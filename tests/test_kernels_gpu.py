@@ -433,3 +433,20 @@ def test_dense_wgrad_group_matches_single(dev, K):
         tot = slab[: sg * (d + 1) * n].view(sg, d + 1, n).sum(0)
         exp = torch.cat([x.float().t() @ dy.float(), dy.float().sum(0, keepdim=True)])
         close(tot, exp, rel=1e-3)
+
+
+def test_prep_images_perm_matches_two_step(dev, K):
+    """Fused Feistel row + gather + normalise == perm_positions + prep_images."""
+    from distributed_tensorflow_ibm_mnist_amd.data.device_loader import _half_bits, perm_positions
+    torch.manual_seed(4)
+    N, B = 1000, 300
+    src = torch.randint(0, 256, (N, 784), dtype=torch.uint8, device=dev)
+    lab = torch.randint(0, 10, (N,), dtype=torch.int32, device=dev)
+    out = torch.empty(B, 28, 28, 1, dtype=torch.bfloat16, device=dev)
+    lo = torch.empty(B, dtype=torch.int32, device=dev)
+    K.prep_images_perm(src, lab, out, lo, B, 2500, 77, _half_bits(N))
+    idx = perm_positions(2500, B, N, 77, device=dev)
+    out2 = torch.empty_like(out)
+    lo2 = torch.empty_like(lo)
+    K.prep_images(src, idx, lab, out2, lo2, 784, 1, 1)
+    assert torch.equal(out, out2) and torch.equal(lo, lo2)

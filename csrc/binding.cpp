@@ -294,6 +294,33 @@ void lrn_bwd(Tensor x, Tensor dy, Tensor dx, int64_t P_, int64_t C, int64_t r, d
          "lrn_bwd");
 }
 
+bool lrn_pool_supported(int64_t H, int64_t W, int64_t C, int64_t r) {
+  return mnistx::lrn_pool_supported((int)H, (int)W, (int)C, (int)r);
+}
+
+void lrn_pool_fwd(Tensor x, Tensor y, Tensor arg, int64_t Nb, int64_t H, int64_t W, int64_t C, int64_t r,
+                  double bias, double alpha, double beta) {
+  TORCH_CHECK(mnistx::lrn_pool_supported((int)H, (int)W, (int)C, (int)r), "lrn_pool: unsupported geometry");
+  check(x, at::kBFloat16, Nb * H * W * C, "x");
+  check(y, at::kBFloat16, Nb * (H / 2) * (W / 2) * C, "y");
+  check(arg, at::kByte, Nb * (H / 2) * (W / 2) * C, "arg");
+  hip_ok(mnistx::lrn_pool_fwd(BF(x), (int)Nb, (int)H, (int)W, (int)C, (int)r, (float)bias, (float)alpha,
+                              (float)beta, BFm(y), P<uint8_t>(arg), cur_stream()),
+         "lrn_pool_fwd");
+}
+
+void lrn_pool_bwd(Tensor x, Tensor dP, Tensor arg, Tensor dx, int64_t Nb, int64_t H, int64_t W, int64_t C,
+                  int64_t r, double bias, double alpha, double beta, bool relu_mask) {
+  TORCH_CHECK(mnistx::lrn_pool_supported((int)H, (int)W, (int)C, (int)r), "lrn_pool: unsupported geometry");
+  check(x, at::kBFloat16, Nb * H * W * C, "x");
+  check(dP, at::kBFloat16, Nb * (H / 2) * (W / 2) * C, "dP");
+  check(arg, at::kByte, Nb * (H / 2) * (W / 2) * C, "arg");
+  check(dx, at::kBFloat16, Nb * H * W * C, "dx");
+  hip_ok(mnistx::lrn_pool_bwd(BF(x), BF(dP), P<const uint8_t>(arg), (int)Nb, (int)H, (int)W, (int)C, (int)r,
+                              (float)bias, (float)alpha, (float)beta, relu_mask ? 1 : 0, BFm(dx), cur_stream()),
+         "lrn_pool_bwd");
+}
+
 void softmax_ce(Tensor logits, int64_t ldl, optional<Tensor> labels, int64_t B, int64_t NC, double scale,
                 optional<Tensor> dlogits, int64_t ldd, optional<Tensor> stats, optional<Tensor> probs,
                 optional<Tensor> work) {
@@ -671,6 +698,9 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("lrn_fwd", &lrn_fwd);
   m.def("lrn_bwd", &lrn_bwd);
+  m.def("lrn_pool_supported", &lrn_pool_supported);
+  m.def("lrn_pool_fwd", &lrn_pool_fwd);
+  m.def("lrn_pool_bwd", &lrn_pool_bwd);
   m.def("softmax_ce", &softmax_ce, py::arg("logits"), py::arg("ldl"), py::arg("labels"), py::arg("B"), py::arg("NC"),
         py::arg("scale"), py::arg("dlogits"), py::arg("ldd"), py::arg("stats"), py::arg("probs"),
         py::arg("work") = py::none());

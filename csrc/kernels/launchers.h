@@ -97,6 +97,13 @@ hipError_t lrn_fwd(const bf16_t* x, int P, int C, int r, float bias, float alpha
                    hipStream_t st);
 hipError_t lrn_bwd(const bf16_t* x, const bf16_t* dy, int P, int C, int r, float bias, float alpha, float beta,
                    int relu_mask, bf16_t* dx, hipStream_t st);
+// fused LRN -> 2x2/2 max-pool (even H, W; C 32/64, radius 4): pooled y + argmax bytes,
+// and its backward from the pooled gradient
+bool lrn_pool_supported(int H, int W, int C, int r);
+hipError_t lrn_pool_fwd(const bf16_t* x, int Nb, int H, int W, int C, int r, float bias, float alpha, float beta,
+                        bf16_t* y, uint8_t* arg, hipStream_t st);
+hipError_t lrn_pool_bwd(const bf16_t* x, const bf16_t* dP, const uint8_t* arg, int Nb, int H, int W, int C, int r,
+                        float bias, float alpha, float beta, int relu_mask, bf16_t* dx, hipStream_t st);
 // work (optional): >= 4*1024+1 floats, zero-initialised once; makes the loss /
 // accuracy sums deterministic (per-block partials combined in block order)
 hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B, int NC, float scale,

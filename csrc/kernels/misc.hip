@@ -369,6 +369,123 @@ __global__ __launch_bounds__(TPB) void lrn_bwd_k(const bf16_t* __restrict__ x, c
   }
 }
 
+// ------------------------------------------------------------------ K7+K6 fused: LRN -> 2x2/2 max-pool
+// The reference CNN's norm2 -> pool2 (mnist_input.py:168-172) as one pass: lane
+// group = one pool window, lane = 8 channels of it; the LRN of the window's 4 pixels
+// is computed in registers and only the pooled maximum (+ argmax byte) is written,
+// so the full-resolution LRN output never goes to HBM (and is never re-read by the
+// pool).  Pooling compares the bf16-rounded LRN values in window order, exactly
+// like lrn_fwd + maxpool_fwd.  Backward: unpool dP through the argmax into the 4
+// pixels' dY in registers and apply the LRN gradient directly (no dY image).
+template <int C, int R>
+__global__ __launch_bounds__(TPB) void lrn_pool_fwd_k(const bf16_t* __restrict__ x, int Nb, int H, int W, float bias,
+                                                      float alpha, float beta, bf16_t* __restrict__ y,
+                                                      uint8_t* __restrict__ arg) {
+  constexpr int G = C / 8;
+  const int OH = H / 2, OW = W / 2;
+  const int64_t total = (int64_t)Nb * OH * OW * G;
+  const int c8 = threadIdx.x % G;
+  for (int64_t base = (int64_t)blockIdx.x * TPB; base < total; base += (int64_t)gridDim.x * TPB) {
+    const int64_t t = base + threadIdx.x;
+    const bool ok = t < total;
+    const int64_t win = ok ? t / G : 0;
+    const int ow = (int)(win % OW);
+    const int64_t r = win / OW;
+    const int oh = (int)(r % OH);
+    const int64_t n = r / OH;
+    float best[8];
+    uint32_t bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int ih = 2 * oh + (d >> 1), iw = 2 * ow + (d & 1);
+      const u32x4 xv = ok ? *(const u32x4*)(x + ((n * H + ih) * W + iw) * C + c8 * 8) : u32x4{0u, 0u, 0u, 0u};
+      float v[8], sq[8], s[8];
+      unpack8(xv, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sq[j] = v[j] * v[j];
+      lane_window_sums<G, R>(sq, c8, s);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = bf2f(f2bf(v[j] * powp(bias + alpha * s[j], -beta)));
+        if (f > best[j]) { best[j] = f; bi[j] = d; }
+      }
+    }
+    if (ok) {
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = pack2(best[2 * j], best[2 * j + 1]);
+      const int64_t off = win * C + c8 * 8;
+      *(u32x4*)(y + off) = o;
+      *(u32x2*)(arg + off) = u32x2{bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24),
+                                   bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24)};
+    }
+  }
+}
+
+template <int C, int R>
+__global__ __launch_bounds__(TPB) void lrn_pool_bwd_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dP,
+                                                      const uint8_t* __restrict__ arg, int Nb, int H, int W,
+                                                      float bias, float alpha, float beta, int relu_mask,
+                                                      bf16_t* __restrict__ dx) {
+  constexpr int G = C / 8;
+  const int OH = H / 2, OW = W / 2;
+  const int64_t total = (int64_t)Nb * OH * OW * G;
+  const int c8 = threadIdx.x % G;
+  for (int64_t base = (int64_t)blockIdx.x * TPB; base < total; base += (int64_t)gridDim.x * TPB) {
+    const int64_t t = base + threadIdx.x;
+    const bool ok = t < total;
+    const int64_t win = ok ? t / G : 0;
+    const int ow = (int)(win % OW);
+    const int64_t r = win / OW;
+    const int oh = (int)(r % OH);
+    const int64_t n = r / OH;
+    const int64_t poff = win * C + c8 * 8;
+    const u32x4 pv = ok ? *(const u32x4*)(dP + poff) : u32x4{0u, 0u, 0u, 0u};
+    const u32x2 av = ok ? *(const u32x2*)(arg + poff) : u32x2{0u, 0u};
+    float pg[8];
+    unpack8(pv, pg);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int ih = 2 * oh + (d >> 1), iw = 2 * ow + (d & 1);
+      const int64_t xoff = ((n * H + ih) * W + iw) * C + c8 * 8;
+      const u32x4 xv = ok ? *(const u32x4*)(x + xoff) : u32x4{0u, 0u, 0u, 0u};
+      float v[8], g[8], w[8], s[8], u[8];
+      unpack8(xv, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t aj = ((j < 4 ? av[0] : av[1]) >> (8 * (j & 3))) & 0xffu;
+        g[j] = aj == (uint32_t)d ? pg[j] : 0.f;          // max-unpool
+        w[j] = v[j] * v[j];
+      }
+      lane_window_sums<G, R>(w, c8, s);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float sc = bias + alpha * s[j];
+        const float pw = powp(sc, -beta);
+        s[j] = pw;
+        w[j] = g[j] * v[j] * pw * __builtin_amdgcn_rcpf(sc);
+      }
+      lane_window_sums<G, R>(w, c8, u);
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float r2[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int c = 2 * j + h;
+          float dd = g[c] * s[c] - 2.f * alpha * beta * v[c] * u[c];
+          if (relu_mask && !(v[c] > 0.f)) dd = 0.f;
+          r2[h] = dd;
+        }
+        o[j] = pack2(r2[0], r2[1]);
+      }
+      if (ok) *(u32x4*)(dx + xoff) = o;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ K8 softmax cross-entropy
 // stats[0] += sum(-log p[label]) ; stats[1] += #(logit[label] == max) ; stats[2] = 1 if non-finite.
 __global__ void softmax_ce_k(const float* __restrict__ logits, int ldl, const int32_t* __restrict__ labels, int B,
@@ -829,6 +946,30 @@ hipError_t lrn_fwd(const bf16_t* x, int P, int C, int r, float bias, float alpha
   dim3 grid(nblocks((int64_t)P * (C / 8), TPB, 16384));   // one lane per 8-channel vector
   LRN_ALL(lrn_fwd_k, x, (int64_t)P, bias, alpha, beta, y)
   return hipErrorInvalidValue;  // (C, depth_radius) combination not instantiated
+}
+
+bool lrn_pool_supported(int H, int W, int C, int r) {
+  return H % 2 == 0 && W % 2 == 0 && (C == 32 || C == 64) && r == 4;
+}
+hipError_t lrn_pool_fwd(const bf16_t* x, int Nb, int H, int W, int C, int r, float bias, float alpha, float beta,
+                        bf16_t* y, uint8_t* arg, hipStream_t st) {
+  if (!lrn_pool_supported(H, W, C, r)) return hipErrorInvalidValue;
+  dim3 grid(nblocks((int64_t)Nb * (H / 2) * (W / 2) * (C / 8), TPB, 16384));
+  if (C == 64) hipLaunchKernelGGL((lrn_pool_fwd_k<64, 4>), grid, dim3(TPB), 0, st, x, Nb, H, W, bias, alpha, beta, y, arg);
+  else hipLaunchKernelGGL((lrn_pool_fwd_k<32, 4>), grid, dim3(TPB), 0, st, x, Nb, H, W, bias, alpha, beta, y, arg);
+  return hipGetLastError();
+}
+hipError_t lrn_pool_bwd(const bf16_t* x, const bf16_t* dP, const uint8_t* arg, int Nb, int H, int W, int C, int r,
+                        float bias, float alpha, float beta, int relu_mask, bf16_t* dx, hipStream_t st) {
+  if (!lrn_pool_supported(H, W, C, r)) return hipErrorInvalidValue;
+  dim3 grid(nblocks((int64_t)Nb * (H / 2) * (W / 2) * (C / 8), TPB, 16384));
+  if (C == 64)
+    hipLaunchKernelGGL((lrn_pool_bwd_k<64, 4>), grid, dim3(TPB), 0, st, x, dP, arg, Nb, H, W, bias, alpha, beta,
+                       relu_mask, dx);
+  else
+    hipLaunchKernelGGL((lrn_pool_bwd_k<32, 4>), grid, dim3(TPB), 0, st, x, dP, arg, Nb, H, W, bias, alpha, beta,
+                       relu_mask, dx);
+  return hipGetLastError();
 }
 
 hipError_t lrn_bwd(const bf16_t* x, const bf16_t* dy, int P, int C, int r, float bias, float alpha, float beta,

@@ -216,6 +216,36 @@ class LRNLayer(_Layer):
                               self.in_relu)
 
 
+class LRNPoolLayer(_Layer):
+    """LRN followed by a 2x2/2 SAME max-pool as ONE kernel each way (misc.hip
+    lrn_pool_fwd_k / lrn_pool_bwd_k): the reference CNN's norm2 -> pool2
+    (mnist_input.py:168-172).  The full-resolution LRN output and its gradient are
+    never materialised; results are bitwise those of LRNLayer + PoolLayer."""
+
+    @staticmethod
+    def supported(lrn: LRN, pool: MaxPool, x_shape) -> bool:
+        _, H, W, C = x_shape
+        return (pool.k == 2 and pool.s == 2 and pool.padding == "SAME"
+                and kernels().lrn_pool_supported(H, W, C, lrn.depth_radius))
+
+    def __init__(self, lrn: LRN, pool: MaxPool, x: torch.Tensor, in_relu: bool, B: int, dev):
+        self.spec, self.pool, self.name, self.x, self.in_relu = lrn, pool, pool.name, x, in_relu
+        _, self.H, self.W, self.C = x.shape
+        self.out = _bf16(B, self.H // 2, self.W // 2, self.C, device=dev)
+        self.arg = torch.zeros(B, self.H // 2, self.W // 2, self.C, dtype=torch.uint8, device=dev)
+
+    def fwd(self, nb: int) -> None:
+        s = self.spec
+        kernels().lrn_pool_fwd(self.x, self.out, self.arg, nb, self.H, self.W, self.C, s.depth_radius, s.bias,
+                               s.alpha, s.beta)
+
+    def bwd_data(self, nb: int, dy, dx) -> None:
+        if dx is not None:
+            s = self.spec
+            kernels().lrn_pool_bwd(self.x, dy, self.arg, dx, nb, self.H, self.W, self.C, s.depth_radius, s.bias,
+                                   s.alpha, s.beta, self.in_relu)
+
+
 class DenseLayer(_Layer):
     has_params = True
 
@@ -285,8 +315,10 @@ class HipNet:
 
     def __init__(self, spec: ModelSpec, batch: int, device, init: Dict[str, torch.Tensor],
                  opt: Optional[OptConfig] = None, fuse_convpool: bool = True, overlap_backward: bool = False,
-                 fuse_head: bool = True):
+                 fuse_head: bool = True, fuse_lrnpool: Optional[bool] = None):
         dev = torch.device(device)
+        if fuse_lrnpool is None:
+            fuse_lrnpool = os.environ.get("MNISTX_FUSE_LRNPOOL", "1") != "0"
         self.spec, self.B, self.device = spec, batch, dev
         self.opt = opt or OptConfig()
         pads = _weight_pads(spec)
@@ -318,6 +350,14 @@ class HipNet:
                     x, in_relu = lay.out, False
                     i += 2
                     continue
+            if (fuse_lrnpool and dev.type == "cuda" and isinstance(L, LRN) and isinstance(nxt, MaxPool)
+                    and LRNPoolLayer.supported(L, nxt, x.shape)):
+                lay = LRNPoolLayer(L, nxt, x, in_relu, batch, dev)
+                lay.idx = i
+                self.layers.append(lay)
+                x, in_relu = lay.out, False
+                i += 2
+                continue
             if isinstance(L, Conv):
                 lay = ConvLayer(L, x, in_relu, i == 0, self.fp, batch, dev)
                 in_relu = L.relu

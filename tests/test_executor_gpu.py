@@ -157,3 +157,27 @@ def test_weight_decay_total_loss(dev, K):
         assert abs(st["total_loss"] - (st["cross_entropy"] + wd_term)) < 1e-4 * max(1.0, wd_term), (st, wd_term)
         totals.append(net.stats[6].item())
     assert totals[0] == totals[1]
+
+
+def test_lrn_pool_fusion_bitwise(dev, K):
+    """reference CNN: the fused norm2+pool2 layer gives the same logits and gradients
+    as the separate LRN and pool layers."""
+    torch.manual_seed(3)
+    spec = get_model("reference_cnn", 1)
+    init = torch_ref.init_params(spec, seed=2)
+    B = 80
+    x = (torch.rand(B, 28, 28, 1, device=dev) - 0.5).to(torch.bfloat16)
+    y = torch.randint(0, 10, (B,), device=dev, dtype=torch.int32)
+    out = []
+    for fuse in (True, False):
+        net = HipNet(spec, B, dev, init, OptConfig(lr0=0.05), fuse_lrnpool=fuse)
+        assert any(type(l).__name__ == "LRNPoolLayer" for l in net.layers) == fuse
+        net.x0.copy_(x)
+        net.labels.copy_(y)
+        net.forward(defer_head=True)
+        net.loss_and_grad()
+        net.backward()
+        torch.cuda.synchronize()
+        out.append((net.logits.clone(), net.fp.grads.clone()))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])

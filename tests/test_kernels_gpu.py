@@ -450,3 +450,33 @@ def test_prep_images_perm_matches_two_step(dev, K):
     lo2 = torch.empty_like(lo)
     K.prep_images(src, idx, lab, out2, lo2, 784, 1, 1)
     assert torch.equal(out, out2) and torch.equal(lo, lo2)
+
+
+@pytest.mark.parametrize("N,H,W,C,relu", [(7, 14, 14, 64, True), (3, 14, 14, 32, False), (5, 6, 10, 64, True)])
+def test_lrn_pool_matches_two_step(dev, K, N, H, W, C, relu):
+    """Fused LRN -> 2x2/2 max-pool (forward + backward) == lrn_fwd + maxpool_fwd and
+    maxpool_bwd + lrn_bwd, bitwise (7x7x7 windows x 8 lanes leave a partial wave)."""
+    torch.manual_seed(22)
+    r, bias, alpha, beta = 4, 1.0, 0.05, 0.75
+    x = rnd(N, H, W, C, dev=dev, scale=3.0)
+    if relu:
+        x = x.relu().to(torch.bfloat16)
+    OH, OW = H // 2, W // 2
+    y = torch.empty(N, OH, OW, C, dtype=torch.bfloat16, device=dev)
+    arg = torch.empty(N, OH, OW, C, dtype=torch.uint8, device=dev)
+    assert K.lrn_pool_supported(H, W, C, r)
+    K.lrn_pool_fwd(x, y, arg, N, H, W, C, r, bias, alpha, beta)
+    l = torch.empty_like(x)
+    K.lrn_fwd(x, l, N * H * W, C, r, bias, alpha, beta)
+    y2 = torch.empty_like(y)
+    arg2 = torch.empty_like(arg)
+    K.maxpool_fwd(l, y2, arg2, N, H, W, C, OH, OW)
+    assert torch.equal(y, y2) and torch.equal(arg, arg2)
+    dP = rnd(N, OH, OW, C, dev=dev)
+    dx = torch.empty_like(x)
+    K.lrn_pool_bwd(x, dP, arg, dx, N, H, W, C, r, bias, alpha, beta, relu)
+    dl = torch.empty_like(x)
+    K.maxpool_bwd(dP, arg2, y2, False, dl, N, H, W, C, OH, OW)
+    dx2 = torch.empty_like(x)
+    K.lrn_bwd(x, dl, dx2, N * H * W, C, r, bias, alpha, beta, relu)
+    assert torch.equal(dx, dx2)

@@ -282,7 +282,7 @@ DEV bf16x8 frag_tr(const bf16_t* img, int c0, int kb, int lane) {
 
 // ---------------------------------------------------------------- kernel
 // One (tile t, K split) of C = A.B; the kernels below only choose (t, split).
-template <int BM, int BN, int WM, int WN, class LA, bool AKC, class LB, bool BKC>
+template <int BM, int BN, int WM, int WN, class LA, bool AKC, class LB, bool BKC, int PFO = 0>
 DEV void gemm_body(const LA& la, const LB& lb, const GemmEpi& ep, int M, int N, int K, int kchunk, int tiles_n,
                    int t, int split) {
   constexpr int NT = 64 * WM * WN;
@@ -320,7 +320,7 @@ DEV void gemm_body(const LA& la, const LB& lb, const GemmEpi& ep, int M, int N, 
   // output, so few workgroups per CU: with one step in flight a CU keeps only
   // ~4 x 8 KB of loads outstanding and the split-K GEMMs ran at a fraction of HBM
   // bandwidth, latency-bound.  PF slots let each block keep PF steps in flight.
-  constexpr int PF = (!AKC && !BKC) ? (DENSE ? WG_PF_DENSE : WG_PF_IM2COL) : 1;
+  constexpr int PF = PFO > 0 ? PFO : (!AKC && !BKC) ? (DENSE ? WG_PF_DENSE : WG_PF_IM2COL) : 1;
   u32x4 ra[PF][A_VPT], rb[PF][B_VPT];
 
   // K index past the split's end: every loader returns zeros for it (out of range)
@@ -534,7 +534,7 @@ DEV void gemm_body(const LA& la, const LB& lb, const GemmEpi& ep, int M, int N, 
   }
 }
 
-template <int BM, int BN, int WM, int WN, class LA, bool AKC, class LB, bool BKC>
+template <int BM, int BN, int WM, int WN, class LA, bool AKC, class LB, bool BKC, int PFO = 0>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEpi ep, int M, int N, int K,
                                                             int kchunk, int tiles_n) {
   const int tiles_mn = gridDim.x;
@@ -552,7 +552,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(LA la, LB lb, GemmEp
     t = xcd_remap(blockIdx.x, tiles_mn);
     split = 0;
   }
-  gemm_body<BM, BN, WM, WN, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, kchunk, tiles_n, t, split);
+  gemm_body<BM, BN, WM, WN, LA, AKC, LB, BKC, PFO>(la, lb, ep, M, N, K, kchunk, tiles_n, t, split);
 }
 
 // Grouped weight gradients: up to WG_GROUP_MAX independent split-K problems in ONE
@@ -591,7 +591,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_wg_group_kernel(const WgGro
 }
 
 // ---------------------------------------------------------------- dispatch
-template <int BM, int BN, int WM, int WN, class LA, bool AKC, class LB, bool BKC>
+template <int BM, int BN, int WM, int WN, class LA, bool AKC, class LB, bool BKC, int PFO = 0>
 hipError_t launch_cfg(const LA& la, const LB& lb, const GemmEpi& ep, int M, int N, int K, int splits,
                       hipStream_t st) {
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
@@ -602,7 +602,7 @@ hipError_t launch_cfg(const LA& la, const LB& lb, const GemmEpi& ep, int M, int 
   splits = (K + kchunk - 1) / kchunk;
   if (splits < 1) splits = 1;
   dim3 grid(tm * tn, splits);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, LA, AKC, LB, BKC>), grid, dim3(64 * WM * WN), 0, st, la, lb, ep,
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, LA, AKC, LB, BKC, PFO>), grid, dim3(64 * WM * WN), 0, st, la, lb, ep,
                      M, N, K, kchunk, tn);
   return hipGetLastError();
 }
@@ -613,7 +613,16 @@ hipError_t launch_cfg(const LA& la, const LB& lb, const GemmEpi& ep, int M, int 
 //    so the deterministic fp32 split-K slab (splits x M x N) stays small.
 //  * Everything else drops to 64-row tiles whenever the large tile would leave
 //    the 256 CUs with fewer than 4 workgroups each.
-enum TileCode { T256x16, T256x32, T128x64, T64x128, T128x128, T64x16, T64x32, T64x64 };
+enum TileCode { T256x16, T256x32, T128x64, T64x128, T128x128, T64x16, T64x32, T64x64, T256x128 };
+
+// experiment knobs (non-weight-gradient launches): MNISTX_GEMM_TILE forces a tile
+// code, MNISTX_GEMM_PF the K-step prefetch depth of the 128x128 / 64x128 / 256x128 tiles
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return (e && e[0]) ? atoi(e) : dflt;
+}
+static int gemm_tile_override() { static const int v = env_int("MNISTX_GEMM_TILE", -1); return v; }
+static int gemm_pf() { static const int v = env_int("MNISTX_GEMM_PF", 1); return v; }
 
 int tile_code(int M, int N, bool wgrad) {
   auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
@@ -636,7 +645,23 @@ template <class LA, bool AKC, class LB, bool BKC>
 hipError_t launch_any(const LA& la, const LB& lb, const GemmEpi& ep, int M, int N, int K, int splits,
                       hipStream_t st, int code = -1) {
   constexpr bool WG = !AKC && !BKC;
-  const int c = code >= 0 ? code : tile_code(M, N, WG);
+  int c = code >= 0 ? code : tile_code(M, N, WG);
+  if (!WG && code < 0 && gemm_tile_override() >= 0) c = gemm_tile_override();
+  if constexpr (!WG) {
+    // Large dense fwd / dgrad GEMMs (fully-connected layers at big batch): 256x128
+    // tiles with 2 K-steps in flight, measured on MI355X (profiles/r1s3/gemm_sweep.md:
+    // 16384x3136x1024 fwd 184 -> 151 us, dgrad 174 -> 153 us vs the 128x128 tile).
+    constexpr bool DENSE = IsMat<LA>::value && IsMat<LB>::value;
+    if (DENSE && code < 0 && gemm_tile_override() < 0 && N > 64 && M >= 4096 &&
+        ((M + 255) / 256) * ((N + 127) / 128) >= 512)
+      return launch_cfg<256, 128, 2, 2, LA, AKC, LB, BKC, 2>(la, lb, ep, M, N, K, splits, st);
+    const int pf = gemm_pf();
+    if (c == T128x128 && pf == 2) return launch_cfg<128, 128, 2, 2, LA, AKC, LB, BKC, 2>(la, lb, ep, M, N, K, splits, st);
+    if (c == T128x128 && pf == 3) return launch_cfg<128, 128, 2, 2, LA, AKC, LB, BKC, 3>(la, lb, ep, M, N, K, splits, st);
+    if (c == T64x128 && pf == 2) return launch_cfg<64, 128, 1, 4, LA, AKC, LB, BKC, 2>(la, lb, ep, M, N, K, splits, st);
+    if (c == T256x128 && pf == 2) return launch_cfg<256, 128, 2, 2, LA, AKC, LB, BKC, 2>(la, lb, ep, M, N, K, splits, st);
+    if (c == T256x128) return launch_cfg<256, 128, 2, 2, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+  }
   switch (c) {
     case T64x16: return launch_cfg<64, 16, 4, 1, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
     case T64x32: return launch_cfg<64, 32, 4, 1, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);

@@ -1142,6 +1142,13 @@ hipError_t run_dgrad(const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int 
 
 using LeNetC1 = Geo<1, 8, 5, 2, 28, 28>;
 constexpr int WG_IMGS_C1 = 1;   // conv1 wgrad: one image per group (LDS 28 KB -> 5 workgroups / CU)
+// A/B knob: MNISTX_C1_WG_IMGS=2 runs conv1 wgrad with two images per group (13 -> 26
+// MFMA steps per barrier round over 4 waves, ~52 KB LDS -> 3 workgroups / CU).  Read
+// once; the launch and the slab-sizing grid query both go through it.
+static int c1_wg_imgs() {
+  static const int v = [] { const char* e = getenv("MNISTX_C1_WG_IMGS"); return (e && e[0] == '2') ? 2 : WG_IMGS_C1; }();
+  return v;
+}
 using LeNetC2 = Geo<8, 16, 5, 0, 14, 14>;
 using RefC1g = Geo<1, 32, 5, 2, 28, 28>;
 using RefC1c = Geo<3, 32, 5, 2, 28, 28>;
@@ -1199,7 +1206,8 @@ hipError_t convpool_fwd(int cfg, const XSrc& x, const bf16_t* w, const float* bi
 hipError_t convpool_wgrad(int cfg, const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B, float* slab,
                           int grid, hipStream_t st) {
   switch (cfg) {
-    case 0: return run_wgrad<LeNetC1, WG_IMGS_C1>(x, dP, arg, B, slab, grid, st);
+    case 0: return c1_wg_imgs() == 2 ? run_wgrad<LeNetC1, 2>(x, dP, arg, B, slab, grid, st)
+                                     : run_wgrad<LeNetC1, WG_IMGS_C1>(x, dP, arg, B, slab, grid, st);
     case 1: return run_wgrad<LeNetC2, 4>(x, dP, arg, B, slab, grid, st);
     case 2: return run_wgrad<RefC1g, 2>(x, dP, arg, B, slab, grid, st);
     case 3: return run_wgrad<RefC1c, 2>(x, dP, arg, B, slab, grid, st);
@@ -1228,7 +1236,7 @@ int wgrad_grid_for() {
 // the slab has exactly one partial per resident block.
 int convpool_wgrad_grid(int cfg) {
   switch (cfg) {
-    case 0: return wgrad_grid_for<LeNetC1, WG_IMGS_C1>();
+    case 0: return c1_wg_imgs() == 2 ? wgrad_grid_for<LeNetC1, 2>() : wgrad_grid_for<LeNetC1, WG_IMGS_C1>();
     case 1: return wgrad_grid_for<LeNetC2, 4>();
     case 2: return wgrad_grid_for<RefC1g, 2>();
     case 3: return wgrad_grid_for<RefC1c, 2>();

@@ -1105,10 +1105,17 @@ template <class G, int IMGS>
 hipError_t run_fwd(const XSrc& x, const bf16_t* w, const float* bias, int bias_n, int B, bf16_t* pooled, uint8_t* arg,
                    hipStream_t st) {
   if constexpr (G::PAIR && G::H == 28 && G::W == 28 && G::PAD == 2) {
-    constexpr int QI = 4;
-    // two resident rounds (2048) measured 5 % faster than one for this kernel (same-box A/B)
-    hipLaunchKernelGGL((convpool_fwd_quad_k<QI>), dim3(grid_for(B, QI, 2048)), dim3(NTH), 0, st, x, w, bias, bias_n,
-                       B, pooled, arg);
+    // two resident rounds (2048) measured 5 % faster than one for this kernel (same-box A/B).
+    // A/B knob MNISTX_QUAD_IMGS=3: 3 images per group (LDS 29.1 -> 21.8 KB, 5 -> 7 WGs/CU)
+    // ("5": the same with two resident rounds of the 3-image kernel instead of 2048 blocks)
+    static const int qi = [] { const char* e = getenv("MNISTX_QUAD_IMGS"); return e ? e[0] - '0' : 4; }();
+    if (qi == 3 || qi == 5)
+      hipLaunchKernelGGL((convpool_fwd_quad_k<3>),
+                         dim3(grid_for(B, 3, qi == 3 ? 2048 : 2 * resident_grid<convpool_fwd_quad_k<3>>())), dim3(NTH),
+                         0, st, x, w, bias, bias_n, B, pooled, arg);
+    else
+      hipLaunchKernelGGL((convpool_fwd_quad_k<4>), dim3(grid_for(B, 4, 2048)), dim3(NTH), 0, st, x, w, bias, bias_n,
+                         B, pooled, arg);
   } else if constexpr (G::PAIR) {
     hipLaunchKernelGGL((convpool_fwd_pair_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, x, w, bias,
                        bias_n, B, pooled, arg);

@@ -52,13 +52,99 @@ def parse():
     ap.add_argument("--dist_backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo = host-staged rehearsal of the DP "
                          "path with several ranks sharing one GPU (ranks map to device LOCAL_RANK %% count)")
+    ap.add_argument("--mode", default="dp", choices=["dp", "ps"],
+                    help="dp = synchronous data parallel (headline); ps = asynchronous parameter server: "
+                         "rank 0 is the PS, ranks 1..N-1 are workers (BASELINE config '1 PS + 7 workers')")
+    ap.add_argument("--ps_transport", default="ipc", choices=["ipc", "host"],
+                    help="PS data plane: ipc = xGMI peer copies into PS-owned buffers; host = gloo, host-staged")
+    ap.add_argument("--eager_steps", type=int, default=-1,
+                    help="N=1 with a hipGraph: also time this many EAGER steps after the timed region "
+                         "(ms_per_step_eager, comparable with N>1 runs); -1 = --steps")
     ap.add_argument("--phases", type=int, default=3,
                     help="extra eager steps AFTER the timed region, timed per phase with HIP events (0 = off)")
     return ap.parse_args()
 
 
+def run_ps(args) -> int:
+    """1 PS + (N-1) asynchronous workers.  The PS clock is the
+    authoritative one: it marks the wall time when the shared global step passes
+    warmup*(N-1) and (warmup+steps)*(N-1) applied updates (device synchronised at
+    both marks), so value = steps*(N-1)*batch / that interval -- the aggregate
+    images/sec of updates applied to the model."""
+    import torch
+    import torch.distributed as dist
+
+    from distributed_tensorflow_ibm_mnist_amd.models import get_model
+    from distributed_tensorflow_ibm_mnist_amd.models.torch_ref import init_params
+    from distributed_tensorflow_ibm_mnist_amd.runtime.params import OptConfig
+    from distributed_tensorflow_ibm_mnist_amd.parallel.ps import ParameterServer, PSClient, weight_l2_into
+    from distributed_tensorflow_ibm_mnist_amd.train.trainer import param_specs
+    from distributed_tensorflow_ibm_mnist_amd.data.synthetic import make_synthetic
+    from distributed_tensorflow_ibm_mnist_amd.data.device_loader import DeviceDataset, DeviceLoader
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world < 2:
+        print("[bench] --mode ps needs >= 2 ranks (torchrun --nproc-per-node N)", file=sys.stderr)
+        return 2
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo")          # control plane; data moves on the PS transport
+    spec = get_model(args.model, args.in_channels)
+    init = init_params(spec, seed=args.seed)
+    opt = OptConfig(lr0=args.lr, decay_rate=0.1, decay_steps=0, momentum=0.9 if args.optimizer != "sgd" else 0.0,
+                    nesterov=args.optimizer == "nesterov", use_momentum=args.optimizer != "sgd", ema_max=0.9999)
+    nw = world - 1
+    m0, m1 = args.warmup * nw, (args.warmup + args.steps) * nw
+    if rank == 0:
+        ps = ParameterServer(0, 1, nw, param_specs(spec), init, opt, dev, m1, log=lambda *a: None,
+                             transport=args.ps_transport)
+        ps.marks = {m0: 0.0, m1: 0.0} if m0 > 0 else {m1: 0.0}
+        t_start = time.perf_counter()
+        res = ps.serve()
+        t0 = ps.marks.get(m0, t_start) if m0 > 0 else t_start
+        el = ps.marks[m1] - t0
+        value = args.steps * nw * args.batch / el
+        out = {
+            "metric": f"images/sec (whole node) MNIST {MODEL_LABEL[args.model]} parameter-server mode",
+            "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_update": round(el / (args.steps * nw) * 1e3, 4),
+            "ms_per_worker_step": round(el / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic 28x28x1 (on-device generated MNIST-like glyphs), random-init weights",
+            "config": {"model": MODEL_LABEL[args.model], "per_worker_batch": args.batch,
+                       "parallelism": f"ps1+w{nw}", "ps_transport": args.ps_transport,
+                       "gpus_visible": torch.cuda.device_count(), "optimizer": args.optimizer},
+            "applied_per_worker": res["per_worker"], "global_step": res["global_step"],
+            "param_checksum": float(ps.fp.params.double().sum().item()),
+        }
+        print(json.dumps(out), flush=True)
+    else:
+        from distributed_tensorflow_ibm_mnist_amd.runtime.executor import HipNet
+        net = HipNet(spec, args.batch, dev, init, opt)
+        imgs, labs = make_synthetic(args.dataset_size, seed=args.seed, channels=1, device=dev)
+        loader = DeviceLoader(DeviceDataset(imgs, labs, dev, hw=784, channels=1), net.x0, net.labels,
+                              rank=0, world=1, seed=args.seed + 7919 * rank, shard=False)
+        client = PSClient(net, 1, nw, rank - 1, transport=args.ps_transport)
+        client.hello()
+        while not client.stop:
+            loader.next()
+            net.forward(defer_head=True)
+            net.loss_and_grad()
+            net.backward()
+            weight_l2_into(net.fp)
+            net.finalize(net.B, increment=False)
+            client.push_pull()
+        client.done()
+    dist.destroy_process_group()
+    return 0
+
+
 def main() -> int:
     args = parse()
+    if args.mode == "ps":
+        return run_ps(args)
     import torch
     import torch.distributed as dist
 
@@ -139,6 +225,16 @@ def main() -> int:
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     el = float(elapsed.item())
+    eager_ms = None
+    n_eager = args.steps if args.eager_steps < 0 else args.eager_steps
+    if graph is not None and n_eager > 0:   # outside the timed region: the same step, eager
+        torch.cuda.synchronize()
+        te = time.perf_counter()
+        for _ in range(n_eager):
+            loader.next()
+            step_body()
+        torch.cuda.synchronize()
+        eager_ms = (time.perf_counter() - te) / n_eager * 1e3
     stats = net.read_stats()
     in_sync = None
     if world > 1:                           # outside the timed region: replicas must hold identical weights
@@ -187,6 +283,7 @@ def main() -> int:
             },
             "tflops_per_s": round(tot * value / 1e12, 2),
             "final_train_loss": round(stats["cross_entropy"], 5),
+            "ms_per_step_eager": round(eager_ms, 4) if eager_ms is not None else (None if use_graph else round(ms, 4)),
             "phase_ms_eager": phases,
             "replicas_in_sync": in_sync,
             "grad_bucket_mb": [round(b.nbytes / 2 ** 20, 3) for b in dp.buckets] if world > 1 else None,

@@ -11,9 +11,12 @@ class reproduces each summary type as TensorBoard event data under the same
 names.  Unlike the reference (Q5), "test" scalars come from a real pass over
 the held-out split, not from the next training batch.
 
-Activations are taken from the executor's live buffers (bf16, channel padding
-stripped; a fused conv+pool layer exposes its pooled output) for the first
-``sample`` images of the last batch, so monitoring never adds a forward pass.
+Activations are the reference's ``<layer>/<layer>:0`` tensors (``main.py:97-100``):
+a conv layer's bias+ReLU output BEFORE pooling (conv1: ``[n,28,28,32]``), for the
+first ``sample`` images of the last batch.  Where conv and pool run as one fused
+kernel that tensor never exists, so the executor recomputes it for the sample with
+the unfused conv kernel (``HipNet.layer_activation``); dense layers expose their
+live output buffers.  Channel padding is stripped.
 """
 from __future__ import annotations
 
@@ -119,7 +122,7 @@ class Monitor:
     def _activation(self, layer: str) -> np.ndarray:
         net = self.replica.net
         try:
-            a = net.activation(layer)
+            a = net.layer_activation(layer, self.sample)
         except KeyError:
             return np.zeros(1)
         a = a[: self.sample].detach().float().cpu().numpy()

@@ -40,6 +40,7 @@ class Cluster:
     master: str = ""
     device: Optional[torch.device] = None
     backend: str = ""
+    transport: str = ""             # PS-mode data plane (ipc | host)
 
     @property
     def is_chief(self) -> bool:
@@ -117,10 +118,16 @@ def setup_distribute(job_name: str = "", ps_hosts: str = "", worker_hosts: str =
         cl.backend = "nccl" if cl.device.type == "cuda" else "gloo"
         if cl.mode == "dp" and dp_backend:
             cl.backend = dp_backend
-        if cl.mode == "ps" and ps_backend:
-            # gloo stages GPU tensors through host memory: lets several PS-mode
-            # processes share one GPU (RCCL needs one rank per GPU)
-            cl.backend = ps_backend
+        if cl.mode == "ps":
+            # PS mode: the process group is the gloo control plane; gradients and
+            # parameters move on the PS data plane (parallel/ps.py): xGMI peer copies
+            # ("ipc", default on GPU) or gloo messages staged through host ("host").
+            cl.backend = "gloo"
+            t = {"": "", "gloo": "host", "host": "host", "ipc": "ipc"}.get(ps_backend)
+            if t is None:
+                raise ValueError(f"--ps_backend={ps_backend!r}: expected ipc | host (gloo)")
+            from .ps import default_transport
+            cl.transport = t or default_transport(cl.device)
         if cl.device.type == "cuda":
             torch.cuda.set_device(cl.device)
         kw = {"device_id": cl.device} if cl.backend == "nccl" else {}

@@ -3,28 +3,50 @@
 Reference semantics (between-graph replication, TF1 ``replica_device_setter``):
 variables live on the PS tasks; every worker pulls them, computes gradients on
 its own batch and pushes them; the PS applies each push as it arrives (no
-aggregation, no staleness bound, Hogwild-style); every push increments the
-shared ``global_step`` and ``StopAtStepHook`` compares that shared step.
+aggregation, no staleness bound, Hogwild-style; ``mnist_input.py:261-264``);
+every push increments the shared ``global_step`` and ``StopAtStepHook``
+compares that shared step.
 
-MI355X realisation:
-* one process per GPU; PS and workers talk with point-to-point send/recv over
-  RCCL (``nccl`` backend: every (PS, worker) pair gets its own communicator and
-  stream, so pushes from different workers progress independently over their
-  direct xGMI links) or gloo on CPU;
-* the PS keeps the fp32 masters, momentum slots and EMA shadows of ITS shard
-  and applies each push with the fused K9 kernel on its GPU;
-* k > 1 PS tasks own contiguous, byte-balanced ranges of the flat parameter
-  buffer at tensor granularity (TF placed variables round-robin; here the
-  12.85 MB ``local3/weights`` simply gets a PS of its own when k >= 2);
-* the PS polls posted receives (``Work.is_completed``) and serves whichever
-  worker is ready first — true asynchronous apply in arrival order;
-* shutdown (Q9): when the global step reaches ``max_steps`` PS 0 answers with a
-  stop flag; workers send DONE to every PS; a PS exits once all workers are done.
+MI355X realisation -- ONE serve loop, two planes:
 
-Wire protocol per exchange, worker -> PS j: ctrl f64[8] = (kind, want_state,
-worker_step, global_step_seen, ...) then (GRAD) the fp32 gradient slice;
-PS j -> worker: ctrl f64[8] = (global_step, stop, ...) then the fp32 parameter
-slice, then (STATE) EMA and momentum slices.
+* **control plane** (SURVEY C3): tiny int64 messages on a gloo group over the
+  rendezvous TCPStore.  The PS blocks in a host ``recv`` from ANY worker and so
+  serves workers strictly in arrival order.  Nothing on any GPU waits for an
+  idle worker: no posted-but-unmatched receive kernels, no polling of device
+  work, no host sync on a device ctrl tensor.
+* **data plane** (``Transport``), chosen per run:
+  - ``ipc`` (default on GPU): one-sided copies over xGMI peer memory.  Each PS
+    exports (hipIpc/dmabuf, via ``torch.multiprocessing.reductions``) a
+    gradient mailbox and a parameter reply slot per worker plus a state slot.
+    A worker copies its gradient slice straight into its mailbox on the PS GPU
+    (a DMA over its direct xGMI link), synchronises its own stream and only
+    THEN announces the push on the control plane; the PS applies the fused K9
+    optimizer reading the mailbox in place, snapshots the parameters into the
+    worker's reply slot, synchronises and answers; the worker pulls the
+    snapshot with one peer copy.  Every copy is bounded DMA work, and several
+    processes can share one GPU (the 1-GPU rehearsal runs the same code).
+  - ``host``: gloo send/recv of the slices on the control group (tagged apart
+    from control words), staged through host memory for GPU tensors.  The CPU
+    test path, and a fallback.
+  (RCCL point-to-point is deliberately not used: its matched send/recv pairs
+  are GPU kernels that spin until the peer arrives, and RCCL refuses two
+  ranks on one GPU, so it could never be exercised on a 1-GPU box.)
+* the PS keeps the fp32 masters, momentum slots and EMA shadows of ITS shard;
+  k > 1 PS tasks own contiguous, byte-balanced tensor ranges of the flat
+  parameter buffer (TF placed variables round-robin; here the 12.85 MB
+  ``local3/weights`` simply gets a PS of its own when k >= 2);
+* every worker pushes to every PS, so each PS sees the same pushes (in its
+  own arrival order); each PS applies the first ``max_steps - start`` it
+  receives and counts its own global step, so all shards end on the same
+  update count (the reference's async PS made no stronger promise);
+* shutdown (Q9): once its global step reaches ``max_steps`` PS 0 answers with
+  a stop flag; workers send DONE to every PS; a PS exits when all are done.
+* the worker computes the weight-decay loss terms (``mnist_input.py:112-114``)
+  from the parameters its forward used, so logged ``total_loss`` and the
+  ``*/weight_loss/avg`` EMAs include them in PS mode too.
+
+Control words (int64[8]) worker -> PS: (kind, want_state, worker_local_step);
+PS -> worker: (global_step, stop, applied).
 """
 from __future__ import annotations
 
@@ -32,7 +54,7 @@ import os
 import signal
 import sys
 import time
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -40,28 +62,9 @@ import torch.distributed as dist
 
 from ..runtime.params import FlatParams, OptConfig
 
-HELLO, GRAD, STATE, DONE = 0.0, 1.0, 2.0, 3.0
+HELLO, GRAD, STATE, DONE = 0, 1, 2, 3
 CTRL = 8
-
-
-def _staged() -> bool:
-    return dist.get_backend() == "gloo"
-
-
-def send(t: torch.Tensor, dst: int) -> None:
-    """p2p send; gloo moves GPU tensors through host memory."""
-    if t.is_cuda and _staged():
-        t = t.cpu()
-    dist.send(t.contiguous(), dst)
-
-
-def recv(t: torch.Tensor, src: Optional[int] = None) -> int:
-    if t.is_cuda and _staged():
-        h = torch.empty(t.shape, dtype=t.dtype)
-        r = dist.recv(h, src)
-        t.copy_(h)
-        return r
-    return dist.recv(t, src)
+TAG_CTRL, TAG_DATA = 1, 2
 
 
 def shard_ranges(fp: FlatParams, num_ps: int) -> List[Tuple[int, int, List[str]]]:
@@ -83,17 +86,154 @@ def shard_ranges(fp: FlatParams, num_ps: int) -> List[Tuple[int, int, List[str]]
     return out
 
 
+def default_transport(device: torch.device) -> str:
+    return "ipc" if torch.device(device).type == "cuda" else "host"
+
+
+def _sync(t: torch.Tensor) -> None:
+    if t.is_cuda:
+        torch.cuda.current_stream(t.device).synchronize()
+
+
+# ---------------------------------------------------------------------------- transports
+class HostTransport:
+    """Slices travel as gloo messages on the control group (tag TAG_DATA)."""
+    name = "host"
+
+    def __init__(self, group, num_ps: int, num_workers: int):
+        self.g, self.k, self.W = group, num_ps, num_workers
+
+    def _send(self, t: torch.Tensor, dst: int) -> None:
+        dist.send(t.detach().cpu().contiguous() if t.is_cuda else t.contiguous(), dst, group=self.g, tag=TAG_DATA)
+
+    def _recv(self, t: torch.Tensor, src: int) -> None:
+        if t.is_cuda:
+            h = torch.empty(t.shape, dtype=t.dtype)
+            dist.recv(h, src, group=self.g, tag=TAG_DATA)
+            t.copy_(h)
+        else:
+            dist.recv(t, src, group=self.g, tag=TAG_DATA)
+
+    # -- PS side
+    def ps_setup(self, ps, is_me: bool) -> None:
+        if is_me:
+            self.grad_in = torch.zeros_like(ps.fp.grads)
+
+    def ps_take_grads(self, ps, r: int) -> torch.Tensor:
+        self._recv(self.grad_in, r)
+        return self.grad_in
+
+    def ps_stage_reply(self, ps, r: int, want_state: bool) -> None:
+        pass
+
+    def ps_after_ctrl(self, ps, r: int, want_state: bool) -> None:
+        self._send(ps.fp.params, r)
+        if want_state:
+            self._send(ps.fp.ema, r)
+            self._send(ps.fp.mom, r)
+
+    # -- worker side
+    def worker_open(self, w_index: int, ranges) -> None:
+        self.wi = w_index
+
+    def worker_before_ctrl(self, j: int, kind: int, grads: Optional[torch.Tensor]) -> None:
+        pass
+
+    def worker_after_ctrl(self, j: int, kind: int, grads: Optional[torch.Tensor]) -> None:
+        if kind == GRAD:
+            self._send(grads, j)
+
+    def worker_pull(self, j: int, params: torch.Tensor, ema: torch.Tensor, mom: torch.Tensor, state: bool) -> None:
+        self._recv(params, j)
+        if state:
+            self._recv(ema, j)
+            self._recv(mom, j)
+
+
+class IpcTransport:
+    """One-sided xGMI peer copies into / out of PS-owned device buffers."""
+    name = "ipc"
+
+    def __init__(self, group, num_ps: int, num_workers: int):
+        self.g, self.k, self.W = group, num_ps, num_workers
+        self.peer: Dict[int, Dict[str, torch.Tensor]] = {}
+
+    def ps_setup(self, ps, is_me: bool) -> None:
+        """Collective over the control group: PS j exports, everyone else imports."""
+        from torch.multiprocessing.reductions import reduce_tensor
+        for j in range(self.k):
+            obj = [None]
+            if is_me and ps.j == j:
+                n, dev = ps.fp.total, ps.fp.params.device
+                self.grad_in = torch.zeros(self.W, n, dtype=torch.float32, device=dev)
+                self.reply = torch.zeros(self.W, n, dtype=torch.float32, device=dev)
+                self.state = torch.zeros(2, n, dtype=torch.float32, device=dev)
+                torch.cuda.synchronize(dev)
+                obj = [{k: reduce_tensor(t) for k, t in
+                        (("grad_in", self.grad_in), ("reply", self.reply), ("state", self.state))}]
+            dist.broadcast_object_list(obj, src=j, group=self.g)
+            if ps is None:                          # a worker maps every PS's buffers
+                self.peer[j] = {k: fn(*args) for k, (fn, args) in obj[0].items()}
+
+    def ps_take_grads(self, ps, r: int) -> torch.Tensor:
+        return self.grad_in[r - self.k]          # the worker wrote it before announcing
+
+    def ps_stage_reply(self, ps, r: int, want_state: bool) -> None:
+        i = r - self.k
+        self.reply[i].copy_(ps.fp.params)
+        if want_state:
+            self.state[0].copy_(ps.fp.ema)
+            self.state[1].copy_(ps.fp.mom)
+        _sync(self.reply)                         # visible to the worker before the ctrl reply
+
+    def ps_after_ctrl(self, ps, r: int, want_state: bool) -> None:
+        pass
+
+    def worker_open(self, w_index: int, ranges) -> None:
+        self.wi = w_index
+
+    def worker_before_ctrl(self, j: int, kind: int, grads: Optional[torch.Tensor]) -> None:
+        if kind == GRAD:
+            self.peer[j]["grad_in"][self.wi].copy_(grads)
+            _sync(grads)                          # landed in the PS's HBM before we announce it
+
+    def worker_after_ctrl(self, j: int, kind: int, grads: Optional[torch.Tensor]) -> None:
+        pass
+
+    def worker_pull(self, j: int, params: torch.Tensor, ema: torch.Tensor, mom: torch.Tensor, state: bool) -> None:
+        params.copy_(self.peer[j]["reply"][self.wi])
+        if state:
+            ema.copy_(self.peer[j]["state"][0])
+            mom.copy_(self.peer[j]["state"][1])
+
+
+def make_transport(name: str, group, num_ps: int, num_workers: int):
+    if name == "ipc":
+        return IpcTransport(group, num_ps, num_workers)
+    if name in ("host", "gloo"):
+        return HostTransport(group, num_ps, num_workers)
+    raise ValueError(f"unknown PS transport {name!r} (ipc | host)")
+
+
+def setup_transport(name: str, group, num_ps: int, num_workers: int, ps=None):
+    """Collective: every PS and worker rank calls this once, in the same order."""
+    tx = make_transport(name, group, num_ps, num_workers)
+    tx.ps_setup(ps, ps is not None)
+    return tx
+
+
+# ---------------------------------------------------------------------------- PS
 class ParameterServer:
     def __init__(self, ps_index: int, num_ps: int, num_workers: int, specs, init: Dict[str, torch.Tensor],
                  opt: OptConfig, device, max_steps: int, restore: Optional[Dict[str, np.ndarray]] = None,
-                 log=print):
+                 log=print, transport: str = "", group=None):
         self.j, self.k, self.W = ps_index, num_ps, num_workers
         self.device = torch.device(device)
+        self.group = group
         full = FlatParams.build(specs, {}, "cpu")
         self.start, self.end, self.names = shard_ranges(full, num_ps)[ps_index]
         mine = [s for s in specs if s[0] in self.names]
-        self.fp = FlatParams.build(mine, {n: init[n] for n in self.names}, self.device,
-                                   pads={})  # bf16 copy unused by the PS; kernel refreshes it harmlessly
+        self.fp = FlatParams.build(mine, {n: init[n] for n in self.names}, self.device, pads={})
         self.opt = opt
         self.max_steps = max_steps
         self.log = log
@@ -102,7 +242,6 @@ class ParameterServer:
         self._kill = tuple(int(v) for v in kr.split(":")) if ":" in kr else (-1, -1)
         self.global_step = 0
         if restore is not None:
-            from ..train.replica import load_state  # noqa: F401  (names match)
             vals = {n: torch.from_numpy(np.asarray(restore[n])) for n in self.names if n in restore}
             emas = {n: torch.from_numpy(np.asarray(restore[f"{n}/ExponentialMovingAverage"])) for n in self.names
                     if f"{n}/ExponentialMovingAverage" in restore}
@@ -110,141 +249,120 @@ class ParameterServer:
                     if f"{n}/Momentum" in restore}
             self.fp.load_state(vals, ema_too=not emas, ema_values=emas, mom_values=moms)
             self.global_step = int(np.asarray(restore.get("global_step", 0)))
-            self.fp.step.fill_(self.global_step)
+        self.fp.step.fill_(self.global_step)
         self.applied = 0
+        self.rejected = 0
         self.per_worker = [0] * num_workers
+        self.arrivals: List[int] = []            # worker index of every applied push, in order
+        self.tx = setup_transport(transport or default_transport(self.device), group, num_ps, num_workers, ps=self)
+        # global-step values at which serve() records a wall-clock mark (bench.py --mode ps)
+        self.marks: Dict[int, float] = {}
 
-    def _ctrl(self) -> torch.Tensor:
-        return torch.zeros(CTRL, dtype=torch.float64, device=self.device)
-
-    def _apply(self) -> None:
+    def _apply(self, grads: torch.Tensor) -> None:
+        fp = self.fp
         if self.device.type == "cuda":
-            self.fp.apply(self.opt, 1.0, track_l2=False)
+            from ..ops._ext import kernels
+            o = self.opt
+            kernels().fused_optimizer(fp.params, grads, fp.mom, fp.ema, fp.bf16, fp.segs, fp.step, o.lr0,
+                                      o.decay_rate, o.decay_steps, o.momentum, o.nesterov, o.use_momentum, 1.0,
+                                      o.ema_max, None)
         else:
             from ..runtime.torchnet import torch_update
-            torch_update(self.fp, self.opt, 1.0)
-            self.fp.l2.zero_()
+            if grads is not fp.grads:
+                fp.grads.copy_(grads)
+            torch_update(fp, self.opt, 1.0)
+            fp.l2.zero_()
 
-    def _reply(self, w_rank: int, want_state: bool) -> None:
-        c = self._ctrl()
-        c[0] = float(self.global_step)
-        c[1] = 1.0 if (self.j == 0 and self.global_step >= self.max_steps) else 0.0
-        c[2] = float(self.applied)
-        send(c, w_rank)
-        send(self.fp.params, w_rank)
-        if want_state:
-            send(self.fp.ema, w_rank)
-            send(self.fp.mom, w_rank)
-
-    def _handle(self, r: int, ctrl: List[float], done: set) -> bool:
-        """Process one message from worker rank r; returns False for DONE."""
-        kind = ctrl[0]
-        if kind == DONE:
-            done.add(r)
-            return False
-        if kind == GRAD:
-            recv(self.fp.grads, r)
-            if self.j == 0 and self.global_step >= self.max_steps:
-                # in-flight push after the stop point: answer with the stop flag, do not apply
-                self._reply(r, want_state=ctrl[1] > 0)
-                return True
-            if self.j != 0:
-                # LR / EMA schedule follows the global step owned by PS 0
-                self.global_step = int(ctrl[3])
-                self.fp.step.fill_(self.global_step)
-            self._apply()
-            self.applied += 1
-            self.per_worker[r - self.k] += 1
-            if self.j == 0:
-                self.global_step += 1
-                self.fp.step.fill_(self.global_step)
-            if self._kill[0] == dist.get_rank() and self.global_step >= self._kill[1]:
-                self.log(f"[ps {self.j}] fault injection: SIGKILL at global step {self.global_step}")
-                sys.stdout.flush()
-                os.kill(os.getpid(), signal.SIGKILL)
-        self._reply(r, want_state=ctrl[1] > 0)
-        return True
+    def _reply(self, r: int, want_state: bool) -> None:
+        self.tx.ps_stage_reply(self, r, want_state)
+        c = torch.zeros(CTRL, dtype=torch.int64)
+        c[0] = self.global_step
+        c[1] = int(self.global_step >= self.max_steps)
+        c[2] = self.applied
+        dist.send(c, r, group=self.group, tag=TAG_CTRL)
+        self.tx.ps_after_ctrl(self, r, want_state)
 
     def serve(self) -> Dict[str, int]:
         """Run until every worker has sent DONE, serving workers in arrival order."""
-        ranks = [self.k + i for i in range(self.W)]
         done: set = set()
         self.log(f"[ps {self.j}] serving {len(self.names)} tensor(s), {self.end - self.start} params, "
-                 f"{self.W} worker(s)")
-        if dist.get_backend() == "gloo":
-            # gloo: blocking receive from ANY source = the next worker to push
-            while len(done) < self.W:
-                c = torch.zeros(CTRL, dtype=torch.float64)
-                r = dist.recv(c)
-                self._handle(r, c.tolist(), done)
-        else:
-            # RCCL: one posted receive per (PS, worker) communicator, polled for completion
-            bufs = {r: self._ctrl() for r in ranks}
-            works = {r: dist.irecv(bufs[r], r) for r in ranks}
-            idle = 0
-            while len(done) < self.W:
-                progressed = False
-                for r in ranks:
-                    if r in done or not works[r].is_completed():
-                        continue
-                    works[r].wait()
-                    if self._handle(r, bufs[r].tolist(), done):
-                        bufs[r] = self._ctrl()
-                        works[r] = dist.irecv(bufs[r], r)
-                    progressed = True
-                if not progressed:
-                    idle += 1
-                    time.sleep(0.00005 if idle < 1000 else 0.0005)
+                 f"{self.W} worker(s), transport {self.tx.name}")
+        t0 = time.perf_counter()
+        while len(done) < self.W:
+            c = torch.zeros(CTRL, dtype=torch.int64)
+            r = dist.recv(c, group=self.group, tag=TAG_CTRL)     # any source: the next worker to arrive
+            kind, want_state = int(c[0]), bool(c[1])
+            if kind == DONE:
+                done.add(r)
+                continue
+            if kind == GRAD:
+                g = self.tx.ps_take_grads(self, r)
+                if self.global_step < self.max_steps:
+                    self._apply(g)
+                    self.global_step += 1
+                    self.fp.step.fill_(self.global_step)
+                    self.applied += 1
+                    self.per_worker[r - self.k] += 1
+                    self.arrivals.append(r - self.k)
                 else:
-                    idle = 0
+                    self.rejected += 1            # in flight past the stop point: answered, not applied
+                if self._kill[0] == dist.get_rank() and self.global_step >= self._kill[1]:
+                    self.log(f"[ps {self.j}] fault injection: SIGKILL at global step {self.global_step}")
+                    sys.stdout.flush()
+                    os.kill(os.getpid(), signal.SIGKILL)
+            self._reply(r, want_state)
+            if self.global_step in self.marks and not self.marks[self.global_step]:
+                if self.device.type == "cuda":
+                    torch.cuda.synchronize(self.device)
+                self.marks[self.global_step] = time.perf_counter()
+        dt = time.perf_counter() - t0
         self.log(f"[ps {self.j}] done: applied {self.applied} update(s), per worker {self.per_worker}, "
-                 f"global_step {self.global_step}")
-        return {"applied": self.applied, "global_step": self.global_step}
+                 f"rejected {self.rejected}, global_step {self.global_step}, {self.applied / max(dt, 1e-9):.1f} "
+                 f"updates/s")
+        return {"applied": self.applied, "global_step": self.global_step, "per_worker": list(self.per_worker),
+                "seconds": dt}
 
 
+# ---------------------------------------------------------------------------- worker
 class PSClient:
     """Worker side: push gradients / pull parameters of every PS shard."""
 
-    def __init__(self, net, num_ps: int):
+    def __init__(self, net, num_ps: int, num_workers: int, worker_index: int, group=None, transport: str = ""):
         self.net = net
-        self.k = num_ps
+        self.k, self.W, self.wi = num_ps, num_workers, worker_index
+        self.group = group
         self.ranges = shard_ranges(net.fp, num_ps)
         self.global_step = 0
         self.stop = False
-        dev = net.fp.params.device
-        self._c = torch.zeros(CTRL, dtype=torch.float64, device=dev)
+        self.tx = setup_transport(transport or default_transport(net.fp.params.device), group, num_ps, num_workers)
+        self.tx.worker_open(worker_index, self.ranges)
+        self.local_step = 0
 
-    def _exchange(self, kind: float, want_state: bool = False) -> Optional[Dict[str, np.ndarray]]:
+    def _exchange(self, kind: int, want_state: bool = False) -> None:
         fp = self.net.fp
-        state: Dict[str, np.ndarray] = {}
-        # push to every PS first (they work in parallel), then collect replies
+        # announce to every PS first (they work in parallel), then collect the replies
         for j, (a, b, _) in enumerate(self.ranges):
-            c = self._c.clone()
-            c[0] = kind
-            c[1] = 1.0 if want_state else 0.0
-            c[3] = float(self.global_step)
-            send(c, j)
-            if kind == GRAD:
-                send(fp.grads[a:b], j)
-        for j, (a, b, names) in enumerate(self.ranges):
-            r = torch.empty_like(self._c)
-            recv(r, j)
-            recv(fp.params[a:b], j)
-            if want_state:
-                recv(fp.ema[a:b], j)
-                recv(fp.mom[a:b], j)
+            g = fp.grads[a:b] if kind == GRAD else None
+            self.tx.worker_before_ctrl(j, kind, g)
+            c = torch.zeros(CTRL, dtype=torch.int64)
+            c[0], c[1], c[2] = kind, int(want_state), self.local_step
+            dist.send(c, j, group=self.group, tag=TAG_CTRL)
+            self.tx.worker_after_ctrl(j, kind, g)
+        for j, (a, b, _) in enumerate(self.ranges):
+            r = torch.zeros(CTRL, dtype=torch.int64)
+            dist.recv(r, j, group=self.group, tag=TAG_CTRL)
+            self.tx.worker_pull(j, fp.params[a:b], fp.ema[a:b], fp.mom[a:b], want_state)
             if j == 0:
-                vals = r.tolist()
-                self.global_step = int(vals[0])
-                self.stop = vals[1] > 0
+                self.global_step = int(r[0])
+                self.stop = bool(r[1])
         fp.step.fill_(self.global_step)
         fp.refresh_bf16()
-        return state if want_state else None
 
     def hello(self) -> None:
         self._exchange(HELLO)
 
     def push_pull(self) -> None:
+        self.local_step += 1
         self._exchange(GRAD)
 
     def fetch_state(self) -> None:
@@ -252,9 +370,9 @@ class PSClient:
 
     def done(self) -> None:
         for j in range(self.k):
-            c = self._c.clone()
+            c = torch.zeros(CTRL, dtype=torch.int64)
             c[0] = DONE
-            send(c, j)
+            dist.send(c, j, group=self.group, tag=TAG_CTRL)
 
     def shard_of(self) -> Dict[str, int]:
         out = {}
@@ -266,22 +384,36 @@ class PSClient:
         return out
 
 
+def weight_l2_into(fp: FlatParams) -> None:
+    """sum(w^2) of every weight-decayed tensor into the per-tensor L2 slots that
+    ``finalize`` turns into the ``*/weight_loss`` terms (``mnist_input.py:112-114``);
+    PS workers run no local optimizer, which is what fills them otherwise."""
+    if not fp.wd_entries:
+        return
+    with torch.no_grad():
+        sq = torch.stack([fp.param_view(e.name).float().square().sum() for e in fp.wd_entries])
+        fp.l2[:len(fp.wd_entries)].copy_(sq)
+
+
 class PSWorkerReplica:
     """A worker replica in PS mode: same executor/input pipeline as ``Replica``
     but no local optimizer — gradients go to the PS tasks, fresh parameters
     and the shared global step come back."""
 
-    def __init__(self, base, num_ps: int):
+    def __init__(self, base, num_ps: int, num_workers: int, worker_index: int, group=None, transport: str = ""):
         self.base = base                  # a train.replica.Replica (built with world=1 semantics)
         self.net = base.net
         self.spec = base.spec
-        self.client = PSClient(base.net, num_ps)
+        self.client = PSClient(base.net, num_ps, num_workers, worker_index, group=group, transport=transport)
         self.world = 1
         self.examples_per_step = base.B
         self.device = base.device
         self.loader = base.loader
         self.eval_ds = base.eval_ds
         self.dp = base.dp
+        # T6-style slow worker (async test): MNIST_FI_SLOW_WORKER=task:seconds sleeps every step
+        sw = os.environ.get("MNIST_FI_SLOW_WORKER", "")
+        self._sleep = float(sw.split(":")[1]) if ":" in sw and int(sw.split(":")[0]) == worker_index else 0.0
         self.client.hello()
 
     @property
@@ -297,7 +429,10 @@ class PSWorkerReplica:
         net.forward(defer_head=True)
         net.loss_and_grad()
         net.backward()
+        weight_l2_into(net.fp)
         net.finalize(net.B, increment=False)
+        if self._sleep:
+            time.sleep(self._sleep)
         self.client.push_pull()
 
     @property

@@ -636,6 +636,31 @@ class HipNet:
                 return lay.out
         raise KeyError(layer_name)
 
+    def layer_activation(self, layer_name: str, n: int) -> torch.Tensor:
+        """The reference's ``<layer>/<layer>:0`` tensor (main.py:97-100) for the first
+        ``n`` images of the current batch: a conv layer's bias+ReLU output BEFORE
+        pooling.  A fused conv+pool layer never materialises it, so it is recomputed
+        here with the unfused implicit-GEMM conv kernel (monitoring only, every
+        ``test_interval`` steps).  Channel padding is kept; callers strip it."""
+        for lay in self.layers:
+            if lay.name != layer_name:
+                continue
+            n = max(1, min(n, self.B))
+            if not isinstance(lay, ConvPoolLayer):
+                return lay.out[:n]
+            s = lay.spec
+            OH, OW = Fk.conv_out_hw(lay.H, lay.W, s.kh, s.kw, s.padding)
+            x = lay.x
+            if lay.u8 is not None and lay.use_u8:
+                # training reads the uint8 dataset through the batch index: normalise those rows
+                u8, idx = lay.u8
+                x = (u8[idx[:n]].float() / 255.0 - 0.5).to(torch.bfloat16).view(n, lay.H, lay.W, lay.C)
+            out = torch.empty(n, OH, OW, lay.Cp, dtype=torch.bfloat16, device=self.device)
+            kernels().conv_fwd(x, self.fp.bf16_view(lay.wname), out, n, lay.H, lay.W, lay.C, OH, OW, s.kh, s.kw,
+                               lay.pad, lay.pad, lay.Cp, self.fp.param_view(lay.bname), s.cout, True)
+            return out
+        raise KeyError(layer_name)
+
     def read_stats(self) -> Dict[str, float]:
         s = self.stats.detach().cpu().tolist()
         return {"cross_entropy": s[4], "accuracy": s[5], "total_loss": s[6], "nan": s[2]}

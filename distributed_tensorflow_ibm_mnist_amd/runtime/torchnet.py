@@ -158,6 +158,16 @@ class TorchNet:
     def activation(self, layer_name: str) -> torch.Tensor:
         return self._acts[layer_name]
 
+    def layer_activation(self, layer_name: str, n: int) -> torch.Tensor:
+        """``<layer>/<layer>:0`` (main.py:97-100) for the first n images of the
+        current batch, recomputed without autograd (monitoring only)."""
+        n = max(1, min(n, self.B))
+        with torch.no_grad():
+            x = self.x0[:n].float() if not self.autocast else self.x0[:n]
+            with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.autocast):
+                _, acts = torch_ref.forward(self.spec, self._params(self.fp.params), x, keep_activations=True)
+        return acts[layer_name]
+
     def read_stats(self) -> Dict[str, float]:
         s = self.stats.detach().cpu().tolist()
         return {"cross_entropy": s[4], "accuracy": s[5], "total_loss": s[6], "nan": s[2]}

@@ -106,13 +106,12 @@ class Replica:
 
     def step(self) -> None:
         self.loader.next()
-        if self.use_graph:
-            if self._graph is None:
-                from ..runtime.graph import StepGraph
-                self._graph = StepGraph(self._body, warmup=1)
-                # warm-up ran one real step; account for it (and reload a batch for the replay)
-                self.global_step += 1
-                self.loader.next()
+        if self.use_graph and self._graph is None:
+            from ..runtime.graph import StepGraph
+            # the warm-up inside StepGraph IS this step (on the batch just loaded);
+            # capture itself executes nothing, so exactly one update happens here
+            self._graph = StepGraph(self._body, warmup=1)
+        elif self.use_graph:
             self._graph.replay()
         else:
             self._body()

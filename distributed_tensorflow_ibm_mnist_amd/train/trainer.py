@@ -60,7 +60,8 @@ def placement_table(replica, cl: Cluster) -> str:
     gradient bucket and kernel runs."""
     net = replica.net
     dev = str(replica.device)
-    lines = [f"device placement (rank {cl.rank}/{cl.world}, mode {cl.mode}, backend {cl.backend or 'none'}):"]
+    lines = [f"device placement (rank {cl.rank}/{cl.world}, mode {cl.mode}, backend {cl.backend or 'none'}"
+             + (f", PS data plane {cl.transport}" if cl.mode == "ps" else "") + "):"]
     for e in net.fp.entries:
         lines.append(f"  {e.name:34s} {str(e.shape):22s} fp32 master + EMA{' + Momentum' if net.opt.use_momentum else ''}"
                      f" -> {dev if cl.mode != 'ps' else 'ps shard'}")
@@ -107,7 +108,7 @@ def _train(FLAGS, cl: Cluster, max_steps, test_interval, batch_size, impl, log) 
         if prefix:
             log(f"[ps {cl.task_id}] restored shard from {prefix}")
         ps = ParameterServer(cl.task_id, cl.num_ps, cl.num_workers, param_specs(spec), init, opt, cl.device,
-                             max_steps, restore=restore, log=log)
+                             max_steps, restore=restore, log=log, transport=cl.transport)
         res = ps.serve()
         return {"global_step": float(res["global_step"])}
 
@@ -126,7 +127,7 @@ def _train(FLAGS, cl: Cluster, max_steps, test_interval, batch_size, impl, log) 
     replica = base
     if cl.mode == "ps":
         from ..parallel.ps import PSWorkerReplica
-        replica = PSWorkerReplica(base, cl.num_ps)
+        replica = PSWorkerReplica(base, cl.num_ps, cl.num_workers, cl.task_id, transport=cl.transport)
     is_chief = cl.is_chief
     if FLAGS.log_device_placement:
         log(placement_table(replica, cl))

@@ -62,7 +62,8 @@ flags.DEFINE_integer("save_summaries_steps", 100, "loss/accuracy scalars every N
 flags.DEFINE_integer("log_step_count_steps", 100, "global_step/sec every N steps")
 flags.DEFINE_integer("max_to_keep", 5, "checkpoints to keep")
 flags.DEFINE_integer("eval_examples", 10000, "examples per test-summary evaluation (0: whole split)")
-flags.DEFINE_string("ps_backend", "", "PS-mode transport override: '' (RCCL on GPU) | gloo (host-staged)")
+flags.DEFINE_string("ps_backend", "", "PS-mode data plane: '' (ipc on GPU, host on CPU) | ipc (xGMI peer copies) | "
+                    "host / gloo (staged through host memory)")
 flags.DEFINE_string("dp_backend", "", "DP transport override: '' (RCCL on GPU, gloo on CPU) | gloo (host-staged; "
                     "lets several ranks share one GPU for a rehearsal)")
 flags.DEFINE_float("collective_timeout", 600.0, "process-group timeout (s): a hung peer fails the job")

@@ -247,3 +247,66 @@ def test_dp_rank_kill_elastic_restart_resumes(tmp_path):
     assert latest_checkpoint(d).endswith("model.ckpt-40")
     ev = [f for f in os.listdir(d) if f.startswith("events.out.tfevents")]
     assert len(ev) <= 2, ev          # one per attempt, chief only
+
+
+def test_ps_async_arrival_order_slow_worker(tmp_path):
+    """Async semantics: with one worker slowed, the PS keeps applying the fast
+    workers' pushes in arrival order (no lock-step): the fast workers' applied
+    counts exceed the slow one's, and the total is exactly max_steps."""
+    base = free_port()
+    ps_hosts = f"localhost:{base}"
+    wk_hosts = ",".join(f"localhost:{base + 100 + i}" for i in range(3))
+    d = str(tmp_path / "train")
+    common = ["--impl=torch", "--cpu", "--model=mlp", "--in_channels=1", "--batch_size=16", "--max_steps=60",
+              "--test_interval=1000", "--log_step_count_steps=0", "--train_data=synthetic://600",
+              "--test_data=synthetic://100?seed=1", f"--train_dir={d}", f"--ps_hosts={ps_hosts}",
+              f"--worker_hosts={wk_hosts}", "--save_checkpoint_secs=0", "--eval_examples=100"]
+    os.environ["MNIST_FI_SLOW_WORKER"] = "2:0.25"
+    try:
+        procs = [("ps0", _spawn_main(common + ["--job_name=ps", "--task_id=0"], tmp_path / "ps0.log"))]
+        for i in range(3):
+            procs.append((f"w{i}", _spawn_main(common + ["--job_name=worker", f"--task_id={i}"],
+                                               tmp_path / f"w{i}.log")))
+    finally:
+        del os.environ["MNIST_FI_SLOW_WORKER"]
+    t0 = time.time()
+    for name, p in procs:
+        try:
+            p.wait(timeout=max(5, 240 - (time.time() - t0)))
+        except subprocess.TimeoutExpired:
+            for _, q in procs:
+                q.kill()
+            pytest.fail(f"{name} hung:\n" + open(tmp_path / f"{name}.log").read()[-3000:])
+    logs = {n: open(tmp_path / f"{n}.log").read() for n, _ in procs}
+    for n, p in procs:
+        assert p.returncode == 0, logs[n][-3000:]
+    import re
+    m = re.search(r"applied (\d+) update\(s\), per worker \[(\d+), (\d+), (\d+)\]", logs["ps0"])
+    assert m, logs["ps0"][-2000:]
+    applied, c0, c1, c2 = map(int, m.groups())
+    assert applied == 60 and c0 + c1 + c2 == 60
+    assert min(c0, c1) > c2, (c0, c1, c2)            # the slow worker did not hold the others back
+    assert "transport host" in logs["ps0"]
+
+
+def test_ps_worker_weight_loss_terms():
+    """PS workers run no local optimizer; the weight-decay loss terms still enter
+    total_loss (mnist_input.py:112-114,231) via ps.weight_l2_into."""
+    from distributed_tensorflow_ibm_mnist_amd.models import get_model, torch_ref
+    from distributed_tensorflow_ibm_mnist_amd.parallel.ps import weight_l2_into
+    from distributed_tensorflow_ibm_mnist_amd.runtime.params import OptConfig
+    from distributed_tensorflow_ibm_mnist_amd.runtime.torchnet import TorchNet
+    spec = get_model("reference_cnn", 1)
+    net = TorchNet(spec, 2, "cpu", torch_ref.init_params(spec, seed=3), OptConfig())
+    net.x0.copy_(torch.rand(2, 28, 28, 1) - 0.5)
+    net.labels.copy_(torch.tensor([1, 7], dtype=torch.int32))
+    net.forward()
+    net.loss_and_grad()
+    net.backward()
+    weight_l2_into(net.fp)
+    net.finalize(2, increment=False)
+    want = sum(0.004 * 0.5 * float(net.fp.param_view(f"{n}/weights").square().sum()) for n in ("local3", "local4"))
+    st = net.read_stats()
+    assert want > 0.01
+    assert abs((st["total_loss"] - st["cross_entropy"]) - want) < 1e-4 * want
+    assert int(net.fp.step.item()) == 0

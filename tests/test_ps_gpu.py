@@ -1,0 +1,128 @@
+"""Parameter-server mode on the MI355X (``/root/reference/main.py:56-62,80-82``,
+``/root/reference/mnist_input.py:261-264``).
+
+One GPU box rehearses the 1 PS + N workers topology with every process on the
+same card: the ``ipc`` data plane (PS-owned device mailboxes, one-sided copies,
+gloo control plane) is exactly the code that runs across 8 GPUs, where the
+copies cross xGMI instead of staying in one HBM.  HIP workers, fused K9 apply
+on the PS, async arrival order, stop at ``max_steps``, clean PS exit, PS-owned
+sharded checkpoint; and the PS bench mode's JSON line.
+"""
+import json
+import os
+import re
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _launch(tmp_path, transport, num_ps=1, num_workers=2, max_steps=60):
+    base = free_port()
+    ps_hosts = ",".join(f"localhost:{base + i}" for i in range(num_ps))
+    wk_hosts = ",".join(f"localhost:{base + 100 + i}" for i in range(num_workers))
+    d = str(tmp_path / f"train_{transport}_{num_ps}")
+    common = ["--model=lenet5", "--in_channels=1", "--batch_size=256", f"--max_steps={max_steps}",
+              "--test_interval=30", "--log_step_count_steps=0", "--train_data=synthetic://8000",
+              "--test_data=synthetic://512?seed=1", "--eval_examples=512", f"--train_dir={d}",
+              f"--ps_hosts={ps_hosts}", f"--worker_hosts={wk_hosts}", f"--ps_backend={transport}",
+              "--optimizer=momentum", "--base_lr=0.02"]
+    env = dict(os.environ, PYTHONUNBUFFERED="1", OMP_NUM_THREADS="2")
+    procs = []
+    for job, n in (("ps", num_ps), ("worker", num_workers)):
+        for i in range(n):
+            log = tmp_path / f"{transport}_{job}{i}.log"
+            procs.append((f"{job}{i}", log, subprocess.Popen(
+                [sys.executable, os.path.join(ROOT, "main.py")] + common + [f"--job_name={job}", f"--task_id={i}"],
+                cwd=ROOT, env=env, stdout=open(log, "w"), stderr=subprocess.STDOUT)))
+    t0 = time.time()
+    for name, log, p in procs:
+        try:
+            p.wait(timeout=max(5, 200 - (time.time() - t0)))
+        except subprocess.TimeoutExpired:
+            for _, _, q in procs:
+                q.kill()
+            pytest.fail(f"{name} hung:\n" + open(log).read()[-3000:])
+    logs = {name: open(log).read() for name, log, _ in procs}
+    for name, _, p in procs:
+        assert p.returncode == 0, (name, logs[name][-3000:])
+    return d, logs
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("transport", ["ipc", "host"])
+def test_ps_mode_hip_workers_one_gpu(tmp_path, dev, transport):
+    d, logs = _launch(tmp_path, transport)
+    assert f"transport {transport}" in logs["ps0"]
+    m = re.search(r"applied (\d+) update\(s\), per worker \[(\d+), (\d+)\]", logs["ps0"])
+    assert m, logs["ps0"][-2000:]
+    assert int(m.group(1)) == 60 and int(m.group(2)) + int(m.group(3)) == 60
+    assert min(int(m.group(2)), int(m.group(3))) > 0            # both workers contributed
+    assert "result: global_step=60" in logs["worker0"]
+    # training made progress: the chief's held-out evaluations (Logger hook) improve
+    accs = [float(a) for a in re.findall(r"test accuracy ([0-9.]+)", logs["worker0"])]
+    assert len(accs) >= 2 and accs[-1] > 0.3, accs
+    from distributed_tensorflow_ibm_mnist_amd.ckpt.saver import Saver, latest_checkpoint
+    p = latest_checkpoint(d)
+    assert p.endswith("model.ckpt-60")
+    t = Saver.restore(p)
+    assert int(t["global_step"]) == 60 and "fc3/weights/Momentum" in t
+
+
+@pytest.mark.timeout(300)
+def test_ps_mode_two_ps_ipc(tmp_path, dev):
+    """k=2 PS shards: both apply exactly max_steps updates (consistent shard counts)."""
+    d, logs = _launch(tmp_path, "ipc", num_ps=2, num_workers=2, max_steps=40)
+    for j in (0, 1):
+        assert re.search(r"applied 40 update\(s\)", logs[f"ps{j}"]), logs[f"ps{j}"][-2000:]
+    from distributed_tensorflow_ibm_mnist_amd.ckpt.bundle import read_index
+    from distributed_tensorflow_ibm_mnist_amd.ckpt.saver import latest_checkpoint
+    n, _ = read_index(latest_checkpoint(d))
+    assert n == 2
+
+
+@pytest.mark.timeout(300)
+def test_ps_transports_bitwise_equal_one_worker(dev):
+    """With ONE worker the PS run is deterministic: the ipc data plane (device
+    mailboxes) and the host-staged one must leave bitwise-identical parameters."""
+    sums = {}
+    for t in ("ipc", "host"):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+               "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.join(ROOT, "bench.py"),
+               "--mode", "ps", "--ps_transport", t, "--batch", "256", "--steps", "20", "--warmup", "2"]
+        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=200,
+                           env=dict(os.environ, OMP_NUM_THREADS="2"))
+        assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+        d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+        assert d["global_step"] == 22
+        sums[t] = d["param_checksum"]
+    assert sums["ipc"] == sums["host"], sums
+
+
+@pytest.mark.timeout(300)
+def test_bench_ps_mode_json(dev):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.join(ROOT, "bench.py"),
+           "--mode", "ps", "--batch", "4096", "--steps", "10", "--warmup", "2"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, OMP_NUM_THREADS="2"))
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1, out[-3000:]
+    d = json.loads(line[0])
+    assert d["config"]["parallelism"] == "ps1+w2" and d["global_step"] == 24
+    assert d["value"] > 0 and sum(d["applied_per_worker"]) == 24

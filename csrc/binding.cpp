@@ -687,6 +687,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("dense_wgrad", &dense_wgrad, py::arg("x"), py::arg("dy"), py::arg("slab"), py::arg("Din"), py::arg("Dout"),
         py::arg("B"), py::arg("ldx"), py::arg("lddy"), py::arg("with_bias"), py::arg("splits"), py::arg("tile") = -1);
   m.def("conv_fwd", &conv_fwd);
+  m.def("set_halo_variants", [](int64_t f, int64_t d) { mnistx::set_halo_variants((int)f, (int)d); });
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("prep_images", &prep_images);

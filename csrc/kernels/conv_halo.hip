@@ -28,13 +28,24 @@ namespace mnistx {
 namespace {
 
 constexpr int HW = 14, KS = 5, HP = HW + 4, NPIX = HW * HW, NTAP = KS * KS;
-constexpr int MFR = (NPIX + 15) / 16;        // 13 M-fragments of 16 pixels
+// Forward / dgrad tile: 18 rows x WR = 20 pixels (interior at rows/cols 2..15).  An
+// M-fragment is ONE output row of 16 pixels (columns 14/15 are padding whose results
+// are dropped; they read the zero columns 16..19), so a fragment's 16 lanes read 16
+// CONSECUTIVE tile pixels -- the property the swizzle below needs.
+constexpr int WR = 20;
+constexpr int MFR = HW;                      // 14 row fragments per image
 
-// 16-byte chunk swizzle of row r (CH chunks per row)
+// 16-byte chunk swizzle of tile/filter row r (CH chunks per row), for ds_read_b128
+// by 16 consecutive rows x one chunk per lane group: with 64-B rows (CH 4, four rows
+// per 256-B bank line) chunk ^= bit2(r)*2, with 128-B rows (CH 8) chunk ^= r & 6 --
+// each of the instruction's four 16-lane bank groups ({0-3,12-15,20-27}, ...) then
+// hits 16 distinct 16-byte bank slots for ANY start row (exhaustive check:
+// bench/lds_sim.py halo).  (The previous c ^ (r & 3) over 13 wrapped 16-pixel runs
+// measured 45-51 % LDS bank-conflict cycles.)
 template <int CH>
 DEV int swz(int r, int c) {
-  if constexpr (CH == 4) return c ^ (r & 3);
-  else return c ^ ((r ^ (r >> 3)) & (CH - 1));
+  if constexpr (CH == 4) return c ^ ((r >> 1) & 2);
+  else return c ^ (r & 6);
 }
 
 // MODE 0 = forward: out[p][n] = relu(sum_{tap,ci} x[p+tap][ci] W[tap][ci][n] + b[n])
@@ -50,7 +61,7 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict
   constexpr int CH = CIN / 8;                 // 16-byte chunks per pixel / filter row
   constexpr int NF = CW / 16;
   constexpr int KC = CIN / 32;                // 32-wide k-steps per tap
-  constexpr int XE = HP * HP * CIN;           // image tile elements (one image)
+  constexpr int XE = HP * WR * CIN;           // image tile elements (one image)
   constexpr int WE = NTAP * CW * CIN;         // filter slice elements
   constexpr int NV = NPIX * CH;               // 16-byte vectors per input image
   constexpr int PER = (IMGS * NV + NT - 1) / NT;
@@ -103,7 +114,7 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict
       if (v < IMGS * NV) {
         const int im = v / NV, vv = v - im * NV;
         const int p = vv / CH, c = vv - p * CH;
-        const int P = (p / HW + 2) * HP + (p % HW) + 2;
+        const int P = (p / HW + 2) * WR + (p % HW) + 2;
         const int PI = im * (XE / CIN) + P;      // pixel index across the group's tiles
         *(u32x4*)(xs + PI * CIN + (swz<CH>(PI, c) << 3)) = pre[u];
       }
@@ -111,13 +122,12 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict
     __syncthreads();
     gload(img0 + gstride);                      // next group in flight during the MFMAs
     for (int gr = wave; gr < NGRP; gr += NW) {
-      // fragments FR*gr .. FR*gr+FR-1 (fragments past the 13th are padding pixels)
-      int P0[FR];                               // element offset of the pixel's tap-(0,0) tile pixel
+      // fragments FR*gr .. FR*gr+FR-1 = (image, output row); lane i = output column
+      int P0[FR];                               // tile pixel under tap (0,0) of this lane's output pixel
 #pragma unroll
       for (int h = 0; h < FR; ++h) {
         const int f = min(FR * gr + h, IMGS * MFR - 1), im = f / MFR;
-        const int p = min((f - im * MFR) * 16 + i, NPIX - 1);
-        P0[h] = im * (XE / CIN) + (p / HW) * HP + (p % HW);
+        P0[h] = im * (XE / CIN) + (f - im * MFR) * WR + i;
       }
       f32x4 acc[FR][NF];
 #pragma unroll
@@ -128,7 +138,7 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict
 #pragma unroll
         for (int kw = 0; kw < KS; ++kw) {
           const int t = kh * KS + kw;
-          const int dP = kh * HP + kw;
+          const int dP = kh * WR + kw;
 #pragma unroll
           for (int kc = 0; kc < KC; ++kc) {
             const int c = 4 * kc + g;
@@ -147,30 +157,43 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict
             for (int h = 0; h < FR; ++h)
 #pragma unroll
               for (int nf = 0; nf < NF; ++nf)
-                acc[h][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[h], b[nf], acc[h][nf], 0, 0, 0);
+                // filter rows as the A operand: D = (W x)^T, so a lane holds 4 CONSECUTIVE
+                // output channels of one pixel (one 8-byte store) instead of one channel of
+                // 4 pixels (four 2-byte stores)
+                acc[h][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nf], a[h], acc[h][nf], 0, 0, 0);
           }
         }
       }
-      // D rows 4g + r = pixels, column i = output channel n0 + nf*16 + i
+      // D row 4g + r = output channel n0 + nf*16 + 4g + r, column i = output column ow
 #pragma unroll
-      for (int h = 0; h < FR; ++h)
+      for (int nf = 0; nf < NF; ++nf) {
+        const int nb = n0 + nf * 16 + 4 * g;
+        float bn[4];
 #pragma unroll
-        for (int nf = 0; nf < NF; ++nf) {
-          const int n = n0 + nf * 16 + i;
-          const float bn = (MODE == 0 && bias != nullptr && n < bias_n) ? bias[n] : 0.f;
+        for (int r = 0; r < 4; ++r)
+          bn[r] = (MODE == 0 && bias != nullptr && nb + r < bias_n) ? bias[nb + r] : 0.f;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int f = FR * gr + h, im = f / MFR;
-            const int q = (f - im * MFR) * 16 + 4 * g + r;
-            if (f < IMGS * MFR && q < NPIX && img0 + im < B) {
-              float v = acc[h][nf][r] + bn;
-              if (relu) v = fmaxf(v, 0.f);
-              const int64_t row = (int64_t)(img0 + im) * NPIX + q;
-              if (mask != nullptr && !(bf2f(mask[row * ldm + n]) > 0.f)) v = 0.f;
-              out[row * ldo + n] = f2bf(v);
+        for (int h = 0; h < FR; ++h) {
+          const int f = FR * gr + h, im = f / MFR;
+          const int q = (f - im * MFR) * HW + i;
+          if (f < IMGS * MFR && i < HW && img0 + im < B) {
+            const int64_t row = (int64_t)(img0 + im) * NPIX + q;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v[r] = acc[h][nf][r] + bn[r];
+              if (relu) v[r] = fmaxf(v[r], 0.f);
             }
+            if (mask != nullptr) {
+              const u32x2 mk = *(const u32x2*)(mask + row * ldm + nb);
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (!(bf2f((bf16_t)((mk[r >> 1] >> (16 * (r & 1))) & 0xffffu)) > 0.f)) v[r] = 0.f;
+            }
+            *(u32x2*)(out + row * ldo + nb) = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
           }
         }
+      }
     }
   }
 }
@@ -354,41 +377,62 @@ bool conv5_halo_dgrad_ok(int OH, int OW, int Cout, int H, int W, int KH, int KW,
          Cin % 32 == 0;
 }
 
-// Variant (MNISTX_HALO_FWD / MNISTX_HALO_DGRAD = index; sweep: bench/gpu_halo_sweep.sh)
+// Variant (MNISTX_HALO_FWD / MNISTX_HALO_DGRAD = index; sweep: bench/gpu_halo_sweep.sh);
+// set_halo_variants() overrides both (tests run every variant in one process).
+static int g_halo_override[2] = {-1, -1};
 static int halo_variant(const char* name, int dflt) {
+  const int which = name[12] == 'F' ? 0 : 1;   // "MNISTX_HALO_FWD" / "MNISTX_HALO_DGRAD"
+  if (g_halo_override[which] >= 0) return g_halo_override[which];
   const char* e = getenv(name);
   return (e && e[0] >= '0' && e[0] <= '9') ? e[0] - '0' : dflt;
 }
 
+// Launch shapes (profiles/r2/halo: per-kernel us at B = 16384).  More resident waves
+// beat bigger per-wave tiles: 8 waves x 2 row fragments 350 us fwd / 326 us dgrad vs
+// 4 x 4 fragments 435 / 520 us.
 hipError_t conv5_halo_fwd(const bf16_t* x, const bf16_t* w, int Nb, int C, int Cout, const float* bias, int bias_n,
                           int relu, bf16_t* out, hipStream_t st) {
-  static const int v = halo_variant("MNISTX_HALO_FWD", 0);
+  const int v = halo_variant("MNISTX_HALO_FWD", 0);
   switch (v) {
-    case 1:   // whole Cout per block (NF = 4): 123 KB LDS, 1 block / CU
+    case 1:   // whole Cout per block (NF = 4): 125 KB LDS, 1 block / CU
       if (Cout == 64) return run_halo<32, 64, 4, 0, 4>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
       break;
-    case 2:   // 8 waves, fragment pairs
-      return run_halo<32, 32, 8, 0, 2>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
-    case 3:   // two images per block, 8 waves x (4 fragments x all 64 channels)
-      if (Cout == 64)
-        return run_halo<32, 64, 8, 0, 4, 2>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
+    case 2:   // 4 waves x 4 row fragments
+      return run_halo<32, 32, 4, 0, 4>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
+    case 3:   // 16 waves x 1 row fragment
+      return run_halo<32, 32, 16, 0, 1>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
+    case 4:   // two images per block, 8 waves x 2 row fragments (7 of 8 groups busy twice)
+      return run_halo<32, 32, 8, 0, 2, 2>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
+    case 5:   // whole Cout, 8 waves x 2 row fragments
+      if (Cout == 64) return run_halo<32, 64, 8, 0, 2>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
       break;
     default: break;
   }
-  return run_halo<32, 32, 4, 0, 4>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
+  return run_halo<32, 32, 8, 0, 2>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
 }
 
 hipError_t conv5_halo_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int Cout, int Cin, const bf16_t* mask,
                             bf16_t* dx, hipStream_t st) {
-  static const int v = halo_variant("MNISTX_HALO_DGRAD", 0);
+  const int v = halo_variant("MNISTX_HALO_DGRAD", 0);
   switch (v) {
-    case 1:   // 8 waves, fragment pairs
-      return run_halo<64, 32, 8, 1, 2>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
+    case 1:   // 4 waves x 4 row fragments
+      return run_halo<64, 32, 4, 1, 4>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
     case 2:   // half the input channels of the conv per block (NF = 1)
       return run_halo<64, 16, 4, 1, 4>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
+    case 3:   // 16 waves x 1 row fragment
+      return run_halo<64, 32, 16, 1, 1>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
+    case 4:   // half the channels, 8 waves x 2 row fragments (97 KB LDS)
+      return run_halo<64, 16, 8, 1, 2>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
+    case 5:   // 2 waves x 7 row fragments
+      return run_halo<64, 32, 2, 1, 7>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
     default: break;
   }
-  return run_halo<64, 32, 4, 1, 4>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
+  return run_halo<64, 32, 8, 1, 2>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
+}
+
+void set_halo_variants(int fwd, int dgrad) {
+  g_halo_override[0] = fwd;
+  g_halo_override[1] = dgrad;
 }
 
 bool conv5_halo_wgrad_ok(int H, int W, int C, int OH, int OW, int KH, int KW, int ph, int pw, int Cout,

@@ -37,6 +37,7 @@ hipError_t dense_wgrad_group(int np, const bf16_t* const* x, const bf16_t* const
                              int B, const int* ldx, const int* lddy, int* splits, const GemmEpi* ep, hipStream_t st);
 // conv_halo.hip: LDS-halo 5x5 convolutions (reference conv2 geometry); conv_fwd /
 // conv_dgrad route there when *_ok() holds
+void set_halo_variants(int fwd, int dgrad);
 bool conv5_halo_fwd_ok(int H, int W, int C, int OH, int OW, int KH, int KW, int ph, int pw, int Cout);
 bool conv5_halo_dgrad_ok(int OH, int OW, int Cout, int H, int W, int KH, int KW, int ph, int pw, int Cin);
 hipError_t conv5_halo_fwd(const bf16_t* x, const bf16_t* w, int Nb, int C, int Cout, const float* bias, int bias_n,

@@ -144,6 +144,29 @@ def test_conv_fwd(dev, K, N, H, W, Ci, Co, k, pad):
     close(y, conv_ref(x, w, b, pad, True))
 
 
+@pytest.mark.parametrize("fv,dv", [(1, 1), (2, 2), (3, 3), (4, 4), (5, 5)])
+def test_conv_halo_variants(dev, K, fv, dv):
+    """Every conv_halo.hip launch variant (reference conv2 geometry; odd batch leaves a
+    partial image group) against the fp32 oracle: forward + bias + ReLU, masked dgrad."""
+    torch.manual_seed(7)
+    N, H, W, Ci, Co, k, pad = 5, 14, 14, 32, 64, 5, "SAME"
+    x = rnd(N, H, W, Ci, dev=dev).float().requires_grad_(True)
+    w = rnd(k, k, Ci, Co, dev=dev, scale=1 / math.sqrt(k * k * Ci))
+    b = torch.randn(Co, device=dev)
+    K.set_halo_variants(fv, dv)
+    try:
+        y = Fk.conv2d(x.detach().to(torch.bfloat16), w, b, pad, relu=True)
+        close(y, conv_ref(x.detach().to(torch.bfloat16), w, b, pad, True))
+        yr = conv_ref(x, w, None, pad, False)
+        dy = rnd(*yr.shape, dev=dev)
+        yr.backward(dy.float())
+        mask = rnd(N, H, W, Ci, dev=dev).relu().to(torch.bfloat16)
+        dxm = Fk.conv2d_dgrad(dy, w, (H, W), pad, mask=mask)
+        close(dxm, x.grad * (mask.float() > 0))
+    finally:
+        K.set_halo_variants(-1, -1)
+
+
 @pytest.mark.parametrize("N,H,W,Ci,Co,k,pad", [c for c in CONV_CASES if c[3] % 8 == 0])
 def test_conv_dgrad(dev, K, N, H, W, Ci, Co, k, pad):
     torch.manual_seed(4)

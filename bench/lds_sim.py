@@ -40,3 +40,25 @@ def cycles(kind: str, addrs) -> int:
 
 def ideal(kind: str) -> int:
     return len(GROUPS[kind])
+
+
+def halo_swz(ch: int, r: int, c: int) -> int:
+    """conv_halo.hip swz<CH>: 16-byte chunk c of tile / filter row r."""
+    return c ^ ((r >> 1) & 2) if ch == 4 else c ^ (r & 6)
+
+
+def check_halo(ch: int) -> int:
+    """Worst ds_read_b128 cycle count of the conv_halo A/B fragment reads: lane
+    (i = l & 15, g = l >> 4) reads chunk 4kc + g of row r0 + i, for every start row
+    r0 and k-step kc (rows of CH 16-byte chunks).  4 = conflict-free."""
+    worst = 0
+    for r0 in range(256):
+        for kc in range(ch // 4):
+            addrs = [((r0 + (l & 15)) * ch + halo_swz(ch, r0 + (l & 15), 4 * kc + (l >> 4))) * 16 for l in range(64)]
+            worst = max(worst, cycles("b128", addrs))
+    return worst
+
+
+if __name__ == "__main__" and len(__import__("sys").argv) > 1 and __import__("sys").argv[1] == "halo":
+    for ch in (4, 8):
+        print(f"conv_halo swizzle, {16 * ch}-byte rows: worst ds_read_b128 = {check_halo(ch)} cycles (4 = conflict-free)")

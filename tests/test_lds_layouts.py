@@ -1,0 +1,13 @@
+"""Offline LDS bank-conflict checks of kernel tile layouts (bench/lds_sim.py, the
+MI355X_MICROARCH.md LDS banking model): no GPU needed."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench"))
+
+
+def test_conv_halo_swizzle_conflict_free():
+    import lds_sim
+    # conv_halo.hip fwd/dgrad A and B fragment reads: 4 LDS cycles per ds_read_b128 = no conflict
+    assert lds_sim.check_halo(4) == 4
+    assert lds_sim.check_halo(8) == 4

@@ -1163,7 +1163,267 @@ using LeNetC2 = Geo<8, 16, 5, 0, 14, 14>;
 using RefC1g = Geo<1, 32, 5, 2, 28, 28>;
 using RefC1c = Geo<3, 32, 5, 2, 28, 28>;
 
+// ------------------------------------------------------------------ LeNet-5: conv2 data gradient -> conv1 weight gradient, fused
+// The pool1 gradient dP1 = conv2 dgrad(unpool(dP2, arg2)) is consumed by conv1's
+// weight gradient image by image inside one kernel, so it never exists in HBM
+// (the two-kernel path writes and re-reads 2 x 3 KB per image: 400 MB per step at
+// B = 65536).  Per image group (persistent blocks, grid stride):
+//   stage   : x -> image tile (copy 0); max-unpool(dP2, arg2) -> haloed dY2 tile;
+//             arg1 bytes -> LDS                                              | barrier
+//   phase 1 : the three kw-shifted copies of x (make_shifted) and, beside them,
+//             conv2 dgrad (convpool_dgrad_pair_k's MFMA layout); its epilogue
+//             rounds dP1 to bf16 (as the stored tensor would be) and max-unpools
+//             it through arg1 straight into conv1 wgrad's U operand         | barrier
+//   phase 2 : conv1 weight gradient (convpool_wgrad_pair_k's MFMA layout)
+// The slab is convpool_wgrad_pair_k's ([KM][8] per block, bias row KE), so the
+// split-K reduce is unchanged.  Bias: each lane owns one dP1 channel; per-lane
+// sums combined in a fixed lane order (deterministic).
+template <int IMGS>
+__global__ __launch_bounds__(NTH, 3) void lenet_c2dgrad_c1wgrad_k(const XSrc x, const bf16_t* __restrict__ dP2,
+                                                               const uint8_t* __restrict__ arg2,
+                                                               const bf16_t* __restrict__ w2,
+                                                               const uint8_t* __restrict__ arg1, int B,
+                                                               float* __restrict__ slab) {
+  using G2 = LeNetC2;
+  using G1 = LeNetC1;
+  // conv2 dgrad geometry (convpool_dgrad_pair_k<G2>)
+  constexpr int Q = G2::KS - 1 - G2::PAD;
+  constexpr int OHQ = G2::OH + 2 * Q, OWQ = G2::OW + 2 * Q;
+  constexpr int DPS = G2::COUT + 8;
+  constexpr int RSE = (OWQ * DPS * 2 + 255) / 256 * 128;
+  constexpr int DT = OHQ * RSE;
+  constexpr int KWQ = G2::KS + 1;
+  constexpr int NTAP = G2::KS * KWQ;
+  constexpr int KSD = (NTAP + 1) / 2;
+  constexpr int MFD = G2::H / 2;
+  constexpr int NWC2 = G2::NWIN * G2::COUT;
+  auto dtap_c = [](int s) constexpr { return (2 * s / KWQ) * RSE + (2 * s % KWQ) * DPS; };
+  // conv1 wgrad geometry (convpool_wgrad_pair_k<G1>)
+  constexpr int RS = (2 * G1::NWIN + 31) / 32;
+  constexpr int URS = 212;
+  static_assert(URS >= RS * 16 && URS % 8 == 4, "U row stride");
+  constexpr int UIMG = 16 * URS;
+  constexpr int NWC1 = G1::NWIN * 8;                  // arg1 bytes per image
+  static_assert(NWC1 % 16 == 0 && G2::H * G2::W == G1::NWIN && G2::CIN == 8, "dP1 = pool1 windows x 8 channels");
+  constexpr int TILE_E = (IMGS * G1::IMG_LDS + 7) / 8 * 8;
+  __shared__ __attribute__((aligned(16))) bf16_t dyt[IMGS * DT];
+  __shared__ __attribute__((aligned(16))) bf16_t tile[TILE_E];
+  __shared__ __attribute__((aligned(16))) uint32_t U[IMGS * UIMG];
+  __shared__ __attribute__((aligned(16))) uint8_t a1s[IMGS * NWC1];
+  float* const red = (float*)dyt;                    // end-of-kernel reductions reuse the dY2 tile
+  static_assert(IMGS * DT * 2 >= G1::KM * 16 * 4, "wgrad reduction reuses dyt");
+  static_assert(IMGS * UIMG >= NTH + 64, "bias combine reuses U");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int ci = li & 7, sx = li >> 3;
+  lds_zero<IMGS * DT>(dyt, tid);
+  lds_zero<TILE_E>(tile, tid);
+  lds_zero<IMGS * UIMG * 2>((bf16_t*)U, tid);         // windows >= NWIN stay zero
+
+  // conv2 dgrad: flipped-filter B fragments (resident).  A-fragment tap of k-step s:
+  // tp = 2s + g/2; since KWQ is even, kh = (2s)/KWQ for both g/2, so the tap offset is
+  // dtap(s) (compile time, a ds_read immediate) + the lane's (g/2)*DPS + 8(g&1)
+  static_assert(KWQ % 2 == 0 && 2 * (KSD - 1) + 1 < NTAP, "tap split");
+  bf16x8 bw[KSD];
+#pragma unroll
+  for (int s = 0; s < KSD; ++s) {
+    const int tp = 2 * s + (g >> 1);
+    const int kh = tp / KWQ, kwq = tp - kh * KWQ;
+    const int kw = kwq - sx;
+    const bool valid = tp < NTAP && kw >= 0 && kw < G2::KS;
+    const int tap = valid ? (G2::KS - 1 - kh) * G2::KS + (G2::KS - 1 - kw) : 0;
+    const u32x4 v = *(const u32x4*)(w2 + (tap * G2::CIN + ci) * G2::COUT + 8 * (g & 1));
+    bw[s] = __builtin_bit_cast(bf16x8, valid ? v : u32x4{0u, 0u, 0u, 0u});
+  }
+  // conv1 wgrad: im2col^T chunk deltas
+  const int q = (lane >> 2) & 3, p = lane & 3;
+  int cd[G1::MFW];
+#pragma unroll
+  for (int mf = 0; mf < G1::MFW; ++mf) {
+    const int k0 = mf * 16 + 4 * p;
+    cd[mf] = k0 < G1::KE ? G1::chunk_delta(k0) : 0;
+  }
+  f32x4 acc1[G1::MFW];
+#pragma unroll
+  for (int mf = 0; mf < G1::MFW; ++mf) acc1[mf] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc = 0.f;                                    // bias gradient of channel ci
+  // conv1 wgrad reduction steps of this wave: it = wave + 4j
+  constexpr int JW = (IMGS * RS + NTH / 64 - 1) / (NTH / 64);
+
+  constexpr int A1V = IMGS * NWC1 / 16;                // 16-byte arg1 vectors per group
+  constexpr int A1PER = (A1V + NTH - 1) / NTH;
+  u32x4 a1v[A1PER];
+  auto load_a1 = [&](int i0) {
+#pragma unroll
+    for (int u = 0; u < A1PER; ++u) {
+      const int e = tid + u * NTH;
+      a1v[u] = u32x4{0x04040404u, 0x04040404u, 0x04040404u, 0x04040404u};   // padded image: ReLU off
+      if (e < A1V && i0 + (16 * e) / NWC1 < B) a1v[u] = *(const u32x4*)(arg1 + (int64_t)i0 * NWC1 + 16 * e);
+    }
+  };
+
+  const int stride = gridDim.x * IMGS;
+  XStage<G1, IMGS> xs;
+  DYStage<G2, IMGS> ys;
+  xs.fetch_rows(x, blockIdx.x * IMGS, B);
+  xs.load(x, blockIdx.x * IMGS, B, tid);
+  xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
+  ys.load(dP2, arg2, blockIdx.x * IMGS, B, tid);
+  load_a1(blockIdx.x * IMGS);
+  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
+    __syncthreads();
+    xs.store(tile, tid);
+#pragma unroll
+    for (int u = 0; u < A1PER; ++u) {
+      const int e = tid + u * NTH;
+      if (e < A1V) *(u32x4*)(a1s + 16 * e) = a1v[u];
+    }
+    // max-unpool of dP2 into the haloed tile (convpool_dgrad_pair_k)
+#pragma unroll
+    for (int u = 0; u < DYStage<G2, IMGS>::PER; ++u) {
+      const int e = 8 * (tid + u * NTH);
+      if (e < IMGS * NWC2) {
+        const int im = e / NWC2, rem = e - im * NWC2;
+        const int win = rem / G2::COUT, co = rem - win * G2::COUT;
+        const int ph = win / G2::PW, pw = win - ph * G2::PW;
+        uint32_t E[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          E[k] = __builtin_amdgcn_perm(0u, ys.a[u][k >> 1], (k & 1) ? 0x0c030c02u : 0x0c010c00u);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int oh = 2 * ph + (d >> 1) + Q, ow = 2 * pw + (d & 1) + Q;
+          u32x4 o;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) o[k] = ys.y[u][k] & half_eq_mask(E[k], (uint32_t)d);
+          *(u32x4*)(dyt + im * DT + oh * RSE + ow * DPS + co) = o;
+        }
+      }
+    }
+    __syncthreads();
+    if (img0 + stride < B) {
+      xs.load(x, img0 + stride, B, tid);
+      xs.fetch_rows(x, img0 + 2 * stride, B);
+      ys.load(dP2, arg2, img0 + stride, B, tid);
+      load_a1(img0 + stride);
+    }
+    // phase 1: shifted copies of x (read only in phase 2) beside conv2 dgrad -> U
+    make_shifted<G1, IMGS>(tile, tid);
+    for (int f = wave; f < IMGS * MFD; f += NTH / 64) {
+      const int im = f / MFD, mf = f - im * MFD;
+      const bf16_t* tb = dyt + im * DT + (2 * mf + (li >> 3)) * RSE + (2 * (li & 7) + (g >> 1)) * DPS + 8 * (g & 1);
+      const int ih = 2 * mf + (g >> 1);
+      // the epilogue's arg1 bytes are read before the MFMA chain (latency hidden)
+      uint32_t av4[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int jr = 4 * (g & 1) + r;
+        av4[r] = 2 * jr < G2::W ? a1s[im * NWC1 + (ih * G2::W + 2 * jr + sx) * 8 + ci] : 4u;
+      }
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      // the chain's A fragments in batches of DB in flight (all 15 at once cost 40 VGPRs
+      // of occupancy: 2 -> 3 waves per SIMD)
+      constexpr int DB = 5;
+      static_assert(KSD % DB == 0, "");
+#pragma unroll
+      for (int b = 0; b < KSD; b += DB) {
+        bf16x8 a[DB];
+#pragma unroll
+        for (int s = 0; s < DB; ++s) a[s] = __builtin_bit_cast(bf16x8, *(const u32x4*)(tb + dtap_c(b + s)));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < DB; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], bw[b + s], acc, 0, 0, 0);
+      }
+      // rows 4g + r: dP1 pixel (ih, iw = 2jr + sx), channel ci; pool1 window w1 = ih*14 + iw
+      uint32_t* Ui = U + im * UIMG;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int jr = 4 * (g & 1) + r;
+        if (2 * jr < G2::W) {
+          const int w1 = ih * G2::W + 2 * jr + sx;
+          const uint32_t yb = f2bf(acc[r]);
+          const uint32_t av = av4[r];
+          bacc += av < 4u ? __uint_as_float(yb << 16) : 0.f;
+          Ui[ci * URS + w1] = (av == 0u ? yb : 0u) | (av == 2u ? yb << 16 : 0u);
+          Ui[(8 + ci) * URS + w1] = (av == 1u ? yb : 0u) | (av == 3u ? yb << 16 : 0u);
+        }
+      }
+    }
+    __syncthreads();
+    // phase 2: conv1 weight gradient (not unrolled: an unrolled loop's image-invariant
+    // tile offsets are hoisted out of the image loop and spill)
+#pragma unroll 1
+    for (int j = 0; j < JW; ++j) {
+      const int it = wave + (NTH / 64) * j;
+      if (it < IMGS * RS) {
+        const int im = it / RS, s = it - im * RS;
+        const uint32_t* ub = U + im * UIMG + li * URS + 16 * s + 2 * g;
+        const bf16x8 bfr = join(*(const s16x4*)ub, *(const s16x4*)(ub + opaque(8)));
+        // image-tile rows of this lane's two windows (arithmetic, no window-table lookup)
+        const int wq = 16 * s + 2 * g + (q >> 1);
+        const int pb0 = im * G1::IMG_LDS + G1::aligned_off(G1::wbase(min(wq, G1::NWIN - 1))) + (q & 1) * G1::WS;
+        const int pb1 = im * G1::IMG_LDS + G1::aligned_off(G1::wbase(min(wq + 8, G1::NWIN - 1))) + (q & 1) * G1::WS;
+#pragma unroll
+        for (int mf = 0; mf < G1::MFW; ++mf) {
+          const bf16x8 a = join(lds_tr4(tile + pb0 + cd[mf]), lds_tr4(tile + pb1 + cd[mf]));
+          acc1[mf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr, acc1[mf], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // cross-wave reduction in a fixed wave order, then the folded [KM][8] slab
+  for (int wv = 0; wv < NTH / 64; ++wv) {
+    __syncthreads();
+    if (wave == wv) {
+#pragma unroll
+      for (int mf = 0; mf < G1::MFW; ++mf)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float& dst = red[(mf * 16 + 4 * g + r) * 16 + li];
+          dst = (wv == 0) ? acc1[mf][r] : dst + acc1[mf][r];
+        }
+    }
+  }
+  float* bred = (float*)U;
+  bred[tid] = bacc;
+  __syncthreads();
+  if (tid < 8) {   // channel c: lanes li = c, c + 8 of every lane group and wave, fixed order
+    float v = 0.f;
+    for (int t = 0; t < NTH; t += 8) v += bred[t + tid];
+    bred[NTH + tid] = v;
+  }
+  __syncthreads();
+  float* out = slab + (int64_t)blockIdx.x * G1::KM * 8;
+  for (int e = tid; e < G1::KM * 8; e += NTH) {
+    const int m = e >> 3, cc = e & 7;
+    float v = 0.f;
+    if (m == G1::KE) v = bred[NTH + cc];
+    else if (m < G1::KE) v = red[m * 16 + cc] + red[(m + 1) * 16 + 8 + cc];
+    out[e] = v;
+  }
+}
+
+// A/B knob MNISTX_LENET_BWD_IMGS=2: two images per group (89 KB LDS, one block per CU)
+static int lenet_bwd_imgs() {
+  static const int v = [] { const char* e = getenv("MNISTX_LENET_BWD_IMGS"); return (e && e[0] == '2') ? 2 : 1; }();
+  return v;
+}
+
 }  // namespace
+
+int lenet_c2dgrad_c1wgrad_grid() {
+  return lenet_bwd_imgs() == 2 ? resident_grid<lenet_c2dgrad_c1wgrad_k<2>>()
+                               : resident_grid<lenet_c2dgrad_c1wgrad_k<1>>();
+}
+
+hipError_t lenet_c2dgrad_c1wgrad(const XSrc& x, const bf16_t* dP2, const uint8_t* arg2, const bf16_t* w2,
+                                 const uint8_t* arg1, int B, float* slab, int grid, hipStream_t st) {
+  if (lenet_bwd_imgs() == 2)
+    hipLaunchKernelGGL((lenet_c2dgrad_c1wgrad_k<2>), dim3(grid), dim3(NTH), 0, st, x, dP2, arg2, w2, arg1, B, slab);
+  else
+    hipLaunchKernelGGL((lenet_c2dgrad_c1wgrad_k<1>), dim3(grid), dim3(NTH), 0, st, x, dP2, arg2, w2, arg1, B, slab);
+  return hipGetLastError();
+}
 
 int convpool_config(int cin, int cout, int ks, int pad, int h, int w) {
   if (ks != 5) return -1;

@@ -81,6 +81,12 @@ hipError_t convpool_wgrad(int cfg, const XSrc& x, const bf16_t* dP, const uint8_
 int convpool_has_dgrad(int cfg);
 hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int B, bf16_t* dx,
                           int grid_cap, hipStream_t st);
+// LeNet-5 conv2 data gradient fused into conv1's weight gradient (dP1 never in HBM):
+// slab = convpool_wgrad(cfg 0)'s layout, one [KM][8] partial per block (grid <= the
+// resident grid lenet_c2dgrad_c1wgrad_grid())
+int lenet_c2dgrad_c1wgrad_grid();
+hipError_t lenet_c2dgrad_c1wgrad(const XSrc& x, const bf16_t* dP2, const uint8_t* arg2, const bf16_t* w2,
+                                 const uint8_t* arg1, int B, float* slab, int grid, hipStream_t st);
 
 // ---- misc.hip
 hipError_t perm_positions(int64_t* out, int64_t start, int n, int64_t N, uint32_t seed, int h, hipStream_t st);

@@ -162,10 +162,22 @@ class ConvPoolLayer(_Layer):
         kernels().convpool_fwd(self.x, self.fp.bf16_view(self.wname), self.fp.param_view(self.bname),
                                self.spec.cout, self.out, self.arg, nb, *self._geo(), **self._src())
 
+    # (dY of the next conv+pool layer, that layer): its data gradient is computed
+    # inside this layer's weight-gradient kernel (HipNet.fuse_c2d_c1w)
+    fused_dgrad: Optional[tuple] = None
+    fused_grid = 0
+    skip_dgrad = False
+
     def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor, red: Optional[list] = None) -> None:
         K = kernels()
-        grid = min(self.grid, max(1, (nb + 3) // 4))
-        K.convpool_wgrad(self.x, dy, self.arg, slab, grid, nb, *self._geo(), **self._src())
+        if self.fused_dgrad is not None:
+            dy2, l1 = self.fused_dgrad
+            grid = min(self.fused_grid, max(1, nb))
+            K.lenet_c2dgrad_c1wgrad(self.x, dy2, l1.arg, self.fp.bf16_view(l1.wname), self.arg, slab, grid, nb,
+                                    **self._src())
+        else:
+            grid = min(self.grid, max(1, (nb + 3) // 4))
+            K.convpool_wgrad(self.x, dy, self.arg, slab, grid, nb, *self._geo(), **self._src())
         G, Ip, I, brow = self.red
         _reduce(red, slab, (grid, self.KM, self.Cp, G, Ip, I, self.spec.cout, brow),
                 self.fp.grad_view(self.wname), self.fp.grad_view(self.bname))
@@ -173,7 +185,7 @@ class ConvPoolLayer(_Layer):
     dgrad_cap = 0   # persistent dgrad blocks (0: one resident wave); set when backward overlaps
 
     def bwd_data(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor]) -> None:
-        if dx is not None:
+        if dx is not None and not self.skip_dgrad:
             kernels().convpool_dgrad(dy, self.arg, self.fp.bf16_view(self.wname), dx, nb, *self._geo(),
                                      grid_cap=self.dgrad_cap)
 
@@ -449,6 +461,25 @@ class HipNet:
                                  and all(l.Dp % 8 == 0 and l.Np % 8 == 0 for l in self.layers[self.head:]))
         self._group_S: Optional[list] = None
         self._head_grads = False                   # loss_and_grad already produced the head's dgrads
+        # LeNet-5: conv2's data gradient inside conv1's weight-gradient kernel
+        # (convpool.hip lenet_c2dgrad_c1wgrad_k), so dP1 never goes to HBM.  Opt-in
+        # (MNISTX_FUSE_C2D_C1W=1): at B=65536 it measures 290-309 us against 140 + 150 us
+        # for the two kernels it replaces (profiles/r2/fused_c2d_c1w.md) -- the pair is
+        # bound by LDS/VALU latency at 3 waves/SIMD, not by the 400 MB it saves.
+        self.fuse_c2d_c1w = self._find_c2d_c1w() and not self.overlap and \
+            os.environ.get("MNISTX_FUSE_C2D_C1W", "0") == "1"
+        if self.fuse_c2d_c1w:
+            l0, l1 = self.layers[0], self.layers[1]
+            l0.fused_grid = min(l0.grid, kernels().lenet_c2dgrad_c1wgrad_grid())
+            l0.fused_dgrad = (self.dbuf[2], l1)   # conv2's incoming gradient + its layer
+            l1.skip_dgrad = True
+
+    def _find_c2d_c1w(self) -> bool:
+        if self.device.type != "cuda" or len(self.layers) < 2:
+            return False
+        l0, l1 = self.layers[0], self.layers[1]
+        return (isinstance(l0, ConvPoolLayer) and isinstance(l1, ConvPoolLayer) and l0.cfg == 0 and l1.cfg == 1
+                and l1.x is l0.out)
 
     def _find_head(self) -> Optional[int]:
         """LeNet-5's fc3 -> fc4 -> fc5 tail (400 -> 120 -> 84 -> 10 with ReLUs on the

@@ -181,3 +181,34 @@ def test_lrn_pool_fusion_bitwise(dev, K):
         out.append((net.logits.clone(), net.fp.grads.clone()))
     assert torch.equal(out[0][0], out[1][0])
     assert torch.equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("B", [77, 512])
+def test_lenet_fused_c2dgrad_c1wgrad(dev, K, B, monkeypatch):
+    """conv2 dgrad inside conv1's weight-gradient kernel (dP1 never in HBM) vs the
+    two-kernel path: conv2 grads bitwise, conv1 grads to fp32 reassociation noise;
+    the fused kernel is bitwise reproducible run to run."""
+    spec = get_model("lenet5", 1)
+    init = torch_ref.init_params(spec, seed=3)
+    x = (torch.rand(B, 28, 28, 1, device=dev) - 0.5).to(torch.bfloat16)
+    y = torch.randint(0, 10, (B,), device=dev, dtype=torch.int32)
+
+    def grads(fuse: str):
+        monkeypatch.setenv("MNISTX_FUSE_C2D_C1W", fuse)   # opt-in path (default off)
+        net = HipNet(spec, B, dev, init, OptConfig(lr0=0.05))
+        assert net.fuse_c2d_c1w == (fuse == "1")
+        net.x0.copy_(x)
+        net.labels.copy_(y)
+        net.forward(defer_head=True)
+        net.loss_and_grad()
+        net.backward()
+        torch.cuda.synchronize()
+        return {n: net.fp.grad_view(n).clone() for n in init}
+
+    ref, fused, again = grads("0"), grads("1"), grads("1")
+    for n in init:
+        assert torch.equal(fused[n], again[n]), f"{n}: fused kernel not reproducible"
+        if n.startswith("conv1/"):
+            assert rel_err(fused[n], ref[n]) < 1e-5, n
+        else:
+            assert torch.equal(fused[n], ref[n]), n

@@ -37,6 +37,8 @@ def parse():
     ap.add_argument("--model", default="lenet5", choices=sorted(MODEL_LABEL))
     ap.add_argument("--batch", type=int, default=65536, help="per-GPU batch (BASELINE stress config: 65536)")
     ap.add_argument("--in_channels", type=int, default=1)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
+                    help="HIP compute precision: bf16 (headline) | fp32 (the reference's tf.float32, fp32 MFMA)")
     ap.add_argument("--impl", default="hip", choices=["hip", "torch"],
                     help="hip = our CDNA4 kernels; torch = PyTorch-ROCm baseline (MIOpen/hipBLASLt, bf16 autocast)")
     ap.add_argument("--bucket_mb", type=float, default=0.125,
@@ -172,7 +174,10 @@ def main() -> int:
     init = init_params(spec, seed=args.seed)
     opt = OptConfig(lr0=args.lr, decay_rate=0.1, decay_steps=0, momentum=0.9 if args.optimizer != "sgd" else 0.0,
                     nesterov=args.optimizer == "nesterov", use_momentum=args.optimizer != "sgd", ema_max=0.9999)
-    if args.impl == "hip":
+    if args.impl == "hip" and args.precision == "fp32":
+        from distributed_tensorflow_ibm_mnist_amd.runtime.executor_f32 import HipNetF32
+        net = HipNetF32(spec, args.batch, dev, init, opt)
+    elif args.impl == "hip":
         from distributed_tensorflow_ibm_mnist_amd.runtime.executor import HipNet
         net = HipNet(spec, args.batch, dev, init, opt,
                      overlap_backward={"none": False, "dense": "dense", "all": True}[args.overlap])
@@ -268,7 +273,7 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": args.precision if args.impl == "hip" else "bf16",
             "data": "synthetic 28x28x1 (on-device generated MNIST-like glyphs), random-init weights",
             "config": {
                 "model": MODEL_LABEL[args.model],

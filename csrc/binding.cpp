@@ -678,6 +678,170 @@ void convpool_dgrad(Tensor dP, Tensor arg, Tensor w, Tensor dx, int64_t B, int64
          "convpool_dgrad");
 }
 
+// ---------------------------------------------------------------- fp32 (reference precision) path
+const float* Fo(const optional<Tensor>& t, int64_t need, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  check(*t, at::kFloat, need, name);
+  return P<const float>(*t);
+}
+
+void f32_dense_fwd(Tensor x, Tensor w, Tensor y, int64_t M, int64_t N, int64_t K, int64_t ldy, optional<Tensor> bias,
+                   bool relu) {
+  check(x, at::kFloat, M * K, "x");
+  check(w, at::kFloat, K * N, "w");
+  TORCH_CHECK(ldy >= N, "ldy");
+  check(y, at::kFloat, span(M, ldy, N), "y");
+  hip_ok(mnistx::f32_dense_fwd(P<const float>(x), P<const float>(w), (int)M, (int)N, (int)K, Fo(bias, N, "bias"),
+                               (int)N, relu ? 1 : 0, P<float>(y), (int)ldy, cur_stream()),
+         "f32_dense_fwd");
+}
+
+void f32_dense_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t M, int64_t Din, int64_t Dout, optional<Tensor> mask) {
+  check(dy, at::kFloat, M * Dout, "dy");
+  check(w, at::kFloat, Din * Dout, "w");
+  check(dx, at::kFloat, M * Din, "dx");
+  hip_ok(mnistx::f32_dense_dgrad(P<const float>(dy), P<const float>(w), (int)M, (int)Din, (int)Dout,
+                                 Fo(mask, M * Din, "mask"), P<float>(dx), cur_stream()),
+         "f32_dense_dgrad");
+}
+
+void f32_dense_wgrad(Tensor x, Tensor dy, Tensor slab, int64_t B, int64_t Din, int64_t Dout, int64_t splits) {
+  check(x, at::kFloat, B * Din, "x");
+  check(dy, at::kFloat, B * Dout, "dy");
+  TORCH_CHECK(splits >= 1 && splits <= 65535, "splits");
+  check(slab, at::kFloat, splits * (Din + 1) * Dout, "slab");
+  hip_ok(mnistx::f32_dense_wgrad(P<const float>(x), P<const float>(dy), (int)B, (int)Din, (int)Dout, (int)splits,
+                                 P<float>(slab), cur_stream()),
+         "f32_dense_wgrad");
+}
+
+void f32_conv_fwd(Tensor x, Tensor w, Tensor y, int64_t Nb, int64_t H, int64_t W, int64_t C, int64_t OH, int64_t OW,
+                  int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t Cout, optional<Tensor> bias, bool relu) {
+  check(x, at::kFloat, Nb * H * W * C, "x");
+  check(w, at::kFloat, KH * KW * C * Cout, "w");
+  check(y, at::kFloat, Nb * OH * OW * Cout, "y");
+  hip_ok(mnistx::f32_conv_fwd(P<const float>(x), P<const float>(w), (int)Nb, (int)H, (int)W, (int)C, (int)OH,
+                              (int)OW, (int)KH, (int)KW, (int)ph, (int)pw, (int)Cout, Fo(bias, Cout, "bias"),
+                              relu ? 1 : 0, P<float>(y), cur_stream()),
+         "f32_conv_fwd");
+}
+
+void f32_conv_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t Nb, int64_t OH, int64_t OW, int64_t Cout, int64_t H,
+                    int64_t W, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t Cin, optional<Tensor> mask) {
+  check(dy, at::kFloat, Nb * OH * OW * Cout, "dy");
+  check(w, at::kFloat, KH * KW * Cin * Cout, "w");
+  check(dx, at::kFloat, Nb * H * W * Cin, "dx");
+  hip_ok(mnistx::f32_conv_dgrad(P<const float>(dy), P<const float>(w), (int)Nb, (int)OH, (int)OW, (int)Cout, (int)H,
+                                (int)W, (int)KH, (int)KW, (int)ph, (int)pw, (int)Cin,
+                                Fo(mask, Nb * H * W * Cin, "mask"), P<float>(dx), cur_stream()),
+         "f32_conv_dgrad");
+}
+
+void f32_conv_wgrad(Tensor x, Tensor dy, Tensor slab, int64_t Nb, int64_t H, int64_t W, int64_t C, int64_t OH,
+                    int64_t OW, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t Cout, int64_t splits) {
+  check(x, at::kFloat, Nb * H * W * C, "x");
+  check(dy, at::kFloat, Nb * OH * OW * Cout, "dy");
+  TORCH_CHECK(splits >= 1 && splits <= 65535, "splits");
+  check(slab, at::kFloat, splits * (KH * KW * C + 1) * Cout, "slab");
+  hip_ok(mnistx::f32_conv_wgrad(P<const float>(x), P<const float>(dy), (int)Nb, (int)H, (int)W, (int)C, (int)OH,
+                                (int)OW, (int)KH, (int)KW, (int)ph, (int)pw, (int)Cout, (int)splits, P<float>(slab),
+                                cur_stream()),
+         "f32_conv_wgrad");
+}
+
+void f32_maxpool_fwd(Tensor x, Tensor y, Tensor arg, int64_t Nb, int64_t H, int64_t W, int64_t C) {
+  const int64_t OH = (H + 1) / 2, OW = (W + 1) / 2;
+  check(x, at::kFloat, Nb * H * W * C, "x");
+  check(y, at::kFloat, Nb * OH * OW * C, "y");
+  check(arg, at::kByte, Nb * OH * OW * C, "arg");
+  hip_ok(mnistx::f32_maxpool_fwd(P<const float>(x), (int)Nb, (int)H, (int)W, (int)C, (int)OH, (int)OW, P<float>(y),
+                                 P<uint8_t>(arg), cur_stream()),
+         "f32_maxpool_fwd");
+}
+
+void f32_maxpool_bwd(Tensor dy, Tensor arg, Tensor y, bool relu_mask, Tensor dx, int64_t Nb, int64_t H, int64_t W,
+                     int64_t C) {
+  const int64_t OH = (H + 1) / 2, OW = (W + 1) / 2;
+  check(dy, at::kFloat, Nb * OH * OW * C, "dy");
+  check(arg, at::kByte, Nb * OH * OW * C, "arg");
+  check(y, at::kFloat, Nb * OH * OW * C, "y");
+  check(dx, at::kFloat, Nb * H * W * C, "dx");
+  hip_ok(mnistx::f32_maxpool_bwd(P<const float>(dy), P<const uint8_t>(arg), P<const float>(y), relu_mask ? 1 : 0,
+                                 (int)Nb, (int)H, (int)W, (int)C, (int)OH, (int)OW, P<float>(dx), cur_stream()),
+         "f32_maxpool_bwd");
+}
+
+void f32_lrn_fwd(Tensor x, Tensor y, int64_t P_, int64_t C, int64_t r, double bias, double alpha, double beta) {
+  TORCH_CHECK(C <= 64, "f32 LRN: C <= 64");
+  check(x, at::kFloat, P_ * C, "x");
+  check(y, at::kFloat, P_ * C, "y");
+  hip_ok(mnistx::f32_lrn_fwd(P<const float>(x), P_, (int)C, (int)r, (float)bias, (float)alpha, (float)beta,
+                             P<float>(y), cur_stream()),
+         "f32_lrn_fwd");
+}
+
+void f32_lrn_bwd(Tensor x, Tensor dy, Tensor dx, int64_t P_, int64_t C, int64_t r, double bias, double alpha,
+                 double beta, bool relu_mask) {
+  TORCH_CHECK(C <= 64, "f32 LRN: C <= 64");
+  check(x, at::kFloat, P_ * C, "x");
+  check(dy, at::kFloat, P_ * C, "dy");
+  check(dx, at::kFloat, P_ * C, "dx");
+  hip_ok(mnistx::f32_lrn_bwd(P<const float>(x), P<const float>(dy), P_, (int)C, (int)r, (float)bias, (float)alpha,
+                             (float)beta, relu_mask ? 1 : 0, P<float>(dx), cur_stream()),
+         "f32_lrn_bwd");
+}
+
+void f32_softmax_ce(Tensor logits, int64_t ldl, optional<Tensor> labels, int64_t B, int64_t NC, double scale,
+                    optional<Tensor> dlogits, int64_t ldd, optional<Tensor> stats, optional<Tensor> probs,
+                    optional<Tensor> work) {
+  TORCH_CHECK(ldl >= NC, "ldl < NC");
+  check(logits, at::kFloat, span(B, ldl, NC), "logits");
+  const int32_t* lab = nullptr;
+  if (labels.has_value() && labels->defined()) {
+    check(*labels, at::kInt, B, "labels");
+    lab = P<const int32_t>(*labels);
+  }
+  float* dl = nullptr;
+  if (dlogits.has_value() && dlogits->defined()) {
+    TORCH_CHECK(lab != nullptr && ldd >= NC, "dlogits needs labels and ldd >= NC");
+    check(*dlogits, at::kFloat, B * ldd, "dlogits");
+    dl = P<float>(*dlogits);
+  }
+  float* st = nullptr;
+  if (stats.has_value() && stats->defined()) {
+    check(*stats, at::kFloat, 8, "stats");
+    st = P<float>(*stats);
+  }
+  float* pr = nullptr;
+  if (probs.has_value() && probs->defined()) {
+    check(*probs, at::kFloat, B * NC, "probs");
+    pr = P<float>(*probs);
+  }
+  float* wk = nullptr;
+  if (work.has_value() && work->defined()) {
+    check(*work, at::kFloat, 4 * 1024 + 1, "work");
+    wk = P<float>(*work);
+  }
+  hip_ok(mnistx::f32_softmax_ce(P<const float>(logits), (int)ldl, lab, (int)B, (int)NC, (float)scale, dl, (int)ldd,
+                                st, pr, wk, cur_stream()),
+         "f32_softmax_ce");
+}
+
+void f32_prep_images(Tensor src, Tensor idx, Tensor lab_src, Tensor out, Tensor lab_out, int64_t HW, int64_t Csrc,
+                     int64_t Cdst) {
+  const int64_t B = idx.numel();
+  check(idx, at::kLong, B, "idx");
+  TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kByte && src.is_contiguous(), "src: uint8 GPU tensor");
+  TORCH_CHECK(src.numel() % (HW * Csrc) == 0, "src size");
+  TORCH_CHECK(Csrc == Cdst || Csrc == 1, "channels: equal or 1 -> C replication");
+  check(lab_src, at::kInt, src.numel() / (HW * Csrc), "lab_src");
+  check(out, at::kFloat, B * HW * Cdst, "out");
+  check(lab_out, at::kInt, B, "lab_out");
+  hip_ok(mnistx::f32_prep_images(P<const uint8_t>(src), P<const int64_t>(idx), P<const int32_t>(lab_src), (int)B,
+                                 (int)HW, (int)Csrc, (int)Cdst, P<float>(out), P<int32_t>(lab_out), cur_stream()),
+         "f32_prep_images");
+}
+
 // LeNet-5 conv2 dgrad -> conv1 wgrad (one kernel): x / u8 source of conv1, the pooled
 // gradient + argmax of conv2, conv2's bf16 weights, conv1's argmax bytes
 void lenet_c2dgrad_c1wgrad(Tensor x, Tensor dP2, Tensor arg2, Tensor w2, Tensor arg1, Tensor slab, int64_t grid,
@@ -698,7 +862,21 @@ void lenet_c2dgrad_c1wgrad(Tensor x, Tensor dP2, Tensor arg2, Tensor w2, Tensor 
 }  // namespace
 
 PYBIND11_MODULE(_kernels, m) {
-  m.def("lenet_c2dgrad_c1wgrad", &lenet_c2dgrad_c1wgrad, py::arg("x"), py::arg("dP2"), py::arg("arg2"), py::arg("w2"),
+  m.def("f32_dense_fwd", &f32_dense_fwd);
+  m.def("f32_dense_dgrad", &f32_dense_dgrad);
+  m.def("f32_dense_wgrad", &f32_dense_wgrad);
+  m.def("f32_conv_fwd", &f32_conv_fwd);
+  m.def("f32_conv_dgrad", &f32_conv_dgrad);
+  m.def("f32_conv_wgrad", &f32_conv_wgrad);
+  m.def("f32_maxpool_fwd", &f32_maxpool_fwd);
+  m.def("f32_maxpool_bwd", &f32_maxpool_bwd);
+  m.def("f32_lrn_fwd", &f32_lrn_fwd);
+  m.def("f32_lrn_bwd", &f32_lrn_bwd);
+  m.def("f32_softmax_ce", &f32_softmax_ce, py::arg("logits"), py::arg("ldl"), py::arg("labels"), py::arg("B"),
+        py::arg("NC"), py::arg("scale"), py::arg("dlogits"), py::arg("ldd"), py::arg("stats"), py::arg("probs"),
+        py::arg("work") = py::none());
+  m.def("f32_prep_images", &f32_prep_images);
+  m.def("lenet_c2dgrad_c1wgrad",&lenet_c2dgrad_c1wgrad, py::arg("x"), py::arg("dP2"), py::arg("arg2"), py::arg("w2"),
         py::arg("arg1"), py::arg("slab"), py::arg("grid"), py::arg("B"), py::arg("u8") = py::none(),
         py::arg("idx") = py::none());
   m.def("lenet_c2dgrad_c1wgrad_grid", []() {

@@ -1,0 +1,470 @@
+// Reference-precision (fp32) kernels for gfx950: --precision fp32.
+//
+// The reference trains in fp32 (mnist_input.py:86,107 `dtype = tf.float32`).  The
+// bf16 kernels stay the default; this file is the fp32 execution path of the
+// same model specs:
+//   * one MFMA GEMM engine on v_mfma_f32_16x16x4_f32 (fp32 operands, fp32
+//     accumulate) with operand "loaders" for dense fwd / dgrad / wgrad and the
+//     implicit-GEMM conv fwd / dgrad (flipped filter) / wgrad (im2col^T, split-K
+//     into deterministic fp32 slabs reduced by misc.hip splitk_reduce);
+//   * fp32 2x2/2 SAME max-pool fwd/bwd (argmax byte), LRN fwd/bwd across
+//     channels, softmax-CE with fp32 logit gradients (ce_stats.h partials) and the
+//     u8 -> fp32 batch gather/normalise.
+//
+// GEMM tiling: 64x64 output tile per 256-thread block, four waves in a 2x2 layout,
+// each wave 2x2 16x16 fragments; K staged 16 at a time through LDS stored k-major
+// ([k][m], 68-float rows: a fragment read is 16 consecutive floats per k row),
+// register double-buffered (global -> VGPR for step t+1 while step t computes).
+// v_mfma_f32_16x16x4_f32: A lane l = (row l%16, k l/16), B lane l = (k l/16, col
+// l%16), D lane l = rows 4(l/16)..+3 of col l%16.
+#include "common.h"
+#include "ce_stats.h"
+#include "launchers.h"
+
+namespace mnistx {
+namespace {
+
+constexpr int FBM = 64, FBN = 64, FBK = 16, FNT = 256;
+constexpr int FLD = FBM + 4;   // LDS row stride (floats)
+
+// ---------------------------------------------------------------- loaders
+// get(r, k): operand element at tile row r (m for A, n for B) and reduction index k;
+// zero outside.  KC: consecutive k are contiguous in memory (thread mapping).
+template <bool KC_>
+struct StridedF {
+  static constexpr bool KC = KC_;
+  const float* p;
+  int R, K, ld;
+  int ones_r;  // virtual row of ones (bias-gradient row), -1 = none
+  DEV float get(int r, int k) const {
+    if (k >= K) return 0.f;
+    if (r == ones_r) return 1.f;
+    if (r >= R) return 0.f;
+    return KC ? p[(int64_t)r * ld + k] : p[(int64_t)k * ld + r];
+  }
+};
+
+// conv fwd A: row m = output pixel (n, oh, ow), k = (kh, kw, ci)
+struct Im2colF {
+  static constexpr bool KC = true;
+  const float* x;
+  int H, W, C, OH, OW, KW, ph, pw, M, K;
+  DEV float get(int m, int k) const {
+    if (m >= M || k >= K) return 0.f;
+    const int n = m / (OH * OW), rem = m - n * (OH * OW);
+    const int oh = rem / OW, ow = rem - oh * OW;
+    const int tap = k / C, ci = k - tap * C;
+    const int kh = tap / KW, kw = tap - kh * KW;
+    const int ih = oh - ph + kh, iw = ow - pw + kw;
+    if (ih < 0 || ih >= H || iw < 0 || iw >= W) return 0.f;
+    return x[(((int64_t)n * H + ih) * W + iw) * C + ci];
+  }
+};
+
+// conv wgrad A (im2col^T): row m = (kh, kw, ci) (+ ones row at Mreal), k = output pixel
+struct Im2colTF {
+  static constexpr bool KC = false;
+  const float* x;
+  int H, W, C, OH, OW, KW, ph, pw, P, Mreal;
+  DEV float get(int m, int k) const {
+    if (k >= P) return 0.f;
+    if (m == Mreal) return 1.f;
+    if (m > Mreal) return 0.f;
+    const int n = k / (OH * OW), rem = k - n * (OH * OW);
+    const int oh = rem / OW, ow = rem - oh * OW;
+    const int tap = m / C, ci = m - tap * C;
+    const int kh = tap / KW, kw = tap - kh * KW;
+    const int ih = oh - ph + kh, iw = ow - pw + kw;
+    if (ih < 0 || ih >= H || iw < 0 || iw >= W) return 0.f;
+    return x[(((int64_t)n * H + ih) * W + iw) * C + ci];
+  }
+};
+
+// conv dgrad A: row m = input pixel (n, ih, iw), k = (kh, kw, co): dy[n, ih+ph-kh, iw+pw-kw, co]
+struct DyIm2colF {
+  static constexpr bool KC = true;
+  const float* dy;
+  int H, W, OH, OW, Co, KW, ph, pw, M, K;
+  DEV float get(int m, int k) const {
+    if (m >= M || k >= K) return 0.f;
+    const int n = m / (H * W), rem = m - n * (H * W);
+    const int ih = rem / W, iw = rem - ih * W;
+    const int tap = k / Co, co = k - tap * Co;
+    const int kh = tap / KW, kw = tap - kh * KW;
+    const int oh = ih + ph - kh, ow = iw + pw - kw;
+    if (oh < 0 || oh >= OH || ow < 0 || ow >= OW) return 0.f;
+    return dy[(((int64_t)n * OH + oh) * OW + ow) * Co + co];
+  }
+};
+
+// conv dgrad B: row = ci, k = (kh, kw, co): W[kh][kw][ci][co]
+struct WFlipF {
+  static constexpr bool KC = true;
+  const float* w;
+  int Ci, Co, K;
+  DEV float get(int ci, int k) const {
+    if (ci >= Ci || k >= K) return 0.f;
+    const int tap = k / Co, co = k - tap * Co;
+    return w[((int64_t)tap * Ci + ci) * Co + co];
+  }
+};
+
+struct EpiF {
+  float* out;            // output (mode 0) or slab base (mode 1)
+  int ldc;
+  int mode;              // 0: store, 1: split-K slab [z][M][N]
+  const float* bias;     // mode 0: + bias[n] (n < bias_n)
+  int bias_n;
+  int relu;
+  const float* mask;     // mode 0: keep v where mask[m * ldm + n] > 0 (ReLU backward)
+  int ldm;
+  int64_t slab_stride;
+};
+
+template <class L>
+DEV void stage_load(const L& ld, int r0, int k0, int tid, float (&v)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int r, k;
+    if constexpr (L::KC) {
+      k = tid & 15;
+      r = (tid >> 4) + 16 * i;
+    } else {
+      r = tid & 63;
+      k = (tid >> 6) + 4 * i;
+    }
+    v[i] = ld.get(r0 + r, k0 + k);
+  }
+}
+
+template <class L>
+DEV void stage_store(float* lds, int tid, const float (&v)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int r, k;
+    if constexpr (L::KC) {
+      k = tid & 15;
+      r = (tid >> 4) + 16 * i;
+    } else {
+      r = tid & 63;
+      k = (tid >> 6) + 4 * i;
+    }
+    lds[k * FLD + r] = v[i];
+  }
+}
+
+// C[M,N] = sum_k A(m,k) B(k,n) over this split's K range [z*kc, min(K, (z+1)*kc))
+template <class AL, class BL>
+__global__ __launch_bounds__(FNT) void gemm_f32_k(AL A, BL Bm, int M, int N, int K, int kc, EpiF ep) {
+  __shared__ float As[2][FBK * FLD];
+  __shared__ float Bs[2][FBK * FLD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_n = (N + FBN - 1) / FBN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / tiles_n) * FBM, n0 = (bid % tiles_n) * FBN;
+  const int z = blockIdx.y;
+  const int kb = z * kc, ke = min(K, kb + kc);
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float va[4], vb[4];
+  if (kb < ke) {
+    stage_load(A, m0, kb, tid, va);
+    stage_load(Bm, n0, kb, tid, vb);
+  }
+  int buf = 0;
+  for (int k0 = kb; k0 < ke; k0 += FBK) {
+    stage_store<AL>(As[buf], tid, va);
+    stage_store<BL>(Bs[buf], tid, vb);
+    __syncthreads();
+    if (k0 + FBK < ke) {
+      stage_load(A, m0, k0 + FBK, tid, va);
+      stage_load(Bm, n0, k0 + FBK, tid, vb);
+    }
+    const float* as = As[buf];
+    const float* bs = Bs[buf];
+    const int kr = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int ks = 0; ks < FBK / 4; ++ks) {
+      float a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = as[(4 * ks + kr) * FLD + wm * 32 + i * 16 + cl];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = bs[(4 * ks + kr) * FLD + wn * 32 + j * 16 + cl];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    buf ^= 1;   // the next step writes the other buffer: one barrier per K step
+  }
+  // epilogue: lane holds rows 4(l/16)+r of column l%16 of each fragment
+  const int rg = lane >> 4, cl = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 32 + i * 16 + 4 * rg + r;
+        const int n = n0 + wn * 32 + j * 16 + cl;
+        if (m >= M || n >= N) continue;
+        float v = acc[i][j][r];
+        if (ep.mode == 1) {
+          ep.out[(int64_t)z * ep.slab_stride + (int64_t)m * N + n] = v;
+        } else {
+          if (ep.bias && n < ep.bias_n) v += ep.bias[n];
+          if (ep.relu) v = fmaxf(v, 0.f);
+          if (ep.mask && !(ep.mask[(int64_t)m * ep.ldm + n] > 0.f)) v = 0.f;
+          ep.out[(int64_t)m * ep.ldc + n] = v;
+        }
+      }
+}
+
+template <class AL, class BL>
+hipError_t launch_f32(const AL& A, const BL& Bm, int M, int N, int K, int splits, const EpiF& ep, hipStream_t st) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  splits = splits < 1 ? 1 : splits;
+  int kc = (K + splits - 1) / splits;
+  kc = (kc + FBK - 1) / FBK * FBK;
+  const int tiles = ((M + FBM - 1) / FBM) * ((N + FBN - 1) / FBN);
+  hipLaunchKernelGGL((gemm_f32_k<AL, BL>), dim3(tiles, splits), dim3(FNT), 0, st, A, Bm, M, N, K, kc, ep);
+  return hipGetLastError();
+}
+
+EpiF store_epi(float* out, int ldc, const float* bias, int bias_n, int relu, const float* mask, int ldm) {
+  return EpiF{out, ldc, 0, bias, bias_n, relu, mask, ldm, 0};
+}
+EpiF slab_epi(float* slab, int64_t stride) { return EpiF{slab, 0, 1, nullptr, 0, 0, nullptr, 0, stride}; }
+
+// ---------------------------------------------------------------- max-pool 2x2/2 SAME
+__global__ void maxpool_f32_fwd_k(const float* __restrict__ x, int Nb, int H, int W, int C, int OH, int OW,
+                                  float* __restrict__ y, uint8_t* __restrict__ arg) {
+  const int64_t total = (int64_t)Nb * OH * OW * C;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(t % C);
+    const int64_t pix = t / C;
+    const int ow = (int)(pix % OW);
+    const int oh = (int)((pix / OW) % OH);
+    const int64_t n = pix / ((int64_t)OW * OH);
+    float best = -INFINITY;
+    int bi = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int ih = 2 * oh + (d >> 1), iw = 2 * ow + (d & 1);
+      if (ih < H && iw < W) {
+        const float v = x[((n * H + ih) * W + iw) * C + c];
+        if (v > best) { best = v; bi = d; }   // first maximum wins (TF MaxPool)
+      }
+    }
+    y[t] = best;
+    arg[t] = (uint8_t)bi;
+  }
+}
+
+// dx at the argmax position gets dy; relu_mask: the pooled input was a ReLU output, so
+// its gradient also needs y > 0 (the max of a ReLU window is > 0 iff its winner is)
+__global__ void maxpool_f32_bwd_k(const float* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                  const float* __restrict__ y, int relu_mask, int Nb, int H, int W, int C, int OH,
+                                  int OW, float* __restrict__ dx) {
+  const int64_t total = (int64_t)Nb * H * W * C;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(t % C);
+    const int64_t pix = t / C;
+    const int iw = (int)(pix % W);
+    const int ih = (int)((pix / W) % H);
+    const int64_t n = pix / ((int64_t)W * H);
+    const int oh = ih >> 1, ow = iw >> 1, d = ((ih & 1) << 1) | (iw & 1);
+    const int64_t o = ((n * OH + oh) * OW + ow) * C + c;
+    float g = 0.f;
+    if (arg[o] == d && (!relu_mask || y[o] > 0.f)) g = dy[o];
+    dx[t] = g;
+  }
+}
+
+// ---------------------------------------------------------------- LRN across channels (C <= 64)
+// y = x * (bias + alpha * sum_{|j-c| <= r} x_j^2)^-beta   (tf.nn.local_response_normalization)
+constexpr int LRN_MAXC = 64;
+__global__ void lrn_f32_fwd_k(const float* __restrict__ x, int64_t P, int C, int r, float bias, float alpha,
+                              float beta, float* __restrict__ y) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < P; p += (int64_t)gridDim.x * blockDim.x) {
+    const float* xp = x + p * C;
+    float sq[LRN_MAXC];
+    for (int c = 0; c < C; ++c) sq[c] = xp[c] * xp[c];
+    for (int c = 0; c < C; ++c) {
+      float s = 0.f;
+      for (int j = max(0, c - r); j <= min(C - 1, c + r); ++j) s += sq[j];
+      y[p * C + c] = xp[c] * powf(bias + alpha * s, -beta);
+    }
+  }
+}
+
+// dx_i = dy_i N_i^-b - 2 a b x_i sum_{j: |i-j| <= r} dy_j x_j N_j^(-b-1),  N_j = bias + a sum x^2
+// relu_mask: x is a ReLU output, dx_i = 0 where x_i <= 0
+__global__ void lrn_f32_bwd_k(const float* __restrict__ x, const float* __restrict__ dy, int64_t P, int C, int r,
+                              float bias, float alpha, float beta, int relu_mask, float* __restrict__ dx) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < P; p += (int64_t)gridDim.x * blockDim.x) {
+    const float* xp = x + p * C;
+    const float* gp = dy + p * C;
+    float nrm[LRN_MAXC], t[LRN_MAXC];
+    for (int c = 0; c < C; ++c) {
+      float s = 0.f;
+      for (int j = max(0, c - r); j <= min(C - 1, c + r); ++j) s += xp[j] * xp[j];
+      nrm[c] = bias + alpha * s;
+      t[c] = gp[c] * xp[c] * powf(nrm[c], -beta - 1.f);
+    }
+    for (int c = 0; c < C; ++c) {
+      float s = 0.f;
+      for (int j = max(0, c - r); j <= min(C - 1, c + r); ++j) s += t[j];
+      float g = gp[c] * powf(nrm[c], -beta) - 2.f * alpha * beta * xp[c] * s;
+      if (relu_mask && !(xp[c] > 0.f)) g = 0.f;
+      dx[p * C + c] = g;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- softmax cross-entropy, fp32 gradient
+__global__ __launch_bounds__(256) void softmax_ce_f32_k(const float* __restrict__ logits, int ldl,
+                                                        const int32_t* __restrict__ labels, int B, int NC,
+                                                        float scale, float* __restrict__ dl, int ldd,
+                                                        float* __restrict__ stats, float* __restrict__ probs,
+                                                        float* __restrict__ work) {
+  float loss = 0.f, corr = 0.f, bad = 0.f;
+  for (int row = blockIdx.x * 256 + threadIdx.x; row < B; row += gridDim.x * 256) {
+    const float* l = logits + (int64_t)row * ldl;
+    float mx = -INFINITY;
+    for (int c = 0; c < NC; ++c) mx = fmaxf(mx, l[c]);
+    float se = 0.f;
+    for (int c = 0; c < NC; ++c) se += expf(l[c] - mx);
+    const float inv = 1.f / se;
+    const int lab = labels ? labels[row] : -1;
+    if (labels) {
+      const float ll = l[lab];
+      const float lo = -(ll - mx - logf(se));
+      loss += lo;
+      corr += ll >= mx ? 1.f : 0.f;
+      if (!isfinite(lo)) bad = 1.f;
+    }
+    if (dl)
+      for (int c = 0; c < ldd; ++c)
+        dl[(int64_t)row * ldd + c] = c < NC ? (expf(l[c] - mx) * inv - (c == lab ? 1.f : 0.f)) * scale : 0.f;
+    if (probs)
+      for (int c = 0; c < NC; ++c) probs[(int64_t)row * NC + c] = expf(l[c] - mx) * inv;
+  }
+  if (stats) ce_block_stats<4>(loss, corr, bad, stats, work);
+}
+
+// ---------------------------------------------------------------- u8 batch -> fp32 x/255 - 0.5
+__global__ void prep_images_f32_k(const uint8_t* __restrict__ src, const int64_t* __restrict__ idx,
+                                  const int32_t* __restrict__ lab_src, int B, int HW, int Csrc, int Cdst,
+                                  float* __restrict__ out, int32_t* __restrict__ lab_out) {
+  const int64_t total = (int64_t)B * HW * Cdst;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(t % Cdst);
+    const int64_t pix = t / Cdst;
+    const int b = (int)(pix / HW), q = (int)(pix % HW);
+    const int cs = Csrc == Cdst ? c : 0;   // 1 -> Cdst channel replication
+    out[t] = u8_norm(src[(idx[b] * HW + q) * Csrc + cs]);
+    if (lab_out && t < B) lab_out[t] = lab_src[idx[t]];
+  }
+}
+
+int ew_grid(int64_t n) {
+  const int64_t g = (n + 255) / 256;
+  return (int)(g < 8192 ? (g < 1 ? 1 : g) : 8192);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- host launchers
+hipError_t f32_dense_fwd(const float* x, const float* w, int M, int N, int K, const float* bias, int bias_n, int relu,
+                         float* y, int ldy, hipStream_t st) {
+  return launch_f32(StridedF<true>{x, M, K, K, -1}, StridedF<false>{w, N, K, N, -1}, M, N, K, 1,
+                    store_epi(y, ldy, bias, bias_n, relu, nullptr, 0), st);
+}
+
+hipError_t f32_dense_dgrad(const float* dy, const float* w, int M, int Din, int Dout, const float* mask, float* dx,
+                           hipStream_t st) {
+  // dx[m][i] = sum_o dy[m][o] W[i][o]
+  return launch_f32(StridedF<true>{dy, M, Dout, Dout, -1}, StridedF<true>{w, Din, Dout, Dout, -1}, M, Din, Dout, 1,
+                    store_epi(dx, Din, nullptr, 0, 0, mask, Din), st);
+}
+
+hipError_t f32_dense_wgrad(const float* x, const float* dy, int B, int Din, int Dout, int splits, float* slab,
+                           hipStream_t st) {
+  // slab[z][Din + 1][Dout]: rows < Din = x^T dy, row Din = column sums of dy (bias)
+  return launch_f32(StridedF<false>{x, Din, B, Din, Din}, StridedF<false>{dy, Dout, B, Dout, -1}, Din + 1, Dout, B,
+                    splits, slab_epi(slab, (int64_t)(Din + 1) * Dout), st);
+}
+
+hipError_t f32_conv_fwd(const float* x, const float* w, int Nb, int H, int W, int C, int OH, int OW, int KH, int KW,
+                        int ph, int pw, int Cout, const float* bias, int relu, float* y, hipStream_t st) {
+  const int M = Nb * OH * OW, K = KH * KW * C;
+  return launch_f32(Im2colF{x, H, W, C, OH, OW, KW, ph, pw, M, K}, StridedF<false>{w, Cout, K, Cout, -1}, M, Cout, K,
+                    1, store_epi(y, Cout, bias, Cout, relu, nullptr, 0), st);
+}
+
+hipError_t f32_conv_dgrad(const float* dy, const float* w, int Nb, int OH, int OW, int Cout, int H, int W, int KH,
+                          int KW, int ph, int pw, int Cin, const float* mask, float* dx, hipStream_t st) {
+  const int M = Nb * H * W, K = KH * KW * Cout;
+  return launch_f32(DyIm2colF{dy, H, W, OH, OW, Cout, KW, ph, pw, M, K}, WFlipF{w, Cin, Cout, K}, M, Cin, K, 1,
+                    store_epi(dx, Cin, nullptr, 0, 0, mask, Cin), st);
+}
+
+hipError_t f32_conv_wgrad(const float* x, const float* dy, int Nb, int H, int W, int C, int OH, int OW, int KH,
+                          int KW, int ph, int pw, int Cout, int splits, float* slab, hipStream_t st) {
+  // slab[z][KH*KW*C + 1][Cout], row KH*KW*C = bias
+  const int P = Nb * OH * OW, Mr = KH * KW * C;
+  return launch_f32(Im2colTF{x, H, W, C, OH, OW, KW, ph, pw, P, Mr}, StridedF<false>{dy, Cout, P, Cout, -1}, Mr + 1,
+                    Cout, P, splits, slab_epi(slab, (int64_t)(Mr + 1) * Cout), st);
+}
+
+hipError_t f32_maxpool_fwd(const float* x, int Nb, int H, int W, int C, int OH, int OW, float* y, uint8_t* arg,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(maxpool_f32_fwd_k, dim3(ew_grid((int64_t)Nb * OH * OW * C)), dim3(256), 0, st, x, Nb, H, W, C,
+                     OH, OW, y, arg);
+  return hipGetLastError();
+}
+
+hipError_t f32_maxpool_bwd(const float* dy, const uint8_t* arg, const float* y, int relu_mask, int Nb, int H, int W,
+                           int C, int OH, int OW, float* dx, hipStream_t st) {
+  hipLaunchKernelGGL(maxpool_f32_bwd_k, dim3(ew_grid((int64_t)Nb * H * W * C)), dim3(256), 0, st, dy, arg, y,
+                     relu_mask, Nb, H, W, C, OH, OW, dx);
+  return hipGetLastError();
+}
+
+hipError_t f32_lrn_fwd(const float* x, int64_t P, int C, int r, float bias, float alpha, float beta, float* y,
+                       hipStream_t st) {
+  if (C > LRN_MAXC) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(lrn_f32_fwd_k, dim3(ew_grid(P)), dim3(256), 0, st, x, P, C, r, bias, alpha, beta, y);
+  return hipGetLastError();
+}
+
+hipError_t f32_lrn_bwd(const float* x, const float* dy, int64_t P, int C, int r, float bias, float alpha, float beta,
+                       int relu_mask, float* dx, hipStream_t st) {
+  if (C > LRN_MAXC) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(lrn_f32_bwd_k, dim3(ew_grid(P)), dim3(256), 0, st, x, dy, P, C, r, bias, alpha, beta,
+                     relu_mask, dx);
+  return hipGetLastError();
+}
+
+hipError_t f32_softmax_ce(const float* logits, int ldl, const int32_t* labels, int B, int NC, float scale, float* dl,
+                          int ldd, float* stats, float* probs, float* work, hipStream_t st) {
+  int nb = (B + 255) / 256;
+  nb = nb < 1 ? 1 : (nb > CE_MAXB ? CE_MAXB : nb);
+  hipLaunchKernelGGL(softmax_ce_f32_k, dim3(nb), dim3(256), 0, st, logits, ldl, labels, B, NC, scale, dl, ldd, stats,
+                     probs, work);
+  return hipGetLastError();
+}
+
+hipError_t f32_prep_images(const uint8_t* src, const int64_t* idx, const int32_t* lab_src, int B, int HW, int Csrc,
+                           int Cdst, float* out, int32_t* lab_out, hipStream_t st) {
+  hipLaunchKernelGGL(prep_images_f32_k, dim3(ew_grid((int64_t)B * HW * Cdst)), dim3(256), 0, st, src, idx, lab_src,
+                     B, HW, Csrc, Cdst, out, lab_out);
+  return hipGetLastError();
+}
+
+}  // namespace mnistx

@@ -88,6 +88,32 @@ int lenet_c2dgrad_c1wgrad_grid();
 hipError_t lenet_c2dgrad_c1wgrad(const XSrc& x, const bf16_t* dP2, const uint8_t* arg2, const bf16_t* w2,
                                  const uint8_t* arg1, int B, float* slab, int grid, hipStream_t st);
 
+// ---- f32.hip: reference-precision (fp32) path, v_mfma_f32_16x16x4_f32
+hipError_t f32_dense_fwd(const float* x, const float* w, int M, int N, int K, const float* bias, int bias_n, int relu,
+                         float* y, int ldy, hipStream_t st);
+hipError_t f32_dense_dgrad(const float* dy, const float* w, int M, int Din, int Dout, const float* mask, float* dx,
+                           hipStream_t st);
+hipError_t f32_dense_wgrad(const float* x, const float* dy, int B, int Din, int Dout, int splits, float* slab,
+                           hipStream_t st);
+hipError_t f32_conv_fwd(const float* x, const float* w, int Nb, int H, int W, int C, int OH, int OW, int KH, int KW,
+                        int ph, int pw, int Cout, const float* bias, int relu, float* y, hipStream_t st);
+hipError_t f32_conv_dgrad(const float* dy, const float* w, int Nb, int OH, int OW, int Cout, int H, int W, int KH,
+                          int KW, int ph, int pw, int Cin, const float* mask, float* dx, hipStream_t st);
+hipError_t f32_conv_wgrad(const float* x, const float* dy, int Nb, int H, int W, int C, int OH, int OW, int KH,
+                          int KW, int ph, int pw, int Cout, int splits, float* slab, hipStream_t st);
+hipError_t f32_maxpool_fwd(const float* x, int Nb, int H, int W, int C, int OH, int OW, float* y, uint8_t* arg,
+                           hipStream_t st);
+hipError_t f32_maxpool_bwd(const float* dy, const uint8_t* arg, const float* y, int relu_mask, int Nb, int H, int W,
+                           int C, int OH, int OW, float* dx, hipStream_t st);
+hipError_t f32_lrn_fwd(const float* x, int64_t P, int C, int r, float bias, float alpha, float beta, float* y,
+                       hipStream_t st);
+hipError_t f32_lrn_bwd(const float* x, const float* dy, int64_t P, int C, int r, float bias, float alpha, float beta,
+                       int relu_mask, float* dx, hipStream_t st);
+hipError_t f32_softmax_ce(const float* logits, int ldl, const int32_t* labels, int B, int NC, float scale, float* dl,
+                          int ldd, float* stats, float* probs, float* work, hipStream_t st);
+hipError_t f32_prep_images(const uint8_t* src, const int64_t* idx, const int32_t* lab_src, int B, int HW, int Csrc,
+                           int Cdst, float* out, int32_t* lab_out, hipStream_t st);
+
 // ---- misc.hip
 hipError_t perm_positions(int64_t* out, int64_t start, int n, int64_t N, uint32_t seed, int h, hipStream_t st);
 // 28x28x1 batch gather + normalise with the Feistel epoch shuffle fused in (rows are

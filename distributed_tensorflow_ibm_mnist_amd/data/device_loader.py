@@ -29,7 +29,10 @@ def gather_into(ds: "DeviceDataset", idx: torch.Tensor, out_images: torch.Tensor
     """K10 on the GPU; a torch equivalent on CPU (the gloo test path)."""
     cdst = int(out_images.shape[-1])
     if ds.device.type == "cuda":
-        kernels().prep_images(ds.images, idx, ds.labels, out_images, out_labels, ds.hw, ds.channels, cdst)
+        if out_images.dtype == torch.float32:     # --precision fp32 input buffer
+            kernels().f32_prep_images(ds.images, idx, ds.labels, out_images, out_labels, ds.hw, ds.channels, cdst)
+        else:
+            kernels().prep_images(ds.images, idx, ds.labels, out_images, out_labels, ds.hw, ds.channels, cdst)
         return
     nb = idx.numel()
     x = ds.images[idx].float().view(nb, ds.hw, ds.channels) * (1.0 / 255.0) - 0.5
@@ -140,7 +143,7 @@ class DeviceLoader:
         start = self.pos + (self.rank * self.B if self.shard else 0)
         N = len(self.ds)
         if (self.shuffle and self.idx_out is None and self.ds.device.type == "cuda" and self.ds.hw == 784
-                and self.ds.channels == 1 and self.cdst == 1):
+                and self.ds.channels == 1 and self.cdst == 1 and self.out_images.dtype == torch.bfloat16):
             # one kernel: Feistel row + gather + normalise (+ labels)
             kernels().prep_images_perm(self.ds.images, self.ds.labels, self.out_images, self.out_labels, nb,
                                        int(start), int(self.seed), _half_bits(N))

@@ -1,0 +1,274 @@
+"""Reference-precision execution plan: fp32 activations, fp32 MFMA (``--precision fp32``).
+
+The reference trains in fp32 (``mnist_input.py:86,107``: ``dtype = tf.float32``).
+``HipNet`` (the default) runs bf16 activations / bf16 MFMA operands with fp32
+accumulation; ``HipNetF32`` runs the same model specs with every activation,
+weight operand and gradient in fp32 on the ``csrc/kernels/f32.hip`` kernels
+(``v_mfma_f32_16x16x4_f32`` GEMM engine with implicit-GEMM conv loaders, fp32
+max-pool / LRN / softmax-CE).  Optimizer, EMA, LR schedule, loss EMA and the
+deterministic split-K reduce are the shared K9 / misc.hip kernels, so the
+checkpoint layout, hooks and data-parallel buckets are identical.
+
+Layer semantics follow the reference graph exactly (no fusion): conv + bias +
+ReLU (``mnist_input.py:142-145``), 2x2/2 SAME max-pool (first maximum wins),
+LRN across channels, dense + bias (+ ReLU).  ReLU backward masks are folded
+into the producer of each gradient, as in the bf16 plan.
+"""
+from __future__ import annotations
+
+import math
+from typing import Callable, Dict, List, Optional
+
+import torch
+
+from ..models.spec import Conv, Dense, LRN, MaxPool, ModelSpec
+from ..ops import functional as Fk
+from ..ops._ext import kernels
+from .executor import HipNet
+from .params import FlatParams, OptConfig
+
+
+def _f32(*shape, device) -> torch.Tensor:
+    return torch.zeros(*shape, dtype=torch.float32, device=device)
+
+
+def wgrad_splits(M: int, N: int, K: int, target: int = 2048, min_k: int = 256, cap: int = 1024) -> int:
+    """Split-K factor of an fp32 weight-gradient GEMM (64x64 tiles): fill the CUs
+    while keeping every split >= min_k reduction elements."""
+    tiles = math.ceil(M / 64) * math.ceil(N / 64)
+    return int(max(1, min(math.ceil(target / tiles), max(1, K // min_k), cap)))
+
+
+class _L:
+    has_params = False
+    idx = -1
+
+    def fwd(self, nb: int) -> None: ...
+
+    def bwd_weight(self, nb: int, dy: torch.Tensor) -> None: ...
+
+    def bwd_data(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor]) -> None: ...
+
+
+class ConvF(_L):
+    has_params = True
+
+    def __init__(self, spec: Conv, x: torch.Tensor, in_relu: bool, fp: FlatParams, B: int, dev):
+        self.spec, self.name, self.x, self.in_relu, self.fp = spec, spec.name, x, in_relu, fp
+        _, self.H, self.W, self.C = x.shape
+        self.OH, self.OW = Fk.conv_out_hw(self.H, self.W, spec.kh, spec.kw, spec.padding)
+        self.ph, self.pw = Fk.conv_pads(spec.kh, spec.kw, spec.padding)
+        self.out = _f32(B, self.OH, self.OW, spec.cout, device=dev)
+        self.wname, self.bname = f"{spec.name}/weights", f"{spec.name}/biases"
+        self.M = spec.kh * spec.kw * self.C + 1
+        self.splits = wgrad_splits(self.M, spec.cout, B * self.OH * self.OW)
+        self.slab = _f32(self.splits * self.M * spec.cout, device=dev)
+
+    def fwd(self, nb: int) -> None:
+        s = self.spec
+        kernels().f32_conv_fwd(self.x, self.fp.param_view(self.wname), self.out, nb, self.H, self.W, self.C, self.OH,
+                               self.OW, s.kh, s.kw, self.ph, self.pw, s.cout, self.fp.param_view(self.bname), s.relu)
+
+    def bwd_weight(self, nb: int, dy: torch.Tensor) -> None:
+        s, K = self.spec, kernels()
+        S = min(self.splits, wgrad_splits(self.M, s.cout, nb * self.OH * self.OW))
+        K.f32_conv_wgrad(self.x, dy, self.slab, nb, self.H, self.W, self.C, self.OH, self.OW, s.kh, s.kw, self.ph,
+                         self.pw, s.cout, S)
+        K.splitk_reduce(self.slab, S, self.M, s.cout, s.kh * s.kw, self.C, self.C, s.cout, s.kh * s.kw * self.C,
+                        self.fp.grad_view(self.wname), self.fp.grad_view(self.bname), 1.0)
+
+    def bwd_data(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor]) -> None:
+        if dx is None:
+            return
+        s = self.spec
+        kernels().f32_conv_dgrad(dy, self.fp.param_view(self.wname), dx, nb, self.OH, self.OW, s.cout, self.H, self.W,
+                                 s.kh, s.kw, self.ph, self.pw, self.C, self.x if self.in_relu else None)
+
+
+class PoolF(_L):
+    def __init__(self, spec: MaxPool, x: torch.Tensor, in_relu: bool, B: int, dev):
+        assert spec.k == 2 and spec.s == 2 and spec.padding == "SAME", "2x2/2 SAME pooling only"
+        self.spec, self.name, self.x, self.in_relu = spec, spec.name, x, in_relu
+        _, self.H, self.W, self.C = x.shape
+        self.out = _f32(B, (self.H + 1) // 2, (self.W + 1) // 2, self.C, device=dev)
+        self.arg = torch.zeros(self.out.shape, dtype=torch.uint8, device=dev)
+
+    def fwd(self, nb: int) -> None:
+        kernels().f32_maxpool_fwd(self.x, self.out, self.arg, nb, self.H, self.W, self.C)
+
+    def bwd_data(self, nb: int, dy, dx) -> None:
+        if dx is not None:
+            kernels().f32_maxpool_bwd(dy, self.arg, self.out, self.in_relu, dx, nb, self.H, self.W, self.C)
+
+
+class LRNF(_L):
+    def __init__(self, spec: LRN, x: torch.Tensor, in_relu: bool, B: int, dev):
+        self.spec, self.name, self.x, self.in_relu = spec, spec.name, x, in_relu
+        self.C = x.shape[-1]
+        self.out = torch.zeros_like(x)
+
+    def _p(self, nb: int) -> int:
+        return nb * (self.x[0].numel() // self.C)
+
+    def fwd(self, nb: int) -> None:
+        s = self.spec
+        kernels().f32_lrn_fwd(self.x, self.out, self._p(nb), self.C, s.depth_radius, s.bias, s.alpha, s.beta)
+
+    def bwd_data(self, nb: int, dy, dx) -> None:
+        if dx is not None:
+            s = self.spec
+            kernels().f32_lrn_bwd(self.x, dy, dx, self._p(nb), self.C, s.depth_radius, s.bias, s.alpha, s.beta,
+                                  self.in_relu)
+
+
+class DenseF(_L):
+    has_params = True
+
+    def __init__(self, spec: Dense, x: torch.Tensor, in_relu: bool, fp: FlatParams, B: int, dev):
+        self.spec, self.name, self.in_relu, self.fp = spec, spec.name, in_relu, fp
+        self.x = x.view(B, -1)
+        assert self.x.shape[1] == spec.din, f"{spec.name}: flatten {self.x.shape[1]} != din {spec.din}"
+        self.out = _f32(B, spec.dout, device=dev)
+        self.wname, self.bname = f"{spec.name}/weights", f"{spec.name}/biases"
+        self.splits = wgrad_splits(spec.din + 1, spec.dout, B)
+        self.slab = _f32(self.splits * (spec.din + 1) * spec.dout, device=dev)
+
+    def fwd(self, nb: int) -> None:
+        s = self.spec
+        kernels().f32_dense_fwd(self.x, self.fp.param_view(self.wname), self.out, nb, s.dout, s.din, s.dout,
+                                self.fp.param_view(self.bname), s.relu)
+
+    def bwd_weight(self, nb: int, dy: torch.Tensor) -> None:
+        s, K = self.spec, kernels()
+        S = min(self.splits, wgrad_splits(s.din + 1, s.dout, nb))
+        K.f32_dense_wgrad(self.x, dy.view(-1, s.dout), self.slab, nb, s.din, s.dout, S)
+        K.splitk_reduce(self.slab, S, s.din + 1, s.dout, 1, s.din, s.din, s.dout, s.din,
+                        self.fp.grad_view(self.wname), self.fp.grad_view(self.bname), 1.0)
+
+    def bwd_data(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor]) -> None:
+        if dx is not None:
+            s = self.spec
+            kernels().f32_dense_dgrad(dy.view(-1, s.dout), self.fp.param_view(self.wname), dx.view(-1, s.din), nb,
+                                      s.din, s.dout, self.x if self.in_relu else None)
+
+
+class HipNetF32:
+    """One fp32 model replica on one GPU: the HipNet interface (forward /
+    loss_and_grad / backward / update, eval, probs, stats) on fp32 kernels."""
+
+    precision = "fp32"
+
+    def __init__(self, spec: ModelSpec, batch: int, device, init: Dict[str, torch.Tensor],
+                 opt: Optional[OptConfig] = None):
+        dev = torch.device(device)
+        assert dev.type == "cuda", "HipNetF32 runs the HIP kernels (use --impl=torch on CPU)"
+        self.spec, self.B, self.device = spec, batch, dev
+        self.opt = opt or OptConfig()
+        specs = []
+        for L in spec.weights():
+            shp = (L.kh, L.kw, L.cin, L.cout) if isinstance(L, Conv) else (L.din, L.dout)
+            specs.append((f"{L.name}/weights", shp, L.wd))
+            specs.append((f"{L.name}/biases", (L.cout if isinstance(L, Conv) else L.dout,), None))
+        self.fp = FlatParams.build(specs, init, dev, bf16_copies=False)   # kernels read the fp32 masters
+        H, W = spec.input_hw
+        self.x0 = _f32(batch, H, W, spec.in_channels, device=dev)
+        self.labels = torch.zeros(batch, dtype=torch.int32, device=dev)
+        self.layers: List[_L] = []
+        x, in_relu = self.x0, False
+        for i, L in enumerate(spec.layers):
+            if isinstance(L, Conv):
+                lay = ConvF(L, x, in_relu, self.fp, batch, dev)
+                in_relu = L.relu
+            elif isinstance(L, MaxPool):
+                lay = PoolF(L, x, in_relu, batch, dev)
+                in_relu = False
+            elif isinstance(L, LRN):
+                lay = LRNF(L, x, in_relu, batch, dev)
+                in_relu = False
+            elif isinstance(L, Dense):
+                lay = DenseF(L, x, in_relu, self.fp, batch, dev)
+                in_relu = L.relu
+            else:
+                raise TypeError(L)
+            lay.idx = i
+            self.layers.append(lay)
+            x = lay.out
+        assert isinstance(self.layers[-1], DenseF), "model must end in a Dense"
+        self.logits = self.layers[-1].out
+        self.n_classes = spec.num_classes
+        self.dlogits = torch.zeros_like(self.logits)
+        self.dbuf: List[Optional[torch.Tensor]] = [None] + [torch.zeros_like(l.out) for l in self.layers[:-1]]
+        self.stats = _f32(8, device=dev)
+        self.eval_stats = _f32(8, device=dev)
+        self.ce_work = _f32(4 * 1024 + 1, device=dev)
+        names = [e.name for e in self.fp.wd_entries]
+        self.loss_names = [n.replace("/weights", "/weight_loss") for n in names] + ["cross_entropy", "total_loss"]
+        self.loss_ema = _f32(3 * len(self.loss_names), device=dev)
+        self.grad_ready_hooks: List[Callable[[int], None]] = []
+        self.hook_layers: Optional[set] = None
+        self.idx_buf: Optional[torch.Tensor] = None
+        self.head = None
+
+    # shared with the bf16 plan: K9 update + finalisation, stats readback
+    update = HipNet.update
+    finalize = HipNet.finalize
+    read_stats = HipNet.read_stats
+
+    def bind_u8_input(self, images_u8: torch.Tensor) -> bool:
+        return False
+
+    def forward(self, nb: Optional[int] = None, from_x0: bool = False, defer_head: bool = False) -> torch.Tensor:
+        nb = self.B if nb is None else nb
+        for lay in self.layers:
+            lay.fwd(nb)
+        return self.logits
+
+    def loss_and_grad(self, nb: Optional[int] = None, scale: Optional[float] = None) -> None:
+        nb = self.B if nb is None else nb
+        kernels().f32_softmax_ce(self.logits, self.logits.shape[1], self.labels, nb, self.n_classes,
+                                 (1.0 / nb) if scale is None else scale, self.dlogits, self.logits.shape[1],
+                                 self.stats, None, self.ce_work)
+
+    def backward(self, nb: Optional[int] = None) -> None:
+        nb = self.B if nb is None else nb
+        dy = self.dlogits
+        for i in range(len(self.layers) - 1, -1, -1):
+            lay = self.layers[i]
+            if lay.has_params:
+                lay.bwd_weight(nb, dy)
+                if self.hook_layers is None or lay.idx in self.hook_layers:
+                    for h in self.grad_ready_hooks:
+                        h(lay.idx)
+            dx = self.dbuf[i]
+            lay.bwd_data(nb, dy, dx)
+            dy = dx
+
+    def train_step(self, grad_scale: float = 1.0) -> None:
+        self.forward()
+        self.loss_and_grad()
+        self.backward()
+        self.update(grad_scale)
+
+    def eval_batch(self, nb: int, stats: Optional[torch.Tensor] = None) -> torch.Tensor:
+        st = self.eval_stats if stats is None else stats
+        self.forward(nb)
+        kernels().f32_softmax_ce(self.logits, self.logits.shape[1], self.labels, nb, self.n_classes, 1.0, None,
+                                 self.logits.shape[1], st, None, self.ce_work)
+        return st
+
+    def probs(self, nb: int) -> torch.Tensor:
+        self.forward(nb)
+        out = torch.empty(nb, self.n_classes, dtype=torch.float32, device=self.device)
+        kernels().f32_softmax_ce(self.logits, self.logits.shape[1], None, nb, self.n_classes, 1.0, None,
+                                 self.logits.shape[1], None, out, None)
+        return out
+
+    def activation(self, layer_name: str) -> torch.Tensor:
+        for lay in self.layers:
+            if lay.name == layer_name:
+                return lay.out
+        raise KeyError(layer_name)
+
+    def layer_activation(self, layer_name: str, n: int) -> torch.Tensor:
+        """``<layer>/<layer>:0`` (main.py:97-100): unfused, so the conv ReLU output itself."""
+        return self.activation(layer_name)[:max(1, min(n, self.B))]

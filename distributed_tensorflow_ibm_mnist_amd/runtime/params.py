@@ -130,9 +130,10 @@ class FlatParams:
     @classmethod
     def build(cls, specs: Sequence[Tuple[str, Tuple[int, ...], Optional[float]]],
               init: Dict[str, torch.Tensor], device, pads: Optional[Dict[str, Tuple[int, int]]] = None,
-              bias_names_have_no_bf16: bool = True) -> "FlatParams":
+              bias_names_have_no_bf16: bool = True, bf16_copies: bool = True) -> "FlatParams":
         """specs: (name, shape, wd) in creation order.  pads: name -> (I_pad, J_pad)
-        for tensors that get a bf16 copy (weights; 4-D = [KH,KW,I,J], 2-D = [I,J])."""
+        for tensors that get a bf16 copy (weights; 4-D = [KH,KW,I,J], 2-D = [I,J]).
+        bf16_copies=False: no bf16 copies at all (the fp32 plan reads the masters)."""
         pads = pads or {}
         entries: List[Entry] = []
         off = 0
@@ -147,7 +148,7 @@ class FlatParams:
                 G, I, J = 1, shape[0], shape[1]
             else:
                 G, I, J = 1, 1, shape[0]
-            has_bf = len(shape) >= 2 or not bias_names_have_no_bf16
+            has_bf = bf16_copies and (len(shape) >= 2 or not bias_names_have_no_bf16)
             Ip, Jp = pads.get(name, (I, J))
             e = Entry(name, shape, wd, off, n, G, I, J, Ip, Jp, bf_off if has_bf else -1,
                       l2i if (wd is not None and len(shape) >= 2) else -1)

@@ -22,8 +22,12 @@ from ..parallel.dp import DataParallel
 from ..runtime.params import FlatParams, OptConfig
 
 
-def build_net(impl: str, spec: ModelSpec, batch: int, device, init, opt: OptConfig):
+def build_net(impl: str, spec: ModelSpec, batch: int, device, init, opt: OptConfig, precision: str = "bf16"):
+    if impl == "hip" and precision == "fp32":
+        from ..runtime.executor_f32 import HipNetF32
+        return HipNetF32(spec, batch, device, init, opt)
     if impl == "hip":
+        assert precision == "bf16", f"unknown precision {precision!r}"
         from ..runtime.executor import HipNet
         return HipNet(spec, batch, device, init, opt)
     from ..runtime.torchnet import TorchNet
@@ -80,9 +84,9 @@ class Replica:
                  train_images: torch.Tensor, train_labels: torch.Tensor, src_channels: int,
                  eval_images: Optional[torch.Tensor] = None, eval_labels: Optional[torch.Tensor] = None,
                  seed: int = 0, shard: bool = True, use_graph: bool = True, bucket_mb: float = 4.0,
-                 group=None, standalone: bool = False, fused_input: bool = False):
+                 group=None, standalone: bool = False, fused_input: bool = False, precision: str = "bf16"):
         self.spec, self.impl, self.B, self.device = spec, impl, batch, torch.device(device)
-        self.net = build_net(impl, spec, batch, self.device, init, opt)
+        self.net = build_net(impl, spec, batch, self.device, init, opt, precision)
         # standalone: a parameter-server worker (no data-parallel group of its own)
         dp_on = dist.is_initialized() and not standalone
         self.world = dist.get_world_size(group) if dp_on else 1

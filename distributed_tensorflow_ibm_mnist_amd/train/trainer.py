@@ -122,7 +122,7 @@ def _train(FLAGS, cl: Cluster, max_steps, test_interval, batch_size, impl, log) 
     base = Replica(spec, impl, batch_size, cl.device, init, opt, x_tr, y_tr, c_tr, x_ev, y_ev,
                    seed=FLAGS.seed, shard=not FLAGS.no_shard, use_graph=FLAGS.hip_graph,
                    bucket_mb=FLAGS.bucket_mb, group=dp_group if cl.mode == "dp" else None,
-                   fused_input=FLAGS.fused_input) \
+                   fused_input=FLAGS.fused_input, precision=getattr(FLAGS, "precision", "bf16")) \
         if cl.mode != "ps" else _ps_base(spec, impl, batch_size, cl, init, opt, x_tr, y_tr, c_tr, x_ev, y_ev, FLAGS)
     replica = base
     if cl.mode == "ps":
@@ -146,6 +146,7 @@ def _train(FLAGS, cl: Cluster, max_steps, test_interval, batch_size, impl, log) 
     if is_chief:
         hooks.append(LoggerHook(test_interval, monitor))                                 # main.py:139
     meta = {"model": spec.name, "in_channels": spec.in_channels, "impl": impl, "mode": cl.mode,
+            "precision": getattr(FLAGS, "precision", "bf16"),
             "world": cl.world, "batch_size": batch_size, "flags": {k: v for k, v in FLAGS.flag_dict().items()
                                                                    if isinstance(v, (int, float, str, bool))}}
     t0 = time.time()
@@ -184,4 +185,4 @@ def _ps_base(spec, impl, batch_size, cl, init, opt, x_tr, y_tr, c_tr, x_ev, y_ev
     """A PS-mode worker: own input stream (reference P3: no sharding), no DP group."""
     return Replica(spec, impl, batch_size, cl.device, init, opt, x_tr, y_tr, c_tr, x_ev, y_ev,
                    seed=FLAGS.seed + 7919 * cl.task_id, shard=False, use_graph=False, bucket_mb=FLAGS.bucket_mb,
-                   standalone=True)
+                   standalone=True, precision=getattr(FLAGS, "precision", "bf16"))

@@ -45,6 +45,7 @@ flags.DEFINE_integer("in_channels", 0, "model input channels (default: from the 
 flags.DEFINE_boolean("use_ema", False, "restore <var>/ExponentialMovingAverage shadows")
 flags.DEFINE_boolean("per_image_standardization", False, "reference preprocessing (parity; Q3)")
 flags.DEFINE_string("impl", "auto", "hip | torch | auto")
+flags.DEFINE_string("precision", "bf16", "HIP compute precision: bf16 | fp32 (the reference's tf.float32)")
 flags.DEFINE_integer("batch_size", 128, "inference batch (inference.py:34)")
 
 BATCH_SIZE = 128
@@ -115,7 +116,7 @@ def predict(FLAGS):
     B = FLAGS.batch_size
     from distributed_tensorflow_ibm_mnist_amd.train.replica import build_net
     from distributed_tensorflow_ibm_mnist_amd.runtime.params import OptConfig
-    net = build_net(impl, spec, B, dev, params, OptConfig())
+    net = build_net(impl, spec, B, dev, params, OptConfig(), FLAGS.precision)
 
     start = time.time()
     probs = []

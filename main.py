@@ -49,6 +49,8 @@ flags.DEFINE_string("model", "reference_cnn", "reference_cnn | lenet5 | mlp")
 flags.DEFINE_integer("in_channels", 3, "model input channels: 3 = DLI RGB records (reference), 1 = grayscale")
 flags.DEFINE_string("impl", "hip", "hip = MI355X HIP kernels; torch = plain PyTorch (CPU path / baseline)")
 flags.DEFINE_boolean("cpu", False, "force the CPU (torch impl, gloo)")
+flags.DEFINE_string("precision", "bf16", "HIP compute precision: bf16 (bf16 operands, fp32 accumulate) | fp32 "
+                    "(the reference's tf.float32: fp32 activations and fp32 MFMA)")
 flags.DEFINE_integer("seed", 0, "random seed (weights, shuffling)")
 flags.DEFINE_boolean("train_on_eval_split", False, "parity with the reference, which trains on getTestData() (Q1)")
 flags.DEFINE_boolean("no_shard", False, "every DP rank reads the whole dataset in its own order (reference P3)")

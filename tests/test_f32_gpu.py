@@ -1,0 +1,165 @@
+"""--precision fp32: the f32.hip kernels (v_mfma_f32_16x16x4_f32 GEMM engine, fp32
+pool / LRN / softmax-CE) against plain PyTorch fp32, and the whole fp32 step
+against the fp32 oracle at rtol 1e-4 (the reference trains in tf.float32,
+mnist_input.py:86,107)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_tensorflow_ibm_mnist_amd.models import get_model, torch_ref
+from distributed_tensorflow_ibm_mnist_amd.runtime.params import OptConfig
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_err(a, b):
+    return ((a.double() - b.double()).norm() / (b.double().norm() + 1e-30)).item()
+
+
+@pytest.mark.parametrize("M,N,Kk,relu", [(77, 10, 192, False), (300, 1024, 3136, True), (5, 130, 33, True)])
+def test_f32_dense(dev, K, M, N, Kk, relu):
+    torch.manual_seed(0)
+    x = torch.randn(M, Kk, device=dev)
+    w = torch.randn(Kk, N, device=dev) * 0.05
+    b = torch.randn(N, device=dev)
+    y = torch.empty(M, N, device=dev)
+    K.f32_dense_fwd(x, w, y, M, N, Kk, N, b, relu)
+    ref = x @ w + b
+    if relu:
+        ref = ref.relu()
+    assert rel_err(y, ref) < 1e-5
+    # dgrad with a ReLU mask, wgrad (+ bias row) through the split-K slab
+    dy = torch.randn(M, N, device=dev)
+    mask = torch.randn(M, Kk, device=dev)
+    dx = torch.empty(M, Kk, device=dev)
+    K.f32_dense_dgrad(dy, w, dx, M, Kk, N, mask)
+    assert rel_err(dx, (dy @ w.t()) * (mask > 0)) < 1e-5
+    for S in (1, 3):
+        slab = torch.empty(S * (Kk + 1) * N, device=dev)
+        K.f32_dense_wgrad(x, dy, slab, M, Kk, N, S)
+        tot = slab.view(S, Kk + 1, N).sum(0)
+        assert rel_err(tot[:Kk], x.t() @ dy) < 1e-5
+        assert rel_err(tot[Kk], dy.sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("Nb,H,Ci,Co,k,pad", [(3, 28, 3, 32, 5, "SAME"), (2, 14, 32, 64, 5, "SAME"),
+                                               (5, 14, 6, 16, 5, "VALID"), (1, 9, 1, 8, 3, "SAME")])
+def test_f32_conv(dev, K, Nb, H, Ci, Co, k, pad):
+    torch.manual_seed(1)
+    x = torch.randn(Nb, H, H, Ci, device=dev)
+    w = torch.randn(k, k, Ci, Co, device=dev) * 0.1
+    b = torch.randn(Co, device=dev)
+    p = (k - 1) // 2 if pad == "SAME" else 0
+    OH = H if pad == "SAME" else H - k + 1
+    xc = x.permute(0, 3, 1, 2).requires_grad_(True)
+    wc = w.permute(3, 2, 0, 1).contiguous().requires_grad_(True)
+    ref = F.conv2d(xc, wc, b, padding=p).permute(0, 2, 3, 1)
+    y = torch.empty(Nb, OH, OH, Co, device=dev)
+    K.f32_conv_fwd(x, w, y, Nb, H, H, Ci, OH, OH, k, k, p, p, Co, b, False)
+    assert rel_err(y, ref) < 1e-5
+    dy = torch.randn_like(ref)
+    ref.backward(dy)
+    dx = torch.empty_like(x)
+    K.f32_conv_dgrad(dy.contiguous(), w, dx, Nb, OH, OH, Co, H, H, k, k, p, p, Ci, None)
+    assert rel_err(dx, xc.grad.permute(0, 2, 3, 1)) < 1e-5
+    M = k * k * Ci + 1
+    for S in (1, 4):
+        slab = torch.empty(S * M * Co, device=dev)
+        K.f32_conv_wgrad(x, dy.contiguous(), slab, Nb, H, H, Ci, OH, OH, k, k, p, p, Co, S)
+        tot = slab.view(S, M, Co).sum(0)
+        assert rel_err(tot[:-1].view(k, k, Ci, Co), wc.grad.permute(2, 3, 1, 0)) < 1e-5
+        assert rel_err(tot[-1], dy.sum((0, 1, 2))) < 1e-5
+
+
+def test_f32_pool_lrn(dev, K):
+    torch.manual_seed(2)
+    x = torch.randn(3, 14, 14, 64, device=dev)
+    y = torch.empty(3, 7, 7, 64, device=dev)
+    arg = torch.empty(3, 7, 7, 64, dtype=torch.uint8, device=dev)
+    K.f32_maxpool_fwd(x, y, arg, 3, 14, 14, 64)
+    xr = x.permute(0, 3, 1, 2).requires_grad_(True)
+    ref = F.max_pool2d(xr, 2, 2).permute(0, 2, 3, 1)
+    assert torch.equal(y, ref)
+    dy = torch.randn_like(ref)
+    ref.backward(dy)
+    dx = torch.empty_like(x)
+    K.f32_maxpool_bwd(dy.contiguous(), arg, y, False, dx, 3, 14, 14, 64)
+    assert torch.equal(dx, xr.grad.permute(0, 2, 3, 1))
+    # LRN (depth_radius 4, the reference's constants) fwd + bwd with the ReLU mask
+    xl = torch.randn(2, 5, 5, 32, device=dev).relu()
+    xt = xl.clone().requires_grad_(True)
+    yt = torch_ref.lrn_tf(xt.permute(0, 3, 1, 2), 4, 1.0, 0.001 / 9.0, 0.75).permute(0, 2, 3, 1)
+    yl = torch.empty_like(xl)
+    K.f32_lrn_fwd(xl, yl, 50, 32, 4, 1.0, 0.001 / 9.0, 0.75)
+    assert rel_err(yl, yt) < 1e-6
+    g = torch.randn_like(yt)
+    yt.backward(g)
+    dl = torch.empty_like(xl)
+    K.f32_lrn_bwd(xl, g.contiguous(), dl, 50, 32, 4, 1.0, 0.001 / 9.0, 0.75, True)
+    assert rel_err(dl, xt.grad * (xl > 0)) < 1e-5
+
+
+@pytest.mark.parametrize("model,cin", [("reference_cnn", 3), ("lenet5", 1), ("mlp", 1)])
+def test_f32_step_matches_oracle(dev, K, model, cin):
+    """The whole fp32 step (fwd + CE + explicit bwd + fused update) vs the fp32
+    oracle at rtol 1e-4 -- no bf16 noise floor in this mode."""
+    from distributed_tensorflow_ibm_mnist_amd.runtime.executor_f32 import HipNetF32
+    torch.manual_seed(0)
+    spec = get_model(model, cin)
+    init = torch_ref.init_params(spec, seed=1)
+    B = 96
+    net = HipNetF32(spec, B, dev, init, OptConfig(lr0=0.05, decay_steps=0, use_momentum=False, ema_max=0.9999))
+    x = torch.rand(B, 28, 28, cin, device=dev) - 0.5
+    y = torch.randint(0, 10, (B,), device=dev, dtype=torch.int32)
+    net.x0.copy_(x)
+    net.labels.copy_(y)
+    logits = net.forward().clone()
+    net.loss_and_grad()
+    net.backward()
+    p = {k: v.to(dev).float().requires_grad_(True) for k, v in init.items()}
+    ref_logits, _ = torch_ref.forward(spec, p, x)
+    assert rel_err(logits, ref_logits) < 1e-5
+    ce = F.cross_entropy(ref_logits, y.long())
+    ce.backward()
+    for name in init:
+        e = rel_err(net.fp.grad_view(name), p[name].grad)
+        assert e < 1e-4, f"{model} {name}: rel err {e:.3e}"
+    before = {n: net.fp.param_view(n).clone() for n in init}
+    grads = {n: net.fp.grad_view(n).clone() for n in init}
+    net.update()
+    torch.cuda.synchronize()
+    wd = {f"{L.name}/weights": (L.wd or 0.0) for L in spec.weights()}
+    for n in init:
+        exp = before[n] - 0.05 * (grads[n] + wd.get(n, 0.0) * before[n])
+        assert torch.allclose(net.fp.param_view(n), exp, rtol=1e-6, atol=1e-7), n
+    st = net.read_stats()
+    assert abs(st["cross_entropy"] - ce.item()) < 1e-5 * max(1.0, ce.item())
+    assert int(net.fp.step.item()) == 1
+
+
+def test_f32_training_cli(dev, K, tmp_path):
+    """main.py --precision=fp32 (reference CNN, 3 channels, hipGraph) trains and the
+    loss falls; inference with --precision=fp32 reads the checkpoint."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    td = str(tmp_path / "run")
+    cmd = [sys.executable, os.path.join(root, "main.py"), "--model=reference_cnn", "--in_channels=3",
+           "--precision=fp32", "--max_steps=60", "--test_interval=30", "--batch_size=128", f"--train_dir={td}",
+           "--train_data=synthetic://4096", "--test_data=synthetic://512?seed=1", "--base_lr=0.05",
+           "--optimizer=momentum", "--eval_examples=512"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("result: ")][-1]
+    res = dict(kv.split("=", 1) for kv in line[len("result: "):].split())
+    assert int(float(res["global_step"])) == 60
+    assert float(res["cross_entropy"]) < 2.2
+    out = tmp_path / "inf"
+    cmd = [sys.executable, os.path.join(root, "inference.py"), f"--model={td}", "--validate",
+           "--val_data=synthetic://300?seed=2", f"--output_dir={out}", "--output_file=val.json", "--impl=hip",
+           "--precision=fp32"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert json.load(open(out / "val.json"))

@@ -28,8 +28,12 @@ constexpr int FBM = 64, FBN = 64, FBK = 16, FNT = 256;
 constexpr int FLD = FBM + 4;   // LDS row stride (floats)
 
 // ---------------------------------------------------------------- loaders
-// get(r, k): operand element at tile row r (m for A, n for B) and reduction index k;
-// zero outside.  KC: consecutive k are contiguous in memory (thread mapping).
+// load4(r, k): 4 operand elements along the operand's contiguous direction -- k..k+3
+// of row r (KC: consecutive k are contiguous in memory) or rows r..r+3 at k (!KC) --
+// zero outside; one 16-byte load when the 4 are contiguous and aligned.
+DEV f32x4 ld4(const float* p) { return *(const f32x4*)p; }
+DEV bool al16(const float* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 template <bool KC_>
 struct StridedF {
   static constexpr bool KC = KC_;
@@ -42,6 +46,16 @@ struct StridedF {
     if (r >= R) return 0.f;
     return KC ? p[(int64_t)r * ld + k] : p[(int64_t)k * ld + r];
   }
+  DEV f32x4 load4(int r, int k) const {
+    if constexpr (KC) {
+      if (r < R && r != ones_r && k + 3 < K && (ld & 3) == 0 && al16(p)) return ld4(p + (int64_t)r * ld + k);
+      return f32x4{get(r, k), get(r, k + 1), get(r, k + 2), get(r, k + 3)};
+    } else {
+      if (k < K && r + 3 < R && (ones_r < r || ones_r > r + 3) && (ld & 3) == 0 && al16(p))
+        return ld4(p + (int64_t)k * ld + r);
+      return f32x4{get(r, k), get(r + 1, k), get(r + 2, k), get(r + 3, k)};
+    }
+  }
 };
 
 // conv fwd A: row m = output pixel (n, oh, ow), k = (kh, kw, ci)
@@ -49,15 +63,28 @@ struct Im2colF {
   static constexpr bool KC = true;
   const float* x;
   int H, W, C, OH, OW, KW, ph, pw, M, K;
+  FastDiv fOHW, fOW, fC, fKW;
   DEV float get(int m, int k) const {
     if (m >= M || k >= K) return 0.f;
-    const int n = m / (OH * OW), rem = m - n * (OH * OW);
-    const int oh = rem / OW, ow = rem - oh * OW;
-    const int tap = k / C, ci = k - tap * C;
-    const int kh = tap / KW, kw = tap - kh * KW;
+    const int n = fOHW.div(m), rem = fOHW.mod(m, n);
+    const int oh = fOW.div(rem), ow = fOW.mod(rem, oh);
+    const int tap = fC.div(k), ci = fC.mod(k, tap);
+    const int kh = fKW.div(tap), kw = fKW.mod(tap, kh);
     const int ih = oh - ph + kh, iw = ow - pw + kw;
     if (ih < 0 || ih >= H || iw < 0 || iw >= W) return 0.f;
     return x[(((int64_t)n * H + ih) * W + iw) * C + ci];
+  }
+  DEV f32x4 load4(int m, int k) const {
+    if ((C & 3) == 0 && al16(x) && m < M && k + 3 < K) {   // k..k+3: 4 channels of one tap
+      const int n = fOHW.div(m), rem = fOHW.mod(m, n);
+      const int oh = fOW.div(rem), ow = fOW.mod(rem, oh);
+      const int tap = fC.div(k), ci = fC.mod(k, tap);
+      const int kh = fKW.div(tap), kw = fKW.mod(tap, kh);
+      const int ih = oh - ph + kh, iw = ow - pw + kw;
+      if (ih < 0 || ih >= H || iw < 0 || iw >= W) return f32x4{0.f, 0.f, 0.f, 0.f};
+      return ld4(x + (((int64_t)n * H + ih) * W + iw) * C + ci);
+    }
+    return f32x4{get(m, k), get(m, k + 1), get(m, k + 2), get(m, k + 3)};
   }
 };
 
@@ -66,17 +93,30 @@ struct Im2colTF {
   static constexpr bool KC = false;
   const float* x;
   int H, W, C, OH, OW, KW, ph, pw, P, Mreal;
+  FastDiv fOHW, fOW, fC, fKW;
   DEV float get(int m, int k) const {
     if (k >= P) return 0.f;
     if (m == Mreal) return 1.f;
     if (m > Mreal) return 0.f;
-    const int n = k / (OH * OW), rem = k - n * (OH * OW);
-    const int oh = rem / OW, ow = rem - oh * OW;
-    const int tap = m / C, ci = m - tap * C;
-    const int kh = tap / KW, kw = tap - kh * KW;
+    const int n = fOHW.div(k), rem = fOHW.mod(k, n);
+    const int oh = fOW.div(rem), ow = fOW.mod(rem, oh);
+    const int tap = fC.div(m), ci = fC.mod(m, tap);
+    const int kh = fKW.div(tap), kw = fKW.mod(tap, kh);
     const int ih = oh - ph + kh, iw = ow - pw + kw;
     if (ih < 0 || ih >= H || iw < 0 || iw >= W) return 0.f;
     return x[(((int64_t)n * H + ih) * W + iw) * C + ci];
+  }
+  DEV f32x4 load4(int m, int k) const {
+    if ((C & 3) == 0 && al16(x) && k < P && m + 3 < Mreal) {   // m..m+3: 4 channels of one tap
+      const int n = fOHW.div(k), rem = fOHW.mod(k, n);
+      const int oh = fOW.div(rem), ow = fOW.mod(rem, oh);
+      const int tap = fC.div(m), ci = fC.mod(m, tap);
+      const int kh = fKW.div(tap), kw = fKW.mod(tap, kh);
+      const int ih = oh - ph + kh, iw = ow - pw + kw;
+      if (ih < 0 || ih >= H || iw < 0 || iw >= W) return f32x4{0.f, 0.f, 0.f, 0.f};
+      return ld4(x + (((int64_t)n * H + ih) * W + iw) * C + ci);
+    }
+    return f32x4{get(m, k), get(m + 1, k), get(m + 2, k), get(m + 3, k)};
   }
 };
 
@@ -85,15 +125,28 @@ struct DyIm2colF {
   static constexpr bool KC = true;
   const float* dy;
   int H, W, OH, OW, Co, KW, ph, pw, M, K;
+  FastDiv fHW, fW, fCo, fKW;
   DEV float get(int m, int k) const {
     if (m >= M || k >= K) return 0.f;
-    const int n = m / (H * W), rem = m - n * (H * W);
-    const int ih = rem / W, iw = rem - ih * W;
-    const int tap = k / Co, co = k - tap * Co;
-    const int kh = tap / KW, kw = tap - kh * KW;
+    const int n = fHW.div(m), rem = fHW.mod(m, n);
+    const int ih = fW.div(rem), iw = fW.mod(rem, ih);
+    const int tap = fCo.div(k), co = fCo.mod(k, tap);
+    const int kh = fKW.div(tap), kw = fKW.mod(tap, kh);
     const int oh = ih + ph - kh, ow = iw + pw - kw;
     if (oh < 0 || oh >= OH || ow < 0 || ow >= OW) return 0.f;
     return dy[(((int64_t)n * OH + oh) * OW + ow) * Co + co];
+  }
+  DEV f32x4 load4(int m, int k) const {
+    if ((Co & 3) == 0 && al16(dy) && m < M && k + 3 < K) {
+      const int n = fHW.div(m), rem = fHW.mod(m, n);
+      const int ih = fW.div(rem), iw = fW.mod(rem, ih);
+      const int tap = fCo.div(k), co = fCo.mod(k, tap);
+      const int kh = fKW.div(tap), kw = fKW.mod(tap, kh);
+      const int oh = ih + ph - kh, ow = iw + pw - kw;
+      if (oh < 0 || oh >= OH || ow < 0 || ow >= OW) return f32x4{0.f, 0.f, 0.f, 0.f};
+      return ld4(dy + (((int64_t)n * OH + oh) * OW + ow) * Co + co);
+    }
+    return f32x4{get(m, k), get(m, k + 1), get(m, k + 2), get(m, k + 3)};
   }
 };
 
@@ -102,10 +155,18 @@ struct WFlipF {
   static constexpr bool KC = true;
   const float* w;
   int Ci, Co, K;
+  FastDiv fCo;
   DEV float get(int ci, int k) const {
     if (ci >= Ci || k >= K) return 0.f;
-    const int tap = k / Co, co = k - tap * Co;
+    const int tap = fCo.div(k), co = fCo.mod(k, tap);
     return w[((int64_t)tap * Ci + ci) * Co + co];
+  }
+  DEV f32x4 load4(int ci, int k) const {
+    if ((Co & 3) == 0 && al16(w) && ci < Ci && k + 3 < K) {
+      const int tap = fCo.div(k), co = fCo.mod(k, tap);
+      return ld4(w + ((int64_t)tap * Ci + ci) * Co + co);
+    }
+    return f32x4{get(ci, k), get(ci, k + 1), get(ci, k + 2), get(ci, k + 3)};
   }
 };
 
@@ -121,35 +182,22 @@ struct EpiF {
   int64_t slab_stride;
 };
 
+// Tile staging: 64 rows x 16 k = 256 four-element vectors, one per thread, taken along
+// the operand's contiguous direction; LDS keeps the tile k-major ([k][row]).
 template <class L>
-DEV void stage_load(const L& ld, int r0, int k0, int tid, float (&v)[4]) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int r, k;
-    if constexpr (L::KC) {
-      k = tid & 15;
-      r = (tid >> 4) + 16 * i;
-    } else {
-      r = tid & 63;
-      k = (tid >> 6) + 4 * i;
-    }
-    v[i] = ld.get(r0 + r, k0 + k);
-  }
+DEV f32x4 stage_load(const L& ld, int r0, int k0, int tid) {
+  if constexpr (L::KC) return ld.load4(r0 + (tid >> 2), k0 + 4 * (tid & 3));
+  else return ld.load4(r0 + 4 * (tid & 15), k0 + (tid >> 4));
 }
 
 template <class L>
-DEV void stage_store(float* lds, int tid, const float (&v)[4]) {
+DEV void stage_store(float* lds, int tid, const f32x4& v) {
+  if constexpr (L::KC) {
+    const int r = tid >> 2, k = 4 * (tid & 3);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int r, k;
-    if constexpr (L::KC) {
-      k = tid & 15;
-      r = (tid >> 4) + 16 * i;
-    } else {
-      r = tid & 63;
-      k = (tid >> 6) + 4 * i;
-    }
-    lds[k * FLD + r] = v[i];
+    for (int i = 0; i < 4; ++i) lds[(k + i) * FLD + r] = v[i];
+  } else {
+    *(f32x4*)(lds + (tid >> 4) * FLD + 4 * (tid & 15)) = v;
   }
 }
 
@@ -170,10 +218,10 @@ __global__ __launch_bounds__(FNT) void gemm_f32_k(AL A, BL Bm, int M, int N, int
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float va[4], vb[4];
+  f32x4 va = {0.f, 0.f, 0.f, 0.f}, vb = {0.f, 0.f, 0.f, 0.f};
   if (kb < ke) {
-    stage_load(A, m0, kb, tid, va);
-    stage_load(Bm, n0, kb, tid, vb);
+    va = stage_load(A, m0, kb, tid);
+    vb = stage_load(Bm, n0, kb, tid);
   }
   int buf = 0;
   for (int k0 = kb; k0 < ke; k0 += FBK) {
@@ -181,8 +229,8 @@ __global__ __launch_bounds__(FNT) void gemm_f32_k(AL A, BL Bm, int M, int N, int
     stage_store<BL>(Bs[buf], tid, vb);
     __syncthreads();
     if (k0 + FBK < ke) {
-      stage_load(A, m0, k0 + FBK, tid, va);
-      stage_load(Bm, n0, k0 + FBK, tid, vb);
+      va = stage_load(A, m0, k0 + FBK, tid);
+      vb = stage_load(Bm, n0, k0 + FBK, tid);
     }
     const float* as = As[buf];
     const float* bs = Bs[buf];
@@ -287,41 +335,54 @@ __global__ void maxpool_f32_bwd_k(const float* __restrict__ dy, const uint8_t* _
 
 // ---------------------------------------------------------------- LRN across channels (C <= 64)
 // y = x * (bias + alpha * sum_{|j-c| <= r} x_j^2)^-beta   (tf.nn.local_response_normalization)
+// One thread per (pixel, channel); a block stages 256 / C whole pixels in LDS, so the
+// window sums read neighbours from LDS and every global access is coalesced.
 constexpr int LRN_MAXC = 64;
-__global__ void lrn_f32_fwd_k(const float* __restrict__ x, int64_t P, int C, int r, float bias, float alpha,
-                              float beta, float* __restrict__ y) {
-  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < P; p += (int64_t)gridDim.x * blockDim.x) {
-    const float* xp = x + p * C;
-    float sq[LRN_MAXC];
-    for (int c = 0; c < C; ++c) sq[c] = xp[c] * xp[c];
-    for (int c = 0; c < C; ++c) {
+DEV float pow_neg(float n, float b) { return exp2f(-b * log2f(n)); }   // n^-b, n >= bias > 0
+
+__global__ __launch_bounds__(256) void lrn_f32_fwd_k(const float* __restrict__ x, int64_t P, int C, int r,
+                                                     float bias, float alpha, float beta, float* __restrict__ y) {
+  __shared__ float xs[256];
+  const int PB = 256 / C, t = threadIdx.x, pl = t / C, c = t - pl * C;
+  for (int64_t p0 = (int64_t)blockIdx.x * PB; p0 < P; p0 += (int64_t)gridDim.x * PB) {
+    const bool ok = pl < PB && p0 + pl < P;
+    __syncthreads();
+    xs[t] = ok ? x[p0 * C + t] : 0.f;
+    __syncthreads();
+    if (ok) {
       float s = 0.f;
-      for (int j = max(0, c - r); j <= min(C - 1, c + r); ++j) s += sq[j];
-      y[p * C + c] = xp[c] * powf(bias + alpha * s, -beta);
+      for (int j = max(0, c - r); j <= min(C - 1, c + r); ++j) s = fmaf(xs[pl * C + j], xs[pl * C + j], s);
+      y[p0 * C + t] = xs[t] * pow_neg(fmaf(alpha, s, bias), beta);
     }
   }
 }
 
 // dx_i = dy_i N_i^-b - 2 a b x_i sum_{j: |i-j| <= r} dy_j x_j N_j^(-b-1),  N_j = bias + a sum x^2
 // relu_mask: x is a ReLU output, dx_i = 0 where x_i <= 0
-__global__ void lrn_f32_bwd_k(const float* __restrict__ x, const float* __restrict__ dy, int64_t P, int C, int r,
-                              float bias, float alpha, float beta, int relu_mask, float* __restrict__ dx) {
-  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < P; p += (int64_t)gridDim.x * blockDim.x) {
-    const float* xp = x + p * C;
-    const float* gp = dy + p * C;
-    float nrm[LRN_MAXC], t[LRN_MAXC];
-    for (int c = 0; c < C; ++c) {
-      float s = 0.f;
-      for (int j = max(0, c - r); j <= min(C - 1, c + r); ++j) s += xp[j] * xp[j];
-      nrm[c] = bias + alpha * s;
-      t[c] = gp[c] * xp[c] * powf(nrm[c], -beta - 1.f);
-    }
-    for (int c = 0; c < C; ++c) {
-      float s = 0.f;
-      for (int j = max(0, c - r); j <= min(C - 1, c + r); ++j) s += t[j];
-      float g = gp[c] * powf(nrm[c], -beta) - 2.f * alpha * beta * xp[c] * s;
-      if (relu_mask && !(xp[c] > 0.f)) g = 0.f;
-      dx[p * C + c] = g;
+__global__ __launch_bounds__(256) void lrn_f32_bwd_k(const float* __restrict__ x, const float* __restrict__ dy,
+                                                     int64_t P, int C, int r, float bias, float alpha, float beta,
+                                                     int relu_mask, float* __restrict__ dx) {
+  __shared__ float xs[256], ts[256];
+  const int PB = 256 / C, t = threadIdx.x, pl = t / C, c = t - pl * C;
+  for (int64_t p0 = (int64_t)blockIdx.x * PB; p0 < P; p0 += (int64_t)gridDim.x * PB) {
+    const bool ok = pl < PB && p0 + pl < P;
+    __syncthreads();
+    const float xv = ok ? x[p0 * C + t] : 0.f, g = ok ? dy[p0 * C + t] : 0.f;
+    xs[t] = xv;
+    __syncthreads();
+    float s = 0.f;
+    if (ok)
+      for (int j = max(0, c - r); j <= min(C - 1, c + r); ++j) s = fmaf(xs[pl * C + j], xs[pl * C + j], s);
+    const float n = fmaf(alpha, s, bias);
+    const float nb = pow_neg(n, beta);
+    ts[t] = g * xv * nb / n;
+    __syncthreads();
+    if (ok) {
+      float u = 0.f;
+      for (int j = max(0, c - r); j <= min(C - 1, c + r); ++j) u += ts[pl * C + j];
+      float d = g * nb - 2.f * alpha * beta * xv * u;
+      if (relu_mask && !(xv > 0.f)) d = 0.f;
+      dx[p0 * C + t] = d;
     }
   }
 }
@@ -403,14 +464,16 @@ hipError_t f32_dense_wgrad(const float* x, const float* dy, int B, int Din, int 
 hipError_t f32_conv_fwd(const float* x, const float* w, int Nb, int H, int W, int C, int OH, int OW, int KH, int KW,
                         int ph, int pw, int Cout, const float* bias, int relu, float* y, hipStream_t st) {
   const int M = Nb * OH * OW, K = KH * KW * C;
-  return launch_f32(Im2colF{x, H, W, C, OH, OW, KW, ph, pw, M, K}, StridedF<false>{w, Cout, K, Cout, -1}, M, Cout, K,
+  const Im2colF A{x, H, W, C, OH, OW, KW, ph, pw, M, K, FastDiv(OH * OW), FastDiv(OW), FastDiv(C), FastDiv(KW)};
+  return launch_f32(A, StridedF<false>{w, Cout, K, Cout, -1}, M, Cout, K,
                     1, store_epi(y, Cout, bias, Cout, relu, nullptr, 0), st);
 }
 
 hipError_t f32_conv_dgrad(const float* dy, const float* w, int Nb, int OH, int OW, int Cout, int H, int W, int KH,
                           int KW, int ph, int pw, int Cin, const float* mask, float* dx, hipStream_t st) {
   const int M = Nb * H * W, K = KH * KW * Cout;
-  return launch_f32(DyIm2colF{dy, H, W, OH, OW, Cout, KW, ph, pw, M, K}, WFlipF{w, Cin, Cout, K}, M, Cin, K, 1,
+  const DyIm2colF A{dy, H, W, OH, OW, Cout, KW, ph, pw, M, K, FastDiv(H * W), FastDiv(W), FastDiv(Cout), FastDiv(KW)};
+  return launch_f32(A, WFlipF{w, Cin, Cout, K, FastDiv(Cout)}, M, Cin, K, 1,
                     store_epi(dx, Cin, nullptr, 0, 0, mask, Cin), st);
 }
 
@@ -418,7 +481,8 @@ hipError_t f32_conv_wgrad(const float* x, const float* dy, int Nb, int H, int W,
                           int KW, int ph, int pw, int Cout, int splits, float* slab, hipStream_t st) {
   // slab[z][KH*KW*C + 1][Cout], row KH*KW*C = bias
   const int P = Nb * OH * OW, Mr = KH * KW * C;
-  return launch_f32(Im2colTF{x, H, W, C, OH, OW, KW, ph, pw, P, Mr}, StridedF<false>{dy, Cout, P, Cout, -1}, Mr + 1,
+  const Im2colTF A{x, H, W, C, OH, OW, KW, ph, pw, P, Mr, FastDiv(OH * OW), FastDiv(OW), FastDiv(C), FastDiv(KW)};
+  return launch_f32(A, StridedF<false>{dy, Cout, P, Cout, -1}, Mr + 1,
                     Cout, P, splits, slab_epi(slab, (int64_t)(Mr + 1) * Cout), st);
 }
 
@@ -438,15 +502,15 @@ hipError_t f32_maxpool_bwd(const float* dy, const uint8_t* arg, const float* y, 
 
 hipError_t f32_lrn_fwd(const float* x, int64_t P, int C, int r, float bias, float alpha, float beta, float* y,
                        hipStream_t st) {
-  if (C > LRN_MAXC) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(lrn_f32_fwd_k, dim3(ew_grid(P)), dim3(256), 0, st, x, P, C, r, bias, alpha, beta, y);
+  if (C > LRN_MAXC || C < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(lrn_f32_fwd_k, dim3(ew_grid(P * C)), dim3(256), 0, st, x, P, C, r, bias, alpha, beta, y);
   return hipGetLastError();
 }
 
 hipError_t f32_lrn_bwd(const float* x, const float* dy, int64_t P, int C, int r, float bias, float alpha, float beta,
                        int relu_mask, float* dx, hipStream_t st) {
-  if (C > LRN_MAXC) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(lrn_f32_bwd_k, dim3(ew_grid(P)), dim3(256), 0, st, x, dy, P, C, r, bias, alpha, beta,
+  if (C > LRN_MAXC || C < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(lrn_f32_bwd_k, dim3(ew_grid(P * C)), dim3(256), 0, st, x, dy, P, C, r, bias, alpha, beta,
                      relu_mask, dx);
   return hipGetLastError();
 }

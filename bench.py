@@ -43,7 +43,12 @@ def parse():
                     help="hip = our CDNA4 kernels; torch = PyTorch-ROCm baseline (MIOpen/hipBLASLt, bf16 autocast)")
     ap.add_argument("--bucket_mb", type=float, default=0.125,
                     help="gradient bucket cap (MB); every bucket but the last overlaps backward")
-    ap.add_argument("--graph", type=int, default=1, help="capture the step in a hipGraph (hip impl, N=1)")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="hipGraph capture of the step: 1 on (N > 1: with its RCCL all-reduces), 0 off, -1 auto = "
+                         "on for one GPU at per-GPU batch <= 8192 (launch-bound); at the BASELINE batch eager "
+                         "launches measure as fast (profiles/r2/graph_vs_eager.md), so 1..8 GPUs run one mode")
+    ap.add_argument("--force_collectives", type=int, default=0,
+                    help="issue the bucket all-reduces even at N=1 (one-rank RCCL rehearsal of the DP path)")
     ap.add_argument("--optimizer", default="momentum", choices=["sgd", "momentum", "nesterov"])
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=0)
@@ -160,15 +165,18 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.force_collectives and world == 1:      # one-rank process group: the RCCL path on one GPU
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29561")
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
-    if world > 1:
+    if world > 1 or args.force_collectives:
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     spec = get_model(args.model, args.in_channels)
     init = init_params(spec, seed=args.seed)
@@ -184,7 +192,7 @@ def main() -> int:
     else:
         from distributed_tensorflow_ibm_mnist_amd.runtime.torchnet import TorchNet
         net = TorchNet(spec, args.batch, dev, init, opt)
-    dp = DataParallel(net, bucket_cap_mb=args.bucket_mb)
+    dp = DataParallel(net, bucket_cap_mb=args.bucket_mb, force_collectives=bool(args.force_collectives))
     dp.broadcast_state()
 
     imgs, labs = make_synthetic(args.dataset_size, seed=args.seed, channels=1, device=dev)
@@ -196,7 +204,11 @@ def main() -> int:
     loader = DeviceLoader(ds, net.x0, net.labels, rank=rank, world=world, seed=args.seed,
                           idx_out=net.idx_buf if fused_in else None)
 
-    use_graph = bool(args.graph) and args.impl == "hip" and world == 1
+    collectives = world > 1 or bool(args.force_collectives)
+    if args.graph < 0:
+        use_graph = args.impl == "hip" and not collectives and args.batch <= 8192
+    else:
+        use_graph = bool(args.graph) and args.impl == "hip" and (not collectives or args.dist_backend == "nccl")
     graph = None
 
     def step_body():
@@ -294,7 +306,7 @@ def main() -> int:
             "grad_bucket_mb": [round(b.nbytes / 2 ** 20, 3) for b in dp.buckets] if world > 1 else None,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
     return 0
 

@@ -73,17 +73,20 @@ def plan_buckets(net, cap_bytes: int) -> List[Bucket]:
 
 class DataParallel:
     def __init__(self, net, group=None, bucket_cap_mb: float = 1.0, overlap: bool = True,
-                 world: Optional[int] = None):
+                 world: Optional[int] = None, force_collectives: bool = False):
+        """``force_collectives``: issue the bucket all-reduces even with one rank (a
+        one-GPU rehearsal of the RCCL path, e.g. hipGraph capture of the DP step)."""
         self.net = net
         self.group = group
         if world is None:
             world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.world = world
+        self.active = world > 1 or force_collectives
         self.buckets = plan_buckets(net, int(bucket_cap_mb * (1 << 20)))
         self.trigger = {b.layers[-1]: b for b in self.buckets}
         self.pending: list = []
         self.overlap = overlap
-        if self.world > 1:
+        if self.active:
             net.grad_ready_hooks.append(self._hook)
             if hasattr(net, "hook_layers"):       # reduced gradients are needed only at bucket triggers
                 net.hook_layers = set(self.trigger)
@@ -96,7 +99,7 @@ class DataParallel:
             self.pending.append(dist.all_reduce(self.net.fp.grads[b.start:b.end], group=self.group, async_op=True))
 
     def sync_grads(self) -> None:
-        if self.world == 1:
+        if not self.active:
             return
         if not self.overlap:
             for b in self.buckets:

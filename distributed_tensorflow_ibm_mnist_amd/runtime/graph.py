@@ -7,8 +7,14 @@ synchronise, so forward + backward + fused update + finalisation capture into
 one hipGraph and replay with a single launch.  (The batch gather runs just
 before replay, outside the graph, because its source slice moves every step.)
 
-Collectives are kept out of captured regions: with N > 1 the step runs
-eagerly (RCCL overlaps with backward from the grads-ready hooks instead).
+Data parallel (N > 1): the step's RCCL bucket all-reduces (issued from the
+grads-ready hooks, ``async_op=True``, joined by stream waits) are captured with
+it when asked (``--hip_graph_dp`` / ``bench.py --graph 1``): RCCL kernels become
+graph nodes on the communicator's stream, so a small-batch DP step replays with
+one launch.  Off by default: at the BASELINE batch (65536 / GPU) eager launches
+already keep the GPU busy (profiles/r2/graph_vs_eager.md) and the 1..8-GPU curve
+then runs one execution mode throughout.  Rehearsed on one GPU with a one-rank
+RCCL group (tests/test_dp_graph_gpu.py).
 """
 from __future__ import annotations
 

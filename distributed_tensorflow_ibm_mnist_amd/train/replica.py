@@ -84,7 +84,8 @@ class Replica:
                  train_images: torch.Tensor, train_labels: torch.Tensor, src_channels: int,
                  eval_images: Optional[torch.Tensor] = None, eval_labels: Optional[torch.Tensor] = None,
                  seed: int = 0, shard: bool = True, use_graph: bool = True, bucket_mb: float = 4.0,
-                 group=None, standalone: bool = False, fused_input: bool = False, precision: str = "bf16"):
+                 group=None, standalone: bool = False, fused_input: bool = False, precision: str = "bf16",
+                 dp_graph: bool = False):
         self.spec, self.impl, self.B, self.device = spec, impl, batch, torch.device(device)
         self.net = build_net(impl, spec, batch, self.device, init, opt, precision)
         # standalone: a parameter-server worker (no data-parallel group of its own)
@@ -99,7 +100,9 @@ class Replica:
         fused_in = fused_input and impl == "hip" and self.net.bind_u8_input(self.train_ds.images)
         self.loader = DeviceLoader(self.train_ds, self.net.x0, self.net.labels, rank=self.rank, world=self.world,
                                    seed=seed, shard=shard, idx_out=self.net.idx_buf if fused_in else None)
-        self.use_graph = use_graph and impl == "hip" and self.world == 1 and self.device.type == "cuda"
+        # hipGraph: single replica, or (dp_graph) the DP step with its RCCL all-reduces captured
+        self.use_graph = (use_graph and impl == "hip" and self.device.type == "cuda"
+                          and (self.world == 1 or (dp_graph and dist.get_backend(group) == "nccl")))
         self._graph = None
         self.global_step = 0
         self.examples_per_step = batch * self.world

@@ -553,7 +553,7 @@ struct QuadGeo {
 template <int IMGS>
 __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const bf16_t* __restrict__ w,
                                                            const float* __restrict__ bias, int bias_n, int B,
-                                                           bf16_t* __restrict__ pooled, uint8_t* __restrict__ arg) {
+                                                           bf16_t* __restrict__ pooled, uint8_t* __restrict__ arg, int skip) {
   using Q = QuadGeo;
   constexpr int LDS = IMGS * Q::IMG_LDS;
   constexpr int OUTE = Q::NWIN * 8;                 // pooled elements per image (16-byte multiple)
@@ -655,8 +655,8 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
       const int nimg = min(IMGS, B - img0);
       bf16_t* pg = pooled + (int64_t)img0 * OUTE;
       uint8_t* ag = arg + (int64_t)img0 * OUTE;
-      for (int e = tid; e < nimg * OUTE / 8; e += NTH) *(u32x4*)(pg + 8 * e) = *(const u32x4*)(pout + 8 * e);
-      for (int e = tid; e < nimg * OUTE / 16; e += NTH) *(u32x4*)(ag + 16 * e) = *(const u32x4*)(aout + 16 * e);
+      if (!(skip & 2)) for (int e = tid; e < nimg * OUTE / 8; e += NTH) *(u32x4*)(pg + 8 * e) = *(const u32x4*)(pout + 8 * e);
+      if (!(skip & 1)) for (int e = tid; e < nimg * OUTE / 16; e += NTH) *(u32x4*)(ag + 16 * e) = *(const u32x4*)(aout + 16 * e);
     }
   }
 }
@@ -1109,13 +1109,14 @@ hipError_t run_fwd(const XSrc& x, const bf16_t* w, const float* bias, int bias_n
     // A/B knob MNISTX_QUAD_IMGS=3: 3 images per group (LDS 29.1 -> 21.8 KB, 5 -> 7 WGs/CU)
     // ("5": the same with two resident rounds of the 3-image kernel instead of 2048 blocks)
     static const int qi = [] { const char* e = getenv("MNISTX_QUAD_IMGS"); return e ? e[0] - '0' : 4; }();
+    static const int skip = [] { const char* e = getenv("MNISTX_EXP_SKIP"); return e ? atoi(e) : 0; }();
     if (qi == 3 || qi == 5)
       hipLaunchKernelGGL((convpool_fwd_quad_k<3>),
                          dim3(grid_for(B, 3, qi == 3 ? 2048 : 2 * resident_grid<convpool_fwd_quad_k<3>>())), dim3(NTH),
-                         0, st, x, w, bias, bias_n, B, pooled, arg);
+                         0, st, x, w, bias, bias_n, B, pooled, arg, skip);
     else
       hipLaunchKernelGGL((convpool_fwd_quad_k<4>), dim3(grid_for(B, 4, 2048)), dim3(NTH), 0, st, x, w, bias, bias_n,
-                         B, pooled, arg);
+                         B, pooled, arg, skip);
   } else if constexpr (G::PAIR) {
     hipLaunchKernelGGL((convpool_fwd_pair_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, x, w, bias,
                        bias_n, B, pooled, arg);

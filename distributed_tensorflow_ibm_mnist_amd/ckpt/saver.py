@@ -13,6 +13,17 @@ Variable names follow the reference graph: trainables (``conv1/weights``...),
 (``mnist_input.py:265-267``), optimizer slots ``<var>/Momentum``, and the
 zero-debiased loss averages ``<loss>/avg`` (+ ``/biased``, ``/local_step``;
 ``mnist_input.py:288-290``).  ``max_to_keep`` defaults to TF's 5.
+
+Deliberate deviation (parity unpinned): ``.meta`` and ``graph.pbtxt`` are NOT a
+serialized ``MetaGraphDef`` / ``GraphDef``.  There is no TF graph to serialize --
+the model is a static kernel plan over a ``ModelSpec`` -- and no TensorFlow in the
+image to check a hand-built proto against.  ``.meta`` is a JSON record of what a
+restore needs to rebuild the model (spec name, input channels, precision, mode,
+world size, flags, step); ``graph.pbtxt`` is a human-readable layer listing.  The
+reference's inference (``inference.py:86-91``) rebuilds its graph from code and
+reads only the ``checkpoint`` state file + ``.index``/``.data`` bundle, which ARE
+written in TF's tensor-bundle format, so file names and restore flow match; a
+TF tool that imports the ``.meta`` (``tf.train.import_meta_graph``) would not work.
 """
 from __future__ import annotations
 

@@ -238,7 +238,11 @@ class ParameterServer:
         self.max_steps = max_steps
         self.log = log
         # T6 fault injection: MNIST_FI_KILL_RANK_AT_STEP=r:k SIGKILLs this PS (rank r) at global step k
+        # (attempt 0 only, like train/hooks.FaultInjectionHook, unless MNIST_FI_EVERY_ATTEMPT=1)
         kr = os.environ.get("MNIST_FI_KILL_RANK_AT_STEP", "")
+        if int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")) > 0 and \
+                os.environ.get("MNIST_FI_EVERY_ATTEMPT", "0") != "1":
+            kr = ""
         self._kill = tuple(int(v) for v in kr.split(":")) if ":" in kr else (-1, -1)
         self.global_step = 0
         if restore is not None:

@@ -1,0 +1,146 @@
+"""Parameter-server job supervisor: launch 1..k PS + N workers, restart on failure.
+
+The reference's ``MonitoredTrainingSession`` survives a PS restart: on
+``AbortedError`` / ``UnavailableError`` it recreates the session and the chief
+restores from the latest checkpoint (``/root/reference/main.py:140-146`` [TF1-lib]).
+Here a dead PS makes every worker exit non-zero (bounded collective timeout, no
+hang) and the job is restarted as a whole from the last checkpoint -- the same
+recovery torchrun's elastic agent gives the data-parallel mode
+(``--max-restarts``).  This module is that agent for PS mode:
+
+    python -m distributed_tensorflow_ibm_mnist_amd.parallel.supervisor \\
+        --num_ps 1 --num_workers 7 --max_restarts 3 -- --model=lenet5 --train_dir=/tmp/ps ...
+
+* every process gets ``--job_name/--task_id/--ps_hosts/--worker_hosts`` on
+  127.0.0.1, fresh ports per attempt (no TIME_WAIT collisions with the dead one);
+* the first non-zero exit tears the attempt down (SIGTERM, then SIGKILL after a
+  grace period, whole process groups) and starts the next attempt;
+* ``TORCHELASTIC_RESTART_COUNT`` carries the attempt number, so fault injection
+  (``MNIST_FI_*``, train/hooks.py) fires on attempt 0 only, as under torchrun;
+* the PS restores its shard from ``--train_dir`` (``ps.py``), so an attempt
+  resumes at the last checkpointed global step and applies only the missing
+  updates.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def free_ports(n: int) -> List[int]:
+    socks, ports = [], []
+    for _ in range(n):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        socks.append(s)
+        ports.append(s.getsockname()[1])
+    for s in socks:
+        s.close()
+    return ports
+
+
+class Attempt:
+    def __init__(self, procs: Dict[str, subprocess.Popen]):
+        self.procs = procs
+
+    def poll(self) -> Tuple[bool, Optional[Tuple[str, int]]]:
+        """(all finished, first failure (name, rc) or None)."""
+        done = True
+        for name, p in self.procs.items():
+            rc = p.poll()
+            if rc is None:
+                done = False
+            elif rc != 0:
+                return True, (name, rc)
+        return done, None
+
+    def teardown(self, grace_s: float = 10.0) -> None:
+        for sig in (signal.SIGTERM, signal.SIGKILL):
+            for p in self.procs.values():
+                if p.poll() is None:
+                    try:
+                        os.killpg(p.pid, sig)
+                    except ProcessLookupError:
+                        pass
+            t0 = time.time()
+            while time.time() - t0 < grace_s and any(p.poll() is None for p in self.procs.values()):
+                time.sleep(0.1)
+        for p in self.procs.values():
+            p.wait()
+
+
+def launch(main: str, flags: Sequence[str], num_ps: int, num_workers: int, attempt: int, log_dir: Optional[str],
+           env_extra: Optional[Dict[str, str]] = None) -> Attempt:
+    ports = free_ports(num_ps + num_workers)
+    ps_hosts = ",".join(f"127.0.0.1:{p}" for p in ports[:num_ps])
+    wk_hosts = ",".join(f"127.0.0.1:{p}" for p in ports[num_ps:])
+    env = dict(os.environ, TORCHELASTIC_RESTART_COUNT=str(attempt), PYTHONUNBUFFERED="1", **(env_extra or {}))
+    procs: Dict[str, subprocess.Popen] = {}
+    for job, n in (("ps", num_ps), ("worker", num_workers)):
+        for i in range(n):
+            name = f"{job}{i}"
+            out = open(os.path.join(log_dir, f"attempt{attempt}_{name}.log"), "w") if log_dir else None
+            procs[name] = subprocess.Popen(
+                [sys.executable, main, *flags, f"--job_name={job}", f"--task_id={i}", f"--ps_hosts={ps_hosts}",
+                 f"--worker_hosts={wk_hosts}"],
+                cwd=ROOT, env=env, stdout=out, stderr=subprocess.STDOUT if out else None, start_new_session=True)
+    return Attempt(procs)
+
+
+def supervise(flags: Sequence[str], num_ps: int = 1, num_workers: int = 2, max_restarts: int = 3,
+              main: Optional[str] = None, log_dir: Optional[str] = None, timeout_s: float = 0.0,
+              log=print) -> int:
+    main = main or os.path.join(ROOT, "main.py")
+    if log_dir:
+        os.makedirs(log_dir, exist_ok=True)
+    t_end = time.time() + timeout_s if timeout_s > 0 else None
+    for attempt in range(max_restarts + 1):
+        log(f"[supervisor] attempt {attempt}: {num_ps} PS + {num_workers} worker(s)")
+        att = launch(main, flags, num_ps, num_workers, attempt, log_dir)
+        failure = None
+        while True:
+            done, failure = att.poll()
+            if done:
+                break
+            if t_end is not None and time.time() > t_end:
+                att.teardown()
+                log("[supervisor] job timeout")
+                return 124
+            time.sleep(0.2)
+        if failure is None:
+            log(f"[supervisor] attempt {attempt} finished")
+            return 0
+        name, rc = failure
+        log(f"[supervisor] {name} exited with {rc}; tearing down attempt {attempt}")
+        att.teardown()
+    log(f"[supervisor] giving up after {max_restarts} restart(s)")
+    return 1
+
+
+def main(argv: Optional[Sequence[str]] = None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    flags: List[str] = []
+    if "--" in argv:
+        k = argv.index("--")
+        argv, flags = argv[:k], argv[k + 1:]
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("--num_ps", type=int, default=1)
+    ap.add_argument("--num_workers", type=int, default=2)
+    ap.add_argument("--max_restarts", type=int, default=3)
+    ap.add_argument("--log_dir", default="", help="per-process logs (default: inherit stdout)")
+    ap.add_argument("--timeout", type=float, default=0.0, help="whole-job wall limit in seconds (0: none)")
+    ap.add_argument("--main", default="", help="training entry point (default: the repo's main.py)")
+    a = ap.parse_args(argv)
+    return supervise(flags, a.num_ps, a.num_workers, a.max_restarts, a.main or None, a.log_dir or None, a.timeout)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

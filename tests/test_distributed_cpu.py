@@ -310,3 +310,32 @@ def test_ps_worker_weight_loss_terms():
     assert want > 0.01
     assert abs((st["total_loss"] - st["cross_entropy"]) - want) < 1e-4 * want
     assert int(net.fp.step.item()) == 0
+
+
+def test_ps_supervisor_restarts_after_ps_death(tmp_path):
+    """Recovery without a human: the PS is SIGKILLed at step 17 of attempt 0; the
+    supervisor tears the attempt down, starts attempt 1 (fault injection is off on
+    restarts), the PS restores its shard from the last checkpoint and the job
+    finishes at exactly max_steps."""
+    from distributed_tensorflow_ibm_mnist_amd.parallel.supervisor import supervise
+    d = str(tmp_path / "train")
+    logs = str(tmp_path / "logs")
+    flags = ["--impl=torch", "--cpu", "--model=mlp", "--in_channels=1", "--batch_size=32", "--max_steps=40",
+             "--test_interval=100", "--log_step_count_steps=0", "--train_data=synthetic://1500",
+             "--test_data=synthetic://300?seed=1", f"--train_dir={d}", "--save_checkpoint_steps=5",
+             "--collective_timeout=60"]
+    msgs = []
+    os.environ["MNIST_FI_KILL_RANK_AT_STEP"] = "0:17"
+    try:
+        rc = supervise(flags, num_ps=1, num_workers=2, max_restarts=2, log_dir=logs, timeout_s=400,
+                       log=msgs.append)
+    finally:
+        os.environ.pop("MNIST_FI_KILL_RANK_AT_STEP", None)
+    assert rc == 0, msgs
+    assert any("attempt 1 finished" in m for m in msgs), msgs
+    ps1 = open(os.path.join(logs, "attempt1_ps0.log")).read()
+    assert "restored shard from" in ps1
+    w0 = open(os.path.join(logs, "attempt1_worker0.log")).read()
+    assert "result: global_step=40" in w0, w0[-2000:]
+    from distributed_tensorflow_ibm_mnist_amd.ckpt.saver import latest_checkpoint
+    assert latest_checkpoint(d).endswith("model.ckpt-40")

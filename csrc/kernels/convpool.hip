@@ -550,10 +550,10 @@ struct QuadGeo {
   static_assert((X0 - PAD) % 4 == 0 && WS % 4 == 0, "A runs are 8-byte aligned");
 };
 
-template <int IMGS>
+template <int IMGS, int PIPE = 1>
 __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const bf16_t* __restrict__ w,
                                                            const float* __restrict__ bias, int bias_n, int B,
-                                                           bf16_t* __restrict__ pooled, uint8_t* __restrict__ arg, int skip) {
+                                                           bf16_t* __restrict__ pooled, uint8_t* __restrict__ arg, int skip = 0) {
   using Q = QuadGeo;
   constexpr int LDS = IMGS * Q::IMG_LDS;
   constexpr int OUTE = Q::NWIN * 8;                 // pooled elements per image (16-byte multiple)
@@ -564,7 +564,7 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
   constexpr bool STAGE_OUT = true;
   __shared__ __attribute__((aligned(16))) bf16_t pout[STAGE_OUT ? IMGS * OUTE : 8];
   __shared__ __attribute__((aligned(16))) uint8_t aout[STAGE_OUT ? IMGS * OUTE : 16];
-  static_assert((OUTE * 2) % 16 == 0 && OUTE % 16 == 0, "");
+  static_assert((OUTE * 2) % 16 == 0 && OUTE % 16 == 0 && STAGE_OUT, "");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = lane & 31, h = lane >> 5;
   const int s = n >> 3, c = n & 7, sp = s & 1, wp = s >> 1;
@@ -608,45 +608,75 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
       xs.load(x, img0 + stride, B, tid);
       xs.fetch_rows(x, img0 + 2 * stride, B);
     }
-#pragma unroll 1
-    for (int im = 0; im < IMGS; ++im) {
-      const bf16_t* timg = tile + im * Q::IMG_LDS;
-      if (!STAGE_OUT && img0 + im >= B) break;
-      bf16_t* pimg = STAGE_OUT ? pout + im * OUTE : pooled + (int64_t)(img0 + im) * OUTE;
-      uint8_t* aimg = STAGE_OUT ? aout + im * OUTE : arg + (int64_t)(img0 + im) * OUTE;
-      for (int fm = wave; fm < Q::MFQ; fm += NTH / 64) {
-        const int quad = min(fm * 16 + qw, Q::NQUAD - 1);
-        const int ph = quad / Q::PQ, pq = quad - ph * Q::PQ;
-        // tile row of (oh + kh) for kh = h (+2q): oh = 2ph + dy; column 4pq - PAD + X0
-        const bf16_t* tb = timg + (2 * ph + dyr + h) * Q::WS + 4 * pq - Q::PAD + Q::X0;
-        f32x16 acc = {};
+    // the group's IMGS x MFQ fragments are dealt over the waves as one flat list (a
+    // per-image loop left wave 3 with 1 of every 7 fragments); PIPE = 2: two
+    // fragments per iteration, both MFMA chains issued before either epilogue
+    constexpr int NFR = IMGS * Q::MFQ, NWV = NTH / 64;
+    auto frag_base = [&](int f) {
+      const int im = f / Q::MFQ, fm = f - im * Q::MFQ;
+      const int quad = min(fm * 16 + qw, Q::NQUAD - 1);
+      const int ph = quad / Q::PQ, pq = quad - ph * Q::PQ;
+      // tile row of (oh + kh) for kh = h (+2q): oh = 2ph + dy; column 4pq - PAD + X0
+      return tile + im * Q::IMG_LDS + (2 * ph + dyr + h) * Q::WS + 4 * pq - Q::PAD + Q::X0;
+    };
+    auto epilogue = [&](int f, const f32x16& acc) {
+      const int im = f / Q::MFQ, fm = f - im * Q::MFQ;
+      bf16_t* pimg = pout + im * OUTE;
+      uint8_t* aimg = aout + im * OUTE;
+      // acc[i]: row (i&3) + 8(i>>2) + 4h -> quad t-slot t = i/2 (qw = (t&1) + 4(t>>1) + 2h),
+      // dy = i&1; this lane's pixel column within the window is sp: position 2dy + sp
+      float m[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        m[t] = vmax(pos_embed(acc[2 * t], (uint32_t)sp), pos_embed(acc[2 * t + 1], 2u + sp));
+      // lanes n and n^8 hold the left / right pixel of the same window; the even-s lane
+      // finalises even t-slots, the odd-s lane odd ones
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float oth = swap_half_row(sp ? m[2 * u] : m[2 * u + 1]);
+        const int t = 2 * u + sp;
+        const float best = vmax(sp ? m[2 * u + 1] : m[2 * u], oth);
+        const int qt = fm * 16 + (t & 1) + 4 * (t >> 1) + 2 * h;
+        if (qt < Q::NQUAD) {
+          const int win = 2 * qt + wp;   // ph*14 + 2pq + wp with qt = ph*7 + pq (PW == 2*PQ)
+          const float o = pos_clear(best) + bs;
+          pimg[win * 8 + c] = f2bf(vmax(o, 0.f));
+          aimg[win * 8 + c] = (uint8_t)(o > 0.f ? pos_of(best) : ARG_OFF);
+        }
+      }
+    };
+    auto afrag = [&](const bf16_t* tb, int q) {
+      const int rowoff = min(2 * q, 4 - h) * Q::WS;   // kh = 2q + h; the padded kh = 5 reads row 4 (zero weight)
+      return join(*(const s16x4*)(tb + rowoff), *(const s16x4*)(tb + opaque(rowoff + 4)));
+    };
+    if constexpr (PIPE == 2) {
+      for (int f0 = wave; f0 < NFR; f0 += 2 * NWV) {
+        const int f1 = f0 + NWV;
+        const bool two = f1 < NFR;   // wave-uniform
+        const bf16_t* tb0 = frag_base(f0);
+        const bf16_t* tb1 = frag_base(two ? f1 : f0);
+        bf16x8 a0[3], a1[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          const int rowoff = min(2 * q, 4 - h) * Q::WS;   // kh = 2q + h; the padded kh = 5 reads row 4 (zero weight)
-          const bf16x8 a = join(*(const s16x4*)(tb + rowoff), *(const s16x4*)(tb + opaque(rowoff + 4)));
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[q], acc, 0, 0, 0);
+          a0[q] = afrag(tb0, q);
+          a1[q] = afrag(tb1, q);
         }
-        // acc[i]: row (i&3) + 8(i>>2) + 4h -> quad t-slot t = i/2 (qw = (t&1) + 4(t>>1) + 2h),
-        // dy = i&1; this lane's pixel column within the window is sp: position 2dy + sp
-        float m[8];
+        f32x16 acc0 = {}, acc1 = {};
 #pragma unroll
-        for (int t = 0; t < 8; ++t)
-          m[t] = vmax(pos_embed(acc[2 * t], (uint32_t)sp), pos_embed(acc[2 * t + 1], 2u + sp));
-        // lanes n and n^8 hold the left / right pixel of the same window; the even-s lane
-        // finalises even t-slots, the odd-s lane odd ones
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float oth = swap_half_row(sp ? m[2 * u] : m[2 * u + 1]);
-          const int t = 2 * u + sp;
-          const float best = vmax(sp ? m[2 * u + 1] : m[2 * u], oth);
-          const int qt = fm * 16 + (t & 1) + 4 * (t >> 1) + 2 * h;
-          if (qt < Q::NQUAD) {
-            const int win = 2 * qt + wp;   // ph*14 + 2pq + wp with qt = ph*7 + pq (PW == 2*PQ)
-            const float o = pos_clear(best) + bs;
-            pimg[win * 8 + c] = f2bf(vmax(o, 0.f));
-            aimg[win * 8 + c] = (uint8_t)(o > 0.f ? pos_of(best) : ARG_OFF);
-          }
+        for (int q = 0; q < 3; ++q) {
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[q], bfr[q], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[q], bfr[q], acc1, 0, 0, 0);
         }
+        epilogue(f0, acc0);
+        if (two) epilogue(f1, acc1);
+      }
+    } else {
+      for (int f = wave; f < NFR && !(skip & 4); f += NWV) {
+        const bf16_t* tb = frag_base(f);
+        f32x16 acc = {};
+#pragma unroll
+        for (int q = 0; q < 3; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afrag(tb, q), bfr[q], acc, 0, 0, 0);
+        epilogue(f, acc);
       }
     }
     if constexpr (STAGE_OUT) {
@@ -1101,6 +1131,12 @@ int resident_grid() {
   return n;
 }
 
+// A/B knob MNISTX_QUAD_PIPE=2: conv1 forward issues two fragments' MFMA chains per iteration
+static int quad_pipe() {
+  static const int v = [] { const char* e = getenv("MNISTX_QUAD_PIPE"); return (e && e[0] == '2') ? 2 : 1; }();
+  return v;
+}
+
 template <class G, int IMGS>
 hipError_t run_fwd(const XSrc& x, const bf16_t* w, const float* bias, int bias_n, int B, bf16_t* pooled, uint8_t* arg,
                    hipStream_t st) {
@@ -1109,14 +1145,26 @@ hipError_t run_fwd(const XSrc& x, const bf16_t* w, const float* bias, int bias_n
     // A/B knob MNISTX_QUAD_IMGS=3: 3 images per group (LDS 29.1 -> 21.8 KB, 5 -> 7 WGs/CU)
     // ("5": the same with two resident rounds of the 3-image kernel instead of 2048 blocks)
     static const int qi = [] { const char* e = getenv("MNISTX_QUAD_IMGS"); return e ? e[0] - '0' : 4; }();
-    static const int skip = [] { const char* e = getenv("MNISTX_EXP_SKIP"); return e ? atoi(e) : 0; }();
     if (qi == 3 || qi == 5)
       hipLaunchKernelGGL((convpool_fwd_quad_k<3>),
                          dim3(grid_for(B, 3, qi == 3 ? 2048 : 2 * resident_grid<convpool_fwd_quad_k<3>>())), dim3(NTH),
-                         0, st, x, w, bias, bias_n, B, pooled, arg, skip);
-    else
-      hipLaunchKernelGGL((convpool_fwd_quad_k<4>), dim3(grid_for(B, 4, 2048)), dim3(NTH), 0, st, x, w, bias, bias_n,
+                         0, st, x, w, bias, bias_n, B, pooled, arg);
+    else if (quad_pipe() == 2)
+      hipLaunchKernelGGL((convpool_fwd_quad_k<4, 2>), dim3(grid_for(B, 4, 2048)), dim3(NTH), 0, st, x, w, bias,
+                         bias_n, B, pooled, arg);
+    else {
+      // grid A/B: MNISTX_QUAD_GRID = explicit block count, "r" = one resident wave, "2r" = two
+      static const int gq = [] {
+        const char* e = getenv("MNISTX_QUAD_GRID");
+        if (!e) return 2048;
+        if (e[0] == 'r') return resident_grid<convpool_fwd_quad_k<4>>();
+        if (e[0] == '2' && e[1] == 'r') return 2 * resident_grid<convpool_fwd_quad_k<4>>();
+        return atoi(e);
+      }();
+      static const int skip = [] { const char* e = getenv("MNISTX_EXP_SKIP"); return e ? atoi(e) : 0; }();
+      hipLaunchKernelGGL((convpool_fwd_quad_k<4>), dim3(grid_for(B, 4, gq)), dim3(NTH), 0, st, x, w, bias, bias_n,
                          B, pooled, arg, skip);
+    }
   } else if constexpr (G::PAIR) {
     hipLaunchKernelGGL((convpool_fwd_pair_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, x, w, bias,
                        bias_n, B, pooled, arg);

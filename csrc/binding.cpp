@@ -609,7 +609,8 @@ mnistx::XSrc cp_src(const Tensor& x, const optional<Tensor>& u8, const optional<
     TORCH_CHECK(mnistx::convpool_u8_input(cfg), "convpool: uint8 input only for 1-channel first layers");
     TORCH_CHECK(idx.has_value() && idx->defined(), "convpool: uint8 input needs idx");
     check(*u8, at::kByte, hwc, "u8");
-    TORCH_CHECK(u8->numel() % hwc == 0 && u8->numel() / hwc < (int64_t)INT32_MAX, "u8: [n, H*W*C] images");
+    TORCH_CHECK(u8->numel() % hwc == 0 && u8->numel() < (int64_t)INT32_MAX,
+                "u8: [n, H*W*C] images, < 2 GB (the kernels address it through one buffer resource)");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(u8->data_ptr()) % 4 == 0, "u8 must be 4-byte aligned");
     check(*idx, at::kLong, B, "idx");
     src.u8 = P<const uint8_t>(*u8);

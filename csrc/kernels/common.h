@@ -92,3 +92,21 @@ DEV bf16x8 join(s16x4 lo, s16x4 hi) {
 // supplies the address of 4 consecutive bf16 (row q, columns 4p..4p+3); lane i
 // of the group receives column i of the 4 rows.  Addresses must be 8-byte aligned.
 DEV s16x4 lds_tr4(const bf16_t* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p); }
+
+// Branch-free global loads through a buffer resource (raw buffer loads): an offset
+// at or past num_records returns zeros without touching memory, so a tile's tail
+// needs no per-lane branch.  A per-lane `if` (or a select) around a plain global
+// load makes the compiler wait for the load at the control-flow join
+// (s_waitcnt vmcnt(0)), which serialises a software-prefetch of several loads into
+// one full memory latency each.
+constexpr uint32_t BUF_OOB = 0x80000000u;   // > any num_records used here (< 2 GB)
+DEV __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nbytes, 0x00020000);
+}
+DEV uint32_t buf_b32(__amdgpu_buffer_rsrc_t r, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0); }
+DEV u32x2 buf_b64(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+DEV u32x4 buf_b128(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}

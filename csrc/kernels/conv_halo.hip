@@ -95,13 +95,25 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict
     }
   }
 
+  // this lane's bias values (output channels n0 + nf*16 + 4g + r), loaded once: a
+  // conditional load inside the epilogue stalled every fragment on its latency
+  float bsv[NF][4];
+#pragma unroll
+  for (int nf = 0; nf < NF; ++nf)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int nb = n0 + nf * 16 + 4 * g + r;
+      bsv[nf][r] = (MODE == 0 && bias != nullptr && nb < bias_n) ? bias[nb] : 0.f;
+    }
+
   u32x4 pre[PER];
   auto gload = [&](int img0) {               // images img0 .. img0+IMGS-1 are contiguous in HBM
+    // branch-free buffer loads (common.h): images past the batch read zeros
+    const auto r = buf_rsrc(x + (int64_t)img0 * NPIX * CIN, (uint32_t)(max(0, min(IMGS, B - img0)) * NPIX * CIN * 2));
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int v = tid + u * NT;
-      pre[u] = (v < IMGS * NV && img0 + v / NV < B) ? *(const u32x4*)(x + (int64_t)img0 * NPIX * CIN + 8 * v)
-                                                  : u32x4{0u, 0u, 0u, 0u};
+      pre[u] = buf_b128(r, v < IMGS * NV ? (uint32_t)(16 * v) : BUF_OOB);
     }
   };
   const int gstride = gridDim.x * IMGS;
@@ -168,10 +180,7 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict
 #pragma unroll
       for (int nf = 0; nf < NF; ++nf) {
         const int nb = n0 + nf * 16 + 4 * g;
-        float bn[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          bn[r] = (MODE == 0 && bias != nullptr && nb + r < bias_n) ? bias[nb + r] : 0.f;
+        const float* bn = bsv[nf];
 #pragma unroll
         for (int h = 0; h < FR; ++h) {
           const int f = FR * gr + h, im = f / MFR;
@@ -241,16 +250,19 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_wgrad_k(const bf16_t* __re
     for (int n = 0; n < NFW; ++n) acc[r][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   u32x4 px[PX], pd[PD];
-  auto gload = [&](int img) {
+  auto gload = [&](int img) {                 // branch-free buffer loads; past the batch: zeros
+    const bool in = img < B;
+    const auto rx = buf_rsrc(x + (int64_t)(in ? img : 0) * NPIX * CIN, in ? (uint32_t)(NPIX * CIN * 2) : 0u);
+    const auto rd = buf_rsrc(dy + (int64_t)(in ? img : 0) * NPIX * COUT, in ? (uint32_t)(NPIX * COUT * 2) : 0u);
 #pragma unroll
     for (int u = 0; u < PX; ++u) {
       const int v = tid + u * NT;
-      px[u] = (v < XV && img < B) ? *(const u32x4*)(x + (int64_t)img * NPIX * CIN + 8 * v) : u32x4{0u, 0u, 0u, 0u};
+      px[u] = buf_b128(rx, v < XV ? (uint32_t)(16 * v) : BUF_OOB);
     }
 #pragma unroll
     for (int u = 0; u < PD; ++u) {
       const int v = tid + u * NT;
-      pd[u] = (v < DV && img < B) ? *(const u32x4*)(dy + (int64_t)img * NPIX * COUT + 8 * v) : u32x4{0u, 0u, 0u, 0u};
+      pd[u] = buf_b128(rd, v < DV ? (uint32_t)(16 * v) : BUF_OOB);
     }
   };
   gload(blockIdx.x);

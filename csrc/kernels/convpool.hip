@@ -209,27 +209,38 @@ struct XStage {
   // bf16 activations, or (first layer) the uint8 dataset gathered through the
   // batch index and normalised x/255 - 0.5 exactly like prep_images (K10 fused).
   // uint8: rows[] must hold the rows of this group (fetch_rows one group earlier).
+  // Branch-free buffer loads (common.h buf_*): invalid slots read zeros; the raw
+  // uint8 words are converted only at store time, so no load is waited for here.
+  bool u8mode = false;
   DEV void load(const XSrc& src, int img0, int B, int tid) {
+    const int nimg = max(0, min(IMGS, B - img0));
+    u8mode = U8 && src.u8 != nullptr;
+    if (U8 && src.u8) {
+      const auto r = buf_rsrc(src.u8, (uint32_t)((int64_t)src.n * G::INTERIOR));
 #pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int e = tid + u * NTH;
-      v[u] = u32x2{0u, 0u};
-      if (e < NV) {
+      for (int u = 0; u < PER; ++u) {
+        const int e = tid + u * NTH;
         const int im = e / (G::H * G::ROWV), rem = e - im * (G::H * G::ROWV);
-        if (img0 + im < B) {
-          if (U8 && src.u8) {
-            int row = rows[0];
+        int row = rows[0];
 #pragma unroll
-            for (int k = 1; k < IMGS; ++k) row = im == k ? rows[k] : row;
-            const uint32_t b4 = *(const uint32_t*)(src.u8 + (int64_t)row * G::INTERIOR + rem * 4);
-            v[u] = u32x2{pack2(u8_norm(b4 & 0xff), u8_norm((b4 >> 8) & 0xff)),
-                         pack2(u8_norm((b4 >> 16) & 0xff), u8_norm(b4 >> 24))};
-          } else {
-            v[u] = *(const u32x2*)(src.x + (int64_t)(img0 + im) * G::INTERIOR + rem * 4);
-          }
-        }
+        for (int k = 1; k < IMGS; ++k) row = im == k ? rows[k] : row;
+        const bool ok = e < NV && im < nimg;
+        v[u] = u32x2{buf_b32(r, ok ? (uint32_t)(row * G::INTERIOR + rem * 4) : BUF_OOB), 0u};
+      }
+    } else {
+      const auto r = buf_rsrc(src.x + (int64_t)img0 * G::INTERIOR, (uint32_t)(nimg * G::INTERIOR * 2));
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int e = tid + u * NTH;
+        v[u] = buf_b64(r, e < NV ? (uint32_t)(e * 8) : BUF_OOB);   // e*4 elements = the image-major interior
       }
     }
+  }
+  DEV u32x2 value(int u) const {
+    if (!u8mode) return v[u];
+    const uint32_t b4 = v[u][0];
+    return u32x2{pack2(u8_norm(b4 & 0xff), u8_norm((b4 >> 8) & 0xff)),
+                 pack2(u8_norm((b4 >> 16) & 0xff), u8_norm(b4 >> 24))};
   }
   DEV void store(bf16_t* tile, int tid) const {
 #pragma unroll
@@ -238,7 +249,7 @@ struct XStage {
       if (e < NV) {
         const int im = e / (G::H * G::ROWV), rem = e - im * (G::H * G::ROWV);
         const int hh = rem / G::ROWV, vv = rem - hh * G::ROWV;
-        *(u32x2*)(tile + im * G::IMG_LDS + ((hh + G::PAD) * G::WS + G::X0) * G::CIN + 4 * vv) = v[u];
+        *(u32x2*)(tile + im * G::IMG_LDS + ((hh + G::PAD) * G::WS + G::X0) * G::CIN + 4 * vv) = value(u);
       }
     }
   }
@@ -271,17 +282,18 @@ struct DYStage {
   static_assert(NWC % 8 == 0, "");
   u32x4 y[PER];
   u32x2 a[PER];
+  // branch-free buffer loads: slots past the batch read dP = 0 and arg = 0, which
+  // contribute nothing (every consumer multiplies / selects dP by the argmax)
   DEV void load(const bf16_t* __restrict__ dP, const uint8_t* __restrict__ arg, int img0, int B, int tid) {
+    const int nimg = max(0, min(IMGS, B - img0));
+    const auto ry = buf_rsrc(dP + (int64_t)img0 * NWC, (uint32_t)(nimg * NWC * 2));
+    const auto ra = buf_rsrc(arg + (int64_t)img0 * NWC, (uint32_t)(nimg * NWC));
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int e = 8 * (tid + u * NTH);
-      y[u] = u32x4{0u, 0u, 0u, 0u};
-      a[u] = u32x2{0x04040404u, 0x04040404u};
-      if (e < IMGS * NWC && img0 + e / NWC < B) {
-        const int64_t o = (int64_t)img0 * NWC + e;
-        y[u] = *(const u32x4*)(dP + o);
-        a[u] = *(const u32x2*)(arg + o);
-      }
+      const bool ok = e < IMGS * NWC;
+      y[u] = buf_b128(ry, ok ? (uint32_t)(e * 2) : BUF_OOB);
+      a[u] = buf_b64(ra, ok ? (uint32_t)e : BUF_OOB);
     }
   }
   DEV void store(bf16_t* dys, uint8_t* args, int tid) const {
@@ -553,7 +565,7 @@ struct QuadGeo {
 template <int IMGS, int PIPE = 1>
 __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const bf16_t* __restrict__ w,
                                                            const float* __restrict__ bias, int bias_n, int B,
-                                                           bf16_t* __restrict__ pooled, uint8_t* __restrict__ arg, int skip = 0) {
+                                                           bf16_t* __restrict__ pooled, uint8_t* __restrict__ arg) {
   using Q = QuadGeo;
   constexpr int LDS = IMGS * Q::IMG_LDS;
   constexpr int OUTE = Q::NWIN * 8;                 // pooled elements per image (16-byte multiple)
@@ -599,8 +611,9 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
         const int im = e / (Q::H * Q::ROWV), rem = e - im * (Q::H * Q::ROWV);
         const int hh = rem / Q::ROWV, vv = rem - hh * Q::ROWV;
         bf16_t* dst = tile + im * Q::IMG_LDS + (hh + Q::PAD) * Q::WS + Q::X0 + 4 * vv;
-        *(uint32_t*)dst = xs.v[u][0];
-        *(uint32_t*)(dst + 2) = xs.v[u][1];
+        const u32x2 val = xs.value(u);
+        *(uint32_t*)dst = val[0];
+        *(uint32_t*)(dst + 2) = val[1];
       }
     }
     __syncthreads();
@@ -671,7 +684,7 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
         if (two) epilogue(f1, acc1);
       }
     } else {
-      for (int f = wave; f < NFR && !(skip & 4); f += NWV) {
+      for (int f = wave; f < NFR; f += NWV) {
         const bf16_t* tb = frag_base(f);
         f32x16 acc = {};
 #pragma unroll
@@ -685,8 +698,20 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
       const int nimg = min(IMGS, B - img0);
       bf16_t* pg = pooled + (int64_t)img0 * OUTE;
       uint8_t* ag = arg + (int64_t)img0 * OUTE;
-      if (!(skip & 2)) for (int e = tid; e < nimg * OUTE / 8; e += NTH) *(u32x4*)(pg + 8 * e) = *(const u32x4*)(pout + 8 * e);
-      if (!(skip & 1)) for (int e = tid; e < nimg * OUTE / 16; e += NTH) *(u32x4*)(ag + 16 * e) = *(const u32x4*)(aout + 16 * e);
+      // compile-time store counts (unrolled, exec-masked tails): the loop-top wait for the
+      // prefetched loads is then vmcnt(#stores) -- a runtime-trip-count store loop made it
+      // wait for these stores to complete as well (loads and stores share vmcnt, in order)
+      constexpr int PV = IMGS * OUTE / 8, AV = IMGS * OUTE / 16;
+#pragma unroll
+      for (int u = 0; u < (PV + NTH - 1) / NTH; ++u) {
+        const int e = tid + u * NTH;
+        if (e < nimg * (OUTE / 8)) *(u32x4*)(pg + 8 * e) = *(const u32x4*)(pout + 8 * e);
+      }
+#pragma unroll
+      for (int u = 0; u < (AV + NTH - 1) / NTH; ++u) {
+        const int e = tid + u * NTH;
+        if (e < nimg * (OUTE / 16)) *(u32x4*)(ag + 16 * e) = *(const u32x4*)(aout + 16 * e);
+      }
     }
   }
 }
@@ -1161,9 +1186,8 @@ hipError_t run_fwd(const XSrc& x, const bf16_t* w, const float* bias, int bias_n
         if (e[0] == '2' && e[1] == 'r') return 2 * resident_grid<convpool_fwd_quad_k<4>>();
         return atoi(e);
       }();
-      static const int skip = [] { const char* e = getenv("MNISTX_EXP_SKIP"); return e ? atoi(e) : 0; }();
       hipLaunchKernelGGL((convpool_fwd_quad_k<4>), dim3(grid_for(B, 4, gq)), dim3(NTH), 0, st, x, w, bias, bias_n,
-                         B, pooled, arg, skip);
+                         B, pooled, arg);
     }
   } else if constexpr (G::PAIR) {
     hipLaunchKernelGGL((convpool_fwd_pair_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, x, w, bias,
@@ -1302,12 +1326,12 @@ __global__ __launch_bounds__(NTH, 3) void lenet_c2dgrad_c1wgrad_k(const XSrc x, 
   constexpr int A1V = IMGS * NWC1 / 16;                // 16-byte arg1 vectors per group
   constexpr int A1PER = (A1V + NTH - 1) / NTH;
   u32x4 a1v[A1PER];
-  auto load_a1 = [&](int i0) {
+  auto load_a1 = [&](int i0) {   // branch-free; past the batch: zeros (dP1 is zero there too)
+    const auto ra = buf_rsrc(arg1 + (int64_t)i0 * NWC1, (uint32_t)(max(0, min(IMGS, B - i0)) * NWC1));
 #pragma unroll
     for (int u = 0; u < A1PER; ++u) {
       const int e = tid + u * NTH;
-      a1v[u] = u32x4{0x04040404u, 0x04040404u, 0x04040404u, 0x04040404u};   // padded image: ReLU off
-      if (e < A1V && i0 + (16 * e) / NWC1 < B) a1v[u] = *(const u32x4*)(arg1 + (int64_t)i0 * NWC1 + 16 * e);
+      a1v[u] = buf_b128(ra, e < A1V ? (uint32_t)(16 * e) : BUF_OOB);
     }
   };
 

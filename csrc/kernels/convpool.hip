@@ -562,7 +562,7 @@ struct QuadGeo {
   static_assert((X0 - PAD) % 4 == 0 && WS % 4 == 0, "A runs are 8-byte aligned");
 };
 
-template <int IMGS, int PIPE = 1>
+template <int IMGS>
 __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const bf16_t* __restrict__ w,
                                                            const float* __restrict__ bias, int bias_n, int B,
                                                            bf16_t* __restrict__ pooled, uint8_t* __restrict__ arg) {
@@ -622,8 +622,8 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
       xs.fetch_rows(x, img0 + 2 * stride, B);
     }
     // the group's IMGS x MFQ fragments are dealt over the waves as one flat list (a
-    // per-image loop left wave 3 with 1 of every 7 fragments); PIPE = 2: two
-    // fragments per iteration, both MFMA chains issued before either epilogue
+    // per-image loop left wave 3 with 1 of every 7 fragments).  Measured neutral, as
+    // were two MFMA chains per iteration and other grids (profiles/r2/conv1_fwd_experiments.md)
     constexpr int NFR = IMGS * Q::MFQ, NWV = NTH / 64;
     auto frag_base = [&](int f) {
       const int im = f / Q::MFQ, fm = f - im * Q::MFQ;
@@ -662,35 +662,12 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
       const int rowoff = min(2 * q, 4 - h) * Q::WS;   // kh = 2q + h; the padded kh = 5 reads row 4 (zero weight)
       return join(*(const s16x4*)(tb + rowoff), *(const s16x4*)(tb + opaque(rowoff + 4)));
     };
-    if constexpr (PIPE == 2) {
-      for (int f0 = wave; f0 < NFR; f0 += 2 * NWV) {
-        const int f1 = f0 + NWV;
-        const bool two = f1 < NFR;   // wave-uniform
-        const bf16_t* tb0 = frag_base(f0);
-        const bf16_t* tb1 = frag_base(two ? f1 : f0);
-        bf16x8 a0[3], a1[3];
+    for (int f = wave; f < NFR; f += NWV) {
+      const bf16_t* tb = frag_base(f);
+      f32x16 acc = {};
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          a0[q] = afrag(tb0, q);
-          a1[q] = afrag(tb1, q);
-        }
-        f32x16 acc0 = {}, acc1 = {};
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[q], bfr[q], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[q], bfr[q], acc1, 0, 0, 0);
-        }
-        epilogue(f0, acc0);
-        if (two) epilogue(f1, acc1);
-      }
-    } else {
-      for (int f = wave; f < NFR; f += NWV) {
-        const bf16_t* tb = frag_base(f);
-        f32x16 acc = {};
-#pragma unroll
-        for (int q = 0; q < 3; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afrag(tb, q), bfr[q], acc, 0, 0, 0);
-        epilogue(f, acc);
-      }
+      for (int q = 0; q < 3; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afrag(tb, q), bfr[q], acc, 0, 0, 0);
+      epilogue(f, acc);
     }
     if constexpr (STAGE_OUT) {
       __syncthreads();
@@ -1156,12 +1133,6 @@ int resident_grid() {
   return n;
 }
 
-// A/B knob MNISTX_QUAD_PIPE=2: conv1 forward issues two fragments' MFMA chains per iteration
-static int quad_pipe() {
-  static const int v = [] { const char* e = getenv("MNISTX_QUAD_PIPE"); return (e && e[0] == '2') ? 2 : 1; }();
-  return v;
-}
-
 template <class G, int IMGS>
 hipError_t run_fwd(const XSrc& x, const bf16_t* w, const float* bias, int bias_n, int B, bf16_t* pooled, uint8_t* arg,
                    hipStream_t st) {
@@ -1174,9 +1145,6 @@ hipError_t run_fwd(const XSrc& x, const bf16_t* w, const float* bias, int bias_n
       hipLaunchKernelGGL((convpool_fwd_quad_k<3>),
                          dim3(grid_for(B, 3, qi == 3 ? 2048 : 2 * resident_grid<convpool_fwd_quad_k<3>>())), dim3(NTH),
                          0, st, x, w, bias, bias_n, B, pooled, arg);
-    else if (quad_pipe() == 2)
-      hipLaunchKernelGGL((convpool_fwd_quad_k<4, 2>), dim3(grid_for(B, 4, 2048)), dim3(NTH), 0, st, x, w, bias,
-                         bias_n, B, pooled, arg);
     else {
       // grid A/B: MNISTX_QUAD_GRID = explicit block count, "r" = one resident wave, "2r" = two
       static const int gq = [] {

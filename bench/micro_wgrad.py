@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Dense weight-gradient sweep: GEMM tile x split-K count for the LeNet-5 fc shapes
 at B = 65536 (wgrad GEMM + multi-tensor split-K reduce, CUDA-event timed).
-Usage: python bench/micro_wgrad.py [B]"""
+Usage: python bench/micro_wgrad.py [B] [ref]   (ref: the reference CNN's local3/local4 shapes)"""
 import os
 import sys
 
@@ -19,13 +19,17 @@ def main():
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     shapes = [("fc3", 400, 120, 120), ("fc4", 120, 84, 88), ("fc5", 84, 10, 16)]
+    splits = (16, 32, 64, 128, 256)
+    if len(sys.argv) > 2 and sys.argv[2] == "ref":
+        shapes = [("local3", 3136, 1024, 1024), ("local4", 1024, 192, 192)]
+        splits = (1, 2, 3, 4, 6, 8, 12, 16)
     for name, din, dout, Np in shapes:
         Dp = din if name != "fc5" else 88
         x = (torch.randn(B, Dp, device=dev) * 0.5).to(torch.bfloat16)
         dy = (torch.randn(B, Np, device=dev) * 0.1).to(torch.bfloat16)
         ref = (x.float().t() @ dy.float())[:din, :dout]
         M = Dp + 1
-        slab = torch.empty(256 * M * Np + 64, device=dev)
+        slab = torch.empty(max(splits) * M * Np + 64, device=dev)
         dw = torch.empty(din * dout, device=dev)
         db = torch.empty(dout, device=dev)
         geo_row = lambda S: [S, M, Np, 1, Dp, din, dout, Dp]
@@ -38,7 +42,7 @@ def main():
             if Np > 32 and tname in ("64x16", "64x32"):
                 continue
             row = []
-            for S in (16, 32, 64, 128, 256):
+            for S in splits:
                 def run():
                     s = K.dense_wgrad(x, dy, slab, Dp, Np, B, Dp, Np, True, S, code)
                     K.splitk_reduce_multi([slab], [dw], [db], torch.tensor([geo_row(s)]), [1.0])

@@ -631,7 +631,10 @@ int tile_code(int M, int N, bool wgrad) {
     if (N <= 32) return T64x32;
     if (N <= 64) return T64x64;
     if (N <= 128) return M >= 256 ? T64x128 : T64x64;   // whole N per tile: M operand read once
-    if (tiles(128, 128) < 256) return T64x64;
+    // 128x128 halves the operand traffic per MAC; from 128 tiles up it wins even with
+    // few splits (reference local3 3137x1024xK16384: 64x64/S3 214 us -> 128x128/S2
+    // 156 us incl. the split-K reduce, bench/micro_wgrad.py ref)
+    if (tiles(128, 128) < 128) return T64x64;
     return T128x128;
   }
   if (N <= 16) return tiles(256, 16) >= 1024 ? T256x16 : T64x16;

@@ -308,7 +308,7 @@ __global__ __launch_bounds__(TPB) void lrn_fwd_k(const bf16_t* __restrict__ x, i
   for (int64_t base = (int64_t)blockIdx.x * TPB; base < total; base += (int64_t)gridDim.x * TPB) {
     const int64_t t = base + threadIdx.x;
     const bool ok = t < total;
-    const u32x4 xv = ok ? *(const u32x4*)(x + t * 8) : u32x4{0u, 0u, 0u, 0u};
+    const u32x4 xv = *(const u32x4*)(x + (ok ? t : 0) * 8);   // unconditional (clamped) load
     float v[8], sq[8], s[8];
     unpack8(xv, v);
 #pragma unroll
@@ -336,8 +336,8 @@ __global__ __launch_bounds__(TPB) void lrn_bwd_k(const bf16_t* __restrict__ x, c
   for (int64_t base = (int64_t)blockIdx.x * TPB; base < total; base += (int64_t)gridDim.x * TPB) {
     const int64_t t = base + threadIdx.x;
     const bool ok = t < total;
-    const u32x4 xv = ok ? *(const u32x4*)(x + t * 8) : u32x4{0u, 0u, 0u, 0u};
-    const u32x4 gv = ok ? *(const u32x4*)(dy + t * 8) : u32x4{0u, 0u, 0u, 0u};
+    const u32x4 xv = *(const u32x4*)(x + (ok ? t : 0) * 8);    // unconditional (clamped) loads
+    const u32x4 gv = *(const u32x4*)(dy + (ok ? t : 0) * 8);
     float v[8], g[8], w[8], s[8], u[8];
     unpack8(xv, v);
     unpack8(gv, g);
@@ -397,10 +397,17 @@ __global__ __launch_bounds__(TPB) void lrn_pool_fwd_k(const bf16_t* __restrict__
     uint32_t bi[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    // the window's 4 pixel vectors: unconditional loads (clamped index), all in flight
+    // before any math -- a load under `ok ?` made each wait for its own latency
+    u32x4 xq[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       const int ih = 2 * oh + (d >> 1), iw = 2 * ow + (d & 1);
-      const u32x4 xv = ok ? *(const u32x4*)(x + ((n * H + ih) * W + iw) * C + c8 * 8) : u32x4{0u, 0u, 0u, 0u};
+      xq[d] = *(const u32x4*)(x + ((n * H + ih) * W + iw) * C + c8 * 8);
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const u32x4 xv = xq[d];
       float v[8], sq[8], s[8];
       unpack8(xv, v);
 #pragma unroll
@@ -442,15 +449,22 @@ __global__ __launch_bounds__(TPB) void lrn_pool_bwd_k(const bf16_t* __restrict__
     const int oh = (int)(r % OH);
     const int64_t n = r / OH;
     const int64_t poff = win * C + c8 * 8;
-    const u32x4 pv = ok ? *(const u32x4*)(dP + poff) : u32x4{0u, 0u, 0u, 0u};
-    const u32x2 av = ok ? *(const u32x2*)(arg + poff) : u32x2{0u, 0u};
+    // unconditional loads (clamped index: win = 0 past the end), all issued up front
+    const u32x4 pv = *(const u32x4*)(dP + poff);
+    const u32x2 av = *(const u32x2*)(arg + poff);
+    u32x4 xq[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int ih = 2 * oh + (d >> 1), iw = 2 * ow + (d & 1);
+      xq[d] = *(const u32x4*)(x + ((n * H + ih) * W + iw) * C + c8 * 8);
+    }
     float pg[8];
     unpack8(pv, pg);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       const int ih = 2 * oh + (d >> 1), iw = 2 * ow + (d & 1);
       const int64_t xoff = ((n * H + ih) * W + iw) * C + c8 * 8;
-      const u32x4 xv = ok ? *(const u32x4*)(x + xoff) : u32x4{0u, 0u, 0u, 0u};
+      const u32x4 xv = xq[d];
       float v[8], g[8], w[8], s[8], u[8];
       unpack8(xv, v);
 #pragma unroll

@@ -33,6 +33,10 @@ TARGET_BLOCKS = 2048
 # 0.744 ms).  Gather-bound im2col weight gradients and many-tile dense ones
 # (reference CNN conv2 / local3) measured faster at 2048 (4.16 vs 4.78 ms/step).
 TARGET_BLOCKS_FEW_TILES = int(os.environ.get("MNISTX_WGRAD_BLOCKS", "512"))
+# 128x128-tile dense weight gradients (reference local3): ~2 splits (bench/micro_wgrad.py
+# ref: S=2 155.9 us, S=3 165.0, S=8 154.4, S=16 197.1 -- the fewest splits that fill
+# the GPU keep the slab smallest)
+TARGET_BLOCKS_BIG_TILES = 400
 
 def pad8(c: int) -> int:
     return (c + 7) // 8 * 8
@@ -51,7 +55,7 @@ def gemm_tile(M: int, N: int) -> Tuple[int, int]:
         return 64, 64
     if N <= 128:        # the whole N in one tile: the M operand is read once
         return (64, 128) if M >= 256 else (64, 64)
-    if math.ceil(M / 128) * math.ceil(N / 128) < 256:
+    if math.ceil(M / 128) * math.ceil(N / 128) < 128:
         return 64, 64
     return 128, 128
 
@@ -68,7 +72,10 @@ def pick_splits(M: int, N: int, K: int, target: Optional[int] = None, min_k: int
     bm, bn = (64, 64) if grouped else gemm_tile(M, N)
     tiles = math.ceil(M / bm) * math.ceil(N / bn)
     if target is None:
-        target = TARGET_BLOCKS_FEW_TILES if (dense and tiles < 64) else TARGET_BLOCKS
+        if dense and (bm, bn) == (128, 128):
+            target = TARGET_BLOCKS_BIG_TILES
+        else:
+            target = TARGET_BLOCKS_FEW_TILES if (dense and tiles < 64) else TARGET_BLOCKS
     s = max(1, math.ceil(target / tiles))
     s = min(s, max(1, K // min_k), max(1, SLAB_CAP // max(1, M * N)))
     return eff_splits(K, s)

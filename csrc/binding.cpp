@@ -638,7 +638,8 @@ void convpool_fwd(Tensor x, Tensor w, Tensor bias, int64_t bias_n, Tensor pooled
 }
 
 void convpool_wgrad(Tensor x, Tensor dP, Tensor arg, Tensor slab, int64_t grid, int64_t B, int64_t cin, int64_t cout,
-                    int64_t ks, int64_t pad, int64_t h, int64_t wd, optional<Tensor> u8, optional<Tensor> idx) {
+                    int64_t ks, int64_t pad, int64_t h, int64_t wd, optional<Tensor> u8, optional<Tensor> idx,
+                    optional<Tensor> lrn_p, double lrn_bias, double lrn_alpha, double lrn_beta, int64_t lrn_r) {
   auto g = cp_geo(cin, cout, ks, pad, h, wd);
   TORCH_CHECK(grid >= 1 && grid <= 65535, "grid");
   const int64_t np = B * g.PH * g.PW * cout;
@@ -646,8 +647,14 @@ void convpool_wgrad(Tensor x, Tensor dP, Tensor arg, Tensor slab, int64_t grid, 
   check(dP, at::kBFloat16, np, "dP");
   check(arg, at::kByte, np, "arg");
   check(slab, at::kFloat, grid * g.KM * cout, "slab");
+  const mnistx::bf16_t* lp = nullptr;
+  if (lrn_p.has_value() && lrn_p->defined()) {
+    TORCH_CHECK(lrn_r == 4 && cout == 32 && (g.cfg == 2 || g.cfg == 3), "LRN fold: reference conv1 (Cout 32), radius 4");
+    check(*lrn_p, at::kBFloat16, np, "lrn_p");
+    lp = BF(*lrn_p);
+  }
   hip_ok(mnistx::convpool_wgrad(g.cfg, src, BF(dP), P<const uint8_t>(arg), (int)B, P<float>(slab), (int)grid,
-                                cur_stream()),
+                                cur_stream(), lp, (float)lrn_bias, (float)lrn_alpha, (float)lrn_beta),
          "convpool_wgrad");
 }
 
@@ -938,7 +945,8 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("pad"), py::arg("h"), py::arg("w_"), py::arg("u8") = py::none(), py::arg("idx") = py::none());
   m.def("convpool_wgrad", &convpool_wgrad, py::arg("x"), py::arg("dP"), py::arg("arg"), py::arg("slab"),
         py::arg("grid"), py::arg("B"), py::arg("cin"), py::arg("cout"), py::arg("ks"), py::arg("pad"), py::arg("h"),
-        py::arg("w_"), py::arg("u8") = py::none(), py::arg("idx") = py::none());
+        py::arg("w_"), py::arg("u8") = py::none(), py::arg("idx") = py::none(), py::arg("lrn_p") = py::none(),
+        py::arg("lrn_bias") = 0.0, py::arg("lrn_alpha") = 0.0, py::arg("lrn_beta") = 0.0, py::arg("lrn_r") = 0);
   m.def("convpool_u8_input", &convpool_u8_input);
   m.def("convpool_dgrad", &convpool_dgrad, py::arg("dP"), py::arg("arg"), py::arg("w"), py::arg("dx"), py::arg("B"),
         py::arg("cin"), py::arg("cout"), py::arg("ks"), py::arg("pad"), py::arg("h"), py::arg("w_"),

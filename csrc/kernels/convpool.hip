@@ -29,6 +29,7 @@
 // conv blocks.
 #include "common.h"
 #include "launchers.h"
+#include "lrn_math.h"
 
 #include <cstdlib>
 
@@ -167,6 +168,15 @@ DEV uint32_t half_eq_mask(uint32_t e, uint32_t d) {
 DEV float pos_clear(float v) { return __uint_as_float(__float_as_uint(v) & ~3u); }
 
 constexpr int NTH = 256;
+
+// A following LRN folded into a weight gradient's dY staging (reference CNN norm1
+// after conv1+pool1): the kernel reads dL/d(LRN output) and the LRN input (= the
+// pooled activations) and applies the LRN backward while staging, so the pool-level
+// gradient never goes to HBM.  p == nullptr: no fold.
+struct LrnFold {
+  const bf16_t* p;
+  float bias, alpha, beta;
+};
 // Minimum waves per SIMD the register allocator must leave room for (the
 // __launch_bounds__ second argument).  LeNet conv2 fwd fits 93 VGPRs (5 waves, was
 // 4 at 106) and its wgrad 167 (3 waves, was 2 at 172) without spills; the
@@ -274,14 +284,41 @@ DEV void make_shifted(bf16_t* tile, int tid) {
 }
 
 // Pooled gradient + argmax bytes ([img][window][Cout]), 8 channels per vector.
-template <class G, int IMGS>
+// LRNB: y is dL/d(LRN output) and p the LRN input (LrnFold); store() stages the
+// LRN backward of them (bitwise lrn_bwd_k: same lrn_bwd8, same bf16 rounding).
+template <class G, int IMGS, bool LRNB = false>
 struct DYStage {
   static constexpr int NWC = G::NWIN * G::COUT;
   static constexpr int NV = IMGS * NWC / 8;
   static constexpr int PER = (NV + NTH - 1) / NTH;
   static_assert(NWC % 8 == 0, "");
+  static_assert(!LRNB || (G::COUT == 32 && NTH % (G::COUT / 8) == 0), "LRN fold: 4 lanes per pixel, radius 4");
   u32x4 y[PER];
   u32x2 a[PER];
+  u32x4 p[LRNB ? PER : 1];
+  DEV void load_lrn(const bf16_t* __restrict__ P, int img0, int B, int tid) {
+    if constexpr (LRNB) {
+      const int nimg = max(0, min(IMGS, B - img0));
+      const auto rp = buf_rsrc(P + (int64_t)img0 * NWC, (uint32_t)(nimg * NWC * 2));
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int e = 8 * (tid + u * NTH);
+        p[u] = buf_b128(rp, e < IMGS * NWC ? (uint32_t)(e * 2) : BUF_OOB);
+      }
+    }
+  }
+  // LRN backward in place (every lane takes part: the DPP exchanges read neighbours).
+  // One vector at a time (scheduling barriers): interleaving all of them cost ~100
+  // VGPRs of temporaries and two waves per SIMD.
+  DEV void apply_lrn(const LrnFold& f, int tid) {
+    if constexpr (LRNB) {
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        y[u] = lrn_bwd8<G::COUT / 8, 4>(p[u], y[u], tid % (G::COUT / 8), f.bias, f.alpha, f.beta, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
   // branch-free buffer loads: slots past the batch read dP = 0 and arg = 0, which
   // contribute nothing (every consumer multiplies / selects dP by the argmax)
   DEV void load(const bf16_t* __restrict__ dP, const uint8_t* __restrict__ arg, int img0, int B, int tid) {
@@ -699,10 +736,10 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
 // with ds_read_b64_tr_b16: each lane supplies one pixel row and one 4-column
 // chunk; the bias row (k = KE) reads a constant [1,0,0,0] LDS cell.  dY is
 // rebuilt from (dP, arg): position d of a window gets dP iff arg == d.
-template <class G, int IMGS>
+template <class G, int IMGS, bool LRNB = false>
 __global__ __launch_bounds__(NTH, wgrad_minw<G>()) void convpool_wgrad_k(const XSrc x, const bf16_t* __restrict__ dP,
                                                         const uint8_t* __restrict__ arg, int B,
-                                                        float* __restrict__ slab) {
+                                                        float* __restrict__ slab, const LrnFold lrn) {
   constexpr int CELL = IMGS * G::IMG_LDS;             // [1,0,0,0] then [0,0,0,0]
   constexpr int LDS = (CELL + 8 + 7) / 8 * 8;
   __shared__ __attribute__((aligned(16))) bf16_t tile[LDS];
@@ -740,14 +777,16 @@ __global__ __launch_bounds__(NTH, wgrad_minw<G>()) void convpool_wgrad_k(const X
 
   const int stride = gridDim.x * IMGS;
   XStage<G, IMGS> xs;
-  DYStage<G, IMGS> ys;
+  DYStage<G, IMGS, LRNB> ys;
   xs.fetch_rows(x, blockIdx.x * IMGS, B);
   xs.load(x, blockIdx.x * IMGS, B, tid);
   xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
   ys.load(dP, arg, blockIdx.x * IMGS, B, tid);
+  ys.load_lrn(lrn.p, blockIdx.x * IMGS, B, tid);
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
     __syncthreads();
     xs.store(tile, tid);
+    ys.apply_lrn(lrn, tid);
     ys.store(dys, args, tid);
     __syncthreads();
     if constexpr (G::MODE == 0) {
@@ -758,6 +797,7 @@ __global__ __launch_bounds__(NTH, wgrad_minw<G>()) void convpool_wgrad_k(const X
       xs.load(x, img0 + stride, B, tid);
       xs.fetch_rows(x, img0 + 2 * stride, B);
       ys.load(dP, arg, img0 + stride, B, tid);
+      ys.load_lrn(lrn.p, img0 + stride, B, tid);
     }
     for (int it = wave; it < IMGS * G::RSTEPS; it += NTH / 64) {
       const int im = it / G::RSTEPS, s = it - im * G::RSTEPS;
@@ -1170,11 +1210,18 @@ hipError_t run_fwd(const XSrc& x, const bf16_t* w, const float* bias, int bias_n
 
 template <class G, int IMGS>
 hipError_t run_wgrad(const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B, float* slab, int grid,
-                     hipStream_t st) {
+                     hipStream_t st, const LrnFold& lrn = LrnFold{nullptr, 0.f, 0.f, 0.f}) {
   if constexpr (G::PAIR) {
+    if (lrn.p) return hipErrorInvalidValue;
     hipLaunchKernelGGL((convpool_wgrad_pair_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab);
+  } else if constexpr (G::COUT == 32) {
+    if (lrn.p)
+      hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS, true>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
+    else
+      hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
   } else {
-    hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab);
+    if (lrn.p) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
   }
   return hipGetLastError();
 }
@@ -1515,13 +1562,20 @@ hipError_t convpool_fwd(int cfg, const XSrc& x, const bf16_t* w, const float* bi
 }
 
 hipError_t convpool_wgrad(int cfg, const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B, float* slab,
-                          int grid, hipStream_t st) {
+                          int grid, hipStream_t st, const bf16_t* lrn_p, float lrn_bias, float lrn_alpha,
+                          float lrn_beta) {
+  const LrnFold lrn{lrn_p, lrn_bias, lrn_alpha, lrn_beta};
+  if (lrn_p && cfg != 2 && cfg != 3) return hipErrorInvalidValue;
   switch (cfg) {
     case 0: return c1_wg_imgs() == 2 ? run_wgrad<LeNetC1, 2>(x, dP, arg, B, slab, grid, st)
                                      : run_wgrad<LeNetC1, WG_IMGS_C1>(x, dP, arg, B, slab, grid, st);
     case 1: return run_wgrad<LeNetC2, 4>(x, dP, arg, B, slab, grid, st);
-    case 2: return run_wgrad<RefC1g, 2>(x, dP, arg, B, slab, grid, st);
-    case 3: return run_wgrad<RefC1c, 2>(x, dP, arg, B, slab, grid, st);
+    // the LRN fold stages one image per group (its LRN input vectors and temporaries
+    // would push the 2-image variant past 256 VGPRs: one wave per SIMD)
+    case 2: return lrn_p ? run_wgrad<RefC1g, 1>(x, dP, arg, B, slab, grid, st, lrn)
+                         : run_wgrad<RefC1g, 2>(x, dP, arg, B, slab, grid, st);
+    case 3: return lrn_p ? run_wgrad<RefC1c, 1>(x, dP, arg, B, slab, grid, st, lrn)
+                         : run_wgrad<RefC1c, 2>(x, dP, arg, B, slab, grid, st);
   }
   return hipErrorInvalidValue;
 }

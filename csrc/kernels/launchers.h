@@ -76,8 +76,11 @@ hipError_t convpool_fwd(int cfg, const XSrc& x, const bf16_t* w, const float* bi
 // backward needs only (dP, arg): arg == 4 marks a window whose ReLU output is 0
 // workgroups that fill every CU once for this geometry's wgrad kernel (occupancy API)
 int convpool_wgrad_grid(int cfg);
+// lrn_p != nullptr (Cout 32 geometries): dP is dL/d(LRN output) of an LRN (radius 4)
+// applied to the pooled output lrn_p; the LRN backward is applied while staging
 hipError_t convpool_wgrad(int cfg, const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B, float* slab,
-                          int grid, hipStream_t st);
+                          int grid, hipStream_t st, const bf16_t* lrn_p = nullptr, float lrn_bias = 0.f,
+                          float lrn_alpha = 0.f, float lrn_beta = 0.f);
 int convpool_has_dgrad(int cfg);
 hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int B, bf16_t* dx,
                           int grid_cap, hipStream_t st);

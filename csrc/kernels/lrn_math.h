@@ -1,0 +1,96 @@
+// LRN (tf.nn.local_response_normalization) building blocks shared by the LRN kernels
+// (misc.hip) and the kernels that fold an LRN into their staging (convpool.hip).
+// Channel-parallel: each lane owns 8 channels (one 16-byte bf16 vector) of a pixel,
+// the C/8 lanes of a pixel sit side by side inside one 16-lane DPP row, and the R
+// channels a window needs from the neighbouring vectors come over DPP row shifts
+// (zeroed at the pixel's first / last vector).
+#pragma once
+#include "common.h"
+
+namespace mnistx {
+namespace {
+
+DEV float dpp_from_left(float v) {   // lane i <- lane i-1 within its 16-lane row (0 at the row start)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, true));
+}
+DEV float dpp_from_right(float v) {  // lane i <- lane i+1 within its 16-lane row (0 at the row end)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x101, 0xf, 0xf, true));
+}
+
+// window sums over channels of the 8 values of this lane, with the R neighbours on
+// either side taken from the adjacent lanes of the same pixel (G lanes per pixel)
+template <int G, int R>
+DEV void lane_window_sums(const float (&v)[8], int c8, float (&s)[8]) {
+  static_assert(R <= 8 && 16 % G == 0, "neighbours must come from the adjacent lane of one DPP row");
+  float e[8 + 2 * R];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) e[R + j] = v[j];
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    float l = dpp_from_left(v[8 - R + k]), r = dpp_from_right(v[k]);
+    if constexpr (G == 1) {
+      l = 0.f;
+      r = 0.f;
+    }
+    e[k] = c8 == 0 ? 0.f : l;
+    e[R + 8 + k] = c8 == G - 1 ? 0.f : r;
+  }
+  // sliding window: one full sum, then +entering -leaving (inputs are non-negative
+  // squares or same-scale products, so the running form loses nothing at bf16 output)
+  float a = 0.f;
+#pragma unroll
+  for (int d = 0; d <= 2 * R; ++d) a += e[d];
+  s[0] = a;
+#pragma unroll
+  for (int j = 1; j < 8; ++j) {
+    a += e[j + 2 * R] - e[j - 1];
+    s[j] = a;
+  }
+}
+
+// x^p for x > 0 as exp2(p log2 x): two transcendental ops, no ln/log2e rescaling
+DEV float powp(float x, float p) { return __builtin_amdgcn_exp2f(p * __builtin_amdgcn_logf(x)); }
+
+DEV void unpack8(const u32x4& u, float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = u4_get(u, j);
+}
+
+
+// LRN backward of one 8-channel vector (x = LRN input, g = dL/dy; G lanes per pixel):
+// dx[c] = g[c] s[c]^-b - 2ab x[c] sum_{|c'-c|<=R} g[c'] x[c'] s[c']^(-b-1), s = bias +
+// alpha * window sum of x^2; relu_mask zeroes dx where x <= 0.  Rounded to bf16.
+template <int G, int R>
+DEV u32x4 lrn_bwd8(const u32x4& xv, const u32x4& gv, int c8, float bias, float alpha, float beta, int relu_mask) {
+  float v[8], g[8], w[8], s[8], u[8];
+  unpack8(xv, v);
+  unpack8(gv, g);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) w[j] = v[j] * v[j];
+  lane_window_sums<G, R>(w, c8, s);             // s = window sum of x^2
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float sc = bias + alpha * s[j];
+    const float pw = powp(sc, -beta);               // sc^-beta
+    s[j] = pw;
+    w[j] = g[j] * v[j] * pw * __builtin_amdgcn_rcpf(sc);
+  }
+  lane_window_sums<G, R>(w, c8, u);
+  u32x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float r2[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = 2 * j + h;
+      float d = g[c] * s[c] - 2.f * alpha * beta * v[c] * u[c];
+      if (relu_mask && !(v[c] > 0.f)) d = 0.f;
+      r2[h] = d;
+    }
+    o[j] = pack2(r2[0], r2[1]);
+  }
+  return o;
+}
+
+}  // namespace
+}  // namespace mnistx

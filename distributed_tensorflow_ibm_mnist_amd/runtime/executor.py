@@ -168,9 +168,18 @@ class ConvPoolLayer(_Layer):
     fused_grid = 0
     skip_dgrad = False
 
+    # (LRN spec, dL/d(LRN output)): the following LRN's backward is applied inside this
+    # layer's weight-gradient staging (reference CNN norm1, HipNet.fold_lrn)
+    lrn_fold: Optional[tuple] = None
+
     def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor, red: Optional[list] = None) -> None:
         K = kernels()
-        if self.fused_dgrad is not None:
+        if self.lrn_fold is not None:
+            ls, dn = self.lrn_fold
+            grid = min(self.grid, max(1, (nb + 3) // 4))
+            K.convpool_wgrad(self.x, dn, self.arg, slab, grid, nb, *self._geo(), **self._src(), lrn_p=self.out,
+                             lrn_bias=ls.bias, lrn_alpha=ls.alpha, lrn_beta=ls.beta, lrn_r=ls.depth_radius)
+        elif self.fused_dgrad is not None:
             dy2, l1 = self.fused_dgrad
             grid = min(self.fused_grid, max(1, nb))
             K.lenet_c2dgrad_c1wgrad(self.x, dy2, l1.arg, self.fp.bf16_view(l1.wname), self.arg, slab, grid, nb,
@@ -222,10 +231,12 @@ class LRNLayer(_Layer):
         kernels().lrn_fwd(self.x, self.out, self._p(nb), self.C, s.depth_radius, s.bias, s.alpha, s.beta)
 
     def bwd_data(self, nb: int, dy, dx) -> None:
-        if dx is not None:
+        if dx is not None and not self.skip_bwd:
             s = self.spec
             kernels().lrn_bwd(self.x, dy, dx, self._p(nb), self.C, s.depth_radius, s.bias, s.alpha, s.beta,
                               self.in_relu)
+
+    skip_bwd = False   # the preceding conv+pool layer applies this LRN's backward (HipNet.fold_lrn)
 
 
 class LRNPoolLayer(_Layer):
@@ -468,6 +479,17 @@ class HipNet:
         # bound by LDS/VALU latency at 3 waves/SIMD, not by the 400 MB it saves.
         self.fuse_c2d_c1w = self._find_c2d_c1w() and not self.overlap and \
             os.environ.get("MNISTX_FUSE_C2D_C1W", "0") == "1"
+        # reference CNN: norm1's backward runs in conv1's weight-gradient staging (reads
+        # dL/d norm1 + pool1, no pool-level gradient in HBM, no lrn_bwd launch)
+        self.fold_lrn = False
+        if dev.type == "cuda" and not self.overlap and os.environ.get("MNISTX_FOLD_LRN", "1") != "0":
+            for k in range(len(self.layers) - 1):
+                a, b = self.layers[k], self.layers[k + 1]
+                if (isinstance(a, ConvPoolLayer) and a.cfg in (2, 3) and isinstance(b, LRNLayer) and b.x is a.out
+                        and b.spec.depth_radius == 4 and b.C == 32 and k == 0):
+                    a.lrn_fold = (b.spec, self.dbuf[k + 2])   # dL/d(LRN output) = the LRN's incoming gradient
+                    b.skip_bwd = True
+                    self.fold_lrn = True
         if self.fuse_c2d_c1w:
             l0, l1 = self.layers[0], self.layers[1]
             l0.fused_grid = min(l0.grid, kernels().lenet_c2dgrad_c1wgrad_grid())

@@ -212,3 +212,34 @@ def test_lenet_fused_c2dgrad_c1wgrad(dev, K, B, monkeypatch):
             assert rel_err(fused[n], ref[n]) < 1e-5, n
         else:
             assert torch.equal(fused[n], ref[n]), n
+
+
+@pytest.mark.parametrize("cin", [1, 3])
+def test_refcnn_lrn1_backward_fold(dev, K, cin, monkeypatch):
+    """norm1's backward applied inside conv1's weight-gradient staging (HipNet.fold_lrn)
+    vs lrn_bwd + the plain conv1 wgrad: every other gradient bitwise, conv1's to fp32
+    reassociation (the folded kernel stages one image per group)."""
+    spec = get_model("reference_cnn", cin)
+    init = torch_ref.init_params(spec, seed=5)
+    B = 70
+    x = (torch.rand(B, 28, 28, cin, device=dev) - 0.5).to(torch.bfloat16)
+    y = torch.randint(0, 10, (B,), device=dev, dtype=torch.int32)
+
+    def grads(fold: str):
+        monkeypatch.setenv("MNISTX_FOLD_LRN", fold)
+        net = HipNet(spec, B, dev, init, OptConfig(lr0=0.05))
+        assert net.fold_lrn == (fold == "1")
+        net.x0.copy_(x)
+        net.labels.copy_(y)
+        net.forward(defer_head=True)
+        net.loss_and_grad()
+        net.backward()
+        torch.cuda.synchronize()
+        return {n: net.fp.grad_view(n).clone() for n in init}
+
+    ref, fold = grads("0"), grads("1")
+    for n in init:
+        if n.startswith("conv1/"):
+            assert rel_err(fold[n], ref[n]) < 1e-5, n
+        else:
+            assert torch.equal(fold[n], ref[n]), n

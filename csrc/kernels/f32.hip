@@ -24,7 +24,9 @@
 namespace mnistx {
 namespace {
 
-constexpr int FBM = 64, FBN = 64, FBK = 16, FNT = 256;
+constexpr int FBM = 64, FBN = 64, FBK = 32, FNT = 256;
+constexpr int FVPT = FBM * FBK / 4 / FNT;   // 4-element vectors per thread per operand tile
+static_assert(FBM == FBN && FVPT * 4 * FNT == FBM * FBK, "tile staging");
 constexpr int FLD = FBM + 4;   // LDS row stride (floats)
 
 // ---------------------------------------------------------------- loaders
@@ -182,22 +184,30 @@ struct EpiF {
   int64_t slab_stride;
 };
 
-// Tile staging: 64 rows x 16 k = 256 four-element vectors, one per thread, taken along
+// Tile staging: 64 rows x FBK k = FVPT four-element vectors per thread, taken along
 // the operand's contiguous direction; LDS keeps the tile k-major ([k][row]).
 template <class L>
-DEV f32x4 stage_load(const L& ld, int r0, int k0, int tid) {
-  if constexpr (L::KC) return ld.load4(r0 + (tid >> 2), k0 + 4 * (tid & 3));
-  else return ld.load4(r0 + 4 * (tid & 15), k0 + (tid >> 4));
+DEV void stage_load(const L& ld, int r0, int k0, int tid, f32x4 (&v)[FVPT]) {
+#pragma unroll
+  for (int i = 0; i < FVPT; ++i) {
+    const int idx = tid + i * FNT;
+    if constexpr (L::KC) v[i] = ld.load4(r0 + idx / (FBK / 4), k0 + 4 * (idx % (FBK / 4)));
+    else v[i] = ld.load4(r0 + 4 * (idx % (FBM / 4)), k0 + idx / (FBM / 4));
+  }
 }
 
 template <class L>
-DEV void stage_store(float* lds, int tid, const f32x4& v) {
-  if constexpr (L::KC) {
-    const int r = tid >> 2, k = 4 * (tid & 3);
+DEV void stage_store(float* lds, int tid, const f32x4 (&v)[FVPT]) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) lds[(k + i) * FLD + r] = v[i];
-  } else {
-    *(f32x4*)(lds + (tid >> 4) * FLD + 4 * (tid & 15)) = v;
+  for (int i = 0; i < FVPT; ++i) {
+    const int idx = tid + i * FNT;
+    if constexpr (L::KC) {
+      const int r = idx / (FBK / 4), k = 4 * (idx % (FBK / 4));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) lds[(k + j) * FLD + r] = v[i][j];
+    } else {
+      *(f32x4*)(lds + (idx / (FBM / 4)) * FLD + 4 * (idx % (FBM / 4))) = v[i];
+    }
   }
 }
 
@@ -218,10 +228,10 @@ __global__ __launch_bounds__(FNT) void gemm_f32_k(AL A, BL Bm, int M, int N, int
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 va = {0.f, 0.f, 0.f, 0.f}, vb = {0.f, 0.f, 0.f, 0.f};
+  f32x4 va[FVPT], vb[FVPT];
   if (kb < ke) {
-    va = stage_load(A, m0, kb, tid);
-    vb = stage_load(Bm, n0, kb, tid);
+    stage_load(A, m0, kb, tid, va);
+    stage_load(Bm, n0, kb, tid, vb);
   }
   int buf = 0;
   for (int k0 = kb; k0 < ke; k0 += FBK) {
@@ -229,8 +239,8 @@ __global__ __launch_bounds__(FNT) void gemm_f32_k(AL A, BL Bm, int M, int N, int
     stage_store<BL>(Bs[buf], tid, vb);
     __syncthreads();
     if (k0 + FBK < ke) {
-      va = stage_load(A, m0, k0 + FBK, tid);
-      vb = stage_load(Bm, n0, k0 + FBK, tid);
+      stage_load(A, m0, k0 + FBK, tid, va);
+      stage_load(Bm, n0, k0 + FBK, tid, vb);
     }
     const float* as = As[buf];
     const float* bs = Bs[buf];

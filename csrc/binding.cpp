@@ -171,15 +171,20 @@ std::vector<int64_t> dense_wgrad_group(std::vector<Tensor> x, std::vector<Tensor
   return std::vector<int64_t>(sp, sp + n);
 }
 
+mnistx::LrnParams lrn_params(int64_t lrn_r, double b, double a, double be) {
+  TORCH_CHECK(lrn_r == 0 || lrn_r == 4, "LRN fold: depth_radius 4 only");
+  return mnistx::LrnParams{(float)b, (float)a, (float)be, lrn_r == 4 ? 1 : 0};
+}
+
 void conv_fwd(Tensor x, Tensor w, Tensor out, int64_t Nb, int64_t H, int64_t W, int64_t C, int64_t OH, int64_t OW,
               int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t Cout, optional<Tensor> bias, int64_t bias_n,
-              bool relu) {
+              bool relu, int64_t lrn_r, double lrn_bias, double lrn_alpha, double lrn_beta) {
   check(x, at::kBFloat16, Nb * H * W * C, "x");
   check(w, at::kBFloat16, KH * KW * C * Cout, "w");
   TORCH_CHECK(Cout % 8 == 0, "Cout must be padded to a multiple of 8");
   auto ep = make_epi(out, Nb * OH * OW, Cout, Cout, bias, bias_n, relu, c10::nullopt, 0);
   hip_ok(mnistx::conv_fwd(BF(x), BF(w), (int)Nb, (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)KH, (int)KW, (int)ph,
-                          (int)pw, (int)Cout, ep, cur_stream()),
+                          (int)pw, (int)Cout, ep, cur_stream(), lrn_params(lrn_r, lrn_bias, lrn_alpha, lrn_beta)),
          "conv_fwd");
 }
 
@@ -196,7 +201,7 @@ void conv_dgrad(Tensor dy, Tensor w, Tensor out, int64_t Nb, int64_t OH, int64_t
 
 int64_t conv_wgrad(Tensor x, Tensor dy, Tensor slab, int64_t Nb, int64_t H, int64_t W, int64_t C, int64_t OH,
                    int64_t OW, int64_t KH, int64_t KW, int64_t ph, int64_t pw, int64_t Cout, bool with_bias,
-                   int64_t splits) {
+                   int64_t splits, int64_t lrn_r, double lrn_bias, double lrn_alpha, double lrn_beta) {
   check(x, at::kBFloat16, Nb * H * W * C, "x");
   check(dy, at::kBFloat16, Nb * OH * OW * Cout, "dy");
   TORCH_CHECK(Cout % 8 == 0, "Cout must be padded to a multiple of 8");
@@ -209,7 +214,8 @@ int64_t conv_wgrad(Tensor x, Tensor dy, Tensor slab, int64_t Nb, int64_t H, int6
                          : eff_splits(Nb * OH * OW, splits);
   auto ep = make_slab(slab, S, M, Cout);
   hip_ok(mnistx::conv_wgrad(BF(x), BF(dy), (int)Nb, (int)H, (int)W, (int)C, (int)OH, (int)OW, (int)KH, (int)KW,
-                            (int)ph, (int)pw, (int)Cout, with_bias ? 1 : 0, (int)S, ep, cur_stream()),
+                            (int)ph, (int)pw, (int)Cout, with_bias ? 1 : 0, (int)S, ep, cur_stream(),
+                            lrn_params(lrn_r, lrn_bias, lrn_alpha, lrn_beta)),
          "conv_wgrad");
   return S;
 }
@@ -897,10 +903,16 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("dense_dgrad", &dense_dgrad);
   m.def("dense_wgrad", &dense_wgrad, py::arg("x"), py::arg("dy"), py::arg("slab"), py::arg("Din"), py::arg("Dout"),
         py::arg("B"), py::arg("ldx"), py::arg("lddy"), py::arg("with_bias"), py::arg("splits"), py::arg("tile") = -1);
-  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("out"), py::arg("Nb"), py::arg("H"), py::arg("W"),
+        py::arg("C"), py::arg("OH"), py::arg("OW"), py::arg("KH"), py::arg("KW"), py::arg("ph"), py::arg("pw"),
+        py::arg("Cout"), py::arg("bias"), py::arg("bias_n"), py::arg("relu"), py::arg("lrn_r") = 0,
+        py::arg("lrn_bias") = 0.0, py::arg("lrn_alpha") = 0.0, py::arg("lrn_beta") = 0.0);
   m.def("set_halo_variants", [](int64_t f, int64_t d) { mnistx::set_halo_variants((int)f, (int)d); });
   m.def("conv_dgrad", &conv_dgrad);
-  m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("slab"), py::arg("Nb"), py::arg("H"),
+        py::arg("W"), py::arg("C"), py::arg("OH"), py::arg("OW"), py::arg("KH"), py::arg("KW"), py::arg("ph"),
+        py::arg("pw"), py::arg("Cout"), py::arg("with_bias"), py::arg("splits"), py::arg("lrn_r") = 0,
+        py::arg("lrn_bias") = 0.0, py::arg("lrn_alpha") = 0.0, py::arg("lrn_beta") = 0.0);
   m.def("prep_images", &prep_images);
   m.def("dense_wgrad_group", &dense_wgrad_group);
   m.def("conv_wgrad_pref_splits", &conv_wgrad_pref_splits);

@@ -21,6 +21,7 @@
 // mnist_input.py:161 (reference CNN); the gemm.hip launchers route to it.
 #include "common.h"
 #include "launchers.h"
+#include "lrn_math.h"
 
 #include <cstdlib>
 
@@ -52,11 +53,14 @@ DEV int swz(int r, int c) {
 // MODE 1 = data gradient: out[p][n] = mask * sum_{tap,ci} dy[p+tap][ci] W[24-tap][n][ci]
 //   (W is the conv's [kh][kw][cin][cout] filter; here ci runs over the conv's
 //    output channels and n over its input channels)
-template <int CIN, int CW, int NW, int MODE, int FR, int IMGS>
+// LRNX: x is the input of an LRN (radius 4) whose output is the convolution's input;
+// the LRN is applied to each staged 16-byte vector (the CH lanes of a pixel are
+// adjacent), bitwise lrn_fwd_k, so the LRN output never exists in HBM.
+template <int CIN, int CW, int NW, int MODE, int FR, int IMGS, bool LRNX = false>
 __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                         int wcin, int wcout, const float* __restrict__ bias, int bias_n,
                                                         int relu, const bf16_t* __restrict__ mask, int ldm, int B,
-                                                        bf16_t* __restrict__ out, int ldo) {
+                                                        bf16_t* __restrict__ out, int ldo, const LrnParams lrn) {
   constexpr int NT = 64 * NW;
   constexpr int CH = CIN / 8;                 // 16-byte chunks per pixel / filter row
   constexpr int NF = CW / 16;
@@ -120,6 +124,14 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict
   gload(blockIdx.x * IMGS);
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += gstride) {
     __syncthreads();                            // previous group's fragments consumed
+    if constexpr (LRNX) {                       // every lane: the DPP exchanges read neighbours
+      static_assert(CH == 4 && NT % CH == 0, "LRN fold: 32 channels = 4 lanes per pixel");
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        pre[u] = lrn_fwd8<CH, 4>(pre[u], tid % CH, lrn.bias, lrn.alpha, lrn.beta);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int v = tid + u * NT;
@@ -218,10 +230,10 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict
 // +16 = the next row).  The pixel padding (columns 14/15) multiplies zero dY.
 // One fp32 partial per block goes to the split-K slab ([S][25*CIN+1][COUT] rows
 // (tap*CIN + ci), bias row 25*CIN), reduced by splitk_reduce like the GEMM path.
-template <int CIN, int COUT, int NW>
+template <int CIN, int COUT, int NW, bool LRNX = false>
 __global__ __launch_bounds__(64 * NW) void conv5_halo_wgrad_k(const bf16_t* __restrict__ x,
                                                               const bf16_t* __restrict__ dy, int B,
-                                                              float* __restrict__ slab) {
+                                                              float* __restrict__ slab, const LrnParams lrn) {
   constexpr int NT = 64 * NW;
   constexpr int SX = CIN + 16, SD = COUT + 16;          // tr-read row strides (gemm.hip ImgStride rule)
   constexpr int XP = HP * HP + 8;                       // tile pixels + zero over-read slack
@@ -268,6 +280,14 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_wgrad_k(const bf16_t* __re
   gload(blockIdx.x);
   for (int img = blockIdx.x; img < B; img += gridDim.x) {
     __syncthreads();
+    if constexpr (LRNX) {   // x is the LRN input: normalise while staging (bitwise lrn_fwd_k)
+      static_assert(CIN == 32 && NT % 4 == 0, "LRN fold: 4 lanes per pixel");
+#pragma unroll
+      for (int u = 0; u < PX; ++u) {
+        px[u] = lrn_fwd8<CIN / 8, 4>(px[u], tid % (CIN / 8), lrn.bias, lrn.alpha, lrn.beta);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < PX; ++u) {
       const int v = tid + u * NT;
@@ -349,12 +369,12 @@ int halo_wgrad_resident() {
   return per;
 }
 
-template <int CIN, int CW, int NW, int MODE, int FR, int IMGS>
+template <int CIN, int CW, int NW, int MODE, int FR, int IMGS, bool LRNX = false>
 int halo_grid(int B) {
   static int per = -1;
   if (per < 0) {
     int dev = 0, cus = 0, pc = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, conv5_halo_k<CIN, CW, NW, MODE, FR, IMGS>, 64 * NW, 0) ==
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, conv5_halo_k<CIN, CW, NW, MODE, FR, IMGS, LRNX>, 64 * NW, 0) ==
             hipSuccess &&
         hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && pc > 0)
@@ -366,13 +386,14 @@ int halo_grid(int B) {
   return groups < per ? groups : per;
 }
 
-template <int CIN, int CW, int NW, int MODE, int FR, int IMGS = 1>
+template <int CIN, int CW, int NW, int MODE, int FR, int IMGS = 1, bool LRNX = false>
 hipError_t run_halo(const bf16_t* x, const bf16_t* w, int wcin, int wcout, const float* bias, int bias_n, int relu,
-                    const bf16_t* mask, int ldm, int B, bf16_t* out, int ncols, int ldo, hipStream_t st) {
+                    const bf16_t* mask, int ldm, int B, bf16_t* out, int ncols, int ldo, hipStream_t st,
+                    LrnParams lrn = LrnParams{0.f, 0.f, 0.f, 0}) {
   if (B <= 0) return hipSuccess;
-  dim3 grid(halo_grid<CIN, CW, NW, MODE, FR, IMGS>(B), ncols / CW);
-  hipLaunchKernelGGL((conv5_halo_k<CIN, CW, NW, MODE, FR, IMGS>), grid, dim3(64 * NW), 0, st, x, w, wcin, wcout, bias, bias_n,
-                     relu, mask, ldm, B, out, ldo);
+  dim3 grid(halo_grid<CIN, CW, NW, MODE, FR, IMGS, LRNX>(B), ncols / CW);
+  hipLaunchKernelGGL((conv5_halo_k<CIN, CW, NW, MODE, FR, IMGS, LRNX>), grid, dim3(64 * NW), 0, st, x, w, wcin, wcout, bias,
+                     bias_n, relu, mask, ldm, B, out, ldo, lrn);
   return hipGetLastError();
 }
 
@@ -403,7 +424,10 @@ static int halo_variant(const char* name, int dflt) {
 // beat bigger per-wave tiles: 8 waves x 2 row fragments 350 us fwd / 326 us dgrad vs
 // 4 x 4 fragments 435 / 520 us.
 hipError_t conv5_halo_fwd(const bf16_t* x, const bf16_t* w, int Nb, int C, int Cout, const float* bias, int bias_n,
-                          int relu, bf16_t* out, hipStream_t st) {
+                          int relu, bf16_t* out, hipStream_t st, LrnParams lrn) {
+  if (lrn.on)   // norm1 folded into the staging: the default launch shape only
+    return run_halo<32, 32, 8, 0, 2, 1, true>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st,
+                                               lrn);
   const int v = halo_variant("MNISTX_HALO_FWD", 0);
   switch (v) {
     case 1:   // whole Cout per block (NF = 4): 125 KB LDS, 1 block / CU
@@ -456,9 +480,13 @@ int conv5_halo_wgrad_grid(int Nb) {
   const int r = halo_wgrad_resident<32, 64, 8>();
   return Nb < r ? (Nb < 1 ? 1 : Nb) : r;
 }
-hipError_t conv5_halo_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int grid, float* slab, hipStream_t st) {
+hipError_t conv5_halo_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int grid, float* slab, hipStream_t st,
+                            LrnParams lrn) {
   if (Nb <= 0) return hipSuccess;
-  hipLaunchKernelGGL((conv5_halo_wgrad_k<32, 64, 8>), dim3(grid), dim3(512), 0, st, x, dy, Nb, slab);
+  if (lrn.on)
+    hipLaunchKernelGGL((conv5_halo_wgrad_k<32, 64, 8, true>), dim3(grid), dim3(512), 0, st, x, dy, Nb, slab, lrn);
+  else
+    hipLaunchKernelGGL((conv5_halo_wgrad_k<32, 64, 8>), dim3(grid), dim3(512), 0, st, x, dy, Nb, slab, lrn);
   return hipGetLastError();
 }
 

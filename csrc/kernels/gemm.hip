@@ -776,10 +776,11 @@ bool conv_halo_enabled() {
 static bool halo_enabled() { return conv_halo_enabled(); }
 
 hipError_t conv_fwd(const bf16_t* x, const bf16_t* w, int Nb, int H, int W, int C, int OH, int OW, int KH,
-                    int KW, int ph, int pw, int Cout, const GemmEpi& ep, hipStream_t st) {
-  if (halo_enabled() && ep.mode == EPI_BF16 && ep.ldc == Cout && ep.mask == nullptr &&
-      conv5_halo_fwd_ok(H, W, C, OH, OW, KH, KW, ph, pw, Cout))
-    return conv5_halo_fwd(x, w, Nb, C, Cout, ep.bias, ep.bias_n, ep.relu, (bf16_t*)ep.out, st);
+                    int KW, int ph, int pw, int Cout, const GemmEpi& ep, hipStream_t st, LrnParams lrn) {
+  const bool halo = halo_enabled() && ep.mode == EPI_BF16 && ep.ldc == Cout && ep.mask == nullptr &&
+                    conv5_halo_fwd_ok(H, W, C, OH, OW, KH, KW, ph, pw, Cout);
+  if (halo) return conv5_halo_fwd(x, w, Nb, C, Cout, ep.bias, ep.bias_n, ep.relu, (bf16_t*)ep.out, st, lrn);
+  if (lrn.on) return hipErrorInvalidValue;   // the LRN fold exists in the halo kernels only
   const int M = Nb * OH * OW, K = KH * KW * C;
   Im2colK a{x, H, W, C, OH, OW, KH, KW, ph, pw, M, K,
             FastDiv(OH * OW), FastDiv(OW), FastDiv(C), FastDiv(KW)};
@@ -802,11 +803,12 @@ hipError_t conv_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int OH, int OW,
 
 hipError_t conv_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int H, int W, int C, int OH, int OW, int KH,
                       int KW, int ph, int pw, int Cout, int with_bias, int splits, const GemmEpi& ep,
-                      hipStream_t st) {
+                      hipStream_t st, LrnParams lrn) {
   // halo path: `splits` persistent blocks, one slab partial each (the binding sizes it)
   if (halo_enabled() && ep.mode == EPI_SLAB && ep.ldc == Cout &&
       conv5_halo_wgrad_ok(H, W, C, OH, OW, KH, KW, ph, pw, Cout, with_bias))
-    return conv5_halo_wgrad(x, dy, Nb, splits, (float*)ep.out, st);
+    return conv5_halo_wgrad(x, dy, Nb, splits, (float*)ep.out, st, lrn);
+  if (lrn.on) return hipErrorInvalidValue;
   const int P = Nb * OH * OW, Mreal = KH * KW * C;
   Im2colMN a{x, H, W, C, OH, OW, KH, KW, ph, pw, P, Mreal, with_bias,
              FastDiv(OH * OW), FastDiv(OW), FastDiv(C), FastDiv(KW)};

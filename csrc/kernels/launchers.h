@@ -23,6 +23,13 @@ struct GemmEpi {
   int64_t slab_stride;    // elements between split-K slabs
 };
 
+// An LRN (radius 4, across channels) applied to a conv's input while the conv stages it
+// (reference CNN norm1 -> conv2): x is then the LRN's INPUT.  on == 0: none.
+struct LrnParams {
+  float bias, alpha, beta;
+  int on;
+};
+
 // ---- gemm.hip
 // tile (BM, BN) launch_any picks for an M x N output (wgrad: both operands MN-contiguous)
 void gemm_tile(int M, int N, int wgrad, int* bm, int* bn);
@@ -41,21 +48,23 @@ void set_halo_variants(int fwd, int dgrad);
 bool conv5_halo_fwd_ok(int H, int W, int C, int OH, int OW, int KH, int KW, int ph, int pw, int Cout);
 bool conv5_halo_dgrad_ok(int OH, int OW, int Cout, int H, int W, int KH, int KW, int ph, int pw, int Cin);
 hipError_t conv5_halo_fwd(const bf16_t* x, const bf16_t* w, int Nb, int C, int Cout, const float* bias, int bias_n,
-                          int relu, bf16_t* out, hipStream_t st);
+                          int relu, bf16_t* out, hipStream_t st, LrnParams lrn = LrnParams{0.f, 0.f, 0.f, 0});
 hipError_t conv5_halo_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int Cout, int Cin, const bf16_t* mask,
                             bf16_t* dx, hipStream_t st);
 bool conv5_halo_wgrad_ok(int H, int W, int C, int OH, int OW, int KH, int KW, int ph, int pw, int Cout,
                          int with_bias);
 int conv5_halo_wgrad_grid(int Nb);   // persistent blocks (= slab partials) for Nb images
-hipError_t conv5_halo_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int grid, float* slab, hipStream_t st);
+hipError_t conv5_halo_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int grid, float* slab, hipStream_t st,
+                            LrnParams lrn = LrnParams{0.f, 0.f, 0.f, 0});
 bool conv_halo_enabled();            // MNISTX_CONV_HALO != 0
 hipError_t conv_fwd(const bf16_t* x, const bf16_t* w, int Nb, int H, int W, int C, int OH, int OW, int KH,
-                    int KW, int ph, int pw, int Cout, const GemmEpi& ep, hipStream_t st);
+                    int KW, int ph, int pw, int Cout, const GemmEpi& ep, hipStream_t st,
+                    LrnParams lrn = LrnParams{0.f, 0.f, 0.f, 0});
 hipError_t conv_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int OH, int OW, int Cout, int H, int W,
                       int KH, int KW, int ph, int pw, int Cin, const GemmEpi& ep, hipStream_t st);
 hipError_t conv_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int H, int W, int C, int OH, int OW, int KH,
                       int KW, int ph, int pw, int Cout, int with_bias, int splits, const GemmEpi& ep,
-                      hipStream_t st);
+                      hipStream_t st, LrnParams lrn = LrnParams{0.f, 0.f, 0.f, 0});
 
 // ---- convpool.hip (fused small-channel conv + bias + ReLU + 2x2 max-pool)
 // Input of a fused conv: bf16 NHWC activations, or (Cin == 1 first layer) the

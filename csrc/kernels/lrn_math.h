@@ -57,6 +57,25 @@ DEV void unpack8(const u32x4& u, float (&v)[8]) {
 }
 
 
+// LRN forward of one 8-channel vector (G lanes per pixel): y = x s^-beta, s = bias +
+// alpha * window sum of x^2, rounded to bf16 (bitwise lrn_fwd_k).
+template <int G, int R>
+DEV u32x4 lrn_fwd8(const u32x4& xv, int c8, float bias, float alpha, float beta) {
+  float v[8], sq[8], s[8];
+  unpack8(xv, v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sq[j] = v[j] * v[j];
+  lane_window_sums<G, R>(sq, c8, s);
+  u32x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float a = v[2 * j] * powp(bias + alpha * s[2 * j], -beta);
+    const float b = v[2 * j + 1] * powp(bias + alpha * s[2 * j + 1], -beta);
+    o[j] = pack2(a, b);
+  }
+  return o;
+}
+
 // LRN backward of one 8-channel vector (x = LRN input, g = dL/dy; G lanes per pixel):
 // dx[c] = g[c] s[c]^-b - 2ab x[c] sum_{|c'-c|<=R} g[c'] x[c'] s[c']^(-b-1), s = bias +
 // alpha * window sum of x^2; relu_mask zeroes dx where x <= 0.  Rounded to bf16.

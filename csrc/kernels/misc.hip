@@ -264,18 +264,7 @@ __global__ __launch_bounds__(TPB) void lrn_fwd_k(const bf16_t* __restrict__ x, i
     const int64_t t = base + threadIdx.x;
     const bool ok = t < total;
     const u32x4 xv = *(const u32x4*)(x + (ok ? t : 0) * 8);   // unconditional (clamped) load
-    float v[8], sq[8], s[8];
-    unpack8(xv, v);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sq[j] = v[j] * v[j];
-    lane_window_sums<G, R>(sq, c8, s);
-    u32x4 o;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float a = v[2 * j] * powp(bias + alpha * s[2 * j], -beta);
-      const float b = v[2 * j + 1] * powp(bias + alpha * s[2 * j + 1], -beta);
-      o[j] = pack2(a, b);
-    }
+    const u32x4 o = lrn_fwd8<G, R>(xv, c8, bias, alpha, beta);
     if (ok) *(u32x4*)(y + t * 8) = o;
   }
 }

@@ -86,18 +86,31 @@ class ConvLayer(_Layer):
         self.splits = max(Fk.pick_splits(self.M_wg, self.Cp, B * self.OH * self.OW), self.pref)
         self.slab_elems = self.splits * self.M_wg * self.Cp
 
+    # (LRN spec, LRN input): the preceding LRN is applied while this conv stages its
+    # input (forward and weight gradient), so the LRN output is never written
+    # (HipNet.fold_lrn_fwd; reference CNN norm1 -> conv2 on the LDS-halo kernels)
+    lrn_pre: Optional[tuple] = None
+
+    def _xin(self):
+        if self.lrn_pre is None:
+            return self.x, {}
+        ls, xp = self.lrn_pre
+        return xp, {"lrn_r": ls.depth_radius, "lrn_bias": ls.bias, "lrn_alpha": ls.alpha, "lrn_beta": ls.beta}
+
     def fwd(self, nb: int) -> None:
         s = self.spec
-        kernels().conv_fwd(self.x, self.fp.bf16_view(self.wname), self.out, nb, self.H, self.W, self.C, self.OH,
+        x, lrn = self._xin()
+        kernels().conv_fwd(x, self.fp.bf16_view(self.wname), self.out, nb, self.H, self.W, self.C, self.OH,
                            self.OW, s.kh, s.kw, self.ph, self.pw, self.Cp, self.fp.param_view(self.bname), s.cout,
-                           s.relu)
+                           s.relu, **lrn)
 
     def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor, red: Optional[list] = None) -> None:
         s = self.spec
         K = kernels()
         req = self.pref if self.pref > 0 else Fk.pick_splits(self.M_wg, self.Cp, nb * self.OH * self.OW)
-        S = K.conv_wgrad(self.x, dy, slab, nb, self.H, self.W, self.C, self.OH, self.OW, s.kh, s.kw, self.ph, self.pw,
-                         self.Cp, True, req)
+        x, lrn = self._xin()
+        S = K.conv_wgrad(x, dy, slab, nb, self.H, self.W, self.C, self.OH, self.OW, s.kh, s.kw, self.ph, self.pw,
+                         self.Cp, True, req, **lrn)
         _reduce(red, slab, (S, self.M_wg, self.Cp, s.kh * s.kw, self.C, s.cin, s.cout, s.kh * s.kw * self.C),
                 self.fp.grad_view(self.wname), self.fp.grad_view(self.bname))
 
@@ -226,7 +239,11 @@ class LRNLayer(_Layer):
     def _p(self, nb):
         return nb * (self.x[0].numel() // self.C)
 
+    skip_fwd = False   # the following conv applies this LRN while staging (HipNet.fold_lrn_fwd)
+
     def fwd(self, nb: int) -> None:
+        if self.skip_fwd:
+            return
         s = self.spec
         kernels().lrn_fwd(self.x, self.out, self._p(nb), self.C, s.depth_radius, s.bias, s.alpha, s.beta)
 
@@ -490,6 +507,21 @@ class HipNet:
                     a.lrn_fold = (b.spec, self.dbuf[k + 2])   # dL/d(LRN output) = the LRN's incoming gradient
                     b.skip_bwd = True
                     self.fold_lrn = True
+        # reference CNN: norm1's forward in conv2's input staging (LDS-halo fwd and weight-
+        # gradient kernels read pool1 and normalise it; norm1 never written).  Opt-in
+        # (MNISTX_FOLD_LRN_FWD=1): the LRN math in both staging loops costs more than the
+        # 67 us lrn_fwd launch it removes (2.25-2.28 vs 2.22-2.24 ms/step, profiles/r2/README.md)
+        self.fold_lrn_fwd = False
+        if (dev.type == "cuda" and os.environ.get("MNISTX_FOLD_LRN_FWD", "0") == "1"
+                and os.environ.get("MNISTX_CONV_HALO", "1") != "0"):
+            for k in range(len(self.layers) - 1):
+                a, b = self.layers[k], self.layers[k + 1]
+                if (isinstance(a, LRNLayer) and isinstance(b, ConvLayer) and b.x is a.out and a.C == 32
+                        and a.spec.depth_radius == 4 and not a.in_relu and (b.H, b.W, b.C) == (14, 14, 32)
+                        and (b.spec.kh, b.spec.kw, b.spec.padding) == (5, 5, "SAME") and b.Cp % 32 == 0):
+                    b.lrn_pre = (a.spec, a.x)
+                    a.skip_fwd = True
+                    self.fold_lrn_fwd = True
         if self.fuse_c2d_c1w:
             l0, l1 = self.layers[0], self.layers[1]
             l0.fused_grid = min(l0.grid, kernels().lenet_c2dgrad_c1wgrad_grid())

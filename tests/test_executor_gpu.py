@@ -216,9 +216,11 @@ def test_lenet_fused_c2dgrad_c1wgrad(dev, K, B, monkeypatch):
 
 @pytest.mark.parametrize("cin", [1, 3])
 def test_refcnn_lrn1_backward_fold(dev, K, cin, monkeypatch):
-    """norm1's backward applied inside conv1's weight-gradient staging (HipNet.fold_lrn)
-    vs lrn_bwd + the plain conv1 wgrad: every other gradient bitwise, conv1's to fp32
-    reassociation (the folded kernel stages one image per group)."""
+    """norm1 folded away: its forward runs in conv2's halo staging (fwd + wgrad,
+    HipNet.fold_lrn_fwd) and its backward in conv1's weight-gradient staging
+    (HipNet.fold_lrn), vs lrn_fwd / lrn_bwd launches: logits and every other gradient
+    bitwise (same LRN math, same bf16 rounding), conv1's to fp32 reassociation (the
+    folded kernel stages one image per group)."""
     spec = get_model("reference_cnn", cin)
     init = torch_ref.init_params(spec, seed=5)
     B = 70
@@ -227,17 +229,19 @@ def test_refcnn_lrn1_backward_fold(dev, K, cin, monkeypatch):
 
     def grads(fold: str):
         monkeypatch.setenv("MNISTX_FOLD_LRN", fold)
+        monkeypatch.setenv("MNISTX_FOLD_LRN_FWD", fold)   # opt-in forward fold, tested here too
         net = HipNet(spec, B, dev, init, OptConfig(lr0=0.05))
-        assert net.fold_lrn == (fold == "1")
+        assert net.fold_lrn == (fold == "1") and net.fold_lrn_fwd == (fold == "1")
         net.x0.copy_(x)
         net.labels.copy_(y)
-        net.forward(defer_head=True)
+        logits = net.forward(defer_head=True).clone()
         net.loss_and_grad()
         net.backward()
         torch.cuda.synchronize()
-        return {n: net.fp.grad_view(n).clone() for n in init}
+        return {"logits": logits, **{n: net.fp.grad_view(n).clone() for n in init}}
 
     ref, fold = grads("0"), grads("1")
+    assert torch.equal(fold.pop("logits"), ref.pop("logits"))
     for n in init:
         if n.startswith("conv1/"):
             assert rel_err(fold[n], ref[n]) < 1e-5, n

@@ -24,7 +24,7 @@
 namespace mnistx {
 namespace {
 
-constexpr int FBM = 64, FBN = 64, FBK = 32, FNT = 256;
+constexpr int FBM = 64, FBN = 64, FBK = 16, FNT = 256;
 constexpr int FVPT = FBM * FBK / 4 / FNT;   // 4-element vectors per thread per operand tile
 static_assert(FBM == FBN && FVPT * 4 * FNT == FBM * FBK, "tile staging");
 constexpr int FLD = FBM + 4;   // LDS row stride (floats)

@@ -205,16 +205,18 @@ struct XStage {
   static constexpr int PER = (NV + NTH - 1) / NTH;
   u32x2 v[PER];
   // uint8 source: dataset rows of the group to load next, fetched one group ahead
-  // so the (uniform) index load never stalls the data prefetch behind it
-  int rows[IMGS];
+  // so the (uniform) index load never stalls the data prefetch behind it.  The raw
+  // int64 indices are loaded unconditionally (clamped address) and clamped only when
+  // load() uses them: a conditional load + clamp here waited for each index in turn.
+  int64_t rows[IMGS];
   static constexpr bool U8 = G::CIN == 1;   // uint8 input only for 1-channel first layers
   DEV void fetch_rows(const XSrc& src, int img0, int B) {
-    if (!U8 || !src.u8) return;
+    if (!U8 || !src.u8 || B <= 0) return;
 #pragma unroll
-    for (int im = 0; im < IMGS; ++im) {
-      const int64_t r = img0 + im < B ? src.idx[img0 + im] : 0;
-      rows[im] = (int)min(max(r, (int64_t)0), (int64_t)src.n - 1);
-    }
+    for (int im = 0; im < IMGS; ++im) rows[im] = src.idx[max(0, min(img0 + im, B - 1))];
+  }
+  DEV int row_of(const XSrc& src, int k) const {
+    return (int)min(max(rows[k], (int64_t)0), (int64_t)src.n - 1);
   }
   // bf16 activations, or (first layer) the uint8 dataset gathered through the
   // batch index and normalised x/255 - 0.5 exactly like prep_images (K10 fused).
@@ -231,9 +233,9 @@ struct XStage {
       for (int u = 0; u < PER; ++u) {
         const int e = tid + u * NTH;
         const int im = e / (G::H * G::ROWV), rem = e - im * (G::H * G::ROWV);
-        int row = rows[0];
+        int row = row_of(src, 0);
 #pragma unroll
-        for (int k = 1; k < IMGS; ++k) row = im == k ? rows[k] : row;
+        for (int k = 1; k < IMGS; ++k) row = im == k ? row_of(src, k) : row;
         const bool ok = e < NV && im < nimg;
         v[u] = u32x2{buf_b32(r, ok ? (uint32_t)(row * G::INTERIOR + rem * 4) : BUF_OOB), 0u};
       }

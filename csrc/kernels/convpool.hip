@@ -606,20 +606,29 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
                                                            const float* __restrict__ bias, int bias_n, int B,
                                                            bf16_t* __restrict__ pooled, uint8_t* __restrict__ arg) {
   using Q = QuadGeo;
-  constexpr int LDS = IMGS * Q::IMG_LDS;
+  // one zero row past the last image: the kh = 5 A run (zero weight) of the bottom window row
+  constexpr int LDS = IMGS * Q::IMG_LDS + Q::WS;
   constexpr int OUTE = Q::NWIN * 8;                 // pooled elements per image (16-byte multiple)
   typedef float f32x16 __attribute__((ext_vector_type(16)));
   __shared__ __attribute__((aligned(16))) bf16_t tile[LDS];
+  // quad slot (fragment row pair) -> tile offset of its window row 0 A run; slots past
+  // the last quad repeat it (their outputs are rewritten with identical values)
+  __shared__ int qtab[Q::MFQ * 16];
   // STAGE_OUT: outputs of the block's image group are staged in LDS and written as
   // 16-byte vectors; otherwise each lane stores its (window, channel) directly
   constexpr bool STAGE_OUT = true;
   __shared__ __attribute__((aligned(16))) bf16_t pout[STAGE_OUT ? IMGS * OUTE : 8];
   __shared__ __attribute__((aligned(16))) uint8_t aout[STAGE_OUT ? IMGS * OUTE : 16];
   static_assert((OUTE * 2) % 16 == 0 && OUTE % 16 == 0 && STAGE_OUT, "");
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index in an SGPR: the fragment / image bookkeeping below runs on the scalar unit
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n = lane & 31, h = lane >> 5;
   const int s = n >> 3, c = n & 7, sp = s & 1, wp = s >> 1;
   lds_zero<LDS>(tile, tid);
+  for (int i = tid; i < Q::MFQ * 16; i += NTH) {
+    const int quad = min(i, Q::NQUAD - 1), ph = quad / Q::PQ, pq = quad - ph * Q::PQ;
+    qtab[i] = 2 * ph * Q::WS + 4 * pq - Q::PAD + Q::X0;
+  }
 
   // B operand: k = 16q + 8h + j -> (kh = 2q + h, kw' = j); shift s uses tap kw = kw' - s
   bf16x8 bfr[3];
@@ -666,10 +675,8 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
     constexpr int NFR = IMGS * Q::MFQ, NWV = NTH / 64;
     auto frag_base = [&](int f) {
       const int im = f / Q::MFQ, fm = f - im * Q::MFQ;
-      const int quad = min(fm * 16 + qw, Q::NQUAD - 1);
-      const int ph = quad / Q::PQ, pq = quad - ph * Q::PQ;
       // tile row of (oh + kh) for kh = h (+2q): oh = 2ph + dy; column 4pq - PAD + X0
-      return tile + im * Q::IMG_LDS + (2 * ph + dyr + h) * Q::WS + 4 * pq - Q::PAD + Q::X0;
+      return tile + im * Q::IMG_LDS + qtab[fm * 16 + qw] + (dyr + h) * Q::WS;
     };
     auto epilogue = [&](int f, const f32x16& acc) {
       const int im = f / Q::MFQ, fm = f - im * Q::MFQ;
@@ -688,17 +695,17 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
         const float oth = swap_half_row(sp ? m[2 * u] : m[2 * u + 1]);
         const int t = 2 * u + sp;
         const float best = vmax(sp ? m[2 * u + 1] : m[2 * u], oth);
-        const int qt = fm * 16 + (t & 1) + 4 * (t >> 1) + 2 * h;
-        if (qt < Q::NQUAD) {
-          const int win = 2 * qt + wp;   // ph*14 + 2pq + wp with qt = ph*7 + pq (PW == 2*PQ)
-          const float o = pos_clear(best) + bs;
-          pimg[win * 8 + c] = f2bf(vmax(o, 0.f));
-          aimg[win * 8 + c] = (uint8_t)(o > 0.f ? pos_of(best) : ARG_OFF);
-        }
+        // slots past the last quad computed quad NQUAD-1 (qtab clamp): same values, same place
+        const int qt = min(fm * 16 + (t & 1) + 4 * (t >> 1) + 2 * h, Q::NQUAD - 1);
+        const int win = 2 * qt + wp;   // ph*14 + 2pq + wp with qt = ph*7 + pq (PW == 2*PQ)
+        const float o = pos_clear(best) + bs;
+        pimg[win * 8 + c] = f2bf(vmax(o, 0.f));
+        aimg[win * 8 + c] = (uint8_t)(o > 0.f ? pos_of(best) : ARG_OFF);
       }
     };
     auto afrag = [&](const bf16_t* tb, int q) {
-      const int rowoff = min(2 * q, 4 - h) * Q::WS;   // kh = 2q + h; the padded kh = 5 reads row 4 (zero weight)
+      // kh = 2q + h; the padded kh = 5 (zero weight) reads the next row: finite, or the zero row
+      const int rowoff = 2 * q * Q::WS;
       return join(*(const s16x4*)(tb + rowoff), *(const s16x4*)(tb + opaque(rowoff + 4)));
     };
     for (int f = wave; f < NFR; f += NWV) {

@@ -904,10 +904,12 @@ __global__ __launch_bounds__(NTH, wgrad_minw<G>()) void convpool_wgrad_k(const X
 // built once per image group from the (dP, arg) vectors, so the MFMA B operand of a
 // step is two aligned ds_read_b64 (windows 16s+2g.. and +8) with no per-step unpool
 // arithmetic.  Row stride 212 dwords (4 x odd): the 16 rows x 2 lane groups of a
-// ds_read_b64 half-wave hit 64 distinct banks.  The bias gradient (sum of dP over
-// ReLU-active windows) is accumulated while staging, in a fixed per-thread window
-// order, and combined in a fixed thread order: deterministic, and im2col rows
-// KE..KM-1 carry no bias/zero cells (their accumulators are never read).
+// ds_read_b64 half-wave hit 64 distinct banks.  The unpool is byte-select arithmetic:
+// v_perm replicates y_c into both halves and d_c into all four bytes, and a second
+// v_perm turns (d_c + k) per byte into a 0xff/0x00 byte mask from a one-entry table
+// (8 VALU per channel, no compares).  The bias gradient comes out of the MFMA: the
+// lanes supplying im2col^T rows KE..KE+3 read a constant [1,0,0,0] cell, so row KE
+// accumulates sum(dY) per column (deterministic MFMA order, no staging VALU).
 template <class G, int IMGS>
 __global__ __launch_bounds__(NTH, 6) void convpool_wgrad_pair_k(const XSrc x,
                                                              const bf16_t* __restrict__ dP,
@@ -924,30 +926,31 @@ __global__ __launch_bounds__(NTH, 6) void convpool_wgrad_pair_k(const XSrc x,
   __shared__ __attribute__((aligned(16))) bf16_t tile[TILE_E];
   __shared__ __attribute__((aligned(16))) uint32_t U[IMGS * UIMG];   // also the bias combine at the end
   __shared__ int wtab[G::NWIN];            // window -> aligned LDS offset of its top-left pixel
+  __shared__ __attribute__((aligned(8))) bf16_t one_cell[4];   // [1, 0, 0, 0]: im2col^T rows KE..KE+3
   // the cross-wave reduction reuses the image tile (written only after the barrier
   // that ends the main loop): 2 KB less LDS -> 6 instead of 5 workgroups per CU
   float* const red = (float*)tile;
-  static_assert(IMGS * UIMG >= NTH * 8 + 256, "bias combine reuses U");
   static_assert(TILE_E * 2 >= G::KM * 16 * 4, "reduction reuses the tile");
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  static_assert(G::KE % 4 == 0 && G::KE + 4 <= G::KM, "bias chunk");
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   lds_zero<TILE_E>(tile, tid);
   lds_zero<IMGS * UIMG * 2>((bf16_t*)U, tid);          // windows >= NWIN stay zero
   for (int w = tid; w < G::NWIN; w += NTH) wtab[w] = G::aligned_off(G::wbase(w));
+  if (tid < 4) one_cell[tid] = tid == 0 ? (bf16_t)0x3f80 : (bf16_t)0;
 
   const int q = (lane >> 2) & 3, p = lane & 3;
   int cd[G::MFW];
 #pragma unroll
   for (int mf = 0; mf < G::MFW; ++mf) {
     const int k0 = mf * 16 + 4 * p;
-    cd[mf] = k0 < G::KE ? G::chunk_delta(k0) : 0;   // rows >= KE: any valid pixel (never read back)
+    cd[mf] = k0 < G::KE ? G::chunk_delta(k0) : 0;   // rows > KE+3: any valid pixel (never read back)
   }
+  constexpr int MFB = G::KE / 16;                     // the fragment holding the bias chunk
+  const bool bias_lane = 4 * p == G::KE % 16;
   f32x4 acc[G::MFW];
 #pragma unroll
   for (int mf = 0; mf < G::MFW; ++mf) acc[mf] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bacc[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) bacc[c] = 0.f;
 
   const int stride = gridDim.x * IMGS;
   XStage<G, IMGS> xs;
@@ -968,12 +971,13 @@ __global__ __launch_bounds__(NTH, 6) void convpool_wgrad_pair_k(const XSrc x,
         uint32_t* urow = U + im * UIMG + win;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          const uint32_t yc = (ys.y[u][c >> 1] >> (16 * (c & 1))) & 0xffffu;
-          const uint32_t ac = (ys.a[u][c >> 2] >> (8 * (c & 3))) & 0xffu;
-          bacc[c] += ac < 4u ? __uint_as_float(yc << 16) : 0.f;
-#pragma unroll
-          for (int sx = 0; sx < 2; ++sx)
-            urow[(sx * 8 + c) * URS] = (ac == (uint32_t)sx ? yc : 0u) | (ac == (uint32_t)(2 + sx) ? yc << 16 : 0u);
+          // y_c in both halves, d_c (0..3, ARG_OFF = 4) in all four bytes
+          const uint32_t y2 = __builtin_amdgcn_perm(0u, ys.y[u][c >> 1], (c & 1) ? 0x03020302u : 0x01000100u);
+          const uint32_t r = __builtin_amdgcn_perm(0u, ys.a[u][c >> 2], 0x01010101u * (c & 3));
+          // byte b of the mask = table[d + k_b] with 0xff only at byte 3: set iff d == 3 - k_b.
+          // side 0: (dy0, dy1) = positions (0, 2) -> k = (3, 3, 1, 1); side 1: (1, 3) -> (2, 2, 0, 0)
+          urow[c * URS] = y2 & __builtin_amdgcn_perm(0u, 0xff000000u, r + 0x01010303u);
+          urow[(8 + c) * URS] = y2 & __builtin_amdgcn_perm(0u, 0xff000000u, r + 0x00000202u);
         }
       }
     }
@@ -997,7 +1001,13 @@ __global__ __launch_bounds__(NTH, 6) void convpool_wgrad_pair_k(const XSrc x,
       const int pb1 = im * G::IMG_LDS + wtab[min(wq + 8, G::NWIN - 1)] + (q & 1) * G::WS;
 #pragma unroll
       for (int mf = 0; mf < G::MFW; ++mf) {
-        const bf16x8 a = join(lds_tr4(tile + pb0 + cd[mf]), lds_tr4(tile + pb1 + cd[mf]));
+        const bf16_t* a0 = tile + pb0 + cd[mf];
+        const bf16_t* a1 = tile + pb1 + cd[mf];
+        if (mf == MFB) {
+          a0 = bias_lane ? one_cell : a0;
+          a1 = bias_lane ? one_cell : a1;
+        }
+        const bf16x8 a = join(lds_tr4(a0), lds_tr4(a1));
         acc[mf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr, acc[mf], 0, 0, 0);
       }
     }
@@ -1014,29 +1024,13 @@ __global__ __launch_bounds__(NTH, 6) void convpool_wgrad_pair_k(const XSrc x,
         }
     }
   }
-  float* bred = (float*)U;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) bred[c * NTH + tid] = bacc[c];
-  __syncthreads();
-  // bias: 8 x 256 per-thread sums -> 8 x 32 (8 consecutive threads each) -> 8, fixed order
-  float* bred2 = bred + 8 * NTH;
-  if (tid < 8 * 32) {
-    const float* src = bred + (tid >> 5) * NTH + (tid & 31) * 8;
-    float v = src[0];
-#pragma unroll
-    for (int t = 1; t < 8; ++t) v += src[t];
-    bred2[tid] = v;
-  }
   __syncthreads();
   float* out = slab + (int64_t)blockIdx.x * G::KM * 8;
   for (int e = tid; e < G::KM * 8; e += NTH) {
     const int m = e >> 3, cc = e & 7;
     float v = 0.f;
-    if (m == G::KE) {
-      for (int t = 0; t < 32; ++t) v += bred2[cc * 32 + t];
-    } else if (m < G::KE) {
-      v = red[m * 16 + cc] + red[(m + 1) * 16 + 8 + cc];
-    }
+    if (m == G::KE) v = red[m * 16 + cc] + red[m * 16 + 8 + cc];   // left + right pixels' dY sums
+    else if (m < G::KE) v = red[m * 16 + cc] + red[(m + 1) * 16 + 8 + cc];
     out[e] = v;
   }
 }

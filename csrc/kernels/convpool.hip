@@ -182,7 +182,7 @@ struct LrnFold {
 // 4 at 106) and its wgrad 167 (3 waves, was 2 at 172) without spills; the
 // reference conv1 variants spill under a bound, so they keep the default.
 template <class G> constexpr int fwd_minw() { return (G::CIN == 8 && G::COUT == 16) ? 4 : 1; }
-template <class G> constexpr int wgrad_minw() { return (G::CIN == 8 && G::COUT == 16) ? 3 : 1; }
+template <class G> constexpr int wgrad_minw() { return (G::CIN == 8 && G::COUT == 16) ? 4 : 1; }
 // Argmax byte of a pool window whose ReLU output is 0: matches no position, so
 // the backward kernels need only (dP, arg) -- the ReLU mask is folded in here
 // and the pooled activations are never re-read.
@@ -358,11 +358,21 @@ __global__ __launch_bounds__(NTH, fwd_minw<G>()) void convpool_fwd_k(const XSrc 
   // vectors; wide ones (32 channels) keep direct 32-byte-per-row stores (LDS budget)
   constexpr bool STAGE = IMGS * OUTE * 3 <= 16384 && OUTE % 16 == 0;
   __shared__ __attribute__((aligned(16))) bf16_t tile[LDS];
-  __shared__ __attribute__((aligned(16))) bf16_t pout[STAGE ? IMGS * OUTE : 8];
-  __shared__ __attribute__((aligned(16))) uint8_t aout[STAGE ? IMGS * OUTE : 16];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // staged: one spare window past the group absorbs the rows past the last pixel
+  __shared__ __attribute__((aligned(16))) bf16_t pout[STAGE ? IMGS * OUTE + G::COUT : 8];
+  __shared__ __attribute__((aligned(16))) uint8_t aout[STAGE ? IMGS * OUTE + G::COUT : 16];
+  // small images (LeNet conv2: 112 fragment rows): fragment row -> pixel base offset from
+  // an LDS table instead of ~20 VALU of window / position arithmetic per fragment
+  constexpr bool PTAB = G::MF * 16 <= 128;
+  __shared__ int ptab[PTAB ? G::MF * 16 : 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   lds_zero<LDS>(tile, tid);
+  if constexpr (PTAB)
+    for (int i = tid; i < G::MF * 16; i += NTH) {
+      const int r = min(i, G::NPIX - 1);
+      ptab[i] = G::wbase(r >> 2) + G::doff(r & 3);
+    }
 
   // per-lane A-operand offsets: dd = run deltas (MODE 0: two 4-runs; MODE 1: one 8-run),
   // dl = scalar deltas (MODE 2)
@@ -422,9 +432,14 @@ __global__ __launch_bounds__(NTH, fwd_minw<G>()) void convpool_fwd_k(const XSrc 
     }
     for (int f = wave; f < IMGS * G::MF; f += NTH / 64) {
       const int im = f / G::MF, fm = f - im * G::MF;
-      const int r = min(fm * 16 + li, G::NPIX - 1);
       const bf16_t* tb = tile + im * G::IMG_LDS;
-      const int pb = G::wbase(r >> 2) + G::doff(r & 3);
+      int pb;
+      if constexpr (PTAB) {
+        pb = ptab[fm * 16 + li];
+      } else {
+        const int r = min(fm * 16 + li, G::NPIX - 1);
+        pb = G::wbase(r >> 2) + G::doff(r & 3);
+      }
       f32x4 acc[G::NF];
 #pragma unroll
       for (int nf = 0; nf < G::NF; ++nf) acc[nf] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -450,8 +465,10 @@ __global__ __launch_bounds__(NTH, fwd_minw<G>()) void convpool_fwd_k(const XSrc 
 #pragma unroll
         for (int nf = 0; nf < G::NF; ++nf)
           acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], bfr[s][nf], acc[nf], 0, 0, 0);
-      const int win = fm * 4 + g;
-      if (win < G::NWIN && (STAGE || img0 + im < B)) {
+      // staged: windows past the last one (their rows are clamped copies of pixel
+      // NPIX-1, not a real window) go to the spare window -- a select, not a branch
+      const int win = (STAGE && fm * 4 + g >= G::NWIN) ? G::NWIN * (IMGS - im) : fm * 4 + g;
+      if (STAGE || (win < G::NWIN && img0 + im < B)) {
         bf16_t* pimg = STAGE ? pout + im * OUTE : pooled + (int64_t)(img0 + im) * OUTE;
         uint8_t* aimg = STAGE ? aout + im * OUTE : arg + (int64_t)(img0 + im) * OUTE;
 #pragma unroll
@@ -501,7 +518,7 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_pair_k(const XSrc x, const b
   constexpr int MFP = (G::NWIN + 7) / 8;  // fragments per image (8 windows each)
   __shared__ __attribute__((aligned(16))) bf16_t tile[LDS];
   __shared__ int wtab[G::NWIN];            // window -> aligned LDS offset of its top-left pixel
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int c = li & 7, sx = li >> 3;
   lds_zero<LDS>(tile, tid);
@@ -751,13 +768,31 @@ __global__ __launch_bounds__(NTH, wgrad_minw<G>()) void convpool_wgrad_k(const X
                                                         float* __restrict__ slab, const LrnFold lrn) {
   constexpr int CELL = IMGS * G::IMG_LDS;             // [1,0,0,0] then [0,0,0,0]
   constexpr int LDS = (CELL + 8 + 7) / 8 * 8;
+  // FAST (LeNet conv2, 16 channels x 8-channel taps): dY is max-unpooled ONCE per group
+  // into U2[img][channel][window] = the window's 4 positions (8 bytes), so a step's B
+  // operand is two ds_read_b64 with no per-step select arithmetic; the A reads use
+  // two per-window base registers + compile-time tap offsets (see below).  Row stride
+  // 34 windows = 68 dwords (4 mod 64): the 16 channels x 2 lane groups of a half-wave
+  // hit distinct bank pairs.  The cross-wave reduction reuses U2.
+  constexpr bool FAST = G::MODE == 1 && G::COUT == 16 && G::CIN == 8 && !LRNB;
+  constexpr int URW = 34, NWPAD = G::RSTEPS * 8;
+  static_assert(!FAST || (URW >= NWPAD && (2 * URW) % 64 == 4), "U2 row stride");
+  constexpr int U2E = FAST ? IMGS * G::COUT * URW * 4 : 4;   // bf16 elements
   __shared__ __attribute__((aligned(16))) bf16_t tile[LDS];
-  __shared__ __attribute__((aligned(16))) bf16_t dys[IMGS * G::NWIN * G::COUT];
-  __shared__ __attribute__((aligned(16))) uint8_t args[IMGS * G::NWIN * G::COUT];
-  __shared__ float red[G::KM * G::NCOL];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ __attribute__((aligned(16))) bf16_t dys[FAST ? 8 : IMGS * G::NWIN * G::COUT];
+  __shared__ __attribute__((aligned(16))) uint8_t args[FAST ? 16 : IMGS * G::NWIN * G::COUT];
+  __shared__ __attribute__((aligned(16))) bf16_t U2[U2E];
+  __shared__ float red_own[FAST ? 1 : G::KM * G::NCOL];
+  __shared__ int wtab[FAST ? NWPAD : 1];
+  static_assert(!FAST || U2E * 2 >= G::KM * G::NCOL * 4, "reduction reuses U2");
+  float* const red = FAST ? (float*)U2 : red_own;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   lds_zero<LDS>(tile, tid);
+  if constexpr (FAST) {
+    lds_zero<U2E>(U2, tid);                        // windows >= NWIN stay zero
+    for (int w = tid; w < NWPAD; w += NTH) wtab[w] = G::wbase(min(w, G::NWIN - 1));
+  }
   __syncthreads();
   if (tid == 0) tile[CELL] = (bf16_t)0x3f80;
 
@@ -796,7 +831,29 @@ __global__ __launch_bounds__(NTH, wgrad_minw<G>()) void convpool_wgrad_k(const X
     __syncthreads();
     xs.store(tile, tid);
     ys.apply_lrn(lrn, tid);
-    ys.store(dys, args, tid);
+    if constexpr (FAST) {
+      constexpr int NWC = G::NWIN * G::COUT;
+#pragma unroll
+      for (int u = 0; u < DYStage<G, IMGS, LRNB>::PER; ++u) {
+        const int e = 8 * (tid + u * NTH);
+        if (e < IMGS * NWC) {
+          const int im = e / NWC, rem = e - im * NWC;
+          const int win = rem / G::COUT, co0 = rem - win * G::COUT;
+          bf16_t* urow = U2 + ((im * G::COUT + co0) * URW + win) * 4;
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            // y_c in both halves, d_c in all four bytes; byte b of a mask = table[d + k_b]
+            // (0xff only at byte 3): positions (0, 1) -> k = (3, 3, 2, 2), (2, 3) -> (1, 1, 0, 0)
+            const uint32_t y2 = __builtin_amdgcn_perm(0u, ys.y[u][c >> 1], (c & 1) ? 0x03020302u : 0x01000100u);
+            const uint32_t r = __builtin_amdgcn_perm(0u, ys.a[u][c >> 2], 0x01010101u * (c & 3));
+            *(u32x2*)(urow + c * URW * 4) = u32x2{y2 & __builtin_amdgcn_perm(0u, 0xff000000u, r + 0x02020303u),
+                                                   y2 & __builtin_amdgcn_perm(0u, 0xff000000u, r + 0x00000101u)};
+          }
+        }
+      }
+    } else {
+      ys.store(dys, args, tid);
+    }
     __syncthreads();
     if constexpr (G::MODE == 0) {
       make_shifted<G, IMGS>(tile, tid);
@@ -807,6 +864,39 @@ __global__ __launch_bounds__(NTH, wgrad_minw<G>()) void convpool_wgrad_k(const X
       xs.fetch_rows(x, img0 + 2 * stride, B);
       ys.load(dP, arg, img0 + stride, B, tid);
       ys.load_lrn(lrn.p, img0 + stride, B, tid);
+    }
+    if constexpr (FAST) {
+      // A operand: chunk k0 = 16 mf + 4p is tap t = 2mf + e (e = p >> 1), channels 4(p&1)..+3;
+      // its LDS offset is off(2mf) (compile time) + 4(p&1) + e * 8, except when 2mf is the
+      // last tap of a kernel row (2mf % KS == KS-1): then tap 2mf+1 starts the next row,
+      // e * (WS - KS + 1) * 8 -- two base registers per window, every read an immediate.
+      const int e1 = p >> 1;
+      const int lane_a = 4 * (p & 1) + e1 * G::CIN;
+      const int lane_b = 4 * (p & 1) + e1 * (G::WS - G::KS + 1) * G::CIN;
+      auto toff = [](int t) constexpr { return ((t / G::KS) * G::WS + t % G::KS) * G::CIN; };
+      for (int it = wave; it < IMGS * G::RSTEPS; it += NTH / 64) {
+        const int im = it / G::RSTEPS, s = it - im * G::RSTEPS;
+        const int w0 = 8 * s + g;
+        const bf16_t* ub = U2 + ((im * G::COUT + li) * URW + w0) * 4;
+        const bf16x8 bfr = join(*(const s16x4*)ub, *(const s16x4*)(ub + opaque(16)));
+        // rows supplied by this lane: pixel q of windows w0 / w0 + 4 (clamped; dY is zero there)
+        const bf16_t* t0 = tile + im * G::IMG_LDS + wtab[w0] + G::doff(q);
+        const bf16_t* t1 = tile + im * G::IMG_LDS + wtab[w0 + 4] + G::doff(q);
+#pragma unroll
+        for (int mf = 0; mf < G::MFW; ++mf) {
+          const bool rowend = (2 * mf) % G::KS == G::KS - 1;
+          const int lo = rowend ? lane_b : lane_a;
+          const bf16_t* a0 = t0 + lo + toff(2 * mf);
+          const bf16_t* a1 = t1 + lo + toff(2 * mf);
+          if (16 * mf + 16 > G::KE) {     // the fragment holding the bias / zero cells
+            const int k0 = 16 * mf + 4 * p;
+            if (k0 >= G::KE) a0 = a1 = tile + CELL + (k0 == G::KE ? 0 : 4);
+          }
+          const bf16x8 a = join(lds_tr4(a0), lds_tr4(a1));
+          acc[mf][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr, acc[mf][0], 0, 0, 0);
+        }
+      }
+      continue;
     }
     for (int it = wave; it < IMGS * G::RSTEPS; it += NTH / 64) {
       const int im = it / G::RSTEPS, s = it - im * G::RSTEPS;
@@ -1045,8 +1135,8 @@ __global__ __launch_bounds__(NTH, 6) void convpool_wgrad_pair_k(const XSrc x,
 // (ih, iw + 1).  K-slot order: lane group g, element j -> tap 2s + g/2, co 8(g&1)+j,
 // so each A fragment is ONE ds_read_b128.  The unpooled dY image lives in LDS
 // with a KS-1-PAD halo.
-template <class G, int IMGS>
-__global__ __launch_bounds__(NTH) void convpool_dgrad_pair_k(const bf16_t* __restrict__ dP,
+template <class G, int IMGS, int DB = 0, int MINW = 1>
+__global__ __launch_bounds__(NTH, MINW) void convpool_dgrad_pair_k(const bf16_t* __restrict__ dP,
                                                              const uint8_t* __restrict__ arg,
                                                              const bf16_t* __restrict__ w, int B,
                                                              bf16_t* __restrict__ dx) {
@@ -1070,18 +1160,23 @@ __global__ __launch_bounds__(NTH) void convpool_dgrad_pair_k(const bf16_t* __res
   static_assert(OUTE % 8 == 0, "");
   __shared__ __attribute__((aligned(16))) bf16_t dyt[IMGS * DT];
   __shared__ __attribute__((aligned(16))) bf16_t outs[IMGS * OUTE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int ci = li & 7, sx = li >> 3;
   lds_zero<IMGS * DT>(dyt, tid);
 
-  int dtap[KSD];
+  // A-fragment tap of k-step s: tp = 2s + g/2; KWQ is even, so kh = (2s)/KWQ for both
+  // g/2 and the tap offset is dtap_c(s) (compile time: a ds_read immediate) + the lane's
+  // (g/2)*DPS + 8(g&1) (the padded last tap, tp = NTAP, reads a finite in-tile pixel
+  // against a zero filter)
+  static_assert(KWQ % 2 == 0 && 2 * (KSD - 1) + 1 <= NTAP, "tap split");
+  auto dtap_c = [](int s) constexpr { return (2 * s / KWQ) * RSE + (2 * s % KWQ) * DPS; };
+  const int lane_tap = (g >> 1) * DPS + 8 * (g & 1);
   bf16x8 bw[KSD];
 #pragma unroll
   for (int s = 0; s < KSD; ++s) {
     const int tp = 2 * s + (g >> 1);
     const int kh = tp / KWQ, kwq = tp - kh * KWQ;
-    dtap[s] = tp < NTAP ? kh * RSE + kwq * DPS + 8 * (g & 1) : 0;
     const int kw = kwq - sx;
     const bool valid = tp < NTAP && kw >= 0 && kw < G::KS;
     const int tap = valid ? (G::KS - 1 - kh) * G::KS + (G::KS - 1 - kw) : 0;
@@ -1125,16 +1220,22 @@ __global__ __launch_bounds__(NTH) void convpool_dgrad_pair_k(const bf16_t* __res
     // the group's 2 x MFD fragments are dealt over the 4 waves together (balance)
     for (int f = wave; f < IMGS * MFD; f += NTH / 64) {
       const int im = f / MFD, mf = f - im * MFD;
-      const bf16_t* tb = dyt + im * DT + (2 * mf + (li >> 3)) * RSE + 2 * (li & 7) * DPS;
+      const bf16_t* tb = dyt + im * DT + (2 * mf + (li >> 3)) * RSE + 2 * (li & 7) * DPS + lane_tap;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      // all A fragments in flight before the MFMA chain: one read ahead left every
-      // MFMA waiting out a full LDS latency (wait_any 57 %, MFMA busy 38 %)
-      bf16x8 a[KSD];
+      // all A fragments (DB = 0) or batches of DB in flight before their MFMAs: one read
+      // ahead left every MFMA waiting out a full LDS latency (wait_any 57 %, MFMA busy 38 %)
+      constexpr int NB = DB == 0 ? KSD : DB;
 #pragma unroll
-      for (int s = 0; s < KSD; ++s) a[s] = __builtin_bit_cast(bf16x8, *(const u32x4*)(tb + dtap[s]));
-      __builtin_amdgcn_sched_barrier(0);
+      for (int b = 0; b < KSD; b += NB) {
+        bf16x8 a[NB];
 #pragma unroll
-      for (int s = 0; s < KSD; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], bw[s], acc, 0, 0, 0);
+        for (int s = 0; s < NB; ++s)
+          if (b + s < KSD) a[s] = __builtin_bit_cast(bf16x8, *(const u32x4*)(tb + dtap_c(b + s)));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < NB; ++s)
+          if (b + s < KSD) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], bw[b + s], acc, 0, 0, 0);
+      }
       // accumulator rows 4g + r: image row 2mf + g/2, pair jr = 4(g&1) + r -> LDS staging
       const int ih = 2 * mf + (g >> 1);
       bf16_t* oimg = outs + im * OUTE;
@@ -1234,10 +1335,18 @@ hipError_t run_dgrad(const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int 
                      hipStream_t st) {
   // grid_cap > 0: fewer persistent blocks than one resident wave, leaving CU slots
   // for a kernel running concurrently on another stream (overlapped backward)
-  int cap = resident_grid<convpool_dgrad_pair_k<G, IMGS>>();
+  // One image per group with the A fragments in batches of 8 (122 VGPRs: 4 waves per
+  // SIMD) measured 131 vs 143-149 us for two images with all 15 in flight (150 VGPRs,
+  // 3 waves; MNISTX_DGRAD_VAR=0).  Fewer VGPRs spill (batches of 5 at 5 waves: 183 us).
+  static const bool legacy = [] { const char* e = getenv("MNISTX_DGRAD_VAR"); return e && e[0] == '0'; }();
+  int cap = legacy ? resident_grid<convpool_dgrad_pair_k<G, IMGS>>() : resident_grid<convpool_dgrad_pair_k<G, 1, 8, 4>>();
   if (grid_cap > 0 && grid_cap < cap) cap = grid_cap;
-  hipLaunchKernelGGL((convpool_dgrad_pair_k<G, IMGS>), dim3(grid_for(B, IMGS, cap)), dim3(NTH), 0, st, dP, arg, w,
-                     B, dx);
+  if (legacy)
+    hipLaunchKernelGGL((convpool_dgrad_pair_k<G, IMGS>), dim3(grid_for(B, IMGS, cap)), dim3(NTH), 0, st, dP, arg, w,
+                       B, dx);
+  else
+    hipLaunchKernelGGL((convpool_dgrad_pair_k<G, 1, 8, 4>), dim3(grid_for(B, 1, cap)), dim3(NTH), 0, st, dP, arg, w,
+                       B, dx);
   return hipGetLastError();
 }
 
@@ -1304,7 +1413,7 @@ __global__ __launch_bounds__(NTH, 3) void lenet_c2dgrad_c1wgrad_k(const XSrc x, 
   float* const red = (float*)dyt;                    // end-of-kernel reductions reuse the dY2 tile
   static_assert(IMGS * DT * 2 >= G1::KM * 16 * 4, "wgrad reduction reuses dyt");
   static_assert(IMGS * UIMG >= NTH + 64, "bias combine reuses U");
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int ci = li & 7, sx = li >> 3;
   lds_zero<IMGS * DT>(dyt, tid);

@@ -626,6 +626,7 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
   // one zero row past the last image: the kh = 5 A run (zero weight) of the bottom window row
   constexpr int LDS = IMGS * Q::IMG_LDS + Q::WS;
   constexpr int OUTE = Q::NWIN * 8;                 // pooled elements per image (16-byte multiple)
+  constexpr int OUTS = Q::MFQ * 32 * 8;             // LDS stride per image: every fragment slot
   typedef float f32x16 __attribute__((ext_vector_type(16)));
   __shared__ __attribute__((aligned(16))) bf16_t tile[LDS];
   // quad slot (fragment row pair) -> tile offset of its window row 0 A run; slots past
@@ -634,8 +635,8 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
   // STAGE_OUT: outputs of the block's image group are staged in LDS and written as
   // 16-byte vectors; otherwise each lane stores its (window, channel) directly
   constexpr bool STAGE_OUT = true;
-  __shared__ __attribute__((aligned(16))) bf16_t pout[STAGE_OUT ? IMGS * OUTE : 8];
-  __shared__ __attribute__((aligned(16))) uint8_t aout[STAGE_OUT ? IMGS * OUTE : 16];
+  __shared__ __attribute__((aligned(16))) bf16_t pout[STAGE_OUT ? IMGS * OUTS : 8];
+  __shared__ __attribute__((aligned(16))) uint8_t aout[STAGE_OUT ? IMGS * OUTS : 16];
   static_assert((OUTE * 2) % 16 == 0 && OUTE % 16 == 0 && STAGE_OUT, "");
   // wave index in an SGPR: the fragment / image bookkeeping below runs on the scalar unit
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -697,8 +698,8 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
     };
     auto epilogue = [&](int f, const f32x16& acc) {
       const int im = f / Q::MFQ, fm = f - im * Q::MFQ;
-      bf16_t* pimg = pout + im * OUTE;
-      uint8_t* aimg = aout + im * OUTE;
+      bf16_t* pimg = pout + im * OUTS;
+      uint8_t* aimg = aout + im * OUTS;
       // acc[i]: row (i&3) + 8(i>>2) + 4h -> quad t-slot t = i/2 (qw = (t&1) + 4(t>>1) + 2h),
       // dy = i&1; this lane's pixel column within the window is sp: position 2dy + sp
       float m[8];
@@ -712,9 +713,12 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
         const float oth = swap_half_row(sp ? m[2 * u] : m[2 * u + 1]);
         const int t = 2 * u + sp;
         const float best = vmax(sp ? m[2 * u + 1] : m[2 * u], oth);
-        // slots past the last quad computed quad NQUAD-1 (qtab clamp): same values, same place
-        const int qt = min(fm * 16 + (t & 1) + 4 * (t >> 1) + 2 * h, Q::NQUAD - 1);
-        const int win = 2 * qt + wp;   // ph*14 + 2pq + wp with qt = ph*7 + pq (PW == 2*PQ)
+        // quad slot qt = fm*16 + (t&1) + 4(t>>1) + 2h = fm*16 + 4u + sp + 2h, window 2qt + wp
+        // (ph*14 + 2pq + wp with qt = ph*7 + pq, PW == 2*PQ) = 32 fm (scalar) + 8u
+        // (immediate) + a lane constant.
+        // Slots past the last quad land in the per-image LDS padding (never copied out).
+        const int win = 32 * fm + 8 * u + (2 * sp + 4 * h + wp);
+        (void)t;
         const float o = pos_clear(best) + bs;
         pimg[win * 8 + c] = f2bf(vmax(o, 0.f));
         aimg[win * 8 + c] = (uint8_t)(o > 0.f ? pos_of(best) : ARG_OFF);
@@ -744,13 +748,15 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
       constexpr int PV = IMGS * OUTE / 8, AV = IMGS * OUTE / 16;
 #pragma unroll
       for (int u = 0; u < (PV + NTH - 1) / NTH; ++u) {
-        const int e = tid + u * NTH;
-        if (e < nimg * (OUTE / 8)) *(u32x4*)(pg + 8 * e) = *(const u32x4*)(pout + 8 * e);
+        const int e = tid + u * NTH, im = e / (OUTE / 8);
+        if (e < nimg * (OUTE / 8))
+          *(u32x4*)(pg + 8 * e) = *(const u32x4*)(pout + im * OUTS + 8 * (e - im * (OUTE / 8)));
       }
 #pragma unroll
       for (int u = 0; u < (AV + NTH - 1) / NTH; ++u) {
-        const int e = tid + u * NTH;
-        if (e < nimg * (OUTE / 16)) *(u32x4*)(ag + 16 * e) = *(const u32x4*)(aout + 16 * e);
+        const int e = tid + u * NTH, im = e / (OUTE / 16);
+        if (e < nimg * (OUTE / 16))
+          *(u32x4*)(ag + 16 * e) = *(const u32x4*)(aout + im * OUTS + 16 * (e - im * (OUTE / 16)));
       }
     }
   }

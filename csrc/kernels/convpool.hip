@@ -254,14 +254,26 @@ struct XStage {
     return u32x2{pack2(u8_norm(b4 & 0xff), u8_norm((b4 >> 8) & 0xff)),
                  pack2(u8_norm((b4 >> 16) & 0xff), u8_norm(b4 >> 24))};
   }
+  // offset of vector e in the LDS tile
+  static DEV int tile_off(int e) {
+    const int im = e / (G::H * G::ROWV), rem = e - im * (G::H * G::ROWV);
+    const int hh = rem / G::ROWV, vv = rem - hh * G::ROWV;
+    return im * G::IMG_LDS + ((hh + G::PAD) * G::WS + G::X0) * G::CIN + 4 * vv;
+  }
+  // the uint8 conversion sits behind a uniform branch (a select made every bf16 staging
+  // pay for it: ~10 VALU per vector)
   DEV void store(bf16_t* tile, int tid) const {
+    if (U8 && u8mode) {
 #pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int e = tid + u * NTH;
-      if (e < NV) {
-        const int im = e / (G::H * G::ROWV), rem = e - im * (G::H * G::ROWV);
-        const int hh = rem / G::ROWV, vv = rem - hh * G::ROWV;
-        *(u32x2*)(tile + im * G::IMG_LDS + ((hh + G::PAD) * G::WS + G::X0) * G::CIN + 4 * vv) = value(u);
+      for (int u = 0; u < PER; ++u) {
+        const int e = tid + u * NTH;
+        if (e < NV) *(u32x2*)(tile + tile_off(e)) = value(u);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int e = tid + u * NTH;
+        if (e < NV) *(u32x2*)(tile + tile_off(e)) = v[u];
       }
     }
   }
@@ -669,19 +681,24 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
   xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
     __syncthreads();
-    // interior rows at column X0 = 10 (4-byte aligned): two 4-byte stores per vector
+    // interior rows at column X0 = 10 (4-byte aligned): two 4-byte stores per vector;
+    // the uint8 conversion behind a uniform branch (not a per-vector select)
+    auto stage = [&](auto conv) {
 #pragma unroll
-    for (int u = 0; u < XStage<Q, IMGS>::PER; ++u) {
-      const int e = tid + u * NTH;
-      if (e < XStage<Q, IMGS>::NV) {
-        const int im = e / (Q::H * Q::ROWV), rem = e - im * (Q::H * Q::ROWV);
-        const int hh = rem / Q::ROWV, vv = rem - hh * Q::ROWV;
-        bf16_t* dst = tile + im * Q::IMG_LDS + (hh + Q::PAD) * Q::WS + Q::X0 + 4 * vv;
-        const u32x2 val = xs.value(u);
-        *(uint32_t*)dst = val[0];
-        *(uint32_t*)(dst + 2) = val[1];
+      for (int u = 0; u < XStage<Q, IMGS>::PER; ++u) {
+        const int e = tid + u * NTH;
+        if (e < XStage<Q, IMGS>::NV) {
+          const int im = e / (Q::H * Q::ROWV), rem = e - im * (Q::H * Q::ROWV);
+          const int hh = rem / Q::ROWV, vv = rem - hh * Q::ROWV;
+          bf16_t* dst = tile + im * Q::IMG_LDS + (hh + Q::PAD) * Q::WS + Q::X0 + 4 * vv;
+          const u32x2 val = conv(u);
+          *(uint32_t*)dst = val[0];
+          *(uint32_t*)(dst + 2) = val[1];
+        }
       }
-    }
+    };
+    if (xs.u8mode) stage([&](int u) { return xs.value(u); });
+    else stage([&](int u) { return xs.v[u]; });
     __syncthreads();
     if (img0 + stride < B) {
       xs.load(x, img0 + stride, B, tid);

@@ -32,6 +32,7 @@
 #include "lrn_math.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace mnistx {
 namespace {
@@ -1158,7 +1159,14 @@ __global__ __launch_bounds__(NTH, 6) void convpool_wgrad_pair_k(const XSrc x,
 // (ih, iw + 1).  K-slot order: lane group g, element j -> tap 2s + g/2, co 8(g&1)+j,
 // so each A fragment is ONE ds_read_b128.  The unpooled dY image lives in LDS
 // with a KS-1-PAD halo.
-template <class G, int IMGS, int DB = 0, int MINW = 1>
+//
+// LA > 0 (A-row reuse): the A fragment of (fragment mf, k-step s) is the dY tile at
+// row R = 2mf + kh(s) and tap pair c = s mod 3, so fragments mf and mf+1 share
+// every row but their first / last two.  Each wave owns F consecutive fragments of
+// one image and streams the rows R once (LA rows read ahead), issuing for each the
+// MFMAs of every fragment it feeds: 3(2F+3) ds_read_b128 per wave instead of 15F --
+// the kernel is LDS-bandwidth bound (105 x 1 KB of A reads per image otherwise).
+template <class G, int IMGS, int DB = 0, int MINW = 1, int LA = 0>
 __global__ __launch_bounds__(NTH, MINW) void convpool_dgrad_pair_k(const bf16_t* __restrict__ dP,
                                                              const uint8_t* __restrict__ arg,
                                                              const bf16_t* __restrict__ w, int B,
@@ -1240,8 +1248,57 @@ __global__ __launch_bounds__(NTH, MINW) void convpool_dgrad_pair_k(const bf16_t*
     }
     __syncthreads();
     if (img0 + stride < B) ys.load(dP, arg, img0 + stride, B, tid);
+    if constexpr (LA > 0) {
+      static_assert(KWQ == 6 && KSD == 15 && (NTH / 64) % IMGS == 0, "row reuse: 5 tap rows x 3 tap pairs");
+      constexpr int WPI = (NTH / 64) / IMGS;          // waves per image
+      const int im = wave / WPI, k = wave - im * WPI;
+      const int mf0 = k * MFD / WPI, F = (k + 1) * MFD / WPI - mf0;
+      const bf16_t* tb0 = dyt + im * DT + (2 * mf0 + (li >> 3)) * RSE + 2 * (li & 7) * DPS + lane_tap;
+      bf16_t* oimg = outs + im * OUTE;
+      auto run = [&](auto FC) {
+        constexpr int FF = decltype(FC)::value;
+        constexpr int NR = 2 * FF + 3;                 // rows R' = kh + 2j, kh 0..4, j < FF
+        f32x4 acc[FF];
+#pragma unroll
+        for (int j = 0; j < FF; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        bf16x8 a[LA + 1][3];
+        auto load_row = [&](int r) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+            a[r % (LA + 1)][c] = __builtin_bit_cast(bf16x8, *(const u32x4*)(tb0 + r * RSE + 2 * c * DPS));
+        };
+#pragma unroll
+        for (int r = 0; r < LA; ++r) load_row(r);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          if (r + LA < NR) load_row(r + LA);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int j = 0; j < FF; ++j) {
+              const int kh = r - 2 * j;
+              if (kh >= 0 && kh < G::KS)
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r % (LA + 1)][c], bw[3 * kh + c], acc[j], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < FF; ++j) {
+          const int ih = 2 * (mf0 + j) + (g >> 1);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int jr = 4 * (g & 1) + r;
+            if (2 * jr < G::W) oimg[(ih * G::W + 2 * jr + sx) * 8 + ci] = f2bf(acc[j][r]);
+          }
+        }
+      };
+      constexpr int FMAX = (MFD + WPI - 1) / WPI, FMIN = MFD / WPI;
+      static_assert(FMAX - FMIN <= 1, "");
+      if (F == FMAX) run(std::integral_constant<int, FMAX>{});
+      else run(std::integral_constant<int, FMIN>{});
+    }
     // the group's 2 x MFD fragments are dealt over the 4 waves together (balance)
-    for (int f = wave; f < IMGS * MFD; f += NTH / 64) {
+    for (int f = wave; LA == 0 && f < IMGS * MFD; f += NTH / 64) {
       const int im = f / MFD, mf = f - im * MFD;
       const bf16_t* tb = dyt + im * DT + (2 * mf + (li >> 3)) * RSE + 2 * (li & 7) * DPS + lane_tap;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -1358,18 +1415,22 @@ hipError_t run_dgrad(const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int 
                      hipStream_t st) {
   // grid_cap > 0: fewer persistent blocks than one resident wave, leaving CU slots
   // for a kernel running concurrently on another stream (overlapped backward)
-  // One image per group with the A fragments in batches of 8 (122 VGPRs: 4 waves per
-  // SIMD) measured 131 vs 143-149 us for two images with all 15 in flight (150 VGPRs,
-  // 3 waves; MNISTX_DGRAD_VAR=0).  Fewer VGPRs spill (batches of 5 at 5 waves: 183 us).
-  static const bool legacy = [] { const char* e = getenv("MNISTX_DGRAD_VAR"); return e && e[0] == '0'; }();
-  int cap = legacy ? resident_grid<convpool_dgrad_pair_k<G, IMGS>>() : resident_grid<convpool_dgrad_pair_k<G, 1, 8, 4>>();
-  if (grid_cap > 0 && grid_cap < cap) cap = grid_cap;
-  if (legacy)
-    hipLaunchKernelGGL((convpool_dgrad_pair_k<G, IMGS>), dim3(grid_for(B, IMGS, cap)), dim3(NTH), 0, st, dP, arg, w,
-                       B, dx);
-  else
-    hipLaunchKernelGGL((convpool_dgrad_pair_k<G, 1, 8, 4>), dim3(grid_for(B, 1, cap)), dim3(NTH), 0, st, dP, arg, w,
-                       B, dx);
+  // Default (MNISTX_DGRAD_VAR=4): two images per group, A-row reuse with one row read
+  // ahead (158 VGPRs, 3 waves/SIMD): 120 us at B = 65536.  2: one image, the 15 A
+  // fragments of a fragment in batches of 8 (122 VGPRs, 4 waves): 134 us.  0: two
+  // images, all 15 in flight (150 VGPRs, 3 waves): 143-149 us.  Row reuse at one image
+  // per group (4 waves) or two rows ahead spills (192 / 157 us).
+  static const int var = [] { const char* e = getenv("MNISTX_DGRAD_VAR"); return e ? atoi(e) : 4; }();
+  int cap;
+#define MNISTX_DG(IM, ...)                                                                                   \
+  cap = resident_grid<convpool_dgrad_pair_k<G, __VA_ARGS__>>();                                            \
+  if (grid_cap > 0 && grid_cap < cap) cap = grid_cap;                                                      \
+  hipLaunchKernelGGL((convpool_dgrad_pair_k<G, __VA_ARGS__>), dim3(grid_for(B, IM, cap)), dim3(NTH), 0, st, \
+                     dP, arg, w, B, dx);
+  if (var == 0) { MNISTX_DG(IMGS, IMGS) }
+  else if (var == 2) { MNISTX_DG(1, 1, 8, 4) }
+  else { MNISTX_DG(2, 2, 0, 3, 1) }
+#undef MNISTX_DG
   return hipGetLastError();
 }
 

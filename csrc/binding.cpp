@@ -637,7 +637,7 @@ void convpool_fwd(Tensor x, Tensor w, Tensor bias, int64_t bias_n, Tensor pooled
   check(w, at::kBFloat16, ks * ks * cin * cout, "w");
   check(bias, at::kFloat, bias_n, "bias");
   check(pooled, at::kBFloat16, B * g.PH * g.PW * cout, "pooled");
-  check(arg, at::kByte, B * g.PH * g.PW * cout, "arg");
+  check(arg, at::kByte, B * g.PH * g.PW * mnistx::convpool_arg_bytes(g.cfg), "arg");
   hip_ok(mnistx::convpool_fwd(g.cfg, src, BF(w), P<const float>(bias), (int)bias_n, (int)B, BFm(pooled),
                               P<uint8_t>(arg), cur_stream()),
          "convpool_fwd");
@@ -651,7 +651,7 @@ void convpool_wgrad(Tensor x, Tensor dP, Tensor arg, Tensor slab, int64_t grid, 
   const int64_t np = B * g.PH * g.PW * cout;
   const auto src = cp_src(x, u8, idx, g.cfg, B, h * wd * cin);
   check(dP, at::kBFloat16, np, "dP");
-  check(arg, at::kByte, np, "arg");
+  check(arg, at::kByte, B * g.PH * g.PW * mnistx::convpool_arg_bytes(g.cfg), "arg");
   check(slab, at::kFloat, grid * g.KM * cout, "slab");
   const mnistx::bf16_t* lp = nullptr;
   if (lrn_p.has_value() && lrn_p->defined()) {
@@ -674,6 +674,10 @@ int64_t convpool_wgrad_grid(int64_t cin, int64_t cout, int64_t ks, int64_t pad, 
   return n;
 }
 
+int64_t convpool_arg_bytes(int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t w) {
+  return mnistx::convpool_arg_bytes(cp_geo(cin, cout, ks, pad, h, w).cfg);
+}
+
 bool convpool_has_dgrad(int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t w) {
   return mnistx::convpool_has_dgrad(cp_geo(cin, cout, ks, pad, h, w).cfg) != 0;
 }
@@ -684,7 +688,7 @@ void convpool_dgrad(Tensor dP, Tensor arg, Tensor w, Tensor dx, int64_t B, int64
   TORCH_CHECK(mnistx::convpool_has_dgrad(g.cfg), "convpool_dgrad: no fused dgrad for this geometry");
   const int64_t np = B * g.PH * g.PW * cout;
   check(dP, at::kBFloat16, np, "dP");
-  check(arg, at::kByte, np, "arg");
+  check(arg, at::kByte, B * g.PH * g.PW * mnistx::convpool_arg_bytes(g.cfg), "arg");
   check(w, at::kBFloat16, ks * ks * cin * cout, "w");
   check(dx, at::kBFloat16, B * h * wd * cin, "dx");
   hip_ok(mnistx::convpool_dgrad(g.cfg, BF(dP), P<const uint8_t>(arg), BF(w), (int)B, BFm(dx), (int)grid_cap,
@@ -866,7 +870,7 @@ void lenet_c2dgrad_c1wgrad(Tensor x, Tensor dP2, Tensor arg2, Tensor w2, Tensor 
   check(dP2, at::kBFloat16, B * 5 * 5 * 16, "dP2");
   check(arg2, at::kByte, B * 5 * 5 * 16, "arg2");
   check(w2, at::kBFloat16, 5 * 5 * 8 * 16, "w2");
-  check(arg1, at::kByte, B * 14 * 14 * 8, "arg1");
+  check(arg1, at::kByte, B * 14 * 14 * 4, "arg1");   // packed 4-bit codes
   check(slab, at::kFloat, grid * mnistx::convpool_wgrad_rows(cfg1) * 8, "slab");
   hip_ok(mnistx::lenet_c2dgrad_c1wgrad(src, BF(dP2), P<const uint8_t>(arg2), BF(w2), P<const uint8_t>(arg1), (int)B,
                                        P<float>(slab), (int)grid, cur_stream()),
@@ -963,6 +967,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("convpool_dgrad", &convpool_dgrad, py::arg("dP"), py::arg("arg"), py::arg("w"), py::arg("dx"), py::arg("B"),
         py::arg("cin"), py::arg("cout"), py::arg("ks"), py::arg("pad"), py::arg("h"), py::arg("w_"),
         py::arg("grid_cap") = 0);
+  m.def("convpool_arg_bytes", &convpool_arg_bytes);
   m.def("convpool_has_dgrad", &convpool_has_dgrad);
   m.def("convpool_wgrad_grid", &convpool_wgrad_grid);
   m.attr("ARCH") = "gfx950";

@@ -188,6 +188,13 @@ template <class G> constexpr int wgrad_minw() { return (G::CIN == 8 && G::COUT =
 // the backward kernels need only (dP, arg) -- the ReLU mask is folded in here
 // and the pooled activations are never re-read.
 constexpr uint32_t ARG_OFF = 4;
+// LeNet conv1 (8 channels, quad forward): the argmax codes (0..3, ARG_OFF) are stored
+// packed, 4 bits each: byte k of a window = code(c = k) | code(c = k + 4) << 4
+// (4 bytes per window instead of 8).  Other geometries keep one byte per channel.
+template <class G>
+constexpr bool arg_packed() { return G::MODE == 0 && G::COUT == 8 && G::H == 28 && G::W == 28 && G::PAD == 2; }
+template <class G>
+constexpr int arg_bytes() { return arg_packed<G>() ? G::COUT / 2 : G::COUT; }
 
 template <int N>
 DEV void lds_zero(bf16_t* p, int tid) {
@@ -338,14 +345,18 @@ struct DYStage {
   // contribute nothing (every consumer multiplies / selects dP by the argmax)
   DEV void load(const bf16_t* __restrict__ dP, const uint8_t* __restrict__ arg, int img0, int B, int tid) {
     const int nimg = max(0, min(IMGS, B - img0));
+    constexpr int AB = arg_bytes<G>();                 // arg bytes per window
     const auto ry = buf_rsrc(dP + (int64_t)img0 * NWC, (uint32_t)(nimg * NWC * 2));
-    const auto ra = buf_rsrc(arg + (int64_t)img0 * NWC, (uint32_t)(nimg * NWC));
+    const auto ra = buf_rsrc(arg + (int64_t)img0 * G::NWIN * AB, (uint32_t)(nimg * G::NWIN * AB));
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int e = 8 * (tid + u * NTH);
       const bool ok = e < IMGS * NWC;
       y[u] = buf_b128(ry, ok ? (uint32_t)(e * 2) : BUF_OOB);
-      a[u] = buf_b64(ra, ok ? (uint32_t)e : BUF_OOB);
+      if constexpr (arg_packed<G>())   // one window's 8 packed codes
+        a[u] = u32x2{buf_b32(ra, ok ? (uint32_t)(e / 8 * AB) : BUF_OOB), 0u};
+      else
+        a[u] = buf_b64(ra, ok ? (uint32_t)e : BUF_OOB);
     }
   }
   DEV void store(bf16_t* dys, uint8_t* args, int tid) const {
@@ -759,22 +770,29 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
       // the group's outputs are contiguous in HBM: full 16-byte stores
       const int nimg = min(IMGS, B - img0);
       bf16_t* pg = pooled + (int64_t)img0 * OUTE;
-      uint8_t* ag = arg + (int64_t)img0 * OUTE;
+      uint8_t* ag = arg + (int64_t)img0 * (Q::NWIN * 4);
       // compile-time store counts (unrolled, exec-masked tails): the loop-top wait for the
       // prefetched loads is then vmcnt(#stores) -- a runtime-trip-count store loop made it
       // wait for these stores to complete as well (loads and stores share vmcnt, in order)
-      constexpr int PV = IMGS * OUTE / 8, AV = IMGS * OUTE / 16;
+      constexpr int PV = IMGS * OUTE / 8;
 #pragma unroll
       for (int u = 0; u < (PV + NTH - 1) / NTH; ++u) {
         const int e = tid + u * NTH, im = e / (OUTE / 8);
         if (e < nimg * (OUTE / 8))
           *(u32x4*)(pg + 8 * e) = *(const u32x4*)(pout + im * OUTS + 8 * (e - im * (OUTE / 8)));
       }
+      // argmax codes packed 4 bits each (arg_packed<LeNetC1>): 16 output bytes = 4
+      // windows (32 LDS bytes)
+      constexpr int AV4 = IMGS * Q::NWIN / 4;
+      static_assert(Q::NWIN % 4 == 0, "");
 #pragma unroll
-      for (int u = 0; u < (AV + NTH - 1) / NTH; ++u) {
-        const int e = tid + u * NTH, im = e / (OUTE / 16);
-        if (e < nimg * (OUTE / 16))
-          *(u32x4*)(ag + 16 * e) = *(const u32x4*)(aout + im * OUTS + 16 * (e - im * (OUTE / 16)));
+      for (int u = 0; u < (AV4 + NTH - 1) / NTH; ++u) {
+        const int e = tid + u * NTH, im = e / (Q::NWIN / 4);
+        if (e < nimg * (Q::NWIN / 4)) {
+          const uint8_t* src = aout + im * OUTS + 32 * (e - im * (Q::NWIN / 4));
+          const u32x4 lo = *(const u32x4*)src, hi = *(const u32x4*)(src + 16);
+          *(u32x4*)(ag + 16 * e) = u32x4{lo[0] | lo[1] << 4, lo[2] | lo[3] << 4, hi[0] | hi[1] << 4, hi[2] | hi[3] << 4};
+        }
       }
     }
   }
@@ -1085,9 +1103,16 @@ __global__ __launch_bounds__(NTH, 6) void convpool_wgrad_pair_k(const XSrc x,
         uint32_t* urow = U + im * UIMG + win;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          // y_c in both halves, d_c (0..3, ARG_OFF = 4) in all four bytes
+          // y_c in both halves, d_c (0..3, ARG_OFF = 4) in all four bytes (packed codes:
+          // byte c & 3, nibble c >> 2)
           const uint32_t y2 = __builtin_amdgcn_perm(0u, ys.y[u][c >> 1], (c & 1) ? 0x03020302u : 0x01000100u);
-          const uint32_t r = __builtin_amdgcn_perm(0u, ys.a[u][c >> 2], 0x01010101u * (c & 3));
+          uint32_t r;
+          if constexpr (arg_packed<G>()) {
+            const uint32_t t = __builtin_amdgcn_perm(0u, ys.a[u][0], 0x01010101u * (c & 3));
+            r = ((c >> 2) ? t >> 4 : t) & 0x0f0f0f0fu;
+          } else {
+            r = __builtin_amdgcn_perm(0u, ys.a[u][c >> 2], 0x01010101u * (c & 3));
+          }
           // byte b of the mask = table[d + k_b] with 0xff only at byte 3: set iff d == 3 - k_b.
           // side 0: (dy0, dy1) = positions (0, 2) -> k = (3, 3, 1, 1); side 1: (1, 3) -> (2, 2, 0, 0)
           urow[c * URS] = y2 & __builtin_amdgcn_perm(0u, 0xff000000u, r + 0x01010303u);
@@ -1487,8 +1512,9 @@ __global__ __launch_bounds__(NTH, 3) void lenet_c2dgrad_c1wgrad_k(const XSrc x, 
   constexpr int URS = 212;
   static_assert(URS >= RS * 16 && URS % 8 == 4, "U row stride");
   constexpr int UIMG = 16 * URS;
-  constexpr int NWC1 = G1::NWIN * 8;                  // arg1 bytes per image
-  static_assert(NWC1 % 16 == 0 && G2::H * G2::W == G1::NWIN && G2::CIN == 8, "dP1 = pool1 windows x 8 channels");
+  constexpr int NWC1 = G1::NWIN * arg_bytes<G1>();    // arg1 bytes per image (packed codes)
+  static_assert(arg_packed<G1>() && NWC1 % 16 == 0 && G2::H * G2::W == G1::NWIN && G2::CIN == 8,
+                "dP1 = pool1 windows x 8 channels");
   constexpr int TILE_E = (IMGS * G1::IMG_LDS + 7) / 8 * 8;
   __shared__ __attribute__((aligned(16))) bf16_t dyt[IMGS * DT];
   __shared__ __attribute__((aligned(16))) bf16_t tile[TILE_E];
@@ -1602,7 +1628,9 @@ __global__ __launch_bounds__(NTH, 3) void lenet_c2dgrad_c1wgrad_k(const XSrc x, 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int jr = 4 * (g & 1) + r;
-        av4[r] = 2 * jr < G2::W ? a1s[im * NWC1 + (ih * G2::W + 2 * jr + sx) * 8 + ci] : 4u;
+        av4[r] = 2 * jr < G2::W
+                     ? (uint32_t)(a1s[im * NWC1 + (ih * G2::W + 2 * jr + sx) * 4 + (ci & 3)] >> (4 * (ci >> 2))) & 15u
+                     : 4u;
       }
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       // the chain's A fragments in batches of DB in flight (all 15 at once cost 40 VGPRs
@@ -1806,6 +1834,16 @@ int convpool_wgrad_grid(int cfg) {
 }
 
 int convpool_has_dgrad(int cfg) { return cfg == 1 ? 1 : 0; }
+
+int convpool_arg_bytes(int cfg) {
+  switch (cfg) {
+    case 0: return arg_bytes<LeNetC1>();
+    case 1: return arg_bytes<LeNetC2>();
+    case 2: return arg_bytes<RefC1g>();
+    case 3: return arg_bytes<RefC1c>();
+    default: return -1;
+  }
+}
 
 int convpool_u8_input(int cfg) { return (cfg == 0 || cfg == 2) ? 1 : 0; }  // Cin == 1 first layers
 

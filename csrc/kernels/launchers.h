@@ -91,6 +91,8 @@ hipError_t convpool_wgrad(int cfg, const XSrc& x, const bf16_t* dP, const uint8_
                           int grid, hipStream_t st, const bf16_t* lrn_p = nullptr, float lrn_bias = 0.f,
                           float lrn_alpha = 0.f, float lrn_beta = 0.f);
 int convpool_has_dgrad(int cfg);
+// argmax bytes per pool window (LeNet conv1: 8 codes packed 4 bits each)
+int convpool_arg_bytes(int cfg);
 hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int B, bf16_t* dx,
                           int grid_cap, hipStream_t st);
 // LeNet-5 conv2 data gradient fused into conv1's weight gradient (dP1 never in HBM):

@@ -150,7 +150,9 @@ class ConvPoolLayer(_Layer):
         OH, OW = Fk.conv_out_hw(self.H, self.W, 5, 5, spec.padding)
         self.PH, self.PW = OH // 2, OW // 2
         self.out = _bf16(B, self.PH, self.PW, self.Cp, device=dev)
-        self.arg = torch.zeros(B, self.PH, self.PW, self.Cp, dtype=torch.uint8, device=dev)
+        # argmax codes: one byte per channel, or (LeNet conv1) 4 bits each
+        ab = kernels().convpool_arg_bytes(self.C, self.Cp, 5, self.pad, self.H, self.W)
+        self.arg = torch.zeros(B, self.PH, self.PW, ab, dtype=torch.uint8, device=dev)
         self.wname, self.bname = f"{spec.name}/weights", f"{spec.name}/biases"
         self.KM = kernels().convpool_rows(self.C, self.Cp, 5, self.pad, self.H, self.W)
         self.red = kernels().convpool_reduce_args(*self._geo(), spec.cin)   # (G, Ipad, I, bias_row)

@@ -339,7 +339,8 @@ def test_convpool(dev, K, N, H, W, Ci, ci, Co, co, pad):
     OH, OW = (H, W) if pad else (H - 4, W - 4)
     PH, PW = OH // 2, OW // 2
     pooled = torch.empty(N, PH, PW, Co, dtype=torch.bfloat16, device=dev)
-    arg = torch.empty(N, PH, PW, Co, dtype=torch.uint8, device=dev)
+    ab = K.convpool_arg_bytes(Ci, Co, 5, pad, H, W)     # LeNet conv1: 8 codes packed 4 bits each
+    arg = torch.empty(N, PH, PW, ab, dtype=torch.uint8, device=dev)
     K.convpool_fwd(x, w, b, co, pooled, arg, N, Ci, Co, 5, pad, H, W)
     # oracle: conv -> bias -> relu -> pool (fp32)
     xr = x.float().requires_grad_(True)
@@ -365,8 +366,10 @@ def test_convpool(dev, K, N, H, W, Ci, ci, Co, co, pad):
     K.splitk_reduce(slab, grid, KM, Co, G, Ip, I, co, brow, dw, db, 1.0)
     close(dw, wr.grad[:, :, :ci, :co], rel=3e-2)
     close(db, br.grad[:co], rel=3e-2)
-    # the ReLU mask lives in the argmax byte: 4 exactly where the pooled output is 0
-    assert torch.equal(arg == 4, pooled == 0)
+    # the ReLU mask lives in the argmax code: 4 exactly where the pooled output is 0
+    codes = arg if ab == Co else torch.cat([arg & 15, arg >> 4], dim=-1)   # byte k = code k | code k+4 << 4
+    assert torch.equal(codes == 4, pooled == 0)
+    assert int(codes.max()) <= 4
     if K.convpool_has_dgrad(Ci, Co, 5, pad, H, W):
         dx = torch.empty(N, H, W, Ci, dtype=torch.bfloat16, device=dev)
         K.convpool_dgrad(dP, arg, w, dx, N, Ci, Co, 5, pad, H, W)

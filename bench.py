@@ -52,7 +52,11 @@ def parse():
     ap.add_argument("--optimizer", default="momentum", choices=["sgd", "momentum", "nesterov"])
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--fused_input", type=int, default=0, help="first conv reads the uint8 dataset directly")
+    ap.add_argument("--fused_input", type=int, default=0, help="alias of --input u8")
+    ap.add_argument("--input", default="bf16", choices=["prep", "u8", "bf16"],
+                    help="HIP input path: bf16 (default: the first conv gathers the resident dataset, normalised "
+                         "once to bf16) | u8 (same, uint8 normalised in the kernels) | prep (a per-step "
+                         "gather+normalise kernel writes the batch buffer)")
     ap.add_argument("--overlap", default="none", choices=["none", "dense", "all"],
                     help="weight gradients on a side stream: none / dense layers only / every layer")
     ap.add_argument("--dataset_size", type=int, default=60000)
@@ -197,10 +201,11 @@ def main() -> int:
 
     imgs, labs = make_synthetic(args.dataset_size, seed=args.seed, channels=1, device=dev)
     ds = DeviceDataset(imgs, labs, dev, hw=784, channels=1)
-    # --fused_input: the first fused conv reads the uint8 dataset through the batch index
-    # (K10 fused).  Off by default: measured ~25 us/step slower on LeNet-5 at 65536 than
-    # prep_images + bf16 (profiles/r1_u8_input/).
-    fused_in = args.impl == "hip" and args.fused_input and net.bind_u8_input(ds.images)
+    # --input u8 / bf16: the first fused conv gathers the resident dataset through the
+    # batch index (K10 fused into its staging); prep: one gather+normalise kernel per step
+    mode = "u8" if args.fused_input else args.input
+    fused_in = args.impl == "hip" and mode != "prep" and net.bind_u8_input(
+        ds.images if mode == "u8" else ds.bf16_images())
     loader = DeviceLoader(ds, net.x0, net.labels, rank=rank, world=world, seed=args.seed,
                           idx_out=net.idx_buf if fused_in else None)
 
@@ -297,6 +302,7 @@ def main() -> int:
                 "impl": args.impl,
                 "hip_graph": use_graph,
                 "optimizer": args.optimizer,
+                "input": mode if fused_in else "prep",
             },
             "tflops_per_s": round(tot * value / 1e12, 2),
             "final_train_loss": round(stats["cross_entropy"], 5),

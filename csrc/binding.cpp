@@ -220,11 +220,20 @@ int64_t conv_wgrad(Tensor x, Tensor dy, Tensor slab, int64_t Nb, int64_t H, int6
   return S;
 }
 
-void perm_positions(Tensor out, int64_t start, int64_t N, int64_t seed, int64_t h) {
+// lab_src [N] / lab_out [n] (optional, int32): gather the chosen rows' labels in the same launch
+void perm_positions(Tensor out, int64_t start, int64_t N, int64_t seed, int64_t h, optional<Tensor> lab_src,
+                    optional<Tensor> lab_out) {
   TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kLong && out.is_contiguous(), "perm_positions: out");
   TORCH_CHECK(N > 0 && h >= 1 && h <= 31 && (1ll << (2 * h)) >= N, "perm_positions: bad domain");
+  const bool labs = lab_src.has_value() && lab_src->defined();
+  TORCH_CHECK(labs == (lab_out.has_value() && lab_out->defined()), "perm_positions: lab_src and lab_out together");
+  if (labs) {
+    check(*lab_src, at::kInt, N, "lab_src");
+    check(*lab_out, at::kInt, out.numel(), "lab_out");
+  }
   hip_ok(mnistx::perm_positions(out.data_ptr<int64_t>(), start, (int)out.numel(), N, (uint32_t)seed, (int)h,
-                                cur_stream()),
+                                cur_stream(), labs ? P<const int32_t>(*lab_src) : nullptr,
+                                labs ? P<int32_t>(*lab_out) : nullptr),
          "perm_positions");
 }
 
@@ -622,6 +631,17 @@ mnistx::XSrc cp_src(const Tensor& x, const optional<Tensor>& u8, const optional<
     src.u8 = P<const uint8_t>(*u8);
     src.idx = P<const int64_t>(*idx);
     src.n = (int)(u8->numel() / hwc);       // the kernel clamps every index into [0, n)
+  } else if (idx.has_value() && idx->defined()) {
+    // x is the resident bf16 dataset [n, H*W*C] (normalised once), gathered through idx
+    TORCH_CHECK(mnistx::convpool_u8_input(cfg), "convpool: dataset input only for 1-channel first layers");
+    check(x, at::kBFloat16, hwc, "x (dataset)");
+    TORCH_CHECK(x.numel() % hwc == 0 && x.numel() * 2 < (int64_t)INT32_MAX,
+                "x (dataset): [n, H*W*C] bf16 images, < 2 GB (one buffer resource)");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 8 == 0, "x (dataset) must be 8-byte aligned");
+    check(*idx, at::kLong, B, "idx");
+    src.x = BF(x);
+    src.idx = P<const int64_t>(*idx);
+    src.n = (int)(x.numel() / hwc);
   } else {
     check(x, at::kBFloat16, B * hwc, "x");
     src.x = BF(x);
@@ -920,7 +940,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("prep_images", &prep_images);
   m.def("dense_wgrad_group", &dense_wgrad_group);
   m.def("conv_wgrad_pref_splits", &conv_wgrad_pref_splits);
-  m.def("perm_positions", &perm_positions);
+  m.def("perm_positions", &perm_positions, py::arg("out"), py::arg("start"), py::arg("N"), py::arg("seed"), py::arg("h"),
+        py::arg("lab_src") = py::none(), py::arg("lab_out") = py::none());
   m.def("prep_images_perm", &prep_images_perm);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

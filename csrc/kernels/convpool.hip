@@ -210,42 +210,115 @@ DEV void lds_zero(bf16_t* p, int tid) {
 template <class G, int IMGS>
 struct XStage {
   static constexpr int NV = IMGS * G::H * G::ROWV;
-  static constexpr int PER = (NV + NTH - 1) / NTH;
+  static constexpr int VPI = G::H * G::ROWV;   // vectors per image
+  static constexpr int NWV = NTH / 64;
+  static constexpr bool U8 = G::CIN == 1;      // dataset gathers only for 1-channel first layers
+  // First-layer geometries: whole waves load one image (WPI waves per image), so the
+  // image -- and, for dataset gathers, its row -- is wave-uniform: one index load per
+  // wave per group and no per-vector row select (the select + 64-bit clamp cost
+  // ~25 VALU per vector in the 4-image forward).
+  static constexpr bool WIMG = U8 && IMGS <= NWV;
+  static constexpr int WPI = WIMG ? NWV / IMGS : 1;
+  static constexpr int TPI = 64 * WPI;
+  static constexpr int PER = WIMG ? (VPI + TPI - 1) / TPI : (NV + NTH - 1) / NTH;
+  // vector slot u of thread tid -> image-major vector index e (NV: no vector)
+  static DEV int vec(int u, int tid) {
+    if constexpr (WIMG) {
+      const int im = (tid >> 6) / WPI, j = tid % TPI + u * TPI;
+      return (im < IMGS && j < VPI) ? im * VPI + j : NV;
+    } else {
+      return min(tid + u * NTH, NV);
+    }
+  }
   u32x2 v[PER];
-  // uint8 source: dataset rows of the group to load next, fetched one group ahead
-  // so the (uniform) index load never stalls the data prefetch behind it.  The raw
-  // int64 indices are loaded unconditionally (clamped address) and clamped only when
-  // load() uses them: a conditional load + clamp here waited for each index in turn.
-  int64_t rows[IMGS];
-  static constexpr bool U8 = G::CIN == 1;   // uint8 input only for 1-channel first layers
+  // dataset gathers: row index of the group to load next, fetched one group ahead so
+  // its load never stalls the data prefetch behind it.  WIMG: the wave's own image,
+  // by a VECTOR load (a scalar load would share lgkmcnt with every LDS wait of the
+  // compute phase); raw int64, clamped only when load() uses it.  Otherwise every
+  // image's row by (uniform) scalar loads.
+  u32x2 wrow;
+  int64_t rows[WIMG ? 1 : IMGS];
   DEV void fetch_rows(const XSrc& src, int img0, int B) {
-    if (!U8 || !src.u8 || B <= 0) return;
+    if (!U8 || !src.idx || B <= 0) return;
+    if constexpr (WIMG) {
+      const int im = min((int)(threadIdx.x >> 6) / WPI, IMGS - 1);
+      wrow = buf_b64(buf_rsrc(src.idx, (uint32_t)B * 8u), 8u * (uint32_t)max(0, min(img0 + im, B - 1)));
+    } else {
 #pragma unroll
-    for (int im = 0; im < IMGS; ++im) rows[im] = src.idx[max(0, min(img0 + im, B - 1))];
+      for (int im = 0; im < IMGS; ++im) rows[im] = src.idx[max(0, min(img0 + im, B - 1))];
+    }
   }
   DEV int row_of(const XSrc& src, int k) const {
     return (int)min(max(rows[k], (int64_t)0), (int64_t)src.n - 1);
   }
-  // bf16 activations, or (first layer) the uint8 dataset gathered through the
-  // batch index and normalised x/255 - 0.5 exactly like prep_images (K10 fused).
-  // uint8: rows[] must hold the rows of this group (fetch_rows one group earlier).
+  // byte offset of this wave's image in a dataset of EB-byte pixels (WIMG), wave-uniform
+  template <int EB>
+  DEV uint32_t wave_base(const XSrc& src) const {
+    const int64_t r = (int64_t)(((uint64_t)wrow[1] << 32) | wrow[0]);
+    const uint32_t row = (uint32_t)min(max(r, (int64_t)0), (int64_t)src.n - 1);
+    return __builtin_amdgcn_readfirstlane(row * (uint32_t)(G::INTERIOR * EB));
+  }
+  // bf16 activations, or (first layer) a resident dataset gathered through the
+  // batch index: uint8, normalised x/255 - 0.5 exactly like prep_images (K10 fused),
+  // or bf16 already normalised (XSrc.x with idx set).
+  // gathers: the row(s) of this group must have been fetched (fetch_rows one group earlier).
   // Branch-free buffer loads (common.h buf_*): invalid slots read zeros; the raw
   // uint8 words are converted only at store time, so no load is waited for here.
   bool u8mode = false;
   DEV void load(const XSrc& src, int img0, int B, int tid) {
     const int nimg = max(0, min(IMGS, B - img0));
     u8mode = U8 && src.u8 != nullptr;
-    if (U8 && src.u8) {
+    if constexpr (WIMG) {
+      const int im = (tid >> 6) / WPI;
+      const bool img_ok = im < nimg;
+      if (src.u8) {
+        const auto r = buf_rsrc(src.u8, (uint32_t)((int64_t)src.n * G::INTERIOR));
+        const uint32_t base = wave_base<1>(src);
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+          const int j = tid % TPI + u * TPI;
+          v[u] = u32x2{buf_b32(r, img_ok && j < VPI ? base + (uint32_t)j * 4u : BUF_OOB), 0u};
+        }
+      } else if (src.idx) {
+        // resident bf16 dataset (already normalised): gathered 8-byte vectors, no conversion
+        const auto r = buf_rsrc(src.x, (uint32_t)((int64_t)src.n * G::INTERIOR * 2));
+        const uint32_t base = wave_base<2>(src);
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+          const int j = tid % TPI + u * TPI;
+          v[u] = buf_b64(r, img_ok && j < VPI ? base + (uint32_t)j * 8u : BUF_OOB);
+        }
+      } else {
+        const auto r = buf_rsrc(src.x + (int64_t)img0 * G::INTERIOR, (uint32_t)(nimg * G::INTERIOR * 2));
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+          const int e = vec(u, tid);
+          v[u] = buf_b64(r, e < NV ? (uint32_t)(e * 8) : BUF_OOB);
+        }
+      }
+    } else if (U8 && src.u8) {
       const auto r = buf_rsrc(src.u8, (uint32_t)((int64_t)src.n * G::INTERIOR));
 #pragma unroll
       for (int u = 0; u < PER; ++u) {
         const int e = tid + u * NTH;
-        const int im = e / (G::H * G::ROWV), rem = e - im * (G::H * G::ROWV);
+        const int im = e / VPI, rem = e - im * VPI;
         int row = row_of(src, 0);
 #pragma unroll
         for (int k = 1; k < IMGS; ++k) row = im == k ? row_of(src, k) : row;
         const bool ok = e < NV && im < nimg;
         v[u] = u32x2{buf_b32(r, ok ? (uint32_t)(row * G::INTERIOR + rem * 4) : BUF_OOB), 0u};
+      }
+    } else if (U8 && src.idx) {
+      const auto r = buf_rsrc(src.x, (uint32_t)((int64_t)src.n * G::INTERIOR * 2));
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int e = tid + u * NTH;
+        const int im = e / VPI, rem = e - im * VPI;
+        int row = row_of(src, 0);
+#pragma unroll
+        for (int k = 1; k < IMGS; ++k) row = im == k ? row_of(src, k) : row;
+        const bool ok = e < NV && im < nimg;
+        v[u] = buf_b64(r, ok ? (uint32_t)(row * G::INTERIOR * 2 + rem * 8) : BUF_OOB);
       }
     } else {
       const auto r = buf_rsrc(src.x + (int64_t)img0 * G::INTERIOR, (uint32_t)(nimg * G::INTERIOR * 2));
@@ -262,9 +335,17 @@ struct XStage {
     return u32x2{pack2(u8_norm(b4 & 0xff), u8_norm((b4 >> 8) & 0xff)),
                  pack2(u8_norm((b4 >> 16) & 0xff), u8_norm(b4 >> 24))};
   }
+  // Called at the top of a group, where the previous group's prefetch loads (x, the
+  // next row index, the dY staging) are all about to be consumed: one explicit
+  // vmcnt(0) at this dominating point.  Without it the waitcnt pass, merging over the
+  // per-lane staging branches, inserted full waits BEHIND the new gathered prefetch
+  // loads (a whole memory latency per group in the gathered-input weight gradient).
+  static DEV void drain() {
+    if constexpr (U8) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt/lgkmcnt untouched
+  }
   // offset of vector e in the LDS tile
   static DEV int tile_off(int e) {
-    const int im = e / (G::H * G::ROWV), rem = e - im * (G::H * G::ROWV);
+    const int im = e / VPI, rem = e - im * VPI;
     const int hh = rem / G::ROWV, vv = rem - hh * G::ROWV;
     return im * G::IMG_LDS + ((hh + G::PAD) * G::WS + G::X0) * G::CIN + 4 * vv;
   }
@@ -274,13 +355,13 @@ struct XStage {
     if (U8 && u8mode) {
 #pragma unroll
       for (int u = 0; u < PER; ++u) {
-        const int e = tid + u * NTH;
+        const int e = vec(u, tid);
         if (e < NV) *(u32x2*)(tile + tile_off(e)) = value(u);
       }
     } else {
 #pragma unroll
       for (int u = 0; u < PER; ++u) {
-        const int e = tid + u * NTH;
+        const int e = vec(u, tid);
         if (e < NV) *(u32x2*)(tile + tile_off(e)) = v[u];
       }
     }
@@ -443,6 +524,7 @@ __global__ __launch_bounds__(NTH, fwd_minw<G>()) void convpool_fwd_k(const XSrc 
   xs.load(x, blockIdx.x * IMGS, B, tid);
   xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
+    xs.drain();
     __syncthreads();
     xs.store(tile, tid);
     __syncthreads();
@@ -573,6 +655,7 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_pair_k(const XSrc x, const b
   xs.load(x, blockIdx.x * IMGS, B, tid);
   xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
+    xs.drain();
     __syncthreads();
     xs.store(tile, tid);
     __syncthreads();
@@ -692,13 +775,14 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
   xs.load(x, blockIdx.x * IMGS, B, tid);
   xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
+    xs.drain();
     __syncthreads();
     // interior rows at column X0 = 10 (4-byte aligned): two 4-byte stores per vector;
     // the uint8 conversion behind a uniform branch (not a per-vector select)
     auto stage = [&](auto conv) {
 #pragma unroll
       for (int u = 0; u < XStage<Q, IMGS>::PER; ++u) {
-        const int e = tid + u * NTH;
+        const int e = XStage<Q, IMGS>::vec(u, tid);
         if (e < XStage<Q, IMGS>::NV) {
           const int im = e / (Q::H * Q::ROWV), rem = e - im * (Q::H * Q::ROWV);
           const int hh = rem / Q::ROWV, vv = rem - hh * Q::ROWV;
@@ -870,6 +954,7 @@ __global__ __launch_bounds__(NTH, wgrad_minw<G>()) void convpool_wgrad_k(const X
   ys.load(dP, arg, blockIdx.x * IMGS, B, tid);
   ys.load_lrn(lrn.p, blockIdx.x * IMGS, B, tid);
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
+    xs.drain();
     __syncthreads();
     xs.store(tile, tid);
     ys.apply_lrn(lrn, tid);
@@ -1092,6 +1177,7 @@ __global__ __launch_bounds__(NTH, 6) void convpool_wgrad_pair_k(const XSrc x,
   xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
   ys.load(dP, arg, blockIdx.x * IMGS, B, tid);
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
+    xs.drain();
     __syncthreads();
     xs.store(tile, tid);
     // max-unpool into U: U[sx*8+c][w] = (dy0: arg==sx ? dP : 0, dy1: arg==2+sx ? dP : 0)
@@ -1581,6 +1667,7 @@ __global__ __launch_bounds__(NTH, 3) void lenet_c2dgrad_c1wgrad_k(const XSrc x, 
   ys.load(dP2, arg2, blockIdx.x * IMGS, B, tid);
   load_a1(blockIdx.x * IMGS);
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
+    xs.drain();
     __syncthreads();
     xs.store(tile, tid);
 #pragma unroll

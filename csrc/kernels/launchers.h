@@ -67,8 +67,9 @@ hipError_t conv_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int H, int W, i
                       hipStream_t st, LrnParams lrn = LrnParams{0.f, 0.f, 0.f, 0});
 
 // ---- convpool.hip (fused small-channel conv + bias + ReLU + 2x2 max-pool)
-// Input of a fused conv: bf16 NHWC activations, or (Cin == 1 first layer) the
-// uint8 dataset [n][H*W] gathered through the per-sample index idx[B].
+// Input of a fused conv: bf16 NHWC activations x[B], or (Cin == 1 first layer) a
+// resident dataset [n][H*W] gathered through the per-sample index idx[B]: uint8
+// (u8 set, normalised in the kernel) or bf16 already normalised (x set, u8 null).
 struct XSrc {
   const bf16_t* x;
   const uint8_t* u8;
@@ -129,7 +130,8 @@ hipError_t f32_prep_images(const uint8_t* src, const int64_t* idx, const int32_t
                            int Cdst, float* out, int32_t* lab_out, hipStream_t st);
 
 // ---- misc.hip
-hipError_t perm_positions(int64_t* out, int64_t start, int n, int64_t N, uint32_t seed, int h, hipStream_t st);
+hipError_t perm_positions(int64_t* out, int64_t start, int n, int64_t N, uint32_t seed, int h, hipStream_t st,
+                          const int32_t* lab_src = nullptr, int32_t* lab_out = nullptr);
 // 28x28x1 batch gather + normalise with the Feistel epoch shuffle fused in (rows are
 // perm_positions(start + b)): no index array, no separate permutation launch
 hipError_t prep_images_perm(const uint8_t* src, const int32_t* lab_src, int B, int64_t start, int64_t N,

@@ -48,7 +48,10 @@ DEV uint64_t feistel4(uint64_t x, const uint32_t* key, int h) {
   }
   return (L << h) | R;
 }
-__global__ void perm_positions_k(int64_t* __restrict__ out, int64_t start, int n, int64_t N, uint32_t seed, int h) {
+// lab_src / lab_out (optional): the labels of the chosen rows gathered in the same
+// launch (the resident-dataset input modes need only the index and the labels).
+__global__ void perm_positions_k(int64_t* __restrict__ out, int64_t start, int n, int64_t N, uint32_t seed, int h,
+                                 const int32_t* __restrict__ lab_src, int32_t* __restrict__ lab_out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t p = start + i;
@@ -60,6 +63,7 @@ __global__ void perm_positions_k(int64_t* __restrict__ out, int64_t start, int n
   for (int r = 0; r < 4; ++r) key[r] = mix32(ek + 0x85ebca77u * (uint32_t)(r + 1));
   do { x = feistel4(x, key, h); } while (x >= (uint64_t)N);
   out[i] = (int64_t)x;
+  if (lab_out) lab_out[i] = lab_src[x];
 }
 
 // ------------------------------------------------------------------ K10 input prep
@@ -818,9 +822,11 @@ __global__ void cast_pad_k(const float* __restrict__ src, bf16_t* __restrict__ d
 
 }  // namespace
 
-hipError_t perm_positions(int64_t* out, int64_t start, int n, int64_t N, uint32_t seed, int h, hipStream_t st) {
+hipError_t perm_positions(int64_t* out, int64_t start, int n, int64_t N, uint32_t seed, int h, hipStream_t st,
+                          const int32_t* lab_src, int32_t* lab_out) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(perm_positions_k, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, st, out, start, n, N, seed, h);
+  hipLaunchKernelGGL(perm_positions_k, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, st, out, start, n, N, seed, h,
+                     lab_src, lab_out);
   return hipGetLastError();
 }
 

@@ -50,6 +50,20 @@ class DeviceDataset:
         self.images = images.to(self.device).contiguous()
         self.labels = labels.to(self.device, torch.int32).contiguous()
         self.hw, self.channels = hw, channels
+        self._bf16: Optional[torch.Tensor] = None
+
+    def bf16_images(self) -> torch.Tensor:
+        """The whole split normalised once (x/255 - 0.5, bf16, [n, hw*channels]): the
+        resident input of the bf16 dataset-gather mode (HipNet.bind_u8_input).  Built
+        with the same K10 kernel as the per-step gather, so it is bitwise what
+        ``prep_images`` would write for every row."""
+        if self._bf16 is None:
+            n = len(self)
+            out = torch.empty(n, self.hw * self.channels, dtype=torch.bfloat16, device=self.device)
+            labs = torch.empty(n, dtype=torch.int32, device=self.device)
+            gather_into(self, torch.arange(n, device=self.device), out.view(n, self.hw, self.channels), labs)
+            self._bf16 = out
+        return self._bf16
 
     def __len__(self) -> int:
         return int(self.images.shape[0])
@@ -72,19 +86,24 @@ def _half_bits(n: int) -> int:
     return h
 
 
-def perm_positions(start: int, n: int, N: int, seed: int, device=None, out: Optional[torch.Tensor] = None
-                   ) -> torch.Tensor:
+def perm_positions(start: int, n: int, N: int, seed: int, device=None, out: Optional[torch.Tensor] = None,
+                   labels: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """Dataset rows of stream positions start..start+n-1: position p -> F_e(p mod N),
     e = p // N, F_e a 4-round keyed Feistel bijection on [0, 4^h) restricted to
     [0, N) by cycle walking.  Every epoch is a full permutation of the dataset.
-    On a GPU this is the ``perm_positions`` HIP kernel (misc.hip), bit-identical."""
+    On a GPU this is the ``perm_positions`` HIP kernel (misc.hip), bit-identical.
+    ``labels`` = (dataset labels, out labels): also gather the rows' labels (one
+    launch on the GPU)."""
     h = _half_bits(N)
     seed &= M32
     dev = torch.device(device) if device is not None else (out.device if out is not None else torch.device("cpu"))
     if dev.type == "cuda":
         if out is None:
             out = torch.empty(n, dtype=torch.int64, device=dev)
-        kernels().perm_positions(out[:n], int(start), int(N), int(seed), int(h))
+        if labels is not None:
+            kernels().perm_positions(out[:n], int(start), int(N), int(seed), int(h), labels[0], labels[1][:n])
+        else:
+            kernels().perm_positions(out[:n], int(start), int(N), int(seed), int(h))
         return out[:n]
     mask = (1 << h) - 1
     p = torch.arange(start, start + n, dtype=torch.int64)
@@ -105,6 +124,8 @@ def perm_positions(start: int, n: int, N: int, seed: int, device=None, out: Opti
         if not bool(bad.any()):
             break
         x = torch.where(bad, F(x), x)
+    if labels is not None:
+        labels[1][:n].copy_(labels[0].to(x.device)[x])
     if out is not None:
         out[:n].copy_(x)
         return out[:n]
@@ -147,6 +168,12 @@ class DeviceLoader:
             # one kernel: Feistel row + gather + normalise (+ labels)
             kernels().prep_images_perm(self.ds.images, self.ds.labels, self.out_images, self.out_labels, nb,
                                        int(start), int(self.seed), _half_bits(N))
+            self.pos += self.global_batch
+            return nb
+        if self.shuffle and self.idx_out is not None and self.idx_out.is_cuda:
+            # resident-dataset input: the Feistel rows straight into the executor's index
+            # buffer, labels gathered in the same launch
+            perm_positions(start, nb, N, self.seed, out=self.idx_out, labels=(self.ds.labels, self.out_labels))
             self.pos += self.global_batch
             return nb
         if self.shuffle:

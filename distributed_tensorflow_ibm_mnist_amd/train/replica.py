@@ -84,7 +84,7 @@ class Replica:
                  train_images: torch.Tensor, train_labels: torch.Tensor, src_channels: int,
                  eval_images: Optional[torch.Tensor] = None, eval_labels: Optional[torch.Tensor] = None,
                  seed: int = 0, shard: bool = True, use_graph: bool = True, bucket_mb: float = 4.0,
-                 group=None, standalone: bool = False, fused_input: bool = False, precision: str = "bf16",
+                 group=None, standalone: bool = False, fused_input=False, precision: str = "bf16",
                  dp_graph: bool = False):
         self.spec, self.impl, self.B, self.device = spec, impl, batch, torch.device(device)
         self.net = build_net(impl, spec, batch, self.device, init, opt, precision)
@@ -96,8 +96,11 @@ class Replica:
         self.train_ds = DeviceDataset(train_images, train_labels, self.device, hw=784, channels=src_channels)
         self.eval_ds = (DeviceDataset(eval_images, eval_labels, self.device, hw=784, channels=src_channels)
                         if eval_images is not None else None)
-        # --fused_input (HIP): the first fused conv reads the uint8 training set through the batch index
-        fused_in = fused_input and impl == "hip" and self.net.bind_u8_input(self.train_ds.images)
+        # --input_mode u8 / bf16 (HIP; --fused_input = u8): the first fused conv gathers the
+        # resident training set (uint8, or normalised once to bf16) through the batch index
+        mode = "u8" if fused_input is True else (fused_input or "prep")
+        fused_in = impl == "hip" and mode != "prep" and self.net.bind_u8_input(
+            self.train_ds.images if mode == "u8" else self.train_ds.bf16_images())
         self.loader = DeviceLoader(self.train_ds, self.net.x0, self.net.labels, rank=self.rank, world=self.world,
                                    seed=seed, shard=shard, idx_out=self.net.idx_buf if fused_in else None)
         # hipGraph: single replica, or (dp_graph) the DP step with its RCCL all-reduces captured

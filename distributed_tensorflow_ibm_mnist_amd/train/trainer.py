@@ -122,7 +122,7 @@ def _train(FLAGS, cl: Cluster, max_steps, test_interval, batch_size, impl, log) 
     base = Replica(spec, impl, batch_size, cl.device, init, opt, x_tr, y_tr, c_tr, x_ev, y_ev,
                    seed=FLAGS.seed, shard=not FLAGS.no_shard, use_graph=FLAGS.hip_graph,
                    bucket_mb=FLAGS.bucket_mb, group=dp_group if cl.mode == "dp" else None,
-                   fused_input=FLAGS.fused_input, precision=getattr(FLAGS, "precision", "bf16"),
+                   fused_input=True if FLAGS.fused_input else getattr(FLAGS, "input_mode", "prep"), precision=getattr(FLAGS, "precision", "bf16"),
                    dp_graph=getattr(FLAGS, "hip_graph_dp", False)) \
         if cl.mode != "ps" else _ps_base(spec, impl, batch_size, cl, init, opt, x_tr, y_tr, c_tr, x_ev, y_ev, FLAGS)
     replica = base

@@ -59,6 +59,9 @@ flags.DEFINE_boolean("hip_graph", True, "capture the training step in a hipGraph
 flags.DEFINE_boolean("hip_graph_dp", False, "data parallel: also capture the step with its RCCL all-reduces")
 flags.DEFINE_float("bucket_mb", 0.125, "gradient all-reduce bucket cap (MB); every bucket but the last overlaps backward")
 flags.DEFINE_boolean("fused_input", False, "HIP: first fused conv reads the uint8 dataset through the batch index")
+flags.DEFINE_string("input_mode", "bf16", "HIP input path: bf16 | u8 (the first fused conv gathers the resident "
+                    "training set, normalised once to bf16 / in the kernels from uint8) | prep (a per-step "
+                    "gather+normalise kernel); models whose first layer cannot gather fall back to prep")
 flags.DEFINE_float("save_checkpoint_secs", 600, "checkpoint every N seconds (TF default 600)")
 flags.DEFINE_integer("save_checkpoint_steps", 0, "checkpoint every N steps (0: off)")
 flags.DEFINE_integer("save_summaries_steps", 100, "loss/accuracy scalars every N steps")

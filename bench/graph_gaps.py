@@ -5,7 +5,7 @@ import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 # steps start at the input-gather kernel
-starts = [i for i, r in enumerate(rows) if "prep_images" in r["Kernel_Name"]]
+starts = [i for i, r in enumerate(rows) if "prep_images" in r["Kernel_Name"] or "perm_positions" in r["Kernel_Name"]]
 steps = [(a, b) for a, b in zip(starts, starts[1:])][-10:]
 tot_busy = tot_wall = 0
 for a, b in steps:

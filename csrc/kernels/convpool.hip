@@ -349,6 +349,33 @@ struct XStage {
     const int hh = rem / G::ROWV, vv = rem - hh * G::ROWV;
     return im * G::IMG_LDS + ((hh + G::PAD) * G::WS + G::X0) * G::CIN + 4 * vv;
   }
+  // MODE 0 pair layouts (window-left pixels) read only the shifted copies 0 and 2 (the
+  // window's column offset is even): each staged vector goes to copy 0 as one 8-byte
+  // store and to copy 2 (copy2[j] = copy0[j + 2]) as two dword stores, so no
+  // make_shifted pass -- its 2 reads + 3 writes per vector and one barrier per group.
+  DEV void store_c02(bf16_t* tile, int tid) const {
+    static_assert(G::MODE == 0 && G::X0 >= 2, "copy-2 writes start 2 elements before the interior");
+    auto put = [&](int e, u32x2 val) {
+      const int o = tile_off(e);
+      *(u32x2*)(tile + o) = val;
+      uint32_t* c2 = (uint32_t*)(tile + 2 * G::TSTR + o - 2);
+      c2[0] = val[0];
+      c2[1] = val[1];
+    };
+    if (U8 && u8mode) {
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int e = vec(u, tid);
+        if (e < NV) put(e, value(u));
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int e = vec(u, tid);
+        if (e < NV) put(e, v[u]);
+      }
+    }
+  }
   // the uint8 conversion sits behind a uniform branch (a select made every bf16 staging
   // pay for it: ~10 VALU per vector)
   DEV void store(bf16_t* tile, int tid) const {
@@ -1179,7 +1206,7 @@ __global__ __launch_bounds__(NTH, 6) void convpool_wgrad_pair_k(const XSrc x,
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
     xs.drain();
     __syncthreads();
-    xs.store(tile, tid);
+    xs.store_c02(tile, tid);   // copies 0 and 2 only: this layout reads no others
     // max-unpool into U: U[sx*8+c][w] = (dy0: arg==sx ? dP : 0, dy1: arg==2+sx ? dP : 0)
 #pragma unroll
     for (int u = 0; u < DYStage<G, IMGS>::PER; ++u) {
@@ -1206,8 +1233,6 @@ __global__ __launch_bounds__(NTH, 6) void convpool_wgrad_pair_k(const XSrc x,
         }
       }
     }
-    __syncthreads();
-    make_shifted<G, IMGS>(tile, tid);
     __syncthreads();
     if (img0 + stride < B) {
       xs.load(x, img0 + stride, B, tid);

@@ -353,12 +353,13 @@ struct XStage {
   // window's column offset is even): each staged vector goes to copy 0 as one 8-byte
   // store and to copy 2 (copy2[j] = copy0[j + 2]) as two dword stores, so no
   // make_shifted pass -- its 2 reads + 3 writes per vector and one barrier per group.
-  DEV void store_c02(bf16_t* tile, int tid) const {
+  // c2off: LDS offset of copy 2 (2 * TSTR in the 4-copy layout).
+  DEV void store_c02(bf16_t* tile, int tid, int c2off = 2 * G::TSTR) const {
     static_assert(G::MODE == 0 && G::X0 >= 2, "copy-2 writes start 2 elements before the interior");
     auto put = [&](int e, u32x2 val) {
       const int o = tile_off(e);
       *(u32x2*)(tile + o) = val;
-      uint32_t* c2 = (uint32_t*)(tile + 2 * G::TSTR + o - 2);
+      uint32_t* c2 = (uint32_t*)(tile + c2off + o - 2);
       c2[0] = val[0];
       c2[1] = val[1];
     };
@@ -1155,7 +1156,7 @@ __global__ __launch_bounds__(NTH, wgrad_minw<G>()) void convpool_wgrad_k(const X
 // lanes supplying im2col^T rows KE..KE+3 read a constant [1,0,0,0] cell, so row KE
 // accumulates sum(dY) per column (deterministic MFMA order, no staging VALU).
 template <class G, int IMGS>
-__global__ __launch_bounds__(NTH, 6) void convpool_wgrad_pair_k(const XSrc x,
+__global__ __launch_bounds__(NTH, 7) void convpool_wgrad_pair_k(const XSrc x,
                                                              const bf16_t* __restrict__ dP,
                                                              const uint8_t* __restrict__ arg, int B,
                                                              float* __restrict__ slab) {
@@ -1166,7 +1167,14 @@ __global__ __launch_bounds__(NTH, 6) void convpool_wgrad_pair_k(const XSrc x,
   static_assert(URS >= NWP && URS % 8 == 4, "U row stride");
   constexpr int UIMG = 16 * URS;                      // dwords per image
   constexpr int NWC = G::NWIN * 8;
-  constexpr int TILE_E = (IMGS * G::IMG_LDS + 7) / 8 * 8;
+  // Only copies 0 and 2 are read (window-left columns are even: XOFF even, WS % 4 == 0).
+  // One image per group: the tile holds just those two, copy 2 right after copy 0
+  // (LDS 24.0 -> 19.5 KB per workgroup: 7 instead of 6 per CU); more images keep the
+  // 4-copy stride.
+  static_assert(G::XOFF % 2 == 0 && G::WS % 4 == 0, "window-left offsets are even");
+  constexpr bool CMP = IMGS == 1;
+  constexpr int C2OFF = CMP ? G::TSTR : 2 * G::TSTR;
+  constexpr int TILE_E = CMP ? (2 * G::TSTR + 7) / 8 * 8 : (IMGS * G::IMG_LDS + 7) / 8 * 8;
   __shared__ __attribute__((aligned(16))) bf16_t tile[TILE_E];
   __shared__ __attribute__((aligned(16))) uint32_t U[IMGS * UIMG];   // also the bias combine at the end
   __shared__ int wtab[G::NWIN];            // window -> aligned LDS offset of its top-left pixel
@@ -1180,7 +1188,10 @@ __global__ __launch_bounds__(NTH, 6) void convpool_wgrad_pair_k(const XSrc x,
   const int g = lane >> 4, li = lane & 15;
   lds_zero<TILE_E>(tile, tid);
   lds_zero<IMGS * UIMG * 2>((bf16_t*)U, tid);          // windows >= NWIN stay zero
-  for (int w = tid; w < G::NWIN; w += NTH) wtab[w] = G::aligned_off(G::wbase(w));
+  for (int w = tid; w < G::NWIN; w += NTH) {
+    const int a = G::wbase(w);                 // a & 3 is 0 or 2: copy 0, or copy 2 at C2OFF
+    wtab[w] = (a & 3) ? a - 2 + C2OFF : a;
+  }
   if (tid < 4) one_cell[tid] = tid == 0 ? (bf16_t)0x3f80 : (bf16_t)0;
 
   const int q = (lane >> 2) & 3, p = lane & 3;
@@ -1206,7 +1217,7 @@ __global__ __launch_bounds__(NTH, 6) void convpool_wgrad_pair_k(const XSrc x,
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
     xs.drain();
     __syncthreads();
-    xs.store_c02(tile, tid);   // copies 0 and 2 only: this layout reads no others
+    xs.store_c02(tile, tid, C2OFF);   // copies 0 and 2 only: this layout reads no others
     // max-unpool into U: U[sx*8+c][w] = (dy0: arg==sx ? dP : 0, dy1: arg==2+sx ? dP : 0)
 #pragma unroll
     for (int u = 0; u < DYStage<G, IMGS>::PER; ++u) {

@@ -340,8 +340,14 @@ struct XStage {
   // vmcnt(0) at this dominating point.  Without it the waitcnt pass, merging over the
   // per-lane staging branches, inserted full waits BEHIND the new gathered prefetch
   // loads (a whole memory latency per group in the gathered-input weight gradient).
+  // NST: vector-memory STORES a thread issues after the prefetch loads (the previous
+  // group's output copy-out): they may stay in flight (vmcnt counts loads and stores
+  // in issue order).  NST < 0: no explicit wait.
+  template <int NST = 0>
   static DEV void drain() {
-    if constexpr (U8) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt/lgkmcnt untouched
+    static_assert(NST < 64, "vmcnt is 6 bits");
+    if constexpr (U8 && NST >= 0)   // vmcnt(NST), expcnt / lgkmcnt untouched
+      __builtin_amdgcn_s_waitcnt((NST & 15) | ((NST >> 4) << 14) | 0x0F70);
   }
   // offset of vector e in the LDS tile
   static DEV int tile_off(int e) {
@@ -552,7 +558,7 @@ __global__ __launch_bounds__(NTH, fwd_minw<G>()) void convpool_fwd_k(const XSrc 
   xs.load(x, blockIdx.x * IMGS, B, tid);
   xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
-    xs.drain();
+    xs.template drain<-1>();
     __syncthreads();
     xs.store(tile, tid);
     __syncthreads();
@@ -683,7 +689,7 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_pair_k(const XSrc x, const b
   xs.load(x, blockIdx.x * IMGS, B, tid);
   xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
-    xs.drain();
+    xs.template drain<-1>();
     __syncthreads();
     xs.store(tile, tid);
     __syncthreads();
@@ -773,6 +779,8 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
   __shared__ __attribute__((aligned(16))) bf16_t pout[STAGE_OUT ? IMGS * OUTS : 8];
   __shared__ __attribute__((aligned(16))) uint8_t aout[STAGE_OUT ? IMGS * OUTS : 16];
   static_assert((OUTE * 2) % 16 == 0 && OUTE % 16 == 0 && STAGE_OUT, "");
+  // copy-out stores per thread per group (pooled 16-byte vectors + packed argmax vectors)
+  constexpr int QST = (IMGS * OUTE / 8 + NTH - 1) / NTH + (IMGS * Q::NWIN / 4 + NTH - 1) / NTH;
   // wave index in an SGPR: the fragment / image bookkeeping below runs on the scalar unit
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n = lane & 31, h = lane >> 5;
@@ -802,8 +810,12 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
   xs.fetch_rows(x, blockIdx.x * IMGS, B);
   xs.load(x, blockIdx.x * IMGS, B, tid);
   xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
+  // the first group's loads complete here, so the loop-top vmcnt(QST) is exact on both
+  // the entry and the back edge (a merge of the two made the waitcnt pass wait for the
+  // previous group's output stores inside the staging)
+  xs.template drain<0>();
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
-    xs.drain();
+    xs.template drain<QST>();
     __syncthreads();
     // interior rows at column X0 = 10 (4-byte aligned): two 4-byte stores per vector;
     // the uint8 conversion behind a uniform branch (not a per-vector select)

@@ -100,8 +100,16 @@ DEV s16x4 lds_tr4(const bf16_t* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4
 // (s_waitcnt vmcnt(0)), which serialises a software-prefetch of several loads into
 // one full memory latency each.
 constexpr uint32_t BUF_OOB = 0x80000000u;   // > any num_records used here (< 2 GB)
+// base and nbytes must be wave-uniform (every caller's are: a block's or a wave's image
+// group, a kernel argument).  readfirstlane makes that visible to the compiler, which
+// otherwise wraps each load whose descriptor it cannot prove uniform (e.g. one built
+// from a loop-carried group index) in a waterfall loop: 4 readfirstlane, 2 compares and
+// an exec-mask loop per load (the conv2 weight gradient had 9 of them).
 DEV __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t nbytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nbytes, 0x00020000);
+  const uint64_t b = (uint64_t)base;
+  const uint64_t ub = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                      (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)ub, (short)0, (int)__builtin_amdgcn_readfirstlane(nbytes), 0x00020000);
 }
 DEV uint32_t buf_b32(__amdgpu_buffer_rsrc_t r, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0); }
 DEV u32x2 buf_b64(__amdgpu_buffer_rsrc_t r, uint32_t off) {

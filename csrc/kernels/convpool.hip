@@ -557,16 +557,37 @@ __global__ __launch_bounds__(NTH, fwd_minw<G>()) void convpool_fwd_k(const XSrc 
   xs.fetch_rows(x, blockIdx.x * IMGS, B);
   xs.load(x, blockIdx.x * IMGS, B, tid);
   xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
+  // staged outputs leave in the NEXT group's staging phase, before its prefetch loads
+  // (see convpool_fwd_quad_k: stores pending behind a load make every wait vmcnt(0))
+  auto copy_out = [&](int g0) {
+    if constexpr (STAGE) {
+      const int nimg = min(IMGS, B - g0);
+      bf16_t* pg = pooled + (int64_t)g0 * OUTE;
+      uint8_t* ag = arg + (int64_t)g0 * OUTE;
+      constexpr int PV = IMGS * OUTE / 8, AV = IMGS * OUTE / 16;
+#pragma unroll
+      for (int u = 0; u < (PV + NTH - 1) / NTH; ++u) {
+        const int e = tid + u * NTH;
+        if (e < nimg * OUTE / 8) *(u32x4*)(pg + 8 * e) = *(const u32x4*)(pout + 8 * e);
+      }
+#pragma unroll
+      for (int u = 0; u < (AV + NTH - 1) / NTH; ++u) {
+        const int e = tid + u * NTH;
+        if (e < nimg * OUTE / 16) *(u32x4*)(ag + 16 * e) = *(const u32x4*)(aout + 16 * e);
+      }
+    }
+  };
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
-    xs.template drain<-1>();
     __syncthreads();
     xs.store(tile, tid);
+    if (img0 != (int)blockIdx.x * IMGS) copy_out(img0 - stride);   // the previous group's outputs
     __syncthreads();
     if constexpr (G::MODE == 0) {
       make_shifted<G, IMGS>(tile, tid);
       __syncthreads();
     }
-    if (img0 + stride < B) {
+    {   // unconditional prefetch (past the batch: buffer loads of nothing return 0), so
+        // every path issues the same loads and the waitcnt pass keeps its counts exact
       xs.load(x, img0 + stride, B, tid);
       xs.fetch_rows(x, img0 + 2 * stride, B);
     }
@@ -626,14 +647,10 @@ __global__ __launch_bounds__(NTH, fwd_minw<G>()) void convpool_fwd_k(const XSrc 
         }
       }
     }
-    if constexpr (STAGE) {
-      __syncthreads();
-      const int nimg = min(IMGS, B - img0);
-      bf16_t* pg = pooled + (int64_t)img0 * OUTE;
-      uint8_t* ag = arg + (int64_t)img0 * OUTE;
-      for (int e = tid; e < nimg * OUTE / 8; e += NTH) *(u32x4*)(pg + 8 * e) = *(const u32x4*)(pout + 8 * e);
-      for (int e = tid; e < nimg * OUTE / 16; e += NTH) *(u32x4*)(ag + 16 * e) = *(const u32x4*)(aout + 16 * e);
-    }
+  }
+  if constexpr (STAGE) {   // the last group's outputs
+    __syncthreads();
+    if ((int)blockIdx.x * IMGS < B) copy_out(blockIdx.x * IMGS + (B - 1 - (int)blockIdx.x * IMGS) / stride * stride);
   }
 }
 
@@ -695,7 +712,8 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_pair_k(const XSrc x, const b
     __syncthreads();
     make_shifted<G, IMGS>(tile, tid);
     __syncthreads();
-    if (img0 + stride < B) {
+    {   // unconditional prefetch (past the batch: buffer loads of nothing return 0), so
+        // every path issues the same loads and the waitcnt pass keeps its counts exact
       xs.load(x, img0 + stride, B, tid);
       xs.fetch_rows(x, img0 + 2 * stride, B);
     }
@@ -779,8 +797,6 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
   __shared__ __attribute__((aligned(16))) bf16_t pout[STAGE_OUT ? IMGS * OUTS : 8];
   __shared__ __attribute__((aligned(16))) uint8_t aout[STAGE_OUT ? IMGS * OUTS : 16];
   static_assert((OUTE * 2) % 16 == 0 && OUTE % 16 == 0 && STAGE_OUT, "");
-  // copy-out stores per thread per group (pooled 16-byte vectors + packed argmax vectors)
-  constexpr int QST = (IMGS * OUTE / 8 + NTH - 1) / NTH + (IMGS * Q::NWIN / 4 + NTH - 1) / NTH;
   // wave index in an SGPR: the fragment / image bookkeeping below runs on the scalar unit
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n = lane & 31, h = lane >> 5;
@@ -810,12 +826,38 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
   xs.fetch_rows(x, blockIdx.x * IMGS, B);
   xs.load(x, blockIdx.x * IMGS, B, tid);
   xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
-  // the first group's loads complete here, so the loop-top vmcnt(QST) is exact on both
-  // the entry and the back edge (a merge of the two made the waitcnt pass wait for the
-  // previous group's output stores inside the staging)
-  xs.template drain<0>();
+  // Copy-out of a group's staged outputs (pout / aout): 16-byte stores, the group's
+  // outputs being contiguous in HBM.  It runs in the NEXT group's staging phase, before
+  // that group's prefetch loads are issued: the waitcnt pass treats vmcnt as out of
+  // order once loads and stores are both pending and waits vmcnt(0) for any load, so
+  // stores issued after the prefetch (at the end of the group) were waited for at the
+  // next loop top; issued before it, they drain during the compute phase.
+  auto copy_out = [&](int g0) {
+    const int nimg = min(IMGS, B - g0);
+    bf16_t* pg = pooled + (int64_t)g0 * OUTE;
+    uint8_t* ag = arg + (int64_t)g0 * (Q::NWIN * 4);
+    constexpr int PV = IMGS * OUTE / 8;
+#pragma unroll
+    for (int u = 0; u < (PV + NTH - 1) / NTH; ++u) {
+      const int e = tid + u * NTH, im = e / (OUTE / 8);
+      if (e < nimg * (OUTE / 8))
+        *(u32x4*)(pg + 8 * e) = *(const u32x4*)(pout + im * OUTS + 8 * (e - im * (OUTE / 8)));
+    }
+    // argmax codes packed 4 bits each (arg_packed<LeNetC1>): 16 output bytes = 4
+    // windows (32 LDS bytes)
+    constexpr int AV4 = IMGS * Q::NWIN / 4;
+    static_assert(Q::NWIN % 4 == 0, "");
+#pragma unroll
+    for (int u = 0; u < (AV4 + NTH - 1) / NTH; ++u) {
+      const int e = tid + u * NTH, im = e / (Q::NWIN / 4);
+      if (e < nimg * (Q::NWIN / 4)) {
+        const uint8_t* src = aout + im * OUTS + 32 * (e - im * (Q::NWIN / 4));
+        const u32x4 lo = *(const u32x4*)src, hi = *(const u32x4*)(src + 16);
+        *(u32x4*)(ag + 16 * e) = u32x4{lo[0] | lo[1] << 4, lo[2] | lo[3] << 4, hi[0] | hi[1] << 4, hi[2] | hi[3] << 4};
+      }
+    }
+  };
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
-    xs.template drain<QST>();
     __syncthreads();
     // interior rows at column X0 = 10 (4-byte aligned): two 4-byte stores per vector;
     // the uint8 conversion behind a uniform branch (not a per-vector select)
@@ -835,8 +877,10 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
     };
     if (xs.u8mode) stage([&](int u) { return xs.value(u); });
     else stage([&](int u) { return xs.v[u]; });
+    if (img0 != (int)blockIdx.x * IMGS) copy_out(img0 - stride);   // the previous group's outputs
     __syncthreads();
-    if (img0 + stride < B) {
+    {   // unconditional prefetch (past the batch: buffer loads of nothing return 0), so
+        // every path issues the same loads and the waitcnt pass keeps its counts exact
       xs.load(x, img0 + stride, B, tid);
       xs.fetch_rows(x, img0 + 2 * stride, B);
     }
@@ -889,37 +933,10 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
       for (int q = 0; q < 3; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afrag(tb, q), bfr[q], acc, 0, 0, 0);
       epilogue(f, acc);
     }
-    if constexpr (STAGE_OUT) {
-      __syncthreads();
-      // the group's outputs are contiguous in HBM: full 16-byte stores
-      const int nimg = min(IMGS, B - img0);
-      bf16_t* pg = pooled + (int64_t)img0 * OUTE;
-      uint8_t* ag = arg + (int64_t)img0 * (Q::NWIN * 4);
-      // compile-time store counts (unrolled, exec-masked tails): the loop-top wait for the
-      // prefetched loads is then vmcnt(#stores) -- a runtime-trip-count store loop made it
-      // wait for these stores to complete as well (loads and stores share vmcnt, in order)
-      constexpr int PV = IMGS * OUTE / 8;
-#pragma unroll
-      for (int u = 0; u < (PV + NTH - 1) / NTH; ++u) {
-        const int e = tid + u * NTH, im = e / (OUTE / 8);
-        if (e < nimg * (OUTE / 8))
-          *(u32x4*)(pg + 8 * e) = *(const u32x4*)(pout + im * OUTS + 8 * (e - im * (OUTE / 8)));
-      }
-      // argmax codes packed 4 bits each (arg_packed<LeNetC1>): 16 output bytes = 4
-      // windows (32 LDS bytes)
-      constexpr int AV4 = IMGS * Q::NWIN / 4;
-      static_assert(Q::NWIN % 4 == 0, "");
-#pragma unroll
-      for (int u = 0; u < (AV4 + NTH - 1) / NTH; ++u) {
-        const int e = tid + u * NTH, im = e / (Q::NWIN / 4);
-        if (e < nimg * (Q::NWIN / 4)) {
-          const uint8_t* src = aout + im * OUTS + 32 * (e - im * (Q::NWIN / 4));
-          const u32x4 lo = *(const u32x4*)src, hi = *(const u32x4*)(src + 16);
-          *(u32x4*)(ag + 16 * e) = u32x4{lo[0] | lo[1] << 4, lo[2] | lo[3] << 4, hi[0] | hi[1] << 4, hi[2] | hi[3] << 4};
-        }
-      }
-    }
   }
+  // the last group's outputs
+  __syncthreads();
+  if ((int)blockIdx.x * IMGS < B) copy_out(blockIdx.x * IMGS + (B - 1 - (int)blockIdx.x * IMGS) / stride * stride);
 }
 
 // ------------------------------------------------------------------ weight gradient
@@ -1026,7 +1043,8 @@ __global__ __launch_bounds__(NTH, wgrad_minw<G>()) void convpool_wgrad_k(const X
       make_shifted<G, IMGS>(tile, tid);
       __syncthreads();
     }
-    if (img0 + stride < B) {
+    {   // unconditional prefetch (past the batch: buffer loads of nothing return 0), so
+        // every path issues the same loads and the waitcnt pass keeps its counts exact
       xs.load(x, img0 + stride, B, tid);
       xs.fetch_rows(x, img0 + 2 * stride, B);
       ys.load(dP, arg, img0 + stride, B, tid);
@@ -1257,7 +1275,8 @@ __global__ __launch_bounds__(NTH, 7) void convpool_wgrad_pair_k(const XSrc x,
       }
     }
     __syncthreads();
-    if (img0 + stride < B) {
+    {   // unconditional prefetch (past the batch: buffer loads of nothing return 0), so
+        // every path issues the same loads and the waitcnt pass keeps its counts exact
       xs.load(x, img0 + stride, B, tid);
       xs.fetch_rows(x, img0 + 2 * stride, B);
       ys.load(dP, arg, img0 + stride, B, tid);
@@ -1377,6 +1396,18 @@ __global__ __launch_bounds__(NTH, MINW) void convpool_dgrad_pair_k(const bf16_t*
   const int stride = gridDim.x * IMGS;
   DYStage<G, IMGS> ys;
   ys.load(dP, arg, blockIdx.x * IMGS, B, tid);
+  // dx of a group leaves in the NEXT group's staging phase, before its prefetch loads
+  // (see convpool_fwd_quad_k: stores pending behind a load make every wait vmcnt(0))
+  auto copy_out = [&](int g0) {
+    const int nimg = min(IMGS, B - g0);
+    bf16_t* dg = dx + (int64_t)g0 * OUTE;
+    constexpr int PV = IMGS * OUTE / 8;   // compile-time store count
+#pragma unroll
+    for (int u = 0; u < (PV + NTH - 1) / NTH; ++u) {
+      const int e = tid + u * NTH;
+      if (e < nimg * OUTE / 8) *(u32x4*)(dg + 8 * e) = *(const u32x4*)(outs + 8 * e);
+    }
+  };
   for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
     __syncthreads();
     // max-unpool: position d of a window receives dP where arg == d (arg 4: ReLU off)
@@ -1405,8 +1436,11 @@ __global__ __launch_bounds__(NTH, MINW) void convpool_dgrad_pair_k(const bf16_t*
         }
       }
     }
+    // the previous group's dx: after the staging consumed the prefetched loads (a wait
+    // for them behind pending stores would be vmcnt(0)), before the next prefetch
+    if (img0 != (int)blockIdx.x * IMGS) copy_out(img0 - stride);
     __syncthreads();
-    if (img0 + stride < B) ys.load(dP, arg, img0 + stride, B, tid);
+    ys.load(dP, arg, img0 + stride, B, tid);   // unconditional: past the batch loads return 0
     if constexpr (LA > 0) {
       static_assert(KWQ == 6 && KSD == 15 && (NTH / 64) % IMGS == 0, "row reuse: 5 tap rows x 3 tap pairs");
       constexpr int WPI = (NTH / 64) / IMGS;          // waves per image
@@ -1484,12 +1518,9 @@ __global__ __launch_bounds__(NTH, MINW) void convpool_dgrad_pair_k(const bf16_t*
         if (2 * jr < G::W) oimg[(ih * G::W + 2 * jr + sx) * 8 + ci] = f2bf(acc[r]);
       }
     }
-    __syncthreads();
-    // the group's dx images are contiguous in HBM: 16-byte stores
-    const int nimg = min(IMGS, B - img0);
-    bf16_t* dg = dx + (int64_t)img0 * OUTE;
-    for (int e = tid; e < nimg * OUTE / 8; e += NTH) *(u32x4*)(dg + 8 * e) = *(const u32x4*)(outs + 8 * e);
   }
+  __syncthreads();   // the last group's dx
+  if ((int)blockIdx.x * IMGS < B) copy_out(blockIdx.x * IMGS + (B - 1 - (int)blockIdx.x * IMGS) / stride * stride);
 }
 
 int grid_for(int B, int imgs, int cap) {
@@ -1746,7 +1777,8 @@ __global__ __launch_bounds__(NTH, 3) void lenet_c2dgrad_c1wgrad_k(const XSrc x, 
       }
     }
     __syncthreads();
-    if (img0 + stride < B) {
+    {   // unconditional prefetch (past the batch: buffer loads of nothing return 0), so
+        // every path issues the same loads and the waitcnt pass keeps its counts exact
       xs.load(x, img0 + stride, B, tid);
       xs.fetch_rows(x, img0 + 2 * stride, B);
       ys.load(dP2, arg2, img0 + stride, B, tid);

@@ -25,8 +25,8 @@ def main():
     cols = ["SQ_INSTS_MFMA", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_SALU",
             "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES", "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE",
             "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE"]
-    lines = ["| kernel | MFMA | VALU | LDS | VMEM rd | VALU/MFMA | wait_inst% | wait_any% | MFMA busy% | LDS bank-confl% |",
-             "|---|---|---|---|---|---|---|---|---|---|"]
+    lines = ["| kernel | MFMA | VALU | LDS | VMEM rd | VALU/MFMA | wait_inst% | wait_any% | MFMA busy% | LDS bank-confl% | LDS active / GUI cycle |",
+             "|---|---|---|---|---|---|---|---|---|---|---|"]
     rows = []
     for k, c in per.items():
         if c.get("SQ_INSTS_MFMA", 0) + c.get("SQ_INSTS_VALU", 0) < 1e5:
@@ -38,7 +38,8 @@ def main():
                      f"{c.get('SQ_INSTS_LDS',0):.3g} | {c.get('SQ_INSTS_VMEM_RD',0):.3g} | "
                      f"{c.get('SQ_INSTS_VALU',0)/max(mf,1):.1f} | {100*c.get('SQ_WAIT_INST_ANY',0)/wc:.0f} | "
                      f"{100*c.get('SQ_WAIT_ANY',0)/wc:.0f} | {100*busy:.1f} | "
-                     f"{100*c.get('SQ_LDS_BANK_CONFLICT',0)/max(c.get('SQ_LDS_IDX_ACTIVE',1),1):.1f} |"))
+                     f"{100*c.get('SQ_LDS_BANK_CONFLICT',0)/max(c.get('SQ_LDS_IDX_ACTIVE',1),1):.1f} | "
+                     f"{c.get('SQ_LDS_IDX_ACTIVE',0)/max(c.get('GRBM_GUI_ACTIVE',1),1):.1f} |"))
     rows.sort(key=lambda r: -r[0])
     out = "\n".join(lines + [r[1] for r in rows])
     print(out)

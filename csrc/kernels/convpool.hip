@@ -179,9 +179,10 @@ struct LrnFold {
   float bias, alpha, beta;
 };
 // Minimum waves per SIMD the register allocator must leave room for (the
-// __launch_bounds__ second argument).  LeNet conv2 fwd fits 93 VGPRs (5 waves, was
-// 4 at 106) and its wgrad 167 (3 waves, was 2 at 172) without spills; the
-// reference conv1 variants spill under a bound, so they keep the default.
+// __launch_bounds__ second argument).  LeNet conv2 fwd: 104 VGPRs, 4 waves (a bound
+// of 5 forces 96 with a spill and measured slower); its wgrad: 122 VGPRs, 4 waves,
+// matching its 39 KB of LDS.  The reference conv1 variants spill under a bound, so
+// they keep the default.
 template <class G> constexpr int fwd_minw() { return (G::CIN == 8 && G::COUT == 16) ? 4 : 1; }
 template <class G> constexpr int wgrad_minw() { return (G::CIN == 8 && G::COUT == 16) ? 4 : 1; }
 // Argmax byte of a pool window whose ReLU output is 0: matches no position, so

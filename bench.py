@@ -151,6 +151,9 @@ def run_ps(args) -> int:
                        "parallelism": f"ps1+w{nw}", "ps_transport": args.ps_transport,
                        "gpus_visible": torch.cuda.device_count(), "optimizer": args.optimizer},
             "applied_per_worker": res["per_worker"], "global_step": res["global_step"],
+            # PS host time per served message, by phase (whole run incl. warmup): idle = waiting
+            # for a worker, apply = optimizer launch, reply = stage + sync + control answer
+            "ps_us_per_msg": {k: round(v / max(1, res["applied"]) * 1e6, 1) for k, v in res["phase_s"].items()},
             "param_checksum": float(ps.fp.params.double().sum().item()),
         }
         print(json.dumps(out), flush=True)

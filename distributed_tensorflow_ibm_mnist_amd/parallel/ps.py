@@ -292,9 +292,16 @@ class ParameterServer:
         self.log(f"[ps {self.j}] serving {len(self.names)} tensor(s), {self.end - self.start} params, "
                  f"{self.W} worker(s), transport {self.tx.name}")
         t0 = time.perf_counter()
+        # host seconds per phase of the serve loop (bench.py --mode ps reports them):
+        # idle = blocked waiting for the next worker's control word
+        ph = self.phase_s = {"idle": 0.0, "apply": 0.0, "reply": 0.0}
+        clk = time.perf_counter
+        c = torch.zeros(CTRL, dtype=torch.int64)
         while len(done) < self.W:
-            c = torch.zeros(CTRL, dtype=torch.int64)
+            ta = clk()
             r = dist.recv(c, group=self.group, tag=TAG_CTRL)     # any source: the next worker to arrive
+            tb = clk()
+            ph["idle"] += tb - ta
             kind, want_state = int(c[0]), bool(c[1])
             if kind == DONE:
                 done.add(r)
@@ -314,7 +321,10 @@ class ParameterServer:
                     self.log(f"[ps {self.j}] fault injection: SIGKILL at global step {self.global_step}")
                     sys.stdout.flush()
                     os.kill(os.getpid(), signal.SIGKILL)
+            tc = clk()
+            ph["apply"] += tc - tb
             self._reply(r, want_state)
+            ph["reply"] += clk() - tc
             if self.global_step in self.marks and not self.marks[self.global_step]:
                 if self.device.type == "cuda":
                     torch.cuda.synchronize(self.device)
@@ -324,7 +334,7 @@ class ParameterServer:
                  f"rejected {self.rejected}, global_step {self.global_step}, {self.applied / max(dt, 1e-9):.1f} "
                  f"updates/s")
         return {"applied": self.applied, "global_step": self.global_step, "per_worker": list(self.per_worker),
-                "seconds": dt}
+                "seconds": dt, "phase_s": dict(ph)}
 
 
 # ---------------------------------------------------------------------------- worker

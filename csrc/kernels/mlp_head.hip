@@ -35,6 +35,8 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <cstdlib>
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace mnistx {
@@ -71,25 +73,25 @@ DEV uint32_t half16(const u32x4& v, int f) { return (f & 1) ? (v[f >> 1] >> 16) 
 // W^T [R][C] (zero-padded; FlatParams.enable_transposed): straight 16-byte chunk
 // copies, chunk k of row n to its swizzled (and, for PERM images, bit-2/3-permuted)
 // place.  load_img issues the global loads, store_img writes them.
-template <int R, int C>
+template <int R, int C, int NT>
 struct ImgChunks {
-  static constexpr int N = R * C / 8, PER = (N + NTH - 1) / NTH;
+  static constexpr int N = R * C / 8, PER = (N + NT - 1) / NT;
   u32x4 v[PER];
 };
-template <int R, int C>
-DEV void load_img(ImgChunks<R, C>& ch, const bf16_t* __restrict__ WT, int tid) {
+template <int R, int C, int NT>
+DEV void load_img(ImgChunks<R, C, NT>& ch, const bf16_t* __restrict__ WT, int tid) {
 #pragma unroll
-  for (int i = 0; i < ImgChunks<R, C>::PER; ++i) {
-    const int b = tid + i * NTH;
-    if (b < ImgChunks<R, C>::N) ch.v[i] = *(const u32x4*)(WT + (int64_t)b * 8);
+  for (int i = 0; i < ImgChunks<R, C, NT>::PER; ++i) {
+    const int b = tid + i * NT;
+    if (b < ImgChunks<R, C, NT>::N) ch.v[i] = *(const u32x4*)(WT + (int64_t)b * 8);
   }
 }
-template <int IMG, bool PERM, int R, int C>
-DEV void store_img(bf16_t* img, const ImgChunks<R, C>& ch, int tid) {
+template <int IMG, bool PERM, int R, int C, int NT>
+DEV void store_img(bf16_t* img, const ImgChunks<R, C, NT>& ch, int tid) {
 #pragma unroll
-  for (int i = 0; i < ImgChunks<R, C>::PER; ++i) {
-    const int b = tid + i * NTH;
-    if (b >= ImgChunks<R, C>::N) break;
+  for (int i = 0; i < ImgChunks<R, C, NT>::PER; ++i) {
+    const int b = tid + i * NT;
+    if (b >= ImgChunks<R, C, NT>::N) break;
     const int r = b / (C / 8), c = (b % (C / 8)) * 8;
     const u32x4 o = ch.v[i];
     if constexpr (!PERM) {
@@ -162,8 +164,12 @@ DEV void dx_tiles(int v0, const bf16_t* i3, const uint32_t (&d3p)[T1][8], bf16_t
   }
 }
 
-template <bool GRADS>
-__global__ __launch_bounds__(NTH) void mlp_head_k(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W3t,
+// NW waves per block, TPW 32-row tiles per wave.  TPW = 2 (NW = 4: same 256 rows and
+// LDS images per block, one wave per SIMD) issues the next tile's X loads right after
+// the current tile's fc3, so they and the current tile's stores overlap its backward
+// chain; TPW = 1 runs every wave's load / compute / store phases in lockstep.
+template <bool GRADS, int NW = NWAVE, int TPW = 1>
+__global__ __launch_bounds__(64 * NW) void mlp_head_k(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W3t,
                                                   const float* __restrict__ b3, int n1, const bf16_t* __restrict__ W4t,
                                                   const float* __restrict__ b4, int n2, const bf16_t* __restrict__ W5t,
                                                   const float* __restrict__ b5, int nc,
@@ -177,46 +183,48 @@ __global__ __launch_bounds__(NTH) void mlp_head_k(const bf16_t* __restrict__ X, 
   __shared__ __attribute__((aligned(16))) bf16_t i4[R4 * S4];
   __shared__ __attribute__((aligned(16))) bf16_t i5[R5 * S5];
   __shared__ __attribute__((aligned(16))) float bias[32 * T1 + 32 * T2 + LD3];
-  __shared__ __attribute__((aligned(16))) bf16_t stage[NWAVE * STG];
+  constexpr int NT = 64 * NW;
+  __shared__ __attribute__((aligned(16))) bf16_t stage[NW * STG];
   float* bias3 = bias;
   float* bias4 = bias + 32 * T1;
   float* bias5 = bias4 + 32 * T2;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int m0 = (blockIdx.x * NWAVE + wave) * 32;
-  const int m = m0 + r;
-  const bool valid = m < nb;
-  const bool active = m0 < nb;  // wave-uniform
+  auto tile_m0 = [&](int t) { return ((int)(blockIdx.x * TPW + t) * NW + wave) * 32; };
   bf16_t* stg = stage + wave * STG;
 
   // 1. weight chunks, then the wave's whole 32 x 400 input tile and its labels, are
   // requested up front: the weight loads are older in the in-order vmcnt queue, so the
   // LDS staging below waits only for them while X is still in flight.
-  ImgChunks<R3, S3> c3;
-  ImgChunks<R4, 32 * T1> c4;
-  ImgChunks<R5, S5> c5;
+  ImgChunks<R3, S3, NT> c3;
+  ImgChunks<R4, 32 * T1, NT> c4;
+  ImgChunks<R5, S5, NT> c5;
   load_img(c3, W3t, tid);
   load_img(c4, W4t, tid);
   load_img(c5, W5t, tid);
   // (rows past nb load row nb-1: MFMA columns are independent and invalid ones are never stored)
   u32x4 xr[K1];
-  int lab = -1;
-  if (active) {
-    const int mc = valid ? m : nb - 1;
-    const bf16_t* xrow = X + (int64_t)mc * D0 + 8 * h;
+  auto load_x = [&](int mt) {       // the wave's 32 x 400 tile at row mt; returns the label
+    int lb = -1;
+    if (mt < nb) {
+      const int mc = min(mt + r, nb - 1);
+      const bf16_t* xrow = X + (int64_t)mc * D0 + 8 * h;
 #pragma unroll
-    for (int c = 0; c < K1; ++c) xr[c] = *(const u32x4*)(xrow + 16 * c);
-    lab = labels[mc];
-  } else {
+      for (int c = 0; c < K1; ++c) xr[c] = *(const u32x4*)(xrow + 16 * c);
+      lb = labels[mc];
+    } else {
 #pragma unroll
-    for (int c = 0; c < K1; ++c) xr[c] = u32x4{0u, 0u, 0u, 0u};
-  }
+      for (int c = 0; c < K1; ++c) xr[c] = u32x4{0u, 0u, 0u, 0u};
+    }
+    return lb;
+  };
+  int lab = load_x(tile_m0(0));
   // 2. weights -> LDS images, biases (zero beyond each layer's width)
   store_img<3, false>(i3, c3, tid);
   store_img<4, true>(i4, c4, tid);
   store_img<5, true>(i5, c5, tid);
-  for (int i = tid; i < 32 * T1 + 32 * T2 + LD3; i += NTH) {
+  for (int i = tid; i < 32 * T1 + 32 * T2 + LD3; i += NT) {
     float v = 0.f;
     if (i < 32 * T1) v = i < n1 ? b3[i] : 0.f;
     else if (i < 32 * (T1 + T2)) v = (i - 32 * T1) < n2 ? b4[i - 32 * T1] : 0.f;
@@ -226,6 +234,13 @@ __global__ __launch_bounds__(NTH) void mlp_head_k(const bf16_t* __restrict__ X, 
   __syncthreads();
 
   float loss = 0.f, corr = 0.f, bad = 0.f;
+#pragma unroll
+  for (int ti = 0; ti < TPW; ++ti) {
+  const int m0 = tile_m0(ti);
+  const int m = m0 + r;
+  const bool valid = m < nb;
+  const bool active = m0 < nb;  // wave-uniform
+  int lab_next = -1;
   if (active) {
     // ---------------- fc3: h3^T[128 x 32] = W3^T . X^T
     f32x16 a1[T1];
@@ -240,6 +255,8 @@ __global__ __launch_bounds__(NTH) void mlp_head_k(const bf16_t* __restrict__ X, 
         a1[t] = mfma32(wa, xb, a1[t]);
       }
     }
+    if constexpr (!GRADS)   // forward only: xr is consumed, the next tile's X streams in now
+      if (ti + 1 < TPW) lab_next = load_x(tile_m0(ti + 1));
     // bias + ReLU -> packed bf16 (register w of tile t = features 2w, 2w+1 of its slot list)
     uint32_t h3p[T1][8];
 #pragma unroll
@@ -320,9 +337,9 @@ __global__ __launch_bounds__(NTH) void mlp_head_k(const bf16_t* __restrict__ X, 
     ll += __shfl_xor(ll, 32, 64);
     if (valid && h == 0) {
       const float lo = -(ll - mx - __logf(se));
-      loss = lo;
-      corr = (ll >= mx) ? 1.f : 0.f;
-      bad = isfinite(lo) ? 0.f : 1.f;
+      loss += lo;
+      corr += (ll >= mx) ? 1.f : 0.f;
+      bad = isfinite(lo) ? bad : 1.f;
     }
     if constexpr (GRADS) {
       const float inv = 1.f / se;
@@ -393,16 +410,27 @@ __global__ __launch_bounds__(NTH) void mlp_head_k(const bf16_t* __restrict__ X, 
 
       // ---------------- fc3 dgrad: dX^T[416 x 32] = W3 . dh3^T (no mask: the conv block's
       // pooled output is post-ReLU and its backward applies the mask itself)
+      // the next tile's X streams in under this tile's fc3 data gradient (issued here, where
+      // the forward activations are dead: right after fc3 the 100 live VGPRs spilled)
+      if (ti + 1 < TPW) lab_next = load_x(tile_m0(ti + 1));
       dx_tiles<4>(0, i3, d3p, stg, dx, m0, nb, lane);
       dx_tiles<4>(4, i3, d3p, stg, dx, m0, nb, lane);
       dx_tiles<4>(8, i3, d3p, stg, dx, m0, nb, lane);
       dx_tiles<1>(12, i3, d3p, stg, dx, m0, nb, lane);
     }
   }
-  if (stats) ce_block_stats<NWAVE>(loss, corr, bad, stats, work);
+  lab = lab_next;
+  }
+  if (stats) ce_block_stats<NW>(loss, corr, bad, stats, work);
 }
 
 }  // namespace
+
+// MNISTX_HEAD_TPW=2: the 4-wave, two-tiles-per-wave layout (experiment knob)
+static int head_tpw() {
+  static const int v = [] { const char* e = getenv("MNISTX_HEAD_TPW"); return (e && e[0] == '2') ? 2 : 1; }();
+  return v;
+}
 
 bool mlp_head_supported(int d0, int ld1, int ld2, int ld3, int n1, int n2, int nc, int B) {
   return d0 == D0 && ld1 == LD1 && ld2 == LD2 && ld3 == LD3 && n1 <= LD1 && n2 <= LD2 && nc <= LD3 && nc > 0 &&
@@ -414,7 +442,16 @@ hipError_t mlp_head(const bf16_t* x, const bf16_t* w3t, const float* b3, int n1,
                     bf16_t* h3, bf16_t* h4, float* logits, bf16_t* dl, bf16_t* dh4, bf16_t* dh3, bf16_t* dx,
                     float* stats, float* work, hipStream_t st) {
   if (nb <= 0) return hipSuccess;
-  const dim3 grid((nb + ROWS - 1) / ROWS);
+  const dim3 grid((nb + ROWS - 1) / ROWS);   // ROWS rows per block in both layouts
+  if (head_tpw() == 2) {
+    if (dl)
+      hipLaunchKernelGGL((mlp_head_k<true, NWAVE / 2, 2>), grid, dim3(NTH / 2), 0, st, x, w3t, b3, n1, w4t, b4, n2,
+                         w5t, b5, nc, labels, nb, scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work);
+    else
+      hipLaunchKernelGGL((mlp_head_k<false, NWAVE / 2, 2>), grid, dim3(NTH / 2), 0, st, x, w3t, b3, n1, w4t, b4, n2,
+                         w5t, b5, nc, labels, nb, scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work);
+    return hipGetLastError();
+  }
   if (dl)
     hipLaunchKernelGGL(mlp_head_k<true>, grid, dim3(NTH), 0, st, x, w3t, b3, n1, w4t, b4, n2, w5t, b5, nc, labels, nb,
                        scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work);

@@ -71,3 +71,5 @@ def test_bench_graph_dp_rehearsal(dev):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["config"]["hip_graph"] is True and out["value"] > 0
+    # the driver contract: exactly --steps timed after --warmup (+ the untimed GEMM prewarm)
+    assert out["steps"] == 10 and out["warmup"] == 3 and out["prewarm_ms"] == 300.0

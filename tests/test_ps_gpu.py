@@ -126,3 +126,5 @@ def test_bench_ps_mode_json(dev):
     d = json.loads(line[0])
     assert d["config"]["parallelism"] == "ps1+w2" and d["global_step"] == 24
     assert d["value"] > 0 and sum(d["applied_per_worker"]) == 24
+    # serve-loop phase split (host us per applied update)
+    assert set(d["ps_us_per_msg"]) == {"idle", "apply", "reply"} and d["ps_us_per_msg"]["apply"] > 0

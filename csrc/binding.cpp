@@ -385,7 +385,7 @@ bool mlp_head_supported(int64_t d0, int64_t ld1, int64_t ld2, int64_t ld3, int64
 void mlp_head(Tensor x, Tensor w3t, Tensor b3, int64_t n1, Tensor w4t, Tensor b4, int64_t n2, Tensor w5t, Tensor b5,
               int64_t nc, Tensor labels, int64_t nb, double scale, Tensor h3, Tensor h4, Tensor logits,
               optional<Tensor> dl, optional<Tensor> dh4, optional<Tensor> dh3, optional<Tensor> dx, Tensor stats,
-              Tensor work) {
+              optional<Tensor> work, bool defer_stats) {
   TORCH_CHECK(mnistx::mlp_head_supported(400, 120, 88, 16, (int)n1, (int)n2, (int)nc, (int)std::max<int64_t>(nb, 1)),
               "mlp_head: unsupported geometry");
   check(x, at::kBFloat16, nb * 400, "x");
@@ -400,7 +400,8 @@ void mlp_head(Tensor x, Tensor w3t, Tensor b3, int64_t n1, Tensor w4t, Tensor b4
   check(h4, at::kBFloat16, nb * 88, "h4");
   check(logits, at::kFloat, nb * 16, "logits");
   check(stats, at::kFloat, 8, "stats");
-  check(work, at::kFloat, 4 * 1024 + 1, "work");
+  const bool has_work = work.has_value() && work->defined();   // none: order-dependent atomics
+  if (has_work) check(*work, at::kFloat, 4 * 1024 + 1, "work");
   for (const Tensor* t : {&x, &w3t, &w4t, &w5t, &h3, &h4, &logits})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "mlp_head: operands must be 16-byte aligned");
   mnistx::bf16_t *pdl = nullptr, *pdh4 = nullptr, *pdh3 = nullptr, *pdx = nullptr;
@@ -419,8 +420,8 @@ void mlp_head(Tensor x, Tensor w3t, Tensor b3, int64_t n1, Tensor w4t, Tensor b4
   }
   hip_ok(mnistx::mlp_head(BF(x), BF(w3t), P<const float>(b3), (int)n1, BF(w4t), P<const float>(b4), (int)n2, BF(w5t),
                           P<const float>(b5), (int)nc, P<const int32_t>(labels), (int)nb, (float)scale, BFm(h3),
-                          BFm(h4), P<float>(logits), pdl, pdh4, pdh3, pdx, P<float>(stats), P<float>(work),
-                          cur_stream()),
+                          BFm(h4), P<float>(logits), pdl, pdh4, pdh3, pdx, P<float>(stats), has_work ? P<float>(*work) : nullptr,
+                          cur_stream(), (defer_stats && has_work) ? 1 : 0),
          "mlp_head");
 }
 
@@ -539,7 +540,7 @@ void fused_optimizer(Tensor params, Tensor grads, Tensor mom, Tensor ema, Tensor
 
 void finalize_step(Tensor step, Tensor stats, optional<Tensor> l2, optional<Tensor> wds, int64_t nw,
                    optional<Tensor> loss_ema, int64_t n_ema, int64_t batch, bool increment,
-                   optional<Tensor> l2_ranges) {
+                   optional<Tensor> l2_ranges, optional<Tensor> ce_work, int64_t ce_nblk) {
   check(step, at::kLong, 1, "step");
   check(stats, at::kFloat, 8, "stats");
   const float* l2p = nullptr;
@@ -562,8 +563,15 @@ void finalize_step(Tensor step, Tensor stats, optional<Tensor> l2, optional<Tens
     rp = P<const int>(*l2_ranges);
     // partials follow the nw per-weight slots (binding fused_optimizer: l2n = max track index)
   }
+  const float* cw = nullptr;
+  if (ce_nblk > 0) {
+    TORCH_CHECK(ce_work.has_value() && ce_work->defined() && ce_nblk <= 1024, "ce_work needed for ce_nblk > 0");
+    check(*ce_work, at::kFloat, 4 * 1024 + 1, "ce_work");
+    cw = P<const float>(*ce_work);
+  }
   hip_ok(mnistx::finalize_step(P<int64_t>(step), P<float>(stats), l2p, rp, (int)nw, wp, (int)nw, le,
-                               le ? (int)n_ema : 0, (int)batch, increment ? 1 : 0, cur_stream()),
+                               le ? (int)n_ema : 0, (int)batch, increment ? 1 : 0, cur_stream(), cw,
+                               (int)ce_nblk),
          "finalize_step");
 }
 
@@ -960,7 +968,7 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("b4"), py::arg("n2"), py::arg("w5t"), py::arg("b5"), py::arg("nc"), py::arg("labels"), py::arg("nb"),
         py::arg("scale"), py::arg("h3"), py::arg("h4"), py::arg("logits"), py::arg("dl") = py::none(),
         py::arg("dh4") = py::none(), py::arg("dh3") = py::none(), py::arg("dx") = py::none(), py::arg("stats"),
-        py::arg("work"));
+        py::arg("work"), py::arg("defer_stats") = false);
   m.def("fused_optimizer", &fused_optimizer);
   m.def("fused_optimizer_blocks", [](Tensor segs) {
     TORCH_CHECK(!segs.is_cuda() && segs.scalar_type() == at::kLong && segs.dim() == 2, "segs: CPU int64 [n,14]");
@@ -971,7 +979,8 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.def("finalize_step", &finalize_step, py::arg("step"), py::arg("stats"), py::arg("l2"), py::arg("wds"),
         py::arg("nw"), py::arg("loss_ema"), py::arg("n_ema"), py::arg("batch"), py::arg("increment"),
-        py::arg("l2_ranges") = py::none());
+        py::arg("l2_ranges") = py::none(), py::arg("ce_work") = py::none(), py::arg("ce_nblk") = 0);
+  m.def("mlp_head_blocks", [](int64_t nb) { return (int64_t)mnistx::mlp_head_blocks((int)nb); });
   m.def("cast_f32_bf16_padded", &cast_f32_bf16_padded);
   m.def("convpool_supported", &convpool_supported);
   m.def("convpool_rows", &convpool_rows);

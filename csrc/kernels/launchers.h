@@ -165,7 +165,9 @@ bool mlp_head_supported(int d0, int ld1, int ld2, int ld3, int n1, int n2, int n
 hipError_t mlp_head(const bf16_t* x, const bf16_t* w3t, const float* b3, int n1, const bf16_t* w4t, const float* b4,
                     int n2, const bf16_t* w5t, const float* b5, int nc, const int32_t* labels, int nb, float scale,
                     bf16_t* h3, bf16_t* h4, float* logits, bf16_t* dl, bf16_t* dh4, bf16_t* dh3, bf16_t* dx,
-                    float* stats, float* work, hipStream_t st);
+                    float* stats, float* work, hipStream_t st, int defer_stats = 0);
+// blocks of one mlp_head launch (its per-block CE partials when defer_stats is set)
+int mlp_head_blocks(int nb);
 // NOTE: many splits over a small output are pre-summed IN PLACE (the slab is scratch).
 hipError_t splitk_reduce(float* slab, int splits, int M, int N, int G, int Ipad, int I, int J,
                          int bias_row, float* wdst, float* bdst, float scale, hipStream_t st);
@@ -208,8 +210,11 @@ hipError_t fused_optimizer(float* params, const float* grads, float* mom, float*
                            int nseg, int64_t total, const int64_t* step, OptParams op, float* l2, int l2n, hipStream_t st);
 // l2r (optional, device int32 [nw][3] = {weight index, first block, end block}): sum the
 // fused optimizer's per-block partials at l2[l2base + block] for each weight
+// ce_work / ce_nblk: per-block CE partials of a deferred-stats mlp_head launch, added to
+// stats[0..2] in block order before anything reads them
 hipError_t finalize_step(int64_t* step, float* stats, const float* l2, const int* l2r, int l2base, const float* wds,
-                         int nw, float* loss_ema, int n_ema, int batch, int increment, hipStream_t st);
+                         int nw, float* loss_ema, int n_ema, int batch, int increment, hipStream_t st,
+                         const float* ce_work = nullptr, int ce_nblk = 0);
 hipError_t cast_f32_bf16_padded(const float* src, bf16_t* dst, int G, int I, int J, int Ip, int Jp,
                                 hipStream_t st);
 

@@ -758,12 +758,30 @@ __global__ __launch_bounds__(TPB) void fused_opt_k(float* __restrict__ params, c
 // loss_ema: n_ema x {biased, local_step, avg}  (TF zero-debiased EMA, decay 0.9:
 //           mnist_input.py:288-290); order = weight losses..., cross_entropy, total_loss
 __global__ void finalize_k(int64_t* step, float* stats, float* l2, const int* __restrict__ l2r, int l2base,
-                           const float* wds, int nw, float* loss_ema, int n_ema, int batch, int increment) {
+                           const float* wds, int nw, float* loss_ema, int n_ema, int batch, int increment,
+                           const float* __restrict__ ce_work, int ce_nblk) {
   // one wave; lane i owns loss entry i (weight losses..., cross_entropy, total_loss), so the
   // EMA read-modify-writes run in parallel instead of as one dependent chain
   const int t = threadIdx.x;
-  const float ce = stats[0] / (float)batch;
-  const float acc = stats[1] / (float)batch;
+  float ce_sum = stats[0], corr_sum = stats[1];
+  if (ce_nblk > 0) {
+    // deferred CE partials (ce_block_stats defer): the same lane-strided, fixed-tree sum as
+    // the ticket combine's last block, so the loss is bitwise what that path produced
+    float a = 0.f, b = 0.f, c = 0.f;
+    for (int i = t; i < ce_nblk; i += 64) {
+      a += ce_work[4 * i];
+      b += ce_work[4 * i + 1];
+      c += ce_work[4 * i + 2];
+    }
+    a = warp_sum(a);
+    b = warp_sum(b);
+    c = warp_sum(c);
+    ce_sum += a;
+    corr_sum += b;
+    if (t == 0 && c > 0.f) stats[2] = 1.f;
+  }
+  const float ce = ce_sum / (float)batch;
+  const float acc = corr_sum / (float)batch;
   // sum(w^2) of weight t: the fused optimizer's per-block partials l2[l2base + b],
   // b in [l2r[3w+1], l2r[3w+2]), summed by the whole wave in a fixed order
   float l2v = (l2 && t < nw) ? l2[t] : 0.f;
@@ -938,8 +956,11 @@ hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B
 
 hipError_t splitk_reduce_multi(const RedSpec* specs, int n, hipStream_t st) {
   if (n < 1) return hipSuccess;
+  // one-split slabs (small batches: K below pick_splits' min_k) take the same multi-tensor
+  // launch -- its S = 1 sum is the slab itself -- instead of one generic launch per tensor
+  // (LeNet-5 at B = 128: 5 launches, ~31 us of a ~100 us step)
   bool vec = true;
-  for (int i = 0; i < n; ++i) vec = vec && specs[i].N % 4 == 0 && specs[i].splits > 1;
+  for (int i = 0; i < n; ++i) vec = vec && specs[i].N % 4 == 0 && specs[i].splits >= 1;
   if (!vec) {  // generic path, one launch per tensor
     for (int i = 0; i < n; ++i) {
       const RedSpec& r = specs[i];
@@ -1021,9 +1042,10 @@ hipError_t fused_optimizer(float* params, const float* grads, float* mom, float*
 }
 
 hipError_t finalize_step(int64_t* step, float* stats, const float* l2, const int* l2r, int l2base, const float* wds,
-                         int nw, float* loss_ema, int n_ema, int batch, int increment, hipStream_t st) {
+                         int nw, float* loss_ema, int n_ema, int batch, int increment, hipStream_t st,
+                         const float* ce_work, int ce_nblk) {
   hipLaunchKernelGGL(finalize_k, dim3(1), dim3(64), 0, st, step, stats, (float*)l2, l2r, l2base, wds, nw, loss_ema,
-                     n_ema, batch, increment);
+                     n_ema, batch, increment, ce_work, ce_nblk);
   return hipGetLastError();
 }
 

@@ -178,7 +178,7 @@ __global__ __launch_bounds__(64 * NW) void mlp_head_k(const bf16_t* __restrict__
                                                   float* __restrict__ logits, bf16_t* __restrict__ dl,
                                                   bf16_t* __restrict__ dh4, bf16_t* __restrict__ dh3,
                                                   bf16_t* __restrict__ dx, float* __restrict__ stats,
-                                                  float* __restrict__ work) {
+                                                  float* __restrict__ work, int defer_stats) {
   __shared__ __attribute__((aligned(16))) bf16_t i3[R3 * S3];
   __shared__ __attribute__((aligned(16))) bf16_t i4[R4 * S4];
   __shared__ __attribute__((aligned(16))) bf16_t i5[R5 * S5];
@@ -421,7 +421,7 @@ __global__ __launch_bounds__(64 * NW) void mlp_head_k(const bf16_t* __restrict__
   }
   lab = lab_next;
   }
-  if (stats) ce_block_stats<NW>(loss, corr, bad, stats, work);
+  if (stats) ce_block_stats<NW>(loss, corr, bad, stats, work, defer_stats != 0);
 }
 
 }  // namespace
@@ -432,6 +432,8 @@ static int head_tpw() {
   return v;
 }
 
+int mlp_head_blocks(int nb) { return (nb + ROWS - 1) / ROWS; }
+
 bool mlp_head_supported(int d0, int ld1, int ld2, int ld3, int n1, int n2, int nc, int B) {
   return d0 == D0 && ld1 == LD1 && ld2 == LD2 && ld3 == LD3 && n1 <= LD1 && n2 <= LD2 && nc <= LD3 && nc > 0 &&
          B > 0 && (B + ROWS - 1) / ROWS <= CE_MAXB;
@@ -440,24 +442,24 @@ bool mlp_head_supported(int d0, int ld1, int ld2, int ld3, int n1, int n2, int n
 hipError_t mlp_head(const bf16_t* x, const bf16_t* w3t, const float* b3, int n1, const bf16_t* w4t, const float* b4,
                     int n2, const bf16_t* w5t, const float* b5, int nc, const int32_t* labels, int nb, float scale,
                     bf16_t* h3, bf16_t* h4, float* logits, bf16_t* dl, bf16_t* dh4, bf16_t* dh3, bf16_t* dx,
-                    float* stats, float* work, hipStream_t st) {
+                    float* stats, float* work, hipStream_t st, int defer_stats) {
   if (nb <= 0) return hipSuccess;
   const dim3 grid((nb + ROWS - 1) / ROWS);   // ROWS rows per block in both layouts
   if (head_tpw() == 2) {
     if (dl)
       hipLaunchKernelGGL((mlp_head_k<true, NWAVE / 2, 2>), grid, dim3(NTH / 2), 0, st, x, w3t, b3, n1, w4t, b4, n2,
-                         w5t, b5, nc, labels, nb, scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work);
+                         w5t, b5, nc, labels, nb, scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work, defer_stats);
     else
       hipLaunchKernelGGL((mlp_head_k<false, NWAVE / 2, 2>), grid, dim3(NTH / 2), 0, st, x, w3t, b3, n1, w4t, b4, n2,
-                         w5t, b5, nc, labels, nb, scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work);
+                         w5t, b5, nc, labels, nb, scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work, defer_stats);
     return hipGetLastError();
   }
   if (dl)
     hipLaunchKernelGGL(mlp_head_k<true>, grid, dim3(NTH), 0, st, x, w3t, b3, n1, w4t, b4, n2, w5t, b5, nc, labels, nb,
-                       scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work);
+                       scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work, defer_stats);
   else
     hipLaunchKernelGGL(mlp_head_k<false>, grid, dim3(NTH), 0, st, x, w3t, b3, n1, w4t, b4, n2, w5t, b5, nc, labels, nb,
-                       scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work);
+                       scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work, defer_stats);
   return hipGetLastError();
 }
 

@@ -366,6 +366,10 @@ def _weight_pads(spec: ModelSpec) -> Dict[str, Tuple[int, int]]:
 class HipNet:
     """One model replica on one GPU: buffers + kernels for fwd / bwd / update."""
 
+    # head blocks whose CE partials the next finalize combines (deferred statistics;
+    # class default so subclasses with their own heads, e.g. HipNetF32, never defer)
+    _ce_defer_blocks = 0
+
     def __init__(self, spec: ModelSpec, batch: int, device, init: Dict[str, torch.Tensor],
                  opt: Optional[OptConfig] = None, fuse_convpool: bool = True, overlap_backward: bool = False,
                  fuse_head: bool = True, fuse_lrnpool: Optional[bool] = None):
@@ -485,6 +489,10 @@ class HipNet:
         self.eval_stats = torch.zeros(8, dtype=torch.float32, device=dev)
         # softmax-CE per-block partials + ticket: deterministic loss / accuracy sums
         self.ce_work = torch.zeros(4 * 1024 + 1, dtype=torch.float32, device=dev)
+        # experiment knob: MNISTX_CE_ATOMIC=1 drops the ticket combine (and its agent-scope
+        # fences) for order-dependent float atomics -- for timing the combine only
+        if os.environ.get("MNISTX_CE_ATOMIC", "0") == "1":
+            self.ce_work = None
         names = [e.name for e in self.fp.wd_entries]
         self.loss_names = [n.replace("/weights", "/weight_loss") for n in names] + ["cross_entropy", "total_loss"]
         self.loss_ema = torch.zeros(3 * len(self.loss_names), dtype=torch.float32, device=dev)
@@ -568,6 +576,9 @@ class HipNet:
 
     def _run_head(self, nb: int, scale: float, grads: bool, stats: torch.Tensor) -> None:
         i = self.head
+        # training statistics: the per-block CE partials are combined by this step's
+        # finalize_k (no agent-scope fence / ticket inside the head; ce_stats.h)
+        defer = grads and stats is self.stats and self.ce_work is not None
         l3, l4, l5 = self.layers[i:]
         fp = self.fp
         kernels().mlp_head(l3.x, fp.bf16t_view(l3.wname), fp.param_view(l3.bname), l3.spec.dout,
@@ -576,7 +587,9 @@ class HipNet:
                            self.labels, nb, scale, l3.out, l4.out, l5.out,
                            dl=self.dlogits if grads else None, dh4=self.dbuf[i + 2] if grads else None,
                            dh3=self.dbuf[i + 1] if grads else None, dx=self.dbuf[i] if grads else None,
-                           stats=stats, work=self.ce_work)
+                           stats=stats, work=self.ce_work, defer_stats=defer)
+        if defer:
+            self._ce_defer_blocks = kernels().mlp_head_blocks(nb)
 
     def bind_u8_input(self, images: torch.Tensor) -> bool:
         """Training steps read a resident dataset [n, H*W] directly through ``idx_buf``
@@ -707,9 +720,11 @@ class HipNet:
     def finalize(self, batch: int, increment: bool = True) -> None:
         fp = self.fp
         nw = len(fp.wd_entries)
+        nblk = getattr(self, "_ce_defer_blocks", 0)   # HipNetF32 borrows this method
+        self._ce_defer_blocks = 0
         kernels().finalize_step(fp.step, self.stats, fp.l2 if nw else None, fp.wds if nw else None, nw,
                                 self.loss_ema, len(self.loss_names), batch, increment,
-                                fp.l2_ranges if nw else None)
+                                fp.l2_ranges if nw else None, self.ce_work if nblk else None, nblk)
 
     def train_step(self, grad_scale: float = 1.0) -> None:
         self.forward(defer_head=True)

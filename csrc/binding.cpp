@@ -336,9 +336,9 @@ void lrn_pool_bwd(Tensor x, Tensor dP, Tensor arg, Tensor dx, int64_t Nb, int64_
          "lrn_pool_bwd");
 }
 
-void softmax_ce(Tensor logits, int64_t ldl, optional<Tensor> labels, int64_t B, int64_t NC, double scale,
-                optional<Tensor> dlogits, int64_t ldd, optional<Tensor> stats, optional<Tensor> probs,
-                optional<Tensor> work) {
+int64_t softmax_ce(Tensor logits, int64_t ldl, optional<Tensor> labels, int64_t B, int64_t NC, double scale,
+                   optional<Tensor> dlogits, int64_t ldd, optional<Tensor> stats, optional<Tensor> probs,
+                   optional<Tensor> work, bool defer_stats) {
   TORCH_CHECK(ldl >= NC, "ldl < NC");
   check(logits, at::kFloat, B * ldl, "logits");   // whole padded rows (vector loads)
   const int32_t* lab = nullptr;
@@ -369,9 +369,11 @@ void softmax_ce(Tensor logits, int64_t ldl, optional<Tensor> labels, int64_t B, 
     check(*work, at::kFloat, 4 * 1024 + 1, "work");
     wk = P<float>(*work);
   }
+  int deferred = 0;
   hip_ok(mnistx::softmax_ce(P<const float>(logits), (int)ldl, lab, (int)B, (int)NC, (float)scale, dl, (int)ldd, st, pr,
-                            wk, cur_stream()),
+                            wk, cur_stream(), defer_stats ? &deferred : nullptr),
          "softmax_ce");
+  return deferred;   // blocks whose CE partials the caller's finalize_step must combine
 }
 
 bool mlp_head_supported(int64_t d0, int64_t ld1, int64_t ld2, int64_t ld3, int64_t n1, int64_t n2, int64_t nc,
@@ -960,7 +962,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("lrn_pool_bwd", &lrn_pool_bwd);
   m.def("softmax_ce", &softmax_ce, py::arg("logits"), py::arg("ldl"), py::arg("labels"), py::arg("B"), py::arg("NC"),
         py::arg("scale"), py::arg("dlogits"), py::arg("ldd"), py::arg("stats"), py::arg("probs"),
-        py::arg("work") = py::none());
+        py::arg("work") = py::none(), py::arg("defer_stats") = false);
   m.def("splitk_reduce", &splitk_reduce);
   m.def("splitk_reduce_multi", &splitk_reduce_multi);
   m.def("mlp_head_supported", &mlp_head_supported);

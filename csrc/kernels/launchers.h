@@ -155,8 +155,12 @@ hipError_t lrn_pool_bwd(const bf16_t* x, const bf16_t* dP, const uint8_t* arg, i
                         float bias, float alpha, float beta, int relu_mask, bf16_t* dx, hipStream_t st);
 // work (optional): >= 4*1024+1 floats, zero-initialised once; makes the loss /
 // accuracy sums deterministic (per-block partials combined in block order)
+// defer_blocks (optional out): with it, the row kernel writes per-block partials only and
+// reports its block count there (0 when the fallback kernel ran: plain atomics); the
+// caller's finalize_step combines them (ce_stats.h defer)
 hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B, int NC, float scale,
-                      bf16_t* dlogits, int ldd, float* stats, float* probs, float* work, hipStream_t st);
+                      bf16_t* dlogits, int ldd, float* stats, float* probs, float* work, hipStream_t st,
+                      int* defer_blocks = nullptr);
 // Fused LeNet-5 dense head (mlp_head.hip): fc3/fc4/fc5 + softmax-CE (+ with dl:
 // the data-gradient chain dlogits -> dh4 -> dh3 -> dx).  Writes h3, h4, logits
 // always; dl, dh4, dh3, dx when dl != nullptr.  Same work-buffer contract as softmax_ce.

@@ -477,7 +477,7 @@ __global__ __launch_bounds__(256) void softmax_ce_rows_k(const float* __restrict
                                                          const int32_t* __restrict__ labels, int B, int NC,
                                                          float scale, bf16_t* __restrict__ dl,
                                                          float* __restrict__ stats, float* __restrict__ probs,
-                                                         float* __restrict__ work) {
+                                                         float* __restrict__ work, int defer_stats) {
   float loss = 0.f, corr = 0.f, bad = 0.f;
   for (int row = blockIdx.x * 256 + threadIdx.x; row < B; row += gridDim.x * 256) {
     float l[LD];
@@ -529,7 +529,7 @@ __global__ __launch_bounds__(256) void softmax_ce_rows_k(const float* __restrict
       for (int c = 0; c < LD; ++c)
         if (c < NC) probs[(int64_t)row * NC + c] = e[c] * inv;
   }
-  if (stats) ce_block_stats<4>(loss, corr, bad, stats, work);
+  if (stats) ce_block_stats<4>(loss, corr, bad, stats, work, defer_stats != 0);
 }
 
 // ------------------------------------------------------------------ split-K reduce
@@ -936,17 +936,21 @@ hipError_t lrn_bwd(const bf16_t* x, const bf16_t* dy, int P, int C, int r, float
 }
 
 hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B, int NC, float scale,
-                      bf16_t* dlogits, int ldd, float* stats, float* probs, float* work, hipStream_t st) {
+                      bf16_t* dlogits, int ldd, float* stats, float* probs, float* work, hipStream_t st,
+                      int* defer_blocks) {
   const int nb = (int)std::min<int64_t>(CE_MAXB, ((int64_t)B + 255) / 256);
+  if (defer_blocks) *defer_blocks = 0;
   const bool rows_ok = (ldl == 16 || ldl == 32) && NC <= ldl && (!dlogits || ldd == ldl) &&
                        ((uintptr_t)logits % 16 == 0) && (!dlogits || (uintptr_t)dlogits % 16 == 0);
   if (rows_ok && B > 0) {
+    const int defer = (defer_blocks && work && stats) ? 1 : 0;
+    if (defer) *defer_blocks = nb;
     if (ldl == 16)
       hipLaunchKernelGGL(softmax_ce_rows_k<16>, dim3(nb), dim3(256), 0, st, logits, labels, B, NC, scale, dlogits,
-                         stats, probs, work);
+                         stats, probs, work, defer);
     else
       hipLaunchKernelGGL(softmax_ce_rows_k<32>, dim3(nb), dim3(256), 0, st, logits, labels, B, NC, scale, dlogits,
-                         stats, probs, work);
+                         stats, probs, work, defer);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(softmax_ce_k, dim3((B + TPB - 1) / TPB), dim3(TPB), 0, st, logits, ldl, labels, B, NC, scale,

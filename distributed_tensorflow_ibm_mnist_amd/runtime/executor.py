@@ -637,9 +637,11 @@ class HipNet:
             self._run_head(nb, (1.0 / nb) if scale is None else scale, True, self.stats)
             self._head_pending, self._head_grads = None, True
             return
-        kernels().softmax_ce(self.logits, self.logits.shape[1], self.labels, nb, self.n_classes,
-                             (1.0 / nb) if scale is None else scale, self.dlogits, self.logits.shape[1], self.stats,
-                             None, self.ce_work)
+        # training statistics deferred to this step's finalize_k, as for the fused head
+        self._ce_defer_blocks = kernels().softmax_ce(
+            self.logits, self.logits.shape[1], self.labels, nb, self.n_classes,
+            (1.0 / nb) if scale is None else scale, self.dlogits, self.logits.shape[1], self.stats,
+            None, self.ce_work, defer_stats=self.ce_work is not None)
 
     def backward(self, nb: Optional[int] = None) -> None:
         """Data-gradient chain on the current stream; each layer's weight gradient

@@ -1,0 +1,38 @@
+"""The driver's multi-GPU bench launch form (``torch.distributed.run --nnodes=1
+--nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N``), rehearsed on
+one MI355X: RCCL refuses two ranks on one device, so the ranks share cuda:0 over
+the gloo backend (host-staged all-reduce of the same gradient buckets).  Checks
+the contract the 8-GPU scaling run relies on: exactly one JSON line (rank 0),
+n_gpus / global_batch / parallelism scaled by the world size, the HIP kernels
+running on every rank, and replicas holding identical weights after the timed
+steps."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("model,batch", [("lenet5", 4096), ("reference_cnn", 1024)])
+def test_bench_torchrun_two_ranks_one_gpu(model, batch):
+    port = str(29900 + (os.getpid() % 50) + (0 if model == "lenet5" else 50))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", port,
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
+           "--model", model, "--batch", str(batch), "--dist_backend", "gloo", "--phases", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT,
+                       env={**os.environ, "OMP_NUM_THREADS": "2"})
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 6 and out["warmup"] == 2
+    assert out["config"]["global_batch"] == 2 * batch and out["config"]["per_gpu_batch"] == batch
+    assert out["config"]["parallelism"] == "dp2" and out["config"]["impl"] == "hip"
+    assert out["replicas_in_sync"] is True
+    assert out["grad_bucket_mb"] and out["value"] > 0
+    assert out["final_train_loss"] == out["final_train_loss"]     # not NaN

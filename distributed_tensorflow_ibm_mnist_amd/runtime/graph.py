@@ -15,6 +15,11 @@ one launch.  Off by default: at the BASELINE batch (65536 / GPU) eager launches
 already keep the GPU busy (profiles/r2/graph_vs_eager.md) and the 1..8-GPU curve
 then runs one execution mode throughout.  Rehearsed on one GPU with a one-rank
 RCCL group (tests/test_dp_graph_gpu.py).
+
+With a process group up, capture runs in thread-local error mode: the RCCL
+process group's watchdog thread keeps polling the events of earlier
+collectives, and under the default global mode such a query during capture
+fails the watchdog ("operation not permitted when stream is capturing").
 """
 from __future__ import annotations
 
@@ -34,7 +39,9 @@ class StepGraph:
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        import torch.distributed as dist
+        mode = "thread_local" if dist.is_available() and dist.is_initialized() else "global"
+        with torch.cuda.graph(self.graph, capture_error_mode=mode):
             fn()
         torch.cuda.synchronize()
 

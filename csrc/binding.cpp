@@ -726,6 +726,51 @@ void convpool_dgrad(Tensor dP, Tensor arg, Tensor w, Tensor dx, int64_t B, int64
          "convpool_dgrad");
 }
 
+// LeNet-5 conv1+pool1+conv2+pool2 forward on banded MFMA tiles (lenet_band.hip).
+// x: bf16 images [n, 784] gathered through idx, or the batch itself [B, 784] (idx None).
+void lenet_band_fwd(Tensor x, Tensor w1, Tensor b1, int64_t b1n, Tensor w2, Tensor b2, int64_t B, Tensor p2,
+                    Tensor arg2, optional<Tensor> p1, optional<Tensor> arg1, optional<Tensor> idx,
+                    optional<Tensor> prof) {
+  mnistx::XSrc src{nullptr, nullptr, nullptr, 0};
+  check(x, at::kBFloat16, 784, "x");
+  TORCH_CHECK(x.numel() % 784 == 0 && x.numel() * 2 < (int64_t)INT32_MAX, "x: [n, 784] bf16 images, < 2 GB");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "x must be 16-byte aligned");
+  src.x = BF(x);
+  src.n = (int)(x.numel() / 784);
+  if (idx.has_value() && idx->defined()) {
+    check(*idx, at::kLong, B, "idx");
+    src.idx = P<const int64_t>(*idx);
+  } else {
+    TORCH_CHECK(src.n >= B, "x: needs B images without idx");
+  }
+  check(w1, at::kBFloat16, 5 * 5 * 8, "w1");
+  check(b1, at::kFloat, b1n, "b1");
+  TORCH_CHECK(b1n >= 0 && b1n <= 8, "b1n");
+  check(w2, at::kBFloat16, 5 * 5 * 8 * 16, "w2");
+  check(b2, at::kFloat, 16, "b2");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(w1.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w2.data_ptr()) % 16 == 0,
+              "w1 / w2 must be 16-byte aligned");
+  check(p2, at::kBFloat16, B * 400, "p2");
+  check(arg2, at::kByte, B * 400, "arg2");
+  mnistx::bf16_t* pp1 = nullptr;
+  uint8_t* pa1 = nullptr;
+  if (p1.has_value() && p1->defined()) {
+    TORCH_CHECK(arg1.has_value() && arg1->defined(), "p1 needs arg1");
+    check(*p1, at::kBFloat16, B * 14 * 14 * 8, "p1");
+    check(*arg1, at::kByte, B * 14 * 14 * 4, "arg1");
+    pp1 = BFm(*p1);
+    pa1 = P<uint8_t>(*arg1);
+  }
+  unsigned long long* pr = nullptr;
+  if (prof.has_value() && prof->defined()) {   // experiments: int64[4] clock sums
+    check(*prof, at::kLong, 4, "prof");
+    pr = P<unsigned long long>(*prof);
+  }
+  hip_ok(mnistx::lenet_band_fwd(src, BF(w1), P<const float>(b1), (int)b1n, BF(w2), P<const float>(b2), (int)B, pp1,
+                                pa1, BFm(p2), P<uint8_t>(arg2), cur_stream(), pr),
+         "lenet_band_fwd");
+}
+
 // ---------------------------------------------------------------- fp32 (reference precision) path
 const float* Fo(const optional<Tensor>& t, int64_t need, const char* name) {
   if (!t.has_value() || !t->defined()) return nullptr;
@@ -1002,5 +1047,8 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("convpool_arg_bytes", &convpool_arg_bytes);
   m.def("convpool_has_dgrad", &convpool_has_dgrad);
   m.def("convpool_wgrad_grid", &convpool_wgrad_grid);
+  m.def("lenet_band_fwd", &lenet_band_fwd, py::arg("x"), py::arg("w1"), py::arg("b1"), py::arg("b1n"),
+        py::arg("w2"), py::arg("b2"), py::arg("B"), py::arg("p2"), py::arg("arg2"), py::arg("p1") = py::none(),
+        py::arg("arg1") = py::none(), py::arg("idx") = py::none(), py::arg("prof") = py::none());
   m.attr("ARCH") = "gfx950";
 }

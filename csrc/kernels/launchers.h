@@ -103,6 +103,14 @@ int lenet_c2dgrad_c1wgrad_grid();
 hipError_t lenet_c2dgrad_c1wgrad(const XSrc& x, const bf16_t* dP2, const uint8_t* arg2, const bf16_t* w2,
                                  const uint8_t* arg1, int B, float* slab, int grid, hipStream_t st);
 
+// ---- lenet_band.hip: LeNet-5 conv1+pool1+conv2+pool2 forward on banded MFMA tiles
+// (one persistent kernel; bf16 images only).  x.x = [n][784] images (x.idx: per-sample
+// rows, else sample b = row b).  p1/arg1 (convpool cfg-0 layouts) are written only when
+// p1 != nullptr; p2/arg2 use the convpool cfg-1 layouts.
+hipError_t lenet_band_fwd(const XSrc& x, const bf16_t* w1, const float* b1, int b1n, const bf16_t* w2,
+                          const float* b2, int B, bf16_t* p1, uint8_t* arg1, bf16_t* p2, uint8_t* arg2,
+                          hipStream_t st, unsigned long long* prof = nullptr);
+
 // ---- f32.hip: reference-precision (fp32) path, v_mfma_f32_16x16x4_f32
 hipError_t f32_dense_fwd(const float* x, const float* w, int M, int N, int K, const float* bias, int bias_n, int relu,
                          float* y, int ldy, hipStream_t st);

@@ -1,0 +1,447 @@
+// LeNet-5 conv stack on banded (Toeplitz) MFMA tiles, gfx950.
+//
+// conv1 (5x5 SAME, 1 -> 6) + bias + ReLU + 2x2 max-pool and conv2 (5x5 VALID,
+// 6 -> 16) + bias + ReLU + 2x2 max-pool as ONE persistent kernel per batch.
+//
+// Formulation (why it maps to CDNA4): a convolution over an image row is a GEMM
+// with a banded ("Toeplitz") weight matrix: out[(x, c)] = sum_(x', ci) in[(x', ci)]
+// * T[(x', ci)][(x, c)] with T = W[x' - x + pad] inside the band.  Written with the
+// weights as the MFMA A operand and the activations as B, the B fragment of a lane
+// is 8 CONSECUTIVE elements of one input row (one 16-byte load) -- there is no
+// im2col gather at all, which is what bounds small-channel implicit-GEMM kernels
+// (VALU + LDS address work per MFMA).  The band wastes part of each MFMA; at
+// 2.5 PF of dense bf16 MFMA that is far cheaper than the gather it replaces.
+//
+// v_mfma_f32_32x32x16_bf16, columns = 32 = 16 images x 2 output-row parities
+// (ypar = column & 1), rows = output features:
+//  * conv1 rows = (xq 2, xpar 2, c 8): the four consecutive output columns
+//    x = 4u + 2xq + xpar of window u; K = 16 = (dy parity h, 8 input columns
+//    x' = 4u-2 .. 4u+5): one k-step covers TWO kernel rows, so 3 k-steps = dy 0..4
+//    (+ one zero row).  3 MFMAs per (pooled row, window), 3 A fragments in total.
+//  * conv2 rows = (xpar 2, c2 16) of ONE pooled column x2p; K = 16 = 2 input
+//    pixels x 8 channels; 3 k-steps x 5 kernel rows.  15 A fragments in total.
+//  * bias added after pooling (4 values per lane instead of 16 accumulators).
+//  * 2x2 pool: the x parity is a register pair of the same lane (rows m, m+4 /
+//    m+8); the y parity is the neighbouring lane (one DPP quad-perm swap); the
+//    argmax position rides in the 2 low mantissa bits of the fp32 sums (the same
+//    encoding as convpool.hip, <= 3 ulp, far below bf16 resolution).
+//  * the input tile and pool1 live in LDS (16 images, bank-conflict-free strides;
+//    the next tile's input is loaded into registers while this tile computes);
+//    conv2 reads pool1 as 16-byte B fragments.  pool1 is copied to HBM only when
+//    the backward kernels still need it.
+//
+// Replaces: Conv2D + BiasAdd + Relu + MaxPool of the
+// LeNet-5 conv blocks (BASELINE config; reference topology mnist_input.py:136-172
+// uses the same ops).
+#include "common.h"
+#include "launchers.h"
+
+#include <cstdlib>
+
+namespace mnistx {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int NTH = 512;        // 8 waves: 0-3 conv1 (producers), 4-7 conv2 (consumers)
+constexpr int BT = 8;           // images per tile (MFMA columns = 8 images x 2 row parities x 2 units)
+constexpr int XROW = 28;        // input row (bf16 elements), 28x28x1 images
+constexpr int XIMG = 784;
+// LDS tiles (bf16 elements), rows split by parity into two planes so that the two
+// output-row parities of an image (lanes 2i, 2i+1) read different bank halves;
+// both rings are double-buffered (conv1 of tile k overlaps conv2 of tile k-1).
+//  input : image [plane 2][14 rows][32 cols = x' -2..29], zero pad columns
+constexpr int XRW = 32, XPL = 448, XIS = 900;
+//  pool1 : image [plane 2][7 rows][14 px][8 ch]
+constexpr int PRW = 112, PPL = 792, PIS = 1584;
+constexpr int XBUF = BT * XIS, PBUF = BT * PIS;
+constexpr int XZERO = 2 * XBUF;                 // one zero row: out-of-image input rows
+constexpr int LDS_X = 2 * XBUF + XRW, LDS_P = 2 * PBUF;
+static_assert((LDS_X + LDS_P) * 2 <= 81920, "two workgroups per CU");
+constexpr int P1E = 14 * 14 * 8;    // pool1 elements per image in HBM ([14][14][8])
+constexpr int P2E = 5 * 5 * 16;     // pool2 elements per image ([5][5][16])
+constexpr uint32_t ARG_OFF = 4;     // argmax code of a window whose ReLU output is 0
+constexpr int U1 = 49;              // conv1 units per tile: (pooled row pair yp0 / yp0 + 7, window u)
+constexpr int U2 = 13;              // conv2 units per tile: (pooled pixel f0 / f0 + 13)
+
+DEV f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0); }
+DEV float embed(float v, uint32_t d) { return __uint_as_float((__float_as_uint(v) & ~3u) | d); }
+DEV float vmax(float a, float b) {  // bare v_max_f32 (fmaxf adds NaN-canonicalising moves)
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// value of the neighbouring lane (lane ^ 1): the other output-row parity of the same image
+DEV float swap1(float v) { return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true)); }
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// two floats -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (round to nearest even)
+DEV uint32_t pk2(float lo, float hi) { return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, bf16x2)); }
+DEV bf16x8 as_frag(u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
+// Two LDS reads at a constant distance are fused by the compiler into ds_read2_b64,
+// which runs at half the rate of two ds_read_b64 on gfx950; hiding the offset keeps
+// them separate.
+DEV int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+struct BandFwd {
+  const bf16_t* x;        // images [n][784] bf16, normalised
+  const int64_t* idx;     // per-sample row of x [B]; null: sample b is row b
+  int n;                  // rows in x
+  const bf16_t* w1;       // [5][5][1][8]
+  const float* b1;        // [b1n]
+  int b1n;
+  const bf16_t* w2;       // [5][5][8][16]
+  const float* b2;        // [16]
+  int B;
+  bf16_t* p1;             // [B][14][14][8] pool1 (null: not written)
+  uint8_t* arg1;          // [B][196][4] packed codes (with p1)
+  bf16_t* p2;             // [B][5][5][16]
+  uint8_t* arg2;          // [B][25][16]
+  unsigned long long* prof;   // optional (experiments): per-role busy / barrier-wait clock sums
+};
+
+// Pooled value + argmax code of the window finalised by this lane: keep = this lane's
+// x-pooled (embedded) sum, send = the one its neighbour finalises, b = the channel's
+// bias (added after pooling: max(a + b, c + b) = max(a, c) + b, ReLU is monotone).
+DEV void pool_y(float keep, float send, float b, float& out, uint32_t& code) {
+  const float v = vmax(keep, swap1(send));
+  out = vmax(__uint_as_float(__float_as_uint(v) & ~3u) + b, 0.f);
+  // active on the CLEARED value: an all-zero window (padded channel) embeds to d > 0
+  code = out > 0.f ? (__float_as_uint(v) & 3u) : ARG_OFF;
+}
+
+// input tile fill by the conv1 waves: thread t (0..255) -> image t >> 5, 8-byte chunks
+// (4 pixels) r = (t & 31) + 32 i of the image's 196
+constexpr int FCH = (196 + 31) / 32;
+struct XFill {
+  u32x2 v[FCH];
+  DEV void load(__amdgpu_buffer_rsrc_t rx, const BandFwd& a, int t0, int t) {
+    const int gi = t0 + (t >> 5);
+    uint32_t base = BUF_OOB;
+    if (gi < a.B && t0 >= 0) {
+      int64_t row = a.idx ? a.idx[gi] : (int64_t)gi;
+      row = row < 0 ? 0 : (row >= a.n ? a.n - 1 : row);
+      base = (uint32_t)row * (XIMG * 2);
+    }
+#pragma unroll
+    for (int i = 0; i < FCH; ++i) {
+      const int r = (t & 31) + 32 * i;
+      v[i] = buf_b64(rx, r < 196 ? base + 8u * r : BUF_OOB);
+    }
+  }
+  DEV void store(bf16_t* xb, int t) const {
+    bf16_t* im = xb + (t >> 5) * XIS + 2;
+#pragma unroll
+    for (int i = 0; i < FCH; ++i) {
+      const int r = (t & 31) + 32 * i;
+      if (r < 196) {
+        const int y = r / 7, k = r - 7 * y;
+        uint32_t* d = (uint32_t*)(im + (y & 1) * XPL + (y >> 1) * XRW + 4 * k);   // 4-byte aligned
+        d[0] = v[i][0];
+        d[1] = v[i][1];
+      }
+    }
+  }
+};
+
+// Warp-specialised pipeline over the block's tiles k = 0..nk-1 (tile blockIdx + k * grid):
+// iteration k: conv1 waves turn input[k%2] into pool1[k%2] (and load tile k+1's input),
+// conv2 waves turn pool1[(k-1)%2] into pool2 -- one barrier per iteration, nk+1 iterations.
+template <bool P1OUT>
+__global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_X + LDS_P];
+  bf16_t* xs = lds;
+  bf16_t* p1s = lds + LDS_X;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 31, h = lane >> 5, ypar = col & 1, img = (col >> 1) & 7, half = col >> 4;
+  const int ntiles = (a.B + BT - 1) / BT;
+  const int nk = ntiles > (int)blockIdx.x ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  auto tile0 = [&](int k) { return ((int)blockIdx.x + k * (int)gridDim.x) * BT; };
+
+  // weights -> LDS (pool1 ring, free until the first conv1 epilogue), zero the input ring
+  constexpr int W1E = 5 * 5 * 8, W2E = 5 * 5 * 8 * 16;
+  bf16_t* w1s = p1s;
+  bf16_t* w2s = p1s + W1E + 8;   // zero slot at W1E: out-of-band taps read 0
+  for (int e = tid; e < W2E / 8; e += NTH) *(u32x4*)(w2s + 8 * e) = *(const u32x4*)(a.w2 + 8 * e);
+  for (int e = tid; e < W1E / 8; e += NTH) *(u32x4*)(w1s + 8 * e) = *(const u32x4*)(a.w1 + 8 * e);
+  if (tid == 0) *(u32x4*)(w1s + W1E) = u32x4{0u, 0u, 0u, 0u};
+  for (int e = tid; e < LDS_X / 8; e += NTH) *(u32x4*)(xs + 8 * e) = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+
+  if (wave < 4) {
+    // ================================================================ conv1 + pool1 role
+    const int t = tid;                                   // 0..255
+    bf16x8 a1[3];    // (p): rows (xq, xpar, c), k = (dy parity h, input column j of the window)
+    {
+      const int xq = col >> 4, xpar = (col >> 3) & 1, c = col & 7;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int dy = 2 * p + h;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int dx = j - 2 * xq - xpar;
+          const bool ok = dy <= 4 && dx >= 0 && dx <= 4;
+          a1[p][j] = __builtin_bit_cast(__bf16, w1s[ok ? (dy * 5 + dx) * 8 + c : W1E]);
+        }
+      }
+    }
+    float bias1[4];    // channels c = i + 4h this lane finalises (added after pooling)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias1[i] = i + 4 * h < a.b1n ? a.b1[i + 4 * h] : 0.f;
+    const uint32_t d0 = 2u * ypar, d1 = d0 + 1u;     // argmax codes of this lane's x parities
+    const auto rx = buf_rsrc(a.x, (uint32_t)a.n * (XIMG * 2));
+    // input rows of a unit: row = S + rlane with S = yp0 + p - 1 (uniform) and the lane's
+    // dy parity h / row half; plane (ypar + h) & 1
+    const int rlane = 7 * half + ((ypar + h) >> 1);
+    const int xlane = img * XIS + ((ypar + h) & 1) * XPL + rlane * XRW;
+    // pool1 store offset: lane part + row-half part (yp = yp0 + 7 half)
+    const int plane_off = img * PIS + ypar * 8 + 4 * h;
+    XFill xf;
+    xf.load(rx, a, nk > 0 ? tile0(0) : -1, t);
+    xf.store(xs, t);     // ring slot 0 (only this role reads the input ring; ordered by the first barrier)
+
+    uint64_t busy = 0, wait = 0, tw = __builtin_amdgcn_s_memtime();
+    for (int k = 0; k <= nk; ++k) {
+      __syncthreads();   // input[k%2] landed; pool1[k%2] no longer read by conv2
+      const uint64_t tb = __builtin_amdgcn_s_memtime();
+      wait += tb - tw;
+      if (k < nk) {
+        const bf16_t* xb = xs + (k & 1) * XBUF + xlane;
+        bf16_t* pb = p1s + (k & 1) * PBUF + plane_off;
+        xf.load(rx, a, k + 1 < nk ? tile0(k + 1) : -1, t);
+        struct Frags { bf16x8 b[3]; };
+        auto fetch = [&](int j) {   // unit f = wave + 4j: B fragments, window columns x' = 4u-2 .. 4u+5
+          const int f = min(wave + 4 * j, U1 - 1), yp0 = f / 7, u = f - 7 * yp0;
+          Frags fr;
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            const int S = yp0 + p - 1;
+            const bf16_t* rp = (unsigned)(rlane + S) < 14u ? xb + S * XRW + 4 * u : xs + XZERO;
+            // 8-byte aligned only: two 8-byte loads (ds_read2_b64), never one misaligned b128
+            const u32x2 lo = *(const u32x2*)rp, hi = *(const u32x2*)(rp + 4);
+            fr.b[p] = as_frag(u32x4{lo[0], lo[1], hi[0], hi[1]});
+          }
+          return fr;
+        };
+        auto window = [&](const Frags& fr) {
+          f32x16 acc = {};
+#pragma unroll
+          for (int p = 0; p < 3; ++p) acc = mfma32(a1[p], fr.b[p], acc);
+          return acc;
+        };
+        auto epilogue = [&](const f32x16& acc, int j) {
+          const int f = wave + 4 * j, yp0 = f / 7, u = f - 7 * yp0;
+          // rows: xq = r>>3, xpar = (r>>2)&1, c = (r&3) + 4h; lane ypar finalises xq = ypar
+          float o[4];
+          uint32_t hi;
+          if constexpr (P1OUT) {   // + argmax codes
+            float keep[4], send[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float m0 = vmax(embed(acc[i], d0), embed(acc[i + 4], d1));        // xq 0
+              const float m1 = vmax(embed(acc[8 + i], d0), embed(acc[12 + i], d1));   // xq 1
+              keep[i] = ypar ? m1 : m0;
+              send[i] = ypar ? m0 : m1;
+            }
+            uint32_t cd[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pool_y(keep[i], send[i], bias1[i], o[i], cd[i]);
+            // packed argmax, byte k = code(c = k) | code(c = k + 4) << 4 (lane h holds c = 4h..4h+3),
+            // parked in the pixel's channels 6-7 (always 0 in HBM; zero weights in conv2, and a
+            // nibble-packed word is a finite bf16 pair) until the copy-out splits it off
+            const uint32_t wcode = cd[0] | (cd[1] << 8) | (cd[2] << 16) | (cd[3] << 24);
+            const auto sw = __builtin_amdgcn_permlane32_swap(wcode, wcode, false, false);
+            hi = h ? (sw[0] | (wcode << 4)) : pk2(o[2], o[3]);
+          } else {                 // values only
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float m0 = vmax(acc[i], acc[i + 4]), m1 = vmax(acc[8 + i], acc[12 + i]);
+              o[i] = vmax(vmax(ypar ? m1 : m0, swap1(ypar ? m0 : m1)) + bias1[i], 0.f);
+            }
+            hi = pk2(o[2], o[3]);
+          }
+          if (f < U1) {
+            const int y0 = yp0, y1 = yp0 + 7;   // the lane's pooled row: y0 (half 0) or y1 (half 1)
+            const int off = half ? (y1 & 1) * PPL + (y1 >> 1) * PRW : (y0 & 1) * PPL + (y0 >> 1) * PRW;
+            *(u32x2*)(pb + off + 16 * u) = u32x2{pk2(o[0], o[1]), hi};
+          }
+        };
+        // software pipeline, 13 slots per wave (past 49: a recomputed unit, no store):
+        // unit j+2's LDS reads and unit j+1's MFMAs issue before unit j's epilogue
+        Frags fa = fetch(0), fb = fetch(1);
+        f32x16 acca = window(fa), accb;
+#pragma unroll 1
+        for (int j = 0; j < 14; j += 2) {
+          fa = fetch(j + 2);
+          accb = window(fb);
+          epilogue(acca, j);
+          fb = fetch(j + 3);
+          acca = window(fa);
+          epilogue(accb, j + 1);
+        }
+        xf.store(xs + ((k + 1) & 1) * XBUF, t);   // tile k+1's input (slot read in iteration k-1)
+      }
+      tw = __builtin_amdgcn_s_memtime();
+      busy += tw - tb;
+    }
+    if (a.prof && lane == 0) {
+      atomicAdd(a.prof + 0, (unsigned long long)busy);
+      atomicAdd(a.prof + 2, (unsigned long long)wait);
+    }
+  } else {
+    // ================================================================ conv2 + pool2 role
+    const int t = tid - 256;
+    bf16x8 a2[15];   // (dy, q): rows (xpar, c2), k = (pixel h, channel j)
+    {
+      const int xpar = col >> 4, c2 = col & 15;
+#pragma unroll
+      for (int dy = 0; dy < 5; ++dy)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const int dx = 2 * q + h - xpar;
+          const bool ok = dx >= 0 && dx <= 4;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            a2[dy * 3 + q][j] = __builtin_bit_cast(__bf16, w1s[ok ? W1E + 8 + ((dy * 5 + dx) * 8 + j) * 16 + c2 : W1E]);
+        }
+    }
+    float bias2[4];    // channels c2 = i + 8 ypar + 4h this lane finalises (added after pooling)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias2[i] = a.b2[i + 8 * ypar + 4 * h];
+    // pool1 row yy = 2 y2p + ypar + dy: even dy -> plane ypar, row y2p + dy/2; odd dy -> plane
+    // 1 - ypar, row y2p + (dy - 1)/2 + ypar
+    const int ce = img * PIS + ypar * PPL + 8 * h, co = img * PIS + (1 - ypar) * PPL + ypar * PRW + 8 * h;
+    const uint32_t d0 = 2u * ypar, d1 = d0 + 1u;
+    const int w2v = wave - 4;
+    uint64_t busy = 0, wait = 0, tw = __builtin_amdgcn_s_memtime();
+    for (int k = 0; k <= nk; ++k) {
+      __syncthreads();   // pool1[(k-1)%2] complete
+      const uint64_t tb = __builtin_amdgcn_s_memtime();
+      wait += tb - tw;
+      tw = tb;
+      if (k == 0) continue;
+      const int t0 = tile0(k - 1), gi = t0 + img;
+      const bool iv = gi < a.B;
+      const bf16_t* pb = p1s + ((k - 1) & 1) * PBUF;
+      if constexpr (P1OUT) {   // pool1 + argmax codes to HBM for the backward kernels
+        constexpr int NV = BT * 196;
+        const int nimg = min(BT, a.B - t0);
+        const auto rp1 = buf_rsrc(a.p1 + (int64_t)t0 * P1E, (uint32_t)nimg * (P1E * 2));
+        const auto ra1 = buf_rsrc(a.arg1 + (int64_t)t0 * 784, (uint32_t)nimg * 784);
+#pragma unroll 1
+        for (int e0 = t; e0 < NV; e0 += 4 * 256) {
+          u32x4 cv[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int e = min(e0 + i * 256, NV - 1), im = e / 196, r = e - im * 196, yp = r / 14, xp = r - yp * 14;
+            cv[i] = *(const u32x4*)(pb + im * PIS + (yp & 1) * PPL + (yp >> 1) * PRW + xp * 8);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int e = e0 + i * 256;
+            const uint32_t oob = e < NV ? 0u : BUF_OOB;
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{cv[i][0], cv[i][1], cv[i][2], 0u}, rp1, (uint32_t)e * 16u + oob, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(cv[i][3], ra1, (uint32_t)e * 4u + oob, 0, 0);
+          }
+        }
+      }
+      // unit = lane's pooled pixel f = f0 + 13 half (f0 = w2v + 4j); the 15 B fragments of a
+      // kernel row dy are read one row ahead; two accumulator chains
+#pragma unroll 1
+      for (int j = 0; j < 4; ++j) {
+        const int f0 = w2v + 4 * j;
+        if (f0 >= U2) break;
+        const int fa = f0, fbb = min(f0 + 13, 24);
+        const int ya = fa / 5, yb = fbb / 5;
+        const int uoff = half ? yb * PRW + 16 * (fbb - 5 * yb) : ya * PRW + 16 * (fa - 5 * ya);
+        const int y2p = half ? yb : ya, x2p = (half ? fbb : fa) - 5 * y2p;
+        const bf16_t* re = pb + ce + uoff;
+        const bf16_t* ro = pb + co + uoff;
+        auto rowp = [&](int dy) { return (dy & 1) ? ro + (dy >> 1) * PRW : re + (dy >> 1) * PRW; };
+        bf16x8 bq[2][3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) bq[0][q] = *(const bf16x8*)(rowp(0) + 16 * q);
+        f32x16 acc0 = {}, acc1 = {};
+#pragma unroll
+        for (int dy = 0; dy < 5; ++dy) {
+          if (dy < 4) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) bq[(dy + 1) & 1][q] = *(const bf16x8*)(rowp(dy + 1) + 16 * q);
+          }
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            if ((dy * 3 + q) & 1) acc1 = mfma32(a2[dy * 3 + q], bq[dy & 1][q], acc1);
+            else acc0 = mfma32(a2[dy * 3 + q], bq[dy & 1][q], acc0);
+          }
+        }
+        const f32x16 acc = acc0 + acc1;
+        // rows: xpar = r>>3, c2 = (r&3) + 8((r>>2)&1) + 4h; lane ypar finalises c2 = (i&3) + 8 ypar + 4h
+        float keep[4], send[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float m0 = vmax(embed(acc[i], d0), embed(acc[i + 8], d1));          // c2 = i + 4h
+          const float m1 = vmax(embed(acc[4 + i], d0), embed(acc[12 + i], d1));     // c2 = 8 + i + 4h
+          keep[i] = ypar ? m1 : m0;
+          send[i] = ypar ? m0 : m1;
+        }
+        float o[4];
+        uint32_t cd[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pool_y(keep[i], send[i], bias2[i], o[i], cd[i]);
+        if (iv && (half == 0 || f0 + 13 < 25)) {
+          const int64_t e = (int64_t)gi * P2E + (y2p * 5 + x2p) * 16 + 8 * ypar + 4 * h;
+          *(u32x2*)(a.p2 + e) = u32x2{pk2(o[0], o[1]), pk2(o[2], o[3])};
+          *(uint32_t*)(a.arg2 + e) = cd[0] | (cd[1] << 8) | (cd[2] << 16) | (cd[3] << 24);
+        }
+      }
+      tw = __builtin_amdgcn_s_memtime();
+      busy += tw - tb;
+    }
+    if (a.prof && lane == 0) {
+      atomicAdd(a.prof + 1, (unsigned long long)busy);
+      atomicAdd(a.prof + 3, (unsigned long long)wait);
+    }
+  }
+}
+
+template <bool P1OUT>
+int fwd_grid(int ntiles) {
+  static int per_cu = -1, cus = 0;
+  if (per_cu < 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return -1;
+    cus = prop.multiProcessorCount;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lenet_band_fwd_k<P1OUT>, NTH, 0) != hipSuccess) return -1;
+    per_cu = nb > 0 ? nb : 1;
+  }
+  return ntiles < per_cu * cus ? ntiles : per_cu * cus;
+}
+
+}  // namespace
+
+hipError_t lenet_band_fwd(const XSrc& x, const bf16_t* w1, const float* b1, int b1n, const bf16_t* w2,
+                          const float* b2, int B, bf16_t* p1, uint8_t* arg1, bf16_t* p2, uint8_t* arg2,
+                          hipStream_t st, unsigned long long* prof) {
+  if (B <= 0) return hipSuccess;
+  if (!x.x || x.u8) return hipErrorInvalidValue;   // bf16 images only
+  BandFwd a{x.x, x.idx, x.idx ? x.n : B, w1, b1, b1n, w2, b2, B, p1, arg1, p2, arg2, prof};
+  const int ntiles = (B + BT - 1) / BT;
+  if (p1) {
+    const int grid = fwd_grid<true>(ntiles);
+    if (grid <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(lenet_band_fwd_k<true>, dim3(grid), dim3(NTH), 0, st, a);
+  } else {
+    const int grid = fwd_grid<false>(ntiles);
+    if (grid <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(lenet_band_fwd_k<false>, dim3(grid), dim3(NTH), 0, st, a);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace mnistx

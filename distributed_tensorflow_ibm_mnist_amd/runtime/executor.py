@@ -543,6 +543,10 @@ class HipNet:
                     b.lrn_pre = (a.spec, a.x)
                     a.skip_fwd = True
                     self.fold_lrn_fwd = True
+        # LeNet-5: conv1+pool1+conv2+pool2 forward as ONE banded-MFMA kernel (lenet_band.hip),
+        # bf16 inputs only (x0 or the bf16 resident dataset); MNISTX_BAND_FWD=0 runs the two
+        # convpool kernels instead
+        self.band_fwd = self._find_c2d_c1w() and os.environ.get("MNISTX_BAND_FWD", "1") != "0"
         if self.fuse_c2d_c1w:
             l0, l1 = self.layers[0], self.layers[1]
             l0.fused_grid = min(l0.grid, kernels().lenet_c2dgrad_c1wgrad_grid())
@@ -625,10 +629,24 @@ class HipNet:
         if isinstance(first, ConvPoolLayer):
             first.use_u8 = first.u8 is not None and not from_x0
         stop = self.head if (defer_head and self.head is not None) else len(self.layers)
-        for lay in self.layers[:stop]:
+        start = 0
+        if self.band_fwd and stop >= 2 and not (first.use_u8 and first.u8[0].dtype == torch.uint8):
+            self._band_forward(nb)
+            start = 2
+        for lay in self.layers[start:stop]:
             lay.fwd(nb)
         self._head_pending = nb if stop < len(self.layers) else None
         return self.logits
+
+    def _band_forward(self, nb: int) -> None:
+        """conv1 -> pool1 -> conv2 -> pool2 in one launch; writes both layers' pooled
+        outputs and argmax codes in the convpool layouts the backward kernels read."""
+        l0, l1 = self.layers[0], self.layers[1]
+        fp = self.fp
+        src = l0._src()
+        kernels().lenet_band_fwd(l0._xin(), fp.bf16_view(l0.wname), fp.param_view(l0.bname), l0.spec.cout,
+                                 fp.bf16_view(l1.wname), fp.param_view(l1.bname), nb, l1.out, l1.arg,
+                                 p1=l0.out, arg1=l0.arg, idx=src.get("idx"))
 
     def loss_and_grad(self, nb: Optional[int] = None, scale: Optional[float] = None) -> None:
         nb = self.B if nb is None else nb
@@ -773,7 +791,10 @@ class HipNet:
             s = lay.spec
             OH, OW = Fk.conv_out_hw(lay.H, lay.W, s.kh, s.kw, s.padding)
             x = lay.x
-            if lay.u8 is not None and lay.use_u8:
+            # decided by the binding, not by ``use_u8``: that flag belongs to the last EAGER
+            # forward (an eval pass clears it) and hipGraph replays of the training step never
+            # run the Python forward, so it can be stale while training still reads the dataset
+            if lay.u8 is not None:
                 # training reads a resident dataset through the batch index: those rows, normalised
                 ds, idx = lay.u8
                 rows = ds[idx[:n]]

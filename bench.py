@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--eager_steps", type=int, default=-1,
                     help="N=1 with a hipGraph: also time this many EAGER steps after the timed region "
                          "(ms_per_step_eager, comparable with N>1 runs); -1 = --steps")
+    ap.add_argument("--comm_probe", type=int, default=1,
+                    help="N>1 (or --force_collectives 1): after the timed steps, time each gradient bucket's "
+                         "all-reduce alone (us, bus GB/s) and the exposed communication of an eager step")
     ap.add_argument("--phases", type=int, default=3,
                     help="extra eager steps AFTER the timed region, timed per phase with HIP events (0 = off)")
     return ap.parse_args()
@@ -155,7 +158,13 @@ def run_ps(args) -> int:
             # for a worker, apply = optimizer launch, reply = stage + sync + control answer
             "ps_us_per_msg": {k: round(v / max(1, res["applied"]) * 1e6, 1) for k, v in res["phase_s"].items()},
             "param_checksum": float(ps.fp.params.double().sum().item()),
+            "transport_used": ps.tx.name,
         }
+        comms = [None] * world
+        dist.gather_object(None, comms, dst=0)
+        # per GRAD message, per worker: push (stage + copy + announce) host us and GB/s, the
+        # wait for the PS reply, the pull copy's device us and GB/s
+        out["ps_comm"] = comms[1:]
         print(json.dumps(out), flush=True)
     else:
         from distributed_tensorflow_ibm_mnist_amd.runtime.executor import HipNet
@@ -165,15 +174,27 @@ def run_ps(args) -> int:
                               rank=0, world=1, seed=args.seed + 7919 * rank, shard=False)
         client = PSClient(net, 1, nw, rank - 1, transport=args.ps_transport)
         client.hello()
-        while not client.stop:
-            loader.next()
+
+        def compute():   # no communication inside: one hipGraph per worker step (--graph != 0)
             net.forward(defer_head=True)
             net.loss_and_grad()
             net.backward()
             weight_l2_into(net.fp)
             net.finalize(net.B, increment=False)
+
+        graph = None
+        while not client.stop:
+            loader.next()
+            if args.graph == 0:
+                compute()
+            elif graph is None:
+                from distributed_tensorflow_ibm_mnist_amd.runtime.graph import StepGraph
+                graph = StepGraph(compute, warmup=1)     # the warm-up computes this step
+            else:
+                graph.replay()
             client.push_pull()
         client.done()
+        dist.gather_object(client.comm_summary(), None, dst=0)
     dist.destroy_process_group()
     return 0
 
@@ -230,8 +251,8 @@ def main() -> int:
     # --input u8 / bf16: the first fused conv gathers the resident dataset through the
     # batch index (K10 fused into its staging); prep: one gather+normalise kernel per step
     mode = "u8" if args.fused_input else args.input
-    fused_in = args.impl == "hip" and mode != "prep" and net.bind_u8_input(
-        ds.images if mode == "u8" else ds.bf16_images())
+    fused_in = (args.impl == "hip" and mode != "prep" and getattr(net, "can_gather_input", lambda: True)()
+                and net.bind_u8_input(ds.images if mode == "u8" else ds.bf16_images()))
     loader = DeviceLoader(ds, net.x0, net.labels, rank=rank, world=world, seed=args.seed,
                           idx_out=net.idx_buf if fused_in else None)
 
@@ -292,6 +313,36 @@ def main() -> int:
         dist.all_reduce(lo, op=dist.ReduceOp.MIN)
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         in_sync = bool((hi - lo).abs().item() == 0.0)
+    comm = None
+    if collectives and args.comm_probe:     # outside the timed region, after the replica check
+        #  each bucket's all-reduce alone, then the exposed communication:
+        # eager steps with the collectives on vs off (the off steps let replicas drift:
+        # nothing after this reads the weights)
+        comm = {"buckets": dp.measure_buckets()}
+        ne = max(3, min(args.steps, 10))
+
+        def timed_eager_ms(on: bool) -> float:
+            dp.comm_enabled = on
+            for _ in range(2):
+                loader.next()
+                step_body()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t = time.perf_counter()
+            for _ in range(ne):
+                loader.next()
+                step_body()
+            torch.cuda.synchronize()
+            ms = torch.tensor([(time.perf_counter() - t) / ne * 1e3], dtype=torch.float64, device=dev)
+            if world > 1:
+                dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+            return float(ms.item())
+
+        on, off = timed_eager_ms(True), timed_eager_ms(False)
+        dp.comm_enabled = True
+        comm.update({"eager_ms_comm_on": round(on, 4), "eager_ms_comm_off": round(off, 4),
+                     "comm_exposed_ms": round(on - off, 4)})
     phases = None
     if args.phases > 0:                     # outside the timed region: per-phase breakdown of an eager step
         from distributed_tensorflow_ibm_mnist_amd.runtime.timers import PhaseTimer
@@ -338,6 +389,9 @@ def main() -> int:
             "phase_ms_eager": phases,
             "replicas_in_sync": in_sync,
             "grad_bucket_mb": [round(b.nbytes / 2 ** 20, 3) for b in dp.buckets] if world > 1 else None,
+            # per-bucket all-reduce time / bus bandwidth and the exposed communication
+            # (eager step with minus without collectives), measured after the timed steps
+            "comm": comm,
         }
         print(json.dumps(out), flush=True)
     if dist.is_initialized():

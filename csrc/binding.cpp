@@ -474,7 +474,8 @@ void splitk_reduce_multi(std::vector<Tensor> slabs, std::vector<Tensor> wdsts, s
 //   off, n, G, I, J, Ip, Jp, bf_off, wd_bits(float32 as int), track_l2, bft_off, Jt, It, 0
 void fused_optimizer(Tensor params, Tensor grads, Tensor mom, Tensor ema, Tensor bf, Tensor segs, Tensor step,
                      double lr0, double decay_rate, int64_t decay_steps, double momentum, bool nesterov,
-                     bool use_momentum, double grad_scale, double ema_max, optional<Tensor> l2) {
+                     bool use_momentum, double grad_scale, double ema_max, optional<Tensor> l2,
+                     optional<Tensor> guard, int64_t guard_want, optional<Tensor> guard_err, int64_t guard_id) {
   const int64_t total = params.numel();
   check(params, at::kFloat, total, "params");
   check(grads, at::kFloat, total, "grads");
@@ -534,6 +535,17 @@ void fused_optimizer(Tensor params, Tensor grads, Tensor mom, Tensor ema, Tensor
   op.use_momentum = use_momentum ? 1 : 0;
   op.grad_scale = (float)grad_scale;
   op.ema_max = (float)ema_max;
+  if (guard.has_value() && guard->defined()) {   // PS push guard: int64 stamp on the device
+    check(*guard, at::kLong, 1, "guard");
+    TORCH_CHECK(guard_err.has_value() && guard_err->defined(), "guard needs guard_err");
+    check(*guard_err, at::kInt, 1, "guard_err");
+    TORCH_CHECK(guard->device() == params.device() && guard_err->device() == params.device(),
+                "guard / guard_err: on the parameters' device");
+    op.guard = P<const int64_t>(*guard);
+    op.guard_want = guard_want;
+    op.guard_err = P<int>(*guard_err);
+    op.guard_id = (int)guard_id;
+  }
   hip_ok(mnistx::fused_optimizer(P<float>(params), P<const float>(grads), use_momentum ? P<float>(mom) : nullptr,
                                  ema_max >= 0 ? P<float>(ema) : nullptr, BFm(bf), sv.data(), nseg, total,
                                  P<const int64_t>(step), op, l2p, l2n, cur_stream()),
@@ -732,10 +744,17 @@ void lenet_band_fwd(Tensor x, Tensor w1, Tensor b1, int64_t b1n, Tensor w2, Tens
                     Tensor arg2, optional<Tensor> p1, optional<Tensor> arg1, optional<Tensor> idx,
                     optional<Tensor> prof) {
   mnistx::XSrc src{nullptr, nullptr, nullptr, 0};
-  check(x, at::kBFloat16, 784, "x");
-  TORCH_CHECK(x.numel() % 784 == 0 && x.numel() * 2 < (int64_t)INT32_MAX, "x: [n, 784] bf16 images, < 2 GB");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "x must be 16-byte aligned");
-  src.x = BF(x);
+  if (x.scalar_type() == at::kByte) {   // uint8 images, normalised x/255 - 0.5 in the kernel
+    check(x, at::kByte, 784, "x");
+    TORCH_CHECK(x.numel() % 784 == 0 && x.numel() < (int64_t)INT32_MAX, "x: [n, 784] uint8 images, < 2 GB");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 4 == 0, "x must be 4-byte aligned");
+    src.u8 = P<const uint8_t>(x);
+  } else {
+    check(x, at::kBFloat16, 784, "x");
+    TORCH_CHECK(x.numel() % 784 == 0 && x.numel() * 2 < (int64_t)INT32_MAX, "x: [n, 784] bf16 images, < 2 GB");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "x must be 16-byte aligned");
+    src.x = BF(x);
+  }
   src.n = (int)(x.numel() / 784);
   if (idx.has_value() && idx->defined()) {
     check(*idx, at::kLong, B, "idx");
@@ -1016,7 +1035,11 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("scale"), py::arg("h3"), py::arg("h4"), py::arg("logits"), py::arg("dl") = py::none(),
         py::arg("dh4") = py::none(), py::arg("dh3") = py::none(), py::arg("dx") = py::none(), py::arg("stats"),
         py::arg("work"), py::arg("defer_stats") = false);
-  m.def("fused_optimizer", &fused_optimizer);
+  m.def("fused_optimizer", &fused_optimizer, py::arg("params"), py::arg("grads"), py::arg("mom"), py::arg("ema"),
+        py::arg("bf"), py::arg("segs"), py::arg("step"), py::arg("lr0"), py::arg("decay_rate"),
+        py::arg("decay_steps"), py::arg("momentum"), py::arg("nesterov"), py::arg("use_momentum"),
+        py::arg("grad_scale"), py::arg("ema_max"), py::arg("l2") = py::none(), py::arg("guard") = py::none(),
+        py::arg("guard_want") = 0, py::arg("guard_err") = py::none(), py::arg("guard_id") = 0);
   m.def("fused_optimizer_blocks", [](Tensor segs) {
     TORCH_CHECK(!segs.is_cuda() && segs.scalar_type() == at::kLong && segs.dim() == 2, "segs: CPU int64 [n,14]");
     auto a = segs.accessor<int64_t, 2>();

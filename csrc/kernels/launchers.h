@@ -214,6 +214,12 @@ struct OptParams {
   int use_momentum;
   float grad_scale;      // e.g. 1/world_size
   float ema_max;         // 0.9999 ; <0 disables EMA
+  // push guard (PS mode, optional): skip the whole update unless *guard == guard_want;
+  // a skipped update writes guard_id into *guard_err
+  const int64_t* guard;
+  int64_t guard_want;
+  int* guard_err;
+  int guard_id;
 };
 
 // l2 (optional): [l2n per-tensor sums | fused_optimizer_blocks() per-block partials]

@@ -87,7 +87,8 @@ DEV int opaque(int v) {
 }
 
 struct BandFwd {
-  const bf16_t* x;        // images [n][784] bf16, normalised
+  const bf16_t* x;        // images [n][784] bf16, normalised (or null with u8)
+  const uint8_t* u8;      // images [n][784] uint8, normalised x/255 - 0.5 while staging (or null)
   const int64_t* idx;     // per-sample row of x [B]; null: sample b is row b
   int n;                  // rows in x
   const bf16_t* w1;       // [5][5][1][8]
@@ -117,22 +118,24 @@ DEV void pool_y(float keep, float send, float b, float& out, uint32_t& code) {
 // (4 pixels) r = (t & 31) + 32 i of the image's 196
 constexpr int FCH = (196 + 31) / 32;
 struct XFill {
-  u32x2 v[FCH];
+  u32x2 v[FCH];            // bf16 input: 4 pixels per chunk; uint8 input: v[i][0] = 4 pixels
   DEV void load(__amdgpu_buffer_rsrc_t rx, const BandFwd& a, int t0, int t) {
     const int gi = t0 + (t >> 5);
+    const uint32_t esz = a.u8 ? 1u : 2u;
     uint32_t base = BUF_OOB;
     if (gi < a.B && t0 >= 0) {
       int64_t row = a.idx ? a.idx[gi] : (int64_t)gi;
       row = row < 0 ? 0 : (row >= a.n ? a.n - 1 : row);
-      base = (uint32_t)row * (XIMG * 2);
+      base = (uint32_t)row * (XIMG * esz);
     }
 #pragma unroll
     for (int i = 0; i < FCH; ++i) {
       const int r = (t & 31) + 32 * i;
-      v[i] = buf_b64(rx, r < 196 ? base + 8u * r : BUF_OOB);
+      if (a.u8) v[i] = u32x2{buf_b32(rx, r < 196 ? base + 4u * r : BUF_OOB), 0u};
+      else v[i] = buf_b64(rx, r < 196 ? base + 8u * r : BUF_OOB);
     }
   }
-  DEV void store(bf16_t* xb, int t) const {
+  DEV void store(bf16_t* xb, int t, bool u8) const {
     bf16_t* im = xb + (t >> 5) * XIS + 2;
 #pragma unroll
     for (int i = 0; i < FCH; ++i) {
@@ -140,8 +143,14 @@ struct XFill {
       if (r < 196) {
         const int y = r / 7, k = r - 7 * y;
         uint32_t* d = (uint32_t*)(im + (y & 1) * XPL + (y >> 1) * XRW + 4 * k);   // 4-byte aligned
-        d[0] = v[i][0];
-        d[1] = v[i][1];
+        uint32_t lo = v[i][0], hi = v[i][1];
+        if (u8) {   // mnist_input.py:37-39 normalisation, rounded as prep_images does
+          const uint32_t b = v[i][0];
+          lo = pack2(u8_norm(b & 0xff), u8_norm((b >> 8) & 0xff));
+          hi = pack2(u8_norm((b >> 16) & 0xff), u8_norm(b >> 24));
+        }
+        d[0] = lo;
+        d[1] = hi;
       }
     }
   }
@@ -192,7 +201,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) bias1[i] = i + 4 * h < a.b1n ? a.b1[i + 4 * h] : 0.f;
     const uint32_t d0 = 2u * ypar, d1 = d0 + 1u;     // argmax codes of this lane's x parities
-    const auto rx = buf_rsrc(a.x, (uint32_t)a.n * (XIMG * 2));
+    const auto rx = a.u8 ? buf_rsrc(a.u8, (uint32_t)a.n * XIMG) : buf_rsrc(a.x, (uint32_t)a.n * (XIMG * 2));
     // input rows of a unit: row = S + rlane with S = yp0 + p - 1 (uniform) and the lane's
     // dy parity h / row half; plane (ypar + h) & 1
     const int rlane = 7 * half + ((ypar + h) >> 1);
@@ -201,7 +210,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
     const int plane_off = img * PIS + ypar * 8 + 4 * h;
     XFill xf;
     xf.load(rx, a, nk > 0 ? tile0(0) : -1, t);
-    xf.store(xs, t);     // ring slot 0 (only this role reads the input ring; ordered by the first barrier)
+    xf.store(xs, t, a.u8 != nullptr);     // ring slot 0 (only this role reads the input ring; ordered by the first barrier)
 
     uint64_t busy = 0, wait = 0, tw = __builtin_amdgcn_s_memtime();
     for (int k = 0; k <= nk; ++k) {
@@ -282,7 +291,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
           acca = window(fa);
           epilogue(accb, j + 1);
         }
-        xf.store(xs + ((k + 1) & 1) * XBUF, t);   // tile k+1's input (slot read in iteration k-1)
+        xf.store(xs + ((k + 1) & 1) * XBUF, t, a.u8 != nullptr);   // tile k+1's input (slot read in iteration k-1)
       }
       tw = __builtin_amdgcn_s_memtime();
       busy += tw - tb;
@@ -429,8 +438,8 @@ hipError_t lenet_band_fwd(const XSrc& x, const bf16_t* w1, const float* b1, int 
                           const float* b2, int B, bf16_t* p1, uint8_t* arg1, bf16_t* p2, uint8_t* arg2,
                           hipStream_t st, unsigned long long* prof) {
   if (B <= 0) return hipSuccess;
-  if (!x.x || x.u8) return hipErrorInvalidValue;   // bf16 images only
-  BandFwd a{x.x, x.idx, x.idx ? x.n : B, w1, b1, b1n, w2, b2, B, p1, arg1, p2, arg2, prof};
+  if (!x.x && !x.u8) return hipErrorInvalidValue;
+  BandFwd a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, w1, b1, b1n, w2, b2, B, p1, arg1, p2, arg2, prof};
   const int ntiles = (B + BT - 1) / BT;
   if (p1) {
     const int grid = fwd_grid<true>(ntiles);

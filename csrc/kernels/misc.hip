@@ -695,6 +695,10 @@ __global__ __launch_bounds__(TPB) void fused_opt_k(float* __restrict__ params, c
                                                    const int64_t* __restrict__ step_p, OptParams op,
                                                    float* __restrict__ l2) {
   __shared__ float red[TPB / 64];
+  if (op.guard && *op.guard != op.guard_want) {   // a stale / torn PS push: never applied
+    if (blockIdx.x == 0 && threadIdx.x == 0) *op.guard_err = op.guard_id;
+    return;
+  }
   int si = 0;
   while (si + 1 < tab.n && (int)blockIdx.x >= tab.blk0[si + 1]) ++si;
   const OptSeg sg = tab.s[si];

@@ -86,20 +86,23 @@ class DataParallel:
         self.trigger = {b.layers[-1]: b for b in self.buckets}
         self.pending: list = []
         self.overlap = overlap
+        # comm_enabled = False skips the all-reduces (replicas drift apart): only for
+        # measuring how much of a step the collectives leave exposed (bench.py)
+        self.comm_enabled = True
         if self.active:
             net.grad_ready_hooks.append(self._hook)
             if hasattr(net, "hook_layers"):       # reduced gradients are needed only at bucket triggers
                 net.hook_layers = set(self.trigger)
 
     def _hook(self, layer_index: int) -> None:
-        if not self.overlap:
+        if not self.overlap or not self.comm_enabled:
             return
         b = self.trigger.get(layer_index)
         if b is not None:
             self.pending.append(dist.all_reduce(self.net.fp.grads[b.start:b.end], group=self.group, async_op=True))
 
     def sync_grads(self) -> None:
-        if not self.active:
+        if not self.active or not self.comm_enabled:
             return
         if not self.overlap:
             for b in self.buckets:
@@ -131,6 +134,41 @@ class DataParallel:
         net.update(grad_scale=1.0 / self.world)
         timer.mark("update")
         timer.close()
+
+    def measure_buckets(self, reps: int = 20, warmup: int = 3) -> List[Dict[str, float]]:
+        """Each gradient bucket's all-reduce ALONE (outside any step): mean time of
+        ``reps`` back-to-back all-reduces of a scratch copy of the bucket, host-timed
+        between device synchronisations and a barrier; ring bus bandwidth
+        busbw = 2(N-1)/N * bytes / t (the per-link figure to compare with xGMI's
+        ~153 GB/s), algbw = bytes / t.  Collective: every rank calls it."""
+        import time
+        out = []
+        if not self.active:
+            return out
+        dev = self.net.fp.grads.device
+        n = self.world
+        for b in self.buckets:
+            buf = self.net.fp.grads[b.start:b.end].clone()
+            for _ in range(warmup):
+                dist.all_reduce(buf, group=self.group)
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            dist.barrier(group=self.group)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                dist.all_reduce(buf, group=self.group)
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            t = (time.perf_counter() - t0) / reps
+            tt = torch.tensor([t], dtype=torch.float64, device=dev if dist.get_backend(self.group) == "nccl" else "cpu")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=self.group)     # the slowest rank's view
+            t = float(tt.item())
+            out.append({"mb": round(b.nbytes / 2 ** 20, 4),
+                        "layers": [self.net.spec.layers[i].name for i in b.layers],
+                        "allreduce_us": round(t * 1e6, 2),
+                        "busbw_GBps": round(2 * (n - 1) / n * b.nbytes / t / 1e9, 3),
+                        "algbw_GBps": round(b.nbytes / t / 1e9, 3)})
+        return out
 
     def broadcast_state(self, src: int = 0) -> None:
         """Make every replica start from the chief's parameters / slots / step."""

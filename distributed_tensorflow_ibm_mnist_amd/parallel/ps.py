@@ -45,6 +45,20 @@ MI355X realisation -- ONE serve loop, two planes:
   from the parameters its forward used, so logged ``total_loss`` and the
   ``*/weight_loss/avg`` EMAs include them in PS mode too.
 
+Push integrity (both transports): every gradient slice travels with an int64
+sequence stamp in its last 8 bytes -- the worker's local step, also announced in
+the control word.  The host transport checks it on arrival; the ``ipc`` PS hands
+the mailbox's stamp and the expected value to the fused K9 kernel, which skips
+the update on a mismatch and records the worker in an error word the PS reads
+after its reply sync.  A stale, misdirected or torn push is never applied: the
+PS raises ``PushIntegrityError`` naming the worker (fault injection:
+``MNIST_FI_CORRUPT_PUSH=worker:local_step``).
+
+``ipc`` needs peer access between every worker GPU and every PS GPU
+(``torch.cuda.can_device_access_peer``); the transport is agreed collectively,
+and a cluster where any pair lacks it falls back to ``host`` with the reason
+logged (``MNISTX_PS_STRICT=1`` makes that an error).
+
 Control words (int64[8]) worker -> PS: (kind, want_state, worker_local_step);
 PS -> worker: (global_step, stop, applied).
 """
@@ -95,6 +109,26 @@ def _sync(t: torch.Tensor) -> None:
         torch.cuda.current_stream(t.device).synchronize()
 
 
+class PushIntegrityError(RuntimeError):
+    """A gradient push whose sequence stamp does not match its control word."""
+
+
+def slot_len(n: int) -> int:
+    """Elements of one push slot: the slice padded to an even count + an int64 stamp."""
+    return (n + 1) // 2 * 2 + 2
+
+
+def stamp_view(slot: torch.Tensor) -> torch.Tensor:
+    """The int64 stamp in the last 8 bytes of a push slot (1-D float32 view)."""
+    return slot[-2:].view(torch.int64)
+
+
+def corrupt_push_at() -> Tuple[int, int]:
+    """MNIST_FI_CORRUPT_PUSH=worker:local_step -> that push carries a wrong stamp."""
+    v = os.environ.get("MNIST_FI_CORRUPT_PUSH", "")
+    return tuple(int(x) for x in v.split(":")) if ":" in v else (-1, -1)
+
+
 # ---------------------------------------------------------------------------- transports
 class HostTransport:
     """Slices travel as gloo messages on the control group (tag TAG_DATA)."""
@@ -117,11 +151,25 @@ class HostTransport:
     # -- PS side
     def ps_setup(self, ps, is_me: bool) -> None:
         if is_me:
+            n = ps.fp.total
+            self.n = n
+            self.slot = torch.zeros(slot_len(n), dtype=torch.float32)     # host staging: checked on arrival
             self.grad_in = torch.zeros_like(ps.fp.grads)
 
-    def ps_take_grads(self, ps, r: int) -> torch.Tensor:
-        self._recv(self.grad_in, r)
+    def ps_take_grads(self, ps, r: int, expect: int) -> torch.Tensor:
+        dist.recv(self.slot, r, group=self.g, tag=TAG_DATA)
+        got = int(stamp_view(self.slot))
+        if got != expect:
+            raise PushIntegrityError(f"PS {ps.j}: push from worker {r - self.k} carries stamp {got}, its control "
+                                     f"word announced {expect}: gradient rejected")
+        self.grad_in.copy_(self.slot[:self.n])
         return self.grad_in
+
+    def ps_guard(self, r: int, expect: int):
+        return None               # checked on the host in ps_take_grads
+
+    def ps_check(self, ps, final: bool = False) -> None:
+        pass
 
     def ps_stage_reply(self, ps, r: int, want_state: bool) -> None:
         pass
@@ -141,7 +189,7 @@ class HostTransport:
 
     def worker_after_ctrl(self, j: int, kind: int, grads: Optional[torch.Tensor]) -> None:
         if kind == GRAD:
-            self._send(grads, j)
+            self._send(grads, j)          # the stamped slot (PSClient._stage)
 
     def worker_pull(self, j: int, params: torch.Tensor, ema: torch.Tensor, mom: torch.Tensor, state: bool) -> None:
         self._recv(params, j)
@@ -151,7 +199,15 @@ class HostTransport:
 
 
 class IpcTransport:
-    """One-sided xGMI peer copies into / out of PS-owned device buffers."""
+    """One-sided xGMI peer copies into / out of PS-owned device buffers.
+
+    Per worker the PS exports a stamped gradient mailbox, a parameter reply slot and
+    an optimizer-state slot.  The PS answers once an event recorded after the reply
+    copy has completed (an event sync on that copy, not a stream-wide sync).  Inter-
+    process events -- the worker's stream waiting on the PS's event instead -- were
+    measured and rejected: on this runtime the waiting stream is released ~68 ms after
+    the producer's work completes (``bench/ipc_event_probe.py``,
+    ``profiles/r3/ps/ipc_event_probe.txt``)."""
     name = "ipc"
 
     def __init__(self, group, num_ps: int, num_workers: int):
@@ -165,9 +221,14 @@ class IpcTransport:
             obj = [None]
             if is_me and ps.j == j:
                 n, dev = ps.fp.total, ps.fp.params.device
-                self.grad_in = torch.zeros(self.W, n, dtype=torch.float32, device=dev)
+                self.n = n
+                self.grad_in = torch.zeros(self.W, slot_len(n), dtype=torch.float32, device=dev)
                 self.reply = torch.zeros(self.W, n, dtype=torch.float32, device=dev)
-                self.state = torch.zeros(2, n, dtype=torch.float32, device=dev)
+                self.state = torch.zeros(self.W, 2, n, dtype=torch.float32, device=dev)   # one slot per worker
+                # K9 guard: error word (device) + its pinned host mirror, refreshed by an async copy
+                self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+                self.err_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+                self.err_ev = torch.cuda.Event()
                 torch.cuda.synchronize(dev)
                 obj = [{k: reduce_tensor(t) for k, t in
                         (("grad_in", self.grad_in), ("reply", self.reply), ("state", self.state))}]
@@ -175,16 +236,32 @@ class IpcTransport:
             if ps is None:                          # a worker maps every PS's buffers
                 self.peer[j] = {k: fn(*args) for k, (fn, args) in obj[0].items()}
 
-    def ps_take_grads(self, ps, r: int) -> torch.Tensor:
-        return self.grad_in[r - self.k]          # the worker wrote it before announcing
+    def ps_take_grads(self, ps, r: int, expect: int) -> torch.Tensor:
+        return self.grad_in[r - self.k, :self.n]   # the worker wrote it before announcing
+
+    def ps_guard(self, r: int, expect: int):
+        """(stamp pointer tensor, expected, error word, id) for the K9 kernel's check."""
+        return stamp_view(self.grad_in[r - self.k]), expect, self.err, r - self.k + 1
 
     def ps_stage_reply(self, ps, r: int, want_state: bool) -> None:
         i = r - self.k
         self.reply[i].copy_(ps.fp.params)
         if want_state:
-            self.state[0].copy_(ps.fp.ema)
-            self.state[1].copy_(ps.fp.mom)
-        _sync(self.reply)                         # visible to the worker before the ctrl reply
+            self.state[i, 0].copy_(ps.fp.ema)
+            self.state[i, 1].copy_(ps.fp.mom)
+        self.err_host.copy_(self.err, non_blocking=True)
+        self.err_ev.record()
+        self.err_ev.synchronize()                 # reply + error word landed before the ctrl reply
+
+    def ps_check(self, ps, final: bool = False) -> None:
+        """A push the K9 guard rejected (never applied) is a hard error naming the worker,
+        raised at the reply that follows it (the error word's host mirror is current)."""
+        if final:
+            self.err_ev.synchronize()
+        bad = int(self.err_host[0])
+        if bad:
+            raise PushIntegrityError(f"PS {ps.j}: push from worker {bad - 1} failed its sequence-stamp check "
+                                     f"(stale or torn mailbox): gradient not applied")
 
     def ps_after_ctrl(self, ps, r: int, want_state: bool) -> None:
         pass
@@ -194,7 +271,7 @@ class IpcTransport:
 
     def worker_before_ctrl(self, j: int, kind: int, grads: Optional[torch.Tensor]) -> None:
         if kind == GRAD:
-            self.peer[j]["grad_in"][self.wi].copy_(grads)
+            self.peer[j]["grad_in"][self.wi].copy_(grads)   # the stamped slot (PSClient._stage)
             _sync(grads)                          # landed in the PS's HBM before we announce it
 
     def worker_after_ctrl(self, j: int, kind: int, grads: Optional[torch.Tensor]) -> None:
@@ -203,8 +280,8 @@ class IpcTransport:
     def worker_pull(self, j: int, params: torch.Tensor, ema: torch.Tensor, mom: torch.Tensor, state: bool) -> None:
         params.copy_(self.peer[j]["reply"][self.wi])
         if state:
-            ema.copy_(self.peer[j]["state"][0])
-            mom.copy_(self.peer[j]["state"][1])
+            ema.copy_(self.peer[j]["state"][self.wi, 0])
+            mom.copy_(self.peer[j]["state"][self.wi, 1])
 
 
 def make_transport(name: str, group, num_ps: int, num_workers: int):
@@ -215,8 +292,41 @@ def make_transport(name: str, group, num_ps: int, num_workers: int):
     raise ValueError(f"unknown PS transport {name!r} (ipc | host)")
 
 
-def setup_transport(name: str, group, num_ps: int, num_workers: int, ps=None):
-    """Collective: every PS and worker rank calls this once, in the same order."""
+def ipc_reachable(group, num_ps: int, device) -> Tuple[bool, str]:
+    """Collective: can every worker GPU map and copy every PS GPU's memory?
+    Ranks 0..k-1 are the PS tasks; each rank reports its device, each worker checks
+    ``can_device_access_peer`` towards every PS device, and the verdict is agreed."""
+    dev = torch.device(device)
+    mine = dev.index if dev.type == "cuda" else -1
+    devs = [None] * dist.get_world_size(group)
+    dist.all_gather_object(devs, mine, group=group)
+    me = dist.get_rank(group)
+    reason = ""
+    if mine < 0 or any(d is None or d < 0 for d in devs):
+        reason = "a rank is not on a GPU"
+    elif me >= num_ps:
+        for j in range(num_ps):
+            if devs[j] != mine and not torch.cuda.can_device_access_peer(mine, devs[j]):
+                reason = f"worker GPU {mine} has no peer access to PS {j}'s GPU {devs[j]}"
+                break
+    flag = torch.tensor([0 if reason else 1], dtype=torch.int64)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    if int(flag) == 0 and not reason:
+        reason = "another rank lacks peer access to a PS GPU"
+    return bool(int(flag)), reason
+
+
+def setup_transport(name: str, group, num_ps: int, num_workers: int, ps=None, device=None, log=print):
+    """Collective: every PS and worker rank calls this once, in the same order.
+    ``ipc`` is downgraded to ``host`` (reason logged) unless every worker can reach
+    every PS GPU; ``MNISTX_PS_STRICT=1`` raises instead."""
+    if name == "ipc":
+        ok, why = ipc_reachable(group, num_ps, device if device is not None else torch.device("cpu"))
+        if not ok:
+            if os.environ.get("MNISTX_PS_STRICT", "0") == "1":
+                raise RuntimeError(f"PS ipc transport unavailable: {why}")
+            log(f"[ps] ipc data plane unavailable ({why}): using the host transport")
+            name = "host"
     tx = make_transport(name, group, num_ps, num_workers)
     tx.ps_setup(ps, ps is not None)
     return tx
@@ -258,18 +368,22 @@ class ParameterServer:
         self.rejected = 0
         self.per_worker = [0] * num_workers
         self.arrivals: List[int] = []            # worker index of every applied push, in order
-        self.tx = setup_transport(transport or default_transport(self.device), group, num_ps, num_workers, ps=self)
+        self.tx = setup_transport(transport or default_transport(self.device), group, num_ps, num_workers, ps=self,
+                                  device=self.device, log=log)
         # global-step values at which serve() records a wall-clock mark (bench.py --mode ps)
         self.marks: Dict[int, float] = {}
 
-    def _apply(self, grads: torch.Tensor) -> None:
+    def _apply(self, grads: torch.Tensor, guard=None) -> None:
         fp = self.fp
         if self.device.type == "cuda":
             from ..ops._ext import kernels
             o = self.opt
+            gk = {}
+            if guard is not None:    # the kernel skips the update if the mailbox stamp != expected
+                gk = dict(guard=guard[0], guard_want=guard[1], guard_err=guard[2], guard_id=guard[3])
             kernels().fused_optimizer(fp.params, grads, fp.mom, fp.ema, fp.bf16, fp.segs, fp.step, o.lr0,
                                       o.decay_rate, o.decay_steps, o.momentum, o.nesterov, o.use_momentum, 1.0,
-                                      o.ema_max, None)
+                                      o.ema_max, None, **gk)
         else:
             from ..runtime.torchnet import torch_update
             if grads is not fp.grads:
@@ -279,6 +393,7 @@ class ParameterServer:
 
     def _reply(self, r: int, want_state: bool) -> None:
         self.tx.ps_stage_reply(self, r, want_state)
+        self.tx.ps_check(self)
         c = torch.zeros(CTRL, dtype=torch.int64)
         c[0] = self.global_step
         c[1] = int(self.global_step >= self.max_steps)
@@ -302,14 +417,14 @@ class ParameterServer:
             r = dist.recv(c, group=self.group, tag=TAG_CTRL)     # any source: the next worker to arrive
             tb = clk()
             ph["idle"] += tb - ta
-            kind, want_state = int(c[0]), bool(c[1])
+            kind, want_state, wstep = int(c[0]), bool(c[1]), int(c[2])
             if kind == DONE:
                 done.add(r)
                 continue
             if kind == GRAD:
-                g = self.tx.ps_take_grads(self, r)
+                g = self.tx.ps_take_grads(self, r, wstep)
                 if self.global_step < self.max_steps:
-                    self._apply(g)
+                    self._apply(g, self.tx.ps_guard(r, wstep))
                     self.global_step += 1
                     self.fp.step.fill_(self.global_step)
                     self.applied += 1
@@ -329,6 +444,7 @@ class ParameterServer:
                 if self.device.type == "cuda":
                     torch.cuda.synchronize(self.device)
                 self.marks[self.global_step] = time.perf_counter()
+        self.tx.ps_check(self, final=True)
         dt = time.perf_counter() - t0
         self.log(f"[ps {self.j}] done: applied {self.applied} update(s), per worker {self.per_worker}, "
                  f"rejected {self.rejected}, global_step {self.global_step}, {self.applied / max(dt, 1e-9):.1f} "
@@ -348,29 +464,88 @@ class PSClient:
         self.ranges = shard_ranges(net.fp, num_ps)
         self.global_step = 0
         self.stop = False
-        self.tx = setup_transport(transport or default_transport(net.fp.params.device), group, num_ps, num_workers)
+        dev = net.fp.params.device
+        self.tx = setup_transport(transport or default_transport(dev), group, num_ps, num_workers, device=dev)
         self.tx.worker_open(worker_index, self.ranges)
         self.local_step = 0
+        # one stamped push slot per PS shard: the slice + its int64 sequence stamp, sent as ONE message
+        # (host) / ONE peer copy (ipc)
+        stage_dev = dev if self.tx.name == "ipc" else torch.device("cpu")
+        self.slots = [torch.zeros(slot_len(b - a), dtype=torch.float32, device=stage_dev) for a, b, _ in self.ranges]
+        self._corrupt = corrupt_push_at()
+        # data-plane accounting (bench.py --mode ps): host seconds and bytes of the GRAD
+        # exchanges; push = stage + copy/send + announce to every PS, pull = wait for the
+        # replies + copy the parameters back (so it includes the PS's service time)
+        self.comm = {"push_s": 0.0, "reply_wait_s": 0.0, "push_bytes": 0, "pull_bytes": 0, "msgs": 0}
+        self._pull_ev: List[Tuple] = []      # (start, end) CUDA events around the pull copies
+
+    def _stage(self, j: int, a: int, b: int) -> torch.Tensor:
+        slot = self.slots[j]
+        slot[:b - a].copy_(self.net.fp.grads[a:b])
+        stamp = self.local_step
+        if self._corrupt == (self.wi, self.local_step):
+            stamp += 1000                                   # fault injection: a stale-looking push
+        stamp_view(slot).fill_(stamp)
+        return slot
 
     def _exchange(self, kind: int, want_state: bool = False) -> None:
         fp = self.net.fp
+        t0 = time.perf_counter()
         # announce to every PS first (they work in parallel), then collect the replies
         for j, (a, b, _) in enumerate(self.ranges):
-            g = fp.grads[a:b] if kind == GRAD else None
+            g = self._stage(j, a, b) if kind == GRAD else None
             self.tx.worker_before_ctrl(j, kind, g)
             c = torch.zeros(CTRL, dtype=torch.int64)
             c[0], c[1], c[2] = kind, int(want_state), self.local_step
             dist.send(c, j, group=self.group, tag=TAG_CTRL)
             self.tx.worker_after_ctrl(j, kind, g)
+        t1 = time.perf_counter()
+        wait = 0.0
+        evs = None
+        if kind == GRAD and fp.params.is_cuda and len(self._pull_ev) < 4096:
+            evs = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         for j, (a, b, _) in enumerate(self.ranges):
             r = torch.zeros(CTRL, dtype=torch.int64)
+            tw = time.perf_counter()
             dist.recv(r, j, group=self.group, tag=TAG_CTRL)
+            wait += time.perf_counter() - tw
+            if evs is not None and j == 0:
+                evs[0].record()
             self.tx.worker_pull(j, fp.params[a:b], fp.ema[a:b], fp.mom[a:b], want_state)
             if j == 0:
                 self.global_step = int(r[0])
                 self.stop = bool(r[1])
+        if kind == GRAD:
+            if evs is not None:
+                evs[1].record()
+                self._pull_ev.append(evs)
+            c = self.comm
+            c["push_s"] += t1 - t0
+            c["reply_wait_s"] += wait
+            c["push_bytes"] += sum(sl.numel() * 4 for sl in self.slots)
+            c["pull_bytes"] += fp.total * 4
+            c["msgs"] += 1
         fp.step.fill_(self.global_step)
         fp.refresh_bf16()
+
+    def comm_summary(self) -> Dict[str, float]:
+        """Per GRAD message: push host us (stage + copy + announce) and its GB/s, the wait
+        for the PS reply, the pull copy's device us (events) and its GB/s."""
+        c = self.comm
+        n = max(1, c["msgs"])
+        if self._pull_ev:
+            torch.cuda.synchronize()
+            pull_ms = sum(a.elapsed_time(b) for a, b in self._pull_ev) / len(self._pull_ev)
+        else:
+            pull_ms = float("nan")
+        push_us = c["push_s"] / n * 1e6
+        pull_us = pull_ms * 1e3
+        return {"msgs": c["msgs"], "push_us": round(push_us, 1),
+                "push_GBps": round(c["push_bytes"] / n / max(push_us, 1e-9) / 1e3, 3),
+                "reply_wait_us": round(c["reply_wait_s"] / n * 1e6, 1),
+                "pull_us": round(pull_us, 1),
+                "pull_GBps": round(c["pull_bytes"] / n / max(pull_us, 1e-9) / 1e3, 3) if pull_us == pull_us else None,
+                "bytes_per_push": c["push_bytes"] // n, "bytes_per_pull": c["pull_bytes"] // n}
 
     def hello(self) -> None:
         self._exchange(HELLO)
@@ -437,14 +612,27 @@ class PSWorkerReplica:
     def sync_step_from_device(self) -> None:
         pass
 
-    def step(self) -> None:
+    def _compute(self) -> None:
+        """forward + CE + backward + L2 terms + stats: no communication, so one hipGraph."""
         net = self.net
-        self.loader.next()
         net.forward(defer_head=True)
         net.loss_and_grad()
         net.backward()
         weight_l2_into(net.fp)
         net.finalize(net.B, increment=False)
+
+    _graph = None
+
+    def step(self) -> None:
+        self.loader.next()
+        if getattr(self.base, "use_graph", False):
+            if self._graph is None:
+                from ..runtime.graph import StepGraph
+                self._graph = StepGraph(self._compute, warmup=1)   # the warm-up computes this step
+            else:
+                self._graph.replay()
+        else:
+            self._compute()
         if self._sleep:
             time.sleep(self._sleep)
         self.client.push_pull()

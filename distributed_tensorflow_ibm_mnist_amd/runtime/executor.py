@@ -543,9 +543,9 @@ class HipNet:
                     b.lrn_pre = (a.spec, a.x)
                     a.skip_fwd = True
                     self.fold_lrn_fwd = True
-        # LeNet-5: conv1+pool1+conv2+pool2 forward as ONE banded-MFMA kernel (lenet_band.hip),
-        # bf16 inputs only (x0 or the bf16 resident dataset); MNISTX_BAND_FWD=0 runs the two
-        # convpool kernels instead
+        # LeNet-5: conv1+pool1+conv2+pool2 forward as ONE banded-MFMA kernel (lenet_band.hip)
+        # on x0 or the resident dataset (bf16, or uint8 normalised while staging);
+        # MNISTX_BAND_FWD=0 runs the two convpool kernels instead
         self.band_fwd = self._find_c2d_c1w() and os.environ.get("MNISTX_BAND_FWD", "1") != "0"
         if self.fuse_c2d_c1w:
             l0, l1 = self.layers[0], self.layers[1]
@@ -595,6 +595,13 @@ class HipNet:
         if defer:
             self._ce_defer_blocks = kernels().mlp_head_blocks(nb)
 
+    def can_gather_input(self) -> bool:
+        """Whether ``bind_u8_input`` would accept a resident dataset (checked BEFORE the
+        caller builds a normalised bf16 copy of it)."""
+        first = self.layers[0]
+        return (isinstance(first, ConvPoolLayer) and self.spec.in_channels == 1
+                and bool(kernels().convpool_u8_input(*first._geo())))
+
     def bind_u8_input(self, images: torch.Tensor) -> bool:
         """Training steps read a resident dataset [n, H*W] directly through ``idx_buf``
         (filled by DeviceLoader(idx_out=...)), fusing the gather (K10,
@@ -630,7 +637,7 @@ class HipNet:
             first.use_u8 = first.u8 is not None and not from_x0
         stop = self.head if (defer_head and self.head is not None) else len(self.layers)
         start = 0
-        if self.band_fwd and stop >= 2 and not (first.use_u8 and first.u8[0].dtype == torch.uint8):
+        if self.band_fwd and stop >= 2:
             self._band_forward(nb)
             start = 2
         for lay in self.layers[start:stop]:
@@ -643,8 +650,8 @@ class HipNet:
         outputs and argmax codes in the convpool layouts the backward kernels read."""
         l0, l1 = self.layers[0], self.layers[1]
         fp = self.fp
-        src = l0._src()
-        kernels().lenet_band_fwd(l0._xin(), fp.bf16_view(l0.wname), fp.param_view(l0.bname), l0.spec.cout,
+        src = l0._src()   # {} (x0) | {"idx"} (bf16 dataset = _xin()) | {"u8", "idx"} (uint8 dataset)
+        kernels().lenet_band_fwd(src.get("u8", l0._xin()), fp.bf16_view(l0.wname), fp.param_view(l0.bname), l0.spec.cout,
                                  fp.bf16_view(l1.wname), fp.param_view(l1.bname), nb, l1.out, l1.arg,
                                  p1=l0.out, arg1=l0.arg, idx=src.get("idx"))
 

@@ -214,6 +214,9 @@ class HipNetF32:
     finalize = HipNet.finalize
     read_stats = HipNet.read_stats
 
+    def can_gather_input(self) -> bool:
+        return False
+
     def bind_u8_input(self, images_u8: torch.Tensor) -> bool:
         return False
 

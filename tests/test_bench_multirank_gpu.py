@@ -36,3 +36,27 @@ def test_bench_torchrun_two_ranks_one_gpu(model, batch):
     assert out["replicas_in_sync"] is True
     assert out["grad_bucket_mb"] and out["value"] > 0
     assert out["final_train_loss"] == out["final_train_loss"]     # not NaN
+    # communication evidence for the scaling run: every bucket's all-reduce
+    # alone and the exposed communication of an eager step
+    comm = out["comm"]
+    assert len(comm["buckets"]) == len(out["grad_bucket_mb"])
+    for b in comm["buckets"]:
+        assert b["allreduce_us"] > 0 and b["busbw_GBps"] > 0 and b["algbw_GBps"] > 0 and b["layers"]
+    assert comm["eager_ms_comm_on"] > 0 and comm["eager_ms_comm_off"] > 0
+    assert "comm_exposed_ms" in comm
+
+
+def test_bench_one_rank_rccl_comm_probe():
+    """The RCCL path on one GPU (--force_collectives 1): the per-bucket all-reduce probe
+    and the exposed-communication measurement run on a real RCCL process group."""
+    port = str(29800 + (os.getpid() % 50))
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "6", "--warmup", "2", "--batch", "4096",
+           "--force_collectives", "1", "--phases", "0", "--graph", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT,
+                       env={**os.environ, "OMP_NUM_THREADS": "2", "MASTER_PORT": port})
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    comm = out["comm"]
+    assert comm is not None and len(comm["buckets"]) >= 1
+    assert all(b["allreduce_us"] > 0 and b["algbw_GBps"] > 0 for b in comm["buckets"])
+    assert comm["eager_ms_comm_on"] > 0 and comm["eager_ms_comm_off"] > 0

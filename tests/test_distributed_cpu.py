@@ -289,6 +289,55 @@ def test_ps_async_arrival_order_slow_worker(tmp_path):
     assert "transport host" in logs["ps0"]
 
 
+def test_ps_push_stamp_helpers():
+    """A push slot = the slice padded to an even length + an int64 stamp in its last 8 bytes."""
+    from distributed_tensorflow_ibm_mnist_amd.parallel.ps import slot_len, stamp_view
+    for n in (1, 2, 7, 61706):
+        L = slot_len(n)
+        assert L >= n + 2 and L % 2 == 0
+        slot = torch.zeros(L)
+        stamp_view(slot).fill_(123456789012)
+        assert int(stamp_view(slot)) == 123456789012 and slot[:n].abs().sum() == 0   # stamp never overlaps data
+
+
+def test_ps_corrupt_push_is_rejected_and_names_worker(tmp_path):
+    """Push integrity (host transport): worker 1's 5th push carries a wrong sequence
+    stamp (MNIST_FI_CORRUPT_PUSH=1:5); the PS rejects it BEFORE applying it and exits
+    non-zero naming that worker; the workers do not hang."""
+    base = free_port()
+    ps_hosts = f"localhost:{base}"
+    wk_hosts = ",".join(f"localhost:{base + 100 + i}" for i in range(2))
+    d = str(tmp_path / "train")
+    common = ["--impl=torch", "--cpu", "--model=mlp", "--in_channels=1", "--batch_size=16", "--max_steps=40",
+              "--test_interval=1000", "--log_step_count_steps=0", "--train_data=synthetic://600",
+              "--test_data=synthetic://100?seed=1", f"--train_dir={d}", f"--ps_hosts={ps_hosts}",
+              f"--worker_hosts={wk_hosts}", "--save_checkpoint_secs=0", "--eval_examples=100",
+              "--collective_timeout=60"]
+    os.environ["MNIST_FI_CORRUPT_PUSH"] = "1:5"
+    try:
+        procs = [("ps0", _spawn_main(common + ["--job_name=ps", "--task_id=0"], tmp_path / "ps0.log"))]
+        for i in range(2):
+            procs.append((f"w{i}", _spawn_main(common + ["--job_name=worker", f"--task_id={i}"],
+                                               tmp_path / f"w{i}.log")))
+    finally:
+        del os.environ["MNIST_FI_CORRUPT_PUSH"]
+    t0 = time.time()
+    for name, p in procs:
+        try:
+            p.wait(timeout=max(5, 200 - (time.time() - t0)))
+        except subprocess.TimeoutExpired:
+            for _, q in procs:
+                q.kill()
+            pytest.fail(f"{name} hung:\n" + open(tmp_path / f"{name}.log").read()[-3000:])
+    logs = {n: open(tmp_path / f"{n}.log").read() for n, _ in procs}
+    assert procs[0][1].returncode != 0, logs["ps0"][-2000:]
+    assert "PushIntegrityError" in logs["ps0"] and "push from worker 1 carries stamp 1005" in logs["ps0"], \
+        logs["ps0"][-2000:]
+    assert "announced 5" in logs["ps0"]
+    for n, p in procs[1:]:
+        assert p.returncode is not None            # no hang: the workers fail once the PS is gone
+
+
 def test_ps_worker_weight_loss_terms():
     """PS workers run no local optimizer; the weight-decay loss terms still enter
     total_loss (mnist_input.py:112-114,231) via ps.weight_l2_into."""

@@ -128,3 +128,24 @@ def test_bench_ps_mode_json(dev):
     assert d["value"] > 0 and sum(d["applied_per_worker"]) == 24
     # serve-loop phase split (host us per applied update)
     assert set(d["ps_us_per_msg"]) == {"idle", "apply", "reply"} and d["ps_us_per_msg"]["apply"] > 0
+    # data plane per GRAD message, per worker: push / pull us and GB/s
+    assert len(d["ps_comm"]) == 2 and d["transport_used"] == "ipc"
+    for c in d["ps_comm"]:
+        assert c["msgs"] >= 1 and c["push_us"] > 0 and c["push_GBps"] > 0 and c["pull_us"] > 0
+        assert c["bytes_per_push"] >= c["bytes_per_pull"] > 0          # the push carries the 8-byte stamp
+
+
+@pytest.mark.timeout(300)
+def test_ps_ipc_corrupt_push_aborts_naming_worker(dev):
+    """Push integrity on the device data plane: worker 0's 4th push carries a wrong
+    sequence stamp (MNIST_FI_CORRUPT_PUSH=0:4); the fused K9 kernel skips it and the
+    PS aborts with an error naming worker 0 (a stale / torn gradient is never applied
+    silently)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.join(ROOT, "bench.py"),
+           "--mode", "ps", "--ps_transport", "ipc", "--batch", "256", "--steps", "20", "--warmup", "2"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, OMP_NUM_THREADS="2", MNIST_FI_CORRUPT_PUSH="0:4"))
+    out = r.stdout + r.stderr
+    assert r.returncode != 0, out[-3000:]
+    assert "PushIntegrityError" in out and "push from worker 0 failed its sequence-stamp check" in out, out[-3000:]

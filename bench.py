@@ -119,6 +119,9 @@ def run_ps(args) -> int:
     from distributed_tensorflow_ibm_mnist_amd.data.synthetic import make_synthetic
     from distributed_tensorflow_ibm_mnist_amd.data.device_loader import DeviceDataset, DeviceLoader
 
+    # one hardware queue per PS/worker process (before HIP starts): co-located tasks
+    # otherwise oversubscribe the GPU's queue scheduler (profiles/r3/ps/ps_hwq_ab.txt)
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("MNISTX_PS_HW_QUEUES", "1")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -183,7 +186,10 @@ def run_ps(args) -> int:
             net.finalize(net.B, increment=False)
 
         graph = None
+        evs = []       # device time of the worker's own step (input + fwd/bwd), shared GPU included
         while not client.stop:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
             loader.next()
             if args.graph == 0:
                 compute()
@@ -192,9 +198,15 @@ def run_ps(args) -> int:
                 graph = StepGraph(compute, warmup=1)     # the warm-up computes this step
             else:
                 graph.replay()
+            ev[1].record()
+            if (graph is not None or args.graph == 0) and len(evs) < 4096:
+                evs.append(ev)
             client.push_pull()
         client.done()
-        dist.gather_object(client.comm_summary(), None, dst=0)
+        summary = client.comm_summary()
+        torch.cuda.synchronize()
+        summary["compute_us"] = round(sum(a.elapsed_time(b) for a, b in evs) / max(1, len(evs)) * 1e3, 1)
+        dist.gather_object(summary, None, dst=0)
     dist.destroy_process_group()
     return 0
 

@@ -18,7 +18,19 @@ Design for MI355X:
   while conv2/conv1 backward (~80 % of backward time) runs, leaving a 10 KB
   latency-bound conv bucket at the end; the reference CNN gets [softmax+local4]
   0.8 MB, [local3] 12.85 MB (ring per-link bound on xGMI: ~2·7/8·S / 153 GB/s
-  ≈ 150 µs, hidden behind ~3 ms of conv backward), [conv2], [conv1];
+  ≈ 150 µs), [conv2], [conv1];
+* where the local3 all-reduce runs, reference CNN at the BASELINE batch
+  (B=16384/GPU, ``profiles/r3/dp_overlap/refcnn_b16384_step_timeline.txt``,
+  rocprofv3 kernel trace of a 2.47 ms step): the bucket is ready at 1.16 ms
+  (after the local3 wgrad GEMM + split-K reduce); 1.2 ms of backward follows.
+  The first 650 µs of it leave room for the RCCL kernel on every CU -- local3
+  dgrad is a 1600-workgroup GEMM (2 per CU, retiring in waves), lrn_pool_bwd
+  uses no LDS, conv2 wgrad is one 69 KB-LDS workgroup per CU -- and only then
+  does the conv2 dgrad halo kernel take 148 KB of each CU's 160 KB LDS for
+  315 µs.  A ~150 µs ring all-reduce therefore fits before the one kernel that
+  could lock it out, so no compute grid is capped.  Not yet measured: the ring
+  kernel's actual CU share on a multi-GPU node (a one-rank RCCL group issues no
+  kernel, so the one-GPU trace pins when the bucket is ready, not the contention);
 * split-K weight-gradient reduces of a bucket's layers are flushed as ONE
   multi-tensor launch just before its all-reduce (``HipNet.hook_layers``);
 * ``work.wait()`` only makes the compute stream wait (no host block); the

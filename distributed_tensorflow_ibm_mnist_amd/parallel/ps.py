@@ -402,7 +402,23 @@ class ParameterServer:
         self.tx.ps_after_ctrl(self, r, want_state)
 
     def serve(self) -> Dict[str, int]:
-        """Run until every worker has sent DONE, serving workers in arrival order."""
+        """Run until every worker has sent DONE, serving workers in arrival order.
+
+        On a GPU the PS works on a high-priority stream (``MNISTX_PS_PRIORITY=0`` turns
+        it off): its apply + reply are a few small kernels and copies that every worker
+        is blocked on, while the workers' step graphs are long and can wait -- with
+        workers sharing the PS's GPU, a default-priority PS queue waits behind them."""
+        if self.device.type != "cuda" or os.environ.get("MNISTX_PS_PRIORITY", "1") == "0":
+            return self._serve()
+        lo, hi = torch.cuda.Stream.priority_range()
+        s = torch.cuda.Stream(device=self.device, priority=hi)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            res = self._serve()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        return res
+
+    def _serve(self) -> Dict[str, int]:
         done: set = set()
         self.log(f"[ps {self.j}] serving {len(self.names)} tensor(s), {self.end - self.start} params, "
                  f"{self.W} worker(s), transport {self.tx.name}")

@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--bucket_mb", type=float, default=0.125,
                     help="gradient bucket cap (MB); every bucket but the last overlaps backward")
     ap.add_argument("--graph", type=int, default=-1,
-                    help="hipGraph capture of the step: 1 on (N > 1: with its RCCL all-reduces), 0 off, -1 auto = "
+                    help="hipGraph capture of the step: 1 on (N > 1: with its RCCL all-reduces -- UNVERIFIED on a real "
+                         "multi-GPU node, rehearsed only with one-rank RCCL / gloo ranks), 0 off, -1 auto = "
                          "on for one GPU at per-GPU batch <= 8192 (launch-bound); at the BASELINE batch eager "
                          "launches measure as fast (profiles/r2/graph_vs_eager.md), so 1..8 GPUs run one mode")
     ap.add_argument("--force_collectives", type=int, default=0,

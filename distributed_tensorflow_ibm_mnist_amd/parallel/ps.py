@@ -37,8 +37,13 @@ MI355X realisation -- ONE serve loop, two planes:
   ``local3/weights`` simply gets a PS of its own when k >= 2);
 * every worker pushes to every PS, so each PS sees the same pushes (in its
   own arrival order); each PS applies the first ``max_steps - start`` it
-  receives and counts its own global step, so all shards end on the same
-  update count (the reference's async PS made no stronger promise);
+  receives and counts its own global step, so in an uninterrupted run all
+  shards end on the same update count (the reference's async PS made no
+  stronger promise).  After a restart every shard resumes from the
+  checkpoint's single ``global_step`` (PS 0's count when the chief fetched the
+  state); shard j's tensors may have been fetched up to W-1 pushes away from
+  that count, so restarted shards can end up to W-1 updates apart (the
+  checkpoint keeps the reference's one global_step variable; no per-shard step);
 * shutdown (Q9): once its global step reaches ``max_steps`` PS 0 answers with
   a stop flag; workers send DONE to every PS; a PS exits when all are done.
 * the worker computes the weight-decay loss terms (``mnist_input.py:112-114``)

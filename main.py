@@ -56,7 +56,9 @@ flags.DEFINE_boolean("train_on_eval_split", False, "parity with the reference, w
 flags.DEFINE_boolean("no_shard", False, "every DP rank reads the whole dataset in its own order (reference P3)")
 flags.DEFINE_boolean("verbose_steps", False, "print 'training' + step on every step like the reference (Q11)")
 flags.DEFINE_boolean("hip_graph", True, "capture the training step in a hipGraph (single GPU)")
-flags.DEFINE_boolean("hip_graph_dp", False, "data parallel: also capture the step with its RCCL all-reduces")
+flags.DEFINE_boolean("hip_graph_dp", False, "data parallel: also capture the step with its RCCL all-reduces "
+                     "(rehearsed with one-rank RCCL and gloo ranks sharing a GPU; a real multi-GPU capture is "
+                     "UNVERIFIED -- the eager DP path is the default)")
 flags.DEFINE_float("bucket_mb", 0.125, "gradient all-reduce bucket cap (MB); every bucket but the last overlaps backward")
 flags.DEFINE_boolean("fused_input", False, "HIP: first fused conv reads the uint8 dataset through the batch index")
 flags.DEFINE_string("input_mode", "bf16", "HIP input path: bf16 | u8 (the first fused conv gathers the resident "

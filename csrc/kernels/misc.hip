@@ -761,12 +761,35 @@ __global__ __launch_bounds__(TPB) void fused_opt_k(float* __restrict__ params, c
 //        [4] ce_mean [5] accuracy [6] total_loss [7] steps done (float)
 // loss_ema: n_ema x {biased, local_step, avg}  (TF zero-debiased EMA, decay 0.9:
 //           mnist_input.py:288-290); order = weight losses..., cross_entropy, total_loss
-__global__ void finalize_k(int64_t* step, float* stats, float* l2, const int* __restrict__ l2r, int l2base,
+constexpr int FIN_WAVES = 4, FIN_MAXW = 64;
+__global__ __launch_bounds__(64 * FIN_WAVES) void finalize_k(int64_t* step, float* stats, float* l2, const int* __restrict__ l2r, int l2base,
                            const float* wds, int nw, float* loss_ema, int n_ema, int batch, int increment,
                            const float* __restrict__ ce_work, int ce_nblk) {
-  // one wave; lane i owns loss entry i (weight losses..., cross_entropy, total_loss), so the
-  // EMA read-modify-writes run in parallel instead of as one dependent chain
-  const int t = threadIdx.x;
+  // wave 0 lane i owns loss entry i (weight losses..., cross_entropy, total_loss), so the
+  // EMA read-modify-writes run in parallel instead of as one dependent chain.  The per-
+  // weight sum(w^2) partials are summed by all FIN_WAVES waves (weight w by wave w %
+  // FIN_WAVES, the same per-weight order as one wave): their load latencies overlap
+  // instead of queueing behind each other (LeNet: 5 weights, ~11 -> ~5 us).
+  __shared__ float wsum[FIN_MAXW];
+  const int t = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (l2 && l2r) {
+    for (int w = wv; w < nw && w < FIN_MAXW; w += FIN_WAVES) {
+      const int b0 = l2r[3 * w + 1], b1 = l2r[3 * w + 2];
+      // 4 independent chains per lane (loads in flight), combined in a fixed order
+      float s4[4] = {0.f, 0.f, 0.f, 0.f};
+      int b = b0 + t;
+      for (; b + 192 < b1; b += 256) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s4[u] += l2[l2base + b + 64 * u];
+      }
+      for (; b < b1; b += 64) s4[0] += l2[l2base + b];
+      float sum = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+      sum = warp_sum(sum);
+      if (t == 0) wsum[w] = sum;
+    }
+  }
+  __syncthreads();
+  if (wv != 0) return;
   float ce_sum = stats[0], corr_sum = stats[1];
   if (ce_nblk > 0) {
     // deferred CE partials (ce_block_stats defer): the same lane-strided, fixed-tree sum as
@@ -789,22 +812,9 @@ __global__ void finalize_k(int64_t* step, float* stats, float* l2, const int* __
   // sum(w^2) of weight t: the fused optimizer's per-block partials l2[l2base + b],
   // b in [l2r[3w+1], l2r[3w+2]), summed by the whole wave in a fixed order
   float l2v = (l2 && t < nw) ? l2[t] : 0.f;
-  if (l2 && l2r) {
-    for (int w = 0; w < nw; ++w) {
-      const int idx = l2r[3 * w], b0 = l2r[3 * w + 1], b1 = l2r[3 * w + 2];
-      // 4 independent chains per lane (loads in flight), combined in a fixed order
-      float s4[4] = {0.f, 0.f, 0.f, 0.f};
-      int b = b0 + t;
-      for (; b + 192 < b1; b += 256) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) s4[u] += l2[l2base + b + 64 * u];
-      }
-      for (; b < b1; b += 64) s4[0] += l2[l2base + b];
-      float sum = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-      sum = warp_sum(sum);
-      if (t == idx) l2v += sum;
-    }
-  }
+  if (l2 && l2r)
+    for (int w = 0; w < nw && w < FIN_MAXW; ++w)
+      if (t == l2r[3 * w]) l2v += wsum[w];
   const float wl = t < nw ? wds[t] * 0.5f * l2v : 0.f;
   float total = ce;
   for (int i = 0; i < nw; ++i) total += __shfl(wl, i, 64);   // fixed order (bitwise as before)
@@ -1052,7 +1062,8 @@ hipError_t fused_optimizer(float* params, const float* grads, float* mom, float*
 hipError_t finalize_step(int64_t* step, float* stats, const float* l2, const int* l2r, int l2base, const float* wds,
                          int nw, float* loss_ema, int n_ema, int batch, int increment, hipStream_t st,
                          const float* ce_work, int ce_nblk) {
-  hipLaunchKernelGGL(finalize_k, dim3(1), dim3(64), 0, st, step, stats, (float*)l2, l2r, l2base, wds, nw, loss_ema,
+  if (nw > FIN_MAXW) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(finalize_k, dim3(1), dim3(64 * FIN_WAVES), 0, st, step, stats, (float*)l2, l2r, l2base, wds, nw, loss_ema,
                      n_ema, batch, increment, ce_work, ce_nblk);
   return hipGetLastError();
 }

@@ -861,6 +861,18 @@ void f32_conv_wgrad(Tensor x, Tensor dy, Tensor slab, int64_t Nb, int64_t H, int
          "f32_conv_wgrad");
 }
 
+// Split count the fp32 conv weight gradient prefers: the LDS-halo kernel's resident
+// grid (one partial per workgroup) when it covers the geometry, else -1 (GEMM rule).
+int64_t f32_conv_wgrad_pref_splits(int64_t H, int64_t W, int64_t C, int64_t OH, int64_t OW, int64_t KH, int64_t KW,
+                                   int64_t ph, int64_t pw, int64_t Cout) {
+  if (mnistx::f32_halo_wgrad_ok((int)H, (int)W, (int)C, (int)OH, (int)OW, (int)KH, (int)KW, (int)ph, (int)pw,
+                                (int)Cout))
+    return mnistx::f32_halo_wgrad_grid();
+  if (mnistx::f32_conv1_ok((int)H, (int)W, (int)C, (int)OH, (int)OW, (int)KH, (int)KW, (int)ph, (int)pw, (int)Cout))
+    return mnistx::f32_conv1_wgrad_grid();
+  return -1;
+}
+
 void f32_maxpool_fwd(Tensor x, Tensor y, Tensor arg, int64_t Nb, int64_t H, int64_t W, int64_t C) {
   const int64_t OH = (H + 1) / 2, OW = (W + 1) / 2;
   check(x, at::kFloat, Nb * H * W * C, "x");
@@ -980,6 +992,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("f32_conv_fwd", &f32_conv_fwd);
   m.def("f32_conv_dgrad", &f32_conv_dgrad);
   m.def("f32_conv_wgrad", &f32_conv_wgrad);
+  m.def("f32_conv_wgrad_pref_splits", &f32_conv_wgrad_pref_splits);
   m.def("f32_maxpool_fwd", &f32_maxpool_fwd);
   m.def("f32_maxpool_bwd", &f32_maxpool_bwd);
   m.def("f32_lrn_fwd", &f32_lrn_fwd);

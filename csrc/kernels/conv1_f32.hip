@@ -1,0 +1,209 @@
+// fp32 (--precision fp32) first convolution of the reference CNN / LeNet geometry:
+// 28x28x1 NHWC input, 5x5 SAME, Cout 32, on v_mfma_f32_16x16x4_f32.
+//
+// The generic fp32 GEMM path (f32.hip Im2colF / Im2colTF) spends 1.17 ms (fwd) and
+// 1.89 ms (wgrad) per step on this layer at B = 16384 (profiles/r3/fp32): its loaders
+// recompute the im2col index of every element with four FastDivs, and the 64-wide N
+// tile is half empty at Cout 32.  Both are small problems (25 MACs per output) bound
+// by HBM at the roofline (the 1.64 GB conv output / its gradient), so these kernels
+// only have to get the operand plumbing out of the way:
+//   * forward: the image is staged in LDS once per image as a zero-haloed 32x32 tile,
+//     kept 4x shifted by 0..3 floats so every run of 4 consecutive taps of a kernel
+//     row is ONE aligned ds_read_b128; K = (kh 0..5, kw 0..7) with zero weights in
+//     the padding, A = the filter (held in registers for the whole launch), B = 16
+//     output pixels of one row; D lane (i, g) = channels 4g..4g+3 of pixel i -> one
+//     16-byte store with bias + ReLU;
+//   * weight gradient: M = 32 rows = 25 taps + the bias row (A = 1) + zero rows, N =
+//     32 channels, K = pixels, 4 consecutive pixels of a row per k-step; the patch
+//     operand is a 4-byte LDS read of the staged tile, dY a coalesced 64-byte global
+//     read per lane group (each dY value is read once); one fp32 partial per
+//     workgroup goes to the split-K slab [S][26][32] reduced by splitk_reduce.
+//
+// Replaces (SURVEY.md §2.3 N1, fp32 path): Conv2D / its filter gradient of conv1 at
+// mnist_input.py:142-145 under the reference's tf.float32.
+#include "common.h"
+#include "launchers.h"
+
+namespace mnistx {
+namespace {
+
+constexpr int IH = 28, IW = 28, IPIX = IH * IW, COUT = 32, KS = 5;
+constexpr int TR = 34, TC = 32;               // padded tile rows (2 + 28 + 2, + 2 for kh 5 over-read) x columns
+constexpr int TSZ = TR * TC + 8;              // one shifted copy (+ over-read slack)
+constexpr int NT1 = 256;
+
+// copy s holds T[j + s]; a 4-float run at tile offset a is ONE aligned b128 of copy a & 3
+DEV const float* run4(const float* tile, int a) { return tile + (a & 3) * TSZ + (a & ~3); }
+
+DEV void stage_image(float* tile, const float* __restrict__ x, int img, int tid) {
+  // interior (y, x) -> tile (y + 2, x + 2) of every copy s at offset - s
+  for (int e = tid; e < IPIX; e += NT1) {
+    const int y = e / IW, xx = e - y * IW;
+    const float v = x[(int64_t)img * IPIX + e];
+    const int a = (y + 2) * TC + xx + 2;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      if (a - s >= 0) tile[s * TSZ + a - s] = v;
+  }
+}
+
+__global__ __launch_bounds__(NT1) void conv1_f32_fwd_k(const float* __restrict__ x, const float* __restrict__ w,
+                                                       const float* __restrict__ bias, int relu, int B,
+                                                       float* __restrict__ y) {
+  __shared__ __attribute__((aligned(16))) float tile[4 * TSZ];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  for (int e = tid; e < 4 * TSZ; e += NT1) tile[e] = 0.f;
+  // A = filter: MFMA (b, s) of channel fragment nf, lane (co = 16 nf + i, k-group g):
+  // k = 16 b + 4 g + s -> kh = 2b + g/2, kw = 4(g&1) + s (zero outside the 5x5)
+  float a[3][4][2];
+#pragma unroll
+  for (int b = 0; b < 3; ++b)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) {
+        const int kh = 2 * b + (g >> 1), kw = 4 * (g & 1) + s;
+        a[b][s][nf] = (kh < KS && kw < KS) ? w[(kh * KS + kw) * COUT + 16 * nf + i] : 0.f;
+      }
+  float bs[2][4];
+#pragma unroll
+  for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bs[nf][r] = bias ? bias[16 * nf + 4 * g + r] : 0.f;
+  for (int img = blockIdx.x; img < B; img += gridDim.x) {
+    __syncthreads();
+    stage_image(tile, x, img, tid);
+    __syncthreads();
+    // units (row, 16-column segment): 28 x 2, dealt over the 4 waves
+    for (int u = wave; u < 2 * IH; u += NT1 / 64) {
+      const int row = u >> 1, x0 = 16 * (u & 1);
+      f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        const int kh = 2 * b + (g >> 1);
+        const f32x4 v = *(const f32x4*)run4(tile, (row + kh) * TC + x0 + i + 4 * (g & 1));
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int nf = 0; nf < 2; ++nf)
+            acc[nf] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[b][s][nf], v[s], acc[nf], 0, 0, 0);
+      }
+      const int xx = x0 + i;
+      if (xx < IW) {
+        const int64_t px = (int64_t)img * IPIX + row * IW + xx;
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf) {
+          f32x4 o = acc[nf];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            o[r] += bs[nf][r];
+            if (relu) o[r] = fmaxf(o[r], 0.f);
+          }
+          *(f32x4*)(y + px * COUT + 16 * nf + 4 * g) = o;
+        }
+      }
+    }
+  }
+}
+
+// slab[blockIdx][m][co], m = kh*5 + kw (25 taps) and the bias row 25
+constexpr int WROWS = KS * KS + 1;
+__global__ __launch_bounds__(NT1) void conv1_f32_wgrad_k(const float* __restrict__ x, const float* __restrict__ dy,
+                                                         int B, float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) float tile[4 * TSZ];
+  __shared__ float red[NT1 / 64][2][2][64][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  for (int e = tid; e < 4 * TSZ; e += NT1) tile[e] = 0.f;
+  // A rows of this lane: tap m = 16 mf + i -> tile offset of its (kh, kw), or the bias / zero rows
+  int toff[2];
+  float aconst[2];
+#pragma unroll
+  for (int mf = 0; mf < 2; ++mf) {
+    const int m = 16 * mf + i;
+    toff[mf] = m < KS * KS ? (m / KS) * TC + (m % KS) : -1;
+    aconst[mf] = m == KS * KS ? 1.f : 0.f;
+  }
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int mf = 0; mf < 2; ++mf)
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf) acc[mf][nf] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int img = blockIdx.x; img < B; img += gridDim.x) {
+    __syncthreads();
+    stage_image(tile, x, img, tid);
+    __syncthreads();
+    const float* dyi = dy + (int64_t)img * IPIX * COUT;
+    // k-step q = (row, 4-pixel column block): pixels (row, 4c + g); 196 per image over 4 waves
+#pragma unroll 4
+    for (int q = wave; q < IH * (IW / 4); q += NT1 / 64) {
+      const int row = q / (IW / 4), c4 = q - row * (IW / 4);
+      const int p = row * IW + 4 * c4 + g;
+      const float b0 = dyi[p * COUT + i], b1 = dyi[p * COUT + 16 + i];
+      const int base = row * TC + 4 * c4 + g;     // tile offset of the pixel's tap (0, 0)
+#pragma unroll
+      for (int mf = 0; mf < 2; ++mf) {
+        const float av = toff[mf] >= 0 ? tile[base + toff[mf]] : aconst[mf];
+        acc[mf][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b0, acc[mf][0], 0, 0, 0);
+        acc[mf][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b1, acc[mf][1], 0, 0, 0);
+      }
+    }
+  }
+  // fixed-order cross-wave sum (deterministic), then one partial per block
+#pragma unroll
+  for (int mf = 0; mf < 2; ++mf)
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wave][mf][nf][lane][r] = acc[mf][nf][r];
+  __syncthreads();
+  if (wave == 0) {
+    float* out = slab + (int64_t)blockIdx.x * WROWS * COUT;
+#pragma unroll
+    for (int mf = 0; mf < 2; ++mf)
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = ((red[0][mf][nf][lane][r] + red[1][mf][nf][lane][r]) + red[2][mf][nf][lane][r]) +
+                          red[3][mf][nf][lane][r];
+          const int m = 16 * mf + 4 * g + r;
+          if (m < WROWS) out[m * COUT + 16 * nf + i] = v;
+        }
+  }
+}
+
+int resident(const void* k) {
+  int dev = 0, cus = 0, pc = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k, NT1, 0) == hipSuccess && hipGetDevice(&dev) == hipSuccess &&
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && pc > 0)
+    return pc * cus;
+  return 1024;
+}
+
+}  // namespace
+
+bool f32_conv1_ok(int H, int W, int C, int OH, int OW, int KH, int KW, int ph, int pw, int Cout) {
+  static const bool on = [] { const char* e = getenv("MNISTX_F32_HALO"); return !(e && e[0] == '0'); }();
+  return on && H == IH && W == IW && C == 1 && OH == IH && OW == IW && KH == KS && KW == KS && ph == 2 && pw == 2 &&
+         Cout == COUT;
+}
+int f32_conv1_wgrad_grid() {
+  static const int n = resident((const void*)conv1_f32_wgrad_k);
+  return n;
+}
+hipError_t f32_conv1_fwd(const float* x, const float* w, int Nb, const float* bias, int relu, float* y,
+                         hipStream_t st) {
+  if (Nb <= 0) return hipSuccess;
+  static const int n = resident((const void*)conv1_f32_fwd_k);
+  hipLaunchKernelGGL(conv1_f32_fwd_k, dim3(Nb < n ? Nb : n), dim3(NT1), 0, st, x, w, bias, relu, Nb, y);
+  return hipGetLastError();
+}
+hipError_t f32_conv1_wgrad(const float* x, const float* dy, int Nb, int splits, float* slab, hipStream_t st) {
+  if (Nb <= 0 || splits <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(conv1_f32_wgrad_k, dim3(splits), dim3(NT1), 0, st, x, dy, Nb, slab);
+  return hipGetLastError();
+}
+
+}  // namespace mnistx

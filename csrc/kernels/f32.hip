@@ -21,13 +21,16 @@
 #include "ce_stats.h"
 #include "launchers.h"
 
+#include <cstdlib>
+
 namespace mnistx {
 namespace {
 
-constexpr int FBM = 64, FBN = 64, FBK = 16, FNT = 256;
-constexpr int FVPT = FBM * FBK / 4 / FNT;   // 4-element vectors per thread per operand tile
-static_assert(FBM == FBN && FVPT * 4 * FNT == FBM * FBK, "tile staging");
-constexpr int FLD = FBM + 4;   // LDS row stride (floats)
+constexpr int FBK = 16, FNT = 256;
+// BM x BM output tile per 256-thread block (BM = 64, or 128 for large problems: half the
+// L2 operand traffic per MAC); LDS row stride BM + 4 floats
+template <int BM> constexpr int fvpt() { return BM * FBK / 4 / FNT; }   // 4-vectors per thread per operand tile
+template <int BM> constexpr int fld() { return BM + 4; }
 
 // ---------------------------------------------------------------- loaders
 // load4(r, k): 4 operand elements along the operand's contiguous direction -- k..k+3
@@ -184,91 +187,94 @@ struct EpiF {
   int64_t slab_stride;
 };
 
-// Tile staging: 64 rows x FBK k = FVPT four-element vectors per thread, taken along
+// Tile staging: BM rows x FBK k = fvpt<BM>() four-element vectors per thread, taken along
 // the operand's contiguous direction; LDS keeps the tile k-major ([k][row]).
-template <class L>
-DEV void stage_load(const L& ld, int r0, int k0, int tid, f32x4 (&v)[FVPT]) {
+template <int BM, class L>
+DEV void stage_load(const L& ld, int r0, int k0, int tid, f32x4 (&v)[fvpt<BM>()]) {
 #pragma unroll
-  for (int i = 0; i < FVPT; ++i) {
+  for (int i = 0; i < fvpt<BM>(); ++i) {
     const int idx = tid + i * FNT;
     if constexpr (L::KC) v[i] = ld.load4(r0 + idx / (FBK / 4), k0 + 4 * (idx % (FBK / 4)));
-    else v[i] = ld.load4(r0 + 4 * (idx % (FBM / 4)), k0 + idx / (FBM / 4));
+    else v[i] = ld.load4(r0 + 4 * (idx % (BM / 4)), k0 + idx / (BM / 4));
   }
 }
 
-template <class L>
-DEV void stage_store(float* lds, int tid, const f32x4 (&v)[FVPT]) {
+template <int BM, class L>
+DEV void stage_store(float* lds, int tid, const f32x4 (&v)[fvpt<BM>()]) {
+  constexpr int LD = fld<BM>();
 #pragma unroll
-  for (int i = 0; i < FVPT; ++i) {
+  for (int i = 0; i < fvpt<BM>(); ++i) {
     const int idx = tid + i * FNT;
     if constexpr (L::KC) {
       const int r = idx / (FBK / 4), k = 4 * (idx % (FBK / 4));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) lds[(k + j) * FLD + r] = v[i][j];
+      for (int j = 0; j < 4; ++j) lds[(k + j) * LD + r] = v[i][j];
     } else {
-      *(f32x4*)(lds + (idx / (FBM / 4)) * FLD + 4 * (idx % (FBM / 4))) = v[i];
+      *(f32x4*)(lds + (idx / (BM / 4)) * LD + 4 * (idx % (BM / 4))) = v[i];
     }
   }
 }
 
 // C[M,N] = sum_k A(m,k) B(k,n) over this split's K range [z*kc, min(K, (z+1)*kc))
-template <class AL, class BL>
+// Four waves in a 2x2 layout, each (BM/2)^2 = FI x FI 16x16 fragments.
+template <int BM, class AL, class BL>
 __global__ __launch_bounds__(FNT) void gemm_f32_k(AL A, BL Bm, int M, int N, int K, int kc, EpiF ep) {
-  __shared__ float As[2][FBK * FLD];
-  __shared__ float Bs[2][FBK * FLD];
+  constexpr int LD = fld<BM>(), FI = BM / 32, VP = fvpt<BM>();
+  __shared__ float As[2][FBK * LD];
+  __shared__ float Bs[2][FBK * LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int tiles_n = (N + FBN - 1) / FBN;
+  const int tiles_n = (N + BM - 1) / BM;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (bid / tiles_n) * FBM, n0 = (bid % tiles_n) * FBN;
+  const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BM;
   const int z = blockIdx.y;
   const int kb = z * kc, ke = min(K, kb + kc);
-  f32x4 acc[2][2];
+  f32x4 acc[FI][FI];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 va[FVPT], vb[FVPT];
+    for (int j = 0; j < FI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 va[VP], vb[VP];
   if (kb < ke) {
-    stage_load(A, m0, kb, tid, va);
-    stage_load(Bm, n0, kb, tid, vb);
+    stage_load<BM>(A, m0, kb, tid, va);
+    stage_load<BM>(Bm, n0, kb, tid, vb);
   }
   int buf = 0;
   for (int k0 = kb; k0 < ke; k0 += FBK) {
-    stage_store<AL>(As[buf], tid, va);
-    stage_store<BL>(Bs[buf], tid, vb);
+    stage_store<BM, AL>(As[buf], tid, va);
+    stage_store<BM, BL>(Bs[buf], tid, vb);
     __syncthreads();
     if (k0 + FBK < ke) {
-      stage_load(A, m0, k0 + FBK, tid, va);
-      stage_load(Bm, n0, k0 + FBK, tid, vb);
+      stage_load<BM>(A, m0, k0 + FBK, tid, va);
+      stage_load<BM>(Bm, n0, k0 + FBK, tid, vb);
     }
     const float* as = As[buf];
     const float* bs = Bs[buf];
     const int kr = lane >> 4, cl = lane & 15;
 #pragma unroll
     for (int ks = 0; ks < FBK / 4; ++ks) {
-      float a[2], b[2];
+      float a[FI], b[FI];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = as[(4 * ks + kr) * FLD + wm * 32 + i * 16 + cl];
+      for (int i = 0; i < FI; ++i) a[i] = as[(4 * ks + kr) * LD + wm * (BM / 2) + i * 16 + cl];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = bs[(4 * ks + kr) * FLD + wn * 32 + j * 16 + cl];
+      for (int j = 0; j < FI; ++j) b[j] = bs[(4 * ks + kr) * LD + wn * (BM / 2) + j * 16 + cl];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < FI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FI; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     buf ^= 1;   // the next step writes the other buffer: one barrier per K step
   }
   // epilogue: lane holds rows 4(l/16)+r of column l%16 of each fragment
   const int rg = lane >> 4, cl = lane & 15;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < FI; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 32 + i * 16 + 4 * rg + r;
-        const int n = n0 + wn * 32 + j * 16 + cl;
+        const int m = m0 + wm * (BM / 2) + i * 16 + 4 * rg + r;
+        const int n = n0 + wn * (BM / 2) + j * 16 + cl;
         if (m >= M || n >= N) continue;
         float v = acc[i][j][r];
         if (ep.mode == 1) {
@@ -282,14 +288,26 @@ __global__ __launch_bounds__(FNT) void gemm_f32_k(AL A, BL Bm, int M, int N, int
       }
 }
 
+// 128x128 tiles when both dims fill them and the problem has >= 4 per CU (incl. splits):
+// half the L2 operand traffic per MAC of the 64x64 tile.  Measured (profiles/r3/fp32): the
+// reference CNN's local3 forward 1.12 -> 0.95 ms, dgrad unchanged, and its split-K wgrad
+// (600 tiles) SLOWER (1.29 -> 1.43 ms), hence the 4-per-CU threshold.  MNISTX_F32_TILE=64
+// forces the small tile.
 template <class AL, class BL>
 hipError_t launch_f32(const AL& A, const BL& Bm, int M, int N, int K, int splits, const EpiF& ep, hipStream_t st) {
   if (M <= 0 || N <= 0) return hipSuccess;
   splits = splits < 1 ? 1 : splits;
   int kc = (K + splits - 1) / splits;
   kc = (kc + FBK - 1) / FBK * FBK;
-  const int tiles = ((M + FBM - 1) / FBM) * ((N + FBN - 1) / FBN);
-  hipLaunchKernelGGL((gemm_f32_k<AL, BL>), dim3(tiles, splits), dim3(FNT), 0, st, A, Bm, M, N, K, kc, ep);
+  static const bool small_only = [] { const char* e = getenv("MNISTX_F32_TILE"); return e && e[0] == '6'; }();
+  const int64_t big = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * splits;
+  if (!small_only && big >= 1024 && N >= 128 && M >= 128) {
+    const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+    hipLaunchKernelGGL((gemm_f32_k<128, AL, BL>), dim3(tiles, splits), dim3(FNT), 0, st, A, Bm, M, N, K, kc, ep);
+  } else {
+    const int tiles = ((M + 63) / 64) * ((N + 63) / 64);
+    hipLaunchKernelGGL((gemm_f32_k<64, AL, BL>), dim3(tiles, splits), dim3(FNT), 0, st, A, Bm, M, N, K, kc, ep);
+  }
   return hipGetLastError();
 }
 
@@ -443,6 +461,134 @@ __global__ void prep_images_f32_k(const uint8_t* __restrict__ src, const int64_t
   }
 }
 
+// ---------------------------------------------------------------- vectorised pool / LRN
+// One lane per (pool window | pixel, 4 channels): 16-byte loads and stores, 32-bit
+// FastDiv index math.  The per-element kernels above did three 64-bit divisions per
+// element (1.17 ms for the 411 MB pool1 gradient at B = 16384, ~10x its HBM time);
+// they remain the fallback for odd sizes / unaligned buffers.
+__global__ __launch_bounds__(256) void maxpool_f32_fwd_v4_k(const float* __restrict__ x, int total, FastDiv fC4,
+                                                            FastDiv fOW, FastDiv fOH, int C, float* __restrict__ y,
+                                                            uint32_t* __restrict__ arg) {
+  const int W = 2 * (int)fOW.d;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int win = fC4.div(t), cv = fC4.mod(t, win);
+    const int r = fOW.div(win), ow = fOW.mod(win, r);
+    const int n = fOH.div(r), oh = fOH.mod(r, n);
+    const int64_t base = (((int64_t)n * 2 * fOH.d + 2 * oh) * W + 2 * ow) * C + 4 * cv;
+    f32x4 v[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) v[d] = *(const f32x4*)(x + base + ((d >> 1) * W + (d & 1)) * C);
+    f32x4 best = v[0];
+    uint32_t code = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t bi = 0;
+#pragma unroll
+      for (int d = 1; d < 4; ++d)
+        if (v[d][j] > best[j]) { best[j] = v[d][j]; bi = d; }   // first maximum wins (TF MaxPool)
+      code |= bi << (8 * j);
+    }
+    *(f32x4*)(y + (int64_t)t * 4) = best;
+    arg[t] = code;
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_f32_bwd_v4_k(const float* __restrict__ dy,
+                                                            const uint32_t* __restrict__ arg,
+                                                            const float* __restrict__ y, int relu_mask, int total,
+                                                            FastDiv fC4, FastDiv fOW, FastDiv fOH, int C,
+                                                            float* __restrict__ dx) {
+  const int W = 2 * (int)fOW.d;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const int win = fC4.div(t), cv = fC4.mod(t, win);
+    const int r = fOW.div(win), ow = fOW.mod(win, r);
+    const int n = fOH.div(r), oh = fOH.mod(r, n);
+    const int64_t base = (((int64_t)n * 2 * fOH.d + 2 * oh) * W + 2 * ow) * C + 4 * cv;
+    const f32x4 g = *(const f32x4*)(dy + (int64_t)t * 4);
+    const uint32_t a = arg[t];
+    f32x4 yy = {1.f, 1.f, 1.f, 1.f};
+    if (relu_mask) yy = *(const f32x4*)(y + (int64_t)t * 4);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      f32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (((a >> (8 * j)) & 0xffu) == (uint32_t)d && yy[j] > 0.f) ? g[j] : 0.f;
+      *(f32x4*)(dx + base + ((d >> 1) * W + (d & 1)) * C) = o;
+    }
+  }
+}
+
+// LRN with 4 channels per lane, the C/4 lanes of a pixel adjacent inside one 16-lane
+// DPP row; the window's neighbours (radius r <= 4) come from the adjacent lanes by
+// DPP row shifts (zero at the pixel's first / last lane).
+DEV float f32_from_left(float v) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, true)); }
+DEV float f32_from_right(float v) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x101, 0xf, 0xf, true)); }
+DEV f32x4 win4(const f32x4& v, int c4, int G, int r) {
+  float e[12];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float l = f32_from_left(v[j]), rr = f32_from_right(v[j]);
+    e[j] = c4 == 0 ? 0.f : l;
+    e[8 + j] = c4 == G - 1 ? 0.f : rr;
+    e[4 + j] = v[j];
+  }
+  f32x4 s;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float a = 0.f;
+#pragma unroll
+    for (int d = -4; d <= 4; ++d)
+      if (d >= -r && d <= r) a = fmaf(1.f, e[4 + j + d], a);
+    s[j] = a;
+  }
+  return s;
+}
+
+__global__ __launch_bounds__(256) void lrn_f32_fwd_v4_k(const float* __restrict__ x, int total, int G, int r,
+                                                        float bias, float alpha, float beta, float* __restrict__ y) {
+  // uniform trip count over whole waves: every lane takes part in the DPP exchanges
+  for (int b0 = blockIdx.x * blockDim.x; b0 < total; b0 += gridDim.x * blockDim.x) {
+    const int t = b0 + threadIdx.x;
+    const bool ok = t < total;
+    const int c4 = threadIdx.x % G;
+    const f32x4 v = ok ? *(const f32x4*)(x + (int64_t)t * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 s = win4(v * v, c4, G, r);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = v[j] * pow_neg(fmaf(alpha, s[j], bias), beta);
+    if (ok) *(f32x4*)(y + (int64_t)t * 4) = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void lrn_f32_bwd_v4_k(const float* __restrict__ x, const float* __restrict__ dy,
+                                                        int total, int G, int r, float bias, float alpha, float beta,
+                                                        int relu_mask, float* __restrict__ dx) {
+  for (int b0 = blockIdx.x * blockDim.x; b0 < total; b0 += gridDim.x * blockDim.x) {
+    const int t = b0 + threadIdx.x;
+    const bool ok = t < total;
+    const int c4 = threadIdx.x % G;
+    const f32x4 v = ok ? *(const f32x4*)(x + (int64_t)t * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 g = ok ? *(const f32x4*)(dy + (int64_t)t * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 s = win4(v * v, c4, G, r);
+    f32x4 nb, tt;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float n = fmaf(alpha, s[j], bias);
+      nb[j] = pow_neg(n, beta);
+      tt[j] = g[j] * v[j] * nb[j] / n;
+    }
+    const f32x4 u = win4(tt, c4, G, r);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float d = g[j] * nb[j] - 2.f * alpha * beta * v[j] * u[j];
+      if (relu_mask && !(v[j] > 0.f)) d = 0.f;
+      o[j] = d;
+    }
+    if (ok) *(f32x4*)(dx + (int64_t)t * 4) = o;
+  }
+}
+
 int ew_grid(int64_t n) {
   const int64_t g = (n + 255) / 256;
   return (int)(g < 8192 ? (g < 1 ? 1 : g) : 8192);
@@ -473,6 +619,11 @@ hipError_t f32_dense_wgrad(const float* x, const float* dy, int B, int Din, int 
 
 hipError_t f32_conv_fwd(const float* x, const float* w, int Nb, int H, int W, int C, int OH, int OW, int KH, int KW,
                         int ph, int pw, int Cout, const float* bias, int relu, float* y, hipStream_t st) {
+  if (f32_conv1_ok(H, W, C, OH, OW, KH, KW, ph, pw, Cout) && (reinterpret_cast<uintptr_t>(y) & 15) == 0)
+    return f32_conv1_fwd(x, w, Nb, bias, relu, y, st);
+  if (f32_halo_fwd_ok(H, W, C, OH, OW, KH, KW, ph, pw, Cout) && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(w) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0)
+    return f32_halo_fwd(x, w, Nb, C, Cout, bias, relu, y, st);
   const int M = Nb * OH * OW, K = KH * KW * C;
   const Im2colF A{x, H, W, C, OH, OW, KW, ph, pw, M, K, FastDiv(OH * OW), FastDiv(OW), FastDiv(C), FastDiv(KW)};
   return launch_f32(A, StridedF<false>{w, Cout, K, Cout, -1}, M, Cout, K,
@@ -481,6 +632,10 @@ hipError_t f32_conv_fwd(const float* x, const float* w, int Nb, int H, int W, in
 
 hipError_t f32_conv_dgrad(const float* dy, const float* w, int Nb, int OH, int OW, int Cout, int H, int W, int KH,
                           int KW, int ph, int pw, int Cin, const float* mask, float* dx, hipStream_t st) {
+  if (f32_halo_dgrad_ok(OH, OW, Cout, H, W, KH, KW, ph, pw, Cin) && (reinterpret_cast<uintptr_t>(dy) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(w) & 15) == 0 && (reinterpret_cast<uintptr_t>(dx) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(mask) & 15) == 0)
+    return f32_halo_dgrad(dy, w, Nb, Cout, Cin, mask, dx, st);
   const int M = Nb * H * W, K = KH * KW * Cout;
   const DyIm2colF A{dy, H, W, OH, OW, Cout, KW, ph, pw, M, K, FastDiv(H * W), FastDiv(W), FastDiv(Cout), FastDiv(KW)};
   return launch_f32(A, WFlipF{w, Cin, Cout, K, FastDiv(Cout)}, M, Cin, K, 1,
@@ -490,14 +645,30 @@ hipError_t f32_conv_dgrad(const float* dy, const float* w, int Nb, int OH, int O
 hipError_t f32_conv_wgrad(const float* x, const float* dy, int Nb, int H, int W, int C, int OH, int OW, int KH,
                           int KW, int ph, int pw, int Cout, int splits, float* slab, hipStream_t st) {
   // slab[z][KH*KW*C + 1][Cout], row KH*KW*C = bias
+  if (f32_conv1_ok(H, W, C, OH, OW, KH, KW, ph, pw, Cout))
+    return f32_conv1_wgrad(x, dy, Nb, splits, slab, st);   // one partial per workgroup, `splits` workgroups
+  if (f32_halo_wgrad_ok(H, W, C, OH, OW, KH, KW, ph, pw, Cout) && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(dy) & 15) == 0)
+    return f32_halo_wgrad(x, dy, Nb, splits, slab, st);   // one partial per workgroup, `splits` workgroups
   const int P = Nb * OH * OW, Mr = KH * KW * C;
   const Im2colTF A{x, H, W, C, OH, OW, KW, ph, pw, P, Mr, FastDiv(OH * OW), FastDiv(OW), FastDiv(C), FastDiv(KW)};
   return launch_f32(A, StridedF<false>{dy, Cout, P, Cout, -1}, Mr + 1,
                     Cout, P, splits, slab_epi(slab, (int64_t)(Mr + 1) * Cout), st);
 }
 
+static bool al16h(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+static bool pool_v4_ok(int64_t nwin, int H, int W, int C, int OH, int OW) {
+  return H == 2 * OH && W == 2 * OW && C % 4 == 0 && nwin * (C / 4) < (int64_t)1 << 30;
+}
+
 hipError_t f32_maxpool_fwd(const float* x, int Nb, int H, int W, int C, int OH, int OW, float* y, uint8_t* arg,
                            hipStream_t st) {
+  if (pool_v4_ok((int64_t)Nb * OH * OW, H, W, C, OH, OW) && al16h(x) && al16h(y) && al16h(arg)) {
+    const int total = Nb * OH * OW * (C / 4);
+    hipLaunchKernelGGL(maxpool_f32_fwd_v4_k, dim3(ew_grid(total)), dim3(256), 0, st, x, total, FastDiv(C / 4),
+                       FastDiv(OW), FastDiv(OH), C, y, (uint32_t*)arg);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(maxpool_f32_fwd_k, dim3(ew_grid((int64_t)Nb * OH * OW * C)), dim3(256), 0, st, x, Nb, H, W, C,
                      OH, OW, y, arg);
   return hipGetLastError();
@@ -505,6 +676,12 @@ hipError_t f32_maxpool_fwd(const float* x, int Nb, int H, int W, int C, int OH, 
 
 hipError_t f32_maxpool_bwd(const float* dy, const uint8_t* arg, const float* y, int relu_mask, int Nb, int H, int W,
                            int C, int OH, int OW, float* dx, hipStream_t st) {
+  if (pool_v4_ok((int64_t)Nb * OH * OW, H, W, C, OH, OW) && al16h(dy) && al16h(arg) && al16h(y) && al16h(dx)) {
+    const int total = Nb * OH * OW * (C / 4);
+    hipLaunchKernelGGL(maxpool_f32_bwd_v4_k, dim3(ew_grid(total)), dim3(256), 0, st, dy, (const uint32_t*)arg, y,
+                       relu_mask, total, FastDiv(C / 4), FastDiv(OW), FastDiv(OH), C, dx);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(maxpool_f32_bwd_k, dim3(ew_grid((int64_t)Nb * H * W * C)), dim3(256), 0, st, dy, arg, y,
                      relu_mask, Nb, H, W, C, OH, OW, dx);
   return hipGetLastError();
@@ -513,6 +690,12 @@ hipError_t f32_maxpool_bwd(const float* dy, const uint8_t* arg, const float* y, 
 hipError_t f32_lrn_fwd(const float* x, int64_t P, int C, int r, float bias, float alpha, float beta, float* y,
                        hipStream_t st) {
   if (C > LRN_MAXC || C < 1) return hipErrorInvalidValue;
+  if ((C == 32 || C == 64) && r <= 4 && P * (C / 4) < ((int64_t)1 << 30) && al16h(x) && al16h(y)) {
+    const int total = (int)(P * (C / 4));
+    hipLaunchKernelGGL(lrn_f32_fwd_v4_k, dim3(ew_grid(total)), dim3(256), 0, st, x, total, C / 4, r, bias, alpha,
+                       beta, y);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(lrn_f32_fwd_k, dim3(ew_grid(P * C)), dim3(256), 0, st, x, P, C, r, bias, alpha, beta, y);
   return hipGetLastError();
 }
@@ -520,6 +703,12 @@ hipError_t f32_lrn_fwd(const float* x, int64_t P, int C, int r, float bias, floa
 hipError_t f32_lrn_bwd(const float* x, const float* dy, int64_t P, int C, int r, float bias, float alpha, float beta,
                        int relu_mask, float* dx, hipStream_t st) {
   if (C > LRN_MAXC || C < 1) return hipErrorInvalidValue;
+  if ((C == 32 || C == 64) && r <= 4 && P * (C / 4) < ((int64_t)1 << 30) && al16h(x) && al16h(dy) && al16h(dx)) {
+    const int total = (int)(P * (C / 4));
+    hipLaunchKernelGGL(lrn_f32_bwd_v4_k, dim3(ew_grid(total)), dim3(256), 0, st, x, dy, total, C / 4, r, bias, alpha,
+                       beta, relu_mask, dx);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(lrn_f32_bwd_k, dim3(ew_grid(P * C)), dim3(256), 0, st, x, dy, P, C, r, bias, alpha, beta,
                      relu_mask, dx);
   return hipGetLastError();

@@ -118,6 +118,22 @@ hipError_t f32_dense_dgrad(const float* dy, const float* w, int M, int Din, int 
                            hipStream_t st);
 hipError_t f32_dense_wgrad(const float* x, const float* dy, int B, int Din, int Dout, int splits, float* slab,
                            hipStream_t st);
+// conv_halo_f32.hip: LDS-halo fp32 conv2 of the reference CNN (fwd / dgrad), routed to by f32_conv_*
+bool f32_halo_fwd_ok(int H, int W, int C, int OH, int OW, int KH, int KW, int ph, int pw, int Cout);
+bool f32_halo_dgrad_ok(int OH, int OW, int Cout, int H, int W, int KH, int KW, int ph, int pw, int Cin);
+hipError_t f32_halo_fwd(const float* x, const float* w, int Nb, int C, int Cout, const float* bias, int relu, float* y,
+                        hipStream_t st);
+hipError_t f32_halo_dgrad(const float* dy, const float* w, int Nb, int Cout, int Cin, const float* mask, float* dx,
+                          hipStream_t st);
+// conv1_f32.hip: fp32 28x28x1 -> 32, 5x5 SAME (reference CNN / fp32 conv1), routed to by f32_conv_*
+bool f32_conv1_ok(int H, int W, int C, int OH, int OW, int KH, int KW, int ph, int pw, int Cout);
+int f32_conv1_wgrad_grid();
+hipError_t f32_conv1_fwd(const float* x, const float* w, int Nb, const float* bias, int relu, float* y,
+                         hipStream_t st);
+hipError_t f32_conv1_wgrad(const float* x, const float* dy, int Nb, int splits, float* slab, hipStream_t st);
+bool f32_halo_wgrad_ok(int H, int W, int C, int OH, int OW, int KH, int KW, int ph, int pw, int Cout);
+int f32_halo_wgrad_grid();
+hipError_t f32_halo_wgrad(const float* x, const float* dy, int Nb, int splits, float* slab, hipStream_t st);
 hipError_t f32_conv_fwd(const float* x, const float* w, int Nb, int H, int W, int C, int OH, int OW, int KH, int KW,
                         int ph, int pw, int Cout, const float* bias, int relu, float* y, hipStream_t st);
 hipError_t f32_conv_dgrad(const float* dy, const float* w, int Nb, int OH, int OW, int Cout, int H, int W, int KH,

@@ -5,7 +5,12 @@ The reference trains in fp32 (``mnist_input.py:86,107``: ``dtype = tf.float32``)
 accumulation; ``HipNetF32`` runs the same model specs with every activation,
 weight operand and gradient in fp32 on the ``csrc/kernels/f32.hip`` kernels
 (``v_mfma_f32_16x16x4_f32`` GEMM engine with implicit-GEMM conv loaders, fp32
-max-pool / LRN / softmax-CE).  Optimizer, EMA, LR schedule, loss EMA and the
+max-pool / LRN / softmax-CE).  The f32 launchers route the reference CNN's convs
+to dedicated kernels: conv2 (14x14, 32 -> 64) fwd / dgrad / wgrad on LDS-halo
+tiles (``conv_halo_f32.hip``, the bf16 halo design in fp32), conv1 (28x28x1 ->
+32) fwd / wgrad on shifted-copy image tiles (``conv1_f32.hip``); pool and LRN run
+as 16-byte-vector kernels.  At B=16384 that took the fp32 step from 26.0 to
+~19 ms (``profiles/r3/fp32/``).  Optimizer, EMA, LR schedule, loss EMA and the
 deterministic split-K reduce are the shared K9 / misc.hip kernels, so the
 checkpoint layout, hooks and data-parallel buckets are identical.
 
@@ -61,7 +66,12 @@ class ConvF(_L):
         self.out = _f32(B, self.OH, self.OW, spec.cout, device=dev)
         self.wname, self.bname = f"{spec.name}/weights", f"{spec.name}/biases"
         self.M = spec.kh * spec.kw * self.C + 1
-        self.splits = wgrad_splits(self.M, spec.cout, B * self.OH * self.OW)
+        # the LDS-halo weight gradient (conv_halo_f32.hip) writes one partial per resident
+        # workgroup; other geometries use the split-K GEMM rule
+        pref = kernels().f32_conv_wgrad_pref_splits(self.H, self.W, self.C, self.OH, self.OW, spec.kh, spec.kw,
+                                                    self.ph, self.pw, spec.cout) if dev.type == "cuda" else -1
+        self.halo_wg = pref > 0
+        self.splits = pref if self.halo_wg else wgrad_splits(self.M, spec.cout, B * self.OH * self.OW)
         self.slab = _f32(self.splits * self.M * spec.cout, device=dev)
 
     def fwd(self, nb: int) -> None:
@@ -71,7 +81,8 @@ class ConvF(_L):
 
     def bwd_weight(self, nb: int, dy: torch.Tensor) -> None:
         s, K = self.spec, kernels()
-        S = min(self.splits, wgrad_splits(self.M, s.cout, nb * self.OH * self.OW))
+        S = min(self.splits, max(1, nb)) if self.halo_wg else \
+            min(self.splits, wgrad_splits(self.M, s.cout, nb * self.OH * self.OW))
         K.f32_conv_wgrad(self.x, dy, self.slab, nb, self.H, self.W, self.C, self.OH, self.OW, s.kh, s.kw, self.ph,
                          self.pw, s.cout, S)
         K.splitk_reduce(self.slab, S, self.M, s.cout, s.kh * s.kw, self.C, self.C, s.cout, s.kh * s.kw * self.C,

@@ -16,7 +16,8 @@ def rel_err(a, b):
     return ((a.double() - b.double()).norm() / (b.double().norm() + 1e-30)).item()
 
 
-@pytest.mark.parametrize("M,N,Kk,relu", [(77, 10, 192, False), (300, 1024, 3136, True), (5, 130, 33, True)])
+@pytest.mark.parametrize("M,N,Kk,relu", [(77, 10, 192, False), (300, 1024, 3136, True), (5, 130, 33, True),
+                                         (8200, 1030, 200, True)])   # the last: 128x128 tiles
 def test_f32_dense(dev, K, M, N, Kk, relu):
     torch.manual_seed(0)
     x = torch.randn(M, Kk, device=dev)
@@ -42,7 +43,7 @@ def test_f32_dense(dev, K, M, N, Kk, relu):
         assert rel_err(tot[Kk], dy.sum(0)) < 1e-5
 
 
-@pytest.mark.parametrize("Nb,H,Ci,Co,k,pad", [(3, 28, 3, 32, 5, "SAME"), (2, 14, 32, 64, 5, "SAME"),
+@pytest.mark.parametrize("Nb,H,Ci,Co,k,pad", [(3, 28, 3, 32, 5, "SAME"), (2, 14, 32, 64, 5, "SAME"), (6, 28, 1, 32, 5, "SAME"),
                                                (5, 14, 6, 16, 5, "VALID"), (1, 9, 1, 8, 3, "SAME")])
 def test_f32_conv(dev, K, Nb, H, Ci, Co, k, pad):
     torch.manual_seed(1)
@@ -163,3 +164,49 @@ def test_f32_training_cli(dev, K, tmp_path):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert json.load(open(out / "val.json"))
+
+
+@pytest.mark.parametrize("Nb,Co", [(1, 64), (37, 64), (700, 32)])
+def test_f32_halo_conv2(dev, K, Nb, Co):
+    """conv_halo_f32.hip (reference conv2 geometry: 14x14, 5x5 SAME, 32 -> Co channels;
+    dgrad of 64 dY channels with the input-ReLU mask) against PyTorch fp32, over
+    persistent grids with several images per workgroup."""
+    torch.manual_seed(Nb)
+    x = torch.randn(Nb, 14, 14, 32, device=dev)
+    w = torch.randn(5, 5, 32, Co, device=dev) * 0.05
+    b = torch.randn(Co, device=dev)
+    y = torch.empty(Nb, 14, 14, Co, device=dev)
+    K.f32_conv_fwd(x, w, y, Nb, 14, 14, 32, 14, 14, 5, 5, 2, 2, Co, b, True)
+    ref = F.conv2d(x.permute(0, 3, 1, 2), w.permute(3, 2, 0, 1), b, padding=2).relu().permute(0, 2, 3, 1)
+    assert rel_err(y, ref) < 1e-5
+    # dgrad: a 64-channel dY through the conv2 filter (Cin 32 <- Cout 64), ReLU mask of the input
+    w2 = torch.randn(5, 5, 32, 64, device=dev) * 0.05
+    dy = torch.randn(Nb, 14, 14, 64, device=dev)
+    xm = torch.randn(Nb, 14, 14, 32, device=dev)
+    dx = torch.empty(Nb, 14, 14, 32, device=dev)
+    K.f32_conv_dgrad(dy, w2, dx, Nb, 14, 14, 64, 14, 14, 5, 5, 2, 2, 32, xm)
+    ref_dx = torch.nn.grad.conv2d_input((Nb, 32, 14, 14), w2.permute(3, 2, 0, 1), dy.permute(0, 3, 1, 2),
+                                        padding=2).permute(0, 2, 3, 1) * (xm > 0)
+    assert rel_err(dx, ref_dx) < 1e-5
+
+
+@pytest.mark.parametrize("Nb,S", [(1, 1), (300, 7), (1500, 256)])
+def test_f32_conv1_kernels(dev, K, Nb, S):
+    """conv1_f32.hip (28x28x1 -> 32, 5x5 SAME): forward with bias + ReLU, and the weight
+    gradient's per-workgroup partials (S workgroups, several images each) against PyTorch."""
+    torch.manual_seed(Nb)
+    x = torch.randn(Nb, 28, 28, 1, device=dev)
+    w = torch.randn(5, 5, 1, 32, device=dev) * 0.2
+    b = torch.randn(32, device=dev)
+    y = torch.empty(Nb, 28, 28, 32, device=dev)
+    K.f32_conv_fwd(x, w, y, Nb, 28, 28, 1, 28, 28, 5, 5, 2, 2, 32, b, True)
+    xc = x.permute(0, 3, 1, 2)
+    ref = F.conv2d(xc, w.permute(3, 2, 0, 1), b, padding=2).relu().permute(0, 2, 3, 1)
+    assert rel_err(y, ref) < 1e-5
+    dy = torch.randn(Nb, 28, 28, 32, device=dev)
+    slab = torch.full((S * 26 * 32,), float("nan"), device=dev)
+    K.f32_conv_wgrad(x, dy, slab, Nb, 28, 28, 1, 28, 28, 5, 5, 2, 2, 32, S)
+    tot = slab.view(S, 26, 32).sum(0)
+    ref_w = torch.nn.grad.conv2d_weight(xc, (32, 1, 5, 5), dy.permute(0, 3, 1, 2), padding=2)
+    assert rel_err(tot[:25].view(5, 5, 1, 32), ref_w.permute(2, 3, 1, 0)) < 1e-5
+    assert rel_err(tot[25], dy.sum((0, 1, 2))) < 1e-5

@@ -102,6 +102,7 @@ struct BandFwd {
   bf16_t* p2;             // [B][5][5][16]
   uint8_t* arg2;          // [B][25][16]
   unsigned long long* prof;   // optional (experiments): per-role busy / barrier-wait clock sums
+  int prio;                   // 1 = conv1 waves at s_setprio 1 (default), 2 = conv2 waves, 0 = none
 };
 
 // Pooled value + argmax code of the window finalised by this lane: keep = this lane's
@@ -183,6 +184,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
   if (wave < 4) {
     // ================================================================ conv1 + pool1 role
     const int t = tid;                                   // 0..255
+    if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
     bf16x8 a1[3];    // (p): rows (xq, xpar, c), k = (dy parity h, input column j of the window)
     {
       const int xq = col >> 4, xpar = (col >> 3) & 1, c = col & 7;
@@ -303,6 +305,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
   } else {
     // ================================================================ conv2 + pool2 role
     const int t = tid - 256;
+    if (a.prio == 2) __builtin_amdgcn_s_setprio(1);
     bf16x8 a2[15];   // (dy, q): rows (xpar, c2), k = (pixel h, channel j)
     {
       const int xpar = col >> 4, c2 = col & 15;
@@ -439,7 +442,11 @@ hipError_t lenet_band_fwd(const XSrc& x, const bf16_t* w1, const float* b1, int 
                           hipStream_t st, unsigned long long* prof) {
   if (B <= 0) return hipSuccess;
   if (!x.x && !x.u8) return hipErrorInvalidValue;
-  BandFwd a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, w1, b1, b1n, w2, b2, B, p1, arg1, p2, arg2, prof};
+  // conv1 (the busier role: ~90 % vs ~73 % of the iteration) at s_setprio 1 wins the
+  // SIMD's issue arbitration against the conv2 waves: 219-222 -> 210-211 us, 0.61 -> 0.595
+  // ms/step (profiles/r3/lenet/band_prio_ab.txt); MNISTX_BAND_PRIO=0 / 2 for A/B
+  static const int prio = [] { const char* e = getenv("MNISTX_BAND_PRIO"); return e ? atoi(e) : 1; }();
+  BandFwd a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, w1, b1, b1n, w2, b2, B, p1, arg1, p2, arg2, prof, prio};
   const int ntiles = (B + BT - 1) / BT;
   if (p1) {
     const int grid = fwd_grid<true>(ntiles);

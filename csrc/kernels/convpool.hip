@@ -946,7 +946,7 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
 // with ds_read_b64_tr_b16: each lane supplies one pixel row and one 4-column
 // chunk; the bias row (k = KE) reads a constant [1,0,0,0] LDS cell.  dY is
 // rebuilt from (dP, arg): position d of a window gets dP iff arg == d.
-template <class G, int IMGS, bool LRNB = false>
+template <class G, int IMGS, bool LRNB = false, bool PRIO = false>
 __global__ __launch_bounds__(NTH, wgrad_minw<G>()) void convpool_wgrad_k(const XSrc x, const bf16_t* __restrict__ dP,
                                                         const uint8_t* __restrict__ arg, int B,
                                                         float* __restrict__ slab, const LrnFold lrn) {
@@ -1060,6 +1060,7 @@ __global__ __launch_bounds__(NTH, wgrad_minw<G>()) void convpool_wgrad_k(const X
       const int lane_a = 4 * (p & 1) + e1 * G::CIN;
       const int lane_b = 4 * (p & 1) + e1 * (G::WS - G::KS + 1) * G::CIN;
       auto toff = [](int t) constexpr { return ((t / G::KS) * G::WS + t % G::KS) * G::CIN; };
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
       for (int it = wave; it < IMGS * G::RSTEPS; it += NTH / 64) {
         const int im = it / G::RSTEPS, s = it - im * G::RSTEPS;
         const int w0 = 8 * s + g;
@@ -1082,6 +1083,7 @@ __global__ __launch_bounds__(NTH, wgrad_minw<G>()) void convpool_wgrad_k(const X
           acc[mf][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr, acc[mf][0], 0, 0, 0);
         }
       }
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
       continue;
     }
     for (int it = wave; it < IMGS * G::RSTEPS; it += NTH / 64) {
@@ -1186,7 +1188,7 @@ __global__ __launch_bounds__(NTH, wgrad_minw<G>()) void convpool_wgrad_k(const X
 // (8 VALU per channel, no compares).  The bias gradient comes out of the MFMA: the
 // lanes supplying im2col^T rows KE..KE+3 read a constant [1,0,0,0] cell, so row KE
 // accumulates sum(dY) per column (deterministic MFMA order, no staging VALU).
-template <class G, int IMGS>
+template <class G, int IMGS, bool PRIO = false>
 __global__ __launch_bounds__(NTH, 7) void convpool_wgrad_pair_k(const XSrc x,
                                                              const bf16_t* __restrict__ dP,
                                                              const uint8_t* __restrict__ arg, int B,
@@ -1282,6 +1284,7 @@ __global__ __launch_bounds__(NTH, 7) void convpool_wgrad_pair_k(const XSrc x,
       xs.fetch_rows(x, img0 + 2 * stride, B);
       ys.load(dP, arg, img0 + stride, B, tid);
     }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
     for (int it = wave; it < IMGS * RS; it += NTH / 64) {
       const int im = it / RS, s = it - im * RS;
       // dY operand: element j <-> window 16s + 2g + ((j>>1)&1) + 8(j>>2), dy = j&1
@@ -1304,6 +1307,7 @@ __global__ __launch_bounds__(NTH, 7) void convpool_wgrad_pair_k(const XSrc x,
         acc[mf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr, acc[mf], 0, 0, 0);
       }
     }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   }
   for (int wv = 0; wv < NTH / 64; ++wv) {
     __syncthreads();
@@ -1345,7 +1349,10 @@ __global__ __launch_bounds__(NTH, 7) void convpool_wgrad_pair_k(const XSrc x,
 // one image and streams the rows R once (LA rows read ahead), issuing for each the
 // MFMAs of every fragment it feeds: 3(2F+3) ds_read_b128 per wave instead of 15F --
 // the kernel is LDS-bandwidth bound (105 x 1 KB of A reads per image otherwise).
-template <class G, int IMGS, int DB = 0, int MINW = 1, int LA = 0>
+// PRIO (default; MNISTX_DGRAD_PRIO=0 off): s_setprio 1 around each wave's MFMA phase, so the
+// workgroups co-resident on a CU that are in their staging phase do not take the SIMD's
+// issue slots from the ones feeding the matrix pipe (cdna_hip_programming.md T5)
+template <class G, int IMGS, int DB = 0, int MINW = 1, int LA = 0, bool PRIO = false>
 __global__ __launch_bounds__(NTH, MINW) void convpool_dgrad_pair_k(const bf16_t* __restrict__ dP,
                                                              const uint8_t* __restrict__ arg,
                                                              const bf16_t* __restrict__ w, int B,
@@ -1451,6 +1458,7 @@ __global__ __launch_bounds__(NTH, MINW) void convpool_dgrad_pair_k(const bf16_t*
       bf16_t* oimg = outs + im * OUTE;
       auto run = [&](auto FC) {
         constexpr int FF = decltype(FC)::value;
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
         constexpr int NR = 2 * FF + 3;                 // rows R' = kh + 2j, kh 0..4, j < FF
         f32x4 acc[FF];
 #pragma unroll
@@ -1485,6 +1493,7 @@ __global__ __launch_bounds__(NTH, MINW) void convpool_dgrad_pair_k(const bf16_t*
             if (2 * jr < G::W) oimg[(ih * G::W + 2 * jr + sx) * 8 + ci] = f2bf(acc[j][r]);
           }
         }
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
       };
       constexpr int FMAX = (MFD + WPI - 1) / WPI, FMIN = MFD / WPI;
       static_assert(FMAX - FMIN <= 1, "");
@@ -1586,9 +1595,12 @@ hipError_t run_fwd(const XSrc& x, const bf16_t* w, const float* bias, int bias_n
 template <class G, int IMGS>
 hipError_t run_wgrad(const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B, float* slab, int grid,
                      hipStream_t st, const LrnFold& lrn = LrnFold{nullptr, 0.f, 0.f, 0.f}) {
+  // s_setprio 1 around the MFMA phase (see convpool_dgrad_pair_k); MNISTX_WGRAD_PRIO=0 turns it off
+  static const bool prio = [] { const char* e = getenv("MNISTX_WGRAD_PRIO"); return !(e && e[0] == '0'); }();
   if constexpr (G::PAIR) {
     if (lrn.p) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((convpool_wgrad_pair_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab);
+    if (prio) hipLaunchKernelGGL((convpool_wgrad_pair_k<G, IMGS, true>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab);
+    else hipLaunchKernelGGL((convpool_wgrad_pair_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab);
   } else if constexpr (G::COUT == 32) {
     if (lrn.p)
       hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS, true>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
@@ -1596,7 +1608,8 @@ hipError_t run_wgrad(const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B,
       hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
   } else {
     if (lrn.p) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
+    if (prio) hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS, false, true>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
+    else hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
   }
   return hipGetLastError();
 }
@@ -1618,8 +1631,12 @@ hipError_t run_dgrad(const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int 
   if (grid_cap > 0 && grid_cap < cap) cap = grid_cap;                                                      \
   hipLaunchKernelGGL((convpool_dgrad_pair_k<G, __VA_ARGS__>), dim3(grid_for(B, IM, cap)), dim3(NTH), 0, st, \
                      dP, arg, w, B, dx);
+  // MFMA-phase priority on by default (backward phase 348 -> 338-339 us with the wgrad
+  // kernels' own, profiles/r3/lenet/bwd_prio_ab.txt); MNISTX_DGRAD_PRIO=0 turns it off
+  static const bool prio = [] { const char* e = getenv("MNISTX_DGRAD_PRIO"); return !(e && e[0] == '0'); }();
   if (var == 0) { MNISTX_DG(IMGS, IMGS) }
   else if (var == 2) { MNISTX_DG(1, 1, 8, 4) }
+  else if (prio) { MNISTX_DG(2, 2, 0, 3, 1, true) }
   else { MNISTX_DG(2, 2, 0, 3, 1) }
 #undef MNISTX_DG
   return hipGetLastError();

@@ -5,8 +5,8 @@ Layout written under ``--train_dir`` (SURVEY.md §5.4)::
     checkpoint                           CheckpointState (text proto)
     model.ckpt-<step>.index              tensor-bundle SSTable
     model.ckpt-<step>.data-0000i-of-0000N
-    model.ckpt-<step>.meta               MetaGraphDef stand-in (JSON model spec)
-    graph.pbtxt                          graph description (text)
+    model.ckpt-<step>.meta               MetaGraphDef (variable graph; model description in any_info)
+    graph.pbtxt                          text GraphDef of the variable graph
 
 Variable names follow the reference graph: trainables (``conv1/weights``...),
 ``global_step``, weight-EMA shadows ``<var>/ExponentialMovingAverage``
@@ -14,21 +14,22 @@ Variable names follow the reference graph: trainables (``conv1/weights``...),
 zero-debiased loss averages ``<loss>/avg`` (+ ``/biased``, ``/local_step``;
 ``mnist_input.py:288-290``).  ``max_to_keep`` defaults to TF's 5.
 
-Deliberate deviation (parity unpinned): ``.meta`` and ``graph.pbtxt`` are NOT a
-serialized ``MetaGraphDef`` / ``GraphDef``.  There is no TF graph to serialize --
-the model is a static kernel plan over a ``ModelSpec`` -- and no TensorFlow in the
-image to check a hand-built proto against.  ``.meta`` is a JSON record of what a
-restore needs to rebuild the model (spec name, input channels, precision, mode,
-world size, flags, step); ``graph.pbtxt`` is a human-readable layer listing.  The
-reference's inference (``inference.py:86-91``) rebuilds its graph from code and
-reads only the ``checkpoint`` state file + ``.index``/``.data`` bundle, which ARE
-written in TF's tensor-bundle format, so file names and restore flow match; a
-TF tool that imports the ``.meta`` (``tf.train.import_meta_graph``) would not work.
+``.meta`` is a serialized ``MetaGraphDef`` of the checkpoint's VARIABLE graph
+(``ckpt/metagraph.py``: VariableV2 / initializer / Assign / read nodes and the
+``variables`` / ``trainable_variables`` / ``global_step`` collections, no
+saver_def), so ``tf.train.import_meta_graph`` + a default ``Saver`` can restore the
+bundle by name; the model description (architecture, input channels, precision,
+mode, step) rides in ``MetaInfoDef.any_info`` as JSON.  ``graph.pbtxt`` is the
+text ``GraphDef`` of the same graph.  There is no compute graph to serialize (the
+model is a static kernel plan over a ``ModelSpec``) and no TensorFlow in the image
+to import the result with: parity unpinned, structure pinned by decoding it
+(``tests/test_formats.py``).  The reference's inference (``inference.py:86-91``)
+rebuilds its graph from code and reads only the ``checkpoint`` state file +
+``.index``/``.data`` bundle, which are written in TF's tensor-bundle format.
 """
 from __future__ import annotations
 
 import dataclasses
-import json
 import os
 import re
 import time
@@ -37,6 +38,7 @@ from typing import Dict, List, Mapping, Optional
 import numpy as np
 
 from .bundle import read_bundle, read_index, write_bundle, data_path
+from .metagraph import build_meta_graph, graph_pbtxt, trainable_names
 
 
 @dataclasses.dataclass
@@ -102,8 +104,8 @@ class Saver:
         meta = dict(meta or {})
         meta.update({"global_step": int(step), "saved_at": time.time(),
                      "variables": {k: [str(np.asarray(v).dtype), list(np.shape(v))] for k, v in tensors.items()}})
-        with open(prefix + ".meta", "w") as f:
-            json.dump(meta, f, indent=1, sort_keys=True)
+        with open(prefix + ".meta", "wb") as f:
+            f.write(build_meta_graph(tensors, trainable_names(tensors), meta))
         st = get_checkpoint_state(train_dir)
         paths = [p for p in (st.all_model_checkpoint_paths if st else []) if p != prefix] + [prefix]
         while self.max_to_keep and len(paths) > self.max_to_keep:
@@ -126,10 +128,7 @@ class Saver:
         return read_bundle(prefix, names)
 
 
-def write_graph_pbtxt(train_dir: str, spec) -> None:
-    """Text stand-in for the GraphDef the TF saver hook writes (graph.pbtxt)."""
-    lines = []
-    for L in spec.layers:
-        lines.append(f'node {{ name: "{L.name}" op: "{type(L).__name__}" attr: "{dataclasses.asdict(L)}" }}')
+def write_graph_pbtxt(train_dir: str, tensors: Mapping[str, np.ndarray]) -> None:
+    """graph.pbtxt: the text GraphDef of the checkpoint's variable graph (ckpt/metagraph.py)."""
     with open(os.path.join(train_dir, "graph.pbtxt"), "w") as f:
-        f.write("\n".join(lines) + "\n")
+        f.write(graph_pbtxt(tensors))

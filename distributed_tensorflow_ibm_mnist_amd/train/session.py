@@ -47,7 +47,7 @@ class MonitoredTrainingSession:
                 self.hooks.append(CheckpointSaverHook(save_checkpoint_secs, save_checkpoint_steps))
             if save_summaries_steps:
                 self.hooks.append(SummarySaverHook(self._writer, save_summaries_steps))
-            write_graph_pbtxt(checkpoint_dir, replica.spec)
+            write_graph_pbtxt(checkpoint_dir, state_tensors(replica.net))
         if is_chief and log_step_count_steps:
             self.hooks.append(StepCounterHook(log_step_count_steps, self._writer, replica.examples_per_step, log))
 

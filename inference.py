@@ -18,7 +18,6 @@ count (gray replicated to 3 for the DLI-layout model) and normalised exactly as 
 training (``x/255 - 0.5``); ``--per_image_standardization`` restores the reference's
 preprocessing for parity experiments.
 """
-import json
 import os
 import sys
 import time
@@ -74,9 +73,8 @@ def predict(FLAGS):
     if not (ckpt and ckpt.model_checkpoint_path):
         raise SystemExit(f"no checkpoint found in {FLAGS.model!r}")
     prefix = ckpt.model_checkpoint_path
-    meta = {}
-    if os.path.exists(prefix + ".meta"):
-        meta = json.load(open(prefix + ".meta"))
+    from distributed_tensorflow_ibm_mnist_amd.ckpt.metagraph import read_meta_json
+    meta = read_meta_json(prefix + ".meta") if os.path.exists(prefix + ".meta") else {}
     arch = FLAGS.arch or meta.get("model", "reference_cnn")
     cin = FLAGS.in_channels or int(meta.get("in_channels", 3))
     spec = models.get_model(arch, cin)

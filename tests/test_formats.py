@@ -171,3 +171,48 @@ def test_feistel_epoch_permutation_and_sharding():
         l1b.next()
     l2.next(); l1b.next()
     assert torch.equal(l2.out_labels, l1b.out_labels)
+
+
+def test_meta_graph_def_structure(tmp_path):
+    """model.ckpt-N.meta is a MetaGraphDef of the checkpoint's variable graph: one VariableV2
+    (+ initializer / Assign / read) per saved tensor with its dtype and shape, the variables /
+    trainable_variables / global_step collections of VariableDef records, the model
+    description as JSON in MetaInfoDef.any_info; graph.pbtxt is the same graph as text.
+    (Parity unpinned: no TensorFlow here to import it -- the structure is decoded by hand.)"""
+    import numpy as np
+    from distributed_tensorflow_ibm_mnist_amd.ckpt import metagraph as mg
+    from distributed_tensorflow_ibm_mnist_amd.ckpt.saver import Saver, write_graph_pbtxt
+    from distributed_tensorflow_ibm_mnist_amd.utils.proto import to_dict
+    t = {"conv1/weights": np.zeros((5, 5, 1, 32), np.float32), "conv1/biases": np.ones(32, np.float32),
+         "conv1/weights/ExponentialMovingAverage": np.zeros((5, 5, 1, 32), np.float32),
+         "global_step": np.array(7, np.int64), "total_loss/avg": np.array(0.5, np.float32)}
+    prefix = Saver().save(str(tmp_path), 7, t, meta={"model": "reference_cnn", "in_channels": 1})
+    raw = open(prefix + ".meta", "rb").read()
+    top = to_dict(raw)
+    nodes = [to_dict(n) for n in to_dict(top[2][0])[1]]
+    by_name = {n[1][0].decode(): n for n in nodes}
+    assert len(nodes) == 4 * len(t)
+    v = by_name["conv1/weights"]
+    assert v[2][0] == b"VariableV2"
+    attrs = {to_dict(a)[1][0].decode(): to_dict(to_dict(a)[2][0]) for a in v[5]}
+    assert attrs["dtype"][6][0] == mg.DT_FLOAT
+    dims = [to_dict(d)[1][0] for d in to_dict(attrs["shape"][7][0])[2]]
+    assert dims == [5, 5, 1, 32]
+    gs = {to_dict(a)[1][0].decode(): to_dict(to_dict(a)[2][0]) for a in by_name["global_step"][5]}
+    assert gs["dtype"][6][0] == mg.DT_INT64 and 2 not in to_dict(gs["shape"][7][0])   # scalar
+    assert [i.decode() for i in by_name["conv1/biases/Assign"][3]] == ["conv1/biases", "conv1/biases/Initializer/zeros"]
+    colls = {to_dict(c)[1][0].decode(): to_dict(c)[2][0] for c in top[4]}
+    assert set(colls) == {"variables", "trainable_variables", "global_step"}
+
+    def var_names(c):
+        return [to_dict(d)[1][0].decode() for d in to_dict(to_dict(c)[2][0])[1]]
+    assert sorted(var_names(colls["trainable_variables"])) == ["conv1/biases:0", "conv1/weights:0"]
+    assert len(var_names(colls["variables"])) == len(t)
+    assert mg.read_meta_json(prefix + ".meta")["in_channels"] == 1
+    write_graph_pbtxt(str(tmp_path), t)
+    txt = open(tmp_path / "graph.pbtxt").read()
+    assert txt.count("node {") == 4 * len(t) and 'op: "VariableV2"' in txt and "producer: 134" in txt
+    # a round-1/2 checkpoint's JSON .meta still reads
+    old = tmp_path / "old.meta"
+    old.write_text('{"model": "lenet5", "in_channels": 1}')
+    assert mg.read_meta_json(str(old))["model"] == "lenet5"

@@ -21,10 +21,47 @@ def short(name: str) -> str:
     return base + tmpl
 
 
+def step_windows(d: str, steps: int):
+    """Per-kernel (calls, total ns) inside the training steps, from the kernel trace:
+    the step boundaries are the launches of the earliest kernel that runs exactly once per
+    step; everything before the first boundary (dataset upload, buffer fills, clock
+    prewarm) is setup.  The last step runs to the trace's end."""
+    tr = glob.glob(os.path.join(d, "*kernel_trace.csv"))
+    if not tr:
+        return None
+    rows = sorted(csv.DictReader(open(tr[0])), key=lambda r: int(r["Start_Timestamp"]))
+    count: dict = {}
+    first: dict = {}
+    for r in rows:
+        n = r["Kernel_Name"]
+        count[n] = count.get(n, 0) + 1
+        first.setdefault(n, int(r["Start_Timestamp"]))
+    once = [n for n, c in count.items() if c == steps]
+    if not once:
+        return None
+    k0 = min(once, key=lambda n: first[n])
+    t0 = first[k0]
+    agg: dict = {}
+    setup_ns = 0
+    for r in rows:
+        dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        if int(r["Start_Timestamp"]) < t0:
+            setup_ns += dur
+            continue
+        c, t = agg.get(r["Kernel_Name"], (0, 0))
+        agg[r["Kernel_Name"]] = (c + 1, t + dur)
+    return agg, setup_ns
+
+
 def main():
     d, steps = sys.argv[1], int(sys.argv[2])
-    f = glob.glob(os.path.join(d, "*kernel_stats.csv"))[0]
-    rows = list(csv.DictReader(open(f)))
+    win = step_windows(d, steps)
+    if win is not None:
+        agg, setup_ns = win
+        rows = [{"Name": n, "Calls": str(c), "TotalDurationNs": str(t), "AverageNs": str(t / c)} for n, (c, t) in agg.items()]
+    else:
+        f = glob.glob(os.path.join(d, "*kernel_stats.csv"))[0]
+        rows, setup_ns = list(csv.DictReader(open(f))), 0
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     lines = ["| kernel | calls | avg us | per-step us | share |", "|---|---|---|---|---|"]
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
@@ -34,6 +71,9 @@ def main():
         lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | "
                      f"{t/1e3/steps:.1f} | {100*t/tot:.1f}% |")
     lines.append(f"| **total GPU time / step** | | | **{tot/1e3/steps:.1f}** | |")
+    if setup_ns:
+        lines.append(f"| _setup before the first step (dataset upload, fills, prewarm): not in the total_ | | | "
+                     f"_{setup_ns/1e3:.1f} us in all_ | |")
     out = "\n".join(lines)
     print(out)
     if len(sys.argv) > 3:

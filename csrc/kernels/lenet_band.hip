@@ -14,8 +14,15 @@
 //
 // v_mfma_f32_32x32x16_bf16, columns = 32 = 16 images x 2 output-row parities
 // (ypar = column & 1), rows = output features:
-//  * conv1 rows = (xq 2, xpar 2, c 8): the four consecutive output columns
-//    x = 4u + 2xq + xpar of window u; K = 16 = (dy parity h, 8 input columns
+//  * conv1 (default, INL): rows = (window position g = 2 ypar + xpar, channel 3+1 per
+//    lane half), columns = (pooled row half, image, pooled column parity xq); K = 16 =
+//    (input row parity h, 8 input columns from 4u + 2xq - 2): 3 k-steps cover the 6
+//    input rows of a pooled row.  Each lane then holds the 4 positions of its windows
+//    in 4 registers: the pool is 3 v_max in the lane, no cross-lane exchange, and the
+//    padded channels are never pooled (47 VALU per 3 MFMAs against 85 for the layout
+//    below; band kernel 201 -> 161 us, profiles/r3/lenet/inlane/).
+//  * conv1 (MNISTX_BAND_INLANE=0): rows = (xq 2, xpar 2, c 8): the four consecutive output
+//    columns x = 4u + 2xq + xpar of window u; K = 16 = (dy parity h, 8 input columns
 //    x' = 4u-2 .. 4u+5): one k-step covers TWO kernel rows, so 3 k-steps = dy 0..4
 //    (+ one zero row).  3 MFMAs per (pooled row, window), 3 A fragments in total.
 //  * conv2 rows = (xpar 2, c2 16) of ONE pooled column x2p; K = 16 = 2 input
@@ -69,6 +76,11 @@ DEV float embed(float v, uint32_t d) { return __uint_as_float((__float_as_uint(v
 DEV float vmax(float a, float b) {  // bare v_max_f32 (fmaxf adds NaN-canonicalising moves)
   float r;
   asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+DEV float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
 // value of the neighbouring lane (lane ^ 1): the other output-row parity of the same image
@@ -160,7 +172,7 @@ struct XFill {
 // Warp-specialised pipeline over the block's tiles k = 0..nk-1 (tile blockIdx + k * grid):
 // iteration k: conv1 waves turn input[k%2] into pool1[k%2] (and load tile k+1's input),
 // conv2 waves turn pool1[(k-1)%2] into pool2 -- one barrier per iteration, nk+1 iterations.
-template <bool P1OUT>
+template <bool P1OUT, bool INL>
 __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_X + LDS_P];
   bf16_t* xs = lds;
@@ -181,7 +193,138 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
   for (int e = tid; e < LDS_X / 8; e += NTH) *(u32x4*)(xs + 8 * e) = u32x4{0u, 0u, 0u, 0u};
   __syncthreads();
 
-  if (wave < 4) {
+  if (wave < 4 && INL) {
+    // ================================================================ conv1 + pool1 role, in-lane pooling
+    // rows m = 8 g + 4 hh + i4: window position g = 2 ypar + xpar (= the argmax code), channel
+    // c = ch(hh, i4) (3 per lane half, i4 = 3 is padding), so C register 4 g + i4 of a lane
+    // holds all four positions of ONE 2x2 window: the pool is 3 v_max in the lane (no DPP,
+    // no keep/send selects) and the padded channels 6-7 are never computed on.
+    // columns = (half, img, xq): pooled pixel (yp0 + 7 half, 2u + xq) of image img.
+    // B of column xq starts at input column 4u + 2xq - 2: 4-byte aligned for xq = 1, so a
+    // fragment is two ds_read2_b32 (an 8-byte read off its alignment would replay).
+    const int t = tid;
+    if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
+    // channel of C row (hh, i4): h = 0 holds 0,1,2; h = 1 holds 4,5,3 (so each lane's first
+    // pair packs to its own 8-byte store and channel 3 moves to the h = 0 lane); -1: pad
+    auto chan = [](int hh, int i4) { return i4 == 3 ? -1 : (hh == 0 ? i4 : (i4 == 2 ? 3 : 4 + i4)); };
+    bf16x8 a1[3];
+    {
+      const int g = col >> 3, ypr = g >> 1, xpr = g & 1, c = chan((col >> 2) & 1, col & 3);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int dy = 2 * p + h - ypr, dx = j - xpr;
+          const bool ok = c >= 0 && dy >= 0 && dy <= 4 && dx >= 0 && dx <= 4;
+          a1[p][j] = __builtin_bit_cast(__bf16, w1s[ok ? (dy * 5 + dx) * 8 + c : W1E]);
+        }
+      }
+    }
+    float bias1[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int c = chan(h, i);
+      bias1[i] = c < a.b1n ? a.b1[c] : 0.f;
+    }
+    const int xq = col & 1;
+    const auto rx = a.u8 ? buf_rsrc(a.u8, (uint32_t)a.n * XIMG) : buf_rsrc(a.x, (uint32_t)a.n * (XIMG * 2));
+    // B rows: input row 2 yp - 2 + 2p + h = plane h, row yp0 + 7 half - 1 + p; column 4u + 2xq
+    // (x' = 4u + 2xq - 2 with the 2-column left pad)
+    const int xlane = img * XIS + h * XPL + (7 * half - 1) * XRW + 2 * xq;
+    const bool top = half == 0, bot = half == 1;   // lanes whose p = 0 / p = 2 row can be padding
+    // pool1 store: lane part + the (yp0 parity, half) part of pooled row yp = yp0 + 7 half
+    const int store_lane = img * PIS + 8 * xq + 4 * h;
+    const int row_even = half ? PPL + 3 * PRW : 0;   // yp0 even
+    const int row_odd = half ? 4 * PRW : PPL;        // yp0 odd
+    // code word: byte k = code(c = k) | code(c = k + 4) << 4; channels 6-7 are padding (code 4)
+    const uint32_t sh0 = h ? 4u : 0u, sh1 = h ? 12u : 8u, sh2 = h ? 24u : 16u, kc = h ? 0x40400000u : 0u;
+    XFill xf;
+    xf.load(rx, a, nk > 0 ? tile0(0) : -1, t);
+    xf.store(xs, t, a.u8 != nullptr);
+
+    uint64_t busy = 0, wait = 0, tw = __builtin_amdgcn_s_memtime();
+    for (int k = 0; k <= nk; ++k) {
+      __syncthreads();
+      const uint64_t tb = __builtin_amdgcn_s_memtime();
+      wait += tb - tw;
+      if (k < nk) {
+        const bf16_t* xb = xs + (k & 1) * XBUF + xlane;
+        bf16_t* pb = p1s + (k & 1) * PBUF + store_lane;
+        xf.load(rx, a, k + 1 < nk ? tile0(k + 1) : -1, t);
+        struct Frags { bf16x8 b[3]; };
+        auto fetch = [&](int j) {
+          const int f = min(wave + 4 * j, U1 - 1), yp0 = f / 7, u = f - 7 * yp0;
+          const bf16_t* base = xb + yp0 * XRW + 4 * u;
+          Frags fr;
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            const bf16_t* rp = base + p * XRW;
+            if (p == 0 && yp0 == 0) rp = top ? xs + XZERO : rp;   // input rows -2, -1
+            if (p == 2 && yp0 == 6) rp = bot ? xs + XZERO : rp;   // input rows 28, 29
+            const uint32_t* q = (const uint32_t*)rp;
+            fr.b[p] = as_frag(u32x4{q[0], q[1], q[2], q[3]});
+          }
+          return fr;
+        };
+        auto window = [&](const Frags& fr) {
+          f32x16 acc = {};
+#pragma unroll
+          for (int p = 0; p < 3; ++p) acc = mfma32(a1[p], fr.b[p], acc);
+          return acc;
+        };
+        auto epilogue = [&](const f32x16& acc, int j) {
+          const int f = wave + 4 * j, yp0 = f / 7, u = f - 7 * yp0;
+          float o[3];
+          uint32_t cw = kc;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            if constexpr (P1OUT) {
+              const float v = vmax(vmax3(__uint_as_float(__float_as_uint(acc[i]) & ~3u), embed(acc[4 + i], 1u),
+                                         embed(acc[8 + i], 2u)), embed(acc[12 + i], 3u));
+              o[i] = vmax(__uint_as_float(__float_as_uint(v) & ~3u) + bias1[i], 0.f);
+              const uint32_t cd = o[i] > 0.f ? (__float_as_uint(v) & 3u) : ARG_OFF;
+              cw |= cd << (i == 0 ? sh0 : i == 1 ? sh1 : sh2);
+            } else {
+              o[i] = vmax(vmax(vmax3(acc[i], acc[4 + i], acc[8 + i]), acc[12 + i]) + bias1[i], 0.f);
+            }
+          }
+          const uint32_t w0 = pk2(o[0], o[1]);
+          uint32_t w1;
+          if constexpr (P1OUT) {
+            const uint32_t X = h ? __float_as_uint(o[2]) : cw;
+            const auto sw = __builtin_amdgcn_permlane32_swap(X, X, false, false);
+            w1 = h ? (cw | sw[0]) : pk2(o[2], __uint_as_float(sw[1]));
+          } else {   // channels 6-7 stay 0 (zero weights in conv2)
+            const uint32_t X = __float_as_uint(o[2]);
+            const auto sw = __builtin_amdgcn_permlane32_swap(X, X, false, false);
+            w1 = h ? 0u : pk2(o[2], __uint_as_float(sw[1]));
+          }
+          if (f < U1) {
+            const int off = (yp0 & 1 ? row_odd : row_even) + (yp0 >> 1) * PRW + 16 * u;
+            *(u32x2*)(pb + off) = u32x2{w0, w1};
+          }
+        };
+        Frags fa = fetch(0), fb = fetch(1);
+        f32x16 acca = window(fa), accb;
+#pragma unroll 1
+        for (int j = 0; j < 14; j += 2) {
+          fa = fetch(j + 2);
+          accb = window(fb);
+          epilogue(acca, j);
+          fb = fetch(j + 3);
+          acca = window(fa);
+          epilogue(accb, j + 1);
+        }
+        xf.store(xs + ((k + 1) & 1) * XBUF, t, a.u8 != nullptr);
+      }
+      tw = __builtin_amdgcn_s_memtime();
+      busy += tw - tb;
+    }
+    if (a.prof && lane == 0) {
+      atomicAdd(a.prof + 0, (unsigned long long)busy);
+      atomicAdd(a.prof + 2, (unsigned long long)wait);
+    }
+  } else if (wave < 4) {
     // ================================================================ conv1 + pool1 role
     const int t = tid;                                   // 0..255
     if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
@@ -419,7 +562,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
   }
 }
 
-template <bool P1OUT>
+template <bool P1OUT, bool INL>
 int fwd_grid(int ntiles) {
   static int per_cu = -1, cus = 0;
   if (per_cu < 0) {
@@ -429,7 +572,7 @@ int fwd_grid(int ntiles) {
     if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return -1;
     cus = prop.multiProcessorCount;
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lenet_band_fwd_k<P1OUT>, NTH, 0) != hipSuccess) return -1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lenet_band_fwd_k<P1OUT, INL>, NTH, 0) != hipSuccess) return -1;
     per_cu = nb > 0 ? nb : 1;
   }
   return ntiles < per_cu * cus ? ntiles : per_cu * cus;
@@ -448,15 +591,19 @@ hipError_t lenet_band_fwd(const XSrc& x, const bf16_t* w1, const float* b1, int 
   static const int prio = [] { const char* e = getenv("MNISTX_BAND_PRIO"); return e ? atoi(e) : 1; }();
   BandFwd a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, w1, b1, b1n, w2, b2, B, p1, arg1, p2, arg2, prof, prio};
   const int ntiles = (B + BT - 1) / BT;
-  if (p1) {
-    const int grid = fwd_grid<true>(ntiles);
+  // conv1 pooling in the lane (INL, default) or across lane pairs; MNISTX_BAND_INLANE=0 for A/B
+  static const bool inl = [] { const char* e = getenv("MNISTX_BAND_INLANE"); return !e || atoi(e) != 0; }();
+  auto go = [&](auto ker, int grid) {
     if (grid <= 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(lenet_band_fwd_k<true>, dim3(grid), dim3(NTH), 0, st, a);
-  } else {
-    const int grid = fwd_grid<false>(ntiles);
-    if (grid <= 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(lenet_band_fwd_k<false>, dim3(grid), dim3(NTH), 0, st, a);
-  }
+    hipLaunchKernelGGL(ker, dim3(grid), dim3(NTH), 0, st, a);
+    return hipSuccess;
+  };
+  hipError_t e;
+  if (p1) e = inl ? go(lenet_band_fwd_k<true, true>, fwd_grid<true, true>(ntiles))
+                  : go(lenet_band_fwd_k<true, false>, fwd_grid<true, false>(ntiles));
+  else e = inl ? go(lenet_band_fwd_k<false, true>, fwd_grid<false, true>(ntiles))
+               : go(lenet_band_fwd_k<false, false>, fwd_grid<false, false>(ntiles));
+  if (e != hipSuccess) return e;
   return hipGetLastError();
 }
 

@@ -148,6 +148,33 @@ struct XFill {
       else v[i] = buf_b64(rx, r < 196 ? base + 8u * r : BUF_OOB);
     }
   }
+  // LDS element offsets of this thread's chunks inside an input slot (tile-invariant:
+  // computed once, so a tile's store is 7 ds_write2_b32 with no index arithmetic)
+  int off[FCH];
+  DEV void init(int t) {
+#pragma unroll
+    for (int i = 0; i < FCH; ++i) {
+      const int r = (t & 31) + 32 * i, y = r / 7, k = r - 7 * y;
+      off[i] = (t >> 5) * XIS + 2 + (y & 1) * XPL + (y >> 1) * XRW + 4 * k;
+    }
+  }
+  DEV void store_pre(bf16_t* xb, int t, bool u8) const {
+#pragma unroll
+    for (int i = 0; i < FCH; ++i) {
+      const int r = (t & 31) + 32 * i;
+      if (r < 196) {
+        uint32_t* d = (uint32_t*)(xb + off[i]);
+        uint32_t lo = v[i][0], hi = v[i][1];
+        if (u8) {
+          const uint32_t b = v[i][0];
+          lo = pack2(u8_norm(b & 0xff), u8_norm((b >> 8) & 0xff));
+          hi = pack2(u8_norm((b >> 16) & 0xff), u8_norm(b >> 24));
+        }
+        d[0] = lo;
+        d[1] = hi;
+      }
+    }
+  }
   DEV void store(bf16_t* xb, int t, bool u8) const {
     bf16_t* im = xb + (t >> 5) * XIS + 2;
 #pragma unroll
@@ -239,8 +266,9 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
     // code word: byte k = code(c = k) | code(c = k + 4) << 4; channels 6-7 are padding (code 4)
     const uint32_t sh0 = h ? 4u : 0u, sh1 = h ? 12u : 8u, sh2 = h ? 24u : 16u, kc = h ? 0x40400000u : 0u;
     XFill xf;
+    xf.init(t);
     xf.load(rx, a, nk > 0 ? tile0(0) : -1, t);
-    xf.store(xs, t, a.u8 != nullptr);
+    xf.store_pre(xs, t, a.u8 != nullptr);
 
     uint64_t busy = 0, wait = 0, tw = __builtin_amdgcn_s_memtime();
     for (int k = 0; k <= nk; ++k) {
@@ -315,7 +343,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
           acca = window(fa);
           epilogue(accb, j + 1);
         }
-        xf.store(xs + ((k + 1) & 1) * XBUF, t, a.u8 != nullptr);
+        xf.store_pre(xs + ((k + 1) & 1) * XBUF, t, a.u8 != nullptr);
       }
       tw = __builtin_amdgcn_s_memtime();
       busy += tw - tb;
@@ -471,6 +499,8 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
     const int ce = img * PIS + ypar * PPL + 8 * h, co = img * PIS + (1 - ypar) * PPL + ypar * PRW + 8 * h;
     const uint32_t d0 = 2u * ypar, d1 = d0 + 1u;
     const int w2v = wave - 4;
+    const int cp_r = (t + 192) & 255;   // copy-out pixel of this thread (>= 196: none)
+    const int cp_lds = ((cp_r / 14) & 1) * PPL + ((cp_r / 14) >> 1) * PRW + (cp_r % 14) * 8;
     uint64_t busy = 0, wait = 0, tw = __builtin_amdgcn_s_memtime();
     for (int k = 0; k <= nk; ++k) {
       __syncthreads();   // pool1[(k-1)%2] complete
@@ -481,7 +511,29 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
       const int t0 = tile0(k - 1), gi = t0 + img;
       const bool iv = gi < a.B;
       const bf16_t* pb = p1s + ((k - 1) & 1) * PBUF;
-      if constexpr (P1OUT) {   // pool1 + argmax codes to HBM for the backward kernels
+      if constexpr (P1OUT && INL) {   // pool1 + argmax codes to HBM for the backward kernels
+        // copy thread ct owns pooled pixel ct (< 196) of every image of the tile: one LDS
+        // offset per thread, image strides as instruction / scalar offsets (no per-element
+        // index arithmetic).  ct is rotated so the wave with 4 conv2 units copies least.
+        if (cp_r < 196) {
+          const int nimg = min(BT, a.B - t0);
+          const auto rp1 = buf_rsrc(a.p1 + (int64_t)t0 * P1E, (uint32_t)nimg * (P1E * 2));
+          const auto ra1 = buf_rsrc(a.arg1 + (int64_t)t0 * 784, (uint32_t)nimg * 784);
+          const bf16_t* src = pb + cp_lds;
+#pragma unroll
+          for (int i0 = 0; i0 < BT; i0 += 4) {
+            u32x4 cv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cv[i] = *(const u32x4*)(src + (i0 + i) * PIS);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              __builtin_amdgcn_raw_buffer_store_b128(u32x4{cv[i][0], cv[i][1], cv[i][2], 0u}, rp1, (uint32_t)cp_r * 16u,
+                                                     (i0 + i) * (P1E * 2), 0);
+              __builtin_amdgcn_raw_buffer_store_b32(cv[i][3], ra1, (uint32_t)cp_r * 4u, (i0 + i) * 784, 0);
+            }
+          }
+        }
+      } else if constexpr (P1OUT) {
         constexpr int NV = BT * 196;
         const int nimg = min(BT, a.B - t0);
         const auto rp1 = buf_rsrc(a.p1 + (int64_t)t0 * P1E, (uint32_t)nimg * (P1E * 2));

@@ -9,8 +9,12 @@ Modes:
   Q10; we treat it as synchronous data parallel);
 * **ps** — ``--ps_hosts`` + ``--worker_hosts`` + ``--job_name`` + ``--task_id``:
   1..k parameter-server ranks followed by the workers
-  (rank(ps k) = k, rank(worker i) = num_ps + i), rendezvous at the first PS
-  ``host:port`` (TCPStore), RCCL (``nccl``) between GPU processes, gloo on CPU.
+  (rank(ps k) = k, rank(worker i) = num_ps + i), a gloo control group over a
+  TCPStore hosted by the CHIEF (worker 0's ``host:port``), so the store outlives a
+  parameter server: a restarted PS opens the next *session generation* (a fresh
+  ``PrefixStore`` namespace) and the surviving processes rejoin it in place
+  (``rejoin`` below; ``MonitoredTrainingSession``'s session recreation,
+  ``/root/reference/main.py:140-146`` [TF1-lib]).
 
 Device: one process per GPU; ``LOCAL_RANK`` if set, else rank modulo the
 visible device count.
@@ -41,6 +45,9 @@ class Cluster:
     device: Optional[torch.device] = None
     backend: str = ""
     transport: str = ""             # PS-mode data plane (ipc | host)
+    store: Optional[object] = None  # PS mode: the chief-hosted TCPStore (survives PS restarts)
+    gen: int = 0                    # PS mode: session generation of the current control group
+    timeout: Optional[datetime.timedelta] = None
 
     @property
     def is_chief(self) -> bool:
@@ -89,6 +96,38 @@ def _attempt_store(rank: int, world: int, timeout: datetime.timedelta):
     return dist.PrefixStore(f"mnistx/attempt{attempt}", store)
 
 
+GEN_KEY = "mnistx/gen"
+
+
+def _gen_prefix(gen: int) -> str:
+    return f"mnistx/gen{gen}"
+
+
+def _ps_store(cl: "Cluster", to: datetime.timedelta):
+    """PS mode: the TCPStore lives in the chief (worker 0), which every recovery needs
+    alive anyway; parameter servers and the other workers are clients."""
+    host, _, port = cl.master.rpartition(":")
+    is_master = cl.job_name == "worker" and cl.task_id == 0
+    return dist.TCPStore(host, int(port), is_master=is_master, timeout=to, wait_for_workers=False)
+
+
+def rejoin(cl: "Cluster", gen: int) -> None:
+    """Leave the current control group and join session generation ``gen`` (every
+    rank of the job does, the restarted PS included); blocks until all have."""
+    if dist.is_initialized():
+        try:
+            dist.destroy_process_group()
+        except Exception:                       # a dead peer's pairs may not close cleanly
+            pass
+    dist.init_process_group("gloo", store=dist.PrefixStore(_gen_prefix(gen), cl.store), rank=cl.rank,
+                            world_size=cl.world, timeout=cl.timeout)
+    cl.gen = gen
+
+
+def current_gen(cl: "Cluster") -> int:
+    return int(cl.store.add(GEN_KEY, 0))
+
+
 def setup_distribute(job_name: str = "", ps_hosts: str = "", worker_hosts: str = "", task_id: int = 0,
                      want_gpu: bool = True, timeout_s: float = 600.0, log=print,
                      ps_backend: str = "", dp_backend: str = "") -> Cluster:
@@ -107,7 +146,7 @@ def setup_distribute(job_name: str = "", ps_hosts: str = "", worker_hosts: str =
                 raise ValueError(f"task_id {cl.task_id} out of range for job {cl.job_name} ({n} tasks)")
             cl.rank = cl.task_id if cl.job_name == "ps" else len(ps) + cl.task_id
             cl.world = len(ps) + len(workers)
-            cl.master = _norm_host(ps[0])
+            cl.master = _norm_host(workers[0])
         else:
             if cl.job_name == "ps":
                 raise ValueError("job_name=ps without --ps_hosts")
@@ -130,6 +169,17 @@ def setup_distribute(job_name: str = "", ps_hosts: str = "", worker_hosts: str =
             cl.transport = t or default_transport(cl.device)
         if cl.device.type == "cuda":
             torch.cuda.set_device(cl.device)
+        cl.timeout = to
+        if cl.mode == "ps":
+            cl.store = _ps_store(cl, to)
+            gen = 0
+            if cl.job_name == "ps" and cl.store.add(f"mnistx/ps{cl.task_id}/starts", 1) > 1:
+                # a restarted parameter server: open the next session generation; the
+                # surviving workers / PS tasks notice the failure and rejoin it
+                gen = int(cl.store.add(GEN_KEY, 1))
+                log(f"[ps {cl.task_id}] restarted: opening session generation {gen}")
+            rejoin(cl, gen)
+            return cl
         kw = {"device_id": cl.device} if cl.backend == "nccl" else {}
         dist.init_process_group(cl.backend, init_method=f"tcp://{cl.master}", rank=cl.rank, world_size=cl.world,
                                 timeout=to, **kw)

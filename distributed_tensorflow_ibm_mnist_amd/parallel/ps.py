@@ -64,8 +64,28 @@ PS raises ``PushIntegrityError`` naming the worker (fault injection:
 and a cluster where any pair lacks it falls back to ``host`` with the reason
 logged (``MNISTX_PS_STRICT=1`` makes that an error).
 
-Control words (int64[8]) worker -> PS: (kind, want_state, worker_local_step);
-PS -> worker: (global_step, stop, applied).
+Control words (int64[8]) worker -> PS: (kind, want_state, worker_local_step,
+new generation for RESET); PS -> worker: (global_step, stop, applied).
+
+Session recovery (``MonitoredTrainingSession`` recreates its session on
+``AbortedError`` / ``UnavailableError``, and the workers outlive a PS restart:
+``/root/reference/main.py:140-146`` [TF1-lib]).  The control store lives in the
+chief (``cluster.py``), so it outlives any parameter server.  When a PS dies, the
+workers keep their processes, their hipGraphs and their input position:
+
+1. a worker's exchange fails on the dead peer (gloo connection error);
+2. the PS is restarted (``parallel/supervisor.py`` relaunches just that process,
+   or an operator does): it restores its shard from the latest checkpoint and
+   opens session generation g+1 in the store;
+3. the worker waits for g+1, sends RESET(g+1) to every PS on the old group (the
+   surviving PS tasks are blocked in their any-source receive there; the dead one
+   just errors), and every rank joins generation g+1 and sets the data plane up again;
+4. the worker re-sends the interrupted exchange -- as a parameter pull only to the
+   PS tasks that already took its gradient, so no push is applied twice.
+
+Surviving PS tasks keep their parameters and step counts; the restarted one resumes
+from the checkpoint (TF's PS recovery made the same promise).  Not covered: two PS
+tasks restarting at once, or a worker dying (the supervisor restarts the whole job).
 """
 from __future__ import annotations
 
@@ -81,7 +101,8 @@ import torch.distributed as dist
 
 from ..runtime.params import FlatParams, OptConfig
 
-HELLO, GRAD, STATE, DONE = 0, 1, 2, 3
+HELLO, GRAD, STATE, DONE, RESET = 0, 1, 2, 3, 4
+FATAL_KEY = "mnistx/fatal"      # set by a PS that stops on an error no restart would fix
 CTRL = 8
 TAG_CTRL, TAG_DATA = 1, 2
 
@@ -341,10 +362,12 @@ def setup_transport(name: str, group, num_ps: int, num_workers: int, ps=None, de
 class ParameterServer:
     def __init__(self, ps_index: int, num_ps: int, num_workers: int, specs, init: Dict[str, torch.Tensor],
                  opt: OptConfig, device, max_steps: int, restore: Optional[Dict[str, np.ndarray]] = None,
-                 log=print, transport: str = "", group=None):
+                 log=print, transport: str = "", group=None, cluster=None):
         self.j, self.k, self.W = ps_index, num_ps, num_workers
         self.device = torch.device(device)
         self.group = group
+        self.cluster = cluster
+        self.transport_name = transport
         full = FlatParams.build(specs, {}, "cpu")
         self.start, self.end, self.names = shard_ranges(full, num_ps)[ps_index]
         mine = [s for s in specs if s[0] in self.names]
@@ -355,8 +378,9 @@ class ParameterServer:
         # T6 fault injection: MNIST_FI_KILL_RANK_AT_STEP=r:k SIGKILLs this PS (rank r) at global step k
         # (attempt 0 only, like train/hooks.FaultInjectionHook, unless MNIST_FI_EVERY_ATTEMPT=1)
         kr = os.environ.get("MNIST_FI_KILL_RANK_AT_STEP", "")
-        if int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")) > 0 and \
-                os.environ.get("MNIST_FI_EVERY_ATTEMPT", "0") != "1":
+        restarted = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")) > 0 or \
+            os.environ.get("MNISTX_PS_RESTART", "0") == "1"
+        if restarted and os.environ.get("MNIST_FI_EVERY_ATTEMPT", "0") != "1":
             kr = ""
         self._kill = tuple(int(v) for v in kr.split(":")) if ":" in kr else (-1, -1)
         self.global_step = 0
@@ -406,7 +430,30 @@ class ParameterServer:
         dist.send(c, r, group=self.group, tag=TAG_CTRL)
         self.tx.ps_after_ctrl(self, r, want_state)
 
+    def _rejoin(self, gen: int, r: int) -> None:
+        from .cluster import rejoin
+        if self.cluster is None or gen <= self.cluster.gen:
+            return                        # a stale RESET (this generation is already joined)
+        self.log(f"[ps {self.j}] worker {r - self.k} reports a restarted parameter server: "
+                 f"rejoining session generation {gen} at global step {self.global_step}")
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        rejoin(self.cluster, gen)
+        self.tx = setup_transport(self.transport_name or default_transport(self.device), self.group, self.k,
+                                  self.W, ps=self, device=self.device, log=self.log)
+        self.rejoins = getattr(self, "rejoins", 0) + 1
+
     def serve(self) -> Dict[str, int]:
+        """``_serve`` on the PS stream; a ``PushIntegrityError`` is published to the
+        store first, so the workers stop instead of waiting for a recovery."""
+        try:
+            return self._serve_stream()
+        except PushIntegrityError as e:
+            if self.cluster is not None and self.cluster.store is not None:
+                self.cluster.store.set(FATAL_KEY, f"PS {self.j}: {e}")
+            raise
+
+    def _serve_stream(self) -> Dict[str, int]:
         """Run until every worker has sent DONE, serving workers in arrival order.
 
         On a GPU the PS works on a high-priority stream (``MNISTX_PS_PRIORITY=0`` turns
@@ -441,6 +488,9 @@ class ParameterServer:
             kind, want_state, wstep = int(c[0]), bool(c[1]), int(c[2])
             if kind == DONE:
                 done.add(r)
+                continue
+            if kind == RESET:             # another PS restarted: rejoin at the announced generation
+                self._rejoin(int(c[3]), r)
                 continue
             if kind == GRAD:
                 g = self.tx.ps_take_grads(self, r, wstep)
@@ -478,27 +528,89 @@ class ParameterServer:
 class PSClient:
     """Worker side: push gradients / pull parameters of every PS shard."""
 
-    def __init__(self, net, num_ps: int, num_workers: int, worker_index: int, group=None, transport: str = ""):
+    def __init__(self, net, num_ps: int, num_workers: int, worker_index: int, group=None, transport: str = "",
+                 cluster=None, log=print):
         self.net = net
         self.k, self.W, self.wi = num_ps, num_workers, worker_index
         self.group = group
+        self.cluster = cluster            # PS-mode Cluster (store + generation): enables session recovery
+        self.log = log
+        self.transport_name = transport
+        self.recoveries = 0
         self.ranges = shard_ranges(net.fp, num_ps)
         self.global_step = 0
         self.stop = False
-        dev = net.fp.params.device
-        self.tx = setup_transport(transport or default_transport(dev), group, num_ps, num_workers, device=dev)
-        self.tx.worker_open(worker_index, self.ranges)
+        self._open_transport()
         self.local_step = 0
-        # one stamped push slot per PS shard: the slice + its int64 sequence stamp, sent as ONE message
-        # (host) / ONE peer copy (ipc)
-        stage_dev = dev if self.tx.name == "ipc" else torch.device("cpu")
-        self.slots = [torch.zeros(slot_len(b - a), dtype=torch.float32, device=stage_dev) for a, b, _ in self.ranges]
+        self._pending: set = set()         # PS tasks holding this exchange's control word, reply not taken
+        self._pending_state = False
         self._corrupt = corrupt_push_at()
         # data-plane accounting (bench.py --mode ps): host seconds and bytes of the GRAD
         # exchanges; push = stage + copy/send + announce to every PS, pull = wait for the
         # replies + copy the parameters back (so it includes the PS's service time)
         self.comm = {"push_s": 0.0, "reply_wait_s": 0.0, "push_bytes": 0, "pull_bytes": 0, "msgs": 0}
         self._pull_ev: List[Tuple] = []      # (start, end) CUDA events around the pull copies
+
+    def _open_transport(self) -> None:
+        """Collective with every PS (setup_transport) -- at start and after a rejoin."""
+        dev = self.net.fp.params.device
+        self.tx = setup_transport(self.transport_name or default_transport(dev), self.group, self.k, self.W,
+                                  device=dev)
+        self.tx.worker_open(self.wi, self.ranges)
+        # one stamped push slot per PS shard: the slice + its int64 sequence stamp, sent as ONE message
+        # (host) / ONE peer copy (ipc)
+        stage_dev = dev if self.tx.name == "ipc" else torch.device("cpu")
+        self.slots = [torch.zeros(slot_len(b - a), dtype=torch.float32, device=stage_dev) for a, b, _ in self.ranges]
+
+    def recover(self, err: BaseException, timeout_s: Optional[float] = None) -> None:
+        """Session recreation after a parameter server failed (module docstring): wait
+        for the restarted PS's generation, RESET the survivors, rejoin, re-open the data
+        plane.  Re-raises ``err`` when there is no store or no PS comes back in time."""
+        from .cluster import current_gen, rejoin
+        cl = self.cluster
+        if cl is None or cl.store is None:
+            raise err
+        self.log(f"[worker {self.wi}] An error was raised ({type(err).__name__}: {str(err).splitlines()[0][:160]}). "
+                 f"This may be due to a preemption in a connected parameter server. The current session "
+                 f"will be recreated.")
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("MNISTX_PS_RECOVERY_TIMEOUT", "300"))
+        t_end = time.time() + timeout_s
+        gen = current_gen(cl)
+        while gen <= cl.gen:
+            if cl.store.check([FATAL_KEY]):    # the PS failed on purpose (e.g. a rejected push): no recovery
+                self.log(f"[worker {self.wi}] parameter server reported a fatal error: "
+                         f"{cl.store.get(FATAL_KEY).decode()[:300]}")
+                raise err
+            if time.time() > t_end:
+                self.log(f"[worker {self.wi}] no parameter server came back within {timeout_s:.0f} s")
+                raise err
+            time.sleep(0.05)
+            gen = current_gen(cl)
+        # a surviving PS that took this exchange's control word is blocked sending its reply
+        # (gloo sends complete only when matched): take those replies on the old group first
+        fp = self.net.fp
+        for j in sorted(self._pending):
+            a, b, _ = self.ranges[j]
+            try:
+                dist.recv(torch.zeros(CTRL, dtype=torch.int64), j, group=self.group, tag=TAG_CTRL)
+                self.tx.worker_pull(j, fp.params[a:b], fp.ema[a:b], fp.mom[a:b], self._pending_state)
+            except Exception:
+                pass
+        self._pending.clear()
+        for j in range(self.k):            # best effort: the dead PS is not there to hear it
+            c = torch.zeros(CTRL, dtype=torch.int64)
+            c[0], c[3] = RESET, gen
+            try:
+                dist.send(c, j, group=self.group, tag=TAG_CTRL)
+            except Exception:
+                pass
+        if self.net.fp.params.is_cuda:
+            torch.cuda.synchronize(self.net.fp.params.device)
+        rejoin(cl, gen)
+        self._open_transport()
+        self.recoveries += 1
+        self.log(f"[worker {self.wi}] session recreated: joined generation {gen}")
 
     def _stage(self, j: int, a: int, b: int) -> torch.Tensor:
         slot = self.slots[j]
@@ -510,16 +622,34 @@ class PSClient:
         return slot
 
     def _exchange(self, kind: int, want_state: bool = False) -> None:
+        """One exchange with every PS; on a control-plane failure (a PS died) the session
+        is recreated and the exchange re-sent -- as a pull only to the PS tasks that
+        already took this push."""
+        took: set = set()
+        while True:
+            try:
+                return self._exchange_once(kind, want_state, took)
+            except RuntimeError as e:     # gloo: connection closed / reset / timeout
+                if isinstance(e, PushIntegrityError):
+                    raise
+                self.recover(e)
+
+    def _exchange_once(self, kind: int, want_state: bool, took: set) -> None:
         fp = self.net.fp
         t0 = time.perf_counter()
         # announce to every PS first (they work in parallel), then collect the replies
         for j, (a, b, _) in enumerate(self.ranges):
-            g = self._stage(j, a, b) if kind == GRAD else None
-            self.tx.worker_before_ctrl(j, kind, g)
+            kj = HELLO if (kind == GRAD and j in took) else kind
+            g = self._stage(j, a, b) if kj == GRAD else None
+            self.tx.worker_before_ctrl(j, kj, g)
             c = torch.zeros(CTRL, dtype=torch.int64)
-            c[0], c[1], c[2] = kind, int(want_state), self.local_step
+            c[0], c[1], c[2] = kj, int(want_state), self.local_step
             dist.send(c, j, group=self.group, tag=TAG_CTRL)
-            self.tx.worker_after_ctrl(j, kind, g)
+            self._pending.add(j)
+            self._pending_state = want_state
+            self.tx.worker_after_ctrl(j, kj, g)
+            if kj == GRAD:
+                took.add(j)
         t1 = time.perf_counter()
         wait = 0.0
         evs = None
@@ -533,6 +663,7 @@ class PSClient:
             if evs is not None and j == 0:
                 evs[0].record()
             self.tx.worker_pull(j, fp.params[a:b], fp.ema[a:b], fp.mom[a:b], want_state)
+            self._pending.discard(j)
             if j == 0:
                 self.global_step = int(r[0])
                 self.stop = bool(r[1])
@@ -610,11 +741,13 @@ class PSWorkerReplica:
     but no local optimizer — gradients go to the PS tasks, fresh parameters
     and the shared global step come back."""
 
-    def __init__(self, base, num_ps: int, num_workers: int, worker_index: int, group=None, transport: str = ""):
+    def __init__(self, base, num_ps: int, num_workers: int, worker_index: int, group=None, transport: str = "",
+                 cluster=None, log=print):
         self.base = base                  # a train.replica.Replica (built with world=1 semantics)
         self.net = base.net
         self.spec = base.spec
-        self.client = PSClient(base.net, num_ps, num_workers, worker_index, group=group, transport=transport)
+        self.client = PSClient(base.net, num_ps, num_workers, worker_index, group=group, transport=transport,
+                               cluster=cluster, log=log)
         self.world = 1
         self.examples_per_step = base.B
         self.device = base.device

@@ -1,12 +1,19 @@
 """Parameter-server job supervisor: launch 1..k PS + N workers, restart on failure.
 
 The reference's ``MonitoredTrainingSession`` survives a PS restart: on
-``AbortedError`` / ``UnavailableError`` it recreates the session and the chief
+``AbortedError`` / ``UnavailableError`` it recreates the session and the PS
 restores from the latest checkpoint (``/root/reference/main.py:140-146`` [TF1-lib]).
-Here a dead PS makes every worker exit non-zero (bounded collective timeout, no
-hang) and the job is restarted as a whole from the last checkpoint -- the same
-recovery torchrun's elastic agent gives the data-parallel mode
-(``--max-restarts``).  This module is that agent for PS mode:
+Two levels of recovery here:
+
+* **a parameter server dies** (default ``--recover_ps``): only that process is
+  relaunched, on the same ports; it restores its shard from the latest checkpoint
+  and opens the next session generation, and the workers and the other PS tasks
+  rejoin it IN PLACE (``parallel/ps.py`` "Session recovery") -- no worker restarts;
+* **a worker dies** (or a PS restart fails, or ``--recover_ps 0``): the attempt is
+  torn down and the job restarts as a whole from the last checkpoint -- the same
+  recovery torchrun's elastic agent gives the data-parallel mode (``--max-restarts``).
+
+This module is that agent for PS mode:
 
     python -m distributed_tensorflow_ibm_mnist_amd.parallel.supervisor \\
         --num_ps 1 --num_workers 7 --max_restarts 3 -- --model=lenet5 --train_dir=/tmp/ps ...
@@ -48,8 +55,14 @@ def free_ports(n: int) -> List[int]:
 
 
 class Attempt:
-    def __init__(self, procs: Dict[str, subprocess.Popen]):
+    def __init__(self, procs: Dict[str, subprocess.Popen], spawn=None):
         self.procs = procs
+        self.spawn = spawn                 # spawn(name, env_extra) -> Popen: relaunch one process
+
+    def respawn(self, name: str) -> None:
+        """Relaunch one process of this attempt (same flags and ports) as a restart."""
+        self.procs[name].wait()
+        self.procs[name] = self.spawn(name, {"MNISTX_PS_RESTART": "1"})
 
     def poll(self) -> Tuple[bool, Optional[Tuple[str, int]]]:
         """(all finished, first failure (name, rc) or None)."""
@@ -83,21 +96,29 @@ def launch(main: str, flags: Sequence[str], num_ps: int, num_workers: int, attem
     ps_hosts = ",".join(f"127.0.0.1:{p}" for p in ports[:num_ps])
     wk_hosts = ",".join(f"127.0.0.1:{p}" for p in ports[num_ps:])
     env = dict(os.environ, TORCHELASTIC_RESTART_COUNT=str(attempt), PYTHONUNBUFFERED="1", **(env_extra or {}))
+    starts: Dict[str, int] = {}
+
+    def spawn(name: str, extra: Optional[Dict[str, str]] = None) -> subprocess.Popen:
+        job, i = name.rstrip("0123456789"), int(name.lstrip("pswoker"))
+        n = starts[name] = starts.get(name, -1) + 1
+        suffix = f"_restart{n}" if n else ""
+        out = open(os.path.join(log_dir, f"attempt{attempt}_{name}{suffix}.log"), "w") if log_dir else None
+        return subprocess.Popen(
+            [sys.executable, main, *flags, f"--job_name={job}", f"--task_id={i}", f"--ps_hosts={ps_hosts}",
+             f"--worker_hosts={wk_hosts}"],
+            cwd=ROOT, env=dict(env, **(extra or {})), stdout=out, stderr=subprocess.STDOUT if out else None,
+            start_new_session=True)
+
     procs: Dict[str, subprocess.Popen] = {}
     for job, n in (("ps", num_ps), ("worker", num_workers)):
         for i in range(n):
-            name = f"{job}{i}"
-            out = open(os.path.join(log_dir, f"attempt{attempt}_{name}.log"), "w") if log_dir else None
-            procs[name] = subprocess.Popen(
-                [sys.executable, main, *flags, f"--job_name={job}", f"--task_id={i}", f"--ps_hosts={ps_hosts}",
-                 f"--worker_hosts={wk_hosts}"],
-                cwd=ROOT, env=env, stdout=out, stderr=subprocess.STDOUT if out else None, start_new_session=True)
-    return Attempt(procs)
+            procs[f"{job}{i}"] = spawn(f"{job}{i}")
+    return Attempt(procs, spawn)
 
 
 def supervise(flags: Sequence[str], num_ps: int = 1, num_workers: int = 2, max_restarts: int = 3,
               main: Optional[str] = None, log_dir: Optional[str] = None, timeout_s: float = 0.0,
-              log=print) -> int:
+              log=print, recover_ps: bool = True) -> int:
     main = main or os.path.join(ROOT, "main.py")
     if log_dir:
         os.makedirs(log_dir, exist_ok=True)
@@ -106,8 +127,16 @@ def supervise(flags: Sequence[str], num_ps: int = 1, num_workers: int = 2, max_r
         log(f"[supervisor] attempt {attempt}: {num_ps} PS + {num_workers} worker(s)")
         att = launch(main, flags, num_ps, num_workers, attempt, log_dir)
         failure = None
+        ps_restarts = 0
         while True:
             done, failure = att.poll()
+            if failure is not None and recover_ps and failure[0].startswith("ps") and ps_restarts < max_restarts:
+                # a parameter server died: relaunch just it; workers rejoin in place
+                ps_restarts += 1
+                log(f"[supervisor] {failure[0]} exited with {failure[1]}; restarting it in place "
+                    f"(PS restart {ps_restarts})")
+                att.respawn(failure[0])
+                continue
             if done:
                 break
             if t_end is not None and time.time() > t_end:
@@ -138,8 +167,11 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     ap.add_argument("--log_dir", default="", help="per-process logs (default: inherit stdout)")
     ap.add_argument("--timeout", type=float, default=0.0, help="whole-job wall limit in seconds (0: none)")
     ap.add_argument("--main", default="", help="training entry point (default: the repo's main.py)")
+    ap.add_argument("--recover_ps", type=int, default=1,
+                    help="1: relaunch a dead PS in place (workers rejoin without restarting); 0: restart the job")
     a = ap.parse_args(argv)
-    return supervise(flags, a.num_ps, a.num_workers, a.max_restarts, a.main or None, a.log_dir or None, a.timeout)
+    return supervise(flags, a.num_ps, a.num_workers, a.max_restarts, a.main or None, a.log_dir or None, a.timeout,
+                     recover_ps=bool(a.recover_ps))
 
 
 if __name__ == "__main__":

@@ -108,7 +108,7 @@ def _train(FLAGS, cl: Cluster, max_steps, test_interval, batch_size, impl, log) 
         if prefix:
             log(f"[ps {cl.task_id}] restored shard from {prefix}")
         ps = ParameterServer(cl.task_id, cl.num_ps, cl.num_workers, param_specs(spec), init, opt, cl.device,
-                             max_steps, restore=restore, log=log, transport=cl.transport)
+                             max_steps, restore=restore, log=log, transport=cl.transport, cluster=cl)
         res = ps.serve()
         return {"global_step": float(res["global_step"])}
 
@@ -128,7 +128,8 @@ def _train(FLAGS, cl: Cluster, max_steps, test_interval, batch_size, impl, log) 
     replica = base
     if cl.mode == "ps":
         from ..parallel.ps import PSWorkerReplica
-        replica = PSWorkerReplica(base, cl.num_ps, cl.num_workers, cl.task_id, transport=cl.transport)
+        replica = PSWorkerReplica(base, cl.num_ps, cl.num_workers, cl.task_id, transport=cl.transport, cluster=cl,
+                                  log=log)
     is_chief = cl.is_chief
     if FLAGS.log_device_placement:
         log(placement_table(replica, cl))

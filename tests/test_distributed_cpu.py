@@ -202,7 +202,9 @@ def test_ps_kill_fails_workers_then_resume(tmp_path):
                 pytest.fail(f"{tag} {name} hung:\n" + open(log).read()[-3000:])
         return {name: (p.returncode, open(log).read()) for name, log, p in procs}
 
-    r1 = launch("kill", {"MNIST_FI_KILL_RANK_AT_STEP": "0:17"})
+    # no supervisor restarts the PS here: the workers wait MNISTX_PS_RECOVERY_TIMEOUT for a
+    # new session generation, then give up and exit non-zero
+    r1 = launch("kill", {"MNIST_FI_KILL_RANK_AT_STEP": "0:17", "MNISTX_PS_RECOVERY_TIMEOUT": "10"})
     assert r1["ps0"][0] == -9, r1["ps0"][1][-2000:]
     assert "fault injection: SIGKILL" in r1["ps0"][1]
     for w in ("worker0", "worker1"):
@@ -361,23 +363,26 @@ def test_ps_worker_weight_loss_terms():
     assert int(net.fp.step.item()) == 0
 
 
+def _sup_flags(d):
+    return ["--impl=torch", "--cpu", "--model=mlp", "--in_channels=1", "--batch_size=32", "--max_steps=40",
+            "--test_interval=100", "--log_step_count_steps=0", "--train_data=synthetic://1500",
+            "--test_data=synthetic://300?seed=1", f"--train_dir={d}", "--save_checkpoint_steps=5",
+            "--collective_timeout=60"]
+
+
 def test_ps_supervisor_restarts_after_ps_death(tmp_path):
-    """Recovery without a human: the PS is SIGKILLed at step 17 of attempt 0; the
-    supervisor tears the attempt down, starts attempt 1 (fault injection is off on
+    """Whole-job recovery (--recover_ps 0): the PS is SIGKILLed at step 17 of attempt 0;
+    the supervisor tears the attempt down, starts attempt 1 (fault injection is off on
     restarts), the PS restores its shard from the last checkpoint and the job
     finishes at exactly max_steps."""
     from distributed_tensorflow_ibm_mnist_amd.parallel.supervisor import supervise
     d = str(tmp_path / "train")
     logs = str(tmp_path / "logs")
-    flags = ["--impl=torch", "--cpu", "--model=mlp", "--in_channels=1", "--batch_size=32", "--max_steps=40",
-             "--test_interval=100", "--log_step_count_steps=0", "--train_data=synthetic://1500",
-             "--test_data=synthetic://300?seed=1", f"--train_dir={d}", "--save_checkpoint_steps=5",
-             "--collective_timeout=60"]
     msgs = []
     os.environ["MNIST_FI_KILL_RANK_AT_STEP"] = "0:17"
     try:
-        rc = supervise(flags, num_ps=1, num_workers=2, max_restarts=2, log_dir=logs, timeout_s=400,
-                       log=msgs.append)
+        rc = supervise(_sup_flags(d), num_ps=1, num_workers=2, max_restarts=2, log_dir=logs, timeout_s=400,
+                       log=msgs.append, recover_ps=False)
     finally:
         os.environ.pop("MNIST_FI_KILL_RANK_AT_STEP", None)
     assert rc == 0, msgs
@@ -388,3 +393,45 @@ def test_ps_supervisor_restarts_after_ps_death(tmp_path):
     assert "result: global_step=40" in w0, w0[-2000:]
     from distributed_tensorflow_ibm_mnist_amd.ckpt.saver import latest_checkpoint
     assert latest_checkpoint(d).endswith("model.ckpt-40")
+
+
+@pytest.mark.parametrize("num_ps,kill_rank", [(1, 0), (2, 1)])
+def test_ps_session_recovery_in_place(tmp_path, num_ps, kill_rank):
+    """In-place session recovery (MonitoredTrainingSession's, main.py:140-146): a PS is
+    SIGKILLed at step 17; the supervisor relaunches ONLY that PS, which restores its
+    shard from the last checkpoint and opens session generation 1; both workers (same
+    processes: no attempt 1) recreate their session and rejoin, a surviving PS (2-PS
+    case) rejoins on the workers' RESET keeping its state, and the job ends at
+    max_steps with a checkpoint of every shard."""
+    from distributed_tensorflow_ibm_mnist_amd.parallel.supervisor import supervise
+    d = str(tmp_path / "train")
+    logs = str(tmp_path / "logs")
+    msgs = []
+    os.environ["MNIST_FI_KILL_RANK_AT_STEP"] = f"{kill_rank}:17"
+    try:
+        rc = supervise(_sup_flags(d), num_ps=num_ps, num_workers=2, max_restarts=2, log_dir=logs, timeout_s=400,
+                       log=msgs.append)
+    finally:
+        os.environ.pop("MNIST_FI_KILL_RANK_AT_STEP", None)
+    read = lambda n: open(os.path.join(logs, n)).read()
+    assert rc == 0, (msgs, read(f"attempt0_ps{kill_rank}_restart1.log")[-2000:])
+    assert any(f"ps{kill_rank} exited with -9; restarting it in place" in m for m in msgs), msgs
+    assert not any("attempt 1" in m for m in msgs), msgs              # no whole-job restart
+    assert not os.path.exists(os.path.join(logs, "attempt1_worker0.log"))
+    assert "fault injection: SIGKILL" in read(f"attempt0_ps{kill_rank}.log")
+    rs = read(f"attempt0_ps{kill_rank}_restart1.log")
+    assert "restored shard from" in rs and "opening session generation 1" in rs, rs[-2000:]
+    for w in ("worker0", "worker1"):
+        out = read(f"attempt0_{w}.log")
+        assert "The current session will be recreated" in out and "joined generation 1" in out, out[-2000:]
+    if num_ps == 2:
+        survivor = read(f"attempt0_ps{1 - kill_rank}.log")
+        assert "rejoining session generation 1" in survivor, survivor[-2000:]
+    w0 = read("attempt0_worker0.log")
+    res = [l for l in w0.splitlines() if l.startswith("result:")][-1]
+    assert "global_step=40" in res, w0[-2000:]
+    from distributed_tensorflow_ibm_mnist_amd.ckpt.bundle import read_index
+    from distributed_tensorflow_ibm_mnist_amd.ckpt.saver import latest_checkpoint
+    lc = latest_checkpoint(d)
+    assert lc.endswith("model.ckpt-40")
+    assert read_index(lc)[0] == num_ps

@@ -555,6 +555,58 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
           }
         }
       }
+      if constexpr (INL) {
+        // in-lane pooling: columns = (pooled-pixel slot, image), ONE accumulator per output-row
+        // parity of the window, so a lane holds all 4 positions of 8 channels: the pool is
+        // 3 v_max in the lane (no DPP, no keep/send selects, no chain sum).  Unit u = pooled
+        // pixels 4u .. 4u+3 of the 8 images (7 units, the last 3 slots recomputed, no store);
+        // the 6 pool1 rows 2 y2p .. 2 y2p + 5 are streamed once, each feeding both parities.
+        const int slot = col >> 3, im2 = col & 7, gi2 = t0 + im2;
+#pragma unroll 1
+        for (int j = 0; j < 2; ++j) {
+          const int u = w2v + 4 * j;
+          if (u >= 7) break;
+          const int f = 4 * u + slot, fc = min(f, 24);
+          const int y2p = fc / 5, x2p = fc - 5 * y2p;
+          const bf16_t* rb = pb + im2 * PIS + y2p * PRW + (2 * x2p + h) * 8;
+          auto rowp = [&](int r) { return rb + (r & 1) * PPL + (r >> 1) * PRW; };
+          bf16x8 bq[2][3];
+#pragma unroll
+          for (int q = 0; q < 3; ++q) bq[0][q] = *(const bf16x8*)(rowp(0) + 16 * q);
+          f32x16 y0 = {}, y1 = {};
+#pragma unroll
+          for (int r = 0; r < 6; ++r) {
+            if (r < 5) {
+#pragma unroll
+              for (int q = 0; q < 3; ++q) bq[(r + 1) & 1][q] = *(const bf16x8*)(rowp(r + 1) + 16 * q);
+            }
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+              if (r < 5) y0 = mfma32(a2[r * 3 + q], bq[r & 1][q], y0);
+              if (r > 0) y1 = mfma32(a2[(r - 1) * 3 + q], bq[r & 1][q], y1);
+            }
+          }
+          // channel ch of this lane: c2 = 8 (ch >> 2) + 4h + (ch & 3); xpar 0 / 1 at i0 / i0 + 8
+          const f32x4 bl = *(const f32x4*)(a.b2 + 4 * h), bh = *(const f32x4*)(a.b2 + 8 + 4 * h);
+          float o[8];
+          uint32_t cd[8];
+#pragma unroll
+          for (int ch = 0; ch < 8; ++ch) {
+            const int i0 = 4 * (ch >> 2) + (ch & 3);
+            const float v = vmax(vmax3(__uint_as_float(__float_as_uint(y0[i0]) & ~3u), embed(y0[i0 + 8], 1u),
+                                       embed(y1[i0], 2u)), embed(y1[i0 + 8], 3u));
+            o[ch] = vmax(__uint_as_float(__float_as_uint(v) & ~3u) + (ch < 4 ? bl[ch] : bh[ch - 4]), 0.f);
+            cd[ch] = o[ch] > 0.f ? (__float_as_uint(v) & 3u) : ARG_OFF;
+          }
+          if (gi2 < a.B && f < 25) {
+            const int64_t e = (int64_t)gi2 * P2E + f * 16 + 4 * h;
+            *(u32x2*)(a.p2 + e) = u32x2{pk2(o[0], o[1]), pk2(o[2], o[3])};
+            *(u32x2*)(a.p2 + e + 8) = u32x2{pk2(o[4], o[5]), pk2(o[6], o[7])};
+            *(uint32_t*)(a.arg2 + e) = cd[0] | (cd[1] << 8) | (cd[2] << 16) | (cd[3] << 24);
+            *(uint32_t*)(a.arg2 + e + 8) = cd[4] | (cd[5] << 8) | (cd[6] << 16) | (cd[7] << 24);
+          }
+        }
+      } else {
       // unit = lane's pooled pixel f = f0 + 13 half (f0 = w2v + 4j); the 15 B fragments of a
       // kernel row dy are read one row ahead; two accumulator chains
 #pragma unroll 1
@@ -603,6 +655,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
           *(u32x2*)(a.p2 + e) = u32x2{pk2(o[0], o[1]), pk2(o[2], o[3])};
           *(uint32_t*)(a.arg2 + e) = cd[0] | (cd[1] << 8) | (cd[2] << 16) | (cd[3] << 24);
         }
+      }
       }
       tw = __builtin_amdgcn_s_memtime();
       busy += tw - tb;

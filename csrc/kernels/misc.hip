@@ -710,24 +710,36 @@ __global__ __launch_bounds__(TPB) void fused_opt_k(float* __restrict__ params, c
   const int64_t lo = (int64_t)(blockIdx.x - tab.blk0[si]) * OPT_CHUNK;
   const int64_t ij = (int64_t)sg.I * sg.J;
   float sq = 0.f;
+  // every element's loads issued before any use (one memory round trip per thread, not
+  // one per element); out-of-range slots load element 0 and are never stored
+  float pv[OPT_EPT], gv[OPT_EPT], mv[OPT_EPT], ev[OPT_EPT];
+#pragma unroll
+  for (int u = 0; u < OPT_EPT; ++u) {
+    const int64_t li = lo + u * TPB + threadIdx.x;
+    const int64_t e = sg.off + (li < sg.n ? li : 0);
+    pv[u] = params[e];
+    gv[u] = grads[e];
+    mv[u] = op.use_momentum ? mom[e] : 0.f;
+    ev[u] = op.ema_max >= 0.f ? ema[e] : 0.f;
+  }
 #pragma unroll
   for (int u = 0; u < OPT_EPT; ++u) {
     const int64_t li = lo + u * TPB + threadIdx.x;
     if (li >= sg.n) continue;
     const int64_t e = sg.off + li;
-    float p = params[e];
+    float p = pv[u];
     sq += p * p;
-    const float g = grads[e] * op.grad_scale + sg.wd * p;
+    const float g = gv[u] * op.grad_scale + sg.wd * p;
     float upd = g;
     if (op.use_momentum) {
-      const float v = mom[e] * op.momentum + g;
+      const float v = mv[u] * op.momentum + g;
       mom[e] = v;
       upd = op.nesterov ? g + op.momentum * v : v;
     }
     p -= lr * upd;
     params[e] = p;
     if (op.ema_max >= 0.f) {
-      const float s = ema[e];
+      const float s = ev[u];
       ema[e] = s - (1.f - ema_d) * (s - p);
     }
     if (sg.bf_off >= 0) {
@@ -794,8 +806,22 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void finalize_k(int64_t* step, floa
   if (ce_nblk > 0) {
     // deferred CE partials (ce_block_stats defer): the same lane-strided, fixed-tree sum as
     // the ticket combine's last block, so the loss is bitwise what that path produced
+    // 8 partials per lane in flight per round (a dependent load per iteration made this
+    // loop ~16 serial L2 round trips at B = 65536), summed in the same per-lane order
     float a = 0.f, b = 0.f, c = 0.f;
-    for (int i = t; i < ce_nblk; i += 64) {
+    int i = t;
+    for (; i + 7 * 64 < ce_nblk; i += 8 * 64) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *(const f32x4*)(ce_work + 4 * (i + 64 * u));
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a += v[u][0];
+        b += v[u][1];
+        c += v[u][2];
+      }
+    }
+    for (; i < ce_nblk; i += 64) {
       a += ce_work[4 * i];
       b += ce_work[4 * i + 1];
       c += ce_work[4 * i + 2];

@@ -149,3 +149,32 @@ def test_ps_ipc_corrupt_push_aborts_naming_worker(dev):
     out = r.stdout + r.stderr
     assert r.returncode != 0, out[-3000:]
     assert "PushIntegrityError" in out and "push from worker 0 failed its sequence-stamp check" in out, out[-3000:]
+
+
+def test_ps_session_recovery_ipc(tmp_path):
+    """In-place session recovery on the GPU data plane: HIP workers with the ipc
+    transport, the PS SIGKILLed at step 17 and relaunched alone by the supervisor;
+    the workers (same processes) re-map the new PS's mailboxes and finish at max_steps."""
+    from distributed_tensorflow_ibm_mnist_amd.parallel.supervisor import supervise
+    d = str(tmp_path / "train")
+    logs = str(tmp_path / "logs")
+    flags = ["--model=lenet5", "--in_channels=1", "--batch_size=256", "--max_steps=40", "--test_interval=1000",
+             "--log_step_count_steps=0", "--train_data=synthetic://8000", "--test_data=synthetic://512?seed=1",
+             "--eval_examples=512", f"--train_dir={d}", "--ps_backend=ipc", "--save_checkpoint_steps=5",
+             "--optimizer=momentum", "--base_lr=0.02", "--collective_timeout=60"]
+    msgs = []
+    os.environ["MNIST_FI_KILL_RANK_AT_STEP"] = "0:17"
+    try:
+        rc = supervise(flags, num_ps=1, num_workers=2, max_restarts=1, log_dir=logs, timeout_s=180,
+                       log=msgs.append)
+    finally:
+        os.environ.pop("MNIST_FI_KILL_RANK_AT_STEP", None)
+    read = lambda n: open(os.path.join(logs, n)).read()
+    assert rc == 0, (msgs, read("attempt0_worker0.log")[-2000:])
+    assert not any("attempt 1" in m for m in msgs), msgs
+    rs = read("attempt0_ps0_restart1.log")
+    assert "restored shard from" in rs and "transport ipc" in rs, rs[-2000:]
+    for w in ("worker0", "worker1"):
+        assert "joined generation 1" in read(f"attempt0_{w}.log")
+    res = [l for l in read("attempt0_worker0.log").splitlines() if l.startswith("result:")][-1]
+    assert "global_step=40" in res

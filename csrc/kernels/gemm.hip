@@ -735,9 +735,16 @@ hipError_t dense_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int
   return launch_pick<MatLoaderV, MatLoaderV, false, false>(a, b, ep, M, Dout, B, splits, st, tile);
 }
 
+// Tile width of the grouped weight gradients: 128 columns cover LeNet's fc3 / fc4 outputs
+// (120 / 88) in ONE column tile, so their input activations (fc3: the 52 MB pool2 at
+// B = 65536) are read once instead of twice.  MNISTX_WG_GROUP_BN=64 for A/B; the
+// split choice (ops/functional.py pick_splits, grouped=True) reads the same variable.
+int wg_group_bn() { static const int v = env_int("MNISTX_WG_GROUP_BN", 128); return v == 64 ? 64 : 128; }
+
 hipError_t dense_wgrad_group(int np, const bf16_t* const* x, const bf16_t* const* dy, const int* Din, const int* Dout,
                              int B, const int* ldx, const int* lddy, int* splits, const GemmEpi* ep, hipStream_t st) {
-  constexpr int BM = 64, BN = 64;
+  constexpr int BM = 64;
+  const int BN = wg_group_bn();
   if (np < 1 || np > WG_GROUP_MAX) return hipErrorInvalidValue;
   WgGroup g{};
   g.np = np;
@@ -764,7 +771,8 @@ hipError_t dense_wgrad_group(int np, const bf16_t* const* x, const bf16_t* const
     total += (g.tiles_mn[p] * s + 7) / 8 * 8;
   }
   g.start[np] = total;
-  hipLaunchKernelGGL((gemm_wg_group_kernel<BM, BN, 2, 2>), dim3(total), dim3(256), 0, st, g);
+  if (BN == 128) hipLaunchKernelGGL((gemm_wg_group_kernel<BM, 128, 1, 4>), dim3(total), dim3(256), 0, st, g);
+  else hipLaunchKernelGGL((gemm_wg_group_kernel<BM, 64, 2, 2>), dim3(total), dim3(256), 0, st, g);
   return hipGetLastError();
 }
 

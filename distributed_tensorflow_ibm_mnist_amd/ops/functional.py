@@ -60,6 +60,8 @@ def gemm_tile(M: int, N: int) -> Tuple[int, int]:
     return 128, 128
 
 
+# column tile of the grouped head weight gradients (gemm.hip wg_group_bn, same variable)
+GROUP_BN = 64 if os.environ.get("MNISTX_WG_GROUP_BN", "128") == "64" else 128
 SLAB_CAP = 16 << 20   # fp32 elements of split-K partials (64 MB)
 
 
@@ -69,7 +71,7 @@ def pick_splits(M: int, N: int, K: int, target: Optional[int] = None, min_k: int
     workgroups), but keep every split >= min_k reduction elements and the fp32
     slab under SLAB_CAP.  ``grouped``: one problem of a dense_wgrad_group launch
     (64x64 tiles)."""
-    bm, bn = (64, 64) if grouped else gemm_tile(M, N)
+    bm, bn = (64, GROUP_BN) if grouped else gemm_tile(M, N)
     tiles = math.ceil(M / bm) * math.ceil(N / bn)
     if target is None:
         if dense and (bm, bn) == (128, 128):

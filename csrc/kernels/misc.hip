@@ -784,8 +784,50 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void finalize_k(int64_t* step, floa
   // instead of queueing behind each other (LeNet: 5 weights, ~11 -> ~5 us).
   __shared__ float wsum[FIN_MAXW];
   const int t = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (l2 && l2r) {
-    for (int w = wv; w < nw && w < FIN_MAXW; w += FIN_WAVES) {
+  // wave 0: the CE partials and every per-lane input of the EMA update, loaded up front;
+  // waves 1..FIN_WAVES-1: the per-weight sum(w^2) partials -- the two phases' memory
+  // round trips overlap instead of following each other
+  float ce_sum = 0.f, corr_sum = 0.f, l2t = 0.f, wdt = 0.f, e0 = 0.f, e1 = 0.f;
+  if (wv == 0) {
+    ce_sum = stats[0];
+    corr_sum = stats[1];
+    if (l2 && t < nw) l2t = l2[t];
+    if (t < nw) wdt = wds[t];
+    if (loss_ema && t < n_ema && t < nw + 2) {
+      e0 = loss_ema[3 * t];
+      e1 = loss_ema[3 * t + 1];
+    }
+    if (ce_nblk > 0) {
+      // deferred CE partials (ce_block_stats defer): the same lane-strided, fixed-tree sum as
+      // the ticket combine's last block, so the loss is bitwise what that path produced;
+      // 8 partials per lane in flight per round, summed in the same per-lane order
+      float a = 0.f, b = 0.f, c = 0.f;
+      int i = t;
+      for (; i + 7 * 64 < ce_nblk; i += 8 * 64) {
+        f32x4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = *(const f32x4*)(ce_work + 4 * (i + 64 * u));
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          a += v[u][0];
+          b += v[u][1];
+          c += v[u][2];
+        }
+      }
+      for (; i < ce_nblk; i += 64) {
+        a += ce_work[4 * i];
+        b += ce_work[4 * i + 1];
+        c += ce_work[4 * i + 2];
+      }
+      a = warp_sum(a);
+      b = warp_sum(b);
+      c = warp_sum(c);
+      ce_sum += a;
+      corr_sum += b;
+      if (t == 0 && c > 0.f) stats[2] = 1.f;
+    }
+  } else if (l2 && l2r) {
+    for (int w = wv - 1; w < nw && w < FIN_MAXW; w += FIN_WAVES - 1) {
       const int b0 = l2r[3 * w + 1], b1 = l2r[3 * w + 2];
       // 4 independent chains per lane (loads in flight), combined in a fixed order
       float s4[4] = {0.f, 0.f, 0.f, 0.f};
@@ -802,52 +844,21 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void finalize_k(int64_t* step, floa
   }
   __syncthreads();
   if (wv != 0) return;
-  float ce_sum = stats[0], corr_sum = stats[1];
-  if (ce_nblk > 0) {
-    // deferred CE partials (ce_block_stats defer): the same lane-strided, fixed-tree sum as
-    // the ticket combine's last block, so the loss is bitwise what that path produced
-    // 8 partials per lane in flight per round (a dependent load per iteration made this
-    // loop ~16 serial L2 round trips at B = 65536), summed in the same per-lane order
-    float a = 0.f, b = 0.f, c = 0.f;
-    int i = t;
-    for (; i + 7 * 64 < ce_nblk; i += 8 * 64) {
-      f32x4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *(const f32x4*)(ce_work + 4 * (i + 64 * u));
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        a += v[u][0];
-        b += v[u][1];
-        c += v[u][2];
-      }
-    }
-    for (; i < ce_nblk; i += 64) {
-      a += ce_work[4 * i];
-      b += ce_work[4 * i + 1];
-      c += ce_work[4 * i + 2];
-    }
-    a = warp_sum(a);
-    b = warp_sum(b);
-    c = warp_sum(c);
-    ce_sum += a;
-    corr_sum += b;
-    if (t == 0 && c > 0.f) stats[2] = 1.f;
-  }
   const float ce = ce_sum / (float)batch;
   const float acc = corr_sum / (float)batch;
   // sum(w^2) of weight t: the fused optimizer's per-block partials l2[l2base + b],
   // b in [l2r[3w+1], l2r[3w+2]), summed by the whole wave in a fixed order
-  float l2v = (l2 && t < nw) ? l2[t] : 0.f;
+  float l2v = l2t;
   if (l2 && l2r)
     for (int w = 0; w < nw && w < FIN_MAXW; ++w)
       if (t == l2r[3 * w]) l2v += wsum[w];
-  const float wl = t < nw ? wds[t] * 0.5f * l2v : 0.f;
+  const float wl = t < nw ? wdt * 0.5f * l2v : 0.f;
   float total = ce;
   for (int i = 0; i < nw; ++i) total += __shfl(wl, i, 64);   // fixed order (bitwise as before)
   if (loss_ema && t < n_ema && t < nw + 2) {
     const float v = t < nw ? wl : (t == nw ? ce : total);
     float* e = loss_ema + 3 * t;
-    const float b = 0.9f * e[0] + 0.1f * v, n = e[1] + 1.f;
+    const float b = 0.9f * e0 + 0.1f * v, n = e1 + 1.f;
     e[0] = b;
     e[1] = n;
     e[2] = b / (1.f - powf(0.9f, n));

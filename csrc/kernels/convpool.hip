@@ -1976,8 +1976,10 @@ hipError_t convpool_wgrad(int cfg, const XSrc& x, const bf16_t* dP, const uint8_
   const LrnFold lrn{lrn_p, lrn_bias, lrn_alpha, lrn_beta};
   if (lrn_p && cfg != 2 && cfg != 3) return hipErrorInvalidValue;
   switch (cfg) {
-    case 0: return c1_wg_imgs() == 2 ? run_wgrad<LeNetC1, 2>(x, dP, arg, B, slab, grid, st)
-                                     : run_wgrad<LeNetC1, WG_IMGS_C1>(x, dP, arg, B, slab, grid, st);
+    case 0:
+      if (lenet_c1w_pk_enabled()) return lenet_c1w_pk(x, dP, arg, B, slab, grid, st);
+      return c1_wg_imgs() == 2 ? run_wgrad<LeNetC1, 2>(x, dP, arg, B, slab, grid, st)
+                               : run_wgrad<LeNetC1, WG_IMGS_C1>(x, dP, arg, B, slab, grid, st);
     case 1: return run_wgrad<LeNetC2, 4>(x, dP, arg, B, slab, grid, st);
     // the LRN fold stages one image per group (its LRN input vectors and temporaries
     // would push the 2-image variant past 256 VGPRs: one wave per SIMD)
@@ -2010,7 +2012,9 @@ int wgrad_grid_for() {
 // the slab has exactly one partial per resident block.
 int convpool_wgrad_grid(int cfg) {
   switch (cfg) {
-    case 0: return c1_wg_imgs() == 2 ? wgrad_grid_for<LeNetC1, 2>() : wgrad_grid_for<LeNetC1, WG_IMGS_C1>();
+    case 0:
+      if (lenet_c1w_pk_enabled()) return lenet_c1w_pk_grid();
+      return c1_wg_imgs() == 2 ? wgrad_grid_for<LeNetC1, 2>() : wgrad_grid_for<LeNetC1, WG_IMGS_C1>();
     case 1: return wgrad_grid_for<LeNetC2, 4>();
     case 2: return wgrad_grid_for<RefC1g, 2>();
     case 3: return wgrad_grid_for<RefC1c, 2>();

@@ -77,6 +77,11 @@ struct XSrc {
   int n;
 };
 int convpool_u8_input(int cfg);
+// LeNet-5 conv1 weight gradient, pooled-K form (lenet_c1wgrad.hip); same slab as cfg 0's
+bool lenet_c1w_pk_enabled();
+int lenet_c1w_pk_grid();
+hipError_t lenet_c1w_pk(const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B, float* slab, int grid,
+                        hipStream_t st);
 int convpool_config(int cin, int cout, int ks, int pad, int h, int w);  // -1: unsupported
 int convpool_wgrad_rows(int cfg);                                      // KM (slab rows incl. bias row)
 // slab -> dW layout for splitk_reduce: {G, Ipad, I (-1: real Cin), bias_row}

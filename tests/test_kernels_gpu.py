@@ -506,3 +506,46 @@ def test_lrn_pool_matches_two_step(dev, K, N, H, W, C, relu):
     dx2 = torch.empty_like(x)
     K.lrn_bwd(x, dl, dx2, N * H * W, C, r, bias, alpha, beta, relu)
     assert torch.equal(dx, dx2)
+
+
+@pytest.mark.parametrize("src", ["bf16_idx", "u8_idx"])
+def test_lenet_conv1_wgrad_gathered_input(dev, K, src):
+    # runs whichever conv1 weight-gradient kernel the process selected (MNISTX_C1W_POOLK)
+    """LeNet conv1 weight gradient (lenet_c1wgrad.hip, pooled-K form) reading a resident
+    dataset through the batch index (bf16, or uint8 normalised in the kernel) == the fp32
+    oracle on the gathered, normalised batch; several grids (images per block 1..n)."""
+    torch.manual_seed(5)
+    n, N = 300, 97
+    u8 = torch.randint(0, 256, (n, 784), dtype=torch.uint8, device=dev)
+    norm = (u8.float() / 255.0 - 0.5).to(torch.bfloat16)
+    idx = torch.randint(0, n, (N,), dtype=torch.int64, device=dev)
+    xb = norm[idx].view(N, 28, 28, 1)
+    w = torch.zeros(5, 5, 1, 8, device=dev)
+    w[..., :6] = torch.randn(5, 5, 1, 6, device=dev) / 5
+    w = w.to(torch.bfloat16)
+    b = torch.randn(6, device=dev) * 0.1
+    pooled = torch.empty(N, 14, 14, 8, dtype=torch.bfloat16, device=dev)
+    arg = torch.empty(N, 14, 14, 4, dtype=torch.uint8, device=dev)
+    K.convpool_fwd(xb, w, b, 6, pooled, arg, N, 1, 8, 5, 2, 28, 28)
+    xr = xb.float()
+    wr = w.float().requires_grad_(True)
+    br = torch.zeros(8, device=dev)
+    br[:6] = b
+    br.requires_grad_(True)
+    y = conv_ref(xr, wr, br, "SAME", True)
+    yp = F.max_pool2d(y.permute(0, 3, 1, 2), 2, 2).permute(0, 2, 3, 1)
+    dP = rnd(N, 14, 14, 8, dev=dev)
+    dP[..., 6:] = 0
+    yp.backward(dP.float())
+    KM = K.convpool_rows(1, 8, 5, 2, 28, 28)
+    G, Ip, I, brow = K.convpool_reduce_args(1, 8, 5, 2, 28, 28, 1)
+    kw = {"idx": idx, "u8": u8} if src == "u8_idx" else {"idx": idx}
+    xin = norm if src == "bf16_idx" else xb
+    for grid in (1, 13, 96):
+        slab = torch.full((grid * KM * 8,), float("nan"), dtype=torch.float32, device=dev)
+        K.convpool_wgrad(xin, dP, arg, slab, grid, N, 1, 8, 5, 2, 28, 28, **kw)
+        dw = torch.empty(5, 5, 1, 6, device=dev)
+        db = torch.empty(6, device=dev)
+        K.splitk_reduce(slab, grid, KM, 8, G, Ip, I, 6, brow, dw, db, 1.0)
+        close(dw, wr.grad[:, :, :1, :6], rel=3e-2)
+        close(db, br.grad[:6], rel=3e-2)

@@ -561,7 +561,9 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
         // 3 v_max in the lane (no DPP, no keep/send selects, no chain sum).  Unit u = pooled
         // pixels 4u .. 4u+3 of the 8 images (7 units, the last 3 slots recomputed, no store);
         // the 6 pool1 rows 2 y2p .. 2 y2p + 5 are streamed once, each feeding both parities.
-        const int slot = col >> 3, im2 = col & 7, gi2 = t0 + im2;
+        // column -> (slot, image) bit order chosen for the pool1 B reads' bank groups:
+        // 1.9-way average ds_read_b128 conflicts instead of 3.6-way for (col >> 3, col & 7)
+        const int slot = (col >> 2) & 3, im2 = (col >> 4) | ((col & 3) << 1), gi2 = t0 + im2;
 #pragma unroll 1
         for (int j = 0; j < 2; ++j) {
           const int u = w2v + 4 * j;

@@ -332,17 +332,20 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
             *(u32x2*)(pb + off) = u32x2{w0, w1};
           }
         };
+        // 13 slots per wave (units wave + 4j, j = 0..12: 52 slots for the 49 units) -- the
+        // 2-deep pipeline of the lane-pair layout ran 15 windows for 14 slots
         Frags fa = fetch(0), fb = fetch(1);
         f32x16 acca = window(fa), accb;
 #pragma unroll 1
-        for (int j = 0; j < 14; j += 2) {
+        for (int j = 0; j < 12; j += 2) {
           fa = fetch(j + 2);
           accb = window(fb);
           epilogue(acca, j);
-          fb = fetch(j + 3);
+          if (j + 3 < 13) fb = fetch(j + 3);
           acca = window(fa);
           epilogue(accb, j + 1);
         }
+        epilogue(acca, 12);
         xf.store_pre(xs + ((k + 1) & 1) * XBUF, t, a.u8 != nullptr);
       }
       tw = __builtin_amdgcn_s_memtime();

@@ -1964,7 +1964,9 @@ hipError_t convpool_fwd(int cfg, const XSrc& x, const bf16_t* w, const float* bi
   switch (cfg) {
     case 0: return run_fwd<LeNetC1, 2>(x, w, bias, bias_n, B, pooled, arg, st);
     case 1: return run_fwd<LeNetC2, 4>(x, w, bias, bias_n, B, pooled, arg, st);
-    case 2: return run_fwd<RefC1g, 2>(x, w, bias, bias_n, B, pooled, arg, st);
+    case 2:
+      if (refc1_band_enabled()) return refc1_band_fwd(x, w, bias, bias_n, B, pooled, arg, st);
+      return run_fwd<RefC1g, 2>(x, w, bias, bias_n, B, pooled, arg, st);
     case 3: return run_fwd<RefC1c, 4>(x, w, bias, bias_n, B, pooled, arg, st);
   }
   return hipErrorInvalidValue;

@@ -112,6 +112,9 @@ hipError_t lenet_c2dgrad_c1wgrad(const XSrc& x, const bf16_t* dP2, const uint8_t
 // (one persistent kernel; bf16 images only).  x.x = [n][784] images (x.idx: per-sample
 // rows, else sample b = row b).  p1/arg1 (convpool cfg-0 layouts) are written only when
 // p1 != nullptr; p2/arg2 use the convpool cfg-1 layouts.
+bool refc1_band_enabled();
+hipError_t refc1_band_fwd(const XSrc& x, const bf16_t* w, const float* b, int bn, int B, bf16_t* pooled,
+                          uint8_t* arg, hipStream_t st);
 hipError_t lenet_band_fwd(const XSrc& x, const bf16_t* w1, const float* b1, int b1n, const bf16_t* w2,
                           const float* b2, int B, bf16_t* p1, uint8_t* arg1, bf16_t* p2, uint8_t* arg2,
                           hipStream_t st, unsigned long long* prof = nullptr);

@@ -688,7 +688,156 @@ int fwd_grid(int ntiles) {
   return ntiles < per_cu * cus ? ntiles : per_cu * cus;
 }
 
+
+// ============================================================================ reference CNN conv1
+// conv1 of the reference CNN (5x5 SAME, 1 -> 32 channels) + bias + ReLU + 2x2 max-pool on the
+// same banded formulation and in-lane pooling as the LeNet conv1 role above (SURVEY §2.3 N1/N4/N6;
+// /root/reference/mnist_input.py:146-155 conv1 -> pool1): rows = (window position g, 8 channels),
+// so 32 channels are 4 column-sharing row groups; wave pair wp = wave >> 1 owns groups 2wp, 2wp + 1
+// (6 A fragments), the two waves of a pair split the 49 (pooled row pair, window) units of a
+// tile.  The pooled output and its argmax codes (one byte per channel, 4 = ReLU inactive: the
+// convpool layout the LRN / backward kernels read) are stored straight from the lanes.
+constexpr int RNTH = 256;
+constexpr int RW_E = 5 * 5 * 32;               // weights [5][5][1][32]
+constexpr int R_LDS = LDS_X + RW_E + 8;
+static_assert(R_LDS * 2 <= 40960, "four workgroups per CU");
+
+__global__ __launch_bounds__(RNTH) void refc1_band_fwd_k(const BandFwd a) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[R_LDS];
+  bf16_t* xs = lds;
+  bf16_t* ws = lds + LDS_X;                    // weights, then one zero slot of 8
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 31, h = lane >> 5, img = (col >> 1) & 7, half = col >> 4, xq = col & 1;
+  const int ntiles = (a.B + BT - 1) / BT;
+  const int nk = ntiles > (int)blockIdx.x ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  auto tile0 = [&](int k) { return ((int)blockIdx.x + k * (int)gridDim.x) * BT; };
+  for (int e = tid; e < RW_E / 8; e += RNTH) *(u32x4*)(ws + 8 * e) = *(const u32x4*)(a.w1 + 8 * e);
+  if (tid == 0) *(u32x4*)(ws + RW_E) = u32x4{0u, 0u, 0u, 0u};
+  for (int e = tid; e < LDS_X / 8; e += RNTH) *(u32x4*)(xs + 8 * e) = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  const int wp = wave >> 1, wi = wave & 1;     // channel-group pair, unit parity
+  bf16x8 af[2][3];
+  {
+    const int g = col >> 3, ypr = g >> 1, xpr = g & 1, c8 = col & 7;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int dy = 2 * p + h - ypr, dx = j - xpr, c = 8 * (2 * wp + q) + c8;
+          const bool ok = dy >= 0 && dy <= 4 && dx >= 0 && dx <= 4;
+          af[q][p][j] = __builtin_bit_cast(__bf16, ws[ok ? (dy * 5 + dx) * 32 + c : RW_E]);
+        }
+  }
+  float bias[2][4];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = 8 * (2 * wp + q) + 4 * h + i;
+      bias[q][i] = c < a.b1n ? a.b1[c] : 0.f;
+    }
+  const auto rx = a.u8 ? buf_rsrc(a.u8, (uint32_t)a.n * XIMG) : buf_rsrc(a.x, (uint32_t)a.n * (XIMG * 2));
+  const int xlane = img * XIS + h * XPL + (7 * half - 1) * XRW + 2 * xq;
+  const bool top = half == 0, bot = half == 1;
+  XFill xf;
+  xf.init(tid);
+  xf.load(rx, a, nk > 0 ? tile0(0) : -1, tid);
+  xf.store_pre(xs, tid, a.u8 != nullptr);
+  constexpr int NU = (U1 + 1) / 2;             // 25 slots per wave (units wi + 2j)
+  for (int k = 0; k < nk; ++k) {
+    __syncthreads();                           // input[k % 2] landed; input[(k + 1) % 2] free
+    const bf16_t* xb = xs + (k & 1) * XBUF + xlane;
+    const int t0 = tile0(k), gi = t0 + img;
+    xf.load(rx, a, k + 1 < nk ? tile0(k + 1) : -1, tid);
+    struct Frags { bf16x8 b[3]; };
+    auto fetch = [&](int j) {
+      const int f = min(wi + 2 * j, U1 - 1), yp0 = f / 7, u = f - 7 * yp0;
+      const bf16_t* base = xb + yp0 * XRW + 4 * u;
+      Frags fr;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const bf16_t* rp = base + p * XRW;
+        if (p == 0 && yp0 == 0) rp = top ? xs + XZERO : rp;
+        if (p == 2 && yp0 == 6) rp = bot ? xs + XZERO : rp;
+        const uint32_t* qq = (const uint32_t*)rp;
+        fr.b[p] = as_frag(u32x4{qq[0], qq[1], qq[2], qq[3]});
+      }
+      return fr;
+    };
+    auto window = [&](const Frags& fr, int q) {
+      f32x16 acc = {};
+#pragma unroll
+      for (int p = 0; p < 3; ++p) acc = mfma32(af[q][p], fr.b[p], acc);
+      return acc;
+    };
+    auto epilogue = [&](const f32x16& acc, int j, int q) {
+      const int f = wi + 2 * j, yp0 = f / 7, u = f - 7 * yp0;
+      float o[4];
+      uint32_t cw = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v = vmax(vmax3(__uint_as_float(__float_as_uint(acc[i]) & ~3u), embed(acc[4 + i], 1u),
+                                   embed(acc[8 + i], 2u)), embed(acc[12 + i], 3u));
+        o[i] = vmax(__uint_as_float(__float_as_uint(v) & ~3u) + bias[q][i], 0.f);
+        cw |= (o[i] > 0.f ? (__float_as_uint(v) & 3u) : ARG_OFF) << (8 * i);
+      }
+      if (f < U1 && gi < a.B) {
+        const int yp = yp0 + 7 * half, px = 2 * u + xq;
+        const int64_t e = ((int64_t)gi * 196 + yp * 14 + px) * 32 + 8 * (2 * wp + q) + 4 * h;
+        *(u32x2*)(a.p1 + e) = u32x2{pk2(o[0], o[1]), pk2(o[2], o[3])};
+        *(uint32_t*)(a.arg1 + e) = cw;
+      }
+    };
+    Frags fa = fetch(0);
+#pragma unroll 1
+    for (int j = 0; j < NU; ++j) {
+      const Frags fb = fetch(j + 1 < NU ? j + 1 : j);
+      const f32x16 c0 = window(fa, 0);
+      const f32x16 c1 = window(fa, 1);
+      epilogue(c0, j, 0);
+      epilogue(c1, j, 1);
+      fa = fb;
+    }
+    if (k + 1 < nk) xf.store_pre(xs + ((k + 1) & 1) * XBUF, tid, a.u8 != nullptr);
+  }
+}
+
+int refc1_band_grid(int ntiles) {
+  static int per_cu = -1, cus = 0;
+  if (per_cu < 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return -1;
+    cus = prop.multiProcessorCount;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, refc1_band_fwd_k, RNTH, 0) != hipSuccess) return -1;
+    per_cu = nb > 0 ? nb : 1;
+  }
+  return ntiles < per_cu * cus ? ntiles : per_cu * cus;
+}
+
 }  // namespace
+
+// MNISTX_REFC1_BAND=0 keeps the convpool kernel for the reference CNN's conv1 forward
+bool refc1_band_enabled() {
+  static const int on = [] { const char* e = getenv("MNISTX_REFC1_BAND"); return (e && e[0] == '0') ? 0 : 1; }();
+  return on != 0;
+}
+
+hipError_t refc1_band_fwd(const XSrc& x, const bf16_t* w, const float* b, int bn, int B, bf16_t* pooled,
+                          uint8_t* arg, hipStream_t st) {
+  if (B <= 0) return hipSuccess;
+  if (!x.x && !x.u8) return hipErrorInvalidValue;
+  BandFwd a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, w, b, bn, nullptr, nullptr, B, pooled, arg,
+            nullptr, nullptr, nullptr, 0};
+  const int grid = refc1_band_grid((B + BT - 1) / BT);
+  if (grid <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(refc1_band_fwd_k, dim3(grid), dim3(RNTH), 0, st, a);
+  return hipGetLastError();
+}
 
 hipError_t lenet_band_fwd(const XSrc& x, const bf16_t* w1, const float* b1, int b1n, const bf16_t* w2,
                           const float* b2, int B, bf16_t* p1, uint8_t* arg1, bf16_t* p2, uint8_t* arg2,

@@ -50,6 +50,19 @@ DEV void lane_window_sums(const float (&v)[8], int c8, float (&s)[8]) {
 
 // x^p for x > 0 as exp2(p log2 x): two transcendental ops, no ln/log2e rescaling
 DEV float powp(float x, float p) { return __builtin_amdgcn_exp2f(p * __builtin_amdgcn_logf(x)); }
+// sc^-beta and sc^-(beta+1).  The reference's beta = 0.75 (mnist_input.py:151,167) takes two
+// transcendentals, r = sc^-1/2 and q = r^1/2: sc^-0.75 = r q, sc^-1.75 = r^3 q (log + exp +
+// rcp otherwise); the branch is on a kernel argument (uniform)
+DEV void pow_beta(float sc, float beta, float& pw, float& pw1) {
+  if (beta == 0.75f) {
+    const float r = __builtin_amdgcn_rsqf(sc), q = __builtin_amdgcn_sqrtf(r);
+    pw = r * q;
+    pw1 = pw * (r * r);
+  } else {
+    pw = powp(sc, -beta);
+    pw1 = pw * __builtin_amdgcn_rcpf(sc);
+  }
+}
 
 DEV void unpack8(const u32x4& u, float (&v)[8]) {
 #pragma unroll
@@ -90,9 +103,10 @@ DEV u32x4 lrn_bwd8(const u32x4& xv, const u32x4& gv, int c8, float bias, float a
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float sc = bias + alpha * s[j];
-    const float pw = powp(sc, -beta);               // sc^-beta
+    float pw, pw1;                                  // sc^-beta, sc^-(beta+1)
+    pow_beta(sc, beta, pw, pw1);
     s[j] = pw;
-    w[j] = g[j] * v[j] * pw * __builtin_amdgcn_rcpf(sc);
+    w[j] = g[j] * v[j] * pw1;
   }
   lane_window_sums<G, R>(w, c8, u);
   u32x4 o;

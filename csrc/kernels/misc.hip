@@ -399,9 +399,10 @@ __global__ __launch_bounds__(TPB) void lrn_pool_bwd_k(const bf16_t* __restrict__
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float sc = bias + alpha * s[j];
-        const float pw = powp(sc, -beta);
+        float pw, pw1;                                // sc^-beta, sc^-(beta+1) (lrn_math.h)
+        pow_beta(sc, beta, pw, pw1);
         s[j] = pw;
-        w[j] = g[j] * v[j] * pw * __builtin_amdgcn_rcpf(sc);
+        w[j] = g[j] * v[j] * pw1;
       }
       lane_window_sums<G, R>(w, c8, u);
       u32x4 o;

@@ -424,7 +424,7 @@ DEV void make_shifted(bf16_t* tile, int tid) {
 // Pooled gradient + argmax bytes ([img][window][Cout]), 8 channels per vector.
 // LRNB: y is dL/d(LRN output) and p the LRN input (LrnFold); store() stages the
 // LRN backward of them (bitwise lrn_bwd_k: same lrn_bwd8, same bf16 rounding).
-template <class G, int IMGS, bool LRNB = false>
+template <class G, int IMGS, int LRNB = 0>   // LRNB: 0 no fold, 1 LRN fold, 2 LRN fold with beta = 0.75
 struct DYStage {
   static constexpr int NWC = G::NWIN * G::COUT;
   static constexpr int NV = IMGS * NWC / 8;
@@ -452,7 +452,7 @@ struct DYStage {
     if constexpr (LRNB) {
 #pragma unroll
       for (int u = 0; u < PER; ++u) {
-        y[u] = lrn_bwd8<G::COUT / 8, 4>(p[u], y[u], tid % (G::COUT / 8), f.bias, f.alpha, f.beta, 0);
+        y[u] = lrn_bwd8<G::COUT / 8, 4, LRNB == 2>(p[u], y[u], tid % (G::COUT / 8), f.bias, f.alpha, f.beta, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -946,7 +946,7 @@ __global__ __launch_bounds__(NTH) void convpool_fwd_quad_k(const XSrc x, const b
 // with ds_read_b64_tr_b16: each lane supplies one pixel row and one 4-column
 // chunk; the bias row (k = KE) reads a constant [1,0,0,0] LDS cell.  dY is
 // rebuilt from (dP, arg): position d of a window gets dP iff arg == d.
-template <class G, int IMGS, bool LRNB = false, bool PRIO = false>
+template <class G, int IMGS, int LRNB = 0, bool PRIO = false>
 __global__ __launch_bounds__(NTH, wgrad_minw<G>()) void convpool_wgrad_k(const XSrc x, const bf16_t* __restrict__ dP,
                                                         const uint8_t* __restrict__ arg, int B,
                                                         float* __restrict__ slab, const LrnFold lrn) {
@@ -1602,13 +1602,15 @@ hipError_t run_wgrad(const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B,
     if (prio) hipLaunchKernelGGL((convpool_wgrad_pair_k<G, IMGS, true>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab);
     else hipLaunchKernelGGL((convpool_wgrad_pair_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab);
   } else if constexpr (G::COUT == 32) {
-    if (lrn.p)
-      hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS, true>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
+    if (lrn.p && lrn.beta == 0.75f)   // the reference's beta: pow_beta<true> (lrn_math.h)
+      hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS, 2>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
+    else if (lrn.p)
+      hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS, 1>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
     else
       hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
   } else {
     if (lrn.p) return hipErrorInvalidValue;
-    if (prio) hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS, false, true>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
+    if (prio) hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS, 0, true>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
     else hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
   }
   return hipGetLastError();

@@ -52,9 +52,12 @@ DEV void lane_window_sums(const float (&v)[8], int c8, float (&s)[8]) {
 DEV float powp(float x, float p) { return __builtin_amdgcn_exp2f(p * __builtin_amdgcn_logf(x)); }
 // sc^-beta and sc^-(beta+1).  The reference's beta = 0.75 (mnist_input.py:151,167) takes two
 // transcendentals, r = sc^-1/2 and q = r^1/2: sc^-0.75 = r q, sc^-1.75 = r^3 q (log + exp +
-// rcp otherwise); the branch is on a kernel argument (uniform)
+// rcp otherwise).  B075 is a template argument, chosen on the host from the kernel's beta: a
+// runtime test on beta, uniform as it is, was compiled into one branch per value (32 per
+// pixel vector in lrn_pool_bwd_k, each with its exec-mask juggling and s_nop padding).
+template <bool B075>
 DEV void pow_beta(float sc, float beta, float& pw, float& pw1) {
-  if (beta == 0.75f) {
+  if constexpr (B075) {
     const float r = __builtin_amdgcn_rsqf(sc), q = __builtin_amdgcn_sqrtf(r);
     pw = r * q;
     pw1 = pw * (r * r);
@@ -92,7 +95,7 @@ DEV u32x4 lrn_fwd8(const u32x4& xv, int c8, float bias, float alpha, float beta)
 // LRN backward of one 8-channel vector (x = LRN input, g = dL/dy; G lanes per pixel):
 // dx[c] = g[c] s[c]^-b - 2ab x[c] sum_{|c'-c|<=R} g[c'] x[c'] s[c']^(-b-1), s = bias +
 // alpha * window sum of x^2; relu_mask zeroes dx where x <= 0.  Rounded to bf16.
-template <int G, int R>
+template <int G, int R, bool B075 = false>
 DEV u32x4 lrn_bwd8(const u32x4& xv, const u32x4& gv, int c8, float bias, float alpha, float beta, int relu_mask) {
   float v[8], g[8], w[8], s[8], u[8];
   unpack8(xv, v);
@@ -104,7 +107,7 @@ DEV u32x4 lrn_bwd8(const u32x4& xv, const u32x4& gv, int c8, float bias, float a
   for (int j = 0; j < 8; ++j) {
     const float sc = bias + alpha * s[j];
     float pw, pw1;                                  // sc^-beta, sc^-(beta+1)
-    pow_beta(sc, beta, pw, pw1);
+    pow_beta<B075>(sc, beta, pw, pw1);
     s[j] = pw;
     w[j] = g[j] * v[j] * pw1;
   }

@@ -274,7 +274,7 @@ __global__ __launch_bounds__(TPB) void lrn_fwd_k(const bf16_t* __restrict__ x, i
 }
 
 // dx[c] = dy[c] s[c]^-b - 2ab x[c] sum_{|c'-c|<=R} dy[c'] x[c'] s[c']^(-b-1)
-template <int C, int R>
+template <int C, int R, bool B075 = false>
 __global__ __launch_bounds__(TPB) void lrn_bwd_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
                                                  int64_t P, float bias, float alpha, float beta, int relu_mask,
                                                  bf16_t* __restrict__ dx) {
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(TPB) void lrn_bwd_k(const bf16_t* __restrict__ x, c
     const bool ok = t < total;
     const u32x4 xv = *(const u32x4*)(x + (ok ? t : 0) * 8);    // unconditional (clamped) loads
     const u32x4 gv = *(const u32x4*)(dy + (ok ? t : 0) * 8);
-    const u32x4 o = lrn_bwd8<G, R>(xv, gv, c8, bias, alpha, beta, relu_mask);
+    const u32x4 o = lrn_bwd8<G, R, B075>(xv, gv, c8, bias, alpha, beta, relu_mask);
     if (ok) *(u32x4*)(dx + t * 8) = o;
   }
 }
@@ -353,7 +353,7 @@ __global__ __launch_bounds__(TPB) void lrn_pool_fwd_k(const bf16_t* __restrict__
   }
 }
 
-template <int C, int R>
+template <int C, int R, bool B075 = false>
 __global__ __launch_bounds__(TPB) void lrn_pool_bwd_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dP,
                                                       const uint8_t* __restrict__ arg, int Nb, int H, int W,
                                                       float bias, float alpha, float beta, int relu_mask,
@@ -400,7 +400,7 @@ __global__ __launch_bounds__(TPB) void lrn_pool_bwd_k(const bf16_t* __restrict__
       for (int j = 0; j < 8; ++j) {
         const float sc = bias + alpha * s[j];
         float pw, pw1;                                // sc^-beta, sc^-(beta+1) (lrn_math.h)
-        pow_beta(sc, beta, pw, pw1);
+        pow_beta<B075>(sc, beta, pw, pw1);
         s[j] = pw;
         w[j] = g[j] * v[j] * pw1;
       }
@@ -971,18 +971,28 @@ hipError_t lrn_pool_bwd(const bf16_t* x, const bf16_t* dP, const uint8_t* arg, i
                         float bias, float alpha, float beta, int relu_mask, bf16_t* dx, hipStream_t st) {
   if (!lrn_pool_supported(H, W, C, r)) return hipErrorInvalidValue;
   dim3 grid(nblocks((int64_t)Nb * (H / 2) * (W / 2) * (C / 8), TPB, 16384));
-  if (C == 64)
-    hipLaunchKernelGGL((lrn_pool_bwd_k<64, 4>), grid, dim3(TPB), 0, st, x, dP, arg, Nb, H, W, bias, alpha, beta,
-                       relu_mask, dx);
-  else
-    hipLaunchKernelGGL((lrn_pool_bwd_k<32, 4>), grid, dim3(TPB), 0, st, x, dP, arg, Nb, H, W, bias, alpha, beta,
-                       relu_mask, dx);
+#define LRN_PB(CC, BB) \
+  hipLaunchKernelGGL((lrn_pool_bwd_k<CC, 4, BB>), grid, dim3(TPB), 0, st, x, dP, arg, Nb, H, W, bias, alpha, beta, relu_mask, dx)
+  const bool b075 = beta == 0.75f;   // the reference's beta (lrn_math.h pow_beta)
+  if (C == 64) {
+    if (b075) LRN_PB(64, true);
+    else LRN_PB(64, false);
+  } else {
+    if (b075) LRN_PB(32, true);
+    else LRN_PB(32, false);
+  }
+#undef LRN_PB
   return hipGetLastError();
 }
 
 hipError_t lrn_bwd(const bf16_t* x, const bf16_t* dy, int P, int C, int r, float bias, float alpha, float beta,
                    int relu_mask, bf16_t* dx, hipStream_t st) {
   dim3 grid(nblocks((int64_t)P * (C / 8), TPB, 16384));
+  if (beta == 0.75f && r == 4 && (C == 32 || C == 64)) {   // the reference CNN's layers: pow_beta<true>
+    if (C == 32) hipLaunchKernelGGL((lrn_bwd_k<32, 4, true>), grid, dim3(TPB), 0, st, x, dy, (int64_t)P, bias, alpha, beta, relu_mask, dx);
+    else hipLaunchKernelGGL((lrn_bwd_k<64, 4, true>), grid, dim3(TPB), 0, st, x, dy, (int64_t)P, bias, alpha, beta, relu_mask, dx);
+    return hipGetLastError();
+  }
   LRN_ALL(lrn_bwd_k, x, dy, (int64_t)P, bias, alpha, beta, relu_mask, dx)
   return hipErrorInvalidValue;
 }

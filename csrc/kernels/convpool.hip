@@ -1240,6 +1240,18 @@ __global__ __launch_bounds__(NTH, 7) void convpool_wgrad_pair_k(const XSrc x,
 #pragma unroll
   for (int mf = 0; mf < G::MFW; ++mf) acc[mf] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // IMGS == 1: pixel bases of this wave's steps (wtab's values, computed in registers)
+  constexpr int NSW = (RS + NTH / 64 - 1) / (NTH / 64);
+  int pbs[NSW][2];
+#pragma unroll
+  for (int k = 0; k < NSW; ++k)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int w = min(16 * (wave + k * (NTH / 64)) + 2 * g + (q >> 1) + 8 * h, G::NWIN - 1);
+      const int a = G::wbase(w);
+      pbs[k][h] = ((a & 3) ? a - 2 + C2OFF : a) + (q & 1) * G::WS;
+    }
+
   const int stride = gridDim.x * IMGS;
   XStage<G, IMGS> xs;
   DYStage<G, IMGS> ys;
@@ -1285,16 +1297,11 @@ __global__ __launch_bounds__(NTH, 7) void convpool_wgrad_pair_k(const XSrc x,
       ys.load(dP, arg, img0 + stride, B, tid);
     }
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-    for (int it = wave; it < IMGS * RS; it += NTH / 64) {
-      const int im = it / RS, s = it - im * RS;
+    // one reduction step: dY operand from U, im2col^T rows at this lane's pixel bases pb0 / pb1
+    auto step = [&](int im, int s, int pb0, int pb1) {
       // dY operand: element j <-> window 16s + 2g + ((j>>1)&1) + 8(j>>2), dy = j&1
       const uint32_t* ub = U + im * UIMG + li * URS + 16 * s + 2 * g;
       const bf16x8 bfr = join(*(const s16x4*)ub, *(const s16x4*)(ub + opaque(8)));
-      // im2col^T operand rows supplied by this lane: slot 4g+q (+16): window 16s + 2g + q/2 (+8), dy = q&1
-      // (dy adds WS and the chunk deltas are multiples of 4: the copy is the window's)
-      const int wq = 16 * s + 2 * g + (q >> 1);
-      const int pb0 = im * G::IMG_LDS + wtab[min(wq, G::NWIN - 1)] + (q & 1) * G::WS;
-      const int pb1 = im * G::IMG_LDS + wtab[min(wq + 8, G::NWIN - 1)] + (q & 1) * G::WS;
 #pragma unroll
       for (int mf = 0; mf < G::MFW; ++mf) {
         const bf16_t* a0 = tile + pb0 + cd[mf];
@@ -1305,6 +1312,22 @@ __global__ __launch_bounds__(NTH, 7) void convpool_wgrad_pair_k(const XSrc x,
         }
         const bf16x8 a = join(lds_tr4(a0), lds_tr4(a1));
         acc[mf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr, acc[mf], 0, 0, 0);
+      }
+    };
+    if constexpr (IMGS == 1) {
+      // one image per group: a wave's steps s = wave + 4k are the same every group, so the
+      // pixel bases were computed once (pbs) -- no wtab lookup ahead of the tr reads
+#pragma unroll
+      for (int k = 0; k < NSW; ++k)
+        if (wave + k * (NTH / 64) < RS) step(0, wave + k * (NTH / 64), pbs[k][0], pbs[k][1]);
+    } else {
+      for (int it = wave; it < IMGS * RS; it += NTH / 64) {
+        const int im = it / RS, s = it - im * RS;
+        // im2col^T operand rows supplied by this lane: slot 4g+q (+16): window 16s + 2g + q/2 (+8), dy = q&1
+        // (dy adds WS and the chunk deltas are multiples of 4: the copy is the window's)
+        const int wq = 16 * s + 2 * g + (q >> 1);
+        step(im, s, im * G::IMG_LDS + wtab[min(wq, G::NWIN - 1)] + (q & 1) * G::WS,
+             im * G::IMG_LDS + wtab[min(wq + 8, G::NWIN - 1)] + (q & 1) * G::WS);
       }
     }
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);

@@ -1060,15 +1060,20 @@ __global__ __launch_bounds__(NTH, wgrad_minw<G>()) void convpool_wgrad_k(const X
       const int lane_a = 4 * (p & 1) + e1 * G::CIN;
       const int lane_b = 4 * (p & 1) + e1 * (G::WS - G::KS + 1) * G::CIN;
       auto toff = [](int t) constexpr { return ((t / G::KS) * G::WS + t % G::KS) * G::CIN; };
+      // RSTEPS == waves (LeNet conv2: 4): every step of a wave has s = wave, so its window
+      // bases are fixed -- computed here, not looked up in wtab ahead of each step's tr reads
+      constexpr bool FIXS = G::RSTEPS == NTH / 64;
+      const int fb0 = G::wbase(min(8 * wave + g, G::NWIN - 1)) + G::doff(q);
+      const int fb1 = G::wbase(min(8 * wave + g + 4, G::NWIN - 1)) + G::doff(q);
       if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
       for (int it = wave; it < IMGS * G::RSTEPS; it += NTH / 64) {
-        const int im = it / G::RSTEPS, s = it - im * G::RSTEPS;
+        const int im = it / G::RSTEPS, s = FIXS ? wave : it - im * G::RSTEPS;
         const int w0 = 8 * s + g;
         const bf16_t* ub = U2 + ((im * G::COUT + li) * URW + w0) * 4;
         const bf16x8 bfr = join(*(const s16x4*)ub, *(const s16x4*)(ub + opaque(16)));
         // rows supplied by this lane: pixel q of windows w0 / w0 + 4 (clamped; dY is zero there)
-        const bf16_t* t0 = tile + im * G::IMG_LDS + wtab[w0] + G::doff(q);
-        const bf16_t* t1 = tile + im * G::IMG_LDS + wtab[w0 + 4] + G::doff(q);
+        const bf16_t* t0 = tile + im * G::IMG_LDS + (FIXS ? fb0 : wtab[w0] + G::doff(q));
+        const bf16_t* t1 = tile + im * G::IMG_LDS + (FIXS ? fb1 : wtab[w0 + 4] + G::doff(q));
 #pragma unroll
         for (int mf = 0; mf < G::MFW; ++mf) {
           const bool rowend = (2 * mf) % G::KS == G::KS - 1;

@@ -32,7 +32,10 @@ TARGET_BLOCKS = 2048
 # reduce (fc3 at B=65536: S=64 24.9 us vs S=147 ~34 us; LeNet-5 step 0.761 ->
 # 0.744 ms).  Gather-bound im2col weight gradients and many-tile dense ones
 # (reference CNN conv2 / local3) measured faster at 2048 (4.16 vs 4.78 ms/step).
-TARGET_BLOCKS_FEW_TILES = int(os.environ.get("MNISTX_WGRAD_BLOCKS", "512"))
+# Round 3, with the head weight gradients grouped on 64x128 tiles: 256 (~1 per CU)
+# beat 512 in 5 of 5 same-box pairs, LeNet-5 0.5255 vs 0.5291 ms/step on average
+# (128: 0.5293, 384: 0.5260, 768: 0.5342, 1024: 0.5402; profiles/r3/lenet/wgrad_blocks/).
+TARGET_BLOCKS_FEW_TILES = int(os.environ.get("MNISTX_WGRAD_BLOCKS", "256"))
 # 128x128-tile dense weight gradients (reference local3): ~2 splits (bench/micro_wgrad.py
 # ref: S=2 155.9 us, S=3 165.0, S=8 154.4, S=16 197.1 -- the fewest splits that fill
 # the GPU keep the slab smallest)

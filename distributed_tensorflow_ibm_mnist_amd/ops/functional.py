@@ -38,8 +38,9 @@ TARGET_BLOCKS = 2048
 TARGET_BLOCKS_FEW_TILES = int(os.environ.get("MNISTX_WGRAD_BLOCKS", "256"))
 # 128x128-tile dense weight gradients (reference local3): ~2 splits (bench/micro_wgrad.py
 # ref: S=2 155.9 us, S=3 165.0, S=8 154.4, S=16 197.1 -- the fewest splits that fill
-# the GPU keep the slab smallest)
-TARGET_BLOCKS_BIG_TILES = 400
+# the GPU keep the slab smallest; round 3, whole reference-CNN step: 256 / 400 / 600 / 800
+# within noise, 2.19-2.22 ms, profiles/r3/refcnn/wgrad_blocks_big/)
+TARGET_BLOCKS_BIG_TILES = int(os.environ.get("MNISTX_WGRAD_BLOCKS_BIG", "400"))
 
 def pad8(c: int) -> int:
     return (c + 7) // 8 * 8

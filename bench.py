@@ -103,6 +103,42 @@ def prewarm(dev, ms: float) -> None:
     del a, b, c
 
 
+def pg_block(dev, t_local: float):
+    """The process group as the ranks see it (not the environment): backend, size, each
+    rank's device identity (index, PCI bus / UUID where torch exposes them, host), the
+    RCCL version and the min / max per-rank timed seconds.  ``shared`` lists ranks that
+    sit on the same physical device (the caller exits non-zero for that under nccl)."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+    props = torch.cuda.get_device_properties(dev)
+    pci = tuple(getattr(props, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    uuid = str(getattr(props, "uuid", "") or "")
+    me = {"rank": dist.get_rank(), "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "device": dev.index,
+          "pci": "%04x:%02x:%02x" % tuple(v or 0 for v in pci) if any(v is not None for v in pci) else None,
+          "uuid": uuid or None, "host": socket.gethostname(), "name": props.name, "timed_s": t_local}
+    ranks = [None] * dist.get_world_size()
+    dist.all_gather_object(ranks, me)
+    seen, shared = {}, []
+    for r in ranks:
+        key = (r["host"], r["uuid"] or r["pci"] or f"dev{r['device']}")
+        if key in seen:
+            shared.append([seen[key], r["rank"]])
+        else:
+            seen[key] = r["rank"]
+    try:
+        ver = torch.cuda.nccl.version()
+        rccl = ".".join(str(v) for v in ver) if isinstance(ver, tuple) else str(ver)
+    except Exception:              # noqa: BLE001 -- no RCCL in this build
+        rccl = None
+    ts = [r["timed_s"] for r in ranks]
+    return {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "rccl_version": rccl,
+            "ranks": [{k: v for k, v in r.items() if k != "timed_s"} for r in ranks],
+            "distinct_devices": len(seen), "shared": shared,
+            "timed_s_min": round(min(ts), 6), "timed_s_max": round(max(ts), 6)}
+
+
 def run_ps(args) -> int:
     """1 PS + (N-1) asynchronous workers.  The PS clock is the
     authoritative one: it marks the wall time when the shared global step passes
@@ -121,8 +157,10 @@ def run_ps(args) -> int:
     from distributed_tensorflow_ibm_mnist_amd.data.device_loader import DeviceDataset, DeviceLoader
 
     # one hardware queue per PS/worker process (before HIP starts): co-located tasks
-    # otherwise oversubscribe the GPU's queue scheduler (profiles/r3/ps/ps_hwq_ab.txt)
-    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("MNISTX_PS_HW_QUEUES", "1")
+    # otherwise oversubscribe the GPU's queue scheduler (profiles/r3/ps/ps_hwq_ab.txt);
+    # a value set in the environment is kept
+    if "GPU_MAX_HW_QUEUES" not in os.environ:
+        os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("MNISTX_PS_HW_QUEUES", "1")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -163,6 +201,7 @@ def run_ps(args) -> int:
             "ps_us_per_msg": {k: round(v / max(1, res["applied"]) * 1e6, 1) for k, v in res["phase_s"].items()},
             "param_checksum": float(ps.fp.params.double().sum().item()),
             "transport_used": ps.tx.name,
+            "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
         }
         comms = [None] * world
         dist.gather_object(None, comms, dst=0)
@@ -308,6 +347,8 @@ def main() -> int:
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     el = float(elapsed.item())
+    # N > 1 (or the one-rank RCCL rehearsal): what the process group itself saw
+    pg = pg_block(dev, t1 - t0) if dist.is_initialized() else None
     eager_ms = None
     n_eager = args.steps if args.eager_steps < 0 else args.eager_steps
     if graph is not None and n_eager > 0:   # outside the timed region: the same step, eager
@@ -405,8 +446,17 @@ def main() -> int:
             # per-bucket all-reduce time / bus bandwidth and the exposed communication
             # (eager step with minus without collectives), measured after the timed steps
             "comm": comm,
+            "pg": pg,
+            "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),   # None = HIP's default
         }
         print(json.dumps(out), flush=True)
+    if pg is not None and pg["shared"] and pg["backend"] == "nccl":
+        if rank == 0:
+            print(f"[bench] ERROR: ranks {pg['shared']} share one device under nccl; the multi-GPU number "
+                  f"is not a {world}-GPU measurement", file=sys.stderr)
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        return 3
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0

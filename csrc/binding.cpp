@@ -1001,6 +1001,10 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("NC"), py::arg("scale"), py::arg("dlogits"), py::arg("ldd"), py::arg("stats"), py::arg("probs"),
         py::arg("work") = py::none());
   m.def("f32_prep_images", &f32_prep_images);
+  // test hook: cap every persistent kernel's grid (0 = off) so small-batch oracle tests run
+  // the multi-iteration (several tiles per block) paths the benchmark batches run
+  m.def("set_grid_cap", [](int64_t n) { mnistx::set_grid_cap((int)n); });
+  m.def("grid_cap", []() { return (int64_t)mnistx::grid_cap(); });
   m.def("lenet_c2dgrad_c1wgrad",&lenet_c2dgrad_c1wgrad, py::arg("x"), py::arg("dP2"), py::arg("arg2"), py::arg("w2"),
         py::arg("arg1"), py::arg("slab"), py::arg("grid"), py::arg("B"), py::arg("u8") = py::none(),
         py::arg("idx") = py::none());

@@ -197,7 +197,7 @@ hipError_t f32_conv1_fwd(const float* x, const float* w, int Nb, const float* bi
                          hipStream_t st) {
   if (Nb <= 0) return hipSuccess;
   static const int n = resident((const void*)conv1_f32_fwd_k);
-  hipLaunchKernelGGL(conv1_f32_fwd_k, dim3(Nb < n ? Nb : n), dim3(NT1), 0, st, x, w, bias, relu, Nb, y);
+  hipLaunchKernelGGL(conv1_f32_fwd_k, dim3(cap_grid(Nb < n ? Nb : n)), dim3(NT1), 0, st, x, w, bias, relu, Nb, y);
   return hipGetLastError();
 }
 hipError_t f32_conv1_wgrad(const float* x, const float* dy, int Nb, int splits, float* slab, hipStream_t st) {

@@ -383,7 +383,7 @@ int halo_grid(int B) {
       per = 256;
   }
   const int groups = (B + IMGS - 1) / IMGS;
-  return groups < per ? groups : per;
+  return cap_grid(groups < per ? groups : per);
 }
 
 template <int CIN, int CW, int NW, int MODE, int FR, int IMGS = 1, bool LRNX = false>

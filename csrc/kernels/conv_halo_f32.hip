@@ -335,7 +335,7 @@ int halo_f32_grid(int B) {
     else
       per = 256;
   }
-  return B < per ? B : per;
+  return cap_grid(B < per ? B : per);
 }
 
 template <int CR, int CW, int NW, int MODE, int FR>

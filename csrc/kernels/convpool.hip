@@ -1563,7 +1563,7 @@ __global__ __launch_bounds__(NTH, MINW) void convpool_dgrad_pair_k(const bf16_t*
 
 int grid_for(int B, int imgs, int cap) {
   int n = (B + imgs - 1) / imgs;
-  return n < cap ? (n < 1 ? 1 : n) : cap;
+  return cap_grid(n < cap ? (n < 1 ? 1 : n) : cap);
 }
 
 // Workgroups that fill every CU exactly once (occupancy API, cached per kernel):
@@ -1659,6 +1659,7 @@ hipError_t run_dgrad(const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int 
 #define MNISTX_DG(IM, ...)                                                                                   \
   cap = resident_grid<convpool_dgrad_pair_k<G, __VA_ARGS__>>();                                            \
   if (grid_cap > 0 && grid_cap < cap) cap = grid_cap;                                                      \
+  cap = cap_grid(cap);                                                                                     \
   hipLaunchKernelGGL((convpool_dgrad_pair_k<G, __VA_ARGS__>), dim3(grid_for(B, IM, cap)), dim3(NTH), 0, st, \
                      dP, arg, w, B, dx);
   // MFMA-phase priority on by default (backward phase 348 -> 338-339 us with the wgrad

@@ -9,6 +9,17 @@ namespace mnistx {
 
 typedef uint16_t bf16_t;
 
+// Test hook (binding set_grid_cap, never set in production): an upper bound on the grid of
+// every persistent grid-stride kernel, so the oracle tests run the multi-iteration paths
+// (several tiles / images per block: ring reuse, next-tile prefetch) at small batches.
+// 0 = no cap.
+int grid_cap();
+void set_grid_cap(int n);
+inline int cap_grid(int g) {
+  const int c = grid_cap();
+  return (c > 0 && g > c) ? c : g;
+}
+
 enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_SLAB = 2 };
 
 struct GemmEpi {

@@ -685,7 +685,7 @@ int fwd_grid(int ntiles) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lenet_band_fwd_k<P1OUT, INL>, NTH, 0) != hipSuccess) return -1;
     per_cu = nb > 0 ? nb : 1;
   }
-  return ntiles < per_cu * cus ? ntiles : per_cu * cus;
+  return cap_grid(ntiles < per_cu * cus ? ntiles : per_cu * cus);
 }
 
 
@@ -816,7 +816,7 @@ int refc1_band_grid(int ntiles) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, refc1_band_fwd_k, RNTH, 0) != hipSuccess) return -1;
     per_cu = nb > 0 ? nb : 1;
   }
-  return ntiles < per_cu * cus ? ntiles : per_cu * cus;
+  return cap_grid(ntiles < per_cu * cus ? ntiles : per_cu * cus);
 }
 
 }  // namespace

@@ -901,6 +901,10 @@ __global__ void cast_pad_k(const float* __restrict__ src, bf16_t* __restrict__ d
 
 }  // namespace
 
+static int g_grid_cap = 0;
+int grid_cap() { return g_grid_cap; }
+void set_grid_cap(int n) { g_grid_cap = n > 0 ? n : 0; }
+
 hipError_t perm_positions(int64_t* out, int64_t start, int n, int64_t N, uint32_t seed, int h, hipStream_t st,
                           const int32_t* lab_src, int32_t* lab_out) {
   if (n <= 0) return hipSuccess;

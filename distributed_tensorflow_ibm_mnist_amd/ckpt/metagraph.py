@@ -51,7 +51,7 @@ def _zeros_tensor(dt: int, dims) -> bytes:          # TensorProto: one value bro
     elif dt == DT_INT64:
         body += f_bytes(10, b"\x00")                 # packed int64_val
     else:
-        body += f_bytes(6, b"\x00")                  # packed int_val
+        body += f_bytes(7, b"\x00")                  # packed int_val (TensorProto field 7; 6 is double_val)
     return body
 
 

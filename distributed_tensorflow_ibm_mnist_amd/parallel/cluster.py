@@ -97,6 +97,8 @@ def _attempt_store(rank: int, world: int, timeout: datetime.timedelta):
 
 
 GEN_KEY = "mnistx/gen"
+DONE_KEY = "mnistx/done"        # + /rank<r>: a PS-mode worker that has started its shutdown
+EXIT_NO_INPLACE = 87            # a restarted PS that cannot rejoin in place (supervisor.py: whole-job restart)
 
 
 def _gen_prefix(gen: int) -> str:
@@ -175,7 +177,14 @@ def setup_distribute(job_name: str = "", ps_hosts: str = "", worker_hosts: str =
             gen = 0
             if cl.job_name == "ps" and cl.store.add(f"mnistx/ps{cl.task_id}/starts", 1) > 1:
                 # a restarted parameter server: open the next session generation; the
-                # surviving workers / PS tasks notice the failure and rejoin it
+                # surviving workers / PS tasks notice the failure and rejoin it -- unless a
+                # worker has already finished (it can never rejoin, so the new generation
+                # would wait for it until the collective timeout): exit with EXIT_NO_INPLACE
+                # and let the supervisor restart the whole job from the checkpoint instead
+                gone = [r for r in range(cl.num_ps, cl.world) if cl.store.check([f"{DONE_KEY}/rank{r}"])]
+                if gone:
+                    log(f"[ps {cl.task_id}] restarted after rank(s) {gone} finished: no in-place recovery")
+                    raise SystemExit(EXIT_NO_INPLACE)
                 gen = int(cl.store.add(GEN_KEY, 1))
                 log(f"[ps {cl.task_id}] restarted: opening session generation {gen}")
             rejoin(cl, gen)

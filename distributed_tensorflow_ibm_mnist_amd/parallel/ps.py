@@ -103,6 +103,7 @@ from ..runtime.params import FlatParams, OptConfig
 
 HELLO, GRAD, STATE, DONE, RESET = 0, 1, 2, 3, 4
 FATAL_KEY = "mnistx/fatal"      # set by a PS that stops on an error no restart would fix
+EXIT_FATAL = 86                 # a PS's exit code for such an error: the supervisor never restarts it
 CTRL = 8
 TAG_CTRL, TAG_DATA = 1, 2
 
@@ -133,6 +134,22 @@ def default_transport(device: torch.device) -> str:
 def _sync(t: torch.Tensor) -> None:
     if t.is_cuda:
         torch.cuda.current_stream(t.device).synchronize()
+
+
+def is_peer_loss(e: BaseException) -> bool:
+    """A control-plane failure that a lost / restarted peer explains: torch's
+    ``DistBackendError`` / ``DistNetworkError``, or gloo's connection-closed / reset /
+    timeout errors (raised as plain RuntimeError by some builds).  Never a
+    ``PushIntegrityError`` or a HIP / torch compute error."""
+    if isinstance(e, PushIntegrityError):
+        return False
+    for name in ("DistBackendError", "DistNetworkError", "DistStoreError"):
+        t = getattr(dist, name, None)
+        if t is not None and isinstance(e, t):
+            return True
+    msg = str(e).lower()
+    return any(k in msg for k in ("gloo", "connection", "connect", "timed out", "timeout", "reset by peer",
+                                  "broken pipe", "socket", "closed", "eof"))
 
 
 class PushIntegrityError(RuntimeError):
@@ -576,17 +593,29 @@ class PSClient:
         if timeout_s is None:
             timeout_s = float(os.environ.get("MNISTX_PS_RECOVERY_TIMEOUT", "300"))
         t_end = time.time() + timeout_s
-        gen = current_gen(cl)
-        while gen <= cl.gen:
-            if cl.store.check([FATAL_KEY]):    # the PS failed on purpose (e.g. a rejected push): no recovery
+
+        def fatal() -> bool:               # the PS failed on purpose (e.g. a rejected push): no recovery
+            if cl.store.check([FATAL_KEY]):
                 self.log(f"[worker {self.wi}] parameter server reported a fatal error: "
                          f"{cl.store.get(FATAL_KEY).decode()[:300]}")
+                return True
+            return False
+
+        # checked before AND after the generation compare: a restarted PS that opened the next
+        # generation must not pull the survivors past a rejected push
+        if fatal():
+            raise err
+        gen = current_gen(cl)
+        while gen <= cl.gen:
+            if fatal():
                 raise err
             if time.time() > t_end:
                 self.log(f"[worker {self.wi}] no parameter server came back within {timeout_s:.0f} s")
                 raise err
             time.sleep(0.05)
             gen = current_gen(cl)
+        if fatal():
+            raise err
         # a surviving PS that took this exchange's control word is blocked sending its reply
         # (gloo sends complete only when matched): take those replies on the old group first
         fp = self.net.fp
@@ -624,13 +653,14 @@ class PSClient:
     def _exchange(self, kind: int, want_state: bool = False) -> None:
         """One exchange with every PS; on a control-plane failure (a PS died) the session
         is recreated and the exchange re-sent -- as a pull only to the PS tasks that
-        already took this push."""
+        already took this push.  Any other error (HIP, torch, a rejected push) is re-raised
+        at once instead of waiting for a recovery that cannot come."""
         took: set = set()
         while True:
             try:
                 return self._exchange_once(kind, want_state, took)
-            except RuntimeError as e:     # gloo: connection closed / reset / timeout
-                if isinstance(e, PushIntegrityError):
+            except RuntimeError as e:
+                if not is_peer_loss(e):
                     raise
                 self.recover(e)
 
@@ -710,10 +740,27 @@ class PSClient:
         self._exchange(STATE, want_state=True)
 
     def done(self) -> None:
-        for j in range(self.k):
-            c = torch.zeros(CTRL, dtype=torch.int64)
-            c[0] = DONE
-            dist.send(c, j, group=self.group, tag=TAG_CTRL)
+        """DONE to every PS, through the same recovery as an exchange: a PS that dies
+        while the workers shut down is relaunched and still hears every DONE."""
+        if self.cluster is not None and self.cluster.store is not None:
+            from .cluster import DONE_KEY
+            self.cluster.store.set(f"{DONE_KEY}/rank{dist.get_rank()}", "1")
+        told: set = set()
+        while True:
+            try:
+                for j in range(self.k):
+                    if j in told:
+                        continue
+                    c = torch.zeros(CTRL, dtype=torch.int64)
+                    c[0] = DONE
+                    dist.send(c, j, group=self.group, tag=TAG_CTRL)
+                    told.add(j)
+                return
+            except RuntimeError as e:
+                if not is_peer_loss(e):
+                    raise
+                self.recover(e)
+                told.clear()              # a new generation: every PS (re)counts DONE from scratch
 
     def shard_of(self) -> Dict[str, int]:
         out = {}

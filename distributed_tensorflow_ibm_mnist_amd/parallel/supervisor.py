@@ -39,6 +39,9 @@ import sys
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
+EXIT_FATAL = 86      # parallel/ps.py EXIT_FATAL (kept import-free: the supervisor never loads torch)
+EXIT_NO_INPLACE = 87  # parallel/cluster.py: a restarted PS found a finished worker -> whole-job restart
+
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
@@ -130,7 +133,14 @@ def supervise(flags: Sequence[str], num_ps: int = 1, num_workers: int = 2, max_r
         ps_restarts = 0
         while True:
             done, failure = att.poll()
-            if failure is not None and recover_ps and failure[0].startswith("ps") and ps_restarts < max_restarts:
+            if failure is not None and failure[1] == EXIT_FATAL:
+                # the process stopped on an error no restart would fix (e.g. a rejected push):
+                # neither an in-place PS restart nor a whole-job restart
+                log(f"[supervisor] {failure[0]} exited with {failure[1]} (fatal); not restarting")
+                att.teardown()
+                return EXIT_FATAL
+            if (failure is not None and recover_ps and failure[0].startswith("ps") and ps_restarts < max_restarts
+                    and failure[1] != EXIT_NO_INPLACE):
                 # a parameter server died: relaunch just it; workers rejoin in place
                 ps_restarts += 1
                 log(f"[supervisor] {failure[0]} exited with {failure[1]}; restarting it in place "

@@ -73,37 +73,49 @@ class StopAtStepHook(SessionRunHook):
 
 
 class NanTensorHook(SessionRunHook):
-    """Asynchronous NaN guard: a pinned host mirror of the device flag is
-    refreshed with a non-blocking copy every step and checked the step after."""
+    """Asynchronous NaN guard: the device flag (``stats[2]``, set by the
+    softmax-CE / finalize kernels and never cleared, so no step is missed) is copied to
+    a pinned host mirror with a non-blocking copy every ``every_n_steps`` steps and
+    checked one step later -- a NaN at step k is raised by step k + N, with one host
+    sync per N steps instead of per step.  ``end`` does a final synchronous check."""
 
-    def __init__(self, fail_on_nan_loss: bool = True, every_n_steps: int = 1):
+    def __init__(self, fail_on_nan_loss: bool = True, every_n_steps: int = 1, log=print):
         self.fail, self.every = fail_on_nan_loss, max(1, every_n_steps)
+        self.log = log
         self._host: Optional[torch.Tensor] = None
         self._n = 0
         self._pending = False
+        self.checks = 0                 # host syncs taken (tests: one per N steps)
 
     def _check(self, session) -> None:
         if self._pending:
             if session.stats_event is not None:
                 session.stats_event.synchronize()
+            self.checks += 1
+            self._pending = False
             if float(self._host[0]) != 0.0:
+                self.log(f"NaN loss detected at global step {session.global_step}")
                 if self.fail:
                     raise NanLossDuringTrainingError()
                 print("Model diverged with loss = NaN.", file=sys.stderr)
-            self._pending = False
+
+    def _record(self, s) -> None:
+        if self._host is None:
+            self._host = torch.zeros(1, dtype=torch.float32, pin_memory=s.stats.is_cuda)
+        self._host.copy_(s.stats[2:3], non_blocking=True)
+        s.record_stats_event()
+        self._pending = True
 
     def after_run(self, ctx: RunContext) -> None:
         s = ctx.session
         self._check(s)
         self._n += 1
         if self._n % self.every == 0:
-            if self._host is None:
-                self._host = torch.zeros(1, dtype=torch.float32, pin_memory=s.stats.is_cuda)
-            self._host.copy_(s.stats[2:3], non_blocking=True)
-            s.record_stats_event()
-            self._pending = True
+            self._record(s)
 
     def end(self, session) -> None:
+        self._check(session)
+        self._record(session)            # the steps since the last mirror copy
         self._check(session)
 
 

@@ -109,7 +109,14 @@ def _train(FLAGS, cl: Cluster, max_steps, test_interval, batch_size, impl, log) 
             log(f"[ps {cl.task_id}] restored shard from {prefix}")
         ps = ParameterServer(cl.task_id, cl.num_ps, cl.num_workers, param_specs(spec), init, opt, cl.device,
                              max_steps, restore=restore, log=log, transport=cl.transport, cluster=cl)
-        res = ps.serve()
+        from ..parallel.ps import EXIT_FATAL, PushIntegrityError
+        try:
+            res = ps.serve()
+        except PushIntegrityError as e:
+            # an error no restart would fix: a distinct exit code the supervisor never restarts
+            log(f"[ps {cl.task_id}] fatal: PushIntegrityError: {e}")
+            sys.stdout.flush()
+            raise SystemExit(EXIT_FATAL)
         return {"global_step": float(res["global_step"])}
 
     # Q1: the reference trains on the *test* list (inputs(eval_data=True), main.py:85)
@@ -141,7 +148,12 @@ def _train(FLAGS, cl: Cluster, max_steps, test_interval, batch_size, impl, log) 
                           eval_examples=FLAGS.eval_examples, log=log)
         monitor.register_reference_summaries()
 
-    hooks = [StopAtStepHook(last_step=max_steps), NanTensorHook(fail_on_nan_loss=True)]   # main.py:137-138
+    # main.py:137-138; the NaN flag is checked asynchronously every N steps
+    nan_every = getattr(FLAGS, "nan_check_steps", -1)
+    if nan_every is None or nan_every <= 0:
+        nan_every = FLAGS.log_step_count_steps if FLAGS.log_step_count_steps > 0 else 100
+    hooks = [StopAtStepHook(last_step=max_steps), NanTensorHook(fail_on_nan_loss=True, every_n_steps=nan_every,
+                                                                log=log)]
     fi = FaultInjectionHook(cl.rank)
     if fi.active():
         hooks.insert(0, fi)

@@ -69,6 +69,8 @@ flags.DEFINE_integer("save_checkpoint_steps", 0, "checkpoint every N steps (0: o
 flags.DEFINE_integer("save_summaries_steps", 100, "loss/accuracy scalars every N steps")
 flags.DEFINE_integer("log_step_count_steps", 100, "global_step/sec every N steps")
 flags.DEFINE_integer("max_to_keep", 5, "checkpoints to keep")
+flags.DEFINE_integer("nan_check_steps", -1, "NaN guard: read the device NaN flag every N steps, asynchronously "
+                     "(a NaN at step k raises by step k + N); -1 = --log_step_count_steps (100 when that is 0)")
 flags.DEFINE_integer("eval_examples", 10000, "examples per test-summary evaluation (0: whole split)")
 flags.DEFINE_string("ps_backend", "", "PS-mode data plane: '' (ipc on GPU, host on CPU) | ipc (xGMI peer copies) | "
                     "host / gloo (staged through host memory)")
@@ -78,10 +80,12 @@ flags.DEFINE_float("collective_timeout", 600.0, "process-group timeout (s): a hu
 
 
 def main(argv=None):
-    if FLAGS.job_name in ("ps", "worker"):
-        # PS tasks are often co-located on one GPU; one hardware queue per process keeps
-        # their queues from oversubscribing the GPU's scheduler (measured: 0.21-0.25 ms per
-        # applied update vs 0.47-0.51 at the default 4, profiles/r3/ps/).  Set before HIP starts.
+    if FLAGS.ps_hosts and FLAGS.job_name in ("ps", "worker") and "GPU_MAX_HW_QUEUES" not in os.environ:
+        # PS mode only (data-parallel workers keep HIP's default queues, so the RCCL stream
+        # does not share a queue with compute): PS tasks are often co-located on one GPU,
+        # and one hardware queue per process keeps their queues from oversubscribing the
+        # GPU's scheduler (0.21-0.25 ms per applied update vs 0.47-0.51 at the default 4,
+        # profiles/r3/ps/).  Set before HIP starts; a value the user set is kept.
         os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("MNISTX_PS_HW_QUEUES", "1")
     from distributed_tensorflow_ibm_mnist_amd.train.trainer import train
     res = train(FLAGS)

@@ -26,3 +26,12 @@ def K(dev):
     """The HIP kernel extension; must load on a GPU box (no silent fallback)."""
     from distributed_tensorflow_ibm_mnist_amd.ops._ext import kernels
     return kernels()
+
+
+@pytest.fixture
+def grid_cap(K):
+    """Cap every persistent kernel's grid (K.set_grid_cap) for one test, so a small batch
+    runs the multi-iteration paths (several tiles / images per block) that the benchmark
+    batches run; reset afterwards."""
+    yield K.set_grid_cap
+    K.set_grid_cap(0)

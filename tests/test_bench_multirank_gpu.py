@@ -44,6 +44,11 @@ def test_bench_torchrun_two_ranks_one_gpu(model, batch):
         assert b["allreduce_us"] > 0 and b["busbw_GBps"] > 0 and b["algbw_GBps"] > 0 and b["layers"]
     assert comm["eager_ms_comm_on"] > 0 and comm["eager_ms_comm_off"] > 0
     assert "comm_exposed_ms" in comm
+    # the process group as the ranks saw it: gloo, 2 ranks, both on the one visible device
+    pg = out["pg"]
+    assert pg["backend"] == "gloo" and pg["world_size"] == 2 and len(pg["ranks"]) == 2
+    assert [r["rank"] for r in pg["ranks"]] == [0, 1] and pg["shared"] == [[0, 1]]
+    assert 0 < pg["timed_s_min"] <= pg["timed_s_max"]
 
 
 def test_bench_one_rank_rccl_comm_probe():
@@ -60,3 +65,6 @@ def test_bench_one_rank_rccl_comm_probe():
     assert comm is not None and len(comm["buckets"]) >= 1
     assert all(b["allreduce_us"] > 0 and b["algbw_GBps"] > 0 for b in comm["buckets"])
     assert comm["eager_ms_comm_on"] > 0 and comm["eager_ms_comm_off"] > 0
+    pg = out["pg"]
+    assert pg["backend"] == "nccl" and pg["world_size"] == 1 and pg["shared"] == [] and pg["distinct_devices"] == 1
+    assert pg["rccl_version"] and (pg["ranks"][0]["pci"] or pg["ranks"][0]["uuid"])

@@ -435,3 +435,22 @@ def test_ps_session_recovery_in_place(tmp_path, num_ps, kill_rank):
     lc = latest_checkpoint(d)
     assert lc.endswith("model.ckpt-40")
     assert read_index(lc)[0] == num_ps
+
+
+def test_ps_supervisor_never_restarts_a_fatal_ps(tmp_path):
+    """A PS that rejects a corrupt push (MNIST_FI_CORRUPT_PUSH) exits with EXIT_FATAL;
+    the supervisor neither relaunches it in place nor restarts the job."""
+    from distributed_tensorflow_ibm_mnist_amd.parallel.supervisor import EXIT_FATAL, supervise
+    d = str(tmp_path / "train")
+    logs = str(tmp_path / "logs")
+    msgs = []
+    os.environ["MNIST_FI_CORRUPT_PUSH"] = "1:5"
+    try:
+        rc = supervise(_sup_flags(d) + ["--ps_backend=host"], num_ps=1, num_workers=2, max_restarts=2,
+                       log_dir=logs, timeout_s=300, log=msgs.append)
+    finally:
+        os.environ.pop("MNIST_FI_CORRUPT_PUSH", None)
+    assert rc == EXIT_FATAL, msgs
+    assert any("(fatal); not restarting" in m for m in msgs), msgs
+    assert not any("restarting it in place" in m or "attempt 1" in m for m in msgs), msgs
+    assert "PushIntegrityError" in open(os.path.join(logs, "attempt0_ps0.log")).read()

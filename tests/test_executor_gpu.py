@@ -16,20 +16,26 @@ def rel_err(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("model,cin", [("lenet5", 1), ("reference_cnn", 3), ("reference_cnn", 1), ("mlp", 1)])
-def test_step_matches_oracle(dev, K, model, cin):
-    torch.manual_seed(0)
+def _check_step(dev, model, cin, B, defer_head=False, seed=0):
+    """One training step of the HIP plan vs the fp32 oracle: logits, every gradient (within
+    3x the bf16 autocast noise floor), the fused update and the loss statistics.
+    ``defer_head``: the bench / train_step path (fused head runs inside loss_and_grad)."""
+    torch.manual_seed(seed)
     spec = get_model(model, cin)
     init = torch_ref.init_params(spec, seed=1)
-    B = 96
     opt = OptConfig(lr0=0.05, decay_steps=0, use_momentum=False, ema_max=0.9999)
     net = HipNet(spec, B, dev, init, opt)
     x = (torch.rand(B, 28, 28, cin, device=dev) - 0.5).to(torch.bfloat16)
     y = torch.randint(0, 10, (B,), device=dev, dtype=torch.int32)
     net.x0.copy_(x)
     net.labels.copy_(y)
-    logits = net.forward()[:, :10].clone()
-    net.loss_and_grad()
+    if defer_head:
+        net.forward(defer_head=True)
+        net.loss_and_grad()
+        logits = net.logits[:, :10].clone()
+    else:
+        logits = net.forward()[:, :10].clone()
+        net.loss_and_grad()
     net.backward()
     # oracle on the same bf16-rounded weights
     p = {k: v.to(dev).to(torch.bfloat16).float().requires_grad_(True) for k, v in init.items()}
@@ -47,7 +53,7 @@ def test_step_matches_oracle(dev, K, model, cin):
     for name in init:
         e = rel_err(net.fp.grad_view(name), p[name].grad)
         floor = rel_err(p16[name].grad, p[name].grad)
-        assert e < max(3e-2, 3.0 * floor), f"{model} {name}: rel err {e:.3e} (bf16 floor {floor:.3e})"
+        assert e < max(3e-2, 3.0 * floor), f"{model} B={B} {name}: rel err {e:.3e} (bf16 floor {floor:.3e})"
     # fused update = w - lr * (g + wd w)
     before = {n: net.fp.param_view(n).clone() for n in init}
     grads = {n: net.fp.grad_view(n).clone() for n in init}
@@ -60,6 +66,28 @@ def test_step_matches_oracle(dev, K, model, cin):
     assert int(net.fp.step.item()) == 1
     st = net.read_stats()
     assert abs(st["cross_entropy"] - ce.item()) < 2e-2 * max(1.0, ce.item())
+
+
+@pytest.mark.parametrize("model,cin", [("lenet5", 1), ("reference_cnn", 3), ("reference_cnn", 1), ("mlp", 1)])
+def test_step_matches_oracle(dev, K, model, cin):
+    _check_step(dev, model, cin, 96)
+
+
+@pytest.mark.parametrize("model,cin,B,cap", [("lenet5", 1, 600, 4), ("reference_cnn", 1, 120, 8),
+                                             ("reference_cnn", 3, 64, 5)])
+def test_step_matches_oracle_multi_iteration(dev, K, grid_cap, model, cin, B, cap):
+    """The same check with every persistent kernel's grid capped, so each block loops over
+    several tiles / images (ring reuse and next-tile prefetch: the paths the benchmark
+    batches take), on the train_step path (deferred fused head)."""
+    grid_cap(cap)
+    _check_step(dev, model, cin, B, defer_head=True, seed=1)
+
+
+@pytest.mark.parametrize("model,B", [("lenet5", 65536), ("reference_cnn", 16384)])
+def test_step_matches_oracle_bench_batch(dev, K, model, B):
+    """The benchmarked configs themselves (BASELINE stress batch for LeNet-5, the reference
+    CNN's bench batch), on the bench's train_step path, against the fp32 oracle."""
+    _check_step(dev, model, 1, B, defer_head=True, seed=2)
 
 
 @pytest.mark.parametrize("model", ["lenet5", "reference_cnn"])

@@ -166,11 +166,13 @@ def test_f32_training_cli(dev, K, tmp_path):
     assert json.load(open(out / "val.json"))
 
 
-@pytest.mark.parametrize("Nb,Co", [(1, 64), (37, 64), (700, 32)])
-def test_f32_halo_conv2(dev, K, Nb, Co):
+@pytest.mark.parametrize("Nb,Co,cap", [(1, 64, 0), (37, 64, 0), (700, 32, 0), (37, 64, 3), (50, 32, 4)])
+def test_f32_halo_conv2(dev, K, grid_cap, Nb, Co, cap):
     """conv_halo_f32.hip (reference conv2 geometry: 14x14, 5x5 SAME, 32 -> Co channels;
     dgrad of 64 dY channels with the input-ReLU mask) against PyTorch fp32, over
-    persistent grids with several images per workgroup."""
+    persistent grids with several images per workgroup (cap > 0: `cap` blocks, >= 12
+    images each)."""
+    grid_cap(cap)
     torch.manual_seed(Nb)
     x = torch.randn(Nb, 14, 14, 32, device=dev)
     w = torch.randn(5, 5, 32, Co, device=dev) * 0.05
@@ -190,10 +192,12 @@ def test_f32_halo_conv2(dev, K, Nb, Co):
     assert rel_err(dx, ref_dx) < 1e-5
 
 
-@pytest.mark.parametrize("Nb,S", [(1, 1), (300, 7), (1500, 256)])
-def test_f32_conv1_kernels(dev, K, Nb, S):
+@pytest.mark.parametrize("Nb,S,cap", [(1, 1, 0), (300, 7, 0), (1500, 256, 0), (300, 7, 5)])
+def test_f32_conv1_kernels(dev, K, grid_cap, Nb, S, cap):
     """conv1_f32.hip (28x28x1 -> 32, 5x5 SAME): forward with bias + ReLU, and the weight
-    gradient's per-workgroup partials (S workgroups, several images each) against PyTorch."""
+    gradient's per-workgroup partials (S workgroups, several images each) against PyTorch.
+    cap > 0: the forward's persistent grid capped too (60 images per block)."""
+    grid_cap(cap)
     torch.manual_seed(Nb)
     x = torch.randn(Nb, 28, 28, 1, device=dev)
     w = torch.randn(5, 5, 1, 32, device=dev) * 0.2

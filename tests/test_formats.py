@@ -185,7 +185,8 @@ def test_meta_graph_def_structure(tmp_path):
     from distributed_tensorflow_ibm_mnist_amd.utils.proto import to_dict
     t = {"conv1/weights": np.zeros((5, 5, 1, 32), np.float32), "conv1/biases": np.ones(32, np.float32),
          "conv1/weights/ExponentialMovingAverage": np.zeros((5, 5, 1, 32), np.float32),
-         "global_step": np.array(7, np.int64), "total_loss/avg": np.array(0.5, np.float32)}
+         "global_step": np.array(7, np.int64), "total_loss/avg": np.array(0.5, np.float32),
+         "loader/epoch": np.array([3, 1], np.int32)}
     prefix = Saver().save(str(tmp_path), 7, t, meta={"model": "reference_cnn", "in_channels": 1})
     raw = open(prefix + ".meta", "rb").read()
     top = to_dict(raw)
@@ -201,6 +202,10 @@ def test_meta_graph_def_structure(tmp_path):
     gs = {to_dict(a)[1][0].decode(): to_dict(to_dict(a)[2][0]) for a in by_name["global_step"][5]}
     assert gs["dtype"][6][0] == mg.DT_INT64 and 2 not in to_dict(gs["shape"][7][0])   # scalar
     assert [i.decode() for i in by_name["conv1/biases/Assign"][3]] == ["conv1/biases", "conv1/biases/Initializer/zeros"]
+    # DT_INT32 initializer: TensorProto.int_val is field 7 (6 would be double_val)
+    ia = {to_dict(a)[1][0].decode(): to_dict(to_dict(a)[2][0]) for a in by_name["loader/epoch/Initializer/zeros"][5]}
+    tp = to_dict(ia["value"][8][0])
+    assert tp[1][0] == mg.DT_INT32 and 7 in tp and 6 not in tp
     colls = {to_dict(c)[1][0].decode(): to_dict(c)[2][0] for c in top[4]}
     assert set(colls) == {"variables", "trainable_variables", "global_step"}
 

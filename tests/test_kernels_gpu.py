@@ -144,12 +144,18 @@ def test_conv_fwd(dev, K, N, H, W, Ci, Co, k, pad):
     close(y, conv_ref(x, w, b, pad, True))
 
 
+@pytest.mark.parametrize("cap", [0, 2])
 @pytest.mark.parametrize("fv,dv", [(1, 1), (2, 2), (3, 3), (4, 4), (5, 5)])
-def test_conv_halo_variants(dev, K, fv, dv):
+def test_conv_halo_variants(dev, K, grid_cap, fv, dv, cap):
     """Every conv_halo.hip launch variant (reference conv2 geometry; odd batch leaves a
-    partial image group) against the fp32 oracle: forward + bias + ReLU, masked dgrad."""
+    partial image group) against the fp32 oracle: forward + bias + ReLU, masked dgrad.
+    cap > 0: 2 persistent blocks over 11 images, so every block loops with the next
+    image prefetched (the path of the benchmark batch)."""
     torch.manual_seed(7)
     N, H, W, Ci, Co, k, pad = 5, 14, 14, 32, 64, 5, "SAME"
+    if cap:
+        grid_cap(cap)
+        N = 11
     x = rnd(N, H, W, Ci, dev=dev).float().requires_grad_(True)
     w = rnd(k, k, Ci, Co, dev=dev, scale=1 / math.sqrt(k * k * Ci))
     b = torch.randn(Co, device=dev)
@@ -326,8 +332,15 @@ CP_CASES = [
 ]
 
 
+@pytest.mark.parametrize("cap", [0, 2])
 @pytest.mark.parametrize("N,H,W,Ci,ci,Co,co,pad", CP_CASES)
-def test_convpool(dev, K, N, H, W, Ci, ci, Co, co, pad):
+def test_convpool(dev, K, grid_cap, N, H, W, Ci, ci, Co, co, pad, cap):
+    """cap > 0: 3x the batch on a grid of `cap` persistent blocks (forward, dgrad and the
+    weight gradient), so each block loops over several image groups with the next group
+    prefetched -- the paths the benchmark batches run."""
+    if cap:
+        grid_cap(cap)
+        N *= 3
     torch.manual_seed(11)
     padding = "SAME" if pad else "VALID"
     x = rnd(N, H, W, Ci, dev=dev)
@@ -357,7 +370,7 @@ def test_convpool(dev, K, N, H, W, Ci, ci, Co, co, pad):
     dP = rnd(N, PH, PW, Co, dev=dev)
     yp.backward(dP.float())
     KM = K.convpool_rows(Ci, Co, 5, pad, H, W)
-    grid = 37
+    grid = cap or 37
     slab = torch.empty(grid * KM * Co, dtype=torch.float32, device=dev)
     K.convpool_wgrad(x, dP, arg, slab, grid, N, Ci, Co, 5, pad, H, W)
     dw = torch.empty(5, 5, ci, co, device=dev)

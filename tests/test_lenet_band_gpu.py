@@ -49,8 +49,12 @@ def _band(K, x, w1, b1, w2, b2, B, idx=None, p1=True):
     return P1, A1, P2, A2
 
 
-@pytest.mark.parametrize("B", [1, 3, 16, 17, 100, 1000])
-def test_band_fwd_matches_oracle_and_convpool(dev, K, B):
+@pytest.mark.parametrize("B,cap", [(1, 0), (3, 0), (16, 0), (17, 0), (100, 0), (1000, 0), (200, 4), (333, 3)])
+def test_band_fwd_matches_oracle_and_convpool(dev, K, grid_cap, B, cap):
+    """cap > 0: the grid is capped so every block runs several 8-image tiles (B=200, 4
+    blocks: nk = 7; B=333, 3 blocks: a partial last tile) -- the double-buffered input /
+    pool1 rings are reused, as at the benchmark batch (> 4096 images)."""
+    grid_cap(cap)
     torch.manual_seed(B)
     w1, b1, w2, b2 = _weights(dev)
     x = (torch.rand(B, 28, 28, 1, device=dev) - 0.5).to(torch.bfloat16)

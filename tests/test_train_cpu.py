@@ -72,11 +72,19 @@ def test_monitor_summaries_reference_cnn(tmp_path):
         assert t in tags, t
 
 
-def test_nan_guard_fault_injection(tmp_path):
+@pytest.mark.parametrize("every", [4, -1])
+def test_nan_guard_fault_injection(tmp_path, every):
+    """The NaN guard reads the device flag every N steps, asynchronously: a NaN at
+    step k is raised by step k + N (every=-1: N = 100 > max_steps, caught by the end
+    hook's final check)."""
     r = run_main(["--model=mlp", "--in_channels=1", "--batch_size=16", "--max_steps=50", "--test_interval=100",
-                  f"--train_dir={tmp_path}"], env={"MNIST_FI_NAN_AT_STEP": "5"})
+                  f"--train_dir={tmp_path}", f"--nan_check_steps={every}"], env={"MNIST_FI_NAN_AT_STEP": "5"})
     assert r.returncode != 0
     assert "NaN loss during training" in (r.stderr + r.stdout)
+    import re
+    m = re.search(r"NaN loss detected at global step (\d+)", r.stdout)
+    assert m, r.stdout[-2000:]
+    assert 5 <= int(m.group(1)) <= (5 + every if every > 0 else 50)
     # the final-checkpoint end hook must not run after a NaN
     from distributed_tensorflow_ibm_mnist_amd.ckpt.saver import latest_checkpoint
     lc = latest_checkpoint(str(tmp_path))

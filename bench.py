@@ -78,6 +78,9 @@ def parse():
     ap.add_argument("--comm_probe", type=int, default=1,
                     help="N>1 (or --force_collectives 1): after the timed steps, time each gradient bucket's "
                          "all-reduce alone (us, bus GB/s) and the exposed communication of an eager step")
+    ap.add_argument("--lenet_bwd", default="fused", choices=["fused", "split"],
+                    help="LeNet-5 conv-stack backward: fused = one kernel (lenet_bwd.hip); split = the three "
+                         "per-layer convpool kernels (conv2 dgrad, conv2 / conv1 weight gradients)")
     ap.add_argument("--phases", type=int, default=3,
                     help="extra eager steps AFTER the timed region, timed per phase with HIP events (0 = off)")
     return ap.parse_args()
@@ -291,7 +294,8 @@ def main() -> int:
     elif args.impl == "hip":
         from distributed_tensorflow_ibm_mnist_amd.runtime.executor import HipNet
         net = HipNet(spec, args.batch, dev, init, opt,
-                     overlap_backward={"none": False, "dense": "dense", "all": True}[args.overlap])
+                     overlap_backward={"none": False, "dense": "dense", "all": True}[args.overlap],
+                     fused_lenet_bwd=args.lenet_bwd == "fused")
     else:
         from distributed_tensorflow_ibm_mnist_amd.runtime.torchnet import TorchNet
         net = TorchNet(spec, args.batch, dev, init, opt)
@@ -436,6 +440,7 @@ def main() -> int:
                 "hip_graph": use_graph,
                 "optimizer": args.optimizer,
                 "input": mode if fused_in else "prep",
+                "lenet_bwd": ("fused" if getattr(net, "fused_bwd", False) else "split") if args.model == "lenet5" else None,
             },
             "tflops_per_s": round(tot * value / 1e12, 2),
             "final_train_loss": round(stats["cross_entropy"], 5),

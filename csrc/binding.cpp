@@ -790,6 +790,50 @@ void lenet_band_fwd(Tensor x, Tensor w1, Tensor b1, int64_t b1n, Tensor w2, Tens
          "lenet_band_fwd");
 }
 
+// LeNet-5 conv-stack backward as one kernel (lenet_bwd.hip): conv2 dgrad + both weight
+// gradients; x as for lenet_band_fwd (the forward's input), p1 / arg1 / arg2 from it, dp2 =
+// dL/d pool2 [B, 400].  slab1 [grid, 32, 8], slab2 [grid, 208, 16] (split-K partials).
+void lenet_bwd(Tensor x, Tensor p1, Tensor arg1, Tensor dp2, Tensor arg2, Tensor w2, int64_t B, Tensor slab1,
+               Tensor slab2, int64_t grid, optional<Tensor> idx) {
+  mnistx::XSrc src{nullptr, nullptr, nullptr, 0};
+  if (x.scalar_type() == at::kByte) {
+    check(x, at::kByte, 784, "x");
+    TORCH_CHECK(x.numel() % 784 == 0 && x.numel() < (int64_t)INT32_MAX, "x: [n, 784] uint8 images, < 2 GB");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 4 == 0, "x must be 4-byte aligned");
+    src.u8 = P<const uint8_t>(x);
+  } else {
+    check(x, at::kBFloat16, 784, "x");
+    TORCH_CHECK(x.numel() % 784 == 0 && x.numel() * 2 < (int64_t)INT32_MAX, "x: [n, 784] bf16 images, < 2 GB");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 8 == 0, "x must be 8-byte aligned");
+    src.x = BF(x);
+  }
+  src.n = (int)(x.numel() / 784);
+  if (idx.has_value() && idx->defined()) {
+    check(*idx, at::kLong, B, "idx");
+    src.idx = P<const int64_t>(*idx);
+  } else {
+    TORCH_CHECK(src.n >= B, "x: needs B images without idx");
+  }
+  TORCH_CHECK(B >= 1 && B * 196 * 16 < (int64_t)INT32_MAX, "B");
+  check(p1, at::kBFloat16, B * 196 * 8, "p1");
+  check(arg1, at::kByte, B * 196 * 4, "arg1");
+  check(dp2, at::kBFloat16, B * 400, "dp2");
+  check(arg2, at::kByte, B * 400, "arg2");
+  check(w2, at::kBFloat16, 5 * 5 * 8 * 16, "w2");
+  for (const Tensor* t : {&p1, &dp2, &w2})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "p1 / dp2 / w2 must be 16-byte aligned");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(arg1.data_ptr()) % 4 == 0 && reinterpret_cast<uintptr_t>(arg2.data_ptr()) % 8 == 0,
+              "arg1 / arg2 alignment");
+  const int res = mnistx::lenet_bwd_blocks((int)B);
+  TORCH_CHECK(res > 0, "lenet_bwd: occupancy query failed");
+  TORCH_CHECK(grid >= 1 && grid <= res, "lenet_bwd: grid must be in [1, ", res, "] (one block per CU, <= tiles)");
+  check(slab1, at::kFloat, grid * 32 * 8, "slab1");
+  check(slab2, at::kFloat, grid * 208 * 16, "slab2");
+  hip_ok(mnistx::lenet_bwd(src, BF(p1), P<const uint8_t>(arg1), BF(dp2), P<const uint8_t>(arg2), BF(w2), (int)B,
+                           P<float>(slab1), P<float>(slab2), (int)grid, cur_stream()),
+         "lenet_bwd");
+}
+
 // ---------------------------------------------------------------- fp32 (reference precision) path
 const float* Fo(const optional<Tensor>& t, int64_t need, const char* name) {
   if (!t.has_value() || !t->defined()) return nullptr;
@@ -1090,5 +1134,12 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("lenet_band_fwd", &lenet_band_fwd, py::arg("x"), py::arg("w1"), py::arg("b1"), py::arg("b1n"),
         py::arg("w2"), py::arg("b2"), py::arg("B"), py::arg("p2"), py::arg("arg2"), py::arg("p1") = py::none(),
         py::arg("arg1") = py::none(), py::arg("idx") = py::none(), py::arg("prof") = py::none());
+  m.def("lenet_bwd", &lenet_bwd, py::arg("x"), py::arg("p1"), py::arg("arg1"), py::arg("dp2"), py::arg("arg2"),
+        py::arg("w2"), py::arg("B"), py::arg("slab1"), py::arg("slab2"), py::arg("grid"), py::arg("idx") = py::none());
+  m.def("lenet_bwd_blocks", [](int64_t B) {
+    const int n = mnistx::lenet_bwd_blocks((int)B);
+    TORCH_CHECK(n > 0, "lenet_bwd_blocks: occupancy query failed");
+    return (int64_t)n;
+  });
   m.attr("ARCH") = "gfx950";
 }

@@ -119,6 +119,13 @@ int lenet_c2dgrad_c1wgrad_grid();
 hipError_t lenet_c2dgrad_c1wgrad(const XSrc& x, const bf16_t* dP2, const uint8_t* arg2, const bf16_t* w2,
                                  const uint8_t* arg1, int B, float* slab, int grid, hipStream_t st);
 
+// ---- lenet_bwd.hip: LeNet-5 conv-stack backward (conv2 dgrad + both weight gradients) as ONE
+// persistent kernel; slab1 [grid][32][8] (rows tap 0..24, bias 25), slab2 [grid][208][16]
+// (rows tap * 8 + ci, bias 200) -- the split-K partials splitk_reduce combines
+int lenet_bwd_blocks(int B);         // the grid for a batch (one block per CU, <= tiles); <= 0: error
+hipError_t lenet_bwd(const XSrc& x, const bf16_t* p1, const uint8_t* arg1, const bf16_t* dp2, const uint8_t* arg2,
+                     const bf16_t* w2, int B, float* slab1, float* slab2, int grid, hipStream_t st);
+
 // ---- lenet_band.hip: LeNet-5 conv1+pool1+conv2+pool2 forward on banded MFMA tiles
 // (one persistent kernel; bf16 images only).  x.x = [n][784] images (x.idx: per-sample
 // rows, else sample b = row b).  p1/arg1 (convpool cfg-0 layouts) are written only when

@@ -372,7 +372,7 @@ class HipNet:
 
     def __init__(self, spec: ModelSpec, batch: int, device, init: Dict[str, torch.Tensor],
                  opt: Optional[OptConfig] = None, fuse_convpool: bool = True, overlap_backward: bool = False,
-                 fuse_head: bool = True, fuse_lrnpool: Optional[bool] = None):
+                 fuse_head: bool = True, fuse_lrnpool: Optional[bool] = None, fused_lenet_bwd: bool = True):
         dev = torch.device(device)
         if fuse_lrnpool is None:
             fuse_lrnpool = os.environ.get("MNISTX_FUSE_LRNPOOL", "1") != "0"
@@ -547,6 +547,14 @@ class HipNet:
         # on x0 or the resident dataset (bf16, or uint8 normalised while staging);
         # MNISTX_BAND_FWD=0 runs the two convpool kernels instead
         self.band_fwd = self._find_c2d_c1w() and os.environ.get("MNISTX_BAND_FWD", "1") != "0"
+        # LeNet-5: the conv stack's whole backward (conv2 dgrad + both weight gradients) as ONE
+        # kernel (lenet_bwd.hip): dP1 stays in LDS, the weight gradients accumulate in
+        # registers per block; fused_lenet_bwd=False runs the three convpool kernels
+        self.fused_bwd = self.band_fwd and fused_lenet_bwd and not self.overlap and not self.fuse_c2d_c1w
+        if self.fused_bwd:
+            res = kernels().lenet_bwd_blocks(batch)
+            self.lb_slab1 = torch.zeros(res * 32 * 8, dtype=torch.float32, device=dev)
+            self.lb_slab2 = torch.zeros(res * 208 * 16, dtype=torch.float32, device=dev)
         if self.fuse_c2d_c1w:
             l0, l1 = self.layers[0], self.layers[1]
             l0.fused_grid = min(l0.grid, kernels().lenet_c2dgrad_c1wgrad_grid())
@@ -655,6 +663,22 @@ class HipNet:
                                  fp.bf16_view(l1.wname), fp.param_view(l1.bname), nb, l1.out, l1.arg,
                                  p1=l0.out, arg1=l0.arg, idx=src.get("idx"))
 
+    def _fused_conv_backward(self, nb: int, dp2: torch.Tensor, pending: list) -> None:
+        """LeNet-5 conv1+conv2 backward in one launch (lenet_bwd.hip) reading the band
+        forward's pool1 / argmax outputs and dL/d pool2; both layers' weight / bias gradients
+        go to split-K slabs reduced with the other queued layers (``pending``)."""
+        l0, l1 = self.layers[0], self.layers[1]
+        fp = self.fp
+        src = l0._src()
+        K = kernels()
+        grid = K.lenet_bwd_blocks(nb)
+        K.lenet_bwd(src.get("u8", l0._xin()), l0.out, l0.arg, dp2, l1.arg, fp.bf16_view(l1.wname), nb,
+                    self.lb_slab1, self.lb_slab2, grid, idx=src.get("idx"))
+        _reduce(pending, self.lb_slab2, (grid, 208, 16, 25, 8, l1.spec.cin, l1.spec.cout, 200),
+                fp.grad_view(l1.wname), fp.grad_view(l1.bname))
+        _reduce(pending, self.lb_slab1, (grid, 32, 8, 25, 1, 1, l0.spec.cout, 25),
+                fp.grad_view(l0.wname), fp.grad_view(l0.bname))
+
     def loss_and_grad(self, nb: Optional[int] = None, scale: Optional[float] = None) -> None:
         nb = self.B if nb is None else nb
         if self._head_pending is not None:
@@ -692,6 +716,14 @@ class HipNet:
         for i in range(len(self.layers) - 1, -1, -1):
             lay = self.layers[i]
             dx = self.dbuf[i]
+            if i == 1 and self.fused_bwd:
+                self._fused_conv_backward(nb, dy, pending)
+                for li in (self.layers[1].idx, self.layers[0].idx):
+                    if self.grad_ready_hooks and (self.hook_layers is None or li in self.hook_layers):
+                        self._flush_reduce(pending)
+                        for h in self.grad_ready_hooks:
+                            h(li)
+                break
             if lay.has_params:
                 # the first layer has no data gradient: its weight gradient IS the tail of
                 # the critical path, so it runs on the main stream while the side drains

@@ -18,13 +18,15 @@ OUT=gpurun_out/$1; shift
 mkdir -p $OUT
 for step in "$@"; do
   kind=${step%%:*}; name=${step#*:}; [ "$name" = "$step" ] && name=$kind
-  var="ARGS_${name}"; args=${!var}
+  tag=$(printf '%s' "$name" | tr -c 'A-Za-z0-9_' '_')
+  args=""
+  if [[ "$name" =~ ^[A-Za-z_][A-Za-z0-9_]*$ ]]; then var="ARGS_${name}"; args=${!var}; fi
   case $kind in
     tests)
       sel=(); [ "$name" != "tests" ] && sel=(-k "$name")
       timeout -k 10 1100 python -u -m pytest tests -x -v -m gpu "${sel[@]}" --durations=12 --timeout 240 \
-        --timeout-method thread > $OUT/tests_$name.log 2>&1; rc=$?
-      tail -4 $OUT/tests_$name.log; echo "tests rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+        --timeout-method thread > "$OUT/tests_$tag.log" 2>&1; rc=$?
+      tail -n 4 "$OUT/tests_$tag.log"; echo "tests rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     smoke)
       timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 \
         || { cat $OUT/smoke.txt; exit 1; }

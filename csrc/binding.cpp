@@ -1010,23 +1010,6 @@ void f32_prep_images(Tensor src, Tensor idx, Tensor lab_src, Tensor out, Tensor 
          "f32_prep_images");
 }
 
-// LeNet-5 conv2 dgrad -> conv1 wgrad (one kernel): x / u8 source of conv1, the pooled
-// gradient + argmax of conv2, conv2's bf16 weights, conv1's argmax bytes
-void lenet_c2dgrad_c1wgrad(Tensor x, Tensor dP2, Tensor arg2, Tensor w2, Tensor arg1, Tensor slab, int64_t grid,
-                           int64_t B, optional<Tensor> u8, optional<Tensor> idx) {
-  const int cfg1 = mnistx::convpool_config(1, 8, 5, 2, 28, 28);
-  const auto src = cp_src(x, u8, idx, cfg1, B, 28 * 28);
-  TORCH_CHECK(grid >= 1 && grid <= mnistx::lenet_c2dgrad_c1wgrad_grid(), "grid exceeds the resident grid");
-  check(dP2, at::kBFloat16, B * 5 * 5 * 16, "dP2");
-  check(arg2, at::kByte, B * 5 * 5 * 16, "arg2");
-  check(w2, at::kBFloat16, 5 * 5 * 8 * 16, "w2");
-  check(arg1, at::kByte, B * 14 * 14 * 4, "arg1");   // packed 4-bit codes
-  check(slab, at::kFloat, grid * mnistx::convpool_wgrad_rows(cfg1) * 8, "slab");
-  hip_ok(mnistx::lenet_c2dgrad_c1wgrad(src, BF(dP2), P<const uint8_t>(arg2), BF(w2), P<const uint8_t>(arg1), (int)B,
-                                       P<float>(slab), (int)grid, cur_stream()),
-         "lenet_c2dgrad_c1wgrad");
-}
-
 }  // namespace
 
 PYBIND11_MODULE(_kernels, m) {
@@ -1049,14 +1032,6 @@ PYBIND11_MODULE(_kernels, m) {
   // the multi-iteration (several tiles per block) paths the benchmark batches run
   m.def("set_grid_cap", [](int64_t n) { mnistx::set_grid_cap((int)n); });
   m.def("grid_cap", []() { return (int64_t)mnistx::grid_cap(); });
-  m.def("lenet_c2dgrad_c1wgrad",&lenet_c2dgrad_c1wgrad, py::arg("x"), py::arg("dP2"), py::arg("arg2"), py::arg("w2"),
-        py::arg("arg1"), py::arg("slab"), py::arg("grid"), py::arg("B"), py::arg("u8") = py::none(),
-        py::arg("idx") = py::none());
-  m.def("lenet_c2dgrad_c1wgrad_grid", []() {
-    const int n = mnistx::lenet_c2dgrad_c1wgrad_grid();
-    TORCH_CHECK(n > 0, "occupancy query failed");
-    return (int64_t)n;
-  });
   m.doc() = "MI355X (gfx950) HIP kernels for the MNIST trainer";
   m.def("dense_fwd", &dense_fwd);
   m.def("dense_dgrad", &dense_dgrad);

@@ -410,14 +410,12 @@ bool conv5_halo_dgrad_ok(int OH, int OW, int Cout, int H, int W, int KH, int KW,
          Cin % 32 == 0;
 }
 
-// Variant (MNISTX_HALO_FWD / MNISTX_HALO_DGRAD = index; sweep: bench/gpu_halo_sweep.sh);
-// set_halo_variants() overrides both (tests run every variant in one process).
+// Launch variant (index; measured in profiles/r2/halo): the defaults below, or
+// set_halo_variants() (the tests run every variant in one process).
 static int g_halo_override[2] = {-1, -1};
 static int halo_variant(const char* name, int dflt) {
   const int which = name[12] == 'F' ? 0 : 1;   // "MNISTX_HALO_FWD" / "MNISTX_HALO_DGRAD"
-  if (g_halo_override[which] >= 0) return g_halo_override[which];
-  const char* e = getenv(name);
-  return (e && e[0] >= '0' && e[0] <= '9') ? e[0] - '0' : dflt;
+  return g_halo_override[which] >= 0 ? g_halo_override[which] : dflt;
 }
 
 // Launch shapes (profiles/r2/halo: per-kernel us at B = 16384).  More resident waves

@@ -1573,8 +1573,6 @@ int resident_grid() {
   static int n = 0;
   if (n == 0) {
     int per_cu = 0, dev = 0, cus = 0;
-    const char* env = getenv("MNISTX_RESIDENT_GRID");   // "0": legacy 2048-block grids (A/B runs)
-    if (env && env[0] == '0') return n = 2048;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, KER, NTH, 0) == hipSuccess &&
         hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && per_cu > 0)
@@ -1589,26 +1587,10 @@ template <class G, int IMGS>
 hipError_t run_fwd(const XSrc& x, const bf16_t* w, const float* bias, int bias_n, int B, bf16_t* pooled, uint8_t* arg,
                    hipStream_t st) {
   if constexpr (G::PAIR && G::H == 28 && G::W == 28 && G::PAD == 2) {
-    // two resident rounds (2048) measured 5 % faster than one for this kernel (same-box A/B).
-    // A/B knob MNISTX_QUAD_IMGS=3: 3 images per group (LDS 29.1 -> 21.8 KB, 5 -> 7 WGs/CU)
-    // ("5": the same with two resident rounds of the 3-image kernel instead of 2048 blocks)
-    static const int qi = [] { const char* e = getenv("MNISTX_QUAD_IMGS"); return e ? e[0] - '0' : 4; }();
-    if (qi == 3 || qi == 5)
-      hipLaunchKernelGGL((convpool_fwd_quad_k<3>),
-                         dim3(grid_for(B, 3, qi == 3 ? 2048 : 2 * resident_grid<convpool_fwd_quad_k<3>>())), dim3(NTH),
-                         0, st, x, w, bias, bias_n, B, pooled, arg);
-    else {
-      // grid A/B: MNISTX_QUAD_GRID = explicit block count, "r" = one resident wave, "2r" = two
-      static const int gq = [] {
-        const char* e = getenv("MNISTX_QUAD_GRID");
-        if (!e) return 2048;
-        if (e[0] == 'r') return resident_grid<convpool_fwd_quad_k<4>>();
-        if (e[0] == '2' && e[1] == 'r') return 2 * resident_grid<convpool_fwd_quad_k<4>>();
-        return atoi(e);
-      }();
-      hipLaunchKernelGGL((convpool_fwd_quad_k<4>), dim3(grid_for(B, 4, gq)), dim3(NTH), 0, st, x, w, bias, bias_n,
-                         B, pooled, arg);
-    }
+    // two resident rounds (2048 blocks) measured 5 % faster than one for this kernel (same-box
+    // A/B); 3 images per group (LDS 29.1 -> 21.8 KB, 5 -> 7 WGs/CU) measured no faster
+    hipLaunchKernelGGL((convpool_fwd_quad_k<4>), dim3(grid_for(B, 4, 2048)), dim3(NTH), 0, st, x, w, bias, bias_n, B,
+                       pooled, arg);
   } else if constexpr (G::PAIR) {
     hipLaunchKernelGGL((convpool_fwd_pair_k<G, IMGS>), dim3(grid_for(B, IMGS, 2048)), dim3(NTH), 0, st, x, w, bias,
                        bias_n, B, pooled, arg);
@@ -1623,12 +1605,11 @@ hipError_t run_fwd(const XSrc& x, const bf16_t* w, const float* bias, int bias_n
 template <class G, int IMGS>
 hipError_t run_wgrad(const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B, float* slab, int grid,
                      hipStream_t st, const LrnFold& lrn = LrnFold{nullptr, 0.f, 0.f, 0.f}) {
-  // s_setprio 1 around the MFMA phase (see convpool_dgrad_pair_k); MNISTX_WGRAD_PRIO=0 turns it off
-  static const bool prio = [] { const char* e = getenv("MNISTX_WGRAD_PRIO"); return !(e && e[0] == '0'); }();
+  // s_setprio 1 around the MFMA phase (see convpool_dgrad_pair_k; backward phase 348 ->
+  // 338-339 us, profiles/r3/lenet/bwd_prio_ab.txt)
   if constexpr (G::PAIR) {
     if (lrn.p) return hipErrorInvalidValue;
-    if (prio) hipLaunchKernelGGL((convpool_wgrad_pair_k<G, IMGS, true>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab);
-    else hipLaunchKernelGGL((convpool_wgrad_pair_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab);
+    hipLaunchKernelGGL((convpool_wgrad_pair_k<G, IMGS, true>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab);
   } else if constexpr (G::COUT == 32) {
     if (lrn.p && lrn.beta == 0.75f)   // the reference's beta: pow_beta<true> (lrn_math.h)
       hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS, 2>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
@@ -1638,8 +1619,7 @@ hipError_t run_wgrad(const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B,
       hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
   } else {
     if (lrn.p) return hipErrorInvalidValue;
-    if (prio) hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS, 0, true>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
-    else hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
+    hipLaunchKernelGGL((convpool_wgrad_k<G, IMGS, 0, true>), dim3(grid), dim3(NTH), 0, st, x, dP, arg, B, slab, lrn);
   }
   return hipGetLastError();
 }
@@ -1648,310 +1628,28 @@ template <class G, int IMGS>
 hipError_t run_dgrad(const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int B, bf16_t* dx, int grid_cap,
                      hipStream_t st) {
   // grid_cap > 0: fewer persistent blocks than one resident wave, leaving CU slots
-  // for a kernel running concurrently on another stream (overlapped backward)
-  // Default (MNISTX_DGRAD_VAR=4): two images per group, A-row reuse with one row read
-  // ahead (158 VGPRs, 3 waves/SIMD): 120 us at B = 65536.  2: one image, the 15 A
-  // fragments of a fragment in batches of 8 (122 VGPRs, 4 waves): 134 us.  0: two
-  // images, all 15 in flight (150 VGPRs, 3 waves): 143-149 us.  Row reuse at one image
-  // per group (4 waves) or two rows ahead spills (192 / 157 us).
-  static const int var = [] { const char* e = getenv("MNISTX_DGRAD_VAR"); return e ? atoi(e) : 4; }();
-  int cap;
-#define MNISTX_DG(IM, ...)                                                                                   \
-  cap = resident_grid<convpool_dgrad_pair_k<G, __VA_ARGS__>>();                                            \
-  if (grid_cap > 0 && grid_cap < cap) cap = grid_cap;                                                      \
-  cap = cap_grid(cap);                                                                                     \
-  hipLaunchKernelGGL((convpool_dgrad_pair_k<G, __VA_ARGS__>), dim3(grid_for(B, IM, cap)), dim3(NTH), 0, st, \
-                     dP, arg, w, B, dx);
-  // MFMA-phase priority on by default (backward phase 348 -> 338-339 us with the wgrad
-  // kernels' own, profiles/r3/lenet/bwd_prio_ab.txt); MNISTX_DGRAD_PRIO=0 turns it off
-  static const bool prio = [] { const char* e = getenv("MNISTX_DGRAD_PRIO"); return !(e && e[0] == '0'); }();
-  if (var == 0) { MNISTX_DG(IMGS, IMGS) }
-  else if (var == 2) { MNISTX_DG(1, 1, 8, 4) }
-  else if (prio) { MNISTX_DG(2, 2, 0, 3, 1, true) }
-  else { MNISTX_DG(2, 2, 0, 3, 1) }
-#undef MNISTX_DG
+  // for a kernel running concurrently on another stream (overlapped backward).
+  // Two images per group, A-row reuse with one row read ahead (158 VGPRs, 3 waves/SIMD):
+  // 120 us at B = 65536; one image with the 15 A fragments in batches of 8 (122 VGPRs,
+  // 4 waves) measured 134 us, two images with all 15 in flight 143-149 us.  MFMA-phase
+  // priority on (backward phase 348 -> 338-339 us, profiles/r3/lenet/bwd_prio_ab.txt).
+  int cap = resident_grid<convpool_dgrad_pair_k<G, 2, 0, 3, 1, true>>();
+  if (grid_cap > 0 && grid_cap < cap) cap = grid_cap;
+  cap = cap_grid(cap);
+  hipLaunchKernelGGL((convpool_dgrad_pair_k<G, 2, 0, 3, 1, true>), dim3(grid_for(B, 2, cap)), dim3(NTH), 0, st, dP, arg,
+                     w, B, dx);
   return hipGetLastError();
 }
 
 using LeNetC1 = Geo<1, 8, 5, 2, 28, 28>;
-constexpr int WG_IMGS_C1 = 1;   // conv1 wgrad: one image per group (LDS 25.7 KB -> 6 workgroups / CU)
-// A/B knob: MNISTX_C1_WG_IMGS=2 runs conv1 wgrad with two images per group (13 -> 26
-// MFMA steps per barrier round over 4 waves, ~52 KB LDS -> 3 workgroups / CU).  Read
-// once; the launch and the slab-sizing grid query both go through it.
-static int c1_wg_imgs() {
-  static const int v = [] { const char* e = getenv("MNISTX_C1_WG_IMGS"); return (e && e[0] == '2') ? 2 : WG_IMGS_C1; }();
-  return v;
-}
+// conv1 wgrad: one image per group (LDS 25.7 KB -> 6 workgroups / CU); two images per
+// group (~52 KB, 3 workgroups / CU) measured slower (profiles/r3/lenet/knobs/)
+constexpr int WG_IMGS_C1 = 1;
 using LeNetC2 = Geo<8, 16, 5, 0, 14, 14>;
 using RefC1g = Geo<1, 32, 5, 2, 28, 28>;
 using RefC1c = Geo<3, 32, 5, 2, 28, 28>;
 
-// ------------------------------------------------------------------ LeNet-5: conv2 data gradient -> conv1 weight gradient, fused
-// The pool1 gradient dP1 = conv2 dgrad(unpool(dP2, arg2)) is consumed by conv1's
-// weight gradient image by image inside one kernel, so it never exists in HBM
-// (the two-kernel path writes and re-reads 2 x 3 KB per image: 400 MB per step at
-// B = 65536).  Per image group (persistent blocks, grid stride):
-//   stage   : x -> image tile (copy 0); max-unpool(dP2, arg2) -> haloed dY2 tile;
-//             arg1 bytes -> LDS                                              | barrier
-//   phase 1 : the three kw-shifted copies of x (make_shifted) and, beside them,
-//             conv2 dgrad (convpool_dgrad_pair_k's MFMA layout); its epilogue
-//             rounds dP1 to bf16 (as the stored tensor would be) and max-unpools
-//             it through arg1 straight into conv1 wgrad's U operand         | barrier
-//   phase 2 : conv1 weight gradient (convpool_wgrad_pair_k's MFMA layout)
-// The slab is convpool_wgrad_pair_k's ([KM][8] per block, bias row KE), so the
-// split-K reduce is unchanged.  Bias: each lane owns one dP1 channel; per-lane
-// sums combined in a fixed lane order (deterministic).
-template <int IMGS>
-__global__ __launch_bounds__(NTH, 3) void lenet_c2dgrad_c1wgrad_k(const XSrc x, const bf16_t* __restrict__ dP2,
-                                                               const uint8_t* __restrict__ arg2,
-                                                               const bf16_t* __restrict__ w2,
-                                                               const uint8_t* __restrict__ arg1, int B,
-                                                               float* __restrict__ slab) {
-  using G2 = LeNetC2;
-  using G1 = LeNetC1;
-  // conv2 dgrad geometry (convpool_dgrad_pair_k<G2>)
-  constexpr int Q = G2::KS - 1 - G2::PAD;
-  constexpr int OHQ = G2::OH + 2 * Q, OWQ = G2::OW + 2 * Q;
-  constexpr int DPS = G2::COUT + 8;
-  constexpr int RSE = (OWQ * DPS * 2 + 255) / 256 * 128;
-  constexpr int DT = OHQ * RSE;
-  constexpr int KWQ = G2::KS + 1;
-  constexpr int NTAP = G2::KS * KWQ;
-  constexpr int KSD = (NTAP + 1) / 2;
-  constexpr int MFD = G2::H / 2;
-  constexpr int NWC2 = G2::NWIN * G2::COUT;
-  auto dtap_c = [](int s) constexpr { return (2 * s / KWQ) * RSE + (2 * s % KWQ) * DPS; };
-  // conv1 wgrad geometry (convpool_wgrad_pair_k<G1>)
-  constexpr int RS = (2 * G1::NWIN + 31) / 32;
-  constexpr int URS = 212;
-  static_assert(URS >= RS * 16 && URS % 8 == 4, "U row stride");
-  constexpr int UIMG = 16 * URS;
-  constexpr int NWC1 = G1::NWIN * arg_bytes<G1>();    // arg1 bytes per image (packed codes)
-  static_assert(arg_packed<G1>() && NWC1 % 16 == 0 && G2::H * G2::W == G1::NWIN && G2::CIN == 8,
-                "dP1 = pool1 windows x 8 channels");
-  constexpr int TILE_E = (IMGS * G1::IMG_LDS + 7) / 8 * 8;
-  __shared__ __attribute__((aligned(16))) bf16_t dyt[IMGS * DT];
-  __shared__ __attribute__((aligned(16))) bf16_t tile[TILE_E];
-  __shared__ __attribute__((aligned(16))) uint32_t U[IMGS * UIMG];
-  __shared__ __attribute__((aligned(16))) uint8_t a1s[IMGS * NWC1];
-  float* const red = (float*)dyt;                    // end-of-kernel reductions reuse the dY2 tile
-  static_assert(IMGS * DT * 2 >= G1::KM * 16 * 4, "wgrad reduction reuses dyt");
-  static_assert(IMGS * UIMG >= NTH + 64, "bias combine reuses U");
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, li = lane & 15;
-  const int ci = li & 7, sx = li >> 3;
-  lds_zero<IMGS * DT>(dyt, tid);
-  lds_zero<TILE_E>(tile, tid);
-  lds_zero<IMGS * UIMG * 2>((bf16_t*)U, tid);         // windows >= NWIN stay zero
-
-  // conv2 dgrad: flipped-filter B fragments (resident).  A-fragment tap of k-step s:
-  // tp = 2s + g/2; since KWQ is even, kh = (2s)/KWQ for both g/2, so the tap offset is
-  // dtap(s) (compile time, a ds_read immediate) + the lane's (g/2)*DPS + 8(g&1)
-  static_assert(KWQ % 2 == 0 && 2 * (KSD - 1) + 1 < NTAP, "tap split");
-  bf16x8 bw[KSD];
-#pragma unroll
-  for (int s = 0; s < KSD; ++s) {
-    const int tp = 2 * s + (g >> 1);
-    const int kh = tp / KWQ, kwq = tp - kh * KWQ;
-    const int kw = kwq - sx;
-    const bool valid = tp < NTAP && kw >= 0 && kw < G2::KS;
-    const int tap = valid ? (G2::KS - 1 - kh) * G2::KS + (G2::KS - 1 - kw) : 0;
-    const u32x4 v = *(const u32x4*)(w2 + (tap * G2::CIN + ci) * G2::COUT + 8 * (g & 1));
-    bw[s] = __builtin_bit_cast(bf16x8, valid ? v : u32x4{0u, 0u, 0u, 0u});
-  }
-  // conv1 wgrad: im2col^T chunk deltas
-  const int q = (lane >> 2) & 3, p = lane & 3;
-  int cd[G1::MFW];
-#pragma unroll
-  for (int mf = 0; mf < G1::MFW; ++mf) {
-    const int k0 = mf * 16 + 4 * p;
-    cd[mf] = k0 < G1::KE ? G1::chunk_delta(k0) : 0;
-  }
-  f32x4 acc1[G1::MFW];
-#pragma unroll
-  for (int mf = 0; mf < G1::MFW; ++mf) acc1[mf] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bacc = 0.f;                                    // bias gradient of channel ci
-  // conv1 wgrad reduction steps of this wave: it = wave + 4j
-  constexpr int JW = (IMGS * RS + NTH / 64 - 1) / (NTH / 64);
-
-  constexpr int A1V = IMGS * NWC1 / 16;                // 16-byte arg1 vectors per group
-  constexpr int A1PER = (A1V + NTH - 1) / NTH;
-  u32x4 a1v[A1PER];
-  auto load_a1 = [&](int i0) {   // branch-free; past the batch: zeros (dP1 is zero there too)
-    const auto ra = buf_rsrc(arg1 + (int64_t)i0 * NWC1, (uint32_t)(max(0, min(IMGS, B - i0)) * NWC1));
-#pragma unroll
-    for (int u = 0; u < A1PER; ++u) {
-      const int e = tid + u * NTH;
-      a1v[u] = buf_b128(ra, e < A1V ? (uint32_t)(16 * e) : BUF_OOB);
-    }
-  };
-
-  const int stride = gridDim.x * IMGS;
-  XStage<G1, IMGS> xs;
-  DYStage<G2, IMGS> ys;
-  xs.fetch_rows(x, blockIdx.x * IMGS, B);
-  xs.load(x, blockIdx.x * IMGS, B, tid);
-  xs.fetch_rows(x, blockIdx.x * IMGS + stride, B);
-  ys.load(dP2, arg2, blockIdx.x * IMGS, B, tid);
-  load_a1(blockIdx.x * IMGS);
-  for (int img0 = blockIdx.x * IMGS; img0 < B; img0 += stride) {
-    xs.drain();
-    __syncthreads();
-    xs.store(tile, tid);
-#pragma unroll
-    for (int u = 0; u < A1PER; ++u) {
-      const int e = tid + u * NTH;
-      if (e < A1V) *(u32x4*)(a1s + 16 * e) = a1v[u];
-    }
-    // max-unpool of dP2 into the haloed tile (convpool_dgrad_pair_k)
-#pragma unroll
-    for (int u = 0; u < DYStage<G2, IMGS>::PER; ++u) {
-      const int e = 8 * (tid + u * NTH);
-      if (e < IMGS * NWC2) {
-        const int im = e / NWC2, rem = e - im * NWC2;
-        const int win = rem / G2::COUT, co = rem - win * G2::COUT;
-        const int ph = win / G2::PW, pw = win - ph * G2::PW;
-        uint32_t E[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          E[k] = __builtin_amdgcn_perm(0u, ys.a[u][k >> 1], (k & 1) ? 0x0c030c02u : 0x0c010c00u);
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const int oh = 2 * ph + (d >> 1) + Q, ow = 2 * pw + (d & 1) + Q;
-          u32x4 o;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) o[k] = ys.y[u][k] & half_eq_mask(E[k], (uint32_t)d);
-          *(u32x4*)(dyt + im * DT + oh * RSE + ow * DPS + co) = o;
-        }
-      }
-    }
-    __syncthreads();
-    {   // unconditional prefetch (past the batch: buffer loads of nothing return 0), so
-        // every path issues the same loads and the waitcnt pass keeps its counts exact
-      xs.load(x, img0 + stride, B, tid);
-      xs.fetch_rows(x, img0 + 2 * stride, B);
-      ys.load(dP2, arg2, img0 + stride, B, tid);
-      load_a1(img0 + stride);
-    }
-    // phase 1: shifted copies of x (read only in phase 2) beside conv2 dgrad -> U
-    make_shifted<G1, IMGS>(tile, tid);
-    for (int f = wave; f < IMGS * MFD; f += NTH / 64) {
-      const int im = f / MFD, mf = f - im * MFD;
-      const bf16_t* tb = dyt + im * DT + (2 * mf + (li >> 3)) * RSE + (2 * (li & 7) + (g >> 1)) * DPS + 8 * (g & 1);
-      const int ih = 2 * mf + (g >> 1);
-      // the epilogue's arg1 bytes are read before the MFMA chain (latency hidden)
-      uint32_t av4[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int jr = 4 * (g & 1) + r;
-        av4[r] = 2 * jr < G2::W
-                     ? (uint32_t)(a1s[im * NWC1 + (ih * G2::W + 2 * jr + sx) * 4 + (ci & 3)] >> (4 * (ci >> 2))) & 15u
-                     : 4u;
-      }
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      // the chain's A fragments in batches of DB in flight (all 15 at once cost 40 VGPRs
-      // of occupancy: 2 -> 3 waves per SIMD)
-      constexpr int DB = 5;
-      static_assert(KSD % DB == 0, "");
-#pragma unroll
-      for (int b = 0; b < KSD; b += DB) {
-        bf16x8 a[DB];
-#pragma unroll
-        for (int s = 0; s < DB; ++s) a[s] = __builtin_bit_cast(bf16x8, *(const u32x4*)(tb + dtap_c(b + s)));
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int s = 0; s < DB; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], bw[b + s], acc, 0, 0, 0);
-      }
-      // rows 4g + r: dP1 pixel (ih, iw = 2jr + sx), channel ci; pool1 window w1 = ih*14 + iw
-      uint32_t* Ui = U + im * UIMG;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int jr = 4 * (g & 1) + r;
-        if (2 * jr < G2::W) {
-          const int w1 = ih * G2::W + 2 * jr + sx;
-          const uint32_t yb = f2bf(acc[r]);
-          const uint32_t av = av4[r];
-          bacc += av < 4u ? __uint_as_float(yb << 16) : 0.f;
-          Ui[ci * URS + w1] = (av == 0u ? yb : 0u) | (av == 2u ? yb << 16 : 0u);
-          Ui[(8 + ci) * URS + w1] = (av == 1u ? yb : 0u) | (av == 3u ? yb << 16 : 0u);
-        }
-      }
-    }
-    __syncthreads();
-    // phase 2: conv1 weight gradient (not unrolled: an unrolled loop's image-invariant
-    // tile offsets are hoisted out of the image loop and spill)
-#pragma unroll 1
-    for (int j = 0; j < JW; ++j) {
-      const int it = wave + (NTH / 64) * j;
-      if (it < IMGS * RS) {
-        const int im = it / RS, s = it - im * RS;
-        const uint32_t* ub = U + im * UIMG + li * URS + 16 * s + 2 * g;
-        const bf16x8 bfr = join(*(const s16x4*)ub, *(const s16x4*)(ub + opaque(8)));
-        // image-tile rows of this lane's two windows (arithmetic, no window-table lookup)
-        const int wq = 16 * s + 2 * g + (q >> 1);
-        const int pb0 = im * G1::IMG_LDS + G1::aligned_off(G1::wbase(min(wq, G1::NWIN - 1))) + (q & 1) * G1::WS;
-        const int pb1 = im * G1::IMG_LDS + G1::aligned_off(G1::wbase(min(wq + 8, G1::NWIN - 1))) + (q & 1) * G1::WS;
-#pragma unroll
-        for (int mf = 0; mf < G1::MFW; ++mf) {
-          const bf16x8 a = join(lds_tr4(tile + pb0 + cd[mf]), lds_tr4(tile + pb1 + cd[mf]));
-          acc1[mf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr, acc1[mf], 0, 0, 0);
-        }
-      }
-    }
-  }
-  // cross-wave reduction in a fixed wave order, then the folded [KM][8] slab
-  for (int wv = 0; wv < NTH / 64; ++wv) {
-    __syncthreads();
-    if (wave == wv) {
-#pragma unroll
-      for (int mf = 0; mf < G1::MFW; ++mf)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float& dst = red[(mf * 16 + 4 * g + r) * 16 + li];
-          dst = (wv == 0) ? acc1[mf][r] : dst + acc1[mf][r];
-        }
-    }
-  }
-  float* bred = (float*)U;
-  bred[tid] = bacc;
-  __syncthreads();
-  if (tid < 8) {   // channel c: lanes li = c, c + 8 of every lane group and wave, fixed order
-    float v = 0.f;
-    for (int t = 0; t < NTH; t += 8) v += bred[t + tid];
-    bred[NTH + tid] = v;
-  }
-  __syncthreads();
-  float* out = slab + (int64_t)blockIdx.x * G1::KM * 8;
-  for (int e = tid; e < G1::KM * 8; e += NTH) {
-    const int m = e >> 3, cc = e & 7;
-    float v = 0.f;
-    if (m == G1::KE) v = bred[NTH + cc];
-    else if (m < G1::KE) v = red[m * 16 + cc] + red[(m + 1) * 16 + 8 + cc];
-    out[e] = v;
-  }
-}
-
-// A/B knob MNISTX_LENET_BWD_IMGS=2: two images per group (89 KB LDS, one block per CU)
-static int lenet_bwd_imgs() {
-  static const int v = [] { const char* e = getenv("MNISTX_LENET_BWD_IMGS"); return (e && e[0] == '2') ? 2 : 1; }();
-  return v;
-}
-
 }  // namespace
-
-int lenet_c2dgrad_c1wgrad_grid() {
-  return lenet_bwd_imgs() == 2 ? resident_grid<lenet_c2dgrad_c1wgrad_k<2>>()
-                               : resident_grid<lenet_c2dgrad_c1wgrad_k<1>>();
-}
-
-hipError_t lenet_c2dgrad_c1wgrad(const XSrc& x, const bf16_t* dP2, const uint8_t* arg2, const bf16_t* w2,
-                                 const uint8_t* arg1, int B, float* slab, int grid, hipStream_t st) {
-  if (lenet_bwd_imgs() == 2)
-    hipLaunchKernelGGL((lenet_c2dgrad_c1wgrad_k<2>), dim3(grid), dim3(NTH), 0, st, x, dP2, arg2, w2, arg1, B, slab);
-  else
-    hipLaunchKernelGGL((lenet_c2dgrad_c1wgrad_k<1>), dim3(grid), dim3(NTH), 0, st, x, dP2, arg2, w2, arg1, B, slab);
-  return hipGetLastError();
-}
 
 int convpool_config(int cin, int cout, int ks, int pad, int h, int w) {
   if (ks != 5) return -1;
@@ -2010,9 +1708,7 @@ hipError_t convpool_wgrad(int cfg, const XSrc& x, const bf16_t* dP, const uint8_
   if (lrn_p && cfg != 2 && cfg != 3) return hipErrorInvalidValue;
   switch (cfg) {
     case 0:
-      if (lenet_c1w_pk_enabled()) return lenet_c1w_pk(x, dP, arg, B, slab, grid, st);
-      return c1_wg_imgs() == 2 ? run_wgrad<LeNetC1, 2>(x, dP, arg, B, slab, grid, st)
-                               : run_wgrad<LeNetC1, WG_IMGS_C1>(x, dP, arg, B, slab, grid, st);
+      return run_wgrad<LeNetC1, WG_IMGS_C1>(x, dP, arg, B, slab, grid, st);
     case 1: return run_wgrad<LeNetC2, 4>(x, dP, arg, B, slab, grid, st);
     // the LRN fold stages one image per group (its LRN input vectors and temporaries
     // would push the 2-image variant past 256 VGPRs: one wave per SIMD)
@@ -2046,8 +1742,7 @@ int wgrad_grid_for() {
 int convpool_wgrad_grid(int cfg) {
   switch (cfg) {
     case 0:
-      if (lenet_c1w_pk_enabled()) return lenet_c1w_pk_grid();
-      return c1_wg_imgs() == 2 ? wgrad_grid_for<LeNetC1, 2>() : wgrad_grid_for<LeNetC1, WG_IMGS_C1>();
+      return wgrad_grid_for<LeNetC1, WG_IMGS_C1>();
     case 1: return wgrad_grid_for<LeNetC2, 4>();
     case 2: return wgrad_grid_for<RefC1g, 2>();
     case 3: return wgrad_grid_for<RefC1c, 2>();

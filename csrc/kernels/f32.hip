@@ -299,9 +299,8 @@ hipError_t launch_f32(const AL& A, const BL& Bm, int M, int N, int K, int splits
   splits = splits < 1 ? 1 : splits;
   int kc = (K + splits - 1) / splits;
   kc = (kc + FBK - 1) / FBK * FBK;
-  static const bool small_only = [] { const char* e = getenv("MNISTX_F32_TILE"); return e && e[0] == '6'; }();
   const int64_t big = (int64_t)((M + 127) / 128) * ((N + 127) / 128) * splits;
-  if (!small_only && big >= 1024 && N >= 128 && M >= 128) {
+  if (big >= 1024 && N >= 128 && M >= 128) {
     const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
     hipLaunchKernelGGL((gemm_f32_k<128, AL, BL>), dim3(tiles, splits), dim3(FNT), 0, st, A, Bm, M, N, K, kc, ep);
   } else {

@@ -615,14 +615,6 @@ hipError_t launch_cfg(const LA& la, const LB& lb, const GemmEpi& ep, int M, int 
 //    the 256 CUs with fewer than 4 workgroups each.
 enum TileCode { T256x16, T256x32, T128x64, T64x128, T128x128, T64x16, T64x32, T64x64, T256x128 };
 
-// experiment knobs (non-weight-gradient launches): MNISTX_GEMM_TILE forces a tile
-// code, MNISTX_GEMM_PF the K-step prefetch depth of the 128x128 / 64x128 / 256x128 tiles
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return (e && e[0]) ? atoi(e) : dflt;
-}
-static int gemm_tile_override() { static const int v = env_int("MNISTX_GEMM_TILE", -1); return v; }
-static int gemm_pf() { static const int v = env_int("MNISTX_GEMM_PF", 1); return v; }
 
 int tile_code(int M, int N, bool wgrad) {
   auto tiles = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
@@ -649,20 +641,14 @@ hipError_t launch_any(const LA& la, const LB& lb, const GemmEpi& ep, int M, int 
                       hipStream_t st, int code = -1) {
   constexpr bool WG = !AKC && !BKC;
   int c = code >= 0 ? code : tile_code(M, N, WG);
-  if (!WG && code < 0 && gemm_tile_override() >= 0) c = gemm_tile_override();
   if constexpr (!WG) {
     // Large dense fwd / dgrad GEMMs (fully-connected layers at big batch): 256x128
     // tiles with 2 K-steps in flight, measured on MI355X (profiles/r1s3/gemm_sweep.md:
     // 16384x3136x1024 fwd 184 -> 151 us, dgrad 174 -> 153 us vs the 128x128 tile).
     constexpr bool DENSE = IsMat<LA>::value && IsMat<LB>::value;
-    if (DENSE && code < 0 && gemm_tile_override() < 0 && N > 64 && M >= 4096 &&
+    if (DENSE && code < 0 && N > 64 && M >= 4096 &&
         ((M + 255) / 256) * ((N + 127) / 128) >= 512)
       return launch_cfg<256, 128, 2, 2, LA, AKC, LB, BKC, 2>(la, lb, ep, M, N, K, splits, st);
-    const int pf = gemm_pf();
-    if (c == T128x128 && pf == 2) return launch_cfg<128, 128, 2, 2, LA, AKC, LB, BKC, 2>(la, lb, ep, M, N, K, splits, st);
-    if (c == T128x128 && pf == 3) return launch_cfg<128, 128, 2, 2, LA, AKC, LB, BKC, 3>(la, lb, ep, M, N, K, splits, st);
-    if (c == T64x128 && pf == 2) return launch_cfg<64, 128, 1, 4, LA, AKC, LB, BKC, 2>(la, lb, ep, M, N, K, splits, st);
-    if (c == T256x128 && pf == 2) return launch_cfg<256, 128, 2, 2, LA, AKC, LB, BKC, 2>(la, lb, ep, M, N, K, splits, st);
     if (c == T256x128) return launch_cfg<256, 128, 2, 2, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
   }
   switch (c) {
@@ -737,9 +723,9 @@ hipError_t dense_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int
 
 // Tile width of the grouped weight gradients: 128 columns cover LeNet's fc3 / fc4 outputs
 // (120 / 88) in ONE column tile, so their input activations (fc3: the 52 MB pool2 at
-// B = 65536) are read once instead of twice.  MNISTX_WG_GROUP_BN=64 for A/B; the
-// split choice (ops/functional.py pick_splits, grouped=True) reads the same variable.
-int wg_group_bn() { static const int v = env_int("MNISTX_WG_GROUP_BN", 128); return v == 64 ? 64 : 128; }
+// B = 65536) are read once instead of twice (64: profiles/r3/lenet/knobs/, slower); the
+// split choice (ops/functional.py pick_splits, grouped=True) assumes the same width.
+int wg_group_bn() { return 128; }
 
 hipError_t dense_wgrad_group(int np, const bf16_t* const* x, const bf16_t* const* dy, const int* Din, const int* Dout,
                              int B, const int* ldx, const int* lddy, int* splits, const GemmEpi* ep, hipStream_t st) {

@@ -88,11 +88,6 @@ struct XSrc {
   int n;
 };
 int convpool_u8_input(int cfg);
-// LeNet-5 conv1 weight gradient, pooled-K form (lenet_c1wgrad.hip); same slab as cfg 0's
-bool lenet_c1w_pk_enabled();
-int lenet_c1w_pk_grid();
-hipError_t lenet_c1w_pk(const XSrc& x, const bf16_t* dP, const uint8_t* arg, int B, float* slab, int grid,
-                        hipStream_t st);
 int convpool_config(int cin, int cout, int ks, int pad, int h, int w);  // -1: unsupported
 int convpool_wgrad_rows(int cfg);                                      // KM (slab rows incl. bias row)
 // slab -> dW layout for splitk_reduce: {G, Ipad, I (-1: real Cin), bias_row}
@@ -112,12 +107,6 @@ int convpool_has_dgrad(int cfg);
 int convpool_arg_bytes(int cfg);
 hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int B, bf16_t* dx,
                           int grid_cap, hipStream_t st);
-// LeNet-5 conv2 data gradient fused into conv1's weight gradient (dP1 never in HBM):
-// slab = convpool_wgrad(cfg 0)'s layout, one [KM][8] partial per block (grid <= the
-// resident grid lenet_c2dgrad_c1wgrad_grid())
-int lenet_c2dgrad_c1wgrad_grid();
-hipError_t lenet_c2dgrad_c1wgrad(const XSrc& x, const bf16_t* dP2, const uint8_t* arg2, const bf16_t* w2,
-                                 const uint8_t* arg1, int B, float* slab, int grid, hipStream_t st);
 
 // ---- lenet_bwd.hip: LeNet-5 conv-stack backward (conv2 dgrad + both weight gradients) as ONE
 // persistent kernel; slab1 [grid][32][8] (rows tap 0..24, bias 25), slab2 [grid][208][16]

@@ -14,17 +14,13 @@
 //
 // v_mfma_f32_32x32x16_bf16, columns = 32 = 16 images x 2 output-row parities
 // (ypar = column & 1), rows = output features:
-//  * conv1 (default, INL): rows = (window position g = 2 ypar + xpar, channel 3+1 per
+//  * conv1: rows = (window position g = 2 ypar + xpar, channel 3+1 per
 //    lane half), columns = (pooled row half, image, pooled column parity xq); K = 16 =
 //    (input row parity h, 8 input columns from 4u + 2xq - 2): 3 k-steps cover the 6
 //    input rows of a pooled row.  Each lane then holds the 4 positions of its windows
 //    in 4 registers: the pool is 3 v_max in the lane, no cross-lane exchange, and the
-//    padded channels are never pooled (47 VALU per 3 MFMAs against 85 for the layout
-//    below; band kernel 201 -> 161 us, profiles/r3/lenet/inlane/).
-//  * conv1 (MNISTX_BAND_INLANE=0): rows = (xq 2, xpar 2, c 8): the four consecutive output
-//    columns x = 4u + 2xq + xpar of window u; K = 16 = (dy parity h, 8 input columns
-//    x' = 4u-2 .. 4u+5): one k-step covers TWO kernel rows, so 3 k-steps = dy 0..4
-//    (+ one zero row).  3 MFMAs per (pooled row, window), 3 A fragments in total.
+//    padded channels are never pooled (47 VALU per 3 MFMAs against 85 for a lane-pair
+//    pooling layout; band kernel 201 -> 161 us, profiles/r3/lenet/inlane/).
 //  * conv2 rows = (xpar 2, c2 16) of ONE pooled column x2p; K = 16 = 2 input
 //    pixels x 8 channels; 3 k-steps x 5 kernel rows.  15 A fragments in total.
 //  * bias added after pooling (4 values per lane instead of 16 accumulators).
@@ -83,8 +79,6 @@ DEV float vmax3(float a, float b, float c) {
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
-// value of the neighbouring lane (lane ^ 1): the other output-row parity of the same image
-DEV float swap1(float v) { return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true)); }
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 // two floats -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (round to nearest even)
@@ -116,16 +110,6 @@ struct BandFwd {
   unsigned long long* prof;   // optional (experiments): per-role busy / barrier-wait clock sums
   int prio;                   // 1 = conv1 waves at s_setprio 1 (default), 2 = conv2 waves, 0 = none
 };
-
-// Pooled value + argmax code of the window finalised by this lane: keep = this lane's
-// x-pooled (embedded) sum, send = the one its neighbour finalises, b = the channel's
-// bias (added after pooling: max(a + b, c + b) = max(a, c) + b, ReLU is monotone).
-DEV void pool_y(float keep, float send, float b, float& out, uint32_t& code) {
-  const float v = vmax(keep, swap1(send));
-  out = vmax(__uint_as_float(__float_as_uint(v) & ~3u) + b, 0.f);
-  // active on the CLEARED value: an all-zero window (padded channel) embeds to d > 0
-  code = out > 0.f ? (__float_as_uint(v) & 3u) : ARG_OFF;
-}
 
 // input tile fill by the conv1 waves: thread t (0..255) -> image t >> 5, 8-byte chunks
 // (4 pixels) r = (t & 31) + 32 i of the image's 196
@@ -175,31 +159,12 @@ struct XFill {
       }
     }
   }
-  DEV void store(bf16_t* xb, int t, bool u8) const {
-    bf16_t* im = xb + (t >> 5) * XIS + 2;
-#pragma unroll
-    for (int i = 0; i < FCH; ++i) {
-      const int r = (t & 31) + 32 * i;
-      if (r < 196) {
-        const int y = r / 7, k = r - 7 * y;
-        uint32_t* d = (uint32_t*)(im + (y & 1) * XPL + (y >> 1) * XRW + 4 * k);   // 4-byte aligned
-        uint32_t lo = v[i][0], hi = v[i][1];
-        if (u8) {   // mnist_input.py:37-39 normalisation, rounded as prep_images does
-          const uint32_t b = v[i][0];
-          lo = pack2(u8_norm(b & 0xff), u8_norm((b >> 8) & 0xff));
-          hi = pack2(u8_norm((b >> 16) & 0xff), u8_norm(b >> 24));
-        }
-        d[0] = lo;
-        d[1] = hi;
-      }
-    }
-  }
 };
 
 // Warp-specialised pipeline over the block's tiles k = 0..nk-1 (tile blockIdx + k * grid):
 // iteration k: conv1 waves turn input[k%2] into pool1[k%2] (and load tile k+1's input),
 // conv2 waves turn pool1[(k-1)%2] into pool2 -- one barrier per iteration, nk+1 iterations.
-template <bool P1OUT, bool INL>
+template <bool P1OUT>
 __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_X + LDS_P];
   bf16_t* xs = lds;
@@ -220,7 +185,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
   for (int e = tid; e < LDS_X / 8; e += NTH) *(u32x4*)(xs + 8 * e) = u32x4{0u, 0u, 0u, 0u};
   __syncthreads();
 
-  if (wave < 4 && INL) {
+  if (wave < 4) {
     // ================================================================ conv1 + pool1 role, in-lane pooling
     // rows m = 8 g + 4 hh + i4: window position g = 2 ypar + xpar (= the argmax code), channel
     // c = ch(hh, i4) (3 per lane half, i4 = 3 is padding), so C register 4 g + i4 of a lane
@@ -355,127 +320,6 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
       atomicAdd(a.prof + 0, (unsigned long long)busy);
       atomicAdd(a.prof + 2, (unsigned long long)wait);
     }
-  } else if (wave < 4) {
-    // ================================================================ conv1 + pool1 role
-    const int t = tid;                                   // 0..255
-    if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
-    bf16x8 a1[3];    // (p): rows (xq, xpar, c), k = (dy parity h, input column j of the window)
-    {
-      const int xq = col >> 4, xpar = (col >> 3) & 1, c = col & 7;
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const int dy = 2 * p + h;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int dx = j - 2 * xq - xpar;
-          const bool ok = dy <= 4 && dx >= 0 && dx <= 4;
-          a1[p][j] = __builtin_bit_cast(__bf16, w1s[ok ? (dy * 5 + dx) * 8 + c : W1E]);
-        }
-      }
-    }
-    float bias1[4];    // channels c = i + 4h this lane finalises (added after pooling)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bias1[i] = i + 4 * h < a.b1n ? a.b1[i + 4 * h] : 0.f;
-    const uint32_t d0 = 2u * ypar, d1 = d0 + 1u;     // argmax codes of this lane's x parities
-    const auto rx = a.u8 ? buf_rsrc(a.u8, (uint32_t)a.n * XIMG) : buf_rsrc(a.x, (uint32_t)a.n * (XIMG * 2));
-    // input rows of a unit: row = S + rlane with S = yp0 + p - 1 (uniform) and the lane's
-    // dy parity h / row half; plane (ypar + h) & 1
-    const int rlane = 7 * half + ((ypar + h) >> 1);
-    const int xlane = img * XIS + ((ypar + h) & 1) * XPL + rlane * XRW;
-    // pool1 store offset: lane part + row-half part (yp = yp0 + 7 half)
-    const int plane_off = img * PIS + ypar * 8 + 4 * h;
-    XFill xf;
-    xf.load(rx, a, nk > 0 ? tile0(0) : -1, t);
-    xf.store(xs, t, a.u8 != nullptr);     // ring slot 0 (only this role reads the input ring; ordered by the first barrier)
-
-    uint64_t busy = 0, wait = 0, tw = __builtin_amdgcn_s_memtime();
-    for (int k = 0; k <= nk; ++k) {
-      __syncthreads();   // input[k%2] landed; pool1[k%2] no longer read by conv2
-      const uint64_t tb = __builtin_amdgcn_s_memtime();
-      wait += tb - tw;
-      if (k < nk) {
-        const bf16_t* xb = xs + (k & 1) * XBUF + xlane;
-        bf16_t* pb = p1s + (k & 1) * PBUF + plane_off;
-        xf.load(rx, a, k + 1 < nk ? tile0(k + 1) : -1, t);
-        struct Frags { bf16x8 b[3]; };
-        auto fetch = [&](int j) {   // unit f = wave + 4j: B fragments, window columns x' = 4u-2 .. 4u+5
-          const int f = min(wave + 4 * j, U1 - 1), yp0 = f / 7, u = f - 7 * yp0;
-          Frags fr;
-#pragma unroll
-          for (int p = 0; p < 3; ++p) {
-            const int S = yp0 + p - 1;
-            const bf16_t* rp = (unsigned)(rlane + S) < 14u ? xb + S * XRW + 4 * u : xs + XZERO;
-            // 8-byte aligned only: two 8-byte loads (ds_read2_b64), never one misaligned b128
-            const u32x2 lo = *(const u32x2*)rp, hi = *(const u32x2*)(rp + 4);
-            fr.b[p] = as_frag(u32x4{lo[0], lo[1], hi[0], hi[1]});
-          }
-          return fr;
-        };
-        auto window = [&](const Frags& fr) {
-          f32x16 acc = {};
-#pragma unroll
-          for (int p = 0; p < 3; ++p) acc = mfma32(a1[p], fr.b[p], acc);
-          return acc;
-        };
-        auto epilogue = [&](const f32x16& acc, int j) {
-          const int f = wave + 4 * j, yp0 = f / 7, u = f - 7 * yp0;
-          // rows: xq = r>>3, xpar = (r>>2)&1, c = (r&3) + 4h; lane ypar finalises xq = ypar
-          float o[4];
-          uint32_t hi;
-          if constexpr (P1OUT) {   // + argmax codes
-            float keep[4], send[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float m0 = vmax(embed(acc[i], d0), embed(acc[i + 4], d1));        // xq 0
-              const float m1 = vmax(embed(acc[8 + i], d0), embed(acc[12 + i], d1));   // xq 1
-              keep[i] = ypar ? m1 : m0;
-              send[i] = ypar ? m0 : m1;
-            }
-            uint32_t cd[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) pool_y(keep[i], send[i], bias1[i], o[i], cd[i]);
-            // packed argmax, byte k = code(c = k) | code(c = k + 4) << 4 (lane h holds c = 4h..4h+3),
-            // parked in the pixel's channels 6-7 (always 0 in HBM; zero weights in conv2, and a
-            // nibble-packed word is a finite bf16 pair) until the copy-out splits it off
-            const uint32_t wcode = cd[0] | (cd[1] << 8) | (cd[2] << 16) | (cd[3] << 24);
-            const auto sw = __builtin_amdgcn_permlane32_swap(wcode, wcode, false, false);
-            hi = h ? (sw[0] | (wcode << 4)) : pk2(o[2], o[3]);
-          } else {                 // values only
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float m0 = vmax(acc[i], acc[i + 4]), m1 = vmax(acc[8 + i], acc[12 + i]);
-              o[i] = vmax(vmax(ypar ? m1 : m0, swap1(ypar ? m0 : m1)) + bias1[i], 0.f);
-            }
-            hi = pk2(o[2], o[3]);
-          }
-          if (f < U1) {
-            const int y0 = yp0, y1 = yp0 + 7;   // the lane's pooled row: y0 (half 0) or y1 (half 1)
-            const int off = half ? (y1 & 1) * PPL + (y1 >> 1) * PRW : (y0 & 1) * PPL + (y0 >> 1) * PRW;
-            *(u32x2*)(pb + off + 16 * u) = u32x2{pk2(o[0], o[1]), hi};
-          }
-        };
-        // software pipeline, 13 slots per wave (past 49: a recomputed unit, no store):
-        // unit j+2's LDS reads and unit j+1's MFMAs issue before unit j's epilogue
-        Frags fa = fetch(0), fb = fetch(1);
-        f32x16 acca = window(fa), accb;
-#pragma unroll 1
-        for (int j = 0; j < 14; j += 2) {
-          fa = fetch(j + 2);
-          accb = window(fb);
-          epilogue(acca, j);
-          fb = fetch(j + 3);
-          acca = window(fa);
-          epilogue(accb, j + 1);
-        }
-        xf.store(xs + ((k + 1) & 1) * XBUF, t, a.u8 != nullptr);   // tile k+1's input (slot read in iteration k-1)
-      }
-      tw = __builtin_amdgcn_s_memtime();
-      busy += tw - tb;
-    }
-    if (a.prof && lane == 0) {
-      atomicAdd(a.prof + 0, (unsigned long long)busy);
-      atomicAdd(a.prof + 2, (unsigned long long)wait);
-    }
   } else {
     // ================================================================ conv2 + pool2 role
     const int t = tid - 256;
@@ -494,13 +338,6 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
             a2[dy * 3 + q][j] = __builtin_bit_cast(__bf16, w1s[ok ? W1E + 8 + ((dy * 5 + dx) * 8 + j) * 16 + c2 : W1E]);
         }
     }
-    float bias2[4];    // channels c2 = i + 8 ypar + 4h this lane finalises (added after pooling)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bias2[i] = a.b2[i + 8 * ypar + 4 * h];
-    // pool1 row yy = 2 y2p + ypar + dy: even dy -> plane ypar, row y2p + dy/2; odd dy -> plane
-    // 1 - ypar, row y2p + (dy - 1)/2 + ypar
-    const int ce = img * PIS + ypar * PPL + 8 * h, co = img * PIS + (1 - ypar) * PPL + ypar * PRW + 8 * h;
-    const uint32_t d0 = 2u * ypar, d1 = d0 + 1u;
     const int w2v = wave - 4;
     const int cp_r = (t + 192) & 255;   // copy-out pixel of this thread (>= 196: none)
     const int cp_lds = ((cp_r / 14) & 1) * PPL + ((cp_r / 14) >> 1) * PRW + (cp_r % 14) * 8;
@@ -514,7 +351,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
       const int t0 = tile0(k - 1), gi = t0 + img;
       const bool iv = gi < a.B;
       const bf16_t* pb = p1s + ((k - 1) & 1) * PBUF;
-      if constexpr (P1OUT && INL) {   // pool1 + argmax codes to HBM for the backward kernels
+      if constexpr (P1OUT) {          // pool1 + argmax codes to HBM for the backward kernels
         // copy thread ct owns pooled pixel ct (< 196) of every image of the tile: one LDS
         // offset per thread, image strides as instruction / scalar offsets (no per-element
         // index arithmetic).  ct is rotated so the wave with 4 conv2 units copies least.
@@ -536,29 +373,8 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
             }
           }
         }
-      } else if constexpr (P1OUT) {
-        constexpr int NV = BT * 196;
-        const int nimg = min(BT, a.B - t0);
-        const auto rp1 = buf_rsrc(a.p1 + (int64_t)t0 * P1E, (uint32_t)nimg * (P1E * 2));
-        const auto ra1 = buf_rsrc(a.arg1 + (int64_t)t0 * 784, (uint32_t)nimg * 784);
-#pragma unroll 1
-        for (int e0 = t; e0 < NV; e0 += 4 * 256) {
-          u32x4 cv[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int e = min(e0 + i * 256, NV - 1), im = e / 196, r = e - im * 196, yp = r / 14, xp = r - yp * 14;
-            cv[i] = *(const u32x4*)(pb + im * PIS + (yp & 1) * PPL + (yp >> 1) * PRW + xp * 8);
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int e = e0 + i * 256;
-            const uint32_t oob = e < NV ? 0u : BUF_OOB;
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4{cv[i][0], cv[i][1], cv[i][2], 0u}, rp1, (uint32_t)e * 16u + oob, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(cv[i][3], ra1, (uint32_t)e * 4u + oob, 0, 0);
-          }
-        }
       }
-      if constexpr (INL) {
+      {
         // in-lane pooling: columns = (pooled-pixel slot, image), ONE accumulator per output-row
         // parity of the window, so a lane holds all 4 positions of 8 channels: the pool is
         // 3 v_max in the lane (no DPP, no keep/send selects, no chain sum).  Unit u = pooled
@@ -611,56 +427,6 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
             *(uint32_t*)(a.arg2 + e + 8) = cd[4] | (cd[5] << 8) | (cd[6] << 16) | (cd[7] << 24);
           }
         }
-      } else {
-      // unit = lane's pooled pixel f = f0 + 13 half (f0 = w2v + 4j); the 15 B fragments of a
-      // kernel row dy are read one row ahead; two accumulator chains
-#pragma unroll 1
-      for (int j = 0; j < 4; ++j) {
-        const int f0 = w2v + 4 * j;
-        if (f0 >= U2) break;
-        const int fa = f0, fbb = min(f0 + 13, 24);
-        const int ya = fa / 5, yb = fbb / 5;
-        const int uoff = half ? yb * PRW + 16 * (fbb - 5 * yb) : ya * PRW + 16 * (fa - 5 * ya);
-        const int y2p = half ? yb : ya, x2p = (half ? fbb : fa) - 5 * y2p;
-        const bf16_t* re = pb + ce + uoff;
-        const bf16_t* ro = pb + co + uoff;
-        auto rowp = [&](int dy) { return (dy & 1) ? ro + (dy >> 1) * PRW : re + (dy >> 1) * PRW; };
-        bf16x8 bq[2][3];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) bq[0][q] = *(const bf16x8*)(rowp(0) + 16 * q);
-        f32x16 acc0 = {}, acc1 = {};
-#pragma unroll
-        for (int dy = 0; dy < 5; ++dy) {
-          if (dy < 4) {
-#pragma unroll
-            for (int q = 0; q < 3; ++q) bq[(dy + 1) & 1][q] = *(const bf16x8*)(rowp(dy + 1) + 16 * q);
-          }
-#pragma unroll
-          for (int q = 0; q < 3; ++q) {
-            if ((dy * 3 + q) & 1) acc1 = mfma32(a2[dy * 3 + q], bq[dy & 1][q], acc1);
-            else acc0 = mfma32(a2[dy * 3 + q], bq[dy & 1][q], acc0);
-          }
-        }
-        const f32x16 acc = acc0 + acc1;
-        // rows: xpar = r>>3, c2 = (r&3) + 8((r>>2)&1) + 4h; lane ypar finalises c2 = (i&3) + 8 ypar + 4h
-        float keep[4], send[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float m0 = vmax(embed(acc[i], d0), embed(acc[i + 8], d1));          // c2 = i + 4h
-          const float m1 = vmax(embed(acc[4 + i], d0), embed(acc[12 + i], d1));     // c2 = 8 + i + 4h
-          keep[i] = ypar ? m1 : m0;
-          send[i] = ypar ? m0 : m1;
-        }
-        float o[4];
-        uint32_t cd[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pool_y(keep[i], send[i], bias2[i], o[i], cd[i]);
-        if (iv && (half == 0 || f0 + 13 < 25)) {
-          const int64_t e = (int64_t)gi * P2E + (y2p * 5 + x2p) * 16 + 8 * ypar + 4 * h;
-          *(u32x2*)(a.p2 + e) = u32x2{pk2(o[0], o[1]), pk2(o[2], o[3])};
-          *(uint32_t*)(a.arg2 + e) = cd[0] | (cd[1] << 8) | (cd[2] << 16) | (cd[3] << 24);
-        }
-      }
       }
       tw = __builtin_amdgcn_s_memtime();
       busy += tw - tb;
@@ -672,7 +438,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
   }
 }
 
-template <bool P1OUT, bool INL>
+template <bool P1OUT>
 int fwd_grid(int ntiles) {
   static int per_cu = -1, cus = 0;
   if (per_cu < 0) {
@@ -682,7 +448,7 @@ int fwd_grid(int ntiles) {
     if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return -1;
     cus = prop.multiProcessorCount;
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lenet_band_fwd_k<P1OUT, INL>, NTH, 0) != hipSuccess) return -1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lenet_band_fwd_k<P1OUT>, NTH, 0) != hipSuccess) return -1;
     per_cu = nb > 0 ? nb : 1;
   }
   return cap_grid(ntiles < per_cu * cus ? ntiles : per_cu * cus);
@@ -846,22 +612,16 @@ hipError_t lenet_band_fwd(const XSrc& x, const bf16_t* w1, const float* b1, int 
   if (!x.x && !x.u8) return hipErrorInvalidValue;
   // conv1 (the busier role: ~90 % vs ~73 % of the iteration) at s_setprio 1 wins the
   // SIMD's issue arbitration against the conv2 waves: 219-222 -> 210-211 us, 0.61 -> 0.595
-  // ms/step (profiles/r3/lenet/band_prio_ab.txt); MNISTX_BAND_PRIO=0 / 2 for A/B
-  static const int prio = [] { const char* e = getenv("MNISTX_BAND_PRIO"); return e ? atoi(e) : 1; }();
-  BandFwd a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, w1, b1, b1n, w2, b2, B, p1, arg1, p2, arg2, prof, prio};
+  // ms/step (profiles/r3/lenet/band_prio_ab.txt)
+  BandFwd a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, w1, b1, b1n, w2, b2, B, p1, arg1, p2, arg2, prof, 1};
   const int ntiles = (B + BT - 1) / BT;
-  // conv1 pooling in the lane (INL, default) or across lane pairs; MNISTX_BAND_INLANE=0 for A/B
-  static const bool inl = [] { const char* e = getenv("MNISTX_BAND_INLANE"); return !e || atoi(e) != 0; }();
   auto go = [&](auto ker, int grid) {
     if (grid <= 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(ker, dim3(grid), dim3(NTH), 0, st, a);
     return hipSuccess;
   };
-  hipError_t e;
-  if (p1) e = inl ? go(lenet_band_fwd_k<true, true>, fwd_grid<true, true>(ntiles))
-                  : go(lenet_band_fwd_k<true, false>, fwd_grid<true, false>(ntiles));
-  else e = inl ? go(lenet_band_fwd_k<false, true>, fwd_grid<false, true>(ntiles))
-               : go(lenet_band_fwd_k<false, false>, fwd_grid<false, false>(ntiles));
+  const hipError_t e = p1 ? go(lenet_band_fwd_k<true>, fwd_grid<true>(ntiles))
+                          : go(lenet_band_fwd_k<false>, fwd_grid<false>(ntiles));
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }

@@ -164,10 +164,10 @@ DEV void dx_tiles(int v0, const bf16_t* i3, const uint32_t (&d3p)[T1][8], bf16_t
   }
 }
 
-// NW waves per block, TPW 32-row tiles per wave.  TPW = 2 (NW = 4: same 256 rows and
-// LDS images per block, one wave per SIMD) issues the next tile's X loads right after
-// the current tile's fc3, so they and the current tile's stores overlap its backward
-// chain; TPW = 1 runs every wave's load / compute / store phases in lockstep.
+// NW waves per block, TPW 32-row tiles per wave.  The launch uses TPW = 1 (every wave's
+// load / compute / store phases in lockstep); TPW = 2 with 4 waves (the next tile's X
+// loads under the current tile's backward chain) measured slower (0.540 vs 0.53 ms/step,
+// profiles/r3/lenet/knobs/).
 template <bool GRADS, int NW = NWAVE, int TPW = 1>
 __global__ __launch_bounds__(64 * NW) void mlp_head_k(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W3t,
                                                   const float* __restrict__ b3, int n1, const bf16_t* __restrict__ W4t,
@@ -426,12 +426,6 @@ __global__ __launch_bounds__(64 * NW) void mlp_head_k(const bf16_t* __restrict__
 
 }  // namespace
 
-// MNISTX_HEAD_TPW=2: the 4-wave, two-tiles-per-wave layout (experiment knob)
-static int head_tpw() {
-  static const int v = [] { const char* e = getenv("MNISTX_HEAD_TPW"); return (e && e[0] == '2') ? 2 : 1; }();
-  return v;
-}
-
 int mlp_head_blocks(int nb) { return (nb + ROWS - 1) / ROWS; }
 
 bool mlp_head_supported(int d0, int ld1, int ld2, int ld3, int n1, int n2, int nc, int B) {
@@ -444,16 +438,7 @@ hipError_t mlp_head(const bf16_t* x, const bf16_t* w3t, const float* b3, int n1,
                     bf16_t* h3, bf16_t* h4, float* logits, bf16_t* dl, bf16_t* dh4, bf16_t* dh3, bf16_t* dx,
                     float* stats, float* work, hipStream_t st, int defer_stats) {
   if (nb <= 0) return hipSuccess;
-  const dim3 grid((nb + ROWS - 1) / ROWS);   // ROWS rows per block in both layouts
-  if (head_tpw() == 2) {
-    if (dl)
-      hipLaunchKernelGGL((mlp_head_k<true, NWAVE / 2, 2>), grid, dim3(NTH / 2), 0, st, x, w3t, b3, n1, w4t, b4, n2,
-                         w5t, b5, nc, labels, nb, scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work, defer_stats);
-    else
-      hipLaunchKernelGGL((mlp_head_k<false, NWAVE / 2, 2>), grid, dim3(NTH / 2), 0, st, x, w3t, b3, n1, w4t, b4, n2,
-                         w5t, b5, nc, labels, nb, scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work, defer_stats);
-    return hipGetLastError();
-  }
+  const dim3 grid((nb + ROWS - 1) / ROWS);   // ROWS rows per block
   if (dl)
     hipLaunchKernelGGL(mlp_head_k<true>, grid, dim3(NTH), 0, st, x, w3t, b3, n1, w4t, b4, n2, w5t, b5, nc, labels, nb,
                        scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work, defer_stats);

@@ -188,10 +188,6 @@ class ConvPoolLayer(_Layer):
         kernels().convpool_fwd(self._xin(), self.fp.bf16_view(self.wname), self.fp.param_view(self.bname),
                                self.spec.cout, self.out, self.arg, nb, *self._geo(), **self._src())
 
-    # (dY of the next conv+pool layer, that layer): its data gradient is computed
-    # inside this layer's weight-gradient kernel (HipNet.fuse_c2d_c1w)
-    fused_dgrad: Optional[tuple] = None
-    fused_grid = 0
     skip_dgrad = False
 
     # (LRN spec, dL/d(LRN output)): the following LRN's backward is applied inside this
@@ -205,11 +201,6 @@ class ConvPoolLayer(_Layer):
             grid = min(self.grid, max(1, (nb + 3) // 4))
             K.convpool_wgrad(self._xin(), dn, self.arg, slab, grid, nb, *self._geo(), **self._src(), lrn_p=self.out,
                              lrn_bias=ls.bias, lrn_alpha=ls.alpha, lrn_beta=ls.beta, lrn_r=ls.depth_radius)
-        elif self.fused_dgrad is not None:
-            dy2, l1 = self.fused_dgrad
-            grid = min(self.fused_grid, max(1, nb))
-            K.lenet_c2dgrad_c1wgrad(self._xin(), dy2, l1.arg, self.fp.bf16_view(l1.wname), self.arg, slab, grid, nb,
-                                    **self._src())
         else:
             grid = min(self.grid, max(1, (nb + 3) // 4))
             K.convpool_wgrad(self._xin(), dy, self.arg, slab, grid, nb, *self._geo(), **self._src())
@@ -372,7 +363,8 @@ class HipNet:
 
     def __init__(self, spec: ModelSpec, batch: int, device, init: Dict[str, torch.Tensor],
                  opt: Optional[OptConfig] = None, fuse_convpool: bool = True, overlap_backward: bool = False,
-                 fuse_head: bool = True, fuse_lrnpool: Optional[bool] = None, fused_lenet_bwd: bool = True):
+                 fuse_head: bool = True, fuse_lrnpool: Optional[bool] = None, fused_lenet_bwd: bool = True,
+                 fold_lrn_fwd: bool = False):
         dev = torch.device(device)
         if fuse_lrnpool is None:
             fuse_lrnpool = os.environ.get("MNISTX_FUSE_LRNPOOL", "1") != "0"
@@ -466,33 +458,13 @@ class HipNet:
         if self.overlap:
             self.side = torch.cuda.Stream(device=dev)
             self.ev_dy = [torch.cuda.Event() for _ in self.layers]
-            # Co-residency budget (workgroups per CU) for the persistent conv kernels that
-            # run concurrently: the main-stream dgrad and the side-stream weight gradients
-            # each fill every CU by default, which serialises them.  Measured on LeNet-5 at
-            # B=65536 (profiles/r1s3/overlap_budget.txt): every budget is SLOWER than the
-            # serial plan (0.748 ms): all-default 0.779, "2,2" 0.798, "2,1" 0.842 -- the
-            # conv kernels are LDS/issue-bound on the same units, so sharing a CU does not
-            # add throughput.  Kept as an experiment knob.
-            budget = os.environ.get("MNISTX_OVERLAP_WGS", "")
-            if budget:
-                cus = torch.cuda.get_device_properties(dev).multi_processor_count
-                v = [float(x) for x in budget.split(",")]
-                main_wgs, side_wgs = v[0], v[1]
-                first_wgs = v[2] if len(v) > 2 else 0.0
-                for lay in self.layers:
-                    if isinstance(lay, ConvPoolLayer) and lay.idx > 0:
-                        lay.dgrad_cap = max(1, int(main_wgs * cus))
-                        lay.grid = max(1, min(lay.grid, int(side_wgs * cus)))
-                    elif isinstance(lay, ConvPoolLayer) and first_wgs > 0:
-                        lay.grid = max(1, min(lay.grid, int(first_wgs * cus)))
+            # (Co-residency budgets for the concurrent persistent conv kernels were all SLOWER
+            # than the serial plan: profiles/r1s3/overlap_budget.txt -- the conv kernels are
+            # LDS/issue-bound on the same units, so sharing a CU adds no throughput.)
         self.stats = torch.zeros(8, dtype=torch.float32, device=dev)
         self.eval_stats = torch.zeros(8, dtype=torch.float32, device=dev)
         # softmax-CE per-block partials + ticket: deterministic loss / accuracy sums
         self.ce_work = torch.zeros(4 * 1024 + 1, dtype=torch.float32, device=dev)
-        # experiment knob: MNISTX_CE_ATOMIC=1 drops the ticket combine (and its agent-scope
-        # fences) for order-dependent float atomics -- for timing the combine only
-        if os.environ.get("MNISTX_CE_ATOMIC", "0") == "1":
-            self.ce_work = None
         names = [e.name for e in self.fp.wd_entries]
         self.loss_names = [n.replace("/weights", "/weight_loss") for n in names] + ["cross_entropy", "total_loss"]
         self.loss_ema = torch.zeros(3 * len(self.loss_names), dtype=torch.float32, device=dev)
@@ -505,18 +477,11 @@ class HipNet:
         self.head: Optional[int] = self._find_head() if (fuse_head and dev.type == "cuda") else None
         self._head_pending: Optional[int] = None   # nb of a deferred head (forward(defer_head=True))
         # the head's fc3/fc4/fc5 weight gradients as one grouped launch (gemm.hip
-        # dense_wgrad_group); MNISTX_GROUP_WGRAD=0 launches them one by one
-        self.group_head_wgrad = (self.head is not None and os.environ.get("MNISTX_GROUP_WGRAD", "1") != "0"
+        # dense_wgrad_group)
+        self.group_head_wgrad = (self.head is not None
                                  and all(l.Dp % 8 == 0 and l.Np % 8 == 0 for l in self.layers[self.head:]))
         self._group_S: Optional[list] = None
         self._head_grads = False                   # loss_and_grad already produced the head's dgrads
-        # LeNet-5: conv2's data gradient inside conv1's weight-gradient kernel
-        # (convpool.hip lenet_c2dgrad_c1wgrad_k), so dP1 never goes to HBM.  Opt-in
-        # (MNISTX_FUSE_C2D_C1W=1): at B=65536 it measures 290-309 us against 140 + 150 us
-        # for the two kernels it replaces (profiles/r2/fused_c2d_c1w.md) -- the pair is
-        # bound by LDS/VALU latency at 3 waves/SIMD, not by the 400 MB it saves.
-        self.fuse_c2d_c1w = self._find_c2d_c1w() and not self.overlap and \
-            os.environ.get("MNISTX_FUSE_C2D_C1W", "0") == "1"
         # reference CNN: norm1's backward runs in conv1's weight-gradient staging (reads
         # dL/d norm1 + pool1, no pool-level gradient in HBM, no lrn_bwd launch)
         self.fold_lrn = False
@@ -530,11 +495,10 @@ class HipNet:
                     self.fold_lrn = True
         # reference CNN: norm1's forward in conv2's input staging (LDS-halo fwd and weight-
         # gradient kernels read pool1 and normalise it; norm1 never written).  Opt-in
-        # (MNISTX_FOLD_LRN_FWD=1): the LRN math in both staging loops costs more than the
-        # 67 us lrn_fwd launch it removes (2.25-2.28 vs 2.22-2.24 ms/step, profiles/r2/README.md)
+        # (fold_lrn_fwd=True): the LRN math in both staging loops costs more than the 67 us
+        # lrn_fwd launch it removes (2.25-2.28 vs 2.22-2.24 ms/step, profiles/r2/README.md)
         self.fold_lrn_fwd = False
-        if (dev.type == "cuda" and os.environ.get("MNISTX_FOLD_LRN_FWD", "0") == "1"
-                and os.environ.get("MNISTX_CONV_HALO", "1") != "0"):
+        if dev.type == "cuda" and fold_lrn_fwd and os.environ.get("MNISTX_CONV_HALO", "1") != "0":
             for k in range(len(self.layers) - 1):
                 a, b = self.layers[k], self.layers[k + 1]
                 if (isinstance(a, LRNLayer) and isinstance(b, ConvLayer) and b.x is a.out and a.C == 32
@@ -550,16 +514,11 @@ class HipNet:
         # LeNet-5: the conv stack's whole backward (conv2 dgrad + both weight gradients) as ONE
         # kernel (lenet_bwd.hip): dP1 stays in LDS, the weight gradients accumulate in
         # registers per block; fused_lenet_bwd=False runs the three convpool kernels
-        self.fused_bwd = self.band_fwd and fused_lenet_bwd and not self.overlap and not self.fuse_c2d_c1w
+        self.fused_bwd = self.band_fwd and fused_lenet_bwd and not self.overlap
         if self.fused_bwd:
             res = kernels().lenet_bwd_blocks(batch)
             self.lb_slab1 = torch.zeros(res * 32 * 8, dtype=torch.float32, device=dev)
             self.lb_slab2 = torch.zeros(res * 208 * 16, dtype=torch.float32, device=dev)
-        if self.fuse_c2d_c1w:
-            l0, l1 = self.layers[0], self.layers[1]
-            l0.fused_grid = min(l0.grid, kernels().lenet_c2dgrad_c1wgrad_grid())
-            l0.fused_dgrad = (self.dbuf[2], l1)   # conv2's incoming gradient + its layer
-            l1.skip_dgrad = True
 
     def _find_c2d_c1w(self) -> bool:
         if self.device.type != "cuda" or len(self.layers) < 2:

@@ -66,9 +66,17 @@ def _check_step(dev, model, cin, B, defer_head=False, seed=0):
             l16, _ = torch_ref.forward(spec, p16, xs.float())
         ((F.cross_entropy(l16.float(), ys, reduction="none") * wts).sum() / B).backward()
     assert rel_err(logits, ref_logits) < 3e-2
+    # the HIP plan stores dlogits in bf16: the last layer's bias gradient (a column sum of
+    # dlogits, heavy cancellation at random init) carries that rounding -- its floor is the
+    # same sum over bf16-rounded oracle dlogits
+    dl = (F.softmax(ref_logits, 1) - F.one_hot(y.long(), 10).float()) / B
+    last_b = f"{spec.weights()[-1].name}/biases"
+    floor_last_b = rel_err(dl.to(torch.bfloat16).float().sum(0), dl.sum(0))
     for name in init:
         e = rel_err(net.fp.grad_view(name), p[name].grad)
         floor = rel_err(p16[name].grad, p[name].grad)
+        if name == last_b:
+            floor = max(floor, floor_last_b)
         assert e < max(3e-2, 3.0 * floor), f"{model} B={B} {name}: rel err {e:.3e} (bf16 floor {floor:.3e})"
     # fused update = w - lr * (g + wd w)
     before = {n: net.fp.param_view(n).clone() for n in init}
@@ -232,20 +240,20 @@ def test_lrn_pool_fusion_bitwise(dev, K):
     assert torch.equal(out[0][1], out[1][1])
 
 
-@pytest.mark.parametrize("B", [77, 512])
-def test_lenet_fused_c2dgrad_c1wgrad(dev, K, B, monkeypatch):
-    """conv2 dgrad inside conv1's weight-gradient kernel (dP1 never in HBM) vs the
-    two-kernel path: conv2 grads bitwise, conv1 grads to fp32 reassociation noise;
-    the fused kernel is bitwise reproducible run to run."""
+@pytest.mark.parametrize("B", [77, 1024])
+def test_lenet_fused_conv_backward_step(dev, K, B):
+    """The LeNet-5 conv stack's backward as one kernel (lenet_bwd.hip) vs the three
+    per-layer kernels, whole training step: every gradient to bf16 noise, the head's
+    bitwise (untouched), and the fused kernel bitwise reproducible run to run
+    (deterministic split-K, no atomics)."""
     spec = get_model("lenet5", 1)
     init = torch_ref.init_params(spec, seed=3)
     x = (torch.rand(B, 28, 28, 1, device=dev) - 0.5).to(torch.bfloat16)
     y = torch.randint(0, 10, (B,), device=dev, dtype=torch.int32)
 
-    def grads(fuse: str):
-        monkeypatch.setenv("MNISTX_FUSE_C2D_C1W", fuse)   # opt-in path (default off)
-        net = HipNet(spec, B, dev, init, OptConfig(lr0=0.05))
-        assert net.fuse_c2d_c1w == (fuse == "1")
+    def grads(fused: bool):
+        net = HipNet(spec, B, dev, init, OptConfig(lr0=0.05), fused_lenet_bwd=fused)
+        assert net.fused_bwd == fused
         net.x0.copy_(x)
         net.labels.copy_(y)
         net.forward(defer_head=True)
@@ -254,11 +262,11 @@ def test_lenet_fused_c2dgrad_c1wgrad(dev, K, B, monkeypatch):
         torch.cuda.synchronize()
         return {n: net.fp.grad_view(n).clone() for n in init}
 
-    ref, fused, again = grads("0"), grads("1"), grads("1")
+    ref, fused, again = grads(False), grads(True), grads(True)
     for n in init:
         assert torch.equal(fused[n], again[n]), f"{n}: fused kernel not reproducible"
-        if n.startswith("conv1/"):
-            assert rel_err(fused[n], ref[n]) < 1e-5, n
+        if n.startswith("conv"):
+            assert rel_err(fused[n], ref[n]) < 1e-2, (n, rel_err(fused[n], ref[n]))
         else:
             assert torch.equal(fused[n], ref[n]), n
 
@@ -278,8 +286,8 @@ def test_refcnn_lrn1_backward_fold(dev, K, cin, monkeypatch):
 
     def grads(fold: str):
         monkeypatch.setenv("MNISTX_FOLD_LRN", fold)
-        monkeypatch.setenv("MNISTX_FOLD_LRN_FWD", fold)   # opt-in forward fold, tested here too
-        net = HipNet(spec, B, dev, init, OptConfig(lr0=0.05))
+        # the opt-in forward fold, tested here too
+        net = HipNet(spec, B, dev, init, OptConfig(lr0=0.05), fold_lrn_fwd=fold == "1")
         assert net.fold_lrn == (fold == "1") and net.fold_lrn_fwd == (fold == "1")
         net.x0.copy_(x)
         net.labels.copy_(y)

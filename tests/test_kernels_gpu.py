@@ -523,8 +523,7 @@ def test_lrn_pool_matches_two_step(dev, K, N, H, W, C, relu):
 
 @pytest.mark.parametrize("src", ["bf16_idx", "u8_idx"])
 def test_lenet_conv1_wgrad_gathered_input(dev, K, src):
-    # runs whichever conv1 weight-gradient kernel the process selected (MNISTX_C1W_POOLK)
-    """LeNet conv1 weight gradient (lenet_c1wgrad.hip, pooled-K form) reading a resident
+    """LeNet conv1 weight gradient (convpool_wgrad_pair_k, the split backward path) reading a resident
     dataset through the batch index (bf16, or uint8 normalised in the kernel) == the fp32
     oracle on the gathered, normalised batch; several grids (images per block 1..n)."""
     torch.manual_seed(5)

@@ -40,7 +40,7 @@ def _oracle(x, P1, A1, A2, dP2, w2):
     g1 = dY1.permute(0, 3, 1, 2)
     dW1 = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (8, 1, 5, 5), g1, padding=2).permute(2, 3, 1, 0)
     db1 = _unpool(dP1, c1.long()).sum((0, 1, 2))                      # fp32 dP1 (the kernel's bias path)
-    return dW1[..., :6], db1[:6], dW2[:, :, :6, :], db2
+    return dW1[:, :, 0, :6], db1[:6], dW2[:, :, :6, :], db2
 
 
 def _fused(K, x, P1, A1, A2, dP2, w2, B, idx=None, xsrc=None):
@@ -81,6 +81,7 @@ def test_lenet_bwd_matches_oracle(dev, K, grid_cap, B, cap):
         assert got[4] == min(cap, (B + 7) // 8)
     want = _oracle(x, P1, A1, A2, dP2, w2)
     for name, g, w in zip(("dW1", "db1", "dW2", "db2"), got[:4], want):
+        assert g.shape == w.shape, (name, g.shape, w.shape)
         assert torch.isfinite(g).all(), name
         assert _rel(g, w) < 1e-2, f"{name}: rel err {_rel(g, w):.3e}"
 

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Time the fused LeNet-5 conv-stack backward (lenet_bwd.hip) alone at the BASELINE batch,
+against the three per-layer kernels it replaces, and print its per-phase clock split
+(s_memtime sums over all waves; the prof build of the same launch).
+
+    python bench/micro_lenet_bwd.py [B]
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+PHASES = ["stage_in", "dgrad", "c2_wgrad", "barrier1", "stage_dy2_p1", "c1_wgrad", "barrier2", "epilogue"]
+
+
+def main():
+    import torch
+    from distributed_tensorflow_ibm_mnist_amd.ops._ext import kernels
+    K = kernels()
+    dev = torch.device("cuda", 0)
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    torch.manual_seed(0)
+    n = 60000
+    ds = (torch.rand(n, 784, device=dev) - 0.5).to(torch.bfloat16)
+    idx = torch.randint(0, n, (B,), device=dev, dtype=torch.int64)
+    w1 = torch.zeros(5, 5, 1, 8, device=dev)
+    w1[..., :6] = torch.randn(5, 5, 1, 6, device=dev) / 5
+    w2 = torch.zeros(5, 5, 8, 16, device=dev)
+    w2[:, :, :6] = torch.randn(5, 5, 6, 16, device=dev) / 12
+    w1, w2 = w1.to(torch.bfloat16), w2.to(torch.bfloat16)
+    b1, b2 = torch.randn(6, device=dev) * 0.1, torch.randn(16, device=dev) * 0.1
+    P1 = torch.empty(B, 14, 14, 8, dtype=torch.bfloat16, device=dev)
+    A1 = torch.empty(B, 14, 14, 4, dtype=torch.uint8, device=dev)
+    P2 = torch.empty(B, 5, 5, 16, dtype=torch.bfloat16, device=dev)
+    A2 = torch.empty(B, 5, 5, 16, dtype=torch.uint8, device=dev)
+    K.lenet_band_fwd(ds, w1, b1, 6, w2, b2, B, P2, A2, p1=P1, arg1=A1, idx=idx)
+    dP2 = (torch.randn(B, 400, device=dev) * 1e-3).to(torch.bfloat16)
+    grid = K.lenet_bwd_blocks(B)
+    s1 = torch.zeros(grid * 32 * 8, device=dev)
+    s2 = torch.zeros(grid * 208 * 16, device=dev)
+
+    def timeit(f, iters=30):
+        for _ in range(5):
+            f()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            f()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / iters * 1e3
+
+    fused = timeit(lambda: K.lenet_bwd(ds, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx))
+    # the split path: conv2 dgrad -> dP1 in HBM, conv2 / conv1 weight gradients
+    dP1 = torch.empty(B, 14, 14, 8, dtype=torch.bfloat16, device=dev)
+    g2 = K.convpool_wgrad_grid(8, 16, 5, 0, 14, 14)
+    g1 = K.convpool_wgrad_grid(1, 8, 5, 2, 28, 28)
+    sl2 = torch.zeros(g2 * K.convpool_rows(8, 16, 5, 0, 14, 14) * 16, device=dev)
+    sl1 = torch.zeros(g1 * K.convpool_rows(1, 8, 5, 2, 28, 28) * 8, device=dev)
+    dgr = timeit(lambda: K.convpool_dgrad(dP2.view(B, 5, 5, 16), A2, w2, dP1, B, 8, 16, 5, 0, 14, 14))
+    w2g = timeit(lambda: K.convpool_wgrad(P1, dP2.view(B, 5, 5, 16), A2, sl2, g2, B, 8, 16, 5, 0, 14, 14))
+    w1g = timeit(lambda: K.convpool_wgrad(ds, dP1, A1, sl1, g1, B, 1, 8, 5, 2, 28, 28, idx=idx))
+    prof = torch.zeros(8, dtype=torch.int64, device=dev)
+    K.lenet_bwd(ds, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx, prof=prof)
+    torch.cuda.synchronize()
+    pr = prof.tolist()
+    tot = max(1, sum(pr))
+    print(json.dumps({"B": B, "grid": grid, "fused_us": round(fused, 1),
+                      "split_us": {"c2_dgrad": round(dgr, 1), "c2_wgrad": round(w2g, 1), "c1_wgrad": round(w1g, 1),
+                                   "sum": round(dgr + w2g + w1g, 1)},
+                      "phase_share": {k: round(v / tot, 3) for k, v in zip(PHASES, pr)}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -794,7 +794,7 @@ void lenet_band_fwd(Tensor x, Tensor w1, Tensor b1, int64_t b1n, Tensor w2, Tens
 // gradients; x as for lenet_band_fwd (the forward's input), p1 / arg1 / arg2 from it, dp2 =
 // dL/d pool2 [B, 400].  slab1 [grid, 32, 8], slab2 [grid, 208, 16] (split-K partials).
 void lenet_bwd(Tensor x, Tensor p1, Tensor arg1, Tensor dp2, Tensor arg2, Tensor w2, int64_t B, Tensor slab1,
-               Tensor slab2, int64_t grid, optional<Tensor> idx) {
+               Tensor slab2, int64_t grid, optional<Tensor> idx, optional<Tensor> prof) {
   mnistx::XSrc src{nullptr, nullptr, nullptr, 0};
   if (x.scalar_type() == at::kByte) {
     check(x, at::kByte, 784, "x");
@@ -829,8 +829,13 @@ void lenet_bwd(Tensor x, Tensor p1, Tensor arg1, Tensor dp2, Tensor arg2, Tensor
   TORCH_CHECK(grid >= 1 && grid <= res, "lenet_bwd: grid must be in [1, ", res, "] (one block per CU, <= tiles)");
   check(slab1, at::kFloat, grid * 32 * 8, "slab1");
   check(slab2, at::kFloat, grid * 208 * 16, "slab2");
+  unsigned long long* pr = nullptr;
+  if (prof.has_value() && prof->defined()) {
+    check(*prof, at::kLong, 8, "prof");
+    pr = P<unsigned long long>(*prof);
+  }
   hip_ok(mnistx::lenet_bwd(src, BF(p1), P<const uint8_t>(arg1), BF(dp2), P<const uint8_t>(arg2), BF(w2), (int)B,
-                           P<float>(slab1), P<float>(slab2), (int)grid, cur_stream()),
+                           P<float>(slab1), P<float>(slab2), (int)grid, cur_stream(), pr),
          "lenet_bwd");
 }
 
@@ -1110,7 +1115,8 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("w2"), py::arg("b2"), py::arg("B"), py::arg("p2"), py::arg("arg2"), py::arg("p1") = py::none(),
         py::arg("arg1") = py::none(), py::arg("idx") = py::none(), py::arg("prof") = py::none());
   m.def("lenet_bwd", &lenet_bwd, py::arg("x"), py::arg("p1"), py::arg("arg1"), py::arg("dp2"), py::arg("arg2"),
-        py::arg("w2"), py::arg("B"), py::arg("slab1"), py::arg("slab2"), py::arg("grid"), py::arg("idx") = py::none());
+        py::arg("w2"), py::arg("B"), py::arg("slab1"), py::arg("slab2"), py::arg("grid"), py::arg("idx") = py::none(),
+        py::arg("prof") = py::none());
   m.def("lenet_bwd_blocks", [](int64_t B) {
     const int n = mnistx::lenet_bwd_blocks((int)B);
     TORCH_CHECK(n > 0, "lenet_bwd_blocks: occupancy query failed");

@@ -113,7 +113,8 @@ hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const b
 // (rows tap * 8 + ci, bias 200) -- the split-K partials splitk_reduce combines
 int lenet_bwd_blocks(int B);         // the grid for a batch (one block per CU, <= tiles); <= 0: error
 hipError_t lenet_bwd(const XSrc& x, const bf16_t* p1, const uint8_t* arg1, const bf16_t* dp2, const uint8_t* arg2,
-                     const bf16_t* w2, int B, float* slab1, float* slab2, int grid, hipStream_t st);
+                     const bf16_t* w2, int B, float* slab1, float* slab2, int grid, hipStream_t st,
+                     unsigned long long* prof = nullptr);
 
 // ---- lenet_band.hip: LeNet-5 conv1+pool1+conv2+pool2 forward on banded MFMA tiles
 // (one persistent kernel; bf16 images only).  x.x = [n][784] images (x.idx: per-sample

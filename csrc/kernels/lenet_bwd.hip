@@ -103,7 +103,11 @@ struct BwdArgs {
   int B;
   float* slab1;           // [grid][32][8]: rows tap 0..24, 25 = bias
   float* slab2;           // [grid][208][16]: rows tap * 8 + ci, 200 = bias
+  unsigned long long* prof;   // optional (experiments): per-phase clock sums [NPROF] over all waves
 };
+// phase clocks (s_memtime): 0 stage-in (X / codes + next-tile loads issue), 1 dgrad, 2 conv2
+// wgrad, 3 barrier 1, 4 stage dY2 / pool1, 5 conv1 wgrad, 6 barrier 2 (loop top), 7 epilogue
+constexpr int NPROF = 8;
 
 // ------------------------------------------------------------------ staging (global -> regs -> LDS)
 constexpr int NCH = (T * NWIN1 + NT - 1) / NT;   // 4: pool1 / input / code chunks per thread
@@ -241,11 +245,22 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
   const uint32_t dsel = (uint32_t)(i16 >> 3);
   const auto rarg1 = buf_rsrc(a.arg1, (uint32_t)a.B * (NWIN1 * 4u));
 
+  uint64_t pc_acc[NPROF] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tclk = __builtin_amdgcn_s_memtime();
+  auto mark = [&](int ph) {
+    if (a.prof) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      pc_acc[ph] += t - tclk;
+      tclk = t;
+    }
+  };
   for (int k = 0; k < nk; ++k) {
     const int t0 = tile0(k);
     __syncthreads();   // dY2 / pool1 of this tile stored; the previous conv1 phase is done
+    mark(6);
     st.store_x_codes(lds, tid, a.u8 != nullptr);
     st.load(a, k + 1 < nk ? tile0(k + 1) : -1, tid);
+    mark(0);
 
     // ================================================ phase 1a: conv2 dgrad, one output row pair
     const int pr = dg_row[wave];
@@ -290,6 +305,7 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
       }
     }
 
+    mark(1);
     // ================================================ phase 1b: conv2 weight gradient k-steps
     {
       const int s0 = c2_ks0[wave], s1 = c2_ks1[wave];
@@ -326,8 +342,11 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
       }
     }
 
+    mark(2);
     __syncthreads();   // dP1, input and codes of this tile visible; dY2 / pool1 no longer read
+    mark(3);
     if (k + 1 < nk) st.store_dy2_p1(lds, tid);
+    mark(4);
 
     // ================================================ phase 2: conv1 weight gradient
     const int sig = half;
@@ -363,10 +382,12 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
         acc1[t][1] = mfma16(Af, Bm[1], acc1[t][1]);
       }
     }
+    mark(5);
   }
 
   // ---- epilogue: the 8 waves' partials -> this block's slab rows (fixed summation order)
   __syncthreads();
+  mark(6);
   // conv2: tile T of wave w = half(w) * 7 + t; partials [wave][t][col 16][row 16]
   float* e2 = (float*)lds;
 #pragma unroll
@@ -418,6 +439,11 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
     }
     s1[tap * 8 + c] = v;
   }
+  if (a.prof) {
+    mark(7);
+    if (lane == 0)
+      for (int i = 0; i < NPROF; ++i) atomicAdd(a.prof + i, (unsigned long long)pc_acc[i]);
+  }
 }
 
 }  // namespace
@@ -438,12 +464,13 @@ int lenet_bwd_grid() {
 }
 
 hipError_t lenet_bwd(const XSrc& x, const bf16_t* p1, const uint8_t* arg1, const bf16_t* dp2, const uint8_t* arg2,
-                     const bf16_t* w2, int B, float* slab1, float* slab2, int grid, hipStream_t st) {
+                     const bf16_t* w2, int B, float* slab1, float* slab2, int grid, hipStream_t st,
+                     unsigned long long* prof) {
   if (B <= 0) return hipSuccess;
   if ((!x.x && !x.u8) || grid <= 0) return hipErrorInvalidValue;
   const int res = lenet_bwd_grid();
   if (res <= 0) return hipErrorInvalidValue;
-  BwdArgs a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, p1, arg1, dp2, arg2, w2, B, slab1, slab2};
+  BwdArgs a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, p1, arg1, dp2, arg2, w2, B, slab1, slab2, prof};
   hipLaunchKernelGGL(lenet_bwd_k, dim3(grid), dim3(NT), LDS_BYTES, st, a);
   return hipGetLastError();
 }

@@ -10,6 +10,7 @@
 #   bench[:NAME]        python bench.py ARGS (NAME.json; ARGS from $BENCH_ARGS_<NAME> or none)
 #   prof[:NAME]         rocprofv3 kernel trace of a bench config -> NAME/kernels.md
 #   pmc[:NAME]          PMC passes (bench/pmc.sh) of a bench config -> NAME/pmc.md
+#   py:SCRIPT           python bench/SCRIPT.py (args from $ARGS_SCRIPT) -> SCRIPT.txt, 300 s limit
 # Every step runs under its own timeout; the first failure ends the call (no retries).
 # Per-step bench arguments: export ARGS_<NAME>="--model reference_cnn --batch 16384" before
 # the call (NAME defaults to the step kind).
@@ -42,6 +43,9 @@ for step in "$@"; do
     pmc)
       bash bench/pmc.sh ${OUT#gpurun_out/}/$name -- $args || exit 1
       python3 bench/pmc_summary.py $OUT/$name $OUT/$name/pmc.md > /dev/null 2>&1; head -30 $OUT/$name/pmc.md ;;
+    py)
+      timeout -k 10 300 python -u bench/$name.py $args > $OUT/$name.txt 2>&1 || { tail -8 $OUT/$name.txt; exit 1; }
+      tail -n 5 $OUT/$name.txt ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

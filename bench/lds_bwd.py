@@ -48,20 +48,24 @@ def cycles(addrs, nbytes, kind):
     return tot / len(groups)
 
 
-def kperm(g, rho, q):
-    """Item (pixel / window) of MFMA K row 8g + 4rho + q inside a 32-item k-step: the 8
-    rows one 32-lane half reads in one transposed read are 8 CONSECUTIVE items."""
-    return 16 * (g >> 1) + 8 * rho + 4 * (g & 1) + q
+def kitem(g, rho, q):
+    """(image, pixel / window offset) of MFMA K row 8g + 4rho + q inside a 32-item k-step:
+    items are enumerated image-fastest, so the 32 lanes of one transposed read (fixed g >> 1
+    and rho) cover the 8 images of one pixel."""
+    return 4 * (g & 1) + q, 2 * (g >> 1) + rho
 
 
-DEF = dict(DY2_IMG=3872, DY2_RS=320, P1_IMG=3152, X_IMG=2560, X_RS=80, DP1_IMG=3152, IMGMAP=0)
+DEF = dict(DY2_IMG=4640, DY2_RS=384, P1_IMG=3168, DP1_IMG=3152, X_IMG=2592, X_RS=80)
+# conv2 weight-gradient tiles: tap pairs (25 = the bias row, a broadcast ONES cell)
+C2_TAPS = [(0, 1), (2, 3), (5, 6), (7, 8), (10, 11), (12, 13), (4, 9),
+           (15, 16), (17, 18), (14, 19), (20, 21), (22, 23), (24, 25)]
 
 
 def dgrad_b(S, dy=1, p=2, v=2):
     out = []
     for l in range(64):
         i, g = l & 15, l >> 4
-        img, rr = (i & 7, i >> 3) if S["IMGMAP"] == 0 else (i >> 1, i & 1)
+        img, rr = i >> 1, i & 1
         y = 2 * p + rr - dy
         x = 2 * v + (g >> 1)
         out.append(img * S["DY2_IMG"] + (y + 1) * S["DY2_RS"] + x * 32 + 16 * (g & 1))
@@ -72,28 +76,25 @@ def dgrad_w(S, p=2, u=3):
     out = []
     for l in range(64):
         i, g = l & 15, l >> 4
-        img, rr = (i & 7, i >> 3) if S["IMGMAP"] == 0 else (i >> 1, i & 1)
+        img, rr = i >> 1, i & 1
         xq = 2 * u + (g >> 1)
         out.append(img * S["DP1_IMG"] + ((2 * p + rr) * 14 + xq) * 16 + 8 * (g & 1))
     return cycles(out, 8, "w64")
 
 
 def c2w(S, s, rho, t):
-    """(A p1 tr read of M-tile t, B dY2 tr read) addresses of k-step s, read rho."""
-    taps = [((0, t), (1, t)) if t < 5 else ((2, t - 5), (3, t - 5)) if t < 10 else ((4, 2 * (t - 10)), (4, 2 * (t - 10) + 1))
-            for t in range(13)]
+    """(A pool1 tr read of M-tile t, B dY2 tr read) of k-step s, read rho."""
     a, b = [], []
     for l in range(64):
         g, q, p = l >> 4, (l >> 2) & 3, l & 3
-        k = 32 * s + kperm(g, rho, q)
-        img, pix = k // 100, k % 100
+        img, sub = kitem(g, rho, q)
+        pix = 4 * s + sub
         y, x = pix // 10, pix % 10
-        (dy0, dx0), (dy1, dx1) = taps[t]
-        dy, dx = (dy0, dx0) if p < 2 else (dy1, dx1)
-        if t == 12 and p >= 2:
+        tap = C2_TAPS[t][p >> 1]
+        if tap == 25:
             a.append(100000 + 8 * (p & 1))     # ONES cell
         else:
-            a.append(img * S["P1_IMG"] + ((y + dy) * 14 + x + dx) * 16 + 8 * (p & 1))
+            a.append(img * S["P1_IMG"] + ((y + tap // 5) * 14 + x + tap % 5) * 16 + 8 * (p & 1))
         b.append(img * S["DY2_IMG"] + (y + 1) * S["DY2_RS"] + x * 32 + 8 * p)
     return cycles(a, 8, "tr"), cycles(b, 8, "tr")
 
@@ -102,10 +103,9 @@ def c1w(S, sig, s, rho, t=0):
     a, b = [], []
     for l in range(64):
         g, q, p = l >> 4, (l >> 2) & 3, l & 3
-        k = 32 * s + kperm(g, rho, q)
-        k = min(k, 783)
-        img, r = k // 98, k % 98
-        yp, xi = r // 7, r % 7
+        img, sub = kitem(g, rho, q)
+        tw = min(4 * s + sub, 97)
+        yp, xi = tw // 7, tw % 7
         xp = 2 * xi + sig
         a.append(img * S["X_IMG"] + (2 * yp + 2 * t + (p >> 1)) * S["X_RS"] + (4 * xi + 4 * (p & 1) + 4 * sig) * 2)
         b.append(img * S["DP1_IMG"] + (yp * 14 + xp) * 16 + 8 * (p & 1))
@@ -132,10 +132,11 @@ def report(S):
     for sig in range(2):
         for s in range(25):
             for rho in range(2):
-                x, y = c1w(S, sig, s, rho)
-                ca += x
-                cb += y
-                n += 1
+                for t in range(3):
+                    x, y = c1w(S, sig, s, rho, t)
+                    ca += x
+                    cb += y
+                    n += 1
     r["c1w_A_tr"] = ca / n
     r["c1w_B_tr"] = cb / n
     return r
@@ -150,10 +151,10 @@ def main():
     if "--search" in sys.argv:
         best = {}
         for name, keys, cands in [
-                ("dY2", ["DY2_IMG"], [3840 + 16 * i for i in range(0, 32)]),
+                ("dY2", ["DY2_IMG"], [4608 + 16 * i for i in range(0, 32)]),
                 ("p1", ["P1_IMG"], [3136 + 16 * i for i in range(0, 32)]),
                 ("X", ["X_IMG", "X_RS"], [(xi, xr) for xr in (72, 80, 88, 96, 104) for xi in range(32 * xr, 32 * xr + 512, 16)]),
-                ("dP1", ["DP1_IMG"], [3136 + 16 * i for i in range(0, 32)])]:
+                ]:
             res = []
             for c in cands:
                 T = dict(S)
@@ -163,7 +164,7 @@ def main():
                     T.update(dict(zip(keys, c)))
                 rr = report(T)
                 key = {"dY2": rr["dgrad_B_b128"] + rr["c2w_B_tr"], "p1": rr["c2w_A_tr"],
-                       "X": rr["c1w_A_tr"], "dP1": rr["c1w_B_tr"] + rr["dgrad_W_w64"] / 2}[name]
+                       "X": rr["c1w_A_tr"]}[name]
                 res.append((key, c))
             res.sort()
             print(name, res[:5])

@@ -21,7 +21,8 @@
 //    units (column pairs 0-3: 9 MFMAs per kernel row, 4-6: 6).
 //  * conv2 weight gradient: rows = (2 taps, ci 8), columns = co 16, K = 32 (pixel, image)
 //    items; both operands are ds_read_b64_tr_b16 transposed reads of the NHWC tiles (one
-//    per lane: 4 channels of one pixel); bias = a constant ones row in one tile.
+//    per lane: 4 channels of one pixel).  The bias needs no tile of its own: pool1 channel 6
+//    (zero in HBM) is staged as 1.0, so row (tap 0, ci 6) sums dY2.
 //  * conv1 weight gradient, by pool-window phase: with dY1 = dP1 at the window position
 //    d = 2a + b of each (window, channel)'s argmax, dW1[dy][dx][c] =
 //    sum_d sum_w X[2yp+a+dy-2][2xp+b+dx-2] dP1[w][c] [code(w,c) == d], i.e. one GEMM
@@ -29,19 +30,19 @@
 //    the end.  A = input patches at (2yp + ty - 2, 2xp + tx - 2): a transposed read of 4
 //    consecutive input pixels per lane (8-byte aligned because windows are taken by x
 //    parity: even-xp windows cover tx -2..5, odd ones 0..7 -- two accumulator sets);
-//    B = dP1 masked by the argmax code (VALU: code == d per column).
-//  * Weight-gradient K items are enumerated image-fastest (item = 8 * pixel + image), so a
-//    lane's image is a lane constant and its pixel a wave-uniform step plus one lane bit
-//    (a few VALU of index decode), and the 32 lanes of one transposed read cover the 8
-//    images of one pixel: with the image strides below every read is conflict-free
-//    (bench/lds_bwd.py; the conv2 tiles pair taps whose dx differ by an odd amount).
-// 16 waves (4 per SIMD) share a tile in two phases (two barriers): [store X / codes of
-// this tile, prefetch the next tile, one dgrad unit + conv2 weight-gradient k-steps of the
-// wave's tile group] -> [store dY2 / pool1 of the next tile, conv1 weight-gradient k-steps
-// of the wave's parity set].  The accumulators are split (a wave holds at most 4 conv2
-// tiles and one conv1 set: 40 registers) so the kernel fits 128 VGPRs.
-#include <type_traits>
-
+//    B = dP1 masked by the argmax code (3 packed-u16 VALU per 2 columns).
+//  * Weight-gradient K items are enumerated image-fastest (item = 8 * pixel + image) over
+//    rows padded to a multiple of 4 pixels (dY2: 12, window sets: 8; the pad reads zeros),
+//    so a k-step is one row segment: every lane address is a per-lane base plus a
+//    wave-uniform step offset (one VALU add per operand per k-step, no index decode), the
+//    32 lanes of one transposed read cover the 8 images of one pixel, and with the image
+//    strides below the reads are conflict-free (bench/lds_bwd.py; conv2 tiles pair taps one
+//    pixel apart, except three pairs one row apart: 2-way).
+// 16 waves (4 per SIMD) share a tile in two phases (two barriers): [store input / codes of
+// this tile, load the next tile's input, one dgrad unit + conv2 weight-gradient k-steps of
+// the wave's tile group] -> [load the next tile's dY2 / pool1, conv1 weight-gradient k-steps
+// of the wave's parity set, store dY2 / pool1].  The accumulators are split (a wave holds at
+// most 4 conv2 tiles and one conv1 set: 40 registers) so the kernel fits 128 VGPRs.
 #include "common.h"
 #include "launchers.h"
 
@@ -56,51 +57,49 @@ constexpr int NWIN1 = 196;                                 // pool1 windows per 
 constexpr int AF_OFF = 0, AF_SZ = 15 * 64 * 16;            // dgrad A fragments [dy*3+j][lane] x 16 B
 constexpr int DY2_RS = 384, DY2_IMG = 4640;                // dY2 [img][row -1..10][12 px][16 co] bf16
 constexpr int DY2_OFF = AF_OFF + AF_SZ, DY2_SZ = T * DY2_IMG;
-constexpr int P1_IMG = 3168;                               // pool1 [img][196][8] bf16
+constexpr int P1_RS = 256, P1_IMG = 3616;                  // pool1 [img][14][16 px][8] bf16 (px 14, 15 zero)
 constexpr int P1_OFF = DY2_OFF + DY2_SZ, P1_SZ = T * P1_IMG;
-constexpr int DP1_IMG = 3152;                              // dP1 / codes [img][196][8] x 2 B
 constexpr int X_RS = 80, X_IMG = 2592;                     // input [img][row -2..29][col -4..35] bf16
 constexpr int X_OFF = P1_OFF + P1_SZ, X_SZ = T * X_IMG;
-constexpr int DP1_OFF = X_OFF + X_SZ, DP1_SZ = T * DP1_IMG;
-constexpr int CD_OFF = DP1_OFF + DP1_SZ;                   // argmax codes (u16 per channel)
-constexpr int ZERO_OFF = CD_OFF + DP1_SZ;                   // 16 zero bytes (padded conv1 K)
-constexpr int ONES_OFF = ZERO_OFF + 16;                    // bf16 {1, 0 x 7}: conv2 bias row
-constexpr int LDS_BYTES = ONES_OFF + 16;
+constexpr int D_RS = 272, D_IMG = 3808;                    // dP1 / codes [img][14][17 windows][8] x 2 B
+constexpr int DP1_OFF = X_OFF + X_SZ, D_SZ = T * D_IMG;
+constexpr int CD_OFF = DP1_OFF + D_SZ;                     // argmax codes (u16 per channel)
+constexpr int LDS_BYTES = CD_OFF + D_SZ;
 static_assert(LDS_BYTES <= 163840, "one workgroup per CU");
-static_assert(12 * DY2_RS <= DY2_IMG && 32 * X_RS <= X_IMG && NWIN1 * 16 <= DP1_IMG && DP1_IMG <= P1_IMG, "");
-// epilogue scratch (aliases the tiles once the loop is done)
+static_assert(12 * DY2_RS <= DY2_IMG && 32 * X_RS <= X_IMG && 14 * P1_RS <= P1_IMG && 14 * D_RS <= D_IMG, "");
 constexpr int C2MAX = 4;                                   // conv2 tiles per wave group (max)
-static_assert(NW * C2MAX * 256 * 4 <= LDS_BYTES && NW * 6 * 256 * 4 + NW * 64 * 16 <= LDS_BYTES, "");
+static_assert(NW * C2MAX * 256 * 4 <= LDS_BYTES && NW * 6 * 256 * 4 + NW * 8 * 4 <= LDS_BYTES, "epilogue scratch");
 
-// conv2 weight-gradient M tiles: rows h * 8 + ci are tap c2_taps[t][h] (25 = the bias row,
-// read from the ONES cell).  Taps are paired with an odd dx difference, so the two taps'
-// pool1 reads of a pixel land in disjoint banks (only tiles 6 and 9, in different groups, pair
-// even offsets).
-// Tile groups: waves 4G .. 4G + 3 own tiles c2g(G) .. c2g(G + 1) - 1.
-__constant__ int c2_taps[13][2] = {{0, 1},   {2, 3},   {5, 6},   {7, 8},   {10, 11}, {12, 13}, {4, 9},
-                                   {15, 16}, {17, 18}, {14, 19}, {20, 21}, {22, 23}, {24, 25}};
-DEV int c2g(int G) { return G == 0 ? 0 : 3 * G + 1; }   // 0, 4, 7, 10, 13
+// conv2 weight-gradient M tiles: rows h * 8 + ci are tap C2_TAP0[t] + h (tiles 0-9: taps one
+// pixel apart) or C2_TAP0[t] + 5 h (tiles 10-12: one row apart; tap 29 = discarded rows).
+// Tile groups: waves 4G .. 4G + 3 own the tiles of group G (G0: 0-3, G1: 4, 5, 10, G2: 6, 7,
+// 11, G3: 8, 9, 12 -- the row-apart pairs, whose reads are 2-way bank conflicted, spread).
+constexpr int C2_TAP0[13] = {0, 2, 5, 7, 10, 12, 15, 17, 20, 22, 4, 14, 24};
+constexpr int C2_GT[4][C2MAX] = {{0, 1, 2, 3}, {4, 5, 10, -1}, {6, 7, 11, -1}, {8, 9, 12, -1}};
+__constant__ int c2_gt[4][C2MAX] = {{0, 1, 2, 3}, {4, 5, 10, -1}, {6, 7, 11, -1}, {8, 9, 12, -1}};
+__constant__ int c2_tap0[13] = {0, 2, 5, 7, 10, 12, 15, 17, 20, 22, 4, 14, 24};
 
-// 0xffff in each 16-bit half of e that equals d, else 0
-DEV uint32_t heq(uint32_t e, uint32_t d) {
-  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-  const u16x2 x = __builtin_bit_cast(u16x2, e ^ (d * 0x00010001u));
+// packed u16: dv where the code half equals d, else 0 (3 VALU: xor, saturating 1 - x, mul)
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+DEV uint32_t sel_eq(uint32_t dv, uint32_t codes, uint32_t dd) {
+  const u16x2 x = __builtin_bit_cast(u16x2, codes ^ dd);
   const u16x2 one = {1, 1};
-  return __builtin_bit_cast(uint32_t, (u16x2)(__builtin_elementwise_min(x, one) - one));
+  const u16x2 m = __builtin_elementwise_sub_sat(one, x);
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, dv) * m);
 }
 // bytes b0, b1 of w -> u16 pair (b0 | b1 << 16)
 DEV uint32_t bytes01(uint32_t w) { return (w & 0xffu) | ((w & 0xff00u) << 8); }
 DEV uint32_t bytes23(uint32_t w) { return ((w >> 16) & 0xffu) | ((w >> 8) & 0xff0000u); }
 DEV bf16x8 frag(s16x4 lo, s16x4 hi) { return join(lo, hi); }
+DEV s16x4 tr4(const uint8_t* lds, int off) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + off)); }
 // the lane id, re-read where it is needed: per-lane addressing constants derived from it are
 // recomputed each tile (a few VALU) instead of being hoisted out of the tile loop, where they
-// would pin ~30 registers of a kernel that must fit 128
+// would pin registers of a kernel that must fit 128
 DEV int lane_now() {
   int l;
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
   return l;
 }
-DEV s16x4 tr4(const uint8_t* lds, int off) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + off)); }
 
 struct BwdArgs {
   const bf16_t* x;        // input images [n][784] bf16 (or null with u8)
@@ -118,65 +117,68 @@ struct BwdArgs {
   unsigned long long* prof;   // optional (experiments): per-phase clock sums [NPROF] over all waves
 };
 // phase clocks (s_memtime): 0 store input / codes, 1 dgrad (+ next-tile input loads), 2 conv2
-// wgrad, 3 barrier 1, 4 next-tile dY2 / pool1 loads issue, 5 conv1 wgrad + dY2 store, 6 barrier 2
-// (loop top), 7 epilogue
+// wgrad, 3 barrier 1, 4 next-tile dY2 / pool1 loads issue, 5 conv1 wgrad + dY2 / pool1 store,
+// 6 barrier 2 (loop top), 7 epilogue
 constexpr int NPROF = 8;
 
 // ------------------------------------------------------------------ staging (global -> regs -> LDS)
-// dL/dpool2 + codes and pool1 are loaded during phase 2 and stored (dY2 unpooled) at its end;
-// the input + pool1 codes are loaded during phase 1 and stored at the next loop top.  (Pool1
-// by LDS-DMA instead: the compiler then waits for the DMA before every LDS read of phase 2.)
-constexpr int NCH = (T * NWIN1 + NT - 1) / NT;   // 2: input / code chunks per thread
-// U8: the input is the uint8 dataset (normalised while staging); IDX: read through the
-// batch index (its rows are loaded one tile ahead of the input they address, so no load
-// waits on another)
+// Input, pool1 and codes: wave pair 2i stages image i, lane r of the pair windows / input
+// quads r and r + 128 (< 196), so a wave's image and dataset row are wave-uniform (the
+// batch-index entry is one uniform load, a tile ahead of the input it addresses).
+// dL/dpool2 + codes: threads < 400, one pooled pixel (8 channels) each.  The input +
+// pool1 codes are loaded during phase 1 and stored at the next loop top; dY2 + pool1 are
+// loaded during phase 2 and stored at its end.
+constexpr int NCH = 2;
+static_assert(NW == 2 * T && 2 * 128 >= NWIN1 && 128 <= NWIN1, "staging: one wave pair per image, 2 chunks");
 template <bool U8, bool IDX>
 struct Stage {
-  u32x4 dp;               // dL/dpool2: 8 channels of one pooled pixel (threads < 400)
-  u32x2 c2;               // their argmax codes
   u32x2 x[NCH];           // input: 4 pixels per chunk (uint8: x[i][0])
   uint32_t a1[NCH];       // pool1 argmax word per chunk
-  u32x2 rows[NCH];        // IDX: batch-index entries of the chunks' images, one tile ahead
+  u32x2 rowv;             // IDX: the batch-index entry of this wave's image, one tile ahead
+  u32x4 dp;               // dL/dpool2: 8 channels of one pooled pixel (threads < 400)
+  u32x2 c2;               // their argmax codes
   u32x4 p1[NCH];          // pool1: one window (8 channels) per chunk
 
-  DEV void load_rows(const BwdArgs& a, int t0, int tid) {
+  DEV static int img_of(int wave) { return wave >> 1; }
+  DEV void load_row(const BwdArgs& a, int t0, int wave) {
     if constexpr (IDX) {
-      const int nimg = t0 < 0 ? 0 : min(T, a.B - t0);
-      const auto ridx = buf_rsrc(a.idx + (t0 < 0 ? 0 : t0), (uint32_t)nimg * 8u);
-#pragma unroll
-      for (int i = 0; i < NCH; ++i) rows[i] = buf_b64(ridx, 8u * (uint32_t)((tid + NT * i) / NWIN1));
+      const int img = img_of(wave);
+      const bool ok = t0 >= 0 && t0 + img < a.B;
+      const auto ridx = buf_rsrc(a.idx + (ok ? t0 + img : 0), ok ? 8u : 0u);
+      rowv = buf_b64(ridx, 0u);
     }
   }
-  DEV void load_xc(const BwdArgs& a, int t0, int tid) {
-    const int nimg = t0 < 0 ? 0 : min(T, a.B - t0);
-    const int tb = t0 < 0 ? 0 : t0;
-    const auto ra1 = buf_rsrc(a.arg1 + (int64_t)tb * NWIN1 * 4, (uint32_t)nimg * (NWIN1 * 4u));
+  DEV void load_xc(const BwdArgs& a, int t0, int wave, int ln) {
+    const int img = img_of(wave);
+    const bool ok = t0 >= 0 && t0 + img < a.B;
+    int row = ok ? t0 + img : 0;
+    if constexpr (IDX) {
+      const uint32_t lo = __builtin_amdgcn_readfirstlane(rowv[0]), hi = __builtin_amdgcn_readfirstlane(rowv[1]);
+      row = (hi != 0u || (int)lo < 0) ? 0 : ((int)lo >= a.n ? a.n - 1 : (int)lo);
+    }
     constexpr uint32_t esz = U8 ? 1u : 2u;
-    const auto rx = U8 ? buf_rsrc(a.u8, (uint32_t)a.n * 784u) : buf_rsrc(a.x, (uint32_t)a.n * 1568u);
+    const void* xb = U8 ? (const void*)(a.u8 + (int64_t)row * 784) : (const void*)(a.x + (int64_t)row * 784);
+    const auto rx = buf_rsrc(xb, ok ? 784u * esz : 0u);
+    const auto ra1 = buf_rsrc(a.arg1 + (int64_t)(ok ? t0 + img : 0) * NWIN1 * 4, ok ? NWIN1 * 4u : 0u);
+    const int r = ln + 64 * (wave & 1);
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int e = tid + NT * i;
-      const uint32_t ok = e < T * NWIN1 ? 0u : BUF_OOB;
-      a1[i] = buf_b32(ra1, 4u * e + ok);
-      const int img = e / NWIN1, r = e - img * NWIN1;
-      int row = tb + img;
-      if constexpr (IDX) {
-        row = (int)rows[i][0];
-        row = (rows[i][1] != 0u || row < 0) ? 0 : (row >= a.n ? a.n - 1 : row);
-      }
-      const uint32_t xo = (e < T * NWIN1 && img < nimg) ? (uint32_t)row * (784u * esz) + (uint32_t)r * 4u * esz
-                                                        : BUF_OOB;
-      if constexpr (U8) x[i] = u32x2{buf_b32(rx, xo), 0u};
-      else x[i] = buf_b64(rx, xo);
+      const uint32_t q = (uint32_t)(r + 128 * i);
+      const uint32_t oob = q < NWIN1 ? 0u : BUF_OOB;
+      a1[i] = buf_b32(ra1, 4u * q + oob);
+      if constexpr (U8) x[i] = u32x2{buf_b32(rx, 4u * q + oob), 0u};
+      else x[i] = buf_b64(rx, 8u * q + oob);
     }
   }
-  // input chunks + argmax codes (read by the conv1 weight gradient)
-  DEV void store_xc(uint8_t* lds, int tid) const {
+  // input quads + argmax codes (read by the conv1 weight gradient)
+  DEV void store_xc(uint8_t* lds, int wave, int ln) const {
+    const int img = img_of(wave), r = ln + 64 * (wave & 1);
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int e = tid + NT * i;
-      if (e < T * NWIN1) {
-        const int img = e / NWIN1, r = e - img * NWIN1, y = r / 7, k = r - 7 * y;
+      const int q = r + 128 * i;
+      if (i == 0 || q < NWIN1) {
+        const int y = (q * 147) >> 10, k = q - 7 * y;          // input quad: row, 4-pixel group
+        const int yp = (q * 147) >> 11, xp = q - 14 * yp;      // pool window
         uint32_t lo = x[i][0], hi = x[i][1];
         if constexpr (U8) {
           const uint32_t b = x[i][0];
@@ -185,46 +187,54 @@ struct Stage {
         }
         *(u32x2*)(lds + X_OFF + img * X_IMG + (y + 2) * X_RS + (4 * k + 4) * 2) = u32x2{lo, hi};
         const uint32_t l4 = a1[i] & 0x0f0f0f0fu, h4 = (a1[i] >> 4) & 0x0f0f0f0fu;   // codes c 0..3 / 4..7
-        *(u32x4*)(lds + CD_OFF + img * DP1_IMG + r * 16) = u32x4{bytes01(l4), bytes23(l4), bytes01(h4), bytes23(h4)};
+        *(u32x4*)(lds + CD_OFF + img * D_IMG + yp * D_RS + xp * 16) =
+            u32x4{bytes01(l4), bytes23(l4), bytes01(h4), bytes23(h4)};
       }
     }
   }
-  // dL/dpool2 + codes and pool1 of a tile (loaded during phase 2, stored at its end)
-  DEV void load_dy(const BwdArgs& a, int t0, int tid) {
+  DEV void load_dy(const BwdArgs& a, int t0, int wave, int ln) {
     const int nimg = t0 < 0 ? 0 : min(T, a.B - t0);
     const int tb = t0 < 0 ? 0 : t0;
+    const int tid = wave * 64 + ln;
     const auto rdp = buf_rsrc(a.dp2 + (int64_t)tb * 400, (uint32_t)nimg * 800u);
     const auto ra2 = buf_rsrc(a.arg2 + (int64_t)tb * 400, (uint32_t)nimg * 400u);
-    const auto rp1 = buf_rsrc(a.p1 + (int64_t)tb * NWIN1 * 8, (uint32_t)nimg * (NWIN1 * 16u));
     dp = buf_b128(rdp, tid < 400 ? 16u * tid : BUF_OOB);
     c2 = buf_b64(ra2, tid < 400 ? 8u * tid : BUF_OOB);
+    const int img = img_of(wave);
+    const bool ok = t0 >= 0 && t0 + img < a.B;
+    const auto rp1 = buf_rsrc(a.p1 + (int64_t)(ok ? t0 + img : 0) * NWIN1 * 8, ok ? NWIN1 * 16u : 0u);
+    const int r = ln + 64 * (wave & 1);
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int e = tid + NT * i;
-      p1[i] = buf_b128(rp1, e < T * NWIN1 ? 16u * e : BUF_OOB);
+      const uint32_t q = (uint32_t)(r + 128 * i);
+      p1[i] = buf_b128(rp1, q < NWIN1 ? 16u * q : BUF_OOB);
     }
   }
-  // unpooled dY2 (ReLU mask folded in the codes), read by the conv2 kernels
-  // (called at the end of phase 2: the fence keeps the compiler from hoisting the unpooling
-  // above the phase, which would wait for these loads -- and the pool1 DMA -- at its start)
-  DEV void store_dy(uint8_t* lds, int tid) {
+  // unpooled dY2 (ReLU mask folded in the codes) and pool1 with channel 6 = 1.0 (the conv2
+  // bias row), read by the conv2 kernels.  Called at the end of phase 2; the fence keeps the
+  // compiler from hoisting the unpooling above the phase (it would wait for the loads there).
+  DEV void store_dy(uint8_t* lds, int wave, int ln) {
     asm volatile("" : "+v"(dp), "+v"(c2), "+v"(p1[0]), "+v"(p1[1]));
-    static_assert(NCH == 2, "");
+    const int img = img_of(wave), r = ln + 64 * (wave & 1);
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int e = tid + NT * i;
-      if (e < T * NWIN1) {
-        const int img = e / NWIN1, r = e - img * NWIN1;
-        *(u32x4*)(lds + P1_OFF + img * P1_IMG + r * 16) = p1[i];
+      const int q = r + 128 * i;
+      if (i == 0 || q < NWIN1) {
+        const int yp = (q * 147) >> 11, xp = q - 14 * yp;
+        const u32x4 v = {p1[i][0], p1[i][1], p1[i][2], p1[i][3] | 0x3f80u};
+        *(u32x4*)(lds + P1_OFF + img * P1_IMG + yp * P1_RS + xp * 16) = v;
       }
     }
+    const int tid = wave * 64 + ln;
     if (tid < 400) {
-      const int img = tid / 50, rr = tid - 50 * img, w = rr >> 1, yp = w / 5, xp = w - 5 * yp;
-      const int o = DY2_OFF + img * DY2_IMG + (2 * yp + 1) * DY2_RS + 2 * xp * 32 + 16 * (rr & 1);
-      const uint32_t e0 = bytes01(c2[0]), e1 = bytes23(c2[0]), e2 = bytes01(c2[1]), e3 = bytes23(c2[1]);
+      const int im = tid / 50, rr = tid - 50 * im, w = rr >> 1, yp = w / 5, xp = w - 5 * yp;
+      const int o = DY2_OFF + im * DY2_IMG + (2 * yp + 1) * DY2_RS + 2 * xp * 32 + 16 * (rr & 1);
+      const uint32_t e[4] = {bytes01(c2[0]), bytes23(c2[0]), bytes01(c2[1]), bytes23(c2[1])};
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        const u32x4 v = {dp[0] & heq(e0, d), dp[1] & heq(e1, d), dp[2] & heq(e2, d), dp[3] & heq(e3, d)};
+        const uint32_t dd = (uint32_t)d * 0x00010001u;
+        const u32x4 v = {sel_eq(dp[0], e[0], dd), sel_eq(dp[1], e[1], dd), sel_eq(dp[2], e[2], dd),
+                         sel_eq(dp[3], e[3], dd)};
         *(u32x4*)(lds + o + (d >> 1) * DY2_RS + (d & 1) * 32) = v;
       }
     }
@@ -254,44 +264,71 @@ DEV void dgrad_unit(const uint8_t* lds, int bB, int lane, int dylo, int dyhi, f3
   }
 }
 
+// conv2 weight-gradient k-steps ks0 .. ks1 - 1 of tile group G (k-step s: dY2 row s / 3,
+// pixels 4 (s % 3) .. + 3).  Lane bases: B (dY2), A for the pixel-apart tiles and A for the
+// row-apart ones; a step adds one uniform offset to each.
+template <int G>
+DEV void c2w_steps(const uint8_t* lds, int ks0, int ks1, int ln, f32x4 (&acc2)[C2MAX]) {
+  const int g = ln >> 4, q = (ln >> 2) & 3, p = ln & 3;
+  const int img = 4 * (g & 1) + q, sub = 2 * (g >> 1), hA = p >> 1, pc = p & 1;
+  const int bB = DY2_OFF + img * DY2_IMG + DY2_RS + sub * 32 + 8 * p;
+  const int aB = P1_OFF + img * P1_IMG + sub * 16 + 8 * pc;
+  const int aP = aB + hA * 16, aR = aB + hA * P1_RS;        // second tap: next pixel / next row
+  constexpr int NT2 = G == 0 ? 4 : 3;
+#pragma unroll 1
+  for (int s = ks0; s < ks1; ++s) {
+    const int y = s / 3, x0 = 4 * (s - 3 * y);              // uniform
+    const int sb = bB + y * DY2_RS + x0 * 32, sa = (y * 16 + x0) * 16;
+    const bf16x8 Bf = frag(tr4(lds, sb), tr4(lds, sb + 32));
+#pragma unroll
+    for (int t = 0; t < NT2; ++t) {
+      const int tile = C2_GT[G][t], tap = C2_TAP0[tile];
+      const int base = (tile < 10 ? aP : aR) + sa + ((tap / 5) * 16 + tap % 5) * 16;
+      acc2[t] = mfma16(frag(tr4(lds, base), tr4(lds, base + 16)), Bf, acc2[t]);
+    }
+  }
+}
+
 // ---- static work split.  Waves w, w + 4, w + 8, w + 12 share a SIMD; per SIMD the phase-1
-// MFMA counts are 183 / 183 / 181 / 183 (dgrad units: kernel-row counts 2, 4, 5, 5, 5, 4, 2
+// MFMA counts are 199 / 199 / 198 / 199 (dgrad units: kernel-row counts 2, 4, 5, 5, 5, 4, 2
 // x 9 or 6 MFMAs; conv2 k-steps: 4 / 3 / 3 / 3 MFMAs in tile groups 0 / 1 / 2 / 3).
-// dgrad unit of each wave (row pair * 2 + half, -1: none) and its conv2 k-step range.
-__constant__ int dg_unit[NW] = {6, 4, -1, -1, 8, 12, 11, 9, 0, 2, 5, 13, 10, 3, 1, 7};
-__constant__ int c2_ks0[NW] = {0, 0, 0, 13, 0, 0, 8, 17, 0, 7, 12, 18, 0, 6, 13, 19};
-__constant__ int c2_ks1[NW] = {0, 0, 13, 25, 0, 8, 17, 25, 7, 12, 18, 25, 6, 13, 19, 25};
+// dgrad unit of each wave (row pair * 2 + half, -1: none) and its conv2 k-step range
+// (group wave >> 2; the group's 30 steps split end to end).
+__constant__ int dg_unit[NW] = {2, 10, 0, -1, 6, 5, 3, 8, 7, 11, -1, 1, 12, 13, 9, 4};
+__constant__ int c2_ks0[NW] = {0, 1, 8, 23, 0, 8, 16, 23, 0, 7, 15, 22, 0, 7, 14, 22};
+__constant__ int c2_ks1[NW] = {1, 8, 23, 30, 8, 16, 23, 30, 7, 15, 22, 30, 7, 14, 22, 30};
+// conv1 k-steps (s: window row s / 2, windows 4 (s % 2) .. + 3 of the set) of parity set
+// w & 1: rank w >> 1 runs 4, 4, 4, 4, 3, 3, 3, 3 steps (14 per SIMD)
+__constant__ int c1_ks0[8] = {0, 4, 8, 12, 16, 19, 22, 25};
+__constant__ int c1_ks1[8] = {4, 8, 12, 16, 19, 22, 25, 28};
 
 template <bool PROF, bool U8, bool IDX>
 __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int i16 = lane & 15, g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   const int ntiles = (a.B + T - 1) / T;
   const int nk = ntiles > (int)blockIdx.x ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-  auto tile0 = [&](int k) { return ((int)blockIdx.x + k * (int)gridDim.x) * T; };
+  auto tile0 = [&](int k) { return k < nk ? ((int)blockIdx.x + k * (int)gridDim.x) * T : -1; };
 
-  // ---- prologue: zero the tiles (borders stay zero), ONES cell, dgrad A fragments
-  for (int e = tid; e < (ZERO_OFF + 16) / 16; e += NT) *(u32x4*)(lds + 16 * e) = u32x4{0u, 0u, 0u, 0u};
-  if (tid == 0) *(u32x4*)(lds + ONES_OFF) = u32x4{0x3f80u, 0u, 0u, 0u};
+  // ---- prologue: zero the tiles (borders and pads stay zero), dgrad A fragments
+  for (int e = tid; e < LDS_BYTES / 16; e += NT) *(u32x4*)(lds + 16 * e) = u32x4{0u, 0u, 0u, 0u};
   __syncthreads();
   if (tid < 15 * 64) {
     const int f = tid >> 6, dy = f / 3, j = f - 3 * dy;
-    const int r = i16 >> 3, ci = lane & 7, xs = g >> 1, co0 = 8 * (g & 1);
+    const int r = (lane & 15) >> 3, ci = lane & 7, xs = lane >> 5, co0 = 8 * ((lane >> 4) & 1);
     const int dx = r + 4 - 2 * j - xs;
     u32x4 v = {0u, 0u, 0u, 0u};
     if (dx >= 0 && dx <= 4) v = *(const u32x4*)(a.w2 + ((dy * 5 + dx) * 8 + ci) * 16 + co0);
     *(u32x4*)(lds + AF_OFF + 16 * tid) = v;
   }
   Stage<U8, IDX> st;
-  st.load_dy(a, nk > 0 ? tile0(0) : -1, tid);
-  st.load_rows(a, nk > 0 ? tile0(0) : -1, tid);
-  st.load_xc(a, nk > 0 ? tile0(0) : -1, tid);
-  st.load_rows(a, nk > 1 ? tile0(1) : -1, tid);
-  st.store_dy(lds, tid);
+  st.load_row(a, tile0(0), wave);
+  st.load_xc(a, tile0(0), wave, lane);
+  st.load_dy(a, tile0(0), wave, lane);
+  st.load_row(a, tile0(1), wave);
+  st.store_dy(lds, wave, lane);
 
   const int grp = wave >> 2, sig = wave & 1;          // conv2 tile group / conv1 parity set (uniform)
-  const int tg0 = c2g(grp), nt2 = c2g(grp + 1) - tg0;
   f32x4 acc2[C2MAX];
 #pragma unroll
   for (int t = 0; t < C2MAX; ++t) acc2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -302,6 +339,7 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
   const auto rarg1 = buf_rsrc(a.arg1, (uint32_t)a.B * (NWIN1 * 4u));
   const int du = dg_unit[wave];
   const int ks0 = c2_ks0[wave], ks1 = c2_ks1[wave];
+  const int cs0 = c1_ks0[wave >> 1], cs1 = c1_ks1[wave >> 1];
 
   uint64_t pc_acc[NPROF] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tclk = __builtin_amdgcn_s_memtime();
@@ -317,15 +355,12 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
     const int t0 = tile0(k);
     __syncthreads();   // dY2 / pool1 of this tile stored; the previous conv1 phase is done
     mark(6);
-    {
-      const int ln = lane_now(), tl = wave * 64 + ln;
-      st.store_xc(lds, tl);
-    }
+    st.store_xc(lds, wave, lane_now());
     mark(0);
 
     // ================================================ phase 1a: conv2 dgrad unit
     if (du >= 0) {
-      const int ln = lane_now(), tl = wave * 64 + ln;
+      const int ln = lane_now();
       const int i16 = ln & 15, g = ln >> 4;
       const int pr = du >> 1, hx = du & 1;
       const int img = i16 >> 1, rr = i16 & 1, orow = 2 * pr + rr;
@@ -338,7 +373,7 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
         const int w1 = orow * 14 + 2 * (u0 + u) + (g >> 1);
         aw[u] = buf_b32(rarg1, t0 + img < a.B && u0 + u < 7 ? 4u * ((uint32_t)(t0 + img) * NWIN1 + w1) : BUF_OOB);
       }
-      st.load_xc(a, k + 1 < nk ? tile0(k + 1) : -1, tl);
+      st.load_xc(a, tile0(k + 1), wave, ln);
       f32x4 acc[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -346,133 +381,96 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
       if (hx) dgrad_unit<1>(lds, bB, ln, dylo, dyhi, acc);
       else dgrad_unit<0>(lds, bB, ln, dylo, dyhi, acc);
       // dP1 (bf16) for the conv1 weight gradient; the conv1 bias gradient from the fp32
-      // sums of the active windows (code != 4)
+      // sums of the active windows (code != 4, i.e. bit 2 of the nibble clear)
       const int sh = 4 * (g & 1);
+      const int wB = DP1_OFF + img * D_IMG + orow * D_RS + (2 * u0 + (g >> 1)) * 16 + 8 * (g & 1);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (u0 + u < 7) {
-          const int w1 = orow * 14 + 2 * (u0 + u) + (g >> 1);
-          *(u32x2*)(lds + DP1_OFF + img * DP1_IMG + w1 * 16 + 8 * (g & 1)) =
-              u32x2{pack2(acc[u][0], acc[u][1]), pack2(acc[u][2], acc[u][3])};
+          *(u32x2*)(lds + wB + 32 * u) = u32x2{pack2(acc[u][0], acc[u][1]), pack2(acc[u][2], acc[u][3])};
+          const uint32_t act = (~aw[u] >> (sh + 2)) & 0x01010101u;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) db1[i] += ((aw[u] >> (8 * i + sh)) & 15u) != 4u ? acc[u][i] : 0.f;
+          for (int i = 0; i < 4; ++i) db1[i] = fmaf(acc[u][i], (float)((act >> (8 * i)) & 0xffu), db1[i]);
         }
       }
     } else {
-      const int tl = wave * 64 + lane_now();
-      st.load_xc(a, k + 1 < nk ? tile0(k + 1) : -1, tl);
+      st.load_xc(a, tile0(k + 1), wave, lane_now());
     }
     mark(1);
 
     // ================================================ phase 1b: conv2 weight-gradient k-steps
-    // Transposed reads: MFMA K row 8g + 4rho + q is item 16(g>>1) + 8rho + 4(g&1) + q of the
-    // 32-item k-step: image 4(g&1) + q (a lane constant), pixel / window 4s + 2(g>>1) + rho.
     if (ks0 < ks1) {
-      const int ln = lane_now(), g = ln >> 4, q = (ln >> 2) & 3, p = ln & 3;
-      const int img_l = 4 * (g & 1) + q, sub_l = 2 * (g >> 1), hA = p >> 1, pc = p & 1;
-      // this lane's pool1 tap offset per tile of the group; the bias lanes read the ONES cell
-      // (pixel offset masked off)
-      int toff[C2MAX];
-#pragma unroll
-      for (int t = 0; t < C2MAX; ++t) {
-        // (readfirstlane: two scalar loads and a select, not a per-lane load from the table)
-        const int tt = min(tg0 + t, 12);
-        const int tap0 = __builtin_amdgcn_readfirstlane(c2_taps[tt][0]);
-        const int tap1 = __builtin_amdgcn_readfirstlane(c2_taps[tt][1]);
-        const int tap = hA ? tap1 : tap0;
-        toff[t] = tap == 25 ? ONES_OFF + 8 * pc : P1_OFF + img_l * P1_IMG + ((tap / 5) * 14 + tap % 5) * 16 + 8 * pc;
+      const int ln = lane_now();
+      switch (grp) {
+        case 0: c2w_steps<0>(lds, ks0, ks1, ln, acc2); break;
+        case 1: c2w_steps<1>(lds, ks0, ks1, ln, acc2); break;
+        case 2: c2w_steps<2>(lds, ks0, ks1, ln, acc2); break;
+        default: c2w_steps<3>(lds, ks0, ks1, ln, acc2); break;
       }
-      const int pm2 = grp == 3 && hA ? 0 : -1;           // the bias tile is tile 2 of group 3
-      const int b2off = DY2_OFF + img_l * DY2_IMG + DY2_RS + 8 * p;
-#pragma unroll 1
-    for (int s = ks0; s < ks1; ++s) {
-      int pofs[2], bb[2];
-#pragma unroll
-      for (int rho = 0; rho < 2; ++rho) {
-        const int pix = 4 * s + sub_l + rho, y = (pix * 205) >> 11, x = pix - 10 * y;
-        pofs[rho] = (y * 14 + x) * 16;
-        bb[rho] = b2off + y * DY2_RS + x * 32;
-      }
-      const bf16x8 Bf = frag(tr4(lds, bb[0]), tr4(lds, bb[1]));
-#pragma unroll
-      for (int t = 0; t < C2MAX; ++t) {
-        if (t < nt2) {
-          const int m = t == 2 ? pm2 : -1;
-          const bf16x8 Af = frag(tr4(lds, toff[t] + (pofs[0] & m)), tr4(lds, toff[t] + (pofs[1] & m)));
-          acc2[t] = mfma16(Af, Bf, acc2[t]);
-        }
-      }
-    }
     }
 
     mark(2);
     __syncthreads();   // dP1, input and codes of this tile visible; dY2 / pool1 no longer read
     mark(3);
-    if (k + 1 < nk) {
+    {
       const int ln = lane_now();
-      st.load_dy(a, tile0(k + 1), wave * 64 + ln);
+      st.load_dy(a, tile0(k + 1), wave, ln);
+      st.load_row(a, tile0(k + 2), wave);
     }
-    st.load_rows(a, k + 2 < nk ? tile0(k + 2) : -1, wave * 64 + lane_now());
     mark(4);
 
     // ================================================ phase 2: conv1 weight gradient (set sig)
     {
-    const int ln = lane_now(), g = ln >> 4, q = (ln >> 2) & 3, p = ln & 3;
-    const int img_l = 4 * (g & 1) + q, sub_l = 2 * (g >> 1), hA = p >> 1, pc = p & 1;
-    const uint32_t dsel = (uint32_t)((ln & 15) >> 3);
+      const int ln = lane_now(), g = ln >> 4, q = (ln >> 2) & 3, p = ln & 3;
+      const int img = 4 * (g & 1) + q, sub = 2 * (g >> 1), hA = p >> 1, pc = p & 1;
+      const uint32_t dsel = (uint32_t)((ln & 15) >> 3);
+      const uint32_t dd0 = dsel * 0x00010001u, dd1 = (2u + dsel) * 0x00010001u;
+      const int aB = X_OFF + img * X_IMG + hA * X_RS + (4 * sub + 4 * pc + 4 * sig) * 2;
+      const int bB = DP1_OFF + img * D_IMG + (2 * sub + sig) * 16 + 8 * pc;
 #pragma unroll 1
-    for (int s = wave >> 1; s < 25; s += NW / 2) {
-      int ax[2], bx[2];
+      for (int s = cs0; s < cs1; ++s) {
+        const int yp = s >> 1, xi0 = 4 * (s & 1);           // uniform
+        const int sa = aB + 2 * yp * X_RS + 8 * xi0, sb = bB + yp * D_RS + 32 * xi0;
+        const u32x4 dv = __builtin_bit_cast(u32x4, frag(tr4(lds, sb), tr4(lds, sb + 32)));
+        const u32x4 cv = __builtin_bit_cast(u32x4, frag(tr4(lds, sb + (CD_OFF - DP1_OFF)),
+                                                         tr4(lds, sb + (CD_OFF - DP1_OFF) + 32)));
+        const bf16x8 B0 = __builtin_bit_cast(bf16x8, u32x4{sel_eq(dv[0], cv[0], dd0), sel_eq(dv[1], cv[1], dd0),
+                                                           sel_eq(dv[2], cv[2], dd0), sel_eq(dv[3], cv[3], dd0)});
+        const bf16x8 B1 = __builtin_bit_cast(bf16x8, u32x4{sel_eq(dv[0], cv[0], dd1), sel_eq(dv[1], cv[1], dd1),
+                                                           sel_eq(dv[2], cv[2], dd1), sel_eq(dv[3], cv[3], dd1)});
 #pragma unroll
-      for (int rho = 0; rho < 2; ++rho) {
-        const int tw = 4 * s + sub_l + rho;                  // window of the set (98 per image)
-        const bool ok = tw < 98;
-        const int tc = ok ? tw : 97, yp = (tc * 147) >> 10, xi = tc - 7 * yp, xp = 2 * xi + sig;
-        ax[rho] = X_OFF + img_l * X_IMG + (2 * yp + hA) * X_RS + (4 * xi + 4 * pc + 4 * sig) * 2;
-        bx[rho] = ok ? img_l * DP1_IMG + (yp * 14 + xp) * 16 + 8 * pc : -1;
-      }
-      const s16x4 d0 = tr4(lds, bx[0] >= 0 ? DP1_OFF + bx[0] : ZERO_OFF + 8 * pc);
-      const s16x4 d1 = tr4(lds, bx[1] >= 0 ? DP1_OFF + bx[1] : ZERO_OFF + 8 * pc);
-      const s16x4 c0 = tr4(lds, bx[0] >= 0 ? CD_OFF + bx[0] : ZERO_OFF + 8 * pc);
-      const s16x4 c1 = tr4(lds, bx[1] >= 0 ? CD_OFF + bx[1] : ZERO_OFF + 8 * pc);
-      const u32x4 dv = __builtin_bit_cast(u32x4, frag(d0, d1)), cv = __builtin_bit_cast(u32x4, frag(c0, c1));
-      bf16x8 Bm[2];
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const uint32_t d = 2u * nt + dsel;
-        Bm[nt] = __builtin_bit_cast(bf16x8, u32x4{dv[0] & heq(cv[0], d), dv[1] & heq(cv[1], d),
-                                                  dv[2] & heq(cv[2], d), dv[3] & heq(cv[3], d)});
-      }
-#pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const bf16x8 Af = frag(tr4(lds, ax[0] + 2 * t * X_RS), tr4(lds, ax[1] + 2 * t * X_RS));
-        acc1[t][0] = mfma16(Af, Bm[0], acc1[t][0]);
-        acc1[t][1] = mfma16(Af, Bm[1], acc1[t][1]);
+        for (int t = 0; t < 3; ++t) {
+          const bf16x8 Af = frag(tr4(lds, sa + 2 * t * X_RS), tr4(lds, sa + 2 * t * X_RS + 8));
+          acc1[t][0] = mfma16(Af, B0, acc1[t][0]);
+          acc1[t][1] = mfma16(Af, B1, acc1[t][1]);
+        }
       }
     }
-    }
-    if (k + 1 < nk) st.store_dy(lds, wave * 64 + lane_now());
+    if (k + 1 < nk) st.store_dy(lds, wave, lane_now());
     mark(5);
   }
 
   // ---- epilogue: the waves' partials -> this block's slab rows (fixed summation order)
+  const int i16 = lane & 15, g = lane >> 4;
   __syncthreads();
   mark(6);
-  // conv2: partials [wave][t][col 16][row 16]; tile c2g(G) + t is summed over waves 4G..4G+3
+  // conv2: partials [wave][t][col 16][row 16]; tile c2_gt[G][t] is summed over waves 4G..4G+3
   float* e2 = (float*)lds;
 #pragma unroll
   for (int t = 0; t < C2MAX; ++t) *(f32x4*)(e2 + ((wave * C2MAX + t) * 16 + i16) * 16 + 4 * g) = acc2[t];
   __syncthreads();
   float* s2 = a.slab2 + (int64_t)blockIdx.x * 208 * 16;
-  for (int e = tid; e < 13 * 256; e += NT) {
-    const int tt = e >> 8, row = (e >> 4) & 15, col = e & 15;
-    const int h = row >> 3, ci = row & 7, tap = c2_taps[tt][h];
-    if (tap == 25 && ci != 0) continue;
-    const int G = tt < 4 ? 0 : (tt - 1) / 3, t = tt - c2g(G);
+  for (int e = tid; e < 4 * C2MAX * 256; e += NT) {
+    const int G = e >> 10, t = (e >> 8) & 3, row = (e >> 4) & 15, col = e & 15;
+    const int tile = c2_gt[G][t];
+    if (tile < 0) continue;
+    const int h = row >> 3, ci = row & 7, tap = c2_tap0[tile] + h * (tile < 10 ? 1 : 5);
+    const bool bias = tile == 0 && h == 0 && ci == 6;
+    if (tap >= 25 || (ci >= 6 && !bias)) continue;
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) v += e2[(((4 * G + w) * C2MAX + t) * 16 + col) * 16 + row];
-    s2[(tap == 25 ? 200 : tap * 8 + ci) * 16 + col] = v;
+    s2[(bias ? 200 : tap * 8 + ci) * 16 + col] = v;
   }
   __syncthreads();
   float* e1 = (float*)lds;                       // [wave][t][nt][col 16][row 16] (set = wave & 1)

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Time the fused LeNet-5 conv-stack backward (lenet_bwd.hip) alone at the BASELINE batch,
-against the three per-layer kernels it replaces, and print its per-phase clock split
-(s_memtime sums over all waves; the prof build of the same launch).
+against the three per-layer kernels it replaces, at smaller batches on the same grid (the
+fixed vs per-tile cost), and print its per-phase clock split (s_memtime sums over all
+waves; the prof build of the same launch).
 
     python bench/micro_lenet_bwd.py [B]
 """
@@ -41,19 +42,31 @@ def main():
     s1 = torch.zeros(grid * 32 * 8, device=dev)
     s2 = torch.zeros(grid * 208 * 16, device=dev)
 
-    def timeit(f, iters=30):
+    def timeit(f, iters=30, reps=3):
+        """best of `reps` means over `iters` back-to-back launches (us)"""
         for _ in range(5):
             f()
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(iters):
-            f()
-        e1.record()
-        torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / iters * 1e3
+        best = float("inf")
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(iters):
+                f()
+            e1.record()
+            torch.cuda.synchronize()
+            best = min(best, e0.elapsed_time(e1) / iters * 1e3)
+        return best
 
+    timeit(lambda: K.lenet_bwd(ds, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx), iters=200, reps=1)  # clocks up
     fused = timeit(lambda: K.lenet_bwd(ds, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx))
+    # fixed vs per-tile cost: the same kernel over the first Bs images (grid stays 256 blocks
+    # while Bs / 8 >= 256), 1 .. B/2048 tiles per block
+    scaling = {}
+    for Bs in (2048, 4096, 8192, 16384, 32768, B):
+        if Bs <= B:
+            gs = K.lenet_bwd_blocks(Bs)
+            scaling[Bs] = round(timeit(lambda: K.lenet_bwd(ds, P1, A1, dP2, A2, w2, Bs, s1, s2, gs, idx=idx)), 1)
     # the split path: conv2 dgrad -> dP1 in HBM, conv2 / conv1 weight gradients
     dP1 = torch.empty(B, 14, 14, 8, dtype=torch.bfloat16, device=dev)
     g2 = K.convpool_wgrad_grid(8, 16, 5, 0, 14, 14)
@@ -63,12 +76,21 @@ def main():
     dgr = timeit(lambda: K.convpool_dgrad(dP2.view(B, 5, 5, 16), A2, w2, dP1, B, 8, 16, 5, 0, 14, 14))
     w2g = timeit(lambda: K.convpool_wgrad(P1, dP2.view(B, 5, 5, 16), A2, sl2, g2, B, 8, 16, 5, 0, 14, 14))
     w1g = timeit(lambda: K.convpool_wgrad(ds, dP1, A1, sl1, g1, B, 1, 8, 5, 2, 28, 28, idx=idx))
+    # time attribution (prof launches, experiments): skip bits 1 dgrad, 2 conv2 wgrad, 4 conv1
+    # wgrad, 8 staging, 16 loop barriers
+    skip_us = {}
+    pr_buf = torch.zeros(8, dtype=torch.int64, device=dev)
+    for sk in (0, 1, 2, 4, 8, 16, 7, 15):
+        os.environ["MNISTX_BWD_SKIP"] = str(sk)
+        skip_us[sk] = round(timeit(lambda: K.lenet_bwd(ds, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx,
+                                                       prof=pr_buf)), 1)
+    os.environ.pop("MNISTX_BWD_SKIP", None)
     prof = torch.zeros(8, dtype=torch.int64, device=dev)
     K.lenet_bwd(ds, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx, prof=prof)
     torch.cuda.synchronize()
     pr = prof.tolist()
     tot = max(1, sum(pr))
-    print(json.dumps({"B": B, "grid": grid, "fused_us": round(fused, 1),
+    print(json.dumps({"B": B, "grid": grid, "fused_us": round(fused, 1), "fused_us_by_batch": scaling, "prof_us_by_skip": skip_us,
                       "split_us": {"c2_dgrad": round(dgr, 1), "c2_wgrad": round(w2g, 1), "c1_wgrad": round(w1g, 1),
                                    "sum": round(dgr + w2g + w1g, 1)},
                       "phase_share": {k: round(v / tot, 3) for k, v in zip(PHASES, pr)}}), flush=True)

@@ -39,10 +39,12 @@
 //    strides below the reads are conflict-free (bench/lds_bwd.py; conv2 tiles pair taps one
 //    pixel apart, except three pairs one row apart: 2-way).
 // 16 waves (4 per SIMD) share a tile in two phases (two barriers): [store input / codes of
-// this tile, load the next tile's input, one dgrad unit + conv2 weight-gradient k-steps of
-// the wave's tile group] -> [load the next tile's dY2 / pool1, conv1 weight-gradient k-steps
-// of the wave's parity set, store dY2 / pool1].  The accumulators are split (a wave holds at
+// this tile, load the next tile's data, one dgrad unit + conv2 weight-gradient k-steps of
+// the wave's tile group] -> [conv1 weight-gradient k-steps of the wave's parity set, store
+// the next tile's dY2 / pool1].  The accumulators are split (a wave holds at
 // most 4 conv2 tiles and one conv1 set: 40 registers) so the kernel fits 128 VGPRs.
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -115,6 +117,7 @@ struct BwdArgs {
   float* slab1;           // [grid][32][8]: rows tap 0..24, 25 = bias
   float* slab2;           // [grid][208][16]: rows tap * 8 + ci, 200 = bias
   unsigned long long* prof;   // optional (experiments): per-phase clock sums [NPROF] over all waves
+  int skip;               // experiments (prof launches only): work to skip, for time attribution
 };
 // phase clocks (s_memtime): 0 store input / codes, 1 dgrad (+ next-tile input loads), 2 conv2
 // wgrad, 3 barrier 1, 4 next-tile dY2 / pool1 loads issue, 5 conv1 wgrad + dY2 / pool1 store,
@@ -125,9 +128,9 @@ constexpr int NPROF = 8;
 // Input, pool1 and codes: wave pair 2i stages image i, lane r of the pair windows / input
 // quads r and r + 128 (< 196), so a wave's image and dataset row are wave-uniform (the
 // batch-index entry is one uniform load, a tile ahead of the input it addresses).
-// dL/dpool2 + codes: threads < 400, one pooled pixel (8 channels) each.  The input +
-// pool1 codes are loaded during phase 1 and stored at the next loop top; dY2 + pool1 are
-// loaded during phase 2 and stored at its end.
+// dL/dpool2 + codes: threads < 400, one pooled pixel (8 channels) each.  Everything for
+// the next tile is loaded at the start of phase 1: the input + pool1 codes are stored at the
+// next loop top, dY2 + pool1 at the end of phase 2.
 constexpr int NCH = 2;
 static_assert(NW == 2 * T && 2 * 128 >= NWIN1 && 128 <= NWIN1, "staging: one wave pair per image, 2 chunks");
 template <bool U8, bool IDX>
@@ -275,7 +278,7 @@ DEV void c2w_steps(const uint8_t* lds, int ks0, int ks1, int ln, f32x4 (&acc2)[C
   const int aB = P1_OFF + img * P1_IMG + sub * 16 + 8 * pc;
   const int aP = aB + hA * 16, aR = aB + hA * P1_RS;        // second tap: next pixel / next row
   constexpr int NT2 = G == 0 ? 4 : 3;
-#pragma unroll 1
+#pragma unroll 2
   for (int s = ks0; s < ks1; ++s) {
     const int y = s / 3, x0 = 4 * (s - 3 * y);              // uniform
     const int sb = bB + y * DY2_RS + x0 * 32, sa = (y * 16 + x0) * 16;
@@ -353,13 +356,16 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
 
   for (int k = 0; k < nk; ++k) {
     const int t0 = tile0(k);
-    __syncthreads();   // dY2 / pool1 of this tile stored; the previous conv1 phase is done
+    if (!(PROF && (a.skip & 16))) __syncthreads();   // dY2 / pool1 of this tile stored; the previous conv1 phase is done
     mark(6);
-    st.store_xc(lds, wave, lane_now());
+    if (!(PROF && (a.skip & 8))) {
+      const int ln = lane_now();
+      st.store_xc(lds, wave, ln);
+    }
     mark(0);
 
     // ================================================ phase 1a: conv2 dgrad unit
-    if (du >= 0) {
+    if (du >= 0 && !(PROF && (a.skip & 1))) {
       const int ln = lane_now();
       const int i16 = ln & 15, g = ln >> 4;
       const int pr = du >> 1, hx = du & 1;
@@ -373,7 +379,8 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
         const int w1 = orow * 14 + 2 * (u0 + u) + (g >> 1);
         aw[u] = buf_b32(rarg1, t0 + img < a.B && u0 + u < 7 ? 4u * ((uint32_t)(t0 + img) * NWIN1 + w1) : BUF_OOB);
       }
-      st.load_xc(a, tile0(k + 1), wave, ln);
+      // the next tile's input after this unit's code loads (vmcnt is in order)
+      if (!(PROF && (a.skip & 8))) st.load_xc(a, tile0(k + 1), wave, ln);
       f32x4 acc[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -393,13 +400,16 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
           for (int i = 0; i < 4; ++i) db1[i] = fmaf(acc[u][i], (float)((act >> (8 * i)) & 0xffu), db1[i]);
         }
       }
-    } else {
+    } else if (!(PROF && (a.skip & 8))) {
       st.load_xc(a, tile0(k + 1), wave, lane_now());
     }
+    // the next tile's dY2 / pool1 (stored at the end of phase 2), issued apart from the input
+    // loads so the 16 waves' load bursts do not queue behind each other
+    if (!(PROF && (a.skip & 8))) st.load_dy(a, tile0(k + 1), wave, lane_now());
     mark(1);
 
     // ================================================ phase 1b: conv2 weight-gradient k-steps
-    if (ks0 < ks1) {
+    if (ks0 < ks1 && !(PROF && (a.skip & 2))) {
       const int ln = lane_now();
       switch (grp) {
         case 0: c2w_steps<0>(lds, ks0, ks1, ln, acc2); break;
@@ -410,13 +420,9 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
     }
 
     mark(2);
-    __syncthreads();   // dP1, input and codes of this tile visible; dY2 / pool1 no longer read
+    if (!(PROF && (a.skip & 16))) __syncthreads();   // dP1, input and codes of this tile visible; dY2 / pool1 no longer read
     mark(3);
-    {
-      const int ln = lane_now();
-      st.load_dy(a, tile0(k + 1), wave, ln);
-      st.load_row(a, tile0(k + 2), wave);
-    }
+    if (!(PROF && (a.skip & 8))) st.load_row(a, tile0(k + 2), wave);
     mark(4);
 
     // ================================================ phase 2: conv1 weight gradient (set sig)
@@ -427,8 +433,8 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
       const uint32_t dd0 = dsel * 0x00010001u, dd1 = (2u + dsel) * 0x00010001u;
       const int aB = X_OFF + img * X_IMG + hA * X_RS + (4 * sub + 4 * pc + 4 * sig) * 2;
       const int bB = DP1_OFF + img * D_IMG + (2 * sub + sig) * 16 + 8 * pc;
-#pragma unroll 1
-      for (int s = cs0; s < cs1; ++s) {
+#pragma unroll 2
+      for (int s = cs0; s < (PROF && (a.skip & 4) ? cs0 : cs1); ++s) {
         const int yp = s >> 1, xi0 = 4 * (s & 1);           // uniform
         const int sa = aB + 2 * yp * X_RS + 8 * xi0, sb = bB + yp * D_RS + 32 * xi0;
         const u32x4 dv = __builtin_bit_cast(u32x4, frag(tr4(lds, sb), tr4(lds, sb + 32)));
@@ -446,7 +452,7 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
         }
       }
     }
-    if (k + 1 < nk) st.store_dy(lds, wave, lane_now());
+    if (k + 1 < nk && !(PROF && (a.skip & 8))) st.store_dy(lds, wave, lane_now());
     mark(5);
   }
 
@@ -510,10 +516,18 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
     }
     s1[tap * 8 + c] = v;
   }
-  if constexpr (PROF) {
+  if constexpr (PROF) {   // one atomic per phase and block (the block's waves summed in LDS)
     mark(7);
+    __syncthreads();
+    unsigned long long* ep = (unsigned long long*)lds;
     if (lane == 0)
-      for (int i = 0; i < NPROF; ++i) atomicAdd(a.prof + i, (unsigned long long)pc_acc[i]);
+      for (int i = 0; i < NPROF; ++i) ep[wave * NPROF + i] = pc_acc[i];
+    __syncthreads();
+    if (tid < NPROF) {
+      unsigned long long v = 0;
+      for (int w = 0; w < NW; ++w) v += ep[w * NPROF + tid];
+      atomicAdd(a.prof + tid, v);
+    }
   }
 }
 
@@ -549,7 +563,11 @@ hipError_t lenet_bwd(const XSrc& x, const bf16_t* p1, const uint8_t* arg1, const
   if ((!x.x && !x.u8) || grid <= 0) return hipErrorInvalidValue;
   const int res = lenet_bwd_grid();
   if (res <= 0) return hipErrorInvalidValue;
-  BwdArgs a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, p1, arg1, dp2, arg2, w2, B, slab1, slab2, prof};
+  BwdArgs a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, p1, arg1, dp2, arg2, w2, B, slab1, slab2, prof, 0};
+  if (prof) {   // experiments only: skip bits 1 dgrad, 2 conv2 wgrad, 4 conv1 wgrad, 8 staging, 16 loop barriers
+    const char* e = getenv("MNISTX_BWD_SKIP");
+    a.skip = e ? atoi(e) : 0;
+  }
   const BwdKernel k = kBwd[(prof ? 4 : 0) + (x.u8 ? 2 : 0) + (x.idx ? 1 : 0)];
   void* args[] = {&a};
   return hipLaunchKernel((const void*)k, dim3(grid), dim3(NT), args, LDS_BYTES, st);

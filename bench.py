@@ -308,7 +308,8 @@ def main() -> int:
     # batch index (K10 fused into its staging); prep: one gather+normalise kernel per step
     mode = "u8" if args.fused_input else args.input
     fused_in = (args.impl == "hip" and mode != "prep" and getattr(net, "can_gather_input", lambda: True)()
-                and net.bind_u8_input(ds.images if mode == "u8" else ds.bf16_images()))
+                and net.bind_u8_input(ds.images if mode == "u8" else ds.bf16_images(),
+                                       bwd_images=None if mode == "u8" else ds.images))
     loader = DeviceLoader(ds, net.x0, net.labels, rank=rank, world=world, seed=args.seed,
                           idx_out=net.idx_buf if fused_in else None)
 

@@ -249,7 +249,7 @@ struct Stage {
 template <int H>
 DEV void dgrad_unit(const uint8_t* lds, int bB, int lane, int dylo, int dyhi, f32x4 (&acc)[4]) {
   constexpr int VLO = H ? 2 : 0, VHI = H ? 4 : 3, NU = H ? 3 : 4;
-#pragma unroll 1
+#pragma unroll 2
   for (int dy = dylo; dy <= dyhi; ++dy) {
     bf16x8 Bv[VHI - VLO + 1];
     const uint8_t* pb = lds + bB - dy * DY2_RS;

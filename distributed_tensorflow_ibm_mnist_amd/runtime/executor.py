@@ -515,6 +515,7 @@ class HipNet:
         # kernel (lenet_bwd.hip): dP1 stays in LDS, the weight gradients accumulate in
         # registers per block; fused_lenet_bwd=False runs the three convpool kernels
         self.fused_bwd = self.band_fwd and fused_lenet_bwd and not self.overlap
+        self.bwd_u8: Optional[torch.Tensor] = None    # uint8 twin of a bound bf16 dataset (bind_u8_input)
         if self.fused_bwd:
             res = kernels().lenet_bwd_blocks(batch)
             self.lb_slab1 = torch.zeros(res * 32 * 8, dtype=torch.float32, device=dev)
@@ -569,7 +570,7 @@ class HipNet:
         return (isinstance(first, ConvPoolLayer) and self.spec.in_channels == 1
                 and bool(kernels().convpool_u8_input(*first._geo())))
 
-    def bind_u8_input(self, images: torch.Tensor) -> bool:
+    def bind_u8_input(self, images: torch.Tensor, bwd_images: Optional[torch.Tensor] = None) -> bool:
         """Training steps read a resident dataset [n, H*W] directly through ``idx_buf``
         (filled by DeviceLoader(idx_out=...)), fusing the gather (K10,
         mnist_input.py:37-39) into the first fused conv's staging -- its forward and
@@ -579,7 +580,9 @@ class HipNet:
             per-step prep) -- 2x the uint8 footprint (94 MB for MNIST, nothing next
             to 288 GB of HBM) for no per-step conversion work.
         Eval / inference keep using ``x0``.  Returns False when the first layer
-        cannot (Cin != 1 etc.)."""
+        cannot (Cin != 1 etc.).  ``bwd_images``: the same rows as uint8, read by the fused
+        LeNet-5 conv backward when ``images`` is the bf16 copy (half the input bytes; its
+        in-kernel normalisation is bitwise the bf16 copy's, tests/test_lenet_bwd_gpu.py)."""
         first = self.layers[0]
         H, W = self.spec.input_hw
         if not (isinstance(first, ConvPoolLayer) and self.spec.in_channels == 1
@@ -589,6 +592,10 @@ class HipNet:
             return False
         self.idx_buf = torch.zeros(self.B, dtype=torch.int64, device=self.device)
         first.u8 = (images.contiguous(), self.idx_buf)
+        ok_bwd = (self.fused_bwd and bwd_images is not None and images.dtype == torch.bfloat16
+                  and bwd_images.dtype == torch.uint8
+                  and tuple(bwd_images.shape) == tuple(images.shape) and bwd_images.device == self.device)
+        self.bwd_u8 = bwd_images.contiguous() if ok_bwd else None
         return True
 
     # ------------------------------------------------------------------ step parts
@@ -631,7 +638,10 @@ class HipNet:
         src = l0._src()
         K = kernels()
         grid = K.lenet_bwd_blocks(nb)
-        K.lenet_bwd(src.get("u8", l0._xin()), l0.out, l0.arg, dp2, l1.arg, fp.bf16_view(l1.wname), nb,
+        x = src.get("u8", l0._xin())
+        if self.bwd_u8 is not None and l0.use_u8 and "idx" in src:
+            x = self.bwd_u8        # the uint8 copy of the bound bf16 dataset: half the bytes
+        K.lenet_bwd(x, l0.out, l0.arg, dp2, l1.arg, fp.bf16_view(l1.wname), nb,
                     self.lb_slab1, self.lb_slab2, grid, idx=src.get("idx"))
         _reduce(pending, self.lb_slab2, (grid, 208, 16, 25, 8, l1.spec.cin, l1.spec.cout, 200),
                 fp.grad_view(l1.wname), fp.grad_view(l1.bname))

@@ -102,7 +102,8 @@ class Replica:
         # eligibility first: a model that cannot gather (3-channel input, fp32 executor) never
         # gets a normalised bf16 copy of the whole split built for nothing
         fused_in = (impl == "hip" and mode != "prep" and getattr(self.net, "can_gather_input", lambda: True)()
-                    and self.net.bind_u8_input(self.train_ds.images if mode == "u8" else self.train_ds.bf16_images()))
+                    and self.net.bind_u8_input(self.train_ds.images if mode == "u8" else self.train_ds.bf16_images(),
+                                                bwd_images=None if mode == "u8" else self.train_ds.images))
         self.loader = DeviceLoader(self.train_ds, self.net.x0, self.net.labels, rank=self.rank, world=self.world,
                                    seed=seed, shard=shard, idx_out=self.net.idx_buf if fused_in else None)
         # hipGraph: single replica, or (dp_graph) the DP step with its RCCL all-reduces captured

@@ -160,13 +160,14 @@ def test_graph_replay_matches_eager(dev, K):
     assert torch.equal(nets[0].fp.params, nets[1].fp.params)
 
 
-@pytest.mark.parametrize("mode", ["u8", "bf16"])
+@pytest.mark.parametrize("mode", ["u8", "bf16", "bf16_u8bwd"])
 @pytest.mark.parametrize("model", ["lenet5", "reference_cnn"])
 def test_u8_input_path_bitwise_equal(dev, K, model, mode):
     """First fused conv gathering the resident dataset through the batch index (fused
-    K10) -- uint8 normalised in the kernels, or bf16 normalised once -- must equal
-    prep_images + bf16 x0, bitwise, through full train steps (forward, weight
-    gradient, update) and the Feistel index+label launch must equal the prep's."""
+    K10) -- uint8 normalised in the kernels, or bf16 normalised once (bf16_u8bwd: with
+    the fused LeNet-5 conv backward reading the uint8 twin) -- must equal prep_images +
+    bf16 x0, bitwise, through full train steps (forward, weight gradient, update) and the
+    Feistel index+label launch must equal the prep's."""
     from distributed_tensorflow_ibm_mnist_amd.data.synthetic import make_synthetic
     from distributed_tensorflow_ibm_mnist_amd.data.device_loader import DeviceDataset, DeviceLoader
     spec = get_model(model, 1)
@@ -176,13 +177,15 @@ def test_u8_input_path_bitwise_equal(dev, K, model, mode):
     ds = DeviceDataset(imgs, labs, dev)
     a = HipNet(spec, 200, dev, init, opt)
     b = HipNet(spec, 200, dev, init, opt)
-    assert b.bind_u8_input(ds.images if mode == "u8" else ds.bf16_images())
+    assert b.bind_u8_input(ds.images if mode == "u8" else ds.bf16_images(),
+                           bwd_images=ds.images if mode == "bf16_u8bwd" else None)
+    assert (b.bwd_u8 is not None) == (mode == "bf16_u8bwd" and b.fused_bwd)
     la = DeviceLoader(ds, a.x0, a.labels, seed=9)
     lb = DeviceLoader(ds, b.x0, b.labels, seed=9, idx_out=b.idx_buf)
     for _ in range(3):
         la.next()
         lb.next()
-        if mode == "bf16":       # the once-normalised rows are bitwise the per-step prep's
+        if mode != "u8":         # the once-normalised rows are bitwise the per-step prep's
             assert torch.equal(ds.bf16_images()[b.idx_buf].view_as(a.x0), a.x0)
         a.train_step()
         b.train_step()

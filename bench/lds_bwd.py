@@ -8,10 +8,9 @@ LDS cycle per group when conflict-free; extra distinct dwords on one bank add cy
   ds_write_b64       4 x 16 contiguous lanes,   bank (a/4) % 32
   ds_write_b128      8 x 8 contiguous lanes,    bank (a/4) % 32
 Prints the average cycles per group (1.0 = conflict-free) of every access pattern for
-the strides given on the command line / the defaults the kernel uses, and searches the
-image strides.
+the strides given on the command line / the defaults the kernel uses.
 
-    python bench/lds_bwd.py [--search]
+    python bench/lds_bwd.py [NAME=value ...]
 """
 import itertools
 import sys
@@ -55,10 +54,11 @@ def kitem(g, rho, q):
     return 4 * (g & 1) + q, 2 * (g >> 1) + rho
 
 
-DEF = dict(DY2_IMG=4640, DY2_RS=384, P1_IMG=3168, DP1_IMG=3152, X_IMG=2592, X_RS=80)
-# conv2 weight-gradient tiles: tap pairs (25 = the bias row, a broadcast ONES cell)
-C2_TAPS = [(0, 1), (2, 3), (5, 6), (7, 8), (10, 11), (12, 13), (4, 9),
-           (15, 16), (17, 18), (14, 19), (20, 21), (22, 23), (24, 25)]
+DEF = dict(DY2_IMG=3872, DY2_RS=384, P1_IMG=3808, P1_RS=272, D_IMG=3920, D_RS=280, X_IMG=2592, X_RS=80)
+# conv2 weight-gradient tiles: (first tap, second-tap step): one pixel apart (+1) or one
+# row apart (+5; tap 29 = discarded rows)
+C2_TILES = [(0, 1), (2, 1), (5, 1), (7, 1), (10, 1), (12, 1), (15, 1), (17, 1), (20, 1), (22, 1),
+            (4, 5), (14, 5), (24, 5)]
 
 
 def dgrad_b(S, dy=1, p=2, v=2):
@@ -68,7 +68,10 @@ def dgrad_b(S, dy=1, p=2, v=2):
         img, rr = i >> 1, i & 1
         y = 2 * p + rr - dy
         x = 2 * v + (g >> 1)
-        out.append(img * S["DY2_IMG"] + (y + 1) * S["DY2_RS"] + x * 32 + 16 * (g & 1))
+        if 0 <= y <= 9:
+            out.append(img * S["DY2_IMG"] + y * S["DY2_RS"] + x * 32 + 16 * (g & 1))
+        else:
+            out.append(10 ** 6 + x * 32 + 16 * (g & 1))   # the shared zero row
     return cycles(out, 16, "b128")
 
 
@@ -78,47 +81,97 @@ def dgrad_w(S, p=2, u=3):
         i, g = l & 15, l >> 4
         img, rr = i >> 1, i & 1
         xq = 2 * u + (g >> 1)
-        out.append(img * S["DP1_IMG"] + ((2 * p + rr) * 14 + xq) * 16 + 8 * (g & 1))
+        out.append(img * S["D_IMG"] + (2 * p + rr) * S["D_RS"] + xq * 16 + 8 * (g & 1))
     return cycles(out, 8, "w64")
 
 
 def c2w(S, s, rho, t):
-    """(A pool1 tr read of M-tile t, B dY2 tr read) of k-step s, read rho."""
+    """(A pool1 tr read of M-tile t, B dY2 tr read) of k-step s (dY2 row s // 3, pixels
+    4 (s % 3) .. + 3), read rho."""
     a, b = [], []
+    y, x0 = s // 3, 4 * (s % 3)
     for l in range(64):
         g, q, p = l >> 4, (l >> 2) & 3, l & 3
         img, sub = kitem(g, rho, q)
-        pix = 4 * s + sub
-        y, x = pix // 10, pix % 10
-        tap = C2_TAPS[t][p >> 1]
-        if tap == 25:
-            a.append(100000 + 8 * (p & 1))     # ONES cell
-        else:
-            a.append(img * S["P1_IMG"] + ((y + tap // 5) * 14 + x + tap % 5) * 16 + 8 * (p & 1))
-        b.append(img * S["DY2_IMG"] + (y + 1) * S["DY2_RS"] + x * 32 + 8 * p)
+        x = x0 + sub
+        tap0, step = C2_TILES[t]
+        tap = tap0 + (p >> 1) * step
+        a.append(img * S["P1_IMG"] + (y + tap // 5) * S["P1_RS"] + (x + tap % 5) * 16 + 8 * (p & 1))
+        b.append(img * S["DY2_IMG"] + y * S["DY2_RS"] + x * 32 + 8 * p)
     return cycles(a, 8, "tr"), cycles(b, 8, "tr")
 
 
 def c1w(S, sig, s, rho, t=0):
+    """(A input tr read of M-tile t, B dP1 / code tr read) of k-step s (window row s // 2,
+    windows 4 (s % 2) .. + 3 of parity set sig)."""
     a, b = [], []
+    yp, xi0 = s // 2, 4 * (s % 2)
     for l in range(64):
         g, q, p = l >> 4, (l >> 2) & 3, l & 3
         img, sub = kitem(g, rho, q)
-        tw = min(4 * s + sub, 97)
-        yp, xi = tw // 7, tw % 7
+        xi = xi0 + sub
         xp = 2 * xi + sig
         a.append(img * S["X_IMG"] + (2 * yp + 2 * t + (p >> 1)) * S["X_RS"] + (4 * xi + 4 * (p & 1) + 4 * sig) * 2)
-        b.append(img * S["DP1_IMG"] + (yp * 14 + xp) * 16 + 8 * (p & 1))
+        b.append(img * S["D_IMG"] + yp * S["D_RS"] + xp * 16 + 8 * (p & 1))
     return cycles(a, 8, "tr"), cycles(b, 8, "tr")
+
+
+def stores(S, rotate=True):
+    """Staging stores per tile: dY2 unpool (threads < 400: pooled pixel x 8 channels, 4
+    window positions d; `rotate`: the d of instruction i is rotated per lane), pool1 and code
+    windows (wave pair per image, lane r -> window r / r + 128), input quads."""
+    r = {}
+    tot = n = 0
+    for w in range(7):
+        for i in range(4):
+            addrs = []
+            for l in range(64):
+                t = 64 * w + l
+                if t >= 400:
+                    addrs.append(None)
+                    continue
+                im, rr = t // 50, t % 50
+                pw, hf = rr >> 1, rr & 1
+                yp, xp = pw // 5, pw % 5
+                d = (i ^ ((xp >> 1) & 1)) if rotate else i
+                addrs.append(im * S["DY2_IMG"] + (2 * yp + (d >> 1)) * S["DY2_RS"] + (2 * xp + (d & 1)) * 32 + 16 * hf)
+            tot += cycles(addrs, 16, "w128")
+            n += 1
+    r["dY2_w128"] = tot / n
+    for name, rs, size, kind in (("P1_w128", S["P1_RS"], 16, "w128"), ("CD_w64x2", S["D_RS"], 8, "w64")):
+        tot = n = 0
+        for wp in range(2):
+            for ch in range(2):
+                addrs = []
+                for l in range(64):
+                    q = l + 64 * wp + 128 * ch
+                    if q >= 196:
+                        addrs.append(None)
+                        continue
+                    addrs.append((q // 14) * rs + (q % 14) * 16)
+                tot += cycles(addrs, size, kind)
+                n += 1
+        r[name] = tot / n
+    tot = n = 0
+    for wp in range(2):
+        for ch in range(2):
+            addrs = []
+            for l in range(64):
+                q = l + 64 * wp + 128 * ch
+                addrs.append(None if q >= 196 else (q // 7 + 2) * S["X_RS"] + (4 * (q % 7) + 4) * 2)
+            tot += cycles(addrs, 8, "w64")
+            n += 1
+    r["X_w64"] = tot / n
+    return r
 
 
 def report(S):
     r = {}
-    r["dgrad_B_b128"] = sum(dgrad_b(S, dy, p, v) for dy in range(5) for p in range(1, 6) for v in range(5)) / 125
+    r["dgrad_B_b128"] = sum(dgrad_b(S, dy, p, v) for dy in range(5) for p in range(7) for v in range(5)) / 175
     r["dgrad_W_w64"] = sum(dgrad_w(S, p, u) for p in range(7) for u in range(7)) / 49
     ca = cb = 0
     n = 0
-    for s in range(25):
+    for s in range(30):
         for rho in range(2):
             for t in range(13):
                 x, y = c2w(S, s, rho, t)
@@ -130,7 +183,7 @@ def report(S):
     ca = cb = 0
     n = 0
     for sig in range(2):
-        for s in range(25):
+        for s in range(28):
             for rho in range(2):
                 for t in range(3):
                     x, y = c1w(S, sig, s, rho, t)
@@ -139,6 +192,7 @@ def report(S):
                     n += 1
     r["c1w_A_tr"] = ca / n
     r["c1w_B_tr"] = cb / n
+    r.update(stores(S))
     return r
 
 
@@ -148,27 +202,6 @@ def main():
         if "=" in a:
             k, v = a.split("=")
             S[k] = int(v)
-    if "--search" in sys.argv:
-        best = {}
-        for name, keys, cands in [
-                ("dY2", ["DY2_IMG"], [4608 + 16 * i for i in range(0, 32)]),
-                ("p1", ["P1_IMG"], [3136 + 16 * i for i in range(0, 32)]),
-                ("X", ["X_IMG", "X_RS"], [(xi, xr) for xr in (72, 80, 88, 96, 104) for xi in range(32 * xr, 32 * xr + 512, 16)]),
-                ]:
-            res = []
-            for c in cands:
-                T = dict(S)
-                if len(keys) == 1:
-                    T[keys[0]] = c
-                else:
-                    T.update(dict(zip(keys, c)))
-                rr = report(T)
-                key = {"dY2": rr["dgrad_B_b128"] + rr["c2w_B_tr"], "p1": rr["c2w_A_tr"],
-                       "X": rr["c1w_A_tr"]}[name]
-                res.append((key, c))
-            res.sort()
-            print(name, res[:5])
-        return
     for k, v in report(S).items():
         print(f"{k:14s} {v:.3f}")
 

@@ -83,7 +83,7 @@ def main():
     # wgrad, 8 staging, 16 loop barriers
     skip_us = {}
     pr_buf = torch.zeros(8, dtype=torch.int64, device=dev)
-    for sk in (0, 1, 2, 4, 8, 16, 7, 15):
+    for sk in [int(v) for v in os.environ.get("SKIPS", "0,1,2,4,8,16,7,15").split(",")]:
         os.environ["MNISTX_BWD_SKIP"] = str(sk)
         skip_us[sk] = round(timeit(lambda: K.lenet_bwd(ds, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx,
                                                        prof=pr_buf)), 1)

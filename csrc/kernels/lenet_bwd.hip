@@ -37,7 +37,7 @@
 //    wave-uniform step offset (one VALU add per operand per k-step, no index decode), the
 //    32 lanes of one transposed read cover the 8 images of one pixel, and with the image
 //    strides below the reads are conflict-free (bench/lds_bwd.py; conv2 tiles pair taps one
-//    pixel apart, except three pairs one row apart: 2-way).
+//    pixel or one 17-pixel row apart: 4 dwords mod 8 either way).
 // 16 waves (4 per SIMD) share a tile in two phases (two barriers): [store input / codes of
 // this tile, load the next tile's data, one dgrad unit + conv2 weight-gradient k-steps of
 // the wave's tile group] -> [conv1 weight-gradient k-steps of the wave's parity set, store
@@ -57,25 +57,27 @@ constexpr int NT = 1024, NW = 16, T = 8;
 constexpr int NWIN1 = 196;                                 // pool1 windows per image
 // ---- LDS layout (bytes); image / row strides from bench/lds_bwd.py (bank model)
 constexpr int AF_OFF = 0, AF_SZ = 15 * 64 * 16;            // dgrad A fragments [dy*3+j][lane] x 16 B
-constexpr int DY2_RS = 384, DY2_IMG = 4640;                // dY2 [img][row -1..10][12 px][16 co] bf16
+constexpr int DY2_RS = 384, DY2_IMG = 3872;                // dY2 [img][10 rows][12 px][16 co] bf16 (px 10, 11 zero)
 constexpr int DY2_OFF = AF_OFF + AF_SZ, DY2_SZ = T * DY2_IMG;
-constexpr int P1_RS = 256, P1_IMG = 3616;                  // pool1 [img][14][16 px][8] bf16 (px 14, 15 zero)
-constexpr int P1_OFF = DY2_OFF + DY2_SZ, P1_SZ = T * P1_IMG;
+constexpr int ZERO_OFF = DY2_OFF + DY2_SZ;                 // one zero dY2 row: the dgrad's rows -1 / 10
+constexpr int P1_RS = 272, P1_IMG = 3808;                  // pool1 [img][14][17 px][8] bf16 (px 14.. zero)
+constexpr int P1_OFF = ZERO_OFF + DY2_RS, P1_SZ = T * P1_IMG;
 constexpr int X_RS = 80, X_IMG = 2592;                     // input [img][row -2..29][col -4..35] bf16
 constexpr int X_OFF = P1_OFF + P1_SZ, X_SZ = T * X_IMG;
-constexpr int D_RS = 272, D_IMG = 3808;                    // dP1 / codes [img][14][17 windows][8] x 2 B
+constexpr int D_RS = 280, D_IMG = 3920;                    // dP1 / codes [img][14][17.5 windows][8] x 2 B
 constexpr int DP1_OFF = X_OFF + X_SZ, D_SZ = T * D_IMG;
 constexpr int CD_OFF = DP1_OFF + D_SZ;                     // argmax codes (u16 per channel)
 constexpr int LDS_BYTES = CD_OFF + D_SZ;
 static_assert(LDS_BYTES <= 163840, "one workgroup per CU");
-static_assert(12 * DY2_RS <= DY2_IMG && 32 * X_RS <= X_IMG && 14 * P1_RS <= P1_IMG && 14 * D_RS <= D_IMG, "");
+static_assert(10 * DY2_RS <= DY2_IMG && 32 * X_RS <= X_IMG && 14 * P1_RS <= P1_IMG && 14 * D_RS <= D_IMG, "");
+static_assert((ZERO_OFF - DY2_OFF) % 256 == 0, "zero row bank-aligned with the dY2 rows (bench/lds_bwd.py)");
 constexpr int C2MAX = 4;                                   // conv2 tiles per wave group (max)
 static_assert(NW * C2MAX * 256 * 4 <= LDS_BYTES && NW * 6 * 256 * 4 + NW * 8 * 4 <= LDS_BYTES, "epilogue scratch");
 
 // conv2 weight-gradient M tiles: rows h * 8 + ci are tap C2_TAP0[t] + h (tiles 0-9: taps one
 // pixel apart) or C2_TAP0[t] + 5 h (tiles 10-12: one row apart; tap 29 = discarded rows).
 // Tile groups: waves 4G .. 4G + 3 own the tiles of group G (G0: 0-3, G1: 4, 5, 10, G2: 6, 7,
-// 11, G3: 8, 9, 12 -- the row-apart pairs, whose reads are 2-way bank conflicted, spread).
+// 11, G3: 8, 9, 12).
 constexpr int C2_TAP0[13] = {0, 2, 5, 7, 10, 12, 15, 17, 20, 22, 4, 14, 24};
 constexpr int C2_GT[4][C2MAX] = {{0, 1, 2, 3}, {4, 5, 10, -1}, {6, 7, 11, -1}, {8, 9, 12, -1}};
 __constant__ int c2_gt[4][C2MAX] = {{0, 1, 2, 3}, {4, 5, 10, -1}, {6, 7, 11, -1}, {8, 9, 12, -1}};
@@ -190,8 +192,9 @@ struct Stage {
         }
         *(u32x2*)(lds + X_OFF + img * X_IMG + (y + 2) * X_RS + (4 * k + 4) * 2) = u32x2{lo, hi};
         const uint32_t l4 = a1[i] & 0x0f0f0f0fu, h4 = (a1[i] >> 4) & 0x0f0f0f0fu;   // codes c 0..3 / 4..7
-        *(u32x4*)(lds + CD_OFF + img * D_IMG + yp * D_RS + xp * 16) =
-            u32x4{bytes01(l4), bytes23(l4), bytes01(h4), bytes23(h4)};
+        uint8_t* cd = lds + CD_OFF + img * D_IMG + yp * D_RS + xp * 16;   // 8-byte aligned rows
+        *(u32x2*)cd = u32x2{bytes01(l4), bytes23(l4)};
+        *(u32x2*)(cd + 8) = u32x2{bytes01(h4), bytes23(h4)};
       }
     }
   }
@@ -231,14 +234,16 @@ struct Stage {
     const int tid = wave * 64 + ln;
     if (tid < 400) {
       const int im = tid / 50, rr = tid - 50 * im, w = rr >> 1, yp = w / 5, xp = w - 5 * yp;
-      const int o = DY2_OFF + im * DY2_IMG + (2 * yp + 1) * DY2_RS + 2 * xp * 32 + 16 * (rr & 1);
+      const int o = DY2_OFF + im * DY2_IMG + 2 * yp * DY2_RS + 2 * xp * 32 + 16 * (rr & 1);
       const uint32_t e[4] = {bytes01(c2[0]), bytes23(c2[0]), bytes01(c2[1]), bytes23(c2[1])};
+      const int rot = (xp >> 1) & 1;   // window column of store i rotated per lane: 2-way -> 1.4 (bench/lds_bwd.py)
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
+      for (int i = 0; i < 4; ++i) {
+        const int d = i ^ rot;
         const uint32_t dd = (uint32_t)d * 0x00010001u;
         const u32x4 v = {sel_eq(dp[0], e[0], dd), sel_eq(dp[1], e[1], dd), sel_eq(dp[2], e[2], dd),
                          sel_eq(dp[3], e[3], dd)};
-        *(u32x4*)(lds + o + (d >> 1) * DY2_RS + (d & 1) * 32) = v;
+        *(u32x4*)(lds + o + (i >> 1) * DY2_RS + (d & 1) * 32) = v;
       }
     }
   }
@@ -247,12 +252,13 @@ struct Stage {
 // dgrad unit: column pairs 4H .. 4H + 3 (H = 1: 4..6) of one output row pair, kernel rows
 // dylo..dyhi.  B fragment v (x pairs 2v, 2v + 1) and A fragment j feed column pair v + 2 - j.
 template <int H>
-DEV void dgrad_unit(const uint8_t* lds, int bB, int lane, int dylo, int dyhi, f32x4 (&acc)[4]) {
+DEV void dgrad_unit(const uint8_t* lds, int bB, int bZ, int orow, int lane, int dylo, int dyhi, f32x4 (&acc)[4]) {
   constexpr int VLO = H ? 2 : 0, VHI = H ? 4 : 3, NU = H ? 3 : 4;
 #pragma unroll 2
   for (int dy = dylo; dy <= dyhi; ++dy) {
     bf16x8 Bv[VHI - VLO + 1];
-    const uint8_t* pb = lds + bB - dy * DY2_RS;
+    const int r = orow - dy;                                 // dY2 row; -1 / 10: the shared zero row
+    const uint8_t* pb = lds + ((unsigned)r <= 9u ? bB - dy * DY2_RS : bZ);
 #pragma unroll
     for (int v = VLO; v <= VHI; ++v) Bv[v - VLO] = *(const bf16x8*)(pb + 64 * v);
 #pragma unroll
@@ -274,19 +280,19 @@ template <int G>
 DEV void c2w_steps(const uint8_t* lds, int ks0, int ks1, int ln, f32x4 (&acc2)[C2MAX]) {
   const int g = ln >> 4, q = (ln >> 2) & 3, p = ln & 3;
   const int img = 4 * (g & 1) + q, sub = 2 * (g >> 1), hA = p >> 1, pc = p & 1;
-  const int bB = DY2_OFF + img * DY2_IMG + DY2_RS + sub * 32 + 8 * p;
+  const int bB = DY2_OFF + img * DY2_IMG + sub * 32 + 8 * p;
   const int aB = P1_OFF + img * P1_IMG + sub * 16 + 8 * pc;
   const int aP = aB + hA * 16, aR = aB + hA * P1_RS;        // second tap: next pixel / next row
   constexpr int NT2 = G == 0 ? 4 : 3;
 #pragma unroll 2
   for (int s = ks0; s < ks1; ++s) {
     const int y = s / 3, x0 = 4 * (s - 3 * y);              // uniform
-    const int sb = bB + y * DY2_RS + x0 * 32, sa = (y * 16 + x0) * 16;
+    const int sb = bB + y * DY2_RS + x0 * 32, sa = y * P1_RS + x0 * 16;
     const bf16x8 Bf = frag(tr4(lds, sb), tr4(lds, sb + 32));
 #pragma unroll
     for (int t = 0; t < NT2; ++t) {
       const int tile = C2_GT[G][t], tap = C2_TAP0[tile];
-      const int base = (tile < 10 ? aP : aR) + sa + ((tap / 5) * 16 + tap % 5) * 16;
+      const int base = (tile < 10 ? aP : aR) + sa + (tap / 5) * P1_RS + (tap % 5) * 16;
       acc2[t] = mfma16(frag(tr4(lds, base), tr4(lds, base + 16)), Bf, acc2[t]);
     }
   }
@@ -384,9 +390,10 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
       f32x4 acc[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int bB = DY2_OFF + img * DY2_IMG + (orow + 1) * DY2_RS + (g >> 1) * 32 + (g & 1) * 16;
-      if (hx) dgrad_unit<1>(lds, bB, ln, dylo, dyhi, acc);
-      else dgrad_unit<0>(lds, bB, ln, dylo, dyhi, acc);
+      const int lo = (g >> 1) * 32 + (g & 1) * 16;
+      const int bB = DY2_OFF + img * DY2_IMG + orow * DY2_RS + lo, bZ = ZERO_OFF + lo;
+      if (hx) dgrad_unit<1>(lds, bB, bZ, orow, ln, dylo, dyhi, acc);
+      else dgrad_unit<0>(lds, bB, bZ, orow, ln, dylo, dyhi, acc);
       // dP1 (bf16) for the conv1 weight gradient; the conv1 bias gradient from the fp32
       // sums of the active windows (code != 4, i.e. bit 2 of the nibble clear)
       const int sh = 4 * (g & 1);

@@ -170,7 +170,7 @@ struct Stage {
     for (int i = 0; i < NCH; ++i) {
       const uint32_t q = (uint32_t)(r + 128 * i);
       const uint32_t oob = q < NWIN1 ? 0u : BUF_OOB;
-      a1[i] = buf_b32(ra1, 4u * q + oob);
+      a1[i] = a.skip & 32 ? 0u : buf_b32(ra1, 4u * q + oob);   // (skip: prof experiments only)
       if constexpr (U8) x[i] = u32x2{buf_b32(rx, 4u * q + oob), 0u};
       else x[i] = buf_b64(rx, 8u * q + oob);
     }
@@ -213,7 +213,7 @@ struct Stage {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const uint32_t q = (uint32_t)(r + 128 * i);
-      p1[i] = buf_b128(rp1, q < NWIN1 ? 16u * q : BUF_OOB);
+      p1[i] = a.skip & 32 ? u32x4{0u, 0u, 0u, 0u} : buf_b128(rp1, q < NWIN1 ? 16u * q : BUF_OOB);
     }
   }
   // unpooled dY2 (ReLU mask folded in the codes) and pool1 with channel 6 = 1.0 (the conv2
@@ -571,7 +571,8 @@ hipError_t lenet_bwd(const XSrc& x, const bf16_t* p1, const uint8_t* arg1, const
   const int res = lenet_bwd_grid();
   if (res <= 0) return hipErrorInvalidValue;
   BwdArgs a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, p1, arg1, dp2, arg2, w2, B, slab1, slab2, prof, 0};
-  if (prof) {   // experiments only: skip bits 1 dgrad, 2 conv2 wgrad, 4 conv1 wgrad, 8 staging, 16 loop barriers
+  if (prof) {   // experiments only: skip bits 1 dgrad, 2 conv2 wgrad, 4 conv1 wgrad, 8 staging, 16 loop
+                // barriers, 32 pool1 / code loads
     const char* e = getenv("MNISTX_BWD_SKIP");
     a.skip = e ? atoi(e) : 0;
   }

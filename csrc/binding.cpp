@@ -964,6 +964,59 @@ void f32_lrn_bwd(Tensor x, Tensor dy, Tensor dx, int64_t P_, int64_t C, int64_t 
          "f32_lrn_bwd");
 }
 
+// fp32 conv1 (28x28x1 -> 32, 5x5 SAME) + bias + ReLU + 2x2 max-pool in one kernel, and its
+// weight gradient from dL/d pool + the codes (tests/test_f32_gpu.py)
+bool f32_conv1_pool_ok(int64_t H, int64_t W, int64_t C, int64_t OH, int64_t OW, int64_t KH, int64_t KW, int64_t ph,
+                       int64_t pw, int64_t Cout) {
+  return mnistx::f32_conv1_ok((int)H, (int)W, (int)C, (int)OH, (int)OW, (int)KH, (int)KW, (int)ph, (int)pw, (int)Cout);
+}
+void f32_conv1_fwd_pool(Tensor x, Tensor w, optional<Tensor> bias, Tensor y, Tensor arg, int64_t Nb) {
+  check(x, at::kFloat, Nb * 784, "x");
+  check(w, at::kFloat, 25 * 32, "w");
+  check(y, at::kFloat, Nb * 196 * 32, "y");
+  check(arg, at::kByte, Nb * 196 * 32, "arg");
+  TORCH_CHECK(((uintptr_t)y.data_ptr() % 16) == 0 && ((uintptr_t)arg.data_ptr() % 4) == 0, "y / arg alignment");
+  hip_ok(mnistx::f32_conv1_fwd_pool(P<const float>(x), P<const float>(w), (int)Nb, Fo(bias, 32, "bias"), P<float>(y),
+                                    P<uint8_t>(arg), cur_stream()),
+         "f32_conv1_fwd_pool");
+}
+int64_t f32_conv1_wgrad_unpool_grid() { return mnistx::f32_conv1_wgrad_unpool_grid(); }
+void f32_conv1_wgrad_unpool(Tensor x, Tensor dp, Tensor codes, Tensor slab, int64_t Nb, int64_t splits) {
+  check(x, at::kFloat, Nb * 784, "x");
+  check(dp, at::kFloat, Nb * 196 * 32, "dp");
+  check(codes, at::kByte, Nb * 196 * 32, "codes");
+  TORCH_CHECK(splits >= 1 && splits <= 65535, "splits");
+  check(slab, at::kFloat, splits * 26 * 32, "slab");
+  hip_ok(mnistx::f32_conv1_wgrad_unpool(P<const float>(x), P<const float>(dp), P<const uint8_t>(codes), (int)Nb,
+                                        (int)splits, P<float>(slab), cur_stream()),
+         "f32_conv1_wgrad_unpool");
+}
+
+// fp32 LRN + 2x2 max-pool fused (the reference's norm2 -> pool2) and its backward
+bool f32_lrn_pool_ok(int64_t H, int64_t W, int64_t C, int64_t r) {
+  return mnistx::f32_lrn_pool_ok((int)H, (int)W, (int)C, (int)r);
+}
+void f32_lrn_pool_fwd(Tensor x, Tensor y, Tensor arg, int64_t Nb, int64_t H, int64_t W, int64_t C, int64_t r,
+                      double bias, double alpha, double beta) {
+  check(x, at::kFloat, Nb * H * W * C, "x");
+  check(y, at::kFloat, Nb * (H / 2) * (W / 2) * C, "y");
+  check(arg, at::kByte, Nb * (H / 2) * (W / 2) * C, "arg");
+  hip_ok(mnistx::f32_lrn_pool_fwd(P<const float>(x), (int)Nb, (int)H, (int)W, (int)C, (int)r, (float)bias,
+                                  (float)alpha, (float)beta, P<float>(y), P<uint8_t>(arg), cur_stream()),
+         "f32_lrn_pool_fwd");
+}
+void f32_lrn_pool_bwd(Tensor x, Tensor dy, Tensor arg, Tensor dx, int64_t Nb, int64_t H, int64_t W, int64_t C,
+                      int64_t r, double bias, double alpha, double beta, bool relu_mask) {
+  check(x, at::kFloat, Nb * H * W * C, "x");
+  check(dy, at::kFloat, Nb * (H / 2) * (W / 2) * C, "dy");
+  check(arg, at::kByte, Nb * (H / 2) * (W / 2) * C, "arg");
+  check(dx, at::kFloat, Nb * H * W * C, "dx");
+  hip_ok(mnistx::f32_lrn_pool_bwd(P<const float>(x), P<const float>(dy), P<const uint8_t>(arg), (int)Nb, (int)H,
+                                  (int)W, (int)C, (int)r, (float)bias, (float)alpha, (float)beta, relu_mask ? 1 : 0,
+                                  P<float>(dx), cur_stream()),
+         "f32_lrn_pool_bwd");
+}
+
 void f32_softmax_ce(Tensor logits, int64_t ldl, optional<Tensor> labels, int64_t B, int64_t NC, double scale,
                     optional<Tensor> dlogits, int64_t ldd, optional<Tensor> stats, optional<Tensor> probs,
                     optional<Tensor> work) {
@@ -1029,6 +1082,13 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("f32_maxpool_bwd", &f32_maxpool_bwd);
   m.def("f32_lrn_fwd", &f32_lrn_fwd);
   m.def("f32_lrn_bwd", &f32_lrn_bwd);
+  m.def("f32_conv1_pool_ok", &f32_conv1_pool_ok);
+  m.def("f32_conv1_fwd_pool", &f32_conv1_fwd_pool);
+  m.def("f32_conv1_wgrad_unpool_grid", &f32_conv1_wgrad_unpool_grid);
+  m.def("f32_conv1_wgrad_unpool", &f32_conv1_wgrad_unpool);
+  m.def("f32_lrn_pool_ok", &f32_lrn_pool_ok);
+  m.def("f32_lrn_pool_fwd", &f32_lrn_pool_fwd);
+  m.def("f32_lrn_pool_bwd", &f32_lrn_pool_bwd);
   m.def("f32_softmax_ce", &f32_softmax_ce, py::arg("logits"), py::arg("ldl"), py::arg("labels"), py::arg("B"),
         py::arg("NC"), py::arg("scale"), py::arg("dlogits"), py::arg("ldd"), py::arg("stats"), py::arg("probs"),
         py::arg("work") = py::none());

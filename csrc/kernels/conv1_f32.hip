@@ -174,6 +174,170 @@ __global__ __launch_bounds__(NT1) void conv1_f32_wgrad_k(const float* __restrict
   }
 }
 
+// conv1 + bias + ReLU + 2x2/2 max-pool (the reference's conv1 -> pool1, mnist_input.py:142-150)
+// in one pass: the 1.64 GB conv1 output at B = 16384 is never written.  Units are (output row
+// pair, 16-column segment), each lane computes the same MFMAs as conv1_f32_fwd_k for its pixel
+// on both rows; the vertical pool is in the lane, the horizontal one with the lane i ^ 1
+// partner (DPP quad swap).  Pooled values and the first-maximum position order (0..3 =
+// row-major window position) are maxpool_f32's; the code is 4 where the pooled ReLU output is
+// 0 (no gradient: the unfused backward's y > 0 mask).  Even lanes store channels 0-15, odd
+// lanes 16-31 of their pooled pixel.
+DEV float quad_swap(float v) {   // lane i <- lane i ^ 1
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xb1, 0xf, 0xf, false));   // quad_perm 1,0,3,2
+}
+constexpr int PH = IH / 2, PW = IW / 2;
+__global__ __launch_bounds__(NT1) void conv1_f32_fwd_pool_k(const float* __restrict__ x, const float* __restrict__ w,
+                                                            const float* __restrict__ bias, int B,
+                                                            float* __restrict__ y, uint32_t* __restrict__ arg) {
+  __shared__ __attribute__((aligned(16))) float tile[4 * TSZ];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  for (int e = tid; e < 4 * TSZ; e += NT1) tile[e] = 0.f;
+  float a[3][4][2];
+#pragma unroll
+  for (int b = 0; b < 3; ++b)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) {
+        const int kh = 2 * b + (g >> 1), kw = 4 * (g & 1) + s;
+        a[b][s][nf] = (kh < KS && kw < KS) ? w[(kh * KS + kw) * COUT + 16 * nf + i] : 0.f;
+      }
+  float bs[2][4];
+#pragma unroll
+  for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bs[nf][r] = bias ? bias[16 * nf + 4 * g + r] : 0.f;
+  const int cp = i & 1;    // this lane's column parity: window positions cp (row 0) and 2 + cp (row 1)
+  for (int img = blockIdx.x; img < B; img += gridDim.x) {
+    __syncthreads();
+    stage_image(tile, x, img, tid);
+    __syncthreads();
+    // units (row pair, 16-column segment): 14 x 2, dealt over the 4 waves
+    for (int u = wave; u < 2 * PH; u += NT1 / 64) {
+      const int rp = u >> 1, x0 = 16 * (u & 1);
+      f32x4 acc[2][2];   // [row][nf]
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        acc[h][0] = acc[h][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int row = 2 * rp + h;
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+          const int kh = 2 * b + (g >> 1);
+          const f32x4 v = *(const f32x4*)run4(tile, (row + kh) * TC + x0 + i + 4 * (g & 1));
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int nf = 0; nf < 2; ++nf)
+              acc[h][nf] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[b][s][nf], v[s], acc[h][nf], 0, 0, 0);
+        }
+      }
+      // bias + ReLU, then the window max in position order 0 (r0 c0), 1 (r0 c1), 2 (r1 c0), 3 (r1 c1)
+      f32x4 best[2];
+      uint32_t code[2] = {0u, 0u};
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v[4];
+          const float m0 = fmaxf(acc[0][nf][r] + bs[nf][r], 0.f), m1 = fmaxf(acc[1][nf][r] + bs[nf][r], 0.f);
+          const float o0 = quad_swap(m0), o1 = quad_swap(m1);      // the partner column's rows 0 / 1
+          v[0] = cp ? o0 : m0;
+          v[1] = cp ? m0 : o0;
+          v[2] = cp ? o1 : m1;
+          v[3] = cp ? m1 : o1;
+          float bv = v[0];
+          uint32_t bd = 0;
+#pragma unroll
+          for (int d = 1; d < 4; ++d)
+            if (v[d] > bv) { bv = v[d]; bd = d; }   // first maximum wins (TF MaxPool)
+          best[nf][r] = bv;
+          code[nf] |= (bv > 0.f ? bd : 4u) << (8 * r);
+        }
+      const int pc = (x0 + i) >> 1;
+      if (pc < PW) {
+        const int64_t pp = (int64_t)img * (PH * PW) + rp * PW + pc;
+        const int nf = cp;                     // even lanes: channels 0-15, odd lanes 16-31
+        *(f32x4*)(y + pp * COUT + 16 * nf + 4 * g) = nf ? best[1] : best[0];
+        arg[(pp * COUT + 16 * nf + 4 * g) >> 2] = nf ? code[1] : code[0];
+      }
+    }
+  }
+}
+
+// conv1 weight gradient from dL/d pool1 and the pool codes (the unfused pool backward's
+// dL/d conv1 -- 1.64 GB at B = 16384 -- is never written): a pixel's gradient is its pooled
+// pixel's where the code names its window position, else 0 (code 4: ReLU output 0).
+// Otherwise conv1_f32_wgrad_k.
+__global__ __launch_bounds__(NT1) void conv1_f32_wgrad_unpool_k(const float* __restrict__ x,
+                                                                const float* __restrict__ dp,
+                                                                const uint8_t* __restrict__ codes, int B,
+                                                                float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) float tile[4 * TSZ];
+  __shared__ float red[NT1 / 64][2][2][64][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  for (int e = tid; e < 4 * TSZ; e += NT1) tile[e] = 0.f;
+  int toff[2];
+  float aconst[2];
+#pragma unroll
+  for (int mf = 0; mf < 2; ++mf) {
+    const int m = 16 * mf + i;
+    toff[mf] = m < KS * KS ? (m / KS) * TC + (m % KS) : -1;
+    aconst[mf] = m == KS * KS ? 1.f : 0.f;
+  }
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int mf = 0; mf < 2; ++mf)
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf) acc[mf][nf] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int img = blockIdx.x; img < B; img += gridDim.x) {
+    __syncthreads();
+    stage_image(tile, x, img, tid);
+    __syncthreads();
+    const float* dpi = dp + (int64_t)img * (PH * PW) * COUT;
+    const uint8_t* cdi = codes + (int64_t)img * (PH * PW) * COUT;
+#pragma unroll 4
+    for (int q = wave; q < IH * (IW / 4); q += NT1 / 64) {
+      const int row = q / (IW / 4), c4 = q - row * (IW / 4);
+      const int col = 4 * c4 + g;
+      const int pp = (row >> 1) * PW + (col >> 1);
+      const uint32_t pos = (uint32_t)(2 * (row & 1) + (col & 1));
+      const float d0 = dpi[pp * COUT + i], d1 = dpi[pp * COUT + 16 + i];
+      const uint32_t k0 = cdi[pp * COUT + i], k1 = cdi[pp * COUT + 16 + i];
+      const float b0 = k0 == pos ? d0 : 0.f, b1 = k1 == pos ? d1 : 0.f;
+      const int base = row * TC + col;
+#pragma unroll
+      for (int mf = 0; mf < 2; ++mf) {
+        const float av = toff[mf] >= 0 ? tile[base + toff[mf]] : aconst[mf];
+        acc[mf][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b0, acc[mf][0], 0, 0, 0);
+        acc[mf][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b1, acc[mf][1], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int mf = 0; mf < 2; ++mf)
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wave][mf][nf][lane][r] = acc[mf][nf][r];
+  __syncthreads();
+  if (wave == 0) {
+    float* out = slab + (int64_t)blockIdx.x * WROWS * COUT;
+#pragma unroll
+    for (int mf = 0; mf < 2; ++mf)
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = ((red[0][mf][nf][lane][r] + red[1][mf][nf][lane][r]) + red[2][mf][nf][lane][r]) +
+                          red[3][mf][nf][lane][r];
+          const int m = 16 * mf + 4 * g + r;
+          if (m < WROWS) out[m * COUT + 16 * nf + i] = v;
+        }
+  }
+}
+
 int resident(const void* k) {
   int dev = 0, cus = 0, pc = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k, NT1, 0) == hipSuccess && hipGetDevice(&dev) == hipSuccess &&
@@ -198,6 +362,24 @@ hipError_t f32_conv1_fwd(const float* x, const float* w, int Nb, const float* bi
   if (Nb <= 0) return hipSuccess;
   static const int n = resident((const void*)conv1_f32_fwd_k);
   hipLaunchKernelGGL(conv1_f32_fwd_k, dim3(cap_grid(Nb < n ? Nb : n)), dim3(NT1), 0, st, x, w, bias, relu, Nb, y);
+  return hipGetLastError();
+}
+hipError_t f32_conv1_fwd_pool(const float* x, const float* w, int Nb, const float* bias, float* y, uint8_t* arg,
+                              hipStream_t st) {
+  if (Nb <= 0) return hipSuccess;
+  static const int n = resident((const void*)conv1_f32_fwd_pool_k);
+  hipLaunchKernelGGL(conv1_f32_fwd_pool_k, dim3(cap_grid(Nb < n ? Nb : n)), dim3(NT1), 0, st, x, w, bias, Nb, y,
+                     (uint32_t*)arg);
+  return hipGetLastError();
+}
+int f32_conv1_wgrad_unpool_grid() {
+  static const int n = resident((const void*)conv1_f32_wgrad_unpool_k);
+  return n;
+}
+hipError_t f32_conv1_wgrad_unpool(const float* x, const float* dp, const uint8_t* codes, int Nb, int splits,
+                                  float* slab, hipStream_t st) {
+  if (Nb <= 0 || splits <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(conv1_f32_wgrad_unpool_k, dim3(splits), dim3(NT1), 0, st, x, dp, codes, Nb, slab);
   return hipGetLastError();
 }
 hipError_t f32_conv1_wgrad(const float* x, const float* dy, int Nb, int splits, float* slab, hipStream_t st) {

@@ -588,6 +588,95 @@ __global__ __launch_bounds__(256) void lrn_f32_bwd_v4_k(const float* __restrict_
   }
 }
 
+// LRN then 2x2/2 max-pool in one pass (the reference's norm2 -> pool2, mnist_input.py:166-172):
+// the LRN output (the 822 MB conv2-sized tensor at B = 16384) is never written.  Thread =
+// (pooled pixel, 4 channels), the C/4 lanes of a pixel in one DPP row; each of the 4 window
+// positions is normalised exactly as lrn_f32_fwd_v4_k does and the max taken in position
+// order with the first maximum winning (maxpool_f32_fwd_v4_k), so outputs and codes are
+// bitwise the unfused pair's.
+__global__ __launch_bounds__(256) void lrn_pool_f32_fwd_k(const float* __restrict__ x, int total, FastDiv fC4,
+                                                          FastDiv fOW, FastDiv fOH, int C, int r, float bias,
+                                                          float alpha, float beta, float* __restrict__ y,
+                                                          uint32_t* __restrict__ arg) {
+  const int W = 2 * (int)fOW.d, G = (int)fC4.d;
+  for (int b0 = blockIdx.x * blockDim.x; b0 < total; b0 += gridDim.x * blockDim.x) {
+    const int t = b0 + threadIdx.x;
+    const bool ok = t < total;
+    const int tt = ok ? t : total - 1;
+    const int win = fC4.div(tt), cv = fC4.mod(tt, win);
+    const int rr = fOW.div(win), ow = fOW.mod(win, rr);
+    const int n = fOH.div(rr), oh = fOH.mod(rr, n);
+    const int64_t base = (((int64_t)n * 2 * fOH.d + 2 * oh) * W + 2 * ow) * C + 4 * cv;
+    f32x4 best = {0.f, 0.f, 0.f, 0.f};
+    uint32_t code = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const f32x4 v = ok ? *(const f32x4*)(x + base + ((d >> 1) * W + (d & 1)) * C) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 sq = v * v;
+      const f32x4 sw = win4(sq, threadIdx.x % G, G, r);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float o = v[j] * pow_neg(fmaf(alpha, sw[j], bias), beta);
+        if (d == 0 || o > best[j]) {
+          best[j] = o;
+          code = (code & ~(0xffu << (8 * j))) | ((uint32_t)d << (8 * j));
+        }
+      }
+    }
+    if (ok) {
+      *(f32x4*)(y + (int64_t)t * 4) = best;
+      arg[t] = code;
+    }
+  }
+}
+
+// the backward of that pair: un-pool dL/d pool into the LRN output gradient of each window
+// position (the code's position only) and run the LRN backward there (lrn_f32_bwd_v4_k's
+// arithmetic), writing dL/d(LRN input) once -- the unpooled gradient is never stored.
+__global__ __launch_bounds__(256) void lrn_pool_f32_bwd_k(const float* __restrict__ x, const float* __restrict__ dy,
+                                                          const uint32_t* __restrict__ arg, int total, FastDiv fC4,
+                                                          FastDiv fOW, FastDiv fOH, int C, int r, float bias,
+                                                          float alpha, float beta, int relu_mask,
+                                                          float* __restrict__ dx) {
+  const int W = 2 * (int)fOW.d, G = (int)fC4.d;
+  for (int b0 = blockIdx.x * blockDim.x; b0 < total; b0 += gridDim.x * blockDim.x) {
+    const int t = b0 + threadIdx.x;
+    const bool ok = t < total;
+    const int tt = ok ? t : total - 1;
+    const int win = fC4.div(tt), cv = fC4.mod(tt, win);
+    const int rr = fOW.div(win), ow = fOW.mod(win, rr);
+    const int n = fOH.div(rr), oh = fOH.mod(rr, n);
+    const int64_t base = (((int64_t)n * 2 * fOH.d + 2 * oh) * W + 2 * ow) * C + 4 * cv;
+    const f32x4 gp = ok ? *(const f32x4*)(dy + (int64_t)t * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint32_t a = ok ? arg[t] : 0u;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int64_t off = base + ((d >> 1) * W + (d & 1)) * C;
+      const f32x4 v = ok ? *(const f32x4*)(x + off) : f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 g;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[j] = ((a >> (8 * j)) & 0xffu) == (uint32_t)d ? gp[j] : 0.f;
+      const f32x4 s = win4(v * v, threadIdx.x % G, G, r);
+      f32x4 nb, tv;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float nn = fmaf(alpha, s[j], bias);
+        nb[j] = pow_neg(nn, beta);
+        tv[j] = g[j] * v[j] * nb[j] / nn;
+      }
+      const f32x4 u = win4(tv, threadIdx.x % G, G, r);
+      f32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float dd = g[j] * nb[j] - 2.f * alpha * beta * v[j] * u[j];
+        if (relu_mask && !(v[j] > 0.f)) dd = 0.f;
+        o[j] = dd;
+      }
+      if (ok) *(f32x4*)(dx + off) = o;
+    }
+  }
+}
+
 int ew_grid(int64_t n) {
   const int64_t g = (n + 255) / 256;
   return (int)(g < 8192 ? (g < 1 ? 1 : g) : 8192);
@@ -710,6 +799,34 @@ hipError_t f32_lrn_bwd(const float* x, const float* dy, int64_t P, int C, int r,
   }
   hipLaunchKernelGGL(lrn_f32_bwd_k, dim3(ew_grid(P * C)), dim3(256), 0, st, x, dy, P, C, r, bias, alpha, beta,
                      relu_mask, dx);
+  return hipGetLastError();
+}
+
+bool f32_lrn_pool_ok(int H, int W, int C, int r) {
+  return (C == 32 || C == 64) && r <= 4 && H % 2 == 0 && W % 2 == 0;
+}
+hipError_t f32_lrn_pool_fwd(const float* x, int Nb, int H, int W, int C, int r, float bias, float alpha, float beta,
+                            float* y, uint8_t* arg, hipStream_t st) {
+  const int OH = H / 2, OW = W / 2;
+  if (!f32_lrn_pool_ok(H, W, C, r) || !al16h(x) || !al16h(y) || !al16h(arg) ||
+      (int64_t)Nb * OH * OW * (C / 4) >= ((int64_t)1 << 30))
+    return hipErrorInvalidValue;
+  if (Nb <= 0) return hipSuccess;
+  const int total = Nb * OH * OW * (C / 4);
+  hipLaunchKernelGGL(lrn_pool_f32_fwd_k, dim3(ew_grid(total)), dim3(256), 0, st, x, total, FastDiv(C / 4), FastDiv(OW),
+                     FastDiv(OH), C, r, bias, alpha, beta, y, (uint32_t*)arg);
+  return hipGetLastError();
+}
+hipError_t f32_lrn_pool_bwd(const float* x, const float* dy, const uint8_t* arg, int Nb, int H, int W, int C, int r,
+                            float bias, float alpha, float beta, int relu_mask, float* dx, hipStream_t st) {
+  const int OH = H / 2, OW = W / 2;
+  if (!f32_lrn_pool_ok(H, W, C, r) || !al16h(x) || !al16h(dy) || !al16h(arg) || !al16h(dx) ||
+      (int64_t)Nb * OH * OW * (C / 4) >= ((int64_t)1 << 30))
+    return hipErrorInvalidValue;
+  if (Nb <= 0) return hipSuccess;
+  const int total = Nb * OH * OW * (C / 4);
+  hipLaunchKernelGGL(lrn_pool_f32_bwd_k, dim3(ew_grid(total)), dim3(256), 0, st, x, dy, (const uint32_t*)arg, total,
+                     FastDiv(C / 4), FastDiv(OW), FastDiv(OH), C, r, bias, alpha, beta, relu_mask, dx);
   return hipGetLastError();
 }
 

@@ -147,6 +147,13 @@ int f32_conv1_wgrad_grid();
 hipError_t f32_conv1_fwd(const float* x, const float* w, int Nb, const float* bias, int relu, float* y,
                          hipStream_t st);
 hipError_t f32_conv1_wgrad(const float* x, const float* dy, int Nb, int splits, float* slab, hipStream_t st);
+// fused with the following 2x2 max-pool: pooled output [Nb][14][14][32] + codes (one byte per
+// channel: window position 0..3, 4 = ReLU output 0); the weight gradient from dL/d pool + codes
+hipError_t f32_conv1_fwd_pool(const float* x, const float* w, int Nb, const float* bias, float* y, uint8_t* arg,
+                              hipStream_t st);
+int f32_conv1_wgrad_unpool_grid();
+hipError_t f32_conv1_wgrad_unpool(const float* x, const float* dp, const uint8_t* codes, int Nb, int splits,
+                                  float* slab, hipStream_t st);
 bool f32_halo_wgrad_ok(int H, int W, int C, int OH, int OW, int KH, int KW, int ph, int pw, int Cout);
 int f32_halo_wgrad_grid();
 hipError_t f32_halo_wgrad(const float* x, const float* dy, int Nb, int splits, float* slab, hipStream_t st);
@@ -164,6 +171,13 @@ hipError_t f32_lrn_fwd(const float* x, int64_t P, int C, int r, float bias, floa
                        hipStream_t st);
 hipError_t f32_lrn_bwd(const float* x, const float* dy, int64_t P, int C, int r, float bias, float alpha, float beta,
                        int relu_mask, float* dx, hipStream_t st);
+// LRN then 2x2/2 max-pool fused (fp32; the pool's codes: first-maximum window position per
+// channel), and its backward straight to dL/d(LRN input)
+bool f32_lrn_pool_ok(int H, int W, int C, int r);
+hipError_t f32_lrn_pool_fwd(const float* x, int Nb, int H, int W, int C, int r, float bias, float alpha, float beta,
+                            float* y, uint8_t* arg, hipStream_t st);
+hipError_t f32_lrn_pool_bwd(const float* x, const float* dy, const uint8_t* arg, int Nb, int H, int W, int C, int r,
+                            float bias, float alpha, float beta, int relu_mask, float* dx, hipStream_t st);
 hipError_t f32_softmax_ce(const float* logits, int ldl, const int32_t* labels, int B, int NC, float scale, float* dl,
                           int ldd, float* stats, float* probs, float* work, hipStream_t st);
 hipError_t f32_prep_images(const uint8_t* src, const int64_t* idx, const int32_t* lab_src, int B, int HW, int Csrc,

@@ -14,10 +14,13 @@ as 16-byte-vector kernels.  At B=16384 that took the fp32 step from 26.0 to
 deterministic split-K reduce are the shared K9 / misc.hip kernels, so the
 checkpoint layout, hooks and data-parallel buckets are identical.
 
-Layer semantics follow the reference graph exactly (no fusion): conv + bias +
-ReLU (``mnist_input.py:142-145``), 2x2/2 SAME max-pool (first maximum wins),
-LRN across channels, dense + bias (+ ReLU).  ReLU backward masks are folded
-into the producer of each gradient, as in the bf16 plan.
+Layer semantics follow the reference graph exactly: conv + bias + ReLU
+(``mnist_input.py:142-145``), 2x2/2 SAME max-pool (first maximum wins), LRN across
+channels, dense + bias (+ ReLU).  ReLU backward masks are folded into the producer of
+each gradient, as in the bf16 plan.  Two pairs run fused (``fuse=True``, default):
+conv1 + pool1 (ConvPoolF: the 1.64 GB conv1 output and its gradient never reach HBM at
+B = 16384) and norm2 + pool2 (LRNPoolF: the 822 MB LRN output and its gradient); both
+keep the unfused pair's arithmetic (tests/test_f32_gpu.py compares them).
 """
 from __future__ import annotations
 
@@ -132,6 +135,98 @@ class LRNF(_L):
                                   self.in_relu)
 
 
+class ConvPoolF(_L):
+    """conv1 (28x28x1 -> 32, 5x5 SAME) + bias + ReLU + 2x2/2 max-pool as one kernel
+    (conv1_f32.hip): the conv output is never materialised; the weight gradient un-pools
+    dL/d pool through the codes inside its staging.  First layer only (no data gradient)."""
+    has_params = True
+
+    def __init__(self, conv: Conv, pool: MaxPool, x: torch.Tensor, fp: FlatParams, B: int, dev):
+        self.spec, self.pool_spec, self.name, self.x, self.fp = conv, pool, conv.name, x, fp
+        self.in_relu = False
+        _, self.H, self.W, self.C = x.shape
+        self.out = _f32(B, self.H // 2, self.W // 2, conv.cout, device=dev)
+        self.arg = torch.zeros(self.out.shape, dtype=torch.uint8, device=dev)
+        self.wname, self.bname = f"{conv.name}/weights", f"{conv.name}/biases"
+        self.M = conv.kh * conv.kw * self.C + 1
+        # the unfused conv1 weight gradient's split count: same image -> block assignment and
+        # summation order, so the two graphs' gradients are bitwise equal
+        ph, pw = Fk.conv_pads(conv.kh, conv.kw, conv.padding)
+        self.splits = kernels().f32_conv_wgrad_pref_splits(self.H, self.W, self.C, self.H, self.W, conv.kh, conv.kw,
+                                                           ph, pw, conv.cout)
+        self.slab = _f32(self.splits * self.M * conv.cout, device=dev)
+
+    @staticmethod
+    def fits(conv, pool, x: torch.Tensor) -> bool:
+        if not (isinstance(conv, Conv) and isinstance(pool, MaxPool) and conv.relu and pool.k == 2 and pool.s == 2
+                and pool.padding == "SAME"):
+            return False
+        _, H, W, C = x.shape
+        OH, OW = Fk.conv_out_hw(H, W, conv.kh, conv.kw, conv.padding)
+        ph, pw = Fk.conv_pads(conv.kh, conv.kw, conv.padding)
+        return bool(kernels().f32_conv1_pool_ok(H, W, C, OH, OW, conv.kh, conv.kw, ph, pw, conv.cout))
+
+    def fwd(self, nb: int) -> None:
+        kernels().f32_conv1_fwd_pool(self.x, self.fp.param_view(self.wname), self.fp.param_view(self.bname),
+                                     self.out, self.arg, nb)
+
+    def bwd_weight(self, nb: int, dy: torch.Tensor) -> None:
+        s, K = self.spec, kernels()
+        S = min(self.splits, max(1, nb))
+        K.f32_conv1_wgrad_unpool(self.x, dy, self.arg, self.slab, nb, S)
+        K.splitk_reduce(self.slab, S, self.M, s.cout, s.kh * s.kw, self.C, self.C, s.cout, s.kh * s.kw * self.C,
+                        self.fp.grad_view(self.wname), self.fp.grad_view(self.bname), 1.0)
+
+    def bwd_data(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor]) -> None:
+        assert dx is None, "ConvPoolF is a first layer"
+
+    def conv_output(self, n: int) -> torch.Tensor:
+        """The unpooled bias+ReLU conv output of the first n images (monitoring only)."""
+        s = self.spec
+        ph, pw = Fk.conv_pads(s.kh, s.kw, s.padding)
+        out = torch.empty(n, self.H, self.W, s.cout, dtype=torch.float32, device=self.x.device)
+        kernels().f32_conv_fwd(self.x, self.fp.param_view(self.wname), out, n, self.H, self.W, self.C, self.H,
+                               self.W, s.kh, s.kw, ph, pw, s.cout, self.fp.param_view(self.bname), s.relu)
+        return out
+
+
+class LRNPoolF(_L):
+    """LRN then 2x2/2 max-pool in one pass (the reference's norm2 -> pool2): the LRN output
+    is never materialised; the backward un-pools and runs the LRN backward in one kernel.
+    Outputs, codes and gradients are bitwise the unfused LRNF + PoolF pair's."""
+
+    def __init__(self, lrn: LRN, pool: MaxPool, x: torch.Tensor, in_relu: bool, B: int, dev):
+        self.spec, self.pool_spec, self.name, self.x, self.in_relu = lrn, pool, lrn.name, x, in_relu
+        _, self.H, self.W, self.C = x.shape
+        self.out = _f32(B, self.H // 2, self.W // 2, self.C, device=dev)
+        self.arg = torch.zeros(self.out.shape, dtype=torch.uint8, device=dev)
+
+    @staticmethod
+    def fits(lrn, pool, x: torch.Tensor) -> bool:
+        if not (isinstance(lrn, LRN) and isinstance(pool, MaxPool) and pool.k == 2 and pool.s == 2
+                and pool.padding == "SAME"):
+            return False
+        _, H, W, C = x.shape
+        return bool(kernels().f32_lrn_pool_ok(H, W, C, lrn.depth_radius))
+
+    def fwd(self, nb: int) -> None:
+        s = self.spec
+        kernels().f32_lrn_pool_fwd(self.x, self.out, self.arg, nb, self.H, self.W, self.C, s.depth_radius, s.bias,
+                                   s.alpha, s.beta)
+
+    def bwd_data(self, nb: int, dy, dx) -> None:
+        if dx is not None:
+            s = self.spec
+            kernels().f32_lrn_pool_bwd(self.x, dy, self.arg, dx, nb, self.H, self.W, self.C, s.depth_radius,
+                                       s.bias, s.alpha, s.beta, self.in_relu)
+
+    def lrn_output(self, n: int) -> torch.Tensor:
+        s = self.spec
+        out = torch.empty(n, self.H, self.W, self.C, dtype=torch.float32, device=self.x.device)
+        kernels().f32_lrn_fwd(self.x, out, n * self.H * self.W, self.C, s.depth_radius, s.bias, s.alpha, s.beta)
+        return out
+
+
 class DenseF(_L):
     has_params = True
 
@@ -170,7 +265,10 @@ class HipNetF32:
     precision = "fp32"
 
     def __init__(self, spec: ModelSpec, batch: int, device, init: Dict[str, torch.Tensor],
-                 opt: Optional[OptConfig] = None):
+                 opt: Optional[OptConfig] = None, fuse: bool = True):
+        """``fuse``: conv1 + pool1 and LRN + pool runs as one kernel each where the kernels
+        cover the geometry (ConvPoolF, LRNPoolF); False keeps the reference's layer-by-layer
+        graph (tests compare the two)."""
         dev = torch.device(device)
         assert dev.type == "cuda", "HipNetF32 runs the HIP kernels (use --impl=torch on CPU)"
         self.spec, self.B, self.device = spec, batch, dev
@@ -186,8 +284,18 @@ class HipNetF32:
         self.labels = torch.zeros(batch, dtype=torch.int32, device=dev)
         self.layers: List[_L] = []
         x, in_relu = self.x0, False
+        skip = -1
         for i, L in enumerate(spec.layers):
-            if isinstance(L, Conv):
+            if i == skip:
+                continue
+            nxt = spec.layers[i + 1] if i + 1 < len(spec.layers) else None
+            if fuse and i == 0 and ConvPoolF.fits(L, nxt, x):
+                lay = ConvPoolF(L, nxt, x, self.fp, batch, dev)
+                skip, in_relu = i + 1, False
+            elif fuse and LRNPoolF.fits(L, nxt, x):
+                lay = LRNPoolF(L, nxt, x, in_relu, batch, dev)
+                skip, in_relu = i + 1, False
+            elif isinstance(L, Conv):
                 lay = ConvF(L, x, in_relu, self.fp, batch, dev)
                 in_relu = L.relu
             elif isinstance(L, MaxPool):
@@ -278,11 +386,21 @@ class HipNetF32:
         return out
 
     def activation(self, layer_name: str) -> torch.Tensor:
+        """A layer's output tensor (a fused pair's pool output under either name's pool)."""
         for lay in self.layers:
-            if lay.name == layer_name:
+            if lay.name == layer_name and not isinstance(lay, (ConvPoolF, LRNPoolF)):
+                return lay.out
+            if getattr(lay, "pool_spec", None) is not None and lay.pool_spec.name == layer_name:
                 return lay.out
         raise KeyError(layer_name)
 
     def layer_activation(self, layer_name: str, n: int) -> torch.Tensor:
-        """``<layer>/<layer>:0`` (main.py:97-100): unfused, so the conv ReLU output itself."""
-        return self.activation(layer_name)[:max(1, min(n, self.B))]
+        """``<layer>/<layer>:0`` (main.py:97-100) for the first n images: the conv ReLU output
+        itself (recomputed for a fused conv + pool, monitoring only)."""
+        n = max(1, min(n, self.B))
+        for lay in self.layers:
+            if lay.name == layer_name and isinstance(lay, ConvPoolF):
+                return lay.conv_output(n)
+            if lay.name == layer_name and isinstance(lay, LRNPoolF):
+                return lay.lrn_output(n)
+        return self.activation(layer_name)[:n]

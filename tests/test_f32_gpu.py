@@ -100,7 +100,7 @@ def test_f32_pool_lrn(dev, K):
     assert rel_err(dl, xt.grad * (xl > 0)) < 1e-5
 
 
-@pytest.mark.parametrize("model,cin", [("reference_cnn", 3), ("lenet5", 1), ("mlp", 1)])
+@pytest.mark.parametrize("model,cin", [("reference_cnn", 3), ("reference_cnn", 1), ("lenet5", 1), ("mlp", 1)])
 def test_f32_step_matches_oracle(dev, K, model, cin):
     """The whole fp32 step (fwd + CE + explicit bwd + fused update) vs the fp32
     oracle at rtol 1e-4 -- no bf16 noise floor in this mode."""
@@ -214,3 +214,35 @@ def test_f32_conv1_kernels(dev, K, grid_cap, Nb, S, cap):
     ref_w = torch.nn.grad.conv2d_weight(xc, (32, 1, 5, 5), dy.permute(0, 3, 1, 2), padding=2)
     assert rel_err(tot[:25].view(5, 5, 1, 32), ref_w.permute(2, 3, 1, 0)) < 1e-5
     assert rel_err(tot[25], dy.sum((0, 1, 2))) < 1e-5
+
+
+def test_f32_fused_pairs_bitwise(dev, K):
+    """conv1 + pool1 (ConvPoolF) and norm2 + pool2 (LRNPoolF) fused vs the reference's
+    layer-by-layer graph at a batch where the persistent conv1 kernels loop over several
+    images per block: logits and pool outputs bitwise equal; gradients to fp32 rounding
+    (the fused backward kernels contract their FMAs differently)."""
+    from distributed_tensorflow_ibm_mnist_amd.runtime.executor_f32 import ConvPoolF, HipNetF32, LRNPoolF
+    torch.manual_seed(2)
+    spec = get_model("reference_cnn", 1)
+    init = torch_ref.init_params(spec, seed=4)
+    B = 5000
+    x = torch.rand(B, 28, 28, 1, device=dev) - 0.5
+    y = torch.randint(0, 10, (B,), device=dev, dtype=torch.int32)
+    res = []
+    for fuse in (True, False):
+        net = HipNetF32(spec, B, dev, init, OptConfig(lr0=0.05), fuse=fuse)
+        kinds = [type(l).__name__ for l in net.layers]
+        assert ("ConvPoolF" in kinds and "LRNPoolF" in kinds) == fuse, kinds
+        net.x0.copy_(x)
+        net.labels.copy_(y)
+        logits = net.forward().clone()
+        net.loss_and_grad()
+        net.backward()
+        torch.cuda.synchronize()
+        res.append((logits, {n: net.fp.grad_view(n).clone() for n in init}, net.activation("pool1").clone(),
+                    net.activation("pool2").clone(), net.layer_activation("conv1", 7).clone(),
+                    net.layer_activation("norm2", 7).clone()))
+    for i, what in ((0, "logits"), (2, "pool1"), (3, "pool2"), (4, "conv1 act"), (5, "norm2 act")):
+        assert torch.equal(res[0][i], res[1][i]), what
+    errs = {n: rel_err(res[0][1][n], res[1][1][n]) for n in init}
+    assert max(errs.values()) < 1e-6, errs

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Reference-CNN conv1 weight gradient with the norm1 backward folded in: refc1_wgrad.hip vs
+the folded convpool_wgrad it replaces, at the benchmark batch (one JSON line).
+
+    python bench/micro_refc1.py [--batch 16384] [--iters 50]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_tensorflow_ibm_mnist_amd.ops._ext import kernels  # noqa: E402
+
+LRN = (1.0, 0.001 / 9.0, 0.75)
+
+
+def timed(fn, iters):
+    best = float("inf")
+    for _ in range(3):
+        fn()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(iters):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        best = min(best, a.elapsed_time(b) * 1e3 / iters)
+    return round(best, 1)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=16384)
+    ap.add_argument("--iters", type=int, default=50)
+    args = ap.parse_args()
+    K, dev, B = kernels(), torch.device("cuda:0"), args.batch
+    torch.manual_seed(0)
+    x = (torch.rand(B, 28, 28, 1, device=dev) - 0.5).to(torch.bfloat16)
+    w = (torch.randn(5, 5, 1, 32, device=dev) * 0.2).to(torch.bfloat16)
+    b = torch.randn(32, device=dev) * 0.05
+    P1 = torch.empty(B, 14, 14, 32, dtype=torch.bfloat16, device=dev)
+    A1 = torch.empty(B, 14, 14, 32, dtype=torch.uint8, device=dev)
+    K.convpool_fwd(x, w, b, 32, P1, A1, B, 1, 32, 5, 2, 28, 28)
+    dn = (torch.randn(B, 14, 14, 32, device=dev) * 0.1).to(torch.bfloat16)
+    grid = K.refc1_wgrad_blocks(B)
+    slab = torch.empty(grid * 48 * 32, device=dev)
+    cgrid = K.convpool_wgrad_grid(1, 32, 5, 2, 28, 28)
+    cslab = torch.empty(cgrid * K.convpool_rows(1, 32, 5, 2, 28, 28) * 32, device=dev)
+    res = {"B": B, "grid": grid,
+           "refc1_us": timed(lambda: K.refc1_wgrad(x, dn, P1, A1, slab, grid, B, *LRN), args.iters),
+           "convpool_fold_us": timed(lambda: K.convpool_wgrad(x, dn, A1, cslab, cgrid, B, 1, 32, 5, 2, 28, 28, lrn_p=P1,
+                                                              lrn_bias=LRN[0], lrn_alpha=LRN[1], lrn_beta=LRN[2],
+                                                              lrn_r=4), args.iters)}
+    # the HBM floor: dL/d norm1 + pool1 (bf16) + codes + the images, once each
+    gb = B * (196 * 32 * 5 + 784 * 2) / 1e9
+    res["bytes_GB"] = round(gb, 3)
+    res["refc1_TBps"] = round(gb / res["refc1_us"] * 1e-3 * 1e6, 2)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

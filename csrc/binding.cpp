@@ -839,6 +839,32 @@ void lenet_bwd(Tensor x, Tensor p1, Tensor arg1, Tensor dp2, Tensor arg2, Tensor
          "lenet_bwd");
 }
 
+// Reference-CNN conv1 weight gradient with the norm1 backward folded in (refc1_wgrad.hip).
+// x / u8 / idx as for convpool_wgrad (cfg RefC1g); dn = dL/d norm1, p1 = pool1, arg = pool1 codes.
+void refc1_wgrad(Tensor x, Tensor dn, Tensor p1, Tensor arg, Tensor slab, int64_t grid, int64_t B, double lrn_bias,
+                 double lrn_alpha, double lrn_beta, optional<Tensor> u8, optional<Tensor> idx) {
+  const int cfg = mnistx::convpool_config(1, 32, 5, 2, 28, 28);
+  TORCH_CHECK(cfg >= 0, "refc1_wgrad: no RefC1 geometry");
+  TORCH_CHECK(B >= 1 && B < (int64_t)INT32_MAX / 4, "B");
+  const auto src = cp_src(x, u8, idx, cfg, B, 784);
+  if (src.x) TORCH_CHECK(reinterpret_cast<uintptr_t>(src.x) % 8 == 0, "x must be 8-byte aligned");
+  const int64_t np = B * 196 * 32;
+  check(dn, at::kBFloat16, np, "dn");
+  check(p1, at::kBFloat16, np, "p1");
+  check(arg, at::kByte, np, "arg");
+  for (const Tensor* t : {&dn, &p1})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "dn / p1 must be 16-byte aligned");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(arg.data_ptr()) % 8 == 0, "arg must be 8-byte aligned");
+  TORCH_CHECK(lrn_beta == 0.75, "refc1_wgrad: LRN beta 0.75 only");
+  const int res = mnistx::refc1_wgrad_blocks((int)B);
+  TORCH_CHECK(res > 0, "refc1_wgrad: occupancy query failed");
+  TORCH_CHECK(grid >= 1 && grid <= res, "refc1_wgrad: grid must be in [1, ", res, "] (one block per CU, <= tiles)");
+  check(slab, at::kFloat, grid * 48 * 32, "slab");
+  hip_ok(mnistx::refc1_wgrad(src, BF(dn), BF(p1), P<const uint8_t>(arg), (int)B, (float)lrn_bias, (float)lrn_alpha,
+                             (float)lrn_beta, P<float>(slab), (int)grid, cur_stream()),
+         "refc1_wgrad");
+}
+
 // ---------------------------------------------------------------- fp32 (reference precision) path
 const float* Fo(const optional<Tensor>& t, int64_t need, const char* name) {
   if (!t.has_value() || !t->defined()) return nullptr;
@@ -1180,6 +1206,14 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("lenet_bwd_blocks", [](int64_t B) {
     const int n = mnistx::lenet_bwd_blocks((int)B);
     TORCH_CHECK(n > 0, "lenet_bwd_blocks: occupancy query failed");
+    return (int64_t)n;
+  });
+  m.def("refc1_wgrad", &refc1_wgrad, py::arg("x"), py::arg("dn"), py::arg("p1"), py::arg("arg"), py::arg("slab"),
+        py::arg("grid"), py::arg("B"), py::arg("lrn_bias"), py::arg("lrn_alpha"), py::arg("lrn_beta"),
+        py::arg("u8") = py::none(), py::arg("idx") = py::none());
+  m.def("refc1_wgrad_blocks", [](int64_t B) {
+    const int n = mnistx::refc1_wgrad_blocks((int)B);
+    TORCH_CHECK(n > 0, "refc1_wgrad_blocks: occupancy query failed");
     return (int64_t)n;
   });
   m.attr("ARCH") = "gfx950";

@@ -116,6 +116,13 @@ hipError_t lenet_bwd(const XSrc& x, const bf16_t* p1, const uint8_t* arg1, const
                      const bf16_t* w2, int B, float* slab1, float* slab2, int grid, hipStream_t st,
                      unsigned long long* prof = nullptr);
 
+// ---- refc1_wgrad.hip: reference-CNN conv1 weight gradient with the norm1 (LRN, radius 4, beta
+// 0.75) backward folded in: dn = dL/d norm1, p1 = pool1 (the LRN input), arg = pool1 codes (one
+// byte per channel), all [B][196][32].  slab [grid][48][32] in convpool_wgrad's RefC1g layout.
+int refc1_wgrad_blocks(int B);       // the grid for a batch (one block per CU, <= tiles); <= 0: error
+hipError_t refc1_wgrad(const XSrc& x, const bf16_t* dn, const bf16_t* p1, const uint8_t* arg, int B, float bias,
+                       float alpha, float beta, float* slab, int grid, hipStream_t st);
+
 // ---- lenet_band.hip: LeNet-5 conv1+pool1+conv2+pool2 forward on banded MFMA tiles
 // (one persistent kernel; bf16 images only).  x.x = [n][784] images (x.idx: per-sample
 // rows, else sample b = row b).  p1/arg1 (convpool cfg-0 layouts) are written only when

@@ -1,0 +1,316 @@
+// Reference-CNN conv1 weight gradient with the norm1 backward folded in, gfx950 (bf16).
+//
+// conv1 (5x5 SAME, 28x28x1 -> 32) -> ReLU -> pool1 (2x2/2) -> norm1 (LRN, radius 4):
+// /root/reference/mnist_input.py:142-151, differentiated by compute_gradients (:262).  Per
+// 4-image tile the kernel
+//   1. applies the LRN backward to dL/d norm1 (with the pool1 activations, lrn_bwd8: the
+//      same arithmetic and bf16 rounding as lrn_bwd_k) and keeps dP1 = dL/d pool1 in LDS,
+//      with the pool argmax codes (one u16 per channel; 4 = ReLU output 0);
+//   2. accumulates dW1 as the pool-window-phase GEMM of lenet_bwd.hip's conv1 part:
+//      C[(ty, tx)][(c, d)] = sum over windows w of X[2yp + ty - 2][2xp + tx - 2] *
+//      dP1[w][c] [code(w, c) == d], folded to dW1[dy][dx][c] = sum_d C[(dy + a, dx + b)][(c, d)]
+//      at the end (d = 2a + b; tx taken by window x parity: two accumulator sets).
+// Every product is a v_mfma_f32_16x16x32_bf16 on ds_read_b64_tr_b16 fragments; K items are
+// (window, image) with the 4 images fastest over window rows padded to 8 per parity set, so
+// a k-step is one window row: lane addresses are a per-lane base plus a uniform step, and
+// with the strides below every read is bank-conflict-free (per 32-lane half, in dwords mod
+// 64: A = 26 q + 20 ty&1 + 2 (xi + pc) + {0, 1}, B = 4 q + 32 xi + 2 pc + {0, 1}; equal
+// addresses are broadcasts).  16 waves: wave w owns parity set w & 1, channel group (w >> 1) & 3
+// (8 channels x 4 window positions = 2 N tiles) and half (w >> 3) of the 14 window rows.
+// The conv1 bias gradient is the sum of the active windows' dP1.  One deterministic split-K
+// slab [grid][48][32] per launch in convpool_wgrad's layout (rows kh * 8 + kw, bias 40), so
+// the executor's splitk_reduce is the same.
+//
+// Replaces convpool_wgrad_k<RefC1g> with its LRN fold (259.9 us at B = 16384, 6.8 % MFMA
+// busy, VALU/MFMA 37.5: profiles/r4/refcnn/).
+#include "common.h"
+#include "launchers.h"
+#include "lrn_math.h"
+#include "wgrad_tr.h"
+
+namespace mnistx {
+namespace {
+
+constexpr int NT = 1024, NW = 16, T = 4, C = 32, NWIN = 196;
+// ---- LDS layout (bytes)
+constexpr int X_RS = 80, X_IMG = 2664;                      // input [img][row -2..29][col -4..35] bf16
+constexpr int X_OFF = 0, X_SZ = T * X_IMG;
+constexpr int D_RS = 1024, D_IMG = 14352;                   // dP1 / codes [img][14][16 windows][32] x 2 B
+constexpr int DP1_OFF = X_OFF + X_SZ, D_SZ = T * D_IMG;
+constexpr int CD_OFF = DP1_OFF + D_SZ;
+constexpr int LDS_BYTES = CD_OFF + D_SZ;
+static_assert(32 * X_RS <= X_IMG && 14 * D_RS <= D_IMG && LDS_BYTES <= 163840, "");
+static_assert(NW * 6 * 256 * 4 + NW * C * 4 <= LDS_BYTES, "epilogue scratch");
+// slab rows = convpool_wgrad's RefC1g layout (splitk_reduce as for it): kh * 8 + kw, bias 40
+constexpr int SLAB_ROWS = 48;
+constexpr int NTASK = T * NWIN * 4;                        // LRN tasks per tile: (window, 8 channels)
+constexpr int PER = (NTASK + NT - 1) / NT;                  // 4 (the last: wave 0 only)
+static_assert((NTASK - (PER - 1) * NT) % 64 == 0, "the partial task round covers whole waves (DPP rows)");
+
+struct Args {
+  const bf16_t* x;        // input images [n][784] bf16 (or null with u8)
+  const uint8_t* u8;      // input images [n][784] uint8, normalised while staging (or null)
+  const int64_t* idx;     // per-sample row of x / u8 (null: sample b is row b)
+  int n;
+  const bf16_t* dn;       // dL/d norm1 [B][196][32]
+  const bf16_t* p1;       // pool1 = the LRN input [B][196][32]
+  const uint8_t* arg;     // pool1 argmax codes [B][196][32] (4 = ReLU output 0)
+  int B;
+  float bias, alpha, beta;
+  float* slab;            // [grid][48][32]
+};
+
+// staging registers of one tile: LRN task vectors (dL/d norm1, pool1, codes) and the input
+template <bool U8, bool IDX>
+struct Stage {
+  u32x4 y[PER], p[PER];
+  u32x2 a[PER];
+  u32x2 x[4];             // waves 0..3 (one per image): 4-pixel quads r = lane + 64 i (< 196)
+  u32x2 rowv;             // IDX: the batch-index entry of this wave's image, one tile ahead
+
+  DEV void load_row(const Args& g, int t0, int wave) {
+    if constexpr (IDX) {
+      const bool ok = wave < T && t0 >= 0 && t0 + wave < g.B;
+      rowv = buf_b64(buf_rsrc(g.idx + (ok ? t0 + wave : 0), ok ? 8u : 0u), 0u);
+    }
+  }
+  struct Rsrc {
+    __amdgpu_buffer_rsrc_t y, p, a;
+  };
+  DEV Rsrc rsrc(const Args& g, int t0) const {
+    const int nimg = t0 < 0 ? 0 : min(T, g.B - t0);
+    const int tb = t0 < 0 ? 0 : t0;
+    const uint32_t nb = (uint32_t)nimg * NWIN * C * 2u;
+    return Rsrc{buf_rsrc(g.dn + (int64_t)tb * NWIN * C, nb), buf_rsrc(g.p1 + (int64_t)tb * NWIN * C, nb),
+                buf_rsrc(g.arg + (int64_t)tb * NWIN * C, nb / 2u)};
+  }
+  // LRN task vectors of round u (tasks tid + u NT; the last round: wave 0 only)
+  DEV void load_u(const Rsrc& r, int u, int tid) {
+    const int e = tid + u * NT;
+    const uint32_t ok = e < NTASK ? 0u : BUF_OOB;
+    y[u] = buf_b128(r.y, 16u * e + ok);
+    p[u] = buf_b128(r.p, 16u * e + ok);
+    a[u] = buf_b64(r.a, 8u * e + ok);
+  }
+  DEV void load_x(const Args& g, int t0, int wave, int ln) {
+    if (wave < T) {
+      const bool ok = t0 >= 0 && t0 + wave < g.B;
+      int row = ok ? t0 + wave : 0;
+      if constexpr (IDX) {
+        const uint32_t lo = __builtin_amdgcn_readfirstlane(rowv[0]), hi = __builtin_amdgcn_readfirstlane(rowv[1]);
+        row = (hi != 0u || (int)lo < 0) ? 0 : ((int)lo >= g.n ? g.n - 1 : (int)lo);
+      }
+      constexpr uint32_t esz = U8 ? 1u : 2u;
+      const void* xb = U8 ? (const void*)(g.u8 + (int64_t)row * 784) : (const void*)(g.x + (int64_t)row * 784);
+      const auto rx = buf_rsrc(xb, ok ? 784u * esz : 0u);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t q = (uint32_t)(ln + 64 * i), oob = q < 196u ? 0u : BUF_OOB;
+        if constexpr (U8) x[i] = u32x2{buf_b32(rx, 4u * q + oob), 0u};
+        else x[i] = buf_b64(rx, 8u * q + oob);
+      }
+    }
+  }
+  DEV void load(const Args& g, int t0, int tid, int wave, int ln) {
+    load_x(g, t0, wave, ln);
+    const Rsrc r = rsrc(g, t0);
+#pragma unroll
+    for (int u = 0; u < PER; ++u)
+      if (u < PER - 1 || wave == 0) load_u(r, u, tid);
+  }
+  DEV void store_x(uint8_t* lds, int wave, int ln) {
+    if (wave < T) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = ln + 64 * i;
+        if (q < 196) {
+          const int y = (q * 147) >> 10, k = q - 7 * y;
+          uint32_t lo = x[i][0], hi = x[i][1];
+          if constexpr (U8) {
+            const uint32_t b = x[i][0];
+            lo = pack2(u8_norm(b & 0xff), u8_norm((b >> 8) & 0xff));
+            hi = pack2(u8_norm((b >> 16) & 0xff), u8_norm(b >> 24));
+          }
+          *(u32x2*)(lds + X_OFF + wave * X_IMG + (y + 2) * X_RS + (4 * k + 4) * 2) = u32x2{lo, hi};
+        }
+      }
+    }
+  }
+  // Staging of this tile into LDS -- the input, then per round the LRN backward -> dP1 (bf16)
+  // and the codes (u16), with the bias sums of the active windows -- each part's registers
+  // refilled with the next tile's data right after use, so those loads stream in during the
+  // rest of this staging and the GEMM (not only during the GEMM).
+  DEV void store_load(uint8_t* lds, const Args& g, int t_next, int tid, int wave, int ln, float (&db)[8]) {
+    store_x(lds, wave, ln);
+    load_x(g, t_next, wave, ln);
+    const Rsrc r = rsrc(g, t_next);
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = tid + u * NT;
+      if (u < PER - 1 || wave == 0) {
+        const u32x4 d = lrn_bwd8<4, 4, true>(p[u], y[u], tid & 3, g.bias, g.alpha, g.beta, 0);
+        const uint32_t a0 = a[u][0], a1 = a[u][1];
+        const u32x4 cd = u32x4{bytes01(a0), bytes23(a0), bytes01(a1), bytes23(a1)};
+        if (e < NTASK) {
+          const int px = e >> 2, cg = e & 3, img = px / NWIN, w = px - img * NWIN, yp = w / 14, xp = w - 14 * yp;
+          const int o = img * D_IMG + yp * D_RS + xp * 64 + 16 * cg;
+          *(u32x4*)(lds + DP1_OFF + o) = d;
+          *(u32x4*)(lds + CD_OFF + o) = cd;
+          // bias: dP1 of the windows whose ReLU output is not 0 (code != 4), per u16 lane
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const u16x2 x4 = __builtin_bit_cast(u16x2, cd[j] ^ 0x00040004u), one = {1, 1};
+            const uint32_t m = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, d[j]) *
+                                                                __builtin_elementwise_min(x4, one));
+            db[2 * j] += __uint_as_float(m << 16);
+            db[2 * j + 1] += __uint_as_float(m & 0xffff0000u);
+          }
+        }
+        load_u(r, u, tid);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+};
+
+template <bool U8, bool IDX>
+__global__ __launch_bounds__(NT, 1) void refc1_wgrad_k(const Args g) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntiles = (g.B + T - 1) / T;
+  const int nk = ntiles > (int)blockIdx.x ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  auto tile0 = [&](int k) { return k < nk ? ((int)blockIdx.x + k * (int)gridDim.x) * T : -1; };
+
+  for (int e = tid; e < LDS_BYTES / 16; e += NT) *(u32x4*)(lds + 16 * e) = u32x4{0u, 0u, 0u, 0u};
+  Stage<U8, IDX> st;
+  st.load_row(g, tile0(0), wave);
+  st.load(g, tile0(0), tid, wave, lane);
+  st.load_row(g, tile0(1), wave);
+
+  const int sig = wave & 1, cg = (wave >> 1) & 3, kh = wave >> 3;   // uniform
+  f32x4 acc[3][2];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float db[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
+  for (int k = 0; k < nk; ++k) {
+    __syncthreads();   // the previous tile's GEMM no longer reads dP1 / codes / input
+    {
+      const int ln = lane_now();
+      st.store_load(lds, g, tile0(k + 1), wave * 64 + ln, wave, ln, db);
+      st.load_row(g, tile0(k + 2), wave);
+    }
+    __syncthreads();
+    // ---- GEMM: window rows 7 kh .. 7 kh + 6 of parity set sig, channel group cg.  K row
+    // 8g + 4rho + q = item 16(g>>1) + 8rho + 4(g&1) + q: image q, window 4(g>>1) + (g&1) + 2rho.
+    {
+      const int ln = lane_now(), gg = ln >> 4, q = (ln >> 2) & 3, p = ln & 3;
+      const int hA = p >> 1, pc = p & 1, xil = 4 * (gg >> 1) + (gg & 1);
+      const uint32_t dsel = (uint32_t)((ln & 15) >> 3);
+      const uint32_t dd0 = dsel * 0x00010001u, dd1 = (2u + dsel) * 0x00010001u;
+      const int aB = X_OFF + q * X_IMG + hA * X_RS + (4 * xil + 4 * pc + 4 * sig) * 2;
+      const int bB = DP1_OFF + q * D_IMG + (2 * xil + sig) * 64 + 16 * cg + 8 * pc;
+#pragma unroll 2
+      for (int yp = 7 * kh; yp < 7 * kh + 7; ++yp) {
+        const int sa = aB + 2 * yp * X_RS, sb = bB + yp * D_RS;
+        const u32x4 dv = __builtin_bit_cast(u32x4, frag(tr4(lds, sb), tr4(lds, sb + 256)));
+        const u32x4 cv = __builtin_bit_cast(u32x4, frag(tr4(lds, sb + (CD_OFF - DP1_OFF)),
+                                                         tr4(lds, sb + (CD_OFF - DP1_OFF) + 256)));
+        const bf16x8 B0 = __builtin_bit_cast(bf16x8, u32x4{sel_eq(dv[0], cv[0], dd0), sel_eq(dv[1], cv[1], dd0),
+                                                           sel_eq(dv[2], cv[2], dd0), sel_eq(dv[3], cv[3], dd0)});
+        const bf16x8 B1 = __builtin_bit_cast(bf16x8, u32x4{sel_eq(dv[0], cv[0], dd1), sel_eq(dv[1], cv[1], dd1),
+                                                           sel_eq(dv[2], cv[2], dd1), sel_eq(dv[3], cv[3], dd1)});
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const bf16x8 Af = frag(tr4(lds, sa + 2 * t * X_RS), tr4(lds, sa + 2 * t * X_RS + 16));
+          acc[t][0] = mfma16(Af, B0, acc[t][0]);
+          acc[t][1] = mfma16(Af, B1, acc[t][1]);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue: partials of the 16 waves -> one slab (fixed summation order)
+  const int i16 = lane & 15, g4 = lane >> 4;
+  __syncthreads();
+  float* e1 = (float*)lds;                          // [wave][t][nt][col 16][row 16]
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      *(f32x4*)(e1 + (((wave * 3 + t) * 2 + nt) * 16 + i16) * 16 + 4 * g4) = acc[t][nt];
+  // bias: lanes with the same (lane & 3) hold the same 8 channels (8 (lane & 3) + j)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int m = 4; m <= 32; m *= 2) db[j] += __shfl_xor(db[j], m);
+  }
+  float* eb = e1 + NW * 6 * 256;                    // [wave][32]
+  if (lane < 4)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) eb[wave * C + 8 * lane + j] = db[j];
+  __syncthreads();
+  float* s = g.slab + (int64_t)blockIdx.x * SLAB_ROWS * C;
+  for (int e = tid; e < SLAB_ROWS * C; e += NT) {
+    const int r = e >> 5, c = e & 31, cgc = c >> 3, cl = c & 7, dy = r >> 3, dx = r & 7;
+    float v = 0.f;
+    if (r < 40 && dx < 5) {
+      for (int h = 0; h < 2; ++h)
+        for (int sg = 0; sg < 2; ++sg) {
+          const int w = sg + 2 * cgc + 8 * h;
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            const int ty = dy + (d >> 1), tx = dx + (d & 1), txi = tx + (sg ? 0 : 2);
+            const int t = ty >> 1, row = 4 * (2 * (ty & 1) + (txi >> 2)) + (txi & 3);
+            const int nt = d >> 1, col = cl + 8 * (d & 1);
+            v += e1[(((w * 3 + t) * 2 + nt) * 16 + col) * 16 + row];
+          }
+        }
+    } else if (r == 40) {
+      for (int w = 0; w < NW; ++w) v += eb[w * C + c];
+    }
+    s[e] = v;
+  }
+}
+
+using Kern = void (*)(Args);
+constexpr Kern kRefc1[4] = {refc1_wgrad_k<false, false>, refc1_wgrad_k<false, true>, refc1_wgrad_k<true, false>,
+                            refc1_wgrad_k<true, true>};
+
+}  // namespace
+
+int refc1_wgrad_grid() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, cus = 0, per = 0;
+    for (Kern k : kRefc1)
+      if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) != hipSuccess)
+        return -1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kRefc1[0], NT, LDS_BYTES) != hipSuccess ||
+        hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per <= 0)
+      return -1;
+    n = per * cus;
+  }
+  return n;
+}
+
+int refc1_wgrad_blocks(int B) {
+  const int res = refc1_wgrad_grid();
+  if (res <= 0) return -1;
+  const int ntiles = (B + T - 1) / T;
+  return cap_grid(ntiles < res ? ntiles : res);
+}
+
+hipError_t refc1_wgrad(const XSrc& x, const bf16_t* dn, const bf16_t* p1, const uint8_t* arg, int B, float bias,
+                       float alpha, float beta, float* slab, int grid, hipStream_t st) {
+  if (B <= 0) return hipSuccess;
+  if ((!x.x && !x.u8) || grid <= 0 || refc1_wgrad_grid() <= 0) return hipErrorInvalidValue;
+  if (beta != 0.75f) return hipErrorInvalidValue;   // the lrn_bwd8 fast path (the reference's beta)
+  Args a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, dn, p1, arg, B, bias, alpha, beta, slab};
+  const Kern k = kRefc1[(x.u8 ? 2 : 0) + (x.idx ? 1 : 0)];
+  void* args[] = {&a};
+  return hipLaunchKernel((const void*)k, dim3(grid), dim3(NT), args, LDS_BYTES, st);
+}
+
+}  // namespace mnistx

@@ -194,9 +194,21 @@ class ConvPoolLayer(_Layer):
     # layer's weight-gradient staging (reference CNN norm1, HipNet.fold_lrn)
     lrn_fold: Optional[tuple] = None
 
+    def _refc1(self, ls) -> bool:
+        """The reference CNN's conv1 (28x28x1 -> 32, SAME) under norm1 (radius 4, beta 0.75):
+        refc1_wgrad replaces the folded convpool_wgrad (MNISTX_REFC1_WGRAD=0 keeps the latter)."""
+        return (self.C == 1 and self.Cp == 32 and self.spec.cout == 32 and self.pad == 2 and self.H == self.W == 28
+                and ls.depth_radius == 4 and float(ls.beta) == 0.75 and os.environ.get("MNISTX_REFC1_WGRAD", "1") != "0")
+
     def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor, red: Optional[list] = None) -> None:
         K = kernels()
-        if self.lrn_fold is not None:
+        if self.lrn_fold is not None and self._refc1(self.lrn_fold[0]):
+            # reference conv1 + norm1: the MFMA pool-phase kernel (refc1_wgrad.hip), same slab layout
+            ls, dn = self.lrn_fold
+            grid = min(self.grid, K.refc1_wgrad_blocks(nb))
+            K.refc1_wgrad(self._xin(), dn, self.out, self.arg, slab, grid, nb, ls.bias, ls.alpha, ls.beta,
+                          **self._src())
+        elif self.lrn_fold is not None:
             ls, dn = self.lrn_fold
             grid = min(self.grid, max(1, (nb + 3) // 4))
             K.convpool_wgrad(self._xin(), dn, self.arg, slab, grid, nb, *self._geo(), **self._src(), lrn_p=self.out,

@@ -1,141 +1,173 @@
-"""LDS bank model of csrc/kernels/lenet_band.hip's LDS instructions (lds_sim.py rules,
-MI355X_MICROARCH.md § LDS).  Prints worst / mean LDS-array cycles vs the conflict-free
-count for each access, over every unit / row / tile position the kernel issues."""
+#!/usr/bin/env python3
+"""LDS bank-conflict model of the banded LeNet-5 forward (csrc/kernels/lenet_band.hip,
+lenet_band_fwd_k): every LDS access pattern of one tile with its average cycles per lane
+group (1.0 = conflict-free) and its issue count per tile, for the strides on the command
+line or the kernel's defaults.  Bank rules as bench/lds_bwd.py (MI355X_MICROARCH.md §LDS);
+b32 / ds_read2_b32: one 64-lane group, bank (a/4) % 64.
+
+    python bench/lds_band.py [XIS=900 XPL=448 PIS=1584 PPL=792 PRW=112 PSK=8 ...] [--search]
+
+Round 4: PSK = 0 with two 8-byte pool1 stores per pixel modelled 34 % conflict cycles
+(PMC: 31 %); PSK = 8 with one 16-byte store per pixel models 1.0 for the pool1 stores and
+the conv2 B reads.
+"""
 import sys
-sys.path.insert(0, __file__.rsplit("/", 1)[0])
-import lds_sim as L
 
-L.GROUPS["w_b32"] = [list(range(0, 32)), list(range(32, 64))]
-L.NBANK["w_b32"] = 32
-L.WIDTH["w_b32"] = 4
-L.GROUPS["r2_b64"] = [list(range(16 * i, 16 * i + 16)) for i in range(4)]   # per access
-L.NBANK["r2_b64"] = 32
-L.WIDTH["r2_b64"] = 8
+from lds_bwd import cycles
 
-XRW, XPL, XIS = 32, 448, 900
-PRW, PPL, PIS = 112, 792, 1584
-XBUF = 8 * XIS
+DEF = dict(XIS=900, XPL=448, XRW=32, PIS=1584, PPL=792, PRW=112, PSK=8, XSK=0)
 
 
-def lanes():
-    for lane in range(64):
-        col, h = lane & 31, lane >> 5
-        yield lane, col, h, col & 1, (col >> 1) & 7, col >> 4
+def pib(S, i):
+    """pool1 image base (elements): odd images skewed by PSK"""
+    return i * S["PIS"] + (i & 1) * S["PSK"]
 
 
-def report(name, kind, addr_sets):
-    cs = [L.cycles(kind, a) for a in addr_sets]
-    print(f"{name:42s} {kind:7s} worst {max(cs):3d} mean {sum(cs) / len(cs):6.2f} ideal {L.ideal(kind)}")
+def xib(S, i):
+    return i * S["XIS"] + (i & 1) * S["XSK"]
 
 
-XZERO = (2 * XBUF + 127) // 128 * 128
+def b32(addrs):
+    banks = {}
+    for a in addrs:
+        if a is None:
+            continue
+        banks.setdefault((a // 4) % 64, set()).add(a // 4)
+    return max(len(v) for v in banks.values())
 
 
-def conv1_fetch(split):
-    sets = []
-    for kb, wave in [(k, w) for k in (0, 1) for w in range(4)]:
-        for j in range(14):
-            f = min(wave + 4 * j, 48)
-            yp0, u = f // 7, f % 7
-            for p in range(3):
-                S = yp0 + p - 1
-                for part in (0, 1):
-                    addrs = []
-                    for lane, col, h, ypar, img, half in lanes():
-                        rlane = 7 * half + ((ypar + h) >> 1)
-                        xl = img * XIS + ((ypar + h) & 1) * XPL + rlane * XRW
-                        eo = kb * XBUF + xl + S * XRW + 4 * u
-                        if 0 <= rlane + S < 14:
-                            e = eo
-                        elif split == "zrow":
-                            e = XZERO + (eo & 127)
-                        else:
-                            e = 2 * XBUF
-                        addrs.append(2 * (e + 4 * part))
-                    sets.append(addrs)
-    return sets
+def conv1_b(S, u=3, yp0=2, p=1):
+    """B fragment: 4 dwords from element xlane + yp0 XRW + 4u + p XRW (two ds_read2_b32)."""
+    tot = 0
+    for dw in range(4):
+        out = []
+        for l in range(64):
+            col, h = l & 31, l >> 5
+            img, half, xq = (col >> 1) & 7, col >> 4, col & 1
+            e = xib(S, img) + h * S["XPL"] + (7 * half - 1) * S["XRW"] + 2 * xq + yp0 * S["XRW"] + 4 * u + p * S["XRW"]
+            out.append(2 * e + 4 * dw + 4 * S["XRW"])
+        tot += b32(out)
+    return tot / 4
 
 
-def conv1_store():
-    sets = []
-    for wave in range(4):
-        for j in range(13):
-            f = wave + 4 * j
-            if f >= 49:
+def conv1_store(S, u=3, yp0=2):
+    out = []
+    for l in range(64):
+        col, h = l & 31, l >> 5
+        img, half, xq = (col >> 1) & 7, col >> 4, col & 1
+        row_even = S["PPL"] + 3 * S["PRW"] if half else 0
+        row_odd = 4 * S["PRW"] if half else S["PPL"]
+        off = (row_odd if yp0 & 1 else row_even) + (yp0 >> 1) * S["PRW"] + 16 * u
+        out.append(2 * (pib(S, img) + 8 * xq + 4 * h + off))
+    return cycles(out, 8, "w64")
+
+
+def conv1_store16(S, u=3, yp0=2):
+    """the pixel's 8 channels gathered into the h = 0 lane (permlane32 swap), one b128 store"""
+    out = []
+    for l in range(64):
+        col, h = l & 31, l >> 5
+        img, half, xq = (col >> 1) & 7, col >> 4, col & 1
+        if h:
+            out.append(None)
+            continue
+        row_even = S["PPL"] + 3 * S["PRW"] if half else 0
+        row_odd = 4 * S["PRW"] if half else S["PPL"]
+        off = (row_odd if yp0 & 1 else row_even) + (yp0 >> 1) * S["PRW"] + 16 * u
+        out.append(2 * (pib(S, img) + 8 * xq + off))
+    return cycles(out, 16, "w128")
+
+
+def conv2_b(S, w2v=1, r=2, q=1):
+    out = []
+    for l in range(64):
+        col, h = l & 31, l >> 5
+        slot, im2 = (col >> 2) & 3, (col >> 4) | ((col & 3) << 1)
+        f = min(4 * w2v + slot, 24)
+        y2p, x2p = f // 5, f % 5
+        e = pib(S, im2) + y2p * S["PRW"] + (2 * x2p + h) * 8 + (r & 1) * S["PPL"] + (r >> 1) * S["PRW"] + 16 * q
+        out.append(2 * e)
+    return cycles(out, 16, "b128")
+
+
+def copy_out(S, wave=1, i=0):
+    out = []
+    for l in range(64):
+        t = 64 * wave + l
+        cp = (t + 192) & 255
+        if cp >= 196:
+            out.append(None)
+            continue
+        e = ((cp // 14) & 1) * S["PPL"] + ((cp // 14) >> 1) * S["PRW"] + (cp % 14) * 8 + pib(S, i)
+        out.append(2 * e)
+    return cycles(out, 16, "b128")
+
+
+def xfill(S, wave=1, i=2):
+    tot = 0
+    for dw in range(2):
+        out = []
+        for l in range(64):
+            t = 64 * wave + l
+            r = (t & 31) + 32 * i
+            if r >= 196:
+                out.append(None)
                 continue
-            yp0, u = f // 7, f % 7
-            addrs = []
-            for lane, col, h, ypar, img, half in lanes():
-                y = yp0 + 7 * half
-                off = (y & 1) * PPL + (y >> 1) * PRW
-                addrs.append(2 * (img * PIS + ypar * 8 + 4 * h + off + 16 * u))
-            sets.append(addrs)
-    return sets
+            y, k = r // 7, r % 7
+            e = xib(S, t >> 5) + 2 + (y & 1) * S["XPL"] + (y >> 1) * S["XRW"] + 4 * k
+            out.append(2 * e + 4 * dw)
+        tot += b32(out)
+    return tot / 2
 
 
-def xfill_store():
-    sets = []
-    for wave in range(4):
-        for i in range(7):
-            for part in (0, 1):
-                addrs = []
-                for lane in range(64):
-                    t = 64 * wave + lane
-                    r = (t & 31) + 32 * i
-                    if r >= 196:
-                        addrs.append(None)
-                        continue
-                    y, k = r // 7, r % 7
-                    e = (t >> 5) * XIS + 2 + (y & 1) * XPL + (y >> 1) * XRW + 4 * k
-                    addrs.append(2 * e + 4 * part)
-                sets.append(addrs)
-    return sets
+def avg(f, S, **grid):
+    import itertools
+    keys = list(grid)
+    vals = [f(S, **dict(zip(keys, c))) for c in itertools.product(*grid.values())]
+    return sum(vals) / len(vals)
 
 
-def conv2_read():
-    sets = []
-    for w2v in range(4):
-        for j in range(4):
-            f0 = w2v + 4 * j
-            if f0 >= 13:
-                continue
-            for dy in range(5):
-                for q in range(3):
-                    addrs = []
-                    for lane, col, h, ypar, img, half in lanes():
-                        fa, fb = f0, min(f0 + 13, 24)
-                        ya, yb = fa // 5, fb // 5
-                        uoff = yb * PRW + 16 * (fb - 5 * yb) if half else ya * PRW + 16 * (fa - 5 * ya)
-                        ce = img * PIS + ypar * PPL + 8 * h
-                        co = img * PIS + (1 - ypar) * PPL + ypar * PRW + 8 * h
-                        base = (co if dy & 1 else ce) + uoff + (dy >> 1) * PRW
-                        addrs.append(2 * (base + 16 * q))
-                    sets.append(addrs)
-    return sets
+def report(S):
+    # issues per tile (per block): conv1 49 units x 3 k-steps x 2 read2, 49 stores; conv2
+    # 7 units x 6 rows x 3 b128; copy-out 4 waves x 8 b128; fill 4 waves x 7 x write2
+    rows = [("conv1 B (read2_b32 x2)", avg(conv1_b, S, u=range(7), yp0=range(7), p=range(3)), 49 * 3 * 2),
+            ("conv1 pool1 store (w128)", avg(conv1_store16, S, u=range(7), yp0=range(7)), 49),
+            ("conv2 B (b128)", avg(conv2_b, S, w2v=range(4), r=range(6), q=range(3)), 7 * 6 * 3),
+            ("copy-out (b128)", avg(copy_out, S, wave=range(4), i=range(8)), 4 * 8),
+            ("input fill (write2_b32)", avg(xfill, S, wave=range(4), i=range(7)), 4 * 7)]
+    tot_c = sum(c * n for _, c, n in rows)
+    tot_n = sum(n for _, c, n in rows)
+    for name, c, n in rows:
+        print(f"{name:28s} {c:5.2f} cycles/group  x{n}")
+    print(f"{'weighted':28s} {tot_c / tot_n:5.2f}  (conflict share {(1 - tot_n / tot_c) * 100:.0f} %)")
+    return tot_c / tot_n
 
 
-def copyout_read():
-    sets = []
-    NV = 8 * 196
-    for e0 in range(0, 256):
-        for i in range(4):
-            addrs = []
-            for lane in range(64):
-                t = (e0 // 64) * 64 + lane
-                e = min(t + i * 256, NV - 1)
-                im, r = e // 196, e % 196
-                yp, xp = r // 14, r % 14
-                addrs.append(2 * (im * PIS + (yp & 1) * PPL + (yp >> 1) * PRW + xp * 8))
-            sets.append(addrs)
-        break
-    return sets
+def main():
+    S = dict(DEF)
+    search = False
+    for a in sys.argv[1:]:
+        if a == "--search":
+            search = True
+        else:
+            k, v = a.split("=")
+            S[k] = int(v)
+    report(S)
+    if search:
+        best = []
+        import io
+        import contextlib
+        for pis in range(S["PPL"] * 2, S["PPL"] * 2 + 64, 4):
+            for ppl in range(7 * S["PRW"], 7 * S["PRW"] + 64, 4):
+                if pis < 2 * ppl:
+                    continue
+                T = dict(S, PIS=pis, PPL=ppl)
+                with contextlib.redirect_stdout(io.StringIO()):
+                    w = report(T)
+                best.append((w, pis, ppl))
+        best.sort()
+        print("best (weighted, PIS, PPL):", best[:8])
 
 
 if __name__ == "__main__":
-    report("conv1 fetch as ds_read2_b64 (per access)", "r2_b64", conv1_fetch("one"))
-    report("conv1 fetch 2 x ds_read_b64, one zero row", "b64", conv1_fetch("one"))
-    report("conv1 fetch 2 x ds_read_b64, bank-matched 0", "b64", conv1_fetch("zrow"))
-    report("conv1 epilogue pool1 store ds_write_b64", "w_b64", conv1_store())
-    report("input fill ds_write_b32", "w_b32", xfill_store())
-    report("conv2 B-fragment ds_read_b128", "b128", conv2_read())
-    report("pool1 copy-out ds_read_b128", "b128", copyout_read())
+    main()

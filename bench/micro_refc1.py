@@ -58,6 +58,13 @@ def main():
     gb = B * (196 * 32 * 5 + 784 * 2) / 1e9
     res["bytes_GB"] = round(gb, 3)
     res["refc1_TBps"] = round(gb / res["refc1_us"] * 1e-3 * 1e6, 2)
+    # parts left out (experiment bits: 1 GEMM, 2 LRN math, 4 next-tile loads)
+    skips = {}
+    for s in (1, 2, 4, 3, 5, 6, 7):
+        K.refc1_set_skip(s)
+        skips[s] = timed(lambda: K.refc1_wgrad(x, dn, P1, A1, slab, grid, B, *LRN), args.iters)
+    K.refc1_set_skip(0)
+    res["us_by_skip"] = skips
     print(json.dumps(res), flush=True)
 
 

@@ -845,7 +845,7 @@ void refc1_wgrad(Tensor x, Tensor dn, Tensor p1, Tensor arg, Tensor slab, int64_
                  double lrn_alpha, double lrn_beta, optional<Tensor> u8, optional<Tensor> idx) {
   const int cfg = mnistx::convpool_config(1, 32, 5, 2, 28, 28);
   TORCH_CHECK(cfg >= 0, "refc1_wgrad: no RefC1 geometry");
-  TORCH_CHECK(B >= 1 && B < (int64_t)INT32_MAX / 4, "B");
+  TORCH_CHECK(B >= 1 && B * 784 * 2 < (int64_t)INT32_MAX, "B: the batch (and its index) must stay < 2 GB");
   const auto src = cp_src(x, u8, idx, cfg, B, 784);
   if (src.x) TORCH_CHECK(reinterpret_cast<uintptr_t>(src.x) % 8 == 0, "x must be 8-byte aligned");
   const int64_t np = B * 196 * 32;
@@ -1017,6 +1017,23 @@ void f32_conv1_wgrad_unpool(Tensor x, Tensor dp, Tensor codes, Tensor slab, int6
                                         (int)splits, P<float>(slab), cur_stream()),
          "f32_conv1_wgrad_unpool");
 }
+// with norm1's backward folded in: dn = dL/d norm1, p1 = pool1 (the LRN input), radius 4
+void f32_conv1_wgrad_lrn(Tensor x, Tensor dn, Tensor p1, Tensor codes, Tensor slab, int64_t Nb, int64_t splits,
+                         double bias, double alpha, double beta) {
+  check(x, at::kFloat, Nb * 784, "x");
+  check(dn, at::kFloat, Nb * 196 * 32, "dn");
+  check(p1, at::kFloat, Nb * 196 * 32, "p1");
+  check(codes, at::kByte, Nb * 196 * 32, "codes");
+  for (const Tensor* t : {&x, &dn, &p1, &codes})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "x / dn / p1 / codes must be 16-byte aligned");
+  TORCH_CHECK(Nb >= 1 && Nb * 196 * 32 * 4 < (int64_t)INT32_MAX * 2, "Nb");
+  TORCH_CHECK(splits >= 1 && splits <= 65535, "splits");
+  check(slab, at::kFloat, splits * 26 * 32, "slab");
+  hip_ok(mnistx::f32_conv1_wgrad_lrn(P<const float>(x), P<const float>(dn), P<const float>(p1), P<const uint8_t>(codes),
+                                     (int)Nb, (int)splits, (float)bias, (float)alpha, (float)beta, P<float>(slab),
+                                     cur_stream()),
+         "f32_conv1_wgrad_lrn");
+}
 
 // fp32 LRN + 2x2 max-pool fused (the reference's norm2 -> pool2) and its backward
 bool f32_lrn_pool_ok(int64_t H, int64_t W, int64_t C, int64_t r) {
@@ -1112,6 +1129,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("f32_conv1_fwd_pool", &f32_conv1_fwd_pool);
   m.def("f32_conv1_wgrad_unpool_grid", &f32_conv1_wgrad_unpool_grid);
   m.def("f32_conv1_wgrad_unpool", &f32_conv1_wgrad_unpool);
+  m.def("f32_conv1_wgrad_lrn", &f32_conv1_wgrad_lrn);
   m.def("f32_lrn_pool_ok", &f32_lrn_pool_ok);
   m.def("f32_lrn_pool_fwd", &f32_lrn_pool_fwd);
   m.def("f32_lrn_pool_bwd", &f32_lrn_pool_bwd);
@@ -1211,6 +1229,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("refc1_wgrad", &refc1_wgrad, py::arg("x"), py::arg("dn"), py::arg("p1"), py::arg("arg"), py::arg("slab"),
         py::arg("grid"), py::arg("B"), py::arg("lrn_bias"), py::arg("lrn_alpha"), py::arg("lrn_beta"),
         py::arg("u8") = py::none(), py::arg("idx") = py::none());
+  m.def("refc1_set_skip", [](int64_t s) { mnistx::refc1_set_skip((int)s); });
   m.def("refc1_wgrad_blocks", [](int64_t B) {
     const int n = mnistx::refc1_wgrad_blocks((int)B);
     TORCH_CHECK(n > 0, "refc1_wgrad_blocks: occupancy query failed");

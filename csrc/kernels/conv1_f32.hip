@@ -23,6 +23,7 @@
 // mnist_input.py:142-145 under the reference's tf.float32.
 #include "common.h"
 #include "launchers.h"
+#include "lrn_f32.h"
 
 namespace mnistx {
 namespace {
@@ -338,6 +339,137 @@ __global__ __launch_bounds__(NT1) void conv1_f32_wgrad_unpool_k(const float* __r
   }
 }
 
+// The same weight gradient with norm1's backward folded in (reference CNN, pool1 -> norm1 ->
+// conv2, mnist_input.py:149-156): reads dL/d norm1, pool1 (the LRN input) and the codes, and
+// runs lrn_f32_bwd4 -- the unfused lrn_f32_bwd_v4_k's arithmetic -- while staging, so dL/d
+// pool1 (411 MB at B = 16384, written and read back by the unfused pair) never reaches HBM.
+// Per image the staged dL/d pool1 and codes live in LDS; the next image's operands are loaded
+// into registers during this image's MFMAs (the unfused kernel's per-k-step global loads were
+// latency bound: 570 us against a ~170 us MFMA floor).  Summation order = conv1_f32_wgrad_unpool_k
+// for the same grid.
+constexpr int NPP = PH * PW;                   // 196 pooled pixels
+constexpr int LT = NPP * (COUT / 4);           // LRN tasks per image: (pooled pixel, 4 channels)
+constexpr int LR = (LT + NT1 - 1) / NT1;       // 7 staging rounds (the last: 32 tasks)
+constexpr int XR = (IPIX + NT1 - 1) / NT1;     // 4 input rounds
+__global__ __launch_bounds__(NT1) void conv1_f32_wgrad_lrn_k(const float* __restrict__ x,
+                                                             const float* __restrict__ dn,
+                                                             const float* __restrict__ p1,
+                                                             const uint8_t* __restrict__ codes, int B, float lbias,
+                                                             float lalpha, float lbeta, float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) float tile[4 * TSZ];
+  __shared__ __attribute__((aligned(16))) float dps[NPP * COUT];     // dL/d pool1 of the image
+  __shared__ __attribute__((aligned(16))) uint32_t cds[LT];          // its codes, 4 per word
+  static_assert(sizeof(float) * NPP * COUT >= sizeof(float) * (NT1 / 64) * 2 * 2 * 64 * 4, "red aliases dps");
+  float(*red)[2][2][64][4] = (float(*)[2][2][64][4])dps;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  for (int e = tid; e < 4 * TSZ; e += NT1) tile[e] = 0.f;
+  int toff[2];
+  float aconst[2];
+#pragma unroll
+  for (int mf = 0; mf < 2; ++mf) {
+    const int m = 16 * mf + i;
+    toff[mf] = m < KS * KS ? (m / KS) * TC + (m % KS) : -1;
+    aconst[mf] = m == KS * KS ? 1.f : 0.f;
+  }
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int mf = 0; mf < 2; ++mf)
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf) acc[mf][nf] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // next image's operands in registers: branch-free buffer loads, zeros past the batch
+  f32x4 pv[LR], gv[LR];
+  uint32_t cv[LR];
+  float xv[XR];
+  auto load = [&](int img) {
+    const bool ok = img < B;
+    const int64_t b = ok ? img : 0;
+    const auto rx = buf_rsrc(x + b * IPIX, ok ? IPIX * 4u : 0u);
+    const auto rp = buf_rsrc(p1 + b * LT * 4, ok ? LT * 16u : 0u);
+    const auto rg = buf_rsrc(dn + b * LT * 4, ok ? LT * 16u : 0u);
+    const auto rc = buf_rsrc(codes + b * LT * 4, ok ? LT * 4u : 0u);
+#pragma unroll
+    for (int u = 0; u < XR; ++u) {
+      const int e = tid + u * NT1;
+      xv[u] = __uint_as_float(buf_b32(rx, e < IPIX ? 4u * e : BUF_OOB));
+    }
+#pragma unroll
+    for (int u = 0; u < LR; ++u) {
+      const int t = tid + u * NT1;
+      const uint32_t o = t < LT ? 0u : BUF_OOB;
+      pv[u] = __builtin_bit_cast(f32x4, buf_b128(rp, 16u * t + o));
+      gv[u] = __builtin_bit_cast(f32x4, buf_b128(rg, 16u * t + o));
+      cv[u] = buf_b32(rc, 4u * t + o);
+    }
+  };
+  load(blockIdx.x);
+  for (int img = blockIdx.x; img < B; img += gridDim.x) {
+    __syncthreads();   // the previous image's k-steps no longer read tile / dps / cds
+#pragma unroll
+    for (int u = 0; u < XR; ++u) {
+      const int e = tid + u * NT1;
+      if (e < IPIX) {
+        const int y = e / IW, xx = e - y * IW, a = (y + 2) * TC + xx + 2;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          if (a - s >= 0) tile[s * TSZ + a - s] = xv[u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < LR; ++u) {   // every lane runs the DPP exchanges; stores are masked
+      const int t = tid + u * NT1;
+      const f32x4 d = lrn_f32_bwd4(pv[u], gv[u], tid % (COUT / 4), COUT / 4, 4, lbias, lalpha, lbeta, 0);
+      if (t < LT) {
+        *(f32x4*)(dps + 4 * t) = d;
+        cds[t] = cv[u];
+      }
+    }
+    load(img + gridDim.x);
+    __syncthreads();
+    const uint8_t* cdb = (const uint8_t*)cds;
+#pragma unroll 4
+    for (int q = wave; q < IH * (IW / 4); q += NT1 / 64) {
+      const int row = q / (IW / 4), c4 = q - row * (IW / 4);
+      const int col = 4 * c4 + g;
+      const int pp = (row >> 1) * PW + (col >> 1);
+      const uint32_t pos = (uint32_t)(2 * (row & 1) + (col & 1));
+      const float d0 = dps[pp * COUT + i], d1 = dps[pp * COUT + 16 + i];
+      const uint32_t k0 = cdb[pp * COUT + i], k1 = cdb[pp * COUT + 16 + i];
+      const float b0 = k0 == pos ? d0 : 0.f, b1 = k1 == pos ? d1 : 0.f;
+      const int base = row * TC + col;
+#pragma unroll
+      for (int mf = 0; mf < 2; ++mf) {
+        const float av = toff[mf] >= 0 ? tile[base + toff[mf]] : aconst[mf];
+        acc[mf][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b0, acc[mf][0], 0, 0, 0);
+        acc[mf][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b1, acc[mf][1], 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int mf = 0; mf < 2; ++mf)
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wave][mf][nf][lane][r] = acc[mf][nf][r];
+  __syncthreads();
+  if (wave == 0) {
+    float* out = slab + (int64_t)blockIdx.x * WROWS * COUT;
+#pragma unroll
+    for (int mf = 0; mf < 2; ++mf)
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = ((red[0][mf][nf][lane][r] + red[1][mf][nf][lane][r]) + red[2][mf][nf][lane][r]) +
+                          red[3][mf][nf][lane][r];
+          const int m = 16 * mf + 4 * g + r;
+          if (m < WROWS) out[m * COUT + 16 * nf + i] = v;
+        }
+  }
+}
+
 int resident(const void* k) {
   int dev = 0, cus = 0, pc = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, k, NT1, 0) == hipSuccess && hipGetDevice(&dev) == hipSuccess &&
@@ -380,6 +512,17 @@ hipError_t f32_conv1_wgrad_unpool(const float* x, const float* dp, const uint8_t
                                   float* slab, hipStream_t st) {
   if (Nb <= 0 || splits <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(conv1_f32_wgrad_unpool_k, dim3(splits), dim3(NT1), 0, st, x, dp, codes, Nb, slab);
+  return hipGetLastError();
+}
+int f32_conv1_wgrad_lrn_grid() {
+  static const int n = resident((const void*)conv1_f32_wgrad_lrn_k);
+  return n;
+}
+hipError_t f32_conv1_wgrad_lrn(const float* x, const float* dn, const float* p1, const uint8_t* codes, int Nb,
+                               int splits, float bias, float alpha, float beta, float* slab, hipStream_t st) {
+  if (Nb <= 0 || splits <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(conv1_f32_wgrad_lrn_k, dim3(splits), dim3(NT1), 0, st, x, dn, p1, codes, Nb, bias, alpha, beta,
+                     slab);
   return hipGetLastError();
 }
 hipError_t f32_conv1_wgrad(const float* x, const float* dy, int Nb, int splits, float* slab, hipStream_t st) {

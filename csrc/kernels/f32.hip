@@ -20,6 +20,7 @@
 #include "common.h"
 #include "ce_stats.h"
 #include "launchers.h"
+#include "lrn_f32.h"
 
 #include <cstdlib>
 
@@ -365,7 +366,6 @@ __global__ void maxpool_f32_bwd_k(const float* __restrict__ dy, const uint8_t* _
 // One thread per (pixel, channel); a block stages 256 / C whole pixels in LDS, so the
 // window sums read neighbours from LDS and every global access is coalesced.
 constexpr int LRN_MAXC = 64;
-DEV float pow_neg(float n, float b) { return exp2f(-b * log2f(n)); }   // n^-b, n >= bias > 0
 
 __global__ __launch_bounds__(256) void lrn_f32_fwd_k(const float* __restrict__ x, int64_t P, int C, int r,
                                                      float bias, float alpha, float beta, float* __restrict__ y) {
@@ -517,32 +517,8 @@ __global__ __launch_bounds__(256) void maxpool_f32_bwd_v4_k(const float* __restr
   }
 }
 
-// LRN with 4 channels per lane, the C/4 lanes of a pixel adjacent inside one 16-lane
-// DPP row; the window's neighbours (radius r <= 4) come from the adjacent lanes by
-// DPP row shifts (zero at the pixel's first / last lane).
-DEV float f32_from_left(float v) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, true)); }
-DEV float f32_from_right(float v) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x101, 0xf, 0xf, true)); }
-DEV f32x4 win4(const f32x4& v, int c4, int G, int r) {
-  float e[12];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float l = f32_from_left(v[j]), rr = f32_from_right(v[j]);
-    e[j] = c4 == 0 ? 0.f : l;
-    e[8 + j] = c4 == G - 1 ? 0.f : rr;
-    e[4 + j] = v[j];
-  }
-  f32x4 s;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float a = 0.f;
-#pragma unroll
-    for (int d = -4; d <= 4; ++d)
-      if (d >= -r && d <= r) a = fmaf(1.f, e[4 + j + d], a);
-    s[j] = a;
-  }
-  return s;
-}
-
+// LRN with 4 channels per lane (lrn_f32.h: the C/4 lanes of a pixel adjacent inside one
+// 16-lane DPP row, neighbours by DPP row shifts).
 __global__ __launch_bounds__(256) void lrn_f32_fwd_v4_k(const float* __restrict__ x, int total, int G, int r,
                                                         float bias, float alpha, float beta, float* __restrict__ y) {
   // uniform trip count over whole waves: every lane takes part in the DPP exchanges
@@ -568,22 +544,7 @@ __global__ __launch_bounds__(256) void lrn_f32_bwd_v4_k(const float* __restrict_
     const int c4 = threadIdx.x % G;
     const f32x4 v = ok ? *(const f32x4*)(x + (int64_t)t * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
     const f32x4 g = ok ? *(const f32x4*)(dy + (int64_t)t * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
-    const f32x4 s = win4(v * v, c4, G, r);
-    f32x4 nb, tt;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float n = fmaf(alpha, s[j], bias);
-      nb[j] = pow_neg(n, beta);
-      tt[j] = g[j] * v[j] * nb[j] / n;
-    }
-    const f32x4 u = win4(tt, c4, G, r);
-    f32x4 o;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float d = g[j] * nb[j] - 2.f * alpha * beta * v[j] * u[j];
-      if (relu_mask && !(v[j] > 0.f)) d = 0.f;
-      o[j] = d;
-    }
+    const f32x4 o = lrn_f32_bwd4(v, g, c4, G, r, bias, alpha, beta, relu_mask);
     if (ok) *(f32x4*)(dx + (int64_t)t * 4) = o;
   }
 }

@@ -120,6 +120,7 @@ hipError_t lenet_bwd(const XSrc& x, const bf16_t* p1, const uint8_t* arg1, const
 // 0.75) backward folded in: dn = dL/d norm1, p1 = pool1 (the LRN input), arg = pool1 codes (one
 // byte per channel), all [B][196][32].  slab [grid][48][32] in convpool_wgrad's RefC1g layout.
 int refc1_wgrad_blocks(int B);       // the grid for a batch (one block per CU, <= tiles); <= 0: error
+void refc1_set_skip(int s);          // experiments (bench/micro_refc1.py): parts of the kernel left out
 hipError_t refc1_wgrad(const XSrc& x, const bf16_t* dn, const bf16_t* p1, const uint8_t* arg, int B, float bias,
                        float alpha, float beta, float* slab, int grid, hipStream_t st);
 
@@ -161,6 +162,11 @@ hipError_t f32_conv1_fwd_pool(const float* x, const float* w, int Nb, const floa
 int f32_conv1_wgrad_unpool_grid();
 hipError_t f32_conv1_wgrad_unpool(const float* x, const float* dp, const uint8_t* codes, int Nb, int splits,
                                   float* slab, hipStream_t st);
+// the same with norm1's backward (LRN radius 4 over the 32 channels) folded in: dn = dL/d norm1,
+// p1 = pool1 (the LRN input); dL/d pool1 is never written
+int f32_conv1_wgrad_lrn_grid();
+hipError_t f32_conv1_wgrad_lrn(const float* x, const float* dn, const float* p1, const uint8_t* codes, int Nb,
+                               int splits, float bias, float alpha, float beta, float* slab, hipStream_t st);
 bool f32_halo_wgrad_ok(int H, int W, int C, int OH, int OW, int KH, int KW, int ph, int pw, int Cout);
 int f32_halo_wgrad_grid();
 hipError_t f32_halo_wgrad(const float* x, const float* dy, int Nb, int splits, float* slab, hipStream_t st);

@@ -57,6 +57,13 @@ constexpr int XIMG = 784;
 constexpr int XRW = 32, XPL = 448, XIS = 900;
 //  pool1 : image [plane 2][7 rows][14 px][8 ch]
 constexpr int PRW = 112, PPL = 792, PIS = 1584;
+// odd images of the pool1 ring start one 16-byte slot later: the conv2 B reads of a lane
+// group (2 pooled pixels x 4 images of one parity, bench/lds_band.py) then hit 16 distinct
+// bank slots (2-way before), and the conv1 stores (one 16-byte pixel per lane) stay
+// conflict-free; the last image still ends inside the ring (7 PIS + 8 + PPL + 7 PRW = 8 PIS)
+constexpr int PSK = 8;
+constexpr int pib(int i) { return i * PIS + (i & 1) * PSK; }
+static_assert(pib(7) + PPL + 7 * PRW <= 8 * PIS, "");
 constexpr int XBUF = BT * XIS, PBUF = BT * PIS;
 constexpr int XZERO = 2 * XBUF;                 // one zero row: out-of-image input rows
 constexpr int LDS_X = 2 * XBUF + XRW, LDS_P = 2 * PBUF;
@@ -225,7 +232,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
     const int xlane = img * XIS + h * XPL + (7 * half - 1) * XRW + 2 * xq;
     const bool top = half == 0, bot = half == 1;   // lanes whose p = 0 / p = 2 row can be padding
     // pool1 store: lane part + the (yp0 parity, half) part of pooled row yp = yp0 + 7 half
-    const int store_lane = img * PIS + 8 * xq + 4 * h;
+    const int store_lane = pib(img) + 8 * xq;   // the h = 0 lane stores the whole 16-byte pixel
     const int row_even = half ? PPL + 3 * PRW : 0;   // yp0 even
     const int row_odd = half ? 4 * PRW : PPL;        // yp0 odd
     // code word: byte k = code(c = k) | code(c = k + 4) << 4; channels 6-7 are padding (code 4)
@@ -292,9 +299,13 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
             const auto sw = __builtin_amdgcn_permlane32_swap(X, X, false, false);
             w1 = h ? 0u : pk2(o[2], __uint_as_float(sw[1]));
           }
-          if (f < U1) {
+          // the h = 1 half of the pixel (channels 4, 5 and the code word) into the h = 0 lane:
+          // one 16-byte store per pixel (two 8-byte stores from both halves conflicted 2-way)
+          const uint32_t s0 = __builtin_amdgcn_permlane32_swap(w0, w0, false, false)[1];
+          const uint32_t s1 = __builtin_amdgcn_permlane32_swap(w1, w1, false, false)[1];
+          if (f < U1 && h == 0) {
             const int off = (yp0 & 1 ? row_odd : row_even) + (yp0 >> 1) * PRW + 16 * u;
-            *(u32x2*)(pb + off) = u32x2{w0, w1};
+            *(u32x4*)(pb + off) = u32x4{w0, w1, s0, s1};
           }
         };
         // 13 slots per wave (units wave + 4j, j = 0..12: 52 slots for the 49 units) -- the
@@ -364,7 +375,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
           for (int i0 = 0; i0 < BT; i0 += 4) {
             u32x4 cv[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) cv[i] = *(const u32x4*)(src + (i0 + i) * PIS);
+            for (int i = 0; i < 4; ++i) cv[i] = *(const u32x4*)(src + pib(i0 + i));
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               __builtin_amdgcn_raw_buffer_store_b128(u32x4{cv[i][0], cv[i][1], cv[i][2], 0u}, rp1, (uint32_t)cp_r * 16u,
@@ -389,7 +400,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
           if (u >= 7) break;
           const int f = 4 * u + slot, fc = min(f, 24);
           const int y2p = fc / 5, x2p = fc - 5 * y2p;
-          const bf16_t* rb = pb + im2 * PIS + y2p * PRW + (2 * x2p + h) * 8;
+          const bf16_t* rb = pb + pib(im2) + y2p * PRW + (2 * x2p + h) * 8;
           auto rowp = [&](int r) { return rb + (r & 1) * PPL + (r >> 1) * PRW; };
           bf16x8 bq[2][3];
 #pragma unroll

@@ -58,6 +58,7 @@ struct Args {
   int B;
   float bias, alpha, beta;
   float* slab;            // [grid][48][32]
+  int skip;               // experiments only (refc1_set_skip): 1 no GEMM, 2 no LRN math, 4 no next-tile loads
 };
 
 // staging registers of one tile: LRN task vectors (dL/d norm1, pool1, codes) and the input
@@ -65,13 +66,14 @@ template <bool U8, bool IDX>
 struct Stage {
   u32x4 y[PER], p[PER];
   u32x2 a[PER];
-  u32x2 x[4];             // waves 0..3 (one per image): 4-pixel quads r = lane + 64 i (< 196)
-  u32x2 rowv;             // IDX: the batch-index entry of this wave's image, one tile ahead
+  u32x2 x;                // one 4-pixel quad per thread: image tid / 196, quad tid % 196 (tid < 784)
+  u32x2 rowv;             // IDX: the batch-index entry of that image, one tile ahead
 
-  DEV void load_row(const Args& g, int t0, int wave) {
+  DEV void load_row(const Args& g, int t0, int tid) {
     if constexpr (IDX) {
-      const bool ok = wave < T && t0 >= 0 && t0 + wave < g.B;
-      rowv = buf_b64(buf_rsrc(g.idx + (ok ? t0 + wave : 0), ok ? 8u : 0u), 0u);
+      const int img = (tid * 669) >> 17;   // tid / 196 for tid < 1024
+      const bool ok = tid < T * NWIN && t0 >= 0 && t0 + img < g.B;
+      rowv = buf_b64(buf_rsrc(g.idx, (uint32_t)g.B * 8u), ok ? (uint32_t)(t0 + img) * 8u : BUF_OOB);
     }
   }
   struct Rsrc {
@@ -84,7 +86,7 @@ struct Stage {
     return Rsrc{buf_rsrc(g.dn + (int64_t)tb * NWIN * C, nb), buf_rsrc(g.p1 + (int64_t)tb * NWIN * C, nb),
                 buf_rsrc(g.arg + (int64_t)tb * NWIN * C, nb / 2u)};
   }
-  // LRN task vectors of round u (tasks tid + u NT; the last round: wave 0 only)
+  // LRN task vectors of round u (tasks tid + u NT; the last round: wave 0's lanes only)
   DEV void load_u(const Rsrc& r, int u, int tid) {
     const int e = tid + u * NT;
     const uint32_t ok = e < NTASK ? 0u : BUF_OOB;
@@ -92,48 +94,47 @@ struct Stage {
     p[u] = buf_b128(r.p, 16u * e + ok);
     a[u] = buf_b64(r.a, 8u * e + ok);
   }
-  DEV void load_x(const Args& g, int t0, int wave, int ln) {
-    if (wave < T) {
-      const bool ok = t0 >= 0 && t0 + wave < g.B;
-      int row = ok ? t0 + wave : 0;
-      if constexpr (IDX) {
-        const uint32_t lo = __builtin_amdgcn_readfirstlane(rowv[0]), hi = __builtin_amdgcn_readfirstlane(rowv[1]);
-        row = (hi != 0u || (int)lo < 0) ? 0 : ((int)lo >= g.n ? g.n - 1 : (int)lo);
-      }
-      constexpr uint32_t esz = U8 ? 1u : 2u;
-      const void* xb = U8 ? (const void*)(g.u8 + (int64_t)row * 784) : (const void*)(g.x + (int64_t)row * 784);
-      const auto rx = buf_rsrc(xb, ok ? 784u * esz : 0u);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t q = (uint32_t)(ln + 64 * i), oob = q < 196u ? 0u : BUF_OOB;
-        if constexpr (U8) x[i] = u32x2{buf_b32(rx, 4u * q + oob), 0u};
-        else x[i] = buf_b64(rx, 8u * q + oob);
-      }
+  // every wave issues the same loads (out of range: no memory access, zeros), so the load
+  // count per tile is fixed and the compiler's vmcnt waits stay exact across the tile loop
+  DEV void load_x(const Args& g, int t0, int tid) {
+    const int img = (tid * 669) >> 17, q = tid - NWIN * img;
+    const bool ok = tid < T * NWIN && t0 >= 0 && t0 + img < g.B;
+    constexpr uint32_t esz = U8 ? 1u : 2u;
+    const void* base = U8 ? (const void*)g.u8 : (const void*)g.x;
+    uint32_t off;
+    if constexpr (IDX) {   // the dataset (< 2 GB, binding check) through the batch index
+      const uint32_t lo = rowv[0], hi = rowv[1];
+      const int row = (hi != 0u || (int)lo < 0) ? 0 : ((int)lo >= g.n ? g.n - 1 : (int)lo);
+      off = ((uint32_t)row * 196u + (uint32_t)q) * 4u * esz;
+    } else {
+      off = ((uint32_t)(ok ? t0 + img : 0) * 196u + (uint32_t)q) * 4u * esz;
     }
+    const auto rx = buf_rsrc(base, 0x7fffffffu);
+    if (!ok) off = BUF_OOB;
+    if constexpr (U8) x = u32x2{buf_b32(rx, off), 0u};
+    else x = buf_b64(rx, off);
   }
-  DEV void load(const Args& g, int t0, int tid, int wave, int ln) {
-    load_x(g, t0, wave, ln);
+  // (the same issue order as store_load's: the waitcnt pass merges the two at the loop head)
+  DEV void load(const Args& g, int t0, int tid) {
+    load_x(g, t0, tid);
+    __builtin_amdgcn_sched_barrier(0);
     const Rsrc r = rsrc(g, t0);
 #pragma unroll
-    for (int u = 0; u < PER; ++u)
-      if (u < PER - 1 || wave == 0) load_u(r, u, tid);
+    for (int u = 0; u < PER; ++u) {
+      load_u(r, u, tid);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
-  DEV void store_x(uint8_t* lds, int wave, int ln) {
-    if (wave < T) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int q = ln + 64 * i;
-        if (q < 196) {
-          const int y = (q * 147) >> 10, k = q - 7 * y;
-          uint32_t lo = x[i][0], hi = x[i][1];
-          if constexpr (U8) {
-            const uint32_t b = x[i][0];
-            lo = pack2(u8_norm(b & 0xff), u8_norm((b >> 8) & 0xff));
-            hi = pack2(u8_norm((b >> 16) & 0xff), u8_norm(b >> 24));
-          }
-          *(u32x2*)(lds + X_OFF + wave * X_IMG + (y + 2) * X_RS + (4 * k + 4) * 2) = u32x2{lo, hi};
-        }
+  DEV void store_x(uint8_t* lds, int tid) {
+    if (tid < T * NWIN) {
+      const int img = (tid * 669) >> 17, q = tid - NWIN * img, y = (q * 147) >> 10, k = q - 7 * y;
+      uint32_t lo = x[0], hi = x[1];
+      if constexpr (U8) {
+        const uint32_t b = x[0];
+        lo = pack2(u8_norm(b & 0xff), u8_norm((b >> 8) & 0xff));
+        hi = pack2(u8_norm((b >> 16) & 0xff), u8_norm(b >> 24));
       }
+      *(u32x2*)(lds + X_OFF + img * X_IMG + (y + 2) * X_RS + (4 * k + 4) * 2) = u32x2{lo, hi};
     }
   }
   // Staging of this tile into LDS -- the input, then per round the LRN backward -> dP1 (bf16)
@@ -141,14 +142,15 @@ struct Stage {
   // refilled with the next tile's data right after use, so those loads stream in during the
   // rest of this staging and the GEMM (not only during the GEMM).
   DEV void store_load(uint8_t* lds, const Args& g, int t_next, int tid, int wave, int ln, float (&db)[8]) {
-    store_x(lds, wave, ln);
-    load_x(g, t_next, wave, ln);
+    if (g.skip & 4) t_next = -1;
+    store_x(lds, tid);
+    load_x(g, t_next, tid);
     const Rsrc r = rsrc(g, t_next);
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int e = tid + u * NT;
       if (u < PER - 1 || wave == 0) {
-        const u32x4 d = lrn_bwd8<4, 4, true>(p[u], y[u], tid & 3, g.bias, g.alpha, g.beta, 0);
+        const u32x4 d = (g.skip & 2) ? y[u] : lrn_bwd8<4, 4, true>(p[u], y[u], tid & 3, g.bias, g.alpha, g.beta, 0);
         const uint32_t a0 = a[u][0], a1 = a[u][1];
         const u32x4 cd = u32x4{bytes01(a0), bytes23(a0), bytes01(a1), bytes23(a1)};
         if (e < NTASK) {
@@ -156,18 +158,17 @@ struct Stage {
           const int o = img * D_IMG + yp * D_RS + xp * 64 + 16 * cg;
           *(u32x4*)(lds + DP1_OFF + o) = d;
           *(u32x4*)(lds + CD_OFF + o) = cd;
-          // bias: dP1 of the windows whose ReLU output is not 0 (code != 4), per u16 lane
+          // bias: dP1 of the windows whose ReLU output is not 0 (code != 4).  (A packed
+          // u16 multiply by min(code ^ 4, 1) was miscompiled here: d[0] used for every j.)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const u16x2 x4 = __builtin_bit_cast(u16x2, cd[j] ^ 0x00040004u), one = {1, 1};
-            const uint32_t m = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, d[j]) *
-                                                                __builtin_elementwise_min(x4, one));
-            db[2 * j] += __uint_as_float(m << 16);
-            db[2 * j + 1] += __uint_as_float(m & 0xffff0000u);
+            const uint32_t dj = d[j], cj = cd[j];
+            db[2 * j] += (cj & 0xffffu) != 4u ? __uint_as_float(dj << 16) : 0.f;
+            db[2 * j + 1] += (cj >> 16) != 4u ? __uint_as_float(dj & 0xffff0000u) : 0.f;
           }
         }
-        load_u(r, u, tid);
       }
+      load_u(r, u, tid);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -183,9 +184,9 @@ __global__ __launch_bounds__(NT, 1) void refc1_wgrad_k(const Args g) {
 
   for (int e = tid; e < LDS_BYTES / 16; e += NT) *(u32x4*)(lds + 16 * e) = u32x4{0u, 0u, 0u, 0u};
   Stage<U8, IDX> st;
-  st.load_row(g, tile0(0), wave);
-  st.load(g, tile0(0), tid, wave, lane);
-  st.load_row(g, tile0(1), wave);
+  st.load_row(g, tile0(0), tid);
+  st.load(g, tile0(0), tid);
+  st.load_row(g, tile0(1), tid);
 
   const int sig = wave & 1, cg = (wave >> 1) & 3, kh = wave >> 3;   // uniform
   f32x4 acc[3][2];
@@ -198,9 +199,10 @@ __global__ __launch_bounds__(NT, 1) void refc1_wgrad_k(const Args g) {
     {
       const int ln = lane_now();
       st.store_load(lds, g, tile0(k + 1), wave * 64 + ln, wave, ln, db);
-      st.load_row(g, tile0(k + 2), wave);
+      st.load_row(g, tile0(k + 2), wave * 64 + ln);
     }
     __syncthreads();
+    if (g.skip & 1) continue;
     // ---- GEMM: window rows 7 kh .. 7 kh + 6 of parity set sig, channel group cg.  K row
     // 8g + 4rho + q = item 16(g>>1) + 8rho + 4(g&1) + q: image q, window 4(g>>1) + (g&1) + 2rho.
     {
@@ -277,7 +279,11 @@ using Kern = void (*)(Args);
 constexpr Kern kRefc1[4] = {refc1_wgrad_k<false, false>, refc1_wgrad_k<false, true>, refc1_wgrad_k<true, false>,
                             refc1_wgrad_k<true, true>};
 
+int g_skip = 0;
+
 }  // namespace
+
+void refc1_set_skip(int s) { g_skip = s; }
 
 int refc1_wgrad_grid() {
   static int n = 0;
@@ -307,7 +313,7 @@ hipError_t refc1_wgrad(const XSrc& x, const bf16_t* dn, const bf16_t* p1, const 
   if (B <= 0) return hipSuccess;
   if ((!x.x && !x.u8) || grid <= 0 || refc1_wgrad_grid() <= 0) return hipErrorInvalidValue;
   if (beta != 0.75f) return hipErrorInvalidValue;   // the lrn_bwd8 fast path (the reference's beta)
-  Args a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, dn, p1, arg, B, bias, alpha, beta, slab};
+  Args a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, dn, p1, arg, B, bias, alpha, beta, slab, g_skip};
   const Kern k = kRefc1[(x.u8 ? 2 : 0) + (x.idx ? 1 : 0)];
   void* args[] = {&a};
   return hipLaunchKernel((const void*)k, dim3(grid), dim3(NT), args, LDS_BYTES, st);

@@ -25,6 +25,7 @@ keep the unfused pair's arithmetic (tests/test_f32_gpu.py compares them).
 from __future__ import annotations
 
 import math
+import os
 from typing import Callable, Dict, List, Optional
 
 import torch
@@ -128,8 +129,10 @@ class LRNF(_L):
         s = self.spec
         kernels().f32_lrn_fwd(self.x, self.out, self._p(nb), self.C, s.depth_radius, s.bias, s.alpha, s.beta)
 
+    folded = False   # the backward runs inside the preceding ConvPoolF's weight gradient
+
     def bwd_data(self, nb: int, dy, dx) -> None:
-        if dx is not None:
+        if dx is not None and not self.folded:
             s = self.spec
             kernels().f32_lrn_bwd(self.x, dy, dx, self._p(nb), self.C, s.depth_radius, s.bias, s.alpha, s.beta,
                                   self.in_relu)
@@ -170,10 +173,18 @@ class ConvPoolF(_L):
         kernels().f32_conv1_fwd_pool(self.x, self.fp.param_view(self.wname), self.fp.param_view(self.bname),
                                      self.out, self.arg, nb)
 
+    # (LRN spec, dL/d LRN output): the following norm1's backward runs inside this weight
+    # gradient (conv1_f32_wgrad_lrn_k), dL/d pool1 is never written
+    lrn_fold: Optional[tuple] = None
+
     def bwd_weight(self, nb: int, dy: torch.Tensor) -> None:
         s, K = self.spec, kernels()
         S = min(self.splits, max(1, nb))
-        K.f32_conv1_wgrad_unpool(self.x, dy, self.arg, self.slab, nb, S)
+        if self.lrn_fold is not None:
+            ls, dn = self.lrn_fold
+            K.f32_conv1_wgrad_lrn(self.x, dn, self.out, self.arg, self.slab, nb, S, ls.bias, ls.alpha, ls.beta)
+        else:
+            K.f32_conv1_wgrad_unpool(self.x, dy, self.arg, self.slab, nb, S)
         K.splitk_reduce(self.slab, S, self.M, s.cout, s.kh * s.kw, self.C, self.C, s.cout, s.kh * s.kw * self.C,
                         self.fp.grad_view(self.wname), self.fp.grad_view(self.bname), 1.0)
 
@@ -317,6 +328,15 @@ class HipNetF32:
         self.n_classes = spec.num_classes
         self.dlogits = torch.zeros_like(self.logits)
         self.dbuf: List[Optional[torch.Tensor]] = [None] + [torch.zeros_like(l.out) for l in self.layers[:-1]]
+        # norm1's backward folded into conv1's weight gradient (reference CNN: conv1 + pool1 ->
+        # norm1, radius 4 over 32 channels); MNISTX_F32_FOLD_LRN=0 keeps the separate LRN backward
+        self.fold_lrn = False
+        L0, L1 = self.layers[0], self.layers[1] if len(self.layers) > 1 else None
+        if (fuse and isinstance(L0, ConvPoolF) and isinstance(L1, LRNF) and L1.x is L0.out and L1.C == 32
+                and L1.spec.depth_radius == 4 and not L1.in_relu and os.environ.get("MNISTX_F32_FOLD_LRN", "1") != "0"):
+            L0.lrn_fold = (L1.spec, self.dbuf[2])
+            L1.folded = True
+            self.fold_lrn = True
         self.stats = _f32(8, device=dev)
         self.eval_stats = _f32(8, device=dev)
         self.ce_work = _f32(4 * 1024 + 1, device=dev)

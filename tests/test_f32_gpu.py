@@ -246,3 +246,34 @@ def test_f32_fused_pairs_bitwise(dev, K):
         assert torch.equal(res[0][i], res[1][i]), what
     errs = {n: rel_err(res[0][1][n], res[1][1][n]) for n in init}
     assert max(errs.values()) < 1e-6, errs
+
+
+@pytest.mark.parametrize("B", [3, 700])
+def test_f32_lrn1_backward_fold(dev, K, B, grid_cap, monkeypatch):
+    """norm1's backward folded into conv1's weight gradient (conv1_f32_wgrad_lrn_k: dL/d pool1
+    never written) vs the separate LRN backward + un-pooling weight gradient: same LRN
+    arithmetic (lrn_f32.h), same image -> block assignment and summation order, so every
+    gradient is bitwise equal.  B = 700 with the grid capped: several images per block (the
+    next image's operands prefetched during this one's MFMAs)."""
+    from distributed_tensorflow_ibm_mnist_amd.runtime.executor_f32 import HipNetF32
+    torch.manual_seed(3)
+    spec = get_model("reference_cnn", 1)
+    init = torch_ref.init_params(spec, seed=6)
+    x = torch.rand(B, 28, 28, 1, device=dev) - 0.5
+    y = torch.randint(0, 10, (B,), device=dev, dtype=torch.int32)
+    grid_cap(7 if B > 100 else 0)
+    res = []
+    for fold in ("1", "0"):
+        monkeypatch.setenv("MNISTX_F32_FOLD_LRN", fold)
+        net = HipNetF32(spec, B, dev, init, OptConfig(lr0=0.05))
+        assert net.fold_lrn == (fold == "1")
+        net.x0.copy_(x)
+        net.labels.copy_(y)
+        net.forward()
+        net.loss_and_grad()
+        net.backward()
+        torch.cuda.synchronize()
+        res.append({n: net.fp.grad_view(n).clone() for n in init})
+    for n in init:
+        assert torch.isfinite(res[0][n]).all(), n
+        assert torch.equal(res[0][n], res[1][n]), (n, rel_err(res[0][n], res[1][n]))

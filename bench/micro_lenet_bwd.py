@@ -60,6 +60,8 @@ def main():
 
     timeit(lambda: K.lenet_bwd(ds, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx), iters=200, reps=1)  # clocks up
     fused = timeit(lambda: K.lenet_bwd(ds, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx))
+    # the band forward (conv1 + pool1 + conv2 + pool2, pool1 / codes copied out) on the same box
+    band = timeit(lambda: K.lenet_band_fwd(ds, w1, b1, 6, w2, b2, B, P2, A2, p1=P1, arg1=A1, idx=idx))
     # the input read as uint8 (half the bytes of the bf16 copy; normalised while staging)
     ds_u8 = torch.randint(0, 256, (n, 784), device=dev, dtype=torch.uint8)
     fused_u8 = timeit(lambda: K.lenet_bwd(ds_u8, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx))
@@ -93,7 +95,7 @@ def main():
     torch.cuda.synchronize()
     pr = prof.tolist()
     tot = max(1, sum(pr))
-    print(json.dumps({"B": B, "grid": grid, "fused_us": round(fused, 1), "fused_u8_us": round(fused_u8, 1), "fused_us_by_batch": scaling, "prof_us_by_skip": skip_us,
+    print(json.dumps({"B": B, "grid": grid, "fused_us": round(fused, 1), "band_fwd_us": round(band, 1), "fused_u8_us": round(fused_u8, 1), "fused_us_by_batch": scaling, "prof_us_by_skip": skip_us,
                       "split_us": {"c2_dgrad": round(dgr, 1), "c2_wgrad": round(w2g, 1), "c1_wgrad": round(w1g, 1),
                                    "sum": round(dgr + w2g + w1g, 1)},
                       "phase_share": {k: round(v / tot, 3) for k, v in zip(PHASES, pr)}}), flush=True)

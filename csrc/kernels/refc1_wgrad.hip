@@ -2,7 +2,7 @@
 //
 // conv1 (5x5 SAME, 28x28x1 -> 32) -> ReLU -> pool1 (2x2/2) -> norm1 (LRN, radius 4):
 // /root/reference/mnist_input.py:142-151, differentiated by compute_gradients (:262).  Per
-// 4-image tile the kernel
+// 2-image tile the kernel
 //   1. applies the LRN backward to dL/d norm1 (with the pool1 activations, lrn_bwd8: the
 //      same arithmetic and bf16 rounding as lrn_bwd_k) and keeps dP1 = dL/d pool1 in LDS,
 //      with the pool argmax codes (one u16 per channel; 4 = ReLU output 0);
@@ -10,16 +10,20 @@
 //      C[(ty, tx)][(c, d)] = sum over windows w of X[2yp + ty - 2][2xp + tx - 2] *
 //      dP1[w][c] [code(w, c) == d], folded to dW1[dy][dx][c] = sum_d C[(dy + a, dx + b)][(c, d)]
 //      at the end (d = 2a + b; tx taken by window x parity: two accumulator sets).
-// Every product is a v_mfma_f32_16x16x32_bf16 on ds_read_b64_tr_b16 fragments; K items are
-// (window, image) with the 4 images fastest over window rows padded to 8 per parity set, so
-// a k-step is one window row: lane addresses are a per-lane base plus a uniform step, and
-// with the strides below every read is bank-conflict-free (per 32-lane half, in dwords mod
-// 64: A = 26 q + 20 ty&1 + 2 (xi + pc) + {0, 1}, B = 4 q + 32 xi + 2 pc + {0, 1}; equal
-// addresses are broadcasts).  16 waves: wave w owns parity set w & 1, channel group (w >> 1) & 3
-// (8 channels x 4 window positions = 2 N tiles) and half (w >> 3) of the 14 window rows.
-// The conv1 bias gradient is the sum of the active windows' dP1.  One deterministic split-K
-// slab [grid][48][32] per launch in convpool_wgrad's layout (rows kh * 8 + kw, bias 40), so
-// the executor's splitk_reduce is the same.
+// Warp-specialised pipeline (one block of 16 waves per CU, persistent): waves 0-7 stage tile
+// k (LRN backward, VALU) into one LDS buffer while waves 8-15 run tile k-1's GEMM (MFMA) from
+// the other, one barrier per tile.  With every wave doing both phases between barriers the
+// two never overlapped: the LRN math (~60 us), the GEMM (~40 us) and the staging (~40 us)
+// added up to 167 us at B = 16384 (skip-bit attribution, profiles/r4/refcnn/).
+// Every product is a v_mfma_f32_16x16x32_bf16 on ds_read_b64_tr_b16 fragments.  A k-step is
+// one window-row pair of one parity set: K row 8g + 4rho + q = (window 4(g>>1) + (g&1) +
+// 2rho of the set, row 2r + (q >> 1), image q & 1), so a lane address is a per-lane base
+// plus a uniform step, and with the strides below every read is bank-conflict-free
+// (bench/lds_refc1.py).  Consumer wave w owns parity set w & 1 and channel group w >> 1 (8
+// channels x 4 window positions = 2 N tiles) over all 7 row pairs.  The conv1 bias gradient
+// is the sum of the active windows' dP1 (producer lanes).  One deterministic split-K slab
+// [grid][48][32] per launch in convpool_wgrad's layout (rows kh * 8 + kw, bias 40), so the
+// executor's splitk_reduce is the same.
 //
 // Replaces convpool_wgrad_k<RefC1g> with its LRN fold (259.9 us at B = 16384, 6.8 % MFMA
 // busy, VALU/MFMA 37.5: profiles/r4/refcnn/).
@@ -31,21 +35,22 @@
 namespace mnistx {
 namespace {
 
-constexpr int NT = 1024, NW = 16, T = 4, C = 32, NWIN = 196;
-// ---- LDS layout (bytes)
-constexpr int X_RS = 80, X_IMG = 2664;                      // input [img][row -2..29][col -4..35] bf16
-constexpr int X_OFF = 0, X_SZ = T * X_IMG;
-constexpr int D_RS = 1024, D_IMG = 14352;                   // dP1 / codes [img][14][16 windows][32] x 2 B
-constexpr int DP1_OFF = X_OFF + X_SZ, D_SZ = T * D_IMG;
-constexpr int CD_OFF = DP1_OFF + D_SZ;
-constexpr int LDS_BYTES = CD_OFF + D_SZ;
-static_assert(32 * X_RS <= X_IMG && 14 * D_RS <= D_IMG && LDS_BYTES <= 163840, "");
-static_assert(NW * 6 * 256 * 4 + NW * C * 4 <= LDS_BYTES, "epilogue scratch");
+constexpr int NT = 1024, NW = 16, NPW = 8, NPT = 64 * NPW, T = 2, C = 32, NWIN = 196;
+// ---- LDS layout (bytes), two buffers
+constexpr int X_RS = 96, X_IMG = 3192;                      // input [img][row -2..29][col -4..35] bf16
+constexpr int D_RS = 1040, D_IMG = 14560;                   // dP1 / codes [img][14][16 windows][32] x 2 B
+constexpr int X_OFF = 0, DP1_OFF = T * X_IMG, CD_OFF = DP1_OFF + T * D_IMG;
+constexpr int BUF = CD_OFF + T * D_IMG;                     // one buffer
+constexpr int LDS_BYTES = 2 * BUF;
+static_assert(32 * X_RS <= X_IMG && 14 * D_RS <= D_IMG && 16 * 64 <= D_RS && LDS_BYTES <= 163840, "");
+static_assert(BUF % 16 == 0 && DP1_OFF % 16 == 0, "");
+static_assert(NPW * 6 * 256 * 4 + NPW * C * 4 <= LDS_BYTES, "epilogue scratch");
 // slab rows = convpool_wgrad's RefC1g layout (splitk_reduce as for it): kh * 8 + kw, bias 40
 constexpr int SLAB_ROWS = 48;
 constexpr int NTASK = T * NWIN * 4;                        // LRN tasks per tile: (window, 8 channels)
-constexpr int PER = (NTASK + NT - 1) / NT;                  // 4 (the last: wave 0 only)
-static_assert((NTASK - (PER - 1) * NT) % 64 == 0, "the partial task round covers whole waves (DPP rows)");
+constexpr int PER = (NTASK + NPT - 1) / NPT;                // 4 rounds over the 512 producer lanes
+static_assert((NTASK - (PER - 1) * NPT) % 16 == 0, "the partial round covers whole DPP rows");
+static_assert(T * NWIN <= NPT, "one input quad per producer lane");
 
 struct Args {
   const bf16_t* x;        // input images [n][784] bf16 (or null with u8)
@@ -61,18 +66,19 @@ struct Args {
   int skip;               // experiments only (refc1_set_skip): 1 no GEMM, 2 no LRN math, 4 no next-tile loads
 };
 
-// staging registers of one tile: LRN task vectors (dL/d norm1, pool1, codes) and the input
+// producer registers of one tile: LRN task vectors (dL/d norm1, pool1, codes) and the input
 template <bool U8, bool IDX>
 struct Stage {
   u32x4 y[PER], p[PER];
   u32x2 a[PER];
-  u32x2 x;                // one 4-pixel quad per thread: image tid / 196, quad tid % 196 (tid < 784)
+  u32x2 x;                // one 4-pixel quad per lane: image t / 196, quad t % 196 (t < 392)
   u32x2 rowv;             // IDX: the batch-index entry of that image, one tile ahead
 
-  DEV void load_row(const Args& g, int t0, int tid) {
+  static DEV int img_of(int t) { return (t * 669) >> 17; }   // t / 196 for t < 1024
+  DEV void load_row(const Args& g, int t0, int t) {
     if constexpr (IDX) {
-      const int img = (tid * 669) >> 17;   // tid / 196 for tid < 1024
-      const bool ok = tid < T * NWIN && t0 >= 0 && t0 + img < g.B;
+      const int img = img_of(t);
+      const bool ok = t < T * NWIN && t0 >= 0 && t0 + img < g.B;
       rowv = buf_b64(buf_rsrc(g.idx, (uint32_t)g.B * 8u), ok ? (uint32_t)(t0 + img) * 8u : BUF_OOB);
     }
   }
@@ -86,19 +92,18 @@ struct Stage {
     return Rsrc{buf_rsrc(g.dn + (int64_t)tb * NWIN * C, nb), buf_rsrc(g.p1 + (int64_t)tb * NWIN * C, nb),
                 buf_rsrc(g.arg + (int64_t)tb * NWIN * C, nb / 2u)};
   }
-  // LRN task vectors of round u (tasks tid + u NT; the last round: wave 0's lanes only)
-  DEV void load_u(const Rsrc& r, int u, int tid) {
-    const int e = tid + u * NT;
+  // every producer lane issues the same loads (out of range: no memory access, zeros), so
+  // the load count per tile is fixed and the compiler's vmcnt waits stay exact
+  DEV void load_u(const Rsrc& r, int u, int t) {
+    const int e = t + u * NPT;
     const uint32_t ok = e < NTASK ? 0u : BUF_OOB;
     y[u] = buf_b128(r.y, 16u * e + ok);
     p[u] = buf_b128(r.p, 16u * e + ok);
     a[u] = buf_b64(r.a, 8u * e + ok);
   }
-  // every wave issues the same loads (out of range: no memory access, zeros), so the load
-  // count per tile is fixed and the compiler's vmcnt waits stay exact across the tile loop
-  DEV void load_x(const Args& g, int t0, int tid) {
-    const int img = (tid * 669) >> 17, q = tid - NWIN * img;
-    const bool ok = tid < T * NWIN && t0 >= 0 && t0 + img < g.B;
+  DEV void load_x(const Args& g, int t0, int t) {
+    const int img = img_of(t), q = t - NWIN * img;
+    const bool ok = t < T * NWIN && t0 >= 0 && t0 + img < g.B;
     constexpr uint32_t esz = U8 ? 1u : 2u;
     const void* base = U8 ? (const void*)g.u8 : (const void*)g.x;
     uint32_t off;
@@ -115,49 +120,48 @@ struct Stage {
     else x = buf_b64(rx, off);
   }
   // (the same issue order as store_load's: the waitcnt pass merges the two at the loop head)
-  DEV void load(const Args& g, int t0, int tid) {
-    load_x(g, t0, tid);
+  DEV void load(const Args& g, int t0, int t) {
+    load_x(g, t0, t);
     __builtin_amdgcn_sched_barrier(0);
     const Rsrc r = rsrc(g, t0);
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-      load_u(r, u, tid);
+      load_u(r, u, t);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  DEV void store_x(uint8_t* lds, int tid) {
-    if (tid < T * NWIN) {
-      const int img = (tid * 669) >> 17, q = tid - NWIN * img, y = (q * 147) >> 10, k = q - 7 * y;
+  DEV void store_x(uint8_t* buf, int t) {
+    if (t < T * NWIN) {
+      const int img = img_of(t), q = t - NWIN * img, yy = (q * 147) >> 10, k = q - 7 * yy;
       uint32_t lo = x[0], hi = x[1];
       if constexpr (U8) {
         const uint32_t b = x[0];
         lo = pack2(u8_norm(b & 0xff), u8_norm((b >> 8) & 0xff));
         hi = pack2(u8_norm((b >> 16) & 0xff), u8_norm(b >> 24));
       }
-      *(u32x2*)(lds + X_OFF + img * X_IMG + (y + 2) * X_RS + (4 * k + 4) * 2) = u32x2{lo, hi};
+      *(u32x2*)(buf + X_OFF + img * X_IMG + (yy + 2) * X_RS + (4 * k + 4) * 2) = u32x2{lo, hi};
     }
   }
-  // Staging of this tile into LDS -- the input, then per round the LRN backward -> dP1 (bf16)
-  // and the codes (u16), with the bias sums of the active windows -- each part's registers
-  // refilled with the next tile's data right after use, so those loads stream in during the
-  // rest of this staging and the GEMM (not only during the GEMM).
-  DEV void store_load(uint8_t* lds, const Args& g, int t_next, int tid, int wave, int ln, float (&db)[8]) {
+  // This tile into LDS buffer `buf` -- the input, then per round the LRN backward -> dP1
+  // (bf16) and the codes (u16), with the bias sums of the active windows -- each part's
+  // registers refilled with the next tile's data right after use.
+  DEV void store_load(uint8_t* buf, const Args& g, int t_next, int t, float (&db)[8]) {
     if (g.skip & 4) t_next = -1;
-    store_x(lds, tid);
-    load_x(g, t_next, tid);
+    store_x(buf, t);
+    load_x(g, t_next, t);
     const Rsrc r = rsrc(g, t_next);
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-      const int e = tid + u * NT;
-      if (u < PER - 1 || wave == 0) {
-        const u32x4 d = (g.skip & 2) ? y[u] : lrn_bwd8<4, 4, true>(p[u], y[u], tid & 3, g.bias, g.alpha, g.beta, 0);
+      const int e = t + u * NPT;
+      if (u < PER - 1 || t < NTASK - (PER - 1) * NPT) {   // whole DPP rows (lrn_bwd8's exchanges)
+        const u32x4 d = (g.skip & 2) ? y[u] : lrn_bwd8<4, 4, true>(p[u], y[u], t & 3, g.bias, g.alpha, g.beta, 0);
         const uint32_t a0 = a[u][0], a1 = a[u][1];
         const u32x4 cd = u32x4{bytes01(a0), bytes23(a0), bytes01(a1), bytes23(a1)};
         if (e < NTASK) {
           const int px = e >> 2, cg = e & 3, img = px / NWIN, w = px - img * NWIN, yp = w / 14, xp = w - 14 * yp;
           const int o = img * D_IMG + yp * D_RS + xp * 64 + 16 * cg;
-          *(u32x4*)(lds + DP1_OFF + o) = d;
-          *(u32x4*)(lds + CD_OFF + o) = cd;
+          *(u32x4*)(buf + DP1_OFF + o) = d;
+          *(u32x4*)(buf + CD_OFF + o) = cd;
           // bias: dP1 of the windows whose ReLU output is not 0 (code != 4).  (A packed
           // u16 multiply by min(code ^ 4, 1) was miscompiled here: d[0] used for every j.)
 #pragma unroll
@@ -168,11 +172,39 @@ struct Stage {
           }
         }
       }
-      load_u(r, u, tid);
+      load_u(r, u, t);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
 };
+
+// one tile's GEMM (consumer wave w = parity set w & 1, channel group w >> 1) from `buf`
+DEV void gemm_tile(const uint8_t* buf, int w, f32x4 (&acc)[3][2]) {
+  const int sig = w & 1, cg = w >> 1;
+  const int ln = lane_now(), gg = ln >> 4, q = (ln >> 2) & 3, p = ln & 3;
+  const int hA = p >> 1, pc = p & 1, xil = 4 * (gg >> 1) + (gg & 1), yr = q >> 1, im = q & 1;
+  const uint32_t dsel = (uint32_t)((ln & 15) >> 3);
+  const uint32_t dd0 = dsel * 0x00010001u, dd1 = (2u + dsel) * 0x00010001u;
+  const int aB = X_OFF + im * X_IMG + (2 * yr + hA) * X_RS + (4 * xil + 4 * pc + 4 * sig) * 2;
+  const int bB = DP1_OFF + im * D_IMG + yr * D_RS + (2 * xil + sig) * 64 + 16 * cg + 8 * pc;
+#pragma unroll 2
+  for (int r = 0; r < 7; ++r) {
+    const int sa = aB + 4 * r * X_RS, sb = bB + 2 * r * D_RS;
+    const u32x4 dv = __builtin_bit_cast(u32x4, frag(tr4(buf, sb), tr4(buf, sb + 256)));
+    const u32x4 cv = __builtin_bit_cast(u32x4, frag(tr4(buf, sb + (CD_OFF - DP1_OFF)),
+                                                     tr4(buf, sb + (CD_OFF - DP1_OFF) + 256)));
+    const bf16x8 B0 = __builtin_bit_cast(bf16x8, u32x4{sel_eq(dv[0], cv[0], dd0), sel_eq(dv[1], cv[1], dd0),
+                                                       sel_eq(dv[2], cv[2], dd0), sel_eq(dv[3], cv[3], dd0)});
+    const bf16x8 B1 = __builtin_bit_cast(bf16x8, u32x4{sel_eq(dv[0], cv[0], dd1), sel_eq(dv[1], cv[1], dd1),
+                                                       sel_eq(dv[2], cv[2], dd1), sel_eq(dv[3], cv[3], dd1)});
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const bf16x8 Af = frag(tr4(buf, sa + 2 * t * X_RS), tr4(buf, sa + 2 * t * X_RS + 16));
+      acc[t][0] = mfma16(Af, B0, acc[t][0]);
+      acc[t][1] = mfma16(Af, B1, acc[t][1]);
+    }
+  }
+}
 
 template <bool U8, bool IDX>
 __global__ __launch_bounds__(NT, 1) void refc1_wgrad_k(const Args g) {
@@ -183,93 +215,74 @@ __global__ __launch_bounds__(NT, 1) void refc1_wgrad_k(const Args g) {
   auto tile0 = [&](int k) { return k < nk ? ((int)blockIdx.x + k * (int)gridDim.x) * T : -1; };
 
   for (int e = tid; e < LDS_BYTES / 16; e += NT) *(u32x4*)(lds + 16 * e) = u32x4{0u, 0u, 0u, 0u};
-  Stage<U8, IDX> st;
-  st.load_row(g, tile0(0), tid);
-  st.load(g, tile0(0), tid);
-  st.load_row(g, tile0(1), tid);
-
-  const int sig = wave & 1, cg = (wave >> 1) & 3, kh = wave >> 3;   // uniform
   f32x4 acc[3][2];
 #pragma unroll
   for (int t = 0; t < 3; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   float db[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
-  for (int k = 0; k < nk; ++k) {
-    __syncthreads();   // the previous tile's GEMM no longer reads dP1 / codes / input
-    {
-      const int ln = lane_now();
-      st.store_load(lds, g, tile0(k + 1), wave * 64 + ln, wave, ln, db);
-      st.load_row(g, tile0(k + 2), wave * 64 + ln);
-    }
-    __syncthreads();
-    if (g.skip & 1) continue;
-    // ---- GEMM: window rows 7 kh .. 7 kh + 6 of parity set sig, channel group cg.  K row
-    // 8g + 4rho + q = item 16(g>>1) + 8rho + 4(g&1) + q: image q, window 4(g>>1) + (g&1) + 2rho.
-    {
-      const int ln = lane_now(), gg = ln >> 4, q = (ln >> 2) & 3, p = ln & 3;
-      const int hA = p >> 1, pc = p & 1, xil = 4 * (gg >> 1) + (gg & 1);
-      const uint32_t dsel = (uint32_t)((ln & 15) >> 3);
-      const uint32_t dd0 = dsel * 0x00010001u, dd1 = (2u + dsel) * 0x00010001u;
-      const int aB = X_OFF + q * X_IMG + hA * X_RS + (4 * xil + 4 * pc + 4 * sig) * 2;
-      const int bB = DP1_OFF + q * D_IMG + (2 * xil + sig) * 64 + 16 * cg + 8 * pc;
-#pragma unroll 2
-      for (int yp = 7 * kh; yp < 7 * kh + 7; ++yp) {
-        const int sa = aB + 2 * yp * X_RS, sb = bB + yp * D_RS;
-        const u32x4 dv = __builtin_bit_cast(u32x4, frag(tr4(lds, sb), tr4(lds, sb + 256)));
-        const u32x4 cv = __builtin_bit_cast(u32x4, frag(tr4(lds, sb + (CD_OFF - DP1_OFF)),
-                                                         tr4(lds, sb + (CD_OFF - DP1_OFF) + 256)));
-        const bf16x8 B0 = __builtin_bit_cast(bf16x8, u32x4{sel_eq(dv[0], cv[0], dd0), sel_eq(dv[1], cv[1], dd0),
-                                                           sel_eq(dv[2], cv[2], dd0), sel_eq(dv[3], cv[3], dd0)});
-        const bf16x8 B1 = __builtin_bit_cast(bf16x8, u32x4{sel_eq(dv[0], cv[0], dd1), sel_eq(dv[1], cv[1], dd1),
-                                                           sel_eq(dv[2], cv[2], dd1), sel_eq(dv[3], cv[3], dd1)});
-#pragma unroll
-        for (int t = 0; t < 3; ++t) {
-          const bf16x8 Af = frag(tr4(lds, sa + 2 * t * X_RS), tr4(lds, sa + 2 * t * X_RS + 16));
-          acc[t][0] = mfma16(Af, B0, acc[t][0]);
-          acc[t][1] = mfma16(Af, B1, acc[t][1]);
-        }
+  if (wave < NPW) {
+    // ======================================================== producers: LRN backward staging
+    Stage<U8, IDX> st;
+    st.load_row(g, tile0(0), tid);
+    st.load(g, tile0(0), tid);
+    st.load_row(g, tile0(1), tid);
+    for (int k = 0; k <= nk; ++k) {
+      __syncthreads();   // buffer k & 1 is no longer read by the consumers (tile k - 2)
+      if (k < nk) {
+        const int t = wave * 64 + lane_now();
+        st.store_load(lds + (k & 1) * BUF, g, tile0(k + 1), t, db);
+        st.load_row(g, tile0(k + 2), t);
       }
+    }
+  } else {
+    // ======================================================== consumers: the GEMM of tile k - 1
+    for (int k = 0; k <= nk; ++k) {
+      __syncthreads();   // buffer (k - 1) & 1 holds tile k - 1
+      if (k > 0 && !(g.skip & 1)) gemm_tile(lds + ((k - 1) & 1) * BUF, wave - NPW, acc);
     }
   }
 
-  // ---- epilogue: partials of the 16 waves -> one slab (fixed summation order)
+  // ---- epilogue: consumer accumulators + producer bias sums -> one slab (fixed order)
   const int i16 = lane & 15, g4 = lane >> 4;
   __syncthreads();
-  float* e1 = (float*)lds;                          // [wave][t][nt][col 16][row 16]
+  float* e1 = (float*)lds;                          // [consumer w][t][nt][col 16][row 16]
+  float* eb = e1 + NPW * 6 * 256;                   // [producer wave][32]
+  if (wave >= NPW) {
+    const int w = wave - NPW;
 #pragma unroll
-  for (int t = 0; t < 3; ++t)
+    for (int t = 0; t < 3; ++t)
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-      *(f32x4*)(e1 + (((wave * 3 + t) * 2 + nt) * 16 + i16) * 16 + 4 * g4) = acc[t][nt];
-  // bias: lanes with the same (lane & 3) hold the same 8 channels (8 (lane & 3) + j)
+      for (int nt = 0; nt < 2; ++nt)
+        *(f32x4*)(e1 + (((w * 3 + t) * 2 + nt) * 16 + i16) * 16 + 4 * g4) = acc[t][nt];
+  } else {
+    // lanes with the same (lane & 3) hold the same 8 channels (8 (lane & 3) + j)
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < 8; ++j) {
 #pragma unroll
-    for (int m = 4; m <= 32; m *= 2) db[j] += __shfl_xor(db[j], m);
+      for (int m = 4; m <= 32; m *= 2) db[j] += __shfl_xor(db[j], m);
+    }
+    if (lane < 4)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) eb[wave * C + 8 * lane + j] = db[j];
   }
-  float* eb = e1 + NW * 6 * 256;                    // [wave][32]
-  if (lane < 4)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) eb[wave * C + 8 * lane + j] = db[j];
   __syncthreads();
   float* s = g.slab + (int64_t)blockIdx.x * SLAB_ROWS * C;
   for (int e = tid; e < SLAB_ROWS * C; e += NT) {
     const int r = e >> 5, c = e & 31, cgc = c >> 3, cl = c & 7, dy = r >> 3, dx = r & 7;
     float v = 0.f;
     if (r < 40 && dx < 5) {
-      for (int h = 0; h < 2; ++h)
-        for (int sg = 0; sg < 2; ++sg) {
-          const int w = sg + 2 * cgc + 8 * h;
+      for (int sg = 0; sg < 2; ++sg) {
+        const int w = sg + 2 * cgc;
 #pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            const int ty = dy + (d >> 1), tx = dx + (d & 1), txi = tx + (sg ? 0 : 2);
-            const int t = ty >> 1, row = 4 * (2 * (ty & 1) + (txi >> 2)) + (txi & 3);
-            const int nt = d >> 1, col = cl + 8 * (d & 1);
-            v += e1[(((w * 3 + t) * 2 + nt) * 16 + col) * 16 + row];
-          }
+        for (int d = 0; d < 4; ++d) {
+          const int ty = dy + (d >> 1), tx = dx + (d & 1), txi = tx + (sg ? 0 : 2);
+          const int t = ty >> 1, row = 4 * (2 * (ty & 1) + (txi >> 2)) + (txi & 3);
+          const int nt = d >> 1, col = cl + 8 * (d & 1);
+          v += e1[(((w * 3 + t) * 2 + nt) * 16 + col) * 16 + row];
         }
+      }
     } else if (r == 40) {
-      for (int w = 0; w < NW; ++w) v += eb[w * C + c];
+      for (int w = 0; w < NPW; ++w) v += eb[w * C + c];
     }
     s[e] = v;
   }

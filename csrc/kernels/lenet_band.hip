@@ -57,10 +57,14 @@ constexpr int XIMG = 784;
 constexpr int XRW = 32, XPL = 448, XIS = 900;
 //  pool1 : image [plane 2][7 rows][14 px][8 ch]
 constexpr int PRW = 112, PPL = 792, PIS = 1584;
-// odd images of the pool1 ring start one 16-byte slot later: the conv2 B reads of a lane
-// group (2 pooled pixels x 4 images of one parity, bench/lds_band.py) then hit 16 distinct
-// bank slots (2-way before), and the conv1 stores (one 16-byte pixel per lane) stay
-// conflict-free; the last image still ends inside the ring (7 PIS + 8 + PPL + 7 PRW = 8 PIS)
+// SK layout (MNISTX_BAND_SKEW=1, off by default): odd images of the pool1 ring start one
+// 16-byte slot later and each pixel is one 16-byte store from the h = 0 lane -- the bank model
+// (bench/lds_band.py) goes from 34 % to 15 % conflict cycles (conv2 B reads and pool1 stores
+// conflict-free), but the kernel measured 4 us SLOWER on the same box (132.9 vs 128.7 us at
+// B = 65536, profiles/r4/lenet_band_skew_ab.txt): the two permlane32 swaps land on the conv1
+// role, the critical one (~90 % busy vs ~73 % for conv2), while the conv2 reads it speeds up
+// are off the critical path.  The last image still ends inside the ring (7 PIS + 8 + PPL + 7 PRW
+// = 8 PIS).
 constexpr int PSK = 8;
 template <bool SK = true>
 constexpr int pib(int i) { return i * PIS + (SK ? (i & 1) * PSK : 0); }
@@ -172,8 +176,8 @@ struct XFill {
 // Warp-specialised pipeline over the block's tiles k = 0..nk-1 (tile blockIdx + k * grid):
 // iteration k: conv1 waves turn input[k%2] into pool1[k%2] (and load tile k+1's input),
 // conv2 waves turn pool1[(k-1)%2] into pool2 -- one barrier per iteration, nk+1 iterations.
-// SK = false: the round-3 pool1 layout (no skew, two 8-byte stores per pixel), kept for the
-// same-box A/B (MNISTX_BAND_SKEW=0)
+// SK = false (default): the pool1 layout without skew, two 8-byte stores per pixel; SK = true:
+// the skewed layout above (MNISTX_BAND_SKEW=1, same-box A/B)
 template <bool P1OUT, bool SK = true>
 __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_X + LDS_P];
@@ -637,7 +641,7 @@ hipError_t lenet_band_fwd(const XSrc& x, const bf16_t* w1, const float* b1, int 
     hipLaunchKernelGGL(ker, dim3(grid), dim3(NTH), 0, st, a);
     return hipSuccess;
   };
-  static const bool sk = [] { const char* e = getenv("MNISTX_BAND_SKEW"); return !(e && e[0] == '0'); }();
+  static const bool sk = [] { const char* e = getenv("MNISTX_BAND_SKEW"); return e && e[0] == '1'; }();
   hipError_t e;
   if (sk)
     e = p1 ? go(lenet_band_fwd_k<true, true>, fwd_grid<true, true>(ntiles))

@@ -12,9 +12,12 @@
 //      at the end (d = 2a + b; tx taken by window x parity: two accumulator sets).
 // Warp-specialised pipeline (one block of 16 waves per CU, persistent): waves 0-7 stage tile
 // k (LRN backward, VALU) into one LDS buffer while waves 8-15 run tile k-1's GEMM (MFMA) from
-// the other, one barrier per tile.  With every wave doing both phases between barriers the
-// two never overlapped: the LRN math (~60 us), the GEMM (~40 us) and the staging (~40 us)
-// added up to 167 us at B = 16384 (skip-bit attribution, profiles/r4/refcnn/).
+// the other, one barrier per tile.  Measured at B = 16384 (bench/micro_refc1.py skip bits,
+// profiles/r4/refcnn/micro_refc1_v*.txt): 167 us, the same as the serial 4-image-tile version
+// (every wave staging then multiplying between two barriers, 155-167 us): the GEMM is now
+// hidden (no-GEMM 135 us) but the LRN backward -- ~250 VALU + 16 transcendental + 16 DPP
+// instructions per 8 channels -- bounds the staging, and on 8 waves (the last of 4 rounds
+// on wave 0 only) it is exposed longer.
 // Every product is a v_mfma_f32_16x16x32_bf16 on ds_read_b64_tr_b16 fragments.  A k-step is
 // one window-row pair of one parity set: K row 8g + 4rho + q = (window 4(g>>1) + (g&1) +
 // 2rho of the set, row 2r + (q >> 1), image q & 1), so a lane address is a per-lane base

@@ -61,7 +61,7 @@ constexpr int PRW = 112, PPL = 792, PIS = 1584;
 // 16-byte slot later and each pixel is one 16-byte store from the h = 0 lane -- the bank model
 // (bench/lds_band.py) goes from 34 % to 15 % conflict cycles (conv2 B reads and pool1 stores
 // conflict-free), but the kernel measured 4 us SLOWER on the same box (132.9 vs 128.7 us at
-// B = 65536, profiles/r4/lenet_band_skew_ab.txt): the two permlane32 swaps land on the conv1
+// B = 65536, profiles/r4/lenet_band/skew_ab.txt): the two permlane32 swaps land on the conv1
 // role, the critical one (~90 % busy vs ~73 % for conv2), while the conv2 reads it speeds up
 // are off the critical path.  The last image still ends inside the ring (7 PIS + 8 + PPL + 7 PRW
 // = 8 PIS).

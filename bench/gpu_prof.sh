@@ -10,5 +10,5 @@ shift
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 for e in "${ENVS[@]}"; do export "$e"; done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --prewarm_ms 0 --graph 0 --phases 0 --eager_steps 0 "$@" > $OUT/prof.log 2>&1 || { echo "prof failed"; tail -5 $OUT/prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py "$@" --steps 5 --warmup 2 --prewarm_ms 0 --graph 0 --phases 0 --eager_steps 0 > $OUT/prof.log 2>&1 || { echo "prof failed"; tail -5 $OUT/prof.log; exit 1; }
 python3 bench/prof_summary.py $OUT/prof 7 $OUT/kernels.md > /dev/null && head -14 $OUT/kernels.md

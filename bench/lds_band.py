@@ -7,15 +7,16 @@ b32 / ds_read2_b32: one 64-lane group, bank (a/4) % 64.
 
     python bench/lds_band.py [XIS=900 XPL=448 PIS=1584 PPL=792 PRW=112 PSK=8 ...] [--search]
 
-Round 4: PSK = 0 with two 8-byte pool1 stores per pixel modelled 34 % conflict cycles
-(PMC: 31 %); PSK = 8 with one 16-byte store per pixel models 1.0 for the pool1 stores and
-the conv2 B reads.
+The kernel's layout (PSK = 0, two 8-byte pool1 stores per pixel) models 34 % conflict cycles
+(PMC: 31 %).  Round 4 tried PSK = 8 with one 16-byte store per pixel (conv1_store16): it
+models 1.0 for the pool1 stores and the conv2 B reads (15 % overall) but measured 4 us slower
+(profiles/r4/lenet_band/skew_ab.txt: the extra swaps land on the critical conv1 role).
 """
 import sys
 
 from lds_bwd import cycles
 
-DEF = dict(XIS=900, XPL=448, XRW=32, PIS=1584, PPL=792, PRW=112, PSK=8, XSK=0)
+DEF = dict(XIS=900, XPL=448, XRW=32, PIS=1584, PPL=792, PRW=112, PSK=0, XSK=0)
 
 
 def pib(S, i):
@@ -131,7 +132,7 @@ def report(S):
     # issues per tile (per block): conv1 49 units x 3 k-steps x 2 read2, 49 stores; conv2
     # 7 units x 6 rows x 3 b128; copy-out 4 waves x 8 b128; fill 4 waves x 7 x write2
     rows = [("conv1 B (read2_b32 x2)", avg(conv1_b, S, u=range(7), yp0=range(7), p=range(3)), 49 * 3 * 2),
-            ("conv1 pool1 store (w128)", avg(conv1_store16, S, u=range(7), yp0=range(7)), 49),
+            ("conv1 pool1 store (w64)", avg(conv1_store, S, u=range(7), yp0=range(7)), 49),
             ("conv2 B (b128)", avg(conv2_b, S, w2v=range(4), r=range(6), q=range(3)), 7 * 6 * 3),
             ("copy-out (b128)", avg(copy_out, S, wave=range(4), i=range(8)), 4 * 8),
             ("input fill (write2_b32)", avg(xfill, S, wave=range(4), i=range(7)), 4 * 7)]

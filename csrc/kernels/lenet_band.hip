@@ -57,18 +57,6 @@ constexpr int XIMG = 784;
 constexpr int XRW = 32, XPL = 448, XIS = 900;
 //  pool1 : image [plane 2][7 rows][14 px][8 ch]
 constexpr int PRW = 112, PPL = 792, PIS = 1584;
-// SK layout (MNISTX_BAND_SKEW=1, off by default): odd images of the pool1 ring start one
-// 16-byte slot later and each pixel is one 16-byte store from the h = 0 lane -- the bank model
-// (bench/lds_band.py) goes from 34 % to 15 % conflict cycles (conv2 B reads and pool1 stores
-// conflict-free), but the kernel measured 4 us SLOWER on the same box (132.9 vs 128.7 us at
-// B = 65536, profiles/r4/lenet_band/skew_ab.txt): the two permlane32 swaps land on the conv1
-// role, the critical one (~90 % busy vs ~73 % for conv2), while the conv2 reads it speeds up
-// are off the critical path.  The last image still ends inside the ring (7 PIS + 8 + PPL + 7 PRW
-// = 8 PIS).
-constexpr int PSK = 8;
-template <bool SK = true>
-constexpr int pib(int i) { return i * PIS + (SK ? (i & 1) * PSK : 0); }
-static_assert(pib(7) + PPL + 7 * PRW <= 8 * PIS, "");
 constexpr int XBUF = BT * XIS, PBUF = BT * PIS;
 constexpr int XZERO = 2 * XBUF;                 // one zero row: out-of-image input rows
 constexpr int LDS_X = 2 * XBUF + XRW, LDS_P = 2 * PBUF;
@@ -176,9 +164,7 @@ struct XFill {
 // Warp-specialised pipeline over the block's tiles k = 0..nk-1 (tile blockIdx + k * grid):
 // iteration k: conv1 waves turn input[k%2] into pool1[k%2] (and load tile k+1's input),
 // conv2 waves turn pool1[(k-1)%2] into pool2 -- one barrier per iteration, nk+1 iterations.
-// SK = false (default): the pool1 layout without skew, two 8-byte stores per pixel; SK = true:
-// the skewed layout above (MNISTX_BAND_SKEW=1, same-box A/B)
-template <bool P1OUT, bool SK = true>
+template <bool P1OUT>
 __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_X + LDS_P];
   bf16_t* xs = lds;
@@ -239,8 +225,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
     const int xlane = img * XIS + h * XPL + (7 * half - 1) * XRW + 2 * xq;
     const bool top = half == 0, bot = half == 1;   // lanes whose p = 0 / p = 2 row can be padding
     // pool1 store: lane part + the (yp0 parity, half) part of pooled row yp = yp0 + 7 half
-    // SK: the h = 0 lane stores the whole 16-byte pixel
-    const int store_lane = pib<SK>(img) + 8 * xq + (SK ? 0 : 4 * h);
+    const int store_lane = img * PIS + 8 * xq + 4 * h;
     const int row_even = half ? PPL + 3 * PRW : 0;   // yp0 even
     const int row_odd = half ? 4 * PRW : PPL;        // yp0 odd
     // code word: byte k = code(c = k) | code(c = k + 4) << 4; channels 6-7 are padding (code 4)
@@ -307,15 +292,9 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
             const auto sw = __builtin_amdgcn_permlane32_swap(X, X, false, false);
             w1 = h ? 0u : pk2(o[2], __uint_as_float(sw[1]));
           }
-          // the h = 1 half of the pixel (channels 4, 5 and the code word) into the h = 0 lane:
-          // one 16-byte store per pixel (two 8-byte stores from both halves conflicted 2-way)
-          const int off = (yp0 & 1 ? row_odd : row_even) + (yp0 >> 1) * PRW + 16 * u;
-          if constexpr (SK) {
-            const uint32_t s0 = __builtin_amdgcn_permlane32_swap(w0, w0, false, false)[1];
-            const uint32_t s1 = __builtin_amdgcn_permlane32_swap(w1, w1, false, false)[1];
-            if (f < U1 && h == 0) *(u32x4*)(pb + off) = u32x4{w0, w1, s0, s1};
-          } else {
-            if (f < U1) *(u32x2*)(pb + off) = u32x2{w0, w1};
+          if (f < U1) {
+            const int off = (yp0 & 1 ? row_odd : row_even) + (yp0 >> 1) * PRW + 16 * u;
+            *(u32x2*)(pb + off) = u32x2{w0, w1};
           }
         };
         // 13 slots per wave (units wave + 4j, j = 0..12: 52 slots for the 49 units) -- the
@@ -385,7 +364,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
           for (int i0 = 0; i0 < BT; i0 += 4) {
             u32x4 cv[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) cv[i] = *(const u32x4*)(src + pib<SK>(i0 + i));
+            for (int i = 0; i < 4; ++i) cv[i] = *(const u32x4*)(src + (i0 + i) * PIS);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               __builtin_amdgcn_raw_buffer_store_b128(u32x4{cv[i][0], cv[i][1], cv[i][2], 0u}, rp1, (uint32_t)cp_r * 16u,
@@ -410,7 +389,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
           if (u >= 7) break;
           const int f = 4 * u + slot, fc = min(f, 24);
           const int y2p = fc / 5, x2p = fc - 5 * y2p;
-          const bf16_t* rb = pb + pib<SK>(im2) + y2p * PRW + (2 * x2p + h) * 8;
+          const bf16_t* rb = pb + im2 * PIS + y2p * PRW + (2 * x2p + h) * 8;
           auto rowp = [&](int r) { return rb + (r & 1) * PPL + (r >> 1) * PRW; };
           bf16x8 bq[2][3];
 #pragma unroll
@@ -459,7 +438,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
   }
 }
 
-template <bool P1OUT, bool SK>
+template <bool P1OUT>
 int fwd_grid(int ntiles) {
   static int per_cu = -1, cus = 0;
   if (per_cu < 0) {
@@ -469,7 +448,7 @@ int fwd_grid(int ntiles) {
     if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return -1;
     cus = prop.multiProcessorCount;
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lenet_band_fwd_k<P1OUT, SK>, NTH, 0) != hipSuccess) return -1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lenet_band_fwd_k<P1OUT>, NTH, 0) != hipSuccess) return -1;
     per_cu = nb > 0 ? nb : 1;
   }
   return cap_grid(ntiles < per_cu * cus ? ntiles : per_cu * cus);
@@ -641,14 +620,8 @@ hipError_t lenet_band_fwd(const XSrc& x, const bf16_t* w1, const float* b1, int 
     hipLaunchKernelGGL(ker, dim3(grid), dim3(NTH), 0, st, a);
     return hipSuccess;
   };
-  static const bool sk = [] { const char* e = getenv("MNISTX_BAND_SKEW"); return e && e[0] == '1'; }();
-  hipError_t e;
-  if (sk)
-    e = p1 ? go(lenet_band_fwd_k<true, true>, fwd_grid<true, true>(ntiles))
-           : go(lenet_band_fwd_k<false, true>, fwd_grid<false, true>(ntiles));
-  else
-    e = p1 ? go(lenet_band_fwd_k<true, false>, fwd_grid<true, false>(ntiles))
-           : go(lenet_band_fwd_k<false, false>, fwd_grid<false, false>(ntiles));
+  const hipError_t e = p1 ? go(lenet_band_fwd_k<true>, fwd_grid<true>(ntiles))
+                          : go(lenet_band_fwd_k<false>, fwd_grid<false>(ntiles));
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }

@@ -13,20 +13,20 @@
 // Warp-specialised pipeline (one block of 16 waves per CU, persistent): waves 0-7 stage tile
 // k (LRN backward, VALU) into one LDS buffer while waves 8-15 run tile k-1's GEMM (MFMA) from
 // the other, one barrier per tile.  Measured at B = 16384 (bench/micro_refc1.py skip bits,
-// profiles/r4/refcnn/micro_refc1_v*.txt): 167 us, the same as the serial 4-image-tile version
-// (every wave staging then multiplying between two barriers, 155-167 us): the GEMM is now
-// hidden (no-GEMM 135 us) but the LRN backward -- ~250 VALU + 16 transcendental + 16 DPP
-// instructions per 8 channels -- bounds the staging, and on 8 waves (the last of 4 rounds
-// on wave 0 only) it is exposed longer.
+// profiles/r4/refcnn/micro_refc1_v*.txt): 152 us (the serial 4-image-tile version: 155-167).
+// Without the LRN math and the GEMM it is 89 us -- the 0.54 GB of operands at ~6 TB/s, the
+// floor -- and the LRN backward (~200 VALU + 16 transcendental + 16 DPP instructions per 8
+// channels) and the GEMM are not fully hidden behind the loads (115 us without the GEMM).
+// The bias moved off the producers (below) took 167 -> 152 us.
 // Every product is a v_mfma_f32_16x16x32_bf16 on ds_read_b64_tr_b16 fragments.  A k-step is
 // one window-row pair of one parity set: K row 8g + 4rho + q = (window 4(g>>1) + (g&1) +
 // 2rho of the set, row 2r + (q >> 1), image q & 1), so a lane address is a per-lane base
 // plus a uniform step, and with the strides below every read is bank-conflict-free
 // (bench/lds_refc1.py).  Consumer wave w owns parity set w & 1 and channel group w >> 1 (8
 // channels x 4 window positions = 2 N tiles) over all 7 row pairs.  The conv1 bias gradient
-// is the sum of the active windows' dP1 (producer lanes).  One deterministic split-K slab
-// [grid][48][32] per launch in convpool_wgrad's layout (rows kh * 8 + kw, bias 40), so the
-// executor's splitk_reduce is the same.
+// is the sum of the active windows' dP1 (an all-ones A fragment on the consumers).  One
+// deterministic split-K slab [grid][48][32] per launch in convpool_wgrad's layout (rows
+// kh * 8 + kw, bias 40), so the executor's splitk_reduce is the same.
 //
 // Replaces convpool_wgrad_k<RefC1g> with its LRN fold (259.9 us at B = 16384, 6.8 % MFMA
 // busy, VALU/MFMA 37.5: profiles/r4/refcnn/).
@@ -47,7 +47,7 @@ constexpr int BUF = CD_OFF + T * D_IMG;                     // one buffer
 constexpr int LDS_BYTES = 2 * BUF;
 static_assert(32 * X_RS <= X_IMG && 14 * D_RS <= D_IMG && 16 * 64 <= D_RS && LDS_BYTES <= 163840, "");
 static_assert(BUF % 16 == 0 && DP1_OFF % 16 == 0, "");
-static_assert(NPW * 6 * 256 * 4 + NPW * C * 4 <= LDS_BYTES, "epilogue scratch");
+static_assert(NPW * 6 * 256 * 4 + NPW * 16 * 4 <= LDS_BYTES, "epilogue scratch");
 // slab rows = convpool_wgrad's RefC1g layout (splitk_reduce as for it): kh * 8 + kw, bias 40
 constexpr int SLAB_ROWS = 48;
 constexpr int NTASK = T * NWIN * 4;                        // LRN tasks per tile: (window, 8 channels)
@@ -148,31 +148,26 @@ struct Stage {
   // This tile into LDS buffer `buf` -- the input, then per round the LRN backward -> dP1
   // (bf16) and the codes (u16), with the bias sums of the active windows -- each part's
   // registers refilled with the next tile's data right after use.
-  DEV void store_load(uint8_t* buf, const Args& g, int t_next, int t, float (&db)[8]) {
+  // LDS offset of round u's task (the same every tile; -1: no task)
+  static DEV int task_off(int t, int u) {
+    const int e = t + u * NPT;
+    if (e >= NTASK) return -1;
+    const int px = e >> 2, cg = e & 3, img = px / NWIN, w = px - img * NWIN, yp = w / 14, xp = w - 14 * yp;
+    return img * D_IMG + yp * D_RS + xp * 64 + 16 * cg;
+  }
+  DEV void store_load(uint8_t* buf, const Args& g, int t_next, int t, const int (&off)[PER]) {
     if (g.skip & 4) t_next = -1;
     store_x(buf, t);
     load_x(g, t_next, t);
     const Rsrc r = rsrc(g, t_next);
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-      const int e = t + u * NPT;
       if (u < PER - 1 || t < NTASK - (PER - 1) * NPT) {   // whole DPP rows (lrn_bwd8's exchanges)
         const u32x4 d = (g.skip & 2) ? y[u] : lrn_bwd8<4, 4, true>(p[u], y[u], t & 3, g.bias, g.alpha, g.beta, 0);
         const uint32_t a0 = a[u][0], a1 = a[u][1];
-        const u32x4 cd = u32x4{bytes01(a0), bytes23(a0), bytes01(a1), bytes23(a1)};
-        if (e < NTASK) {
-          const int px = e >> 2, cg = e & 3, img = px / NWIN, w = px - img * NWIN, yp = w / 14, xp = w - 14 * yp;
-          const int o = img * D_IMG + yp * D_RS + xp * 64 + 16 * cg;
-          *(u32x4*)(buf + DP1_OFF + o) = d;
-          *(u32x4*)(buf + CD_OFF + o) = cd;
-          // bias: dP1 of the windows whose ReLU output is not 0 (code != 4).  (A packed
-          // u16 multiply by min(code ^ 4, 1) was miscompiled here: d[0] used for every j.)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const uint32_t dj = d[j], cj = cd[j];
-            db[2 * j] += (cj & 0xffffu) != 4u ? __uint_as_float(dj << 16) : 0.f;
-            db[2 * j + 1] += (cj >> 16) != 4u ? __uint_as_float(dj & 0xffff0000u) : 0.f;
-          }
+        if (off[u] >= 0) {
+          *(u32x4*)(buf + DP1_OFF + off[u]) = d;
+          *(u32x4*)(buf + CD_OFF + off[u]) = u32x4{bytes01(a0), bytes23(a0), bytes01(a1), bytes23(a1)};
         }
       }
       load_u(r, u, t);
@@ -182,7 +177,12 @@ struct Stage {
 };
 
 // one tile's GEMM (consumer wave w = parity set w & 1, channel group w >> 1) from `buf`
-DEV void gemm_tile(const uint8_t* buf, int w, f32x4 (&acc)[3][2]) {
+// The conv1 bias gradient (the active windows' dP1 summed) rides along as a product with an
+// all-ones A fragment: every row of accb[nt] is sum_k B[k][n], so sum_d [code == d] dP1 over
+// the tile -- two more MFMAs per k-step on the (hidden) consumer side instead of ~30 VALU
+// per LRN task on the producers.
+DEV void gemm_tile(const uint8_t* buf, int w, f32x4 (&acc)[3][2], f32x4 (&accb)[2]) {
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u});
   const int sig = w & 1, cg = w >> 1;
   const int ln = lane_now(), gg = ln >> 4, q = (ln >> 2) & 3, p = ln & 3;
   const int hA = p >> 1, pc = p & 1, xil = 4 * (gg >> 1) + (gg & 1), yr = q >> 1, im = q & 1;
@@ -206,6 +206,8 @@ DEV void gemm_tile(const uint8_t* buf, int w, f32x4 (&acc)[3][2]) {
       acc[t][0] = mfma16(Af, B0, acc[t][0]);
       acc[t][1] = mfma16(Af, B1, acc[t][1]);
     }
+    accb[0] = mfma16(ones, B0, accb[0]);
+    accb[1] = mfma16(ones, B1, accb[1]);
   }
 }
 
@@ -218,14 +220,17 @@ __global__ __launch_bounds__(NT, 1) void refc1_wgrad_k(const Args g) {
   auto tile0 = [&](int k) { return k < nk ? ((int)blockIdx.x + k * (int)gridDim.x) * T : -1; };
 
   for (int e = tid; e < LDS_BYTES / 16; e += NT) *(u32x4*)(lds + 16 * e) = u32x4{0u, 0u, 0u, 0u};
-  f32x4 acc[3][2];
+  f32x4 acc[3][2], accb[2];
 #pragma unroll
   for (int t = 0; t < 3; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float db[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (wave < NPW) {
     // ======================================================== producers: LRN backward staging
     Stage<U8, IDX> st;
+    int off[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) off[u] = Stage<U8, IDX>::task_off(tid, u);
     st.load_row(g, tile0(0), tid);
     st.load(g, tile0(0), tid);
     st.load_row(g, tile0(1), tid);
@@ -233,7 +238,7 @@ __global__ __launch_bounds__(NT, 1) void refc1_wgrad_k(const Args g) {
       __syncthreads();   // buffer k & 1 is no longer read by the consumers (tile k - 2)
       if (k < nk) {
         const int t = wave * 64 + lane_now();
-        st.store_load(lds + (k & 1) * BUF, g, tile0(k + 1), t, db);
+        st.store_load(lds + (k & 1) * BUF, g, tile0(k + 1), t, off);
         st.load_row(g, tile0(k + 2), t);
       }
     }
@@ -241,15 +246,15 @@ __global__ __launch_bounds__(NT, 1) void refc1_wgrad_k(const Args g) {
     // ======================================================== consumers: the GEMM of tile k - 1
     for (int k = 0; k <= nk; ++k) {
       __syncthreads();   // buffer (k - 1) & 1 holds tile k - 1
-      if (k > 0 && !(g.skip & 1)) gemm_tile(lds + ((k - 1) & 1) * BUF, wave - NPW, acc);
+      if (k > 0 && !(g.skip & 1)) gemm_tile(lds + ((k - 1) & 1) * BUF, wave - NPW, acc, accb);
     }
   }
 
-  // ---- epilogue: consumer accumulators + producer bias sums -> one slab (fixed order)
+  // ---- epilogue: consumer accumulators -> one slab (fixed order)
   const int i16 = lane & 15, g4 = lane >> 4;
   __syncthreads();
   float* e1 = (float*)lds;                          // [consumer w][t][nt][col 16][row 16]
-  float* eb = e1 + NPW * 6 * 256;                   // [producer wave][32]
+  float* eb = e1 + NPW * 6 * 256;                   // [consumer w][col 16]: bias partials
   if (wave >= NPW) {
     const int w = wave - NPW;
 #pragma unroll
@@ -257,16 +262,8 @@ __global__ __launch_bounds__(NT, 1) void refc1_wgrad_k(const Args g) {
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
         *(f32x4*)(e1 + (((w * 3 + t) * 2 + nt) * 16 + i16) * 16 + 4 * g4) = acc[t][nt];
-  } else {
-    // lanes with the same (lane & 3) hold the same 8 channels (8 (lane & 3) + j)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-#pragma unroll
-      for (int m = 4; m <= 32; m *= 2) db[j] += __shfl_xor(db[j], m);
-    }
-    if (lane < 4)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) eb[wave * C + 8 * lane + j] = db[j];
+    // accb rows are all equal: row 0 (lanes 0-15, register 0) = column n's sum over K
+    if (lane < 16) eb[w * 16 + lane] = accb[0][0] + accb[1][0];
   }
   __syncthreads();
   float* s = g.slab + (int64_t)blockIdx.x * SLAB_ROWS * C;
@@ -284,8 +281,8 @@ __global__ __launch_bounds__(NT, 1) void refc1_wgrad_k(const Args g) {
           v += e1[(((w * 3 + t) * 2 + nt) * 16 + col) * 16 + row];
         }
       }
-    } else if (r == 40) {
-      for (int w = 0; w < NPW; ++w) v += eb[w * C + c];
+    } else if (r == 40) {   // columns cl / cl + 8 = window positions d even / odd
+      for (int sg = 0; sg < 2; ++sg) v += eb[(sg + 2 * cgc) * 16 + cl] + eb[(sg + 2 * cgc) * 16 + cl + 8];
     }
     s[e] = v;
   }

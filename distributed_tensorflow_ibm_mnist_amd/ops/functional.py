@@ -65,7 +65,10 @@ def gemm_tile(M: int, N: int) -> Tuple[int, int]:
 
 
 # column tile of the grouped head weight gradients (gemm.hip wg_group_bn, same variable)
-GROUP_BN = 64 if os.environ.get("MNISTX_WG_GROUP_BN", "128") == "64" else 128
+GROUP_BN = 128   # gemm.hip wg_group_bn(): fc3 / fc4 outputs in ONE column tile
+# (64-row tiles: 128-row ones measured equal, 0.4576-0.4599 vs 0.4557-0.4598 ms/step on one
+# box, profiles/r4/lenet_head/group_bm_ab.txt)
+GROUP_BM = 64
 SLAB_CAP = 16 << 20   # fp32 elements of split-K partials (64 MB)
 
 
@@ -75,7 +78,7 @@ def pick_splits(M: int, N: int, K: int, target: Optional[int] = None, min_k: int
     workgroups), but keep every split >= min_k reduction elements and the fp32
     slab under SLAB_CAP.  ``grouped``: one problem of a dense_wgrad_group launch
     (64x64 tiles)."""
-    bm, bn = (64, GROUP_BN) if grouped else gemm_tile(M, N)
+    bm, bn = (GROUP_BM, GROUP_BN) if grouped else gemm_tile(M, N)
     tiles = math.ceil(M / bm) * math.ceil(N / bn)
     if target is None:
         if dense and (bm, bn) == (128, 128):

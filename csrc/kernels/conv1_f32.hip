@@ -33,6 +33,17 @@ constexpr int TR = 34, TC = 32;               // padded tile rows (2 + 28 + 2, +
 constexpr int TSZ = TR * TC + 8;              // one shifted copy (+ over-read slack)
 constexpr int NT1 = 256;
 
+// The weight-gradient kernels read the tile one float per lane (16 taps x 2 pixels per 32-lane
+// half): with 32-float rows the 5 kernel rows of a tap column share a bank (4-way / 2-way
+// ds_read_b32 conflicts); 40-float rows put them 8 banks apart (conflict-free).
+constexpr int TCW = 40, TSZW = TR * TCW + 8;
+DEV void stage_image_w(float* tile, const float* __restrict__ x, int img, int tid) {
+  for (int e = tid; e < IPIX; e += NT1) {
+    const int y = e / IW, xx = e - y * IW;
+    tile[(y + 2) * TCW + xx + 2] = x[(int64_t)img * IPIX + e];
+  }
+}
+
 // copy s holds T[j + s]; a 4-float run at tile offset a is ONE aligned b128 of copy a & 3
 DEV const float* run4(const float* tile, int a) { return tile + (a & 3) * TSZ + (a & ~3); }
 
@@ -112,18 +123,18 @@ __global__ __launch_bounds__(NT1) void conv1_f32_fwd_k(const float* __restrict__
 constexpr int WROWS = KS * KS + 1;
 __global__ __launch_bounds__(NT1) void conv1_f32_wgrad_k(const float* __restrict__ x, const float* __restrict__ dy,
                                                          int B, float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) float tile[4 * TSZ];
+  __shared__ __attribute__((aligned(16))) float tile[TSZW];
   __shared__ float red[NT1 / 64][2][2][64][4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
-  for (int e = tid; e < 4 * TSZ; e += NT1) tile[e] = 0.f;
+  for (int e = tid; e < TSZW; e += NT1) tile[e] = 0.f;
   // A rows of this lane: tap m = 16 mf + i -> tile offset of its (kh, kw), or the bias / zero rows
   int toff[2];
   float aconst[2];
 #pragma unroll
   for (int mf = 0; mf < 2; ++mf) {
     const int m = 16 * mf + i;
-    toff[mf] = m < KS * KS ? (m / KS) * TC + (m % KS) : -1;
+    toff[mf] = m < KS * KS ? (m / KS) * TCW + (m % KS) : -1;
     aconst[mf] = m == KS * KS ? 1.f : 0.f;
   }
   f32x4 acc[2][2];
@@ -133,7 +144,7 @@ __global__ __launch_bounds__(NT1) void conv1_f32_wgrad_k(const float* __restrict
     for (int nf = 0; nf < 2; ++nf) acc[mf][nf] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int img = blockIdx.x; img < B; img += gridDim.x) {
     __syncthreads();
-    stage_image(tile, x, img, tid);
+    stage_image_w(tile, x, img, tid);
     __syncthreads();
     const float* dyi = dy + (int64_t)img * IPIX * COUT;
     // k-step q = (row, 4-pixel column block): pixels (row, 4c + g); 196 per image over 4 waves
@@ -142,7 +153,7 @@ __global__ __launch_bounds__(NT1) void conv1_f32_wgrad_k(const float* __restrict
       const int row = q / (IW / 4), c4 = q - row * (IW / 4);
       const int p = row * IW + 4 * c4 + g;
       const float b0 = dyi[p * COUT + i], b1 = dyi[p * COUT + 16 + i];
-      const int base = row * TC + 4 * c4 + g;     // tile offset of the pixel's tap (0, 0)
+      const int base = row * TCW + 4 * c4 + g;     // tile offset of the pixel's tap (0, 0)
 #pragma unroll
       for (int mf = 0; mf < 2; ++mf) {
         const float av = toff[mf] >= 0 ? tile[base + toff[mf]] : aconst[mf];
@@ -274,17 +285,17 @@ __global__ __launch_bounds__(NT1) void conv1_f32_wgrad_unpool_k(const float* __r
                                                                 const float* __restrict__ dp,
                                                                 const uint8_t* __restrict__ codes, int B,
                                                                 float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) float tile[4 * TSZ];
+  __shared__ __attribute__((aligned(16))) float tile[TSZW];
   __shared__ float red[NT1 / 64][2][2][64][4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
-  for (int e = tid; e < 4 * TSZ; e += NT1) tile[e] = 0.f;
+  for (int e = tid; e < TSZW; e += NT1) tile[e] = 0.f;
   int toff[2];
   float aconst[2];
 #pragma unroll
   for (int mf = 0; mf < 2; ++mf) {
     const int m = 16 * mf + i;
-    toff[mf] = m < KS * KS ? (m / KS) * TC + (m % KS) : -1;
+    toff[mf] = m < KS * KS ? (m / KS) * TCW + (m % KS) : -1;
     aconst[mf] = m == KS * KS ? 1.f : 0.f;
   }
   f32x4 acc[2][2];
@@ -294,7 +305,7 @@ __global__ __launch_bounds__(NT1) void conv1_f32_wgrad_unpool_k(const float* __r
     for (int nf = 0; nf < 2; ++nf) acc[mf][nf] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int img = blockIdx.x; img < B; img += gridDim.x) {
     __syncthreads();
-    stage_image(tile, x, img, tid);
+    stage_image_w(tile, x, img, tid);
     __syncthreads();
     const float* dpi = dp + (int64_t)img * (PH * PW) * COUT;
     const uint8_t* cdi = codes + (int64_t)img * (PH * PW) * COUT;
@@ -307,7 +318,7 @@ __global__ __launch_bounds__(NT1) void conv1_f32_wgrad_unpool_k(const float* __r
       const float d0 = dpi[pp * COUT + i], d1 = dpi[pp * COUT + 16 + i];
       const uint32_t k0 = cdi[pp * COUT + i], k1 = cdi[pp * COUT + 16 + i];
       const float b0 = k0 == pos ? d0 : 0.f, b1 = k1 == pos ? d1 : 0.f;
-      const int base = row * TC + col;
+      const int base = row * TCW + col;
 #pragma unroll
       for (int mf = 0; mf < 2; ++mf) {
         const float av = toff[mf] >= 0 ? tile[base + toff[mf]] : aconst[mf];
@@ -356,20 +367,20 @@ __global__ __launch_bounds__(NT1) void conv1_f32_wgrad_lrn_k(const float* __rest
                                                              const float* __restrict__ p1,
                                                              const uint8_t* __restrict__ codes, int B, float lbias,
                                                              float lalpha, float lbeta, float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) float tile[4 * TSZ];
+  __shared__ __attribute__((aligned(16))) float tile[TSZW];
   __shared__ __attribute__((aligned(16))) float dps[NPP * COUT];     // dL/d pool1 of the image
   __shared__ __attribute__((aligned(16))) uint32_t cds[LT];          // its codes, 4 per word
   static_assert(sizeof(float) * NPP * COUT >= sizeof(float) * (NT1 / 64) * 2 * 2 * 64 * 4, "red aliases dps");
   float(*red)[2][2][64][4] = (float(*)[2][2][64][4])dps;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
-  for (int e = tid; e < 4 * TSZ; e += NT1) tile[e] = 0.f;
+  for (int e = tid; e < TSZW; e += NT1) tile[e] = 0.f;
   int toff[2];
   float aconst[2];
 #pragma unroll
   for (int mf = 0; mf < 2; ++mf) {
     const int m = 16 * mf + i;
-    toff[mf] = m < KS * KS ? (m / KS) * TC + (m % KS) : -1;
+    toff[mf] = m < KS * KS ? (m / KS) * TCW + (m % KS) : -1;
     aconst[mf] = m == KS * KS ? 1.f : 0.f;
   }
   f32x4 acc[2][2];
@@ -410,10 +421,8 @@ __global__ __launch_bounds__(NT1) void conv1_f32_wgrad_lrn_k(const float* __rest
     for (int u = 0; u < XR; ++u) {
       const int e = tid + u * NT1;
       if (e < IPIX) {
-        const int y = e / IW, xx = e - y * IW, a = (y + 2) * TC + xx + 2;
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-          if (a - s >= 0) tile[s * TSZ + a - s] = xv[u];
+        const int y = e / IW, xx = e - y * IW;
+        tile[(y + 2) * TCW + xx + 2] = xv[u];
       }
     }
 #pragma unroll
@@ -437,7 +446,7 @@ __global__ __launch_bounds__(NT1) void conv1_f32_wgrad_lrn_k(const float* __rest
       const float d0 = dps[pp * COUT + i], d1 = dps[pp * COUT + 16 + i];
       const uint32_t k0 = cdb[pp * COUT + i], k1 = cdb[pp * COUT + 16 + i];
       const float b0 = k0 == pos ? d0 : 0.f, b1 = k1 == pos ? d1 : 0.f;
-      const int base = row * TC + col;
+      const int base = row * TCW + col;
 #pragma unroll
       for (int mf = 0; mf < 2; ++mf) {
         const float av = toff[mf] >= 0 ? tile[base + toff[mf]] : aconst[mf];

@@ -73,7 +73,26 @@ def main():
         torch.cuda.synchronize()
         cold.append(e0.elapsed_time(e1) * 1e3)
     fused_cold = sorted(cold[2:])[len(cold[2:]) // 2]
-    del junk
+
+    # the step's order: the band forward (writes pool1 / codes) right before, then ~150 MB of
+    # other traffic (the head / its weight gradients) before the backward
+    def seq_time(pre):
+        ts = []
+        for _ in range(12):
+            pre()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            K.lenet_bwd(ds, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        return round(sorted(ts[2:])[len(ts[2:]) // 2], 1)
+    band_call = lambda: K.lenet_band_fwd(ds, w1, b1, 6, w2, b2, B, P2, A2, p1=P1, arg1=A1, idx=idx)
+    traffic = junk[: 38 * 1024 * 1024]
+    after_band = seq_time(band_call)
+    after_band_traffic = seq_time(lambda: (band_call(), traffic.fill_(2.0)))
+    after_traffic = seq_time(lambda: traffic.fill_(3.0))
+    del junk, traffic
     # the band forward (conv1 + pool1 + conv2 + pool2, pool1 / codes copied out) on the same box
     band = timeit(lambda: K.lenet_band_fwd(ds, w1, b1, 6, w2, b2, B, P2, A2, p1=P1, arg1=A1, idx=idx))
     # the input read as uint8 (half the bytes of the bf16 copy; normalised while staging)
@@ -109,7 +128,8 @@ def main():
     torch.cuda.synchronize()
     pr = prof.tolist()
     tot = max(1, sum(pr))
-    print(json.dumps({"B": B, "grid": grid, "fused_us": round(fused, 1), "fused_cold_us": round(fused_cold, 1), "band_fwd_us": round(band, 1), "fused_u8_us": round(fused_u8, 1), "fused_us_by_batch": scaling, "prof_us_by_skip": skip_us,
+    print(json.dumps({"B": B, "grid": grid, "fused_us": round(fused, 1), "fused_cold_us": round(fused_cold, 1), "after_band_us": after_band,
+                      "after_band_150MB_us": after_band_traffic, "after_150MB_us": after_traffic, "band_fwd_us": round(band, 1), "fused_u8_us": round(fused_u8, 1), "fused_us_by_batch": scaling, "prof_us_by_skip": skip_us,
                       "split_us": {"c2_dgrad": round(dgr, 1), "c2_wgrad": round(w2g, 1), "c1_wgrad": round(w1g, 1),
                                    "sum": round(dgr + w2g + w1g, 1)},
                       "phase_share": {k: round(v / tot, 3) for k, v in zip(PHASES, pr)}}), flush=True)

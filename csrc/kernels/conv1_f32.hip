@@ -7,12 +7,10 @@
 // tile is half empty at Cout 32.  Both are small problems (25 MACs per output) bound
 // by HBM at the roofline (the 1.64 GB conv output / its gradient), so these kernels
 // only have to get the operand plumbing out of the way:
-//   * forward: the image is staged in LDS once per image as a zero-haloed 32x32 tile,
-//     kept 4x shifted by 0..3 floats so every run of 4 consecutive taps of a kernel
-//     row is ONE aligned ds_read_b128; K = (kh 0..5, kw 0..7) with zero weights in
-//     the padding, A = the filter (held in registers for the whole launch), B = 16
-//     output pixels of one row; D lane (i, g) = channels 4g..4g+3 of pixel i -> one
-//     16-byte store with bias + ReLU;
+//   * forward: the image is staged in LDS once per image as a zero-haloed tile; K = the
+//     25 taps in order (7 MFMAs per fragment, Taps7), A = the filter (held in registers for
+//     the whole launch), B = 16 output pixels of one row, one float per lane; D lane (i, g)
+//     = channels 4g..4g+3 of pixel i -> one 16-byte store with bias + ReLU;
 //   * weight gradient: M = 32 rows = 25 taps + the bias row (A = 1) + zero rows, N =
 //     32 channels, K = pixels, 4 consecutive pixels of a row per k-step; the patch
 //     operand is a 4-byte LDS read of the staged tile, dY a coalesced 64-byte global
@@ -29,8 +27,7 @@ namespace mnistx {
 namespace {
 
 constexpr int IH = 28, IW = 28, IPIX = IH * IW, COUT = 32, KS = 5;
-constexpr int TR = 34, TC = 32;               // padded tile rows (2 + 28 + 2, + 2 for kh 5 over-read) x columns
-constexpr int TSZ = TR * TC + 8;              // one shifted copy (+ over-read slack)
+constexpr int TR = 34;                        // padded tile rows (2 + 28 + 2, + 2 slack)
 constexpr int NT1 = 256;
 
 // The weight-gradient kernels read the tile one float per lane (16 taps x 2 pixels per 32-lane
@@ -44,40 +41,54 @@ DEV void stage_image_w(float* tile, const float* __restrict__ x, int img, int ti
   }
 }
 
-// copy s holds T[j + s]; a 4-float run at tile offset a is ONE aligned b128 of copy a & 3
-DEV const float* run4(const float* tile, int a) { return tile + (a & 3) * TSZ + (a & ~3); }
-
-DEV void stage_image(float* tile, const float* __restrict__ x, int img, int tid) {
-  // interior (y, x) -> tile (y + 2, x + 2) of every copy s at offset - s
+// Forward: K = the 25 taps in order, 4 per v_mfma_f32_16x16x4_f32 (7 MFMAs per output row
+// fragment and channel half, 3 zero slots), each lane reading one float of the tile (its tap of
+// its pixel).  The former (kh 0..5) x (kw 0..7) K layout read 4-float runs but spent 12 MFMAs
+// per fragment (48 slots for 25 taps).  Row stride 52 floats: a 32-lane half reads two taps of
+// 16 consecutive pixels, one row apart at a kernel-row wrap (offset 52 - 4 = 48 = 16 mod 32
+// banks), so the two 16-float runs always sit in disjoint banks.
+constexpr int TCF = 52, TSZF = TR * TCF;
+DEV void stage_image_f(float* tile, const float* __restrict__ x, int img, int tid) {
   for (int e = tid; e < IPIX; e += NT1) {
     const int y = e / IW, xx = e - y * IW;
-    const float v = x[(int64_t)img * IPIX + e];
-    const int a = (y + 2) * TC + xx + 2;
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-      if (a - s >= 0) tile[s * TSZ + a - s] = v;
+    tile[(y + 2) * TCF + xx + 2] = x[(int64_t)img * IPIX + e];
   }
 }
+// filter slots of this lane (channel 16 nf + i, k-group g): tap t = 4 j + g
+struct Taps7 {
+  float a[7][2];
+  int off[7];
+  DEV void init(const float* __restrict__ w, int i, int g) {
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const int t = 4 * j + g;
+      off[j] = t < KS * KS ? (t / KS) * TCF + (t % KS) : 0;
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) a[j][nf] = t < KS * KS ? w[t * COUT + 16 * nf + i] : 0.f;
+    }
+  }
+  // acc[nf] += conv of output row `row`, columns x0 + (0..15): D lane (i, g) = channels
+  // 16 nf + 4 g .. + 3 of pixel x0 + i
+  DEV void row(const float* tile, int row, int x0, int i, f32x4 (&acc)[2]) const {
+    const float* b = tile + row * TCF + x0 + i;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const float v = b[off[j]];
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) acc[nf] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][nf], v, acc[nf], 0, 0, 0);
+    }
+  }
+};
 
 __global__ __launch_bounds__(NT1) void conv1_f32_fwd_k(const float* __restrict__ x, const float* __restrict__ w,
                                                        const float* __restrict__ bias, int relu, int B,
                                                        float* __restrict__ y) {
-  __shared__ __attribute__((aligned(16))) float tile[4 * TSZ];
+  __shared__ __attribute__((aligned(16))) float tile[TSZF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
-  for (int e = tid; e < 4 * TSZ; e += NT1) tile[e] = 0.f;
-  // A = filter: MFMA (b, s) of channel fragment nf, lane (co = 16 nf + i, k-group g):
-  // k = 16 b + 4 g + s -> kh = 2b + g/2, kw = 4(g&1) + s (zero outside the 5x5)
-  float a[3][4][2];
-#pragma unroll
-  for (int b = 0; b < 3; ++b)
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int nf = 0; nf < 2; ++nf) {
-        const int kh = 2 * b + (g >> 1), kw = 4 * (g & 1) + s;
-        a[b][s][nf] = (kh < KS && kw < KS) ? w[(kh * KS + kw) * COUT + 16 * nf + i] : 0.f;
-      }
+  for (int e = tid; e < TSZF; e += NT1) tile[e] = 0.f;
+  Taps7 tp;   // A = filter, tap-major K
+  tp.init(w, i, g);
   float bs[2][4];
 #pragma unroll
   for (int nf = 0; nf < 2; ++nf)
@@ -85,22 +96,13 @@ __global__ __launch_bounds__(NT1) void conv1_f32_fwd_k(const float* __restrict__
     for (int r = 0; r < 4; ++r) bs[nf][r] = bias ? bias[16 * nf + 4 * g + r] : 0.f;
   for (int img = blockIdx.x; img < B; img += gridDim.x) {
     __syncthreads();
-    stage_image(tile, x, img, tid);
+    stage_image_f(tile, x, img, tid);
     __syncthreads();
     // units (row, 16-column segment): 28 x 2, dealt over the 4 waves
     for (int u = wave; u < 2 * IH; u += NT1 / 64) {
       const int row = u >> 1, x0 = 16 * (u & 1);
       f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-      for (int b = 0; b < 3; ++b) {
-        const int kh = 2 * b + (g >> 1);
-        const f32x4 v = *(const f32x4*)run4(tile, (row + kh) * TC + x0 + i + 4 * (g & 1));
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int nf = 0; nf < 2; ++nf)
-            acc[nf] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[b][s][nf], v[s], acc[nf], 0, 0, 0);
-      }
+      tp.row(tile, row, x0, i, acc);
       const int xx = x0 + i;
       if (xx < IW) {
         const int64_t px = (int64_t)img * IPIX + row * IW + xx;
@@ -201,20 +203,12 @@ constexpr int PH = IH / 2, PW = IW / 2;
 __global__ __launch_bounds__(NT1) void conv1_f32_fwd_pool_k(const float* __restrict__ x, const float* __restrict__ w,
                                                             const float* __restrict__ bias, int B,
                                                             float* __restrict__ y, uint32_t* __restrict__ arg) {
-  __shared__ __attribute__((aligned(16))) float tile[4 * TSZ];
+  __shared__ __attribute__((aligned(16))) float tile[TSZF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
-  for (int e = tid; e < 4 * TSZ; e += NT1) tile[e] = 0.f;
-  float a[3][4][2];
-#pragma unroll
-  for (int b = 0; b < 3; ++b)
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int nf = 0; nf < 2; ++nf) {
-        const int kh = 2 * b + (g >> 1), kw = 4 * (g & 1) + s;
-        a[b][s][nf] = (kh < KS && kw < KS) ? w[(kh * KS + kw) * COUT + 16 * nf + i] : 0.f;
-      }
+  for (int e = tid; e < TSZF; e += NT1) tile[e] = 0.f;
+  Taps7 tp;   // A = filter, tap-major K
+  tp.init(w, i, g);
   float bs[2][4];
 #pragma unroll
   for (int nf = 0; nf < 2; ++nf)
@@ -223,7 +217,7 @@ __global__ __launch_bounds__(NT1) void conv1_f32_fwd_pool_k(const float* __restr
   const int cp = i & 1;    // this lane's column parity: window positions cp (row 0) and 2 + cp (row 1)
   for (int img = blockIdx.x; img < B; img += gridDim.x) {
     __syncthreads();
-    stage_image(tile, x, img, tid);
+    stage_image_f(tile, x, img, tid);
     __syncthreads();
     // units (row pair, 16-column segment): 14 x 2, dealt over the 4 waves
     for (int u = wave; u < 2 * PH; u += NT1 / 64) {
@@ -232,17 +226,7 @@ __global__ __launch_bounds__(NT1) void conv1_f32_fwd_pool_k(const float* __restr
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         acc[h][0] = acc[h][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int row = 2 * rp + h;
-#pragma unroll
-        for (int b = 0; b < 3; ++b) {
-          const int kh = 2 * b + (g >> 1);
-          const f32x4 v = *(const f32x4*)run4(tile, (row + kh) * TC + x0 + i + 4 * (g & 1));
-#pragma unroll
-          for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int nf = 0; nf < 2; ++nf)
-              acc[h][nf] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[b][s][nf], v[s], acc[h][nf], 0, 0, 0);
-        }
+        tp.row(tile, 2 * rp + h, x0, i, acc[h]);
       }
       // bias + ReLU, then the window max in position order 0 (r0 c0), 1 (r0 c1), 2 (r1 c0), 3 (r1 c1)
       f32x4 best[2];

@@ -401,8 +401,9 @@ __global__ __launch_bounds__(256) void lrn_f32_bwd_k(const float* __restrict__ x
     if (ok)
       for (int j = max(0, c - r); j <= min(C - 1, c + r); ++j) s = fmaf(xs[pl * C + j], xs[pl * C + j], s);
     const float n = fmaf(alpha, s, bias);
-    const float nb = pow_neg(n, beta);
-    ts[t] = g * xv * nb / n;
+    float nb, nb1;
+    pow_neg2(n, beta, nb, nb1);
+    ts[t] = g * xv * nb1;
     __syncthreads();
     if (ok) {
       float u = 0.f;
@@ -621,9 +622,10 @@ __global__ __launch_bounds__(256) void lrn_pool_f32_bwd_k(const float* __restric
       f32x4 nb, tv;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float nn = fmaf(alpha, s[j], bias);
-        nb[j] = pow_neg(nn, beta);
-        tv[j] = g[j] * v[j] * nb[j] / nn;
+        float p0, p1;
+        pow_neg2(fmaf(alpha, s[j], bias), beta, p0, p1);
+        nb[j] = p0;
+        tv[j] = g[j] * v[j] * p1;
       }
       const f32x4 u = win4(tv, threadIdx.x % G, G, r);
       f32x4 o;

@@ -10,6 +10,13 @@ namespace mnistx {
 namespace {
 
 DEV float pow_neg(float n, float b) { return exp2f(-b * log2f(n)); }   // n^-b, n >= bias > 0
+// n^-b (bitwise pow_neg) and n^-(b+1) from one log2: the backward's g x n^-b / n without the
+// IEEE division (~10 VALU per channel; one more v_exp_f32 instead)
+DEV void pow_neg2(float n, float b, float& p, float& p1) {
+  const float lg = log2f(n);
+  p = exp2f(-b * lg);
+  p1 = exp2f(-(b + 1.f) * lg);
+}
 
 DEV float f32_from_left(float v) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, true)); }
 DEV float f32_from_right(float v) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x101, 0xf, 0xf, true)); }
@@ -38,13 +45,17 @@ DEV f32x4 win4(const f32x4& v, int c4, int G, int r) {
 // every lane of the wave must call it (DPP exchanges)
 DEV f32x4 lrn_f32_bwd4(const f32x4& v, const f32x4& g, int c4, int G, int r, float bias, float alpha, float beta,
                        int relu_mask) {
+  // no FMA contraction: every kernel that inlines this rounds alike (the fused norm1 fold in
+  // conv1_f32.hip and lrn_f32_bwd_v4_k give bitwise-equal gradients, tests/test_f32_gpu.py)
+#pragma clang fp contract(off)
   const f32x4 s = win4(v * v, c4, G, r);
   f32x4 nb, tt;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const float n = fmaf(alpha, s[j], bias);
-    nb[j] = pow_neg(n, beta);
-    tt[j] = g[j] * v[j] * nb[j] / n;
+    float p0, p1;
+    pow_neg2(fmaf(alpha, s[j], bias), beta, p0, p1);
+    nb[j] = p0;
+    tt[j] = g[j] * v[j] * p1;
   }
   const f32x4 u = win4(tt, c4, G, r);
   f32x4 o;

@@ -266,7 +266,10 @@ template <int S>
 DEV bf16x8 frag_kc(const bf16_t* img, int r0, int kb, int lane) {
   const int i = lane & 15, g = lane >> 4;
   (void)kb;
-  return __builtin_bit_cast(bf16x8, *(const u32x4*)(img + (r0 + i) * S + 8 * g));
+  // 48-element rows: the 16-byte blocks of odd rows are stored swapped in pairs (kc_store;
+  // r0 is a multiple of 16, so the row parity is i's)
+  const int gs = S == 48 ? (g ^ (i & 1)) : g;
+  return __builtin_bit_cast(bf16x8, *(const u32x4*)(img + (r0 + i) * S + 8 * gs));
 }
 
 // MN-contiguous image [BK][S]: transposed read of 4-row x 16-col blocks.
@@ -354,11 +357,19 @@ DEV void gemm_body(const LA& la, const LB& lb, const GemmEpi& ep, int M, int N, 
     }
   };
   // K-contiguous: the 8 k of a vector land in two 4-column runs of the permuted order
+  // With 48-element rows the 4 rows x 4 vectors of a 16-lane store group hit every bank twice
+  // (2-way; the staging stores were most of the 25-33 % LDS bank-conflict cycles of the
+  // large dense GEMMs, profiles/r4/refcnn/pmc_refcnn_b16384_before.md): odd rows swap their
+  // 16-byte blocks in pairs, which makes the stores conflict-free and keeps the fragment
+  // reads (frag_kc) conflict-free (bench/lds_gemm_kc.py).
   auto kc_store = [&](bf16_t* img, int S, int v, const u32x4& x) {
     const int r = v / (BK / 8), vq = v % (BK / 8);
     bf16_t* row = img + r * S;
-    *(u32x2*)(row + kc_col(8 * vq)) = u32x2{x[0], x[1]};
-    *(u32x2*)(row + kc_col(8 * vq + 4)) = u32x2{x[2], x[3]};
+    // the stores split into two ds_write_b64 (a ds_write2_b64 needs one offset pair for all
+    // lanes); swapping the data instead keeps the pair but measured slower (the selects)
+    const int sw = S == 48 ? ((r & 1) << 3) : 0;
+    *(u32x2*)(row + (kc_col(8 * vq) ^ sw)) = u32x2{x[0], x[1]};
+    *(u32x2*)(row + (kc_col(8 * vq + 4) ^ sw)) = u32x2{x[2], x[3]};
   };
   // fix(): loader post-processing of a waited-for vector (the bias ones column)
   auto sstore = [&](int slot, int buf, int k0) {

@@ -11,3 +11,11 @@ def test_conv_halo_swizzle_conflict_free():
     # conv_halo.hip fwd/dgrad A and B fragment reads: 4 LDS cycles per ds_read_b128 = no conflict
     assert lds_sim.check_halo(4) == 4
     assert lds_sim.check_halo(8) == 4
+
+
+def test_gemm_kc_swap_conflict_free():
+    import lds_gemm_kc as m
+    # gemm.hip K-contiguous images at 48-element rows: odd-row block swap -> 1 cycle per group
+    assert m.store(48, True, False) == 1 and m.store(48, True, True) == 1
+    assert all(m.read(48, True, r0) == 1 for r0 in (0, 16, 32, 48))
+    assert m.store(48, False, False) == 2

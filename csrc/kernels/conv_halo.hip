@@ -49,6 +49,20 @@ DEV int swz(int r, int c) {
   else return c ^ (r & 6);
 }
 
+// Lane i <- lane i + N of its 16-lane row, zero past the row's end (DPP row_shl; the
+// zero is exactly the tile's right halo: see ROWS below)
+template <int N>
+DEV uint32_t row_shl(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 + N, 0xf, 0xf, true);
+}
+DEV u32x4 row_shl4(const u32x4& v, int n) {
+  u32x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    o[j] = n == 1 ? row_shl<1>(v[j]) : n == 2 ? row_shl<2>(v[j]) : n == 3 ? row_shl<3>(v[j]) : row_shl<4>(v[j]);
+  return o;
+}
+
 // MODE 0 = forward: out[p][n] = relu(sum_{tap,ci} x[p+tap][ci] W[tap][ci][n] + b[n])
 // MODE 1 = data gradient: out[p][n] = mask * sum_{tap,ci} dy[p+tap][ci] W[24-tap][n][ci]
 //   (W is the conv's [kh][kw][cin][cout] filter; here ci runs over the conv's
@@ -56,7 +70,15 @@ DEV int swz(int r, int c) {
 // LRNX: x is the input of an LRN (radius 4) whose output is the convolution's input;
 // the LRN is applied to each staged 16-byte vector (the CH lanes of a pixel are
 // adjacent), bitwise lrn_fwd_k, so the LRN output never exists in HBM.
-template <int CIN, int CW, int NW, int MODE, int FR, int IMGS, bool LRNX = false>
+// ROWS: a wave's FR output rows (one image, FR | 14) read each of the FR + 4 tile rows
+// they touch ONCE per channel block (one ds_read_b128 at columns 0..15) instead of once
+// per (row, tap): tap column kw is the fragment shifted by kw lanes (DPP row_shl), and
+// the lanes it shifts in past column 15 are the zero halo columns 16..19 the tile holds
+// there anyway (only output columns i < 14 are kept, i + kw <= 17).  Tile-row reuse
+// across kh comes from fragment h + kh.  The A-side LDS reads drop from 25 FR to FR + 4
+// per channel block: the B (filter) reads, one per (tap, nf) shared by the FR rows, are
+// then most of the LDS traffic.
+template <int CIN, int CW, int NW, int MODE, int FR, int IMGS, bool LRNX = false, bool ROWS = false>
 __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                         int wcin, int wcout, const float* __restrict__ bias, int bias_n,
                                                         int relu, const bf16_t* __restrict__ mask, int ldm, int B,
@@ -158,6 +180,41 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict
       for (int h = 0; h < FR; ++h)
 #pragma unroll
         for (int nf = 0; nf < NF; ++nf) acc[h][nf] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (ROWS) {
+        static_assert(MFR % FR == 0, "ROWS: row groups inside one image");
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          const int c = 4 * kc + g;
+          u32x4 R[FR + 4];
+#pragma unroll
+          for (int t = 0; t < FR + 4; ++t) {
+            const int P = P0[0] + t * WR;
+            R[t] = *(const u32x4*)(xs + P * CIN + (swz<CH>(P, c) << 3));
+          }
+#pragma unroll
+          for (int kw = 0; kw < KS; ++kw) {
+            u32x4 Sh[FR + 4];
+#pragma unroll
+            for (int t = 0; t < FR + 4; ++t) Sh[t] = kw == 0 ? R[t] : row_shl4(R[t], kw);
+#pragma unroll
+            for (int kh = 0; kh < KS; ++kh) {
+              const int t = kh * KS + kw;
+              bf16x8 b[NF];
+#pragma unroll
+              for (int nf = 0; nf < NF; ++nf) {
+                const int r = t * CW + nf * 16 + i;
+                b[nf] = __builtin_bit_cast(bf16x8, *(const u32x4*)(ws + r * CIN + (swz<CH>(r, c) << 3)));
+              }
+#pragma unroll
+              for (int h = 0; h < FR; ++h)
+#pragma unroll
+                for (int nf = 0; nf < NF; ++nf)
+                  acc[h][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nf], __builtin_bit_cast(bf16x8, Sh[h + kh]),
+                                                                       acc[h][nf], 0, 0, 0);
+            }
+          }
+        }
+      } else
       for (int kh = 0; kh < KS; ++kh) {
 #pragma unroll
         for (int kw = 0; kw < KS; ++kw) {
@@ -369,12 +426,12 @@ int halo_wgrad_resident() {
   return per;
 }
 
-template <int CIN, int CW, int NW, int MODE, int FR, int IMGS, bool LRNX = false>
+template <int CIN, int CW, int NW, int MODE, int FR, int IMGS, bool LRNX = false, bool ROWS = false>
 int halo_grid(int B) {
   static int per = -1;
   if (per < 0) {
     int dev = 0, cus = 0, pc = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, conv5_halo_k<CIN, CW, NW, MODE, FR, IMGS, LRNX>, 64 * NW, 0) ==
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, conv5_halo_k<CIN, CW, NW, MODE, FR, IMGS, LRNX, ROWS>, 64 * NW, 0) ==
             hipSuccess &&
         hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && pc > 0)
@@ -386,13 +443,13 @@ int halo_grid(int B) {
   return cap_grid(groups < per ? groups : per);
 }
 
-template <int CIN, int CW, int NW, int MODE, int FR, int IMGS = 1, bool LRNX = false>
+template <int CIN, int CW, int NW, int MODE, int FR, int IMGS = 1, bool LRNX = false, bool ROWS = false>
 hipError_t run_halo(const bf16_t* x, const bf16_t* w, int wcin, int wcout, const float* bias, int bias_n, int relu,
                     const bf16_t* mask, int ldm, int B, bf16_t* out, int ncols, int ldo, hipStream_t st,
                     LrnParams lrn = LrnParams{0.f, 0.f, 0.f, 0}) {
   if (B <= 0) return hipSuccess;
-  dim3 grid(halo_grid<CIN, CW, NW, MODE, FR, IMGS, LRNX>(B), ncols / CW);
-  hipLaunchKernelGGL((conv5_halo_k<CIN, CW, NW, MODE, FR, IMGS, LRNX>), grid, dim3(64 * NW), 0, st, x, w, wcin, wcout, bias,
+  dim3 grid(halo_grid<CIN, CW, NW, MODE, FR, IMGS, LRNX, ROWS>(B), ncols / CW);
+  hipLaunchKernelGGL((conv5_halo_k<CIN, CW, NW, MODE, FR, IMGS, LRNX, ROWS>), grid, dim3(64 * NW), 0, st, x, w, wcin, wcout, bias,
                      bias_n, relu, mask, ldm, B, out, ldo, lrn);
   return hipGetLastError();
 }
@@ -424,8 +481,8 @@ static int halo_variant(const char* name, int dflt) {
 hipError_t conv5_halo_fwd(const bf16_t* x, const bf16_t* w, int Nb, int C, int Cout, const float* bias, int bias_n,
                           int relu, bf16_t* out, hipStream_t st, LrnParams lrn) {
   if (lrn.on)   // norm1 folded into the staging: the default launch shape only
-    return run_halo<32, 32, 8, 0, 2, 1, true>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st,
-                                               lrn);
+    return run_halo<32, 32, 8, 0, 7, 4, true, true>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout,
+                                                     st, lrn);
   const int v = halo_variant("MNISTX_HALO_FWD", 0);
   switch (v) {
     case 1:   // whole Cout per block (NF = 4): 125 KB LDS, 1 block / CU
@@ -440,9 +497,15 @@ hipError_t conv5_halo_fwd(const bf16_t* x, const bf16_t* w, int Nb, int C, int C
     case 5:   // whole Cout, 8 waves x 2 row fragments
       if (Cout == 64) return run_halo<32, 64, 8, 0, 2>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
       break;
+    case 6:   // ROWS: 7 waves x 2 row fragments (every wave busy)
+      return run_halo<32, 32, 7, 0, 2, 1, false, true>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
+    case 7:   // ROWS: four images, 8 waves x 7 row fragments
+      return run_halo<32, 32, 8, 0, 7, 4, false, true>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
+    case 8:   // the pre-ROWS default: 8 waves x 2 row fragments, 25 A reads per row and channel block
+      return run_halo<32, 32, 8, 0, 2>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
     default: break;
   }
-  return run_halo<32, 32, 8, 0, 2>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
+  return run_halo<32, 32, 8, 0, 7, 4, false, true>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
 }
 
 hipError_t conv5_halo_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int Cout, int Cin, const bf16_t* mask,
@@ -459,9 +522,15 @@ hipError_t conv5_halo_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int Cout,
       return run_halo<64, 16, 8, 1, 2>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
     case 5:   // 2 waves x 7 row fragments
       return run_halo<64, 32, 2, 1, 7>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
+    case 6:   // ROWS: 7 waves x 2 row fragments
+      return run_halo<64, 32, 7, 1, 2, 1, false, true>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
+    case 7:   // ROWS: half the channels, two images, 4 waves x 7 row fragments (143 KB LDS)
+      return run_halo<64, 16, 4, 1, 7, 2, false, true>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
+    case 8:   // the pre-ROWS default
+      return run_halo<64, 32, 8, 1, 2>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
     default: break;
   }
-  return run_halo<64, 32, 8, 1, 2>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
+  return run_halo<64, 32, 7, 1, 2, 1, false, true>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
 }
 
 void set_halo_variants(int fwd, int dgrad) {

@@ -501,6 +501,8 @@ hipError_t conv5_halo_fwd(const bf16_t* x, const bf16_t* w, int Nb, int C, int C
       return run_halo<32, 32, 7, 0, 2, 1, false, true>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
     case 7:   // ROWS: four images, 8 waves x 7 row fragments
       return run_halo<32, 32, 8, 0, 7, 4, false, true>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
+    case 9:   // ROWS: two images, 14 waves x 2 row fragments (one workgroup per CU)
+      return run_halo<32, 32, 14, 0, 2, 2, false, true>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
     case 8:   // the pre-ROWS default: 8 waves x 2 row fragments, 25 A reads per row and channel block
       return run_halo<32, 32, 8, 0, 2>(x, w, C, Cout, bias, bias_n, relu, nullptr, 0, Nb, out, Cout, Cout, st);
     default: break;
@@ -526,6 +528,8 @@ hipError_t conv5_halo_dgrad(const bf16_t* dy, const bf16_t* w, int Nb, int Cout,
       return run_halo<64, 32, 7, 1, 2, 1, false, true>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
     case 7:   // ROWS: half the channels, two images, 4 waves x 7 row fragments (143 KB LDS)
       return run_halo<64, 16, 4, 1, 7, 2, false, true>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
+    case 9:   // ROWS: half the channels, two images, 14 waves x 2 row fragments (143 KB LDS)
+      return run_halo<64, 16, 14, 1, 2, 2, false, true>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
     case 8:   // the pre-ROWS default
       return run_halo<64, 32, 8, 1, 2>(dy, w, Cin, Cout, nullptr, 0, 0, mask, Cin, Nb, dx, Cin, Cin, st);
     default: break;

@@ -145,7 +145,7 @@ def test_conv_fwd(dev, K, N, H, W, Ci, Co, k, pad):
 
 
 @pytest.mark.parametrize("cap", [0, 2])
-@pytest.mark.parametrize("fv,dv", [(1, 1), (2, 2), (3, 3), (4, 4), (5, 5), (6, 6), (7, 7), (8, 8)])
+@pytest.mark.parametrize("fv,dv", [(1, 1), (2, 2), (3, 3), (4, 4), (5, 5), (6, 6), (7, 7), (8, 8), (9, 9)])
 def test_conv_halo_variants(dev, K, grid_cap, fv, dv, cap):
     """Every conv_halo.hip launch variant (reference conv2 geometry; odd batch leaves a
     partial image group) against the fp32 oracle: forward + bias + ReLU, masked dgrad.

@@ -11,7 +11,9 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# MICRO_PKG_ROOT: import the package (and its built kernels) from another tree, for
+# same-box A/B runs of two builds
+sys.path.insert(0, os.environ.get("MICRO_PKG_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from distributed_tensorflow_ibm_mnist_amd.ops import functional as Fk
 from distributed_tensorflow_ibm_mnist_amd.ops._ext import kernels

@@ -175,6 +175,21 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict
         const int f = min(FR * gr + h, IMGS * MFR - 1), im = f / MFR;
         P0[h] = im * (XE / CIN) + (f - im * MFR) * WR + i;
       }
+      // dgrad ReLU mask of this group's outputs, loaded before the MFMAs so its latency hides
+      // behind them (loaded in the epilogue, every wave of the block stalled on it at once)
+      u32x2 mkv[FR][NF];
+      if (MODE == 1 && mask != nullptr) {
+#pragma unroll
+        for (int h = 0; h < FR; ++h) {
+          const int f = FR * gr + h, im = f / MFR;
+          const int q = (f - im * MFR) * HW + i;
+          const bool ok = f < IMGS * MFR && i < HW && img0 + im < B;
+          const int64_t row = (int64_t)(img0 + im) * NPIX + q;
+#pragma unroll
+          for (int nf = 0; nf < NF; ++nf)
+            mkv[h][nf] = ok ? *(const u32x2*)(mask + row * ldm + n0 + nf * 16 + 4 * g) : u32x2{0u, 0u};
+        }
+      }
       f32x4 acc[FR][NF];
 #pragma unroll
       for (int h = 0; h < FR; ++h)
@@ -262,8 +277,8 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_k(const bf16_t* __restrict
               v[r] = acc[h][nf][r] + bn[r];
               if (relu) v[r] = fmaxf(v[r], 0.f);
             }
-            if (mask != nullptr) {
-              const u32x2 mk = *(const u32x2*)(mask + row * ldm + nb);
+            if (MODE == 1 && mask != nullptr) {
+              const u32x2 mk = mkv[h][nf];
 #pragma unroll
               for (int r = 0; r < 4; ++r)
                 if (!(bf2f((bf16_t)((mk[r >> 1] >> (16 * (r & 1))) & 0xffffu)) > 0.f)) v[r] = 0.f;

@@ -469,21 +469,53 @@ DEV void gemm_body(const LA& la, const LB& lb, const GemmEpi& ep, int M, int N, 
                    (ep.mask == nullptr || (ep.ldm % 8 == 0 && (uintptr_t)ep.mask % 16 == 0));
   if (vec) {
     constexpr int EP_LD = TN + 4;
+    constexpr int VI = (16 * (TN / 8) + 63) / 64;   // 8-column vectors per lane per fragment row
     static_assert((NT / 64) * 16 * EP_LD * 4 <= 2 * (A_ELEMS + B_ELEMS) * 2, "epilogue staging must fit in smem");
     float* eb = (float*)smem + wave * 16 * EP_LD;
-    __syncthreads();
+    // A lane's columns do not depend on the fragment row i: its bias values are loaded once,
+    // and the mask of fragment row i + 1 is in flight while row i is staged and stored (loaded
+    // inside the row loop, every wave stalled on each of the FM loads in turn).
+    auto vrow = [&](int v) { return v / (TN / 8); };
+    auto vcol = [&](int v) { return n0 + wn * TN + (v - vrow(v) * (TN / 8)) * 8; };
+    float bv[VI][8];
+#pragma unroll
+    for (int k = 0; k < VI; ++k) {
+      const int n = vcol(lane + 64 * k);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bv[k][e] = (ep.bias && n + e < ep.bias_n) ? ep.bias[n + e] : 0.f;
+    }
+    auto mload = [&](int i, u32x4 (&mk)[VI]) {
+#pragma unroll
+      for (int k = 0; k < VI; ++k) {
+        const int v = lane + 64 * k;
+        const int m = m0 + wm * TM + i * 16 + vrow(v), n = vcol(v);
+        const bool ok = ep.mask && v < 16 * (TN / 8) && m < M && n < N;
+        mk[k] = ok ? *(const u32x4*)(ep.mask + (int64_t)m * ep.ldm + n) : u32x4{0u, 0u, 0u, 0u};
+      }
+    };
+    u32x4 mkc[VI];
+    mload(0, mkc);
+    __syncthreads();   // the main loop's operand images are dead from here on
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
+      u32x4 mkn[VI];
+      if (i + 1 < FM) mload(i + 1, mkn);
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) eb[(4 * g + r) * EP_LD + j * 16 + li] = acc[i][j][r];
-      __syncthreads();
-      for (int v = lane; v < 16 * (TN / 8); v += 64) {
-        const int rr = v / (TN / 8), cv = (v - rr * (TN / 8)) * 8;
-        const int m = m0 + wm * TM + i * 16 + rr, n = n0 + wn * TN + cv;
-        if (m < M && n < N) {
-          f32x4 lo = *(const f32x4*)(eb + rr * EP_LD + cv), hi = *(const f32x4*)(eb + rr * EP_LD + cv + 4);
+      // eb is this wave's own: LDS accesses of one wave complete in order, so only the
+      // compiler needs fencing (no workgroup barrier)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int k = 0; k < VI; ++k) {
+        const int v = lane + 64 * k;
+        const int rr = vrow(v), cv = v - rr * (TN / 8);
+        const int m = m0 + wm * TM + i * 16 + rr, n = vcol(v);
+        if (v < 16 * (TN / 8) && m < M && n < N) {
+          f32x4 lo = *(const f32x4*)(eb + rr * EP_LD + 8 * cv), hi = *(const f32x4*)(eb + rr * EP_LD + 8 * cv + 4);
           if (ep.mode == EPI_SLAB) {
             float* o = (float*)ep.out + (int64_t)split * ep.slab_stride + (int64_t)m * ep.ldc + n;
             *(f32x4*)o = lo;
@@ -491,17 +523,15 @@ DEV void gemm_body(const LA& la, const LB& lb, const GemmEpi& ep, int M, int N, 
             continue;
           }
           float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          if (ep.bias)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) x[e] += (n + e < ep.bias_n) ? ep.bias[n + e] : 0.f;
+          for (int e = 0; e < 8; ++e) x[e] += bv[k][e];
           if (ep.relu)
 #pragma unroll
             for (int e = 0; e < 8; ++e) x[e] = fmaxf(x[e], 0.f);
           if (ep.mask) {
-            const u32x4 mk = *(const u32x4*)(ep.mask + (int64_t)m * ep.ldm + n);
 #pragma unroll
             for (int e = 0; e < 8; ++e)
-              if (!(u4_get(mk, e) > 0.f)) x[e] = 0.f;
+              if (!(u4_get(mkc[k], e) > 0.f)) x[e] = 0.f;
           }
           if (ep.mode == EPI_F32) {
             float* o = (float*)ep.out + (int64_t)m * ep.ldc + n;
@@ -513,7 +543,13 @@ DEV void gemm_body(const LA& la, const LB& lb, const GemmEpi& ep, int M, int N, 
           }
         }
       }
-      __syncthreads();
+      // the next row's staging overwrites eb: this row's reads first (same wave: in order)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (i + 1 < FM)
+#pragma unroll
+        for (int k = 0; k < VI; ++k) mkc[k] = mkn[k];
     }
     return;
   }

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Dense weight-gradient sweep: GEMM tile x split-K count for the LeNet-5 fc shapes
 at B = 65536 (wgrad GEMM + multi-tensor split-K reduce, CUDA-event timed).
-Usage: python bench/micro_wgrad.py [B] [ref]   (ref: the reference CNN's local3/local4 shapes)"""
+Usage: python bench/micro_wgrad.py [B] [ref] [TILE,TILE..]   (ref: the reference CNN's local3/local4
+shapes; the tile list restricts the sweep)"""
 import os
 import sys
 
@@ -10,7 +11,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_tensorflow_ibm_mnist_amd.ops._ext import kernels  # noqa: E402
 
-TILES = {"64x64": 7, "128x128": 4, "128x64": 2, "64x128": 3, "64x32": 6, "64x16": 5}
+TILES = {"64x64": 7, "128x128": 4, "128x64": 2, "64x128": 3, "64x32": 6, "64x16": 5, "256x128": 8}
 
 
 def main():
@@ -23,6 +24,9 @@ def main():
     if len(sys.argv) > 2 and sys.argv[2] == "ref":
         shapes = [("local3", 3136, 1024, 1024), ("local4", 1024, 192, 192)]
         splits = (1, 2, 3, 4, 6, 8, 12, 16)
+    only = sys.argv[3].split(",") if len(sys.argv) > 3 else None
+    if len(sys.argv) > 2 and sys.argv[2] == "ref":
+        shapes = shapes[:1]
     for name, din, dout, Np in shapes:
         Dp = din if name != "fc5" else 88
         x = (torch.randn(B, Dp, device=dev) * 0.5).to(torch.bfloat16)
@@ -35,6 +39,8 @@ def main():
         geo_row = lambda S: [S, M, Np, 1, Dp, din, dout, Dp]
         print(f"{name}: M={M} N={Np} K={B}", flush=True)
         for tname, code in TILES.items():
+            if only and tname not in only:
+                continue
             if Np <= 16 and tname not in ("64x16",):
                 continue
             if 16 < Np <= 32 and tname not in ("64x32",):

@@ -698,6 +698,10 @@ hipError_t launch_any(const LA& la, const LB& lb, const GemmEpi& ep, int M, int 
       return launch_cfg<256, 128, 2, 2, LA, AKC, LB, BKC, 2>(la, lb, ep, M, N, K, splits, st);
     if (c == T256x128) return launch_cfg<256, 128, 2, 2, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
   }
+  if constexpr (WG) {
+    // explicit request only (bench/micro_wgrad.py): 256 x 128 weight-gradient tiles
+    if (c == T256x128) return launch_cfg<256, 128, 2, 2, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
+  }
   switch (c) {
     case T64x16: return launch_cfg<64, 16, 4, 1, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);
     case T64x32: return launch_cfg<64, 32, 4, 1, LA, AKC, LB, BKC>(la, lb, ep, M, N, K, splits, st);

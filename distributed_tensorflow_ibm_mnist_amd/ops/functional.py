@@ -40,7 +40,10 @@ TARGET_BLOCKS_FEW_TILES = int(os.environ.get("MNISTX_WGRAD_BLOCKS", "256"))
 # ref: S=2 155.9 us, S=3 165.0, S=8 154.4, S=16 197.1 -- the fewest splits that fill
 # the GPU keep the slab smallest; round 3, whole reference-CNN step: 256 / 400 / 600 / 800
 # within noise, 2.19-2.22 ms, profiles/r3/refcnn/wgrad_blocks_big/)
-TARGET_BLOCKS_BIG_TILES = int(os.environ.get("MNISTX_WGRAD_BLOCKS_BIG", "400"))
+# Round 4 (dense-GEMM epilogue and ROWS conv in): 1000 (local3 S = 5, the SLAB_CAP limit)
+# beat 400 (S = 2) in 3 of 3 same-box pairs, 2.114-2.121 vs 2.135-2.144 ms/step
+# (profiles/r4/gemm_epi/ab_wgrad_blocks_big.txt; standalone sweep micro_wgrad_local3_tiles.txt)
+TARGET_BLOCKS_BIG_TILES = int(os.environ.get("MNISTX_WGRAD_BLOCKS_BIG", "1000"))
 
 def pad8(c: int) -> int:
     return (c + 7) // 8 * 8

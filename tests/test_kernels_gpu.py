@@ -145,17 +145,18 @@ def test_conv_fwd(dev, K, N, H, W, Ci, Co, k, pad):
 
 
 @pytest.mark.parametrize("cap", [0, 2])
-@pytest.mark.parametrize("fv,dv", [(1, 1), (2, 2), (3, 3), (4, 4), (5, 5), (6, 6), (7, 7), (8, 8), (9, 9)])
+@pytest.mark.parametrize("fv,dv", [(0, 0), (1, 1), (2, 2), (3, 3), (4, 4), (5, 5), (6, 6), (7, 7), (8, 8), (9, 9)])
 def test_conv_halo_variants(dev, K, grid_cap, fv, dv, cap):
     """Every conv_halo.hip launch variant (reference conv2 geometry; odd batch leaves a
     partial image group) against the fp32 oracle: forward + bias + ReLU, masked dgrad.
-    cap > 0: 2 persistent blocks over 11 images, so every block loops with the next
-    image prefetched (the path of the benchmark batch)."""
+    cap > 0: 2 persistent blocks over 25 images, so every block loops >= 3 times with the
+    next image group prefetched (the path of the benchmark batch; the 4-image groups of
+    the default forward: 7 groups, the last one partial)."""
     torch.manual_seed(7)
     N, H, W, Ci, Co, k, pad = 5, 14, 14, 32, 64, 5, "SAME"
     if cap:
         grid_cap(cap)
-        N = 11
+        N = 25
     x = rnd(N, H, W, Ci, dev=dev).float().requires_grad_(True)
     w = rnd(k, k, Ci, Co, dev=dev, scale=1 / math.sqrt(k * k * Ci))
     b = torch.randn(Co, device=dev)

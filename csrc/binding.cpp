@@ -1150,6 +1150,7 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("C"), py::arg("OH"), py::arg("OW"), py::arg("KH"), py::arg("KW"), py::arg("ph"), py::arg("pw"),
         py::arg("Cout"), py::arg("bias"), py::arg("bias_n"), py::arg("relu"), py::arg("lrn_r") = 0,
         py::arg("lrn_bias") = 0.0, py::arg("lrn_alpha") = 0.0, py::arg("lrn_beta") = 0.0);
+  m.def("set_f32_halo_fwd_variant", [](int64_t v) { mnistx::set_f32_halo_fwd_variant((int)v); });
   m.def("set_halo_variants", [](int64_t f, int64_t d) { mnistx::set_halo_variants((int)f, (int)d); });
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("slab"), py::arg("Nb"), py::arg("H"),

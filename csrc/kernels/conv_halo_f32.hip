@@ -26,6 +26,7 @@
 // Replaces (SURVEY.md §2.3 N1/N2, fp32 path): Conv2D / Conv2DBackpropInput of conv2
 // at mnist_input.py:161 under the reference's tf.float32.
 #include "common.h"
+#include <type_traits>
 #include "launchers.h"
 
 namespace mnistx {
@@ -44,7 +45,11 @@ DEV int swz(int r, int c) { return c ^ (r & 6); }
 // (W = [kh][kw][cin][cout]; for MODE 1, c runs over the conv's output channels, n over
 // its input channels).  CR = reduction channels (32 fwd, 64 dgrad), CW = output
 // channels per workgroup (grid.y = ncols / CW), FR = row fragments per wave.
-template <int CR, int CW, int NW, int MODE, int FR>
+// UPW > 0 (FR = 1): the block's 14 x NF (output row, 16-channel fragment) units are dealt
+// round-robin to the waves, UPW per wave at most -- with 8 waves and NF = 2 that is 4 + 3
+// units on every SIMD (waves w and w + 4 share one), where 7 two-row groups on 8 waves leave
+// one SIMD's second wave idle and the step waits for the SIMDs that ran two groups.
+template <int CR, int CW, int NW, int MODE, int FR, int UPW = 0>
 __global__ __launch_bounds__(64 * NW) void conv5_halo_f32_k(const float* __restrict__ x, const float* __restrict__ w,
                                                             int wcin, int wcout, const float* __restrict__ bias,
                                                             int relu, const float* __restrict__ mask, int ldm, int B,
@@ -57,7 +62,8 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_f32_k(const float* __restr
   constexpr int NV = NPIX * CHK;                 // 16-byte vectors per image pass
   constexpr int PER = (NV + NT - 1) / NT;
   constexpr int NGRP = (MFR + FR - 1) / FR;
-  static_assert(CR % CP == 0 && CW % 16 == 0 && NGRP <= NW, "conv5_halo_f32 geometry: one row group per wave");
+  static_assert(CR % CP == 0 && CW % 16 == 0 && (UPW > 0 || NGRP <= NW), "conv5_halo_f32 geometry: one row group per wave");
+  static_assert(UPW == 0 || (FR == 1 && UPW * NW >= MFR * NF && (UPW - 1) * NW < MFR * NF), "unit mode geometry");
   __shared__ __attribute__((aligned(16))) float xs[XE];
   __shared__ __attribute__((aligned(16))) float ws[NPASS * WE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -112,6 +118,9 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_f32_k(const float* __restr
   };
   gload(blockIdx.x, 0);
   for (int img = blockIdx.x; img < B; img += gridDim.x) {
+    f32x4 uacc[UPW > 0 ? UPW : 1];
+#pragma unroll
+    for (int j = 0; j < (UPW > 0 ? UPW : 1); ++j) uacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 acc[FR][NF];
 #pragma unroll
     for (int h = 0; h < FR; ++h)
@@ -132,7 +141,38 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_f32_k(const float* __restr
       __syncthreads();
       if (pass + 1 < NPASS) gload(img, pass + 1);   // next pass / image in flight during the MFMAs
       else gload(img + gridDim.x, 0);
-      if (busy) {
+      if constexpr (UPW > 0) {
+        // units u = wave + NW j: output row u % 14, fragment u / 14; this wave owns nmine
+        const int nmine = (MFR * NF - wave + NW - 1) / NW;
+        const float* wp = ws + pass * WE;
+        auto units = [&](auto NUc) {
+          constexpr int NU = decltype(NUc)::value;
+          for (int kh = 0; kh < KS; ++kh) {
+#pragma unroll
+            for (int kw = 0; kw < KS; ++kw) {
+              const int t = kh * KS + kw, dP = kh * WR + kw;
+#pragma unroll
+              for (int cb = 0; cb < CP / 16; ++cb) {
+                const int c = 4 * cb + g;
+                f32x4 a[NU], b[NU];
+#pragma unroll
+                for (int j = 0; j < NU; ++j) {
+                  const int u = wave + NW * j, r = t * CW + (u / MFR) * 16 + i, P = (u % MFR) * WR + i + dP;
+                  a[j] = *(const f32x4*)(wp + r * CP + swz(r, c) * 4);
+                  b[j] = *(const f32x4*)(xs + P * CP + swz(P, c) * 4);
+                }
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                  for (int j = 0; j < NU; ++j)
+                    uacc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][s], b[j][s], uacc[j], 0, 0, 0);
+              }
+            }
+          }
+        };
+        if (nmine == UPW) units(std::integral_constant<int, UPW>{});
+        else units(std::integral_constant<int, (UPW > 1 ? UPW - 1 : 1)>{});
+      } else if (busy) {
         const float* wp = ws + pass * WE;
         for (int kh = 0; kh < KS; ++kh) {
 #pragma unroll
@@ -165,7 +205,32 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_f32_k(const float* __restr
       }
     }
     // D row 4g + r = output channel n0 + nf*16 + 4g + r, column i = output column
-    if (busy && i < HW) {
+    if constexpr (UPW > 0) {
+      if (i < HW) {
+#pragma unroll
+        for (int j = 0; j < UPW; ++j) {
+          const int u = wave + NW * j;
+          if (u < MFR * NF) {
+            const int row = u % MFR, nf = u / MFR;
+            const int64_t px = (int64_t)img * NPIX + row * HW + i;
+            const int nb = n0 + nf * 16 + 4 * g;
+            f32x4 v = uacc[j];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v[r] += bsv[nf][r];
+              if (relu) v[r] = fmaxf(v[r], 0.f);
+            }
+            if (mask != nullptr) {
+              const f32x4 mk = *(const f32x4*)(mask + px * ldm + nb);
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (!(mk[r] > 0.f)) v[r] = 0.f;
+            }
+            *(f32x4*)(out + px * ldo + nb) = v;
+          }
+        }
+      }
+    } else if (busy && i < HW) {
 #pragma unroll
       for (int h = 0; h < FR; ++h) {
         const int row = FR * wave + h;
@@ -322,12 +387,12 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_f32_wgrad_k(const float* _
   }
 }
 
-template <int CR, int CW, int NW, int MODE, int FR>
+template <int CR, int CW, int NW, int MODE, int FR, int UPW = 0>
 int halo_f32_grid(int B) {
   static int per = -1;
   if (per < 0) {
     int dev = 0, cus = 0, pc = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, conv5_halo_f32_k<CR, CW, NW, MODE, FR>, 64 * NW, 0) ==
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, conv5_halo_f32_k<CR, CW, NW, MODE, FR, UPW>, 64 * NW, 0) ==
             hipSuccess &&
         hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && pc > 0)
@@ -338,13 +403,13 @@ int halo_f32_grid(int B) {
   return cap_grid(B < per ? B : per);
 }
 
-template <int CR, int CW, int NW, int MODE, int FR>
+template <int CR, int CW, int NW, int MODE, int FR, int UPW = 0>
 hipError_t run_halo_f32(const float* x, const float* w, int wcin, int wcout, const float* bias, int relu,
                         const float* mask, int ldm, int B, float* out, int ncols, int ldo, hipStream_t st) {
   if (B <= 0) return hipSuccess;
   if (ncols % CW != 0) return hipErrorInvalidValue;
-  dim3 grid(halo_f32_grid<CR, CW, NW, MODE, FR>(B), ncols / CW);
-  hipLaunchKernelGGL((conv5_halo_f32_k<CR, CW, NW, MODE, FR>), grid, dim3(64 * NW), 0, st, x, w, wcin, wcout, bias,
+  dim3 grid(halo_f32_grid<CR, CW, NW, MODE, FR, UPW>(B), ncols / CW);
+  hipLaunchKernelGGL((conv5_halo_f32_k<CR, CW, NW, MODE, FR, UPW>), grid, dim3(64 * NW), 0, st, x, w, wcin, wcout, bias,
                      relu, mask, ldm, B, out, ldo);
   return hipGetLastError();
 }
@@ -365,9 +430,15 @@ bool f32_halo_dgrad_ok(int OH, int OW, int Cout, int H, int W, int KH, int KW, i
   return f32_halo_on() && H == 14 && W == 14 && OH == 14 && OW == 14 && KH == 5 && KW == 5 && ph == 2 && pw == 2 &&
          Cout == 64 && Cin % 16 == 0;
 }
+static int g_f32_halo_fwd_variant = 0;
+void set_f32_halo_fwd_variant(int v) { g_f32_halo_fwd_variant = v; }
+static int f32_halo_fwd_variant() { return g_f32_halo_fwd_variant; }
 hipError_t f32_halo_fwd(const float* x, const float* w, int Nb, int C, int Cout, const float* bias, int relu, float* y,
                         hipStream_t st) {
-  return run_halo_f32<32, 32, 8, 0, 2>(x, w, C, Cout, bias, relu, nullptr, 0, Nb, y, Cout, Cout, st);
+  // A/B hook (tests, bench/micro_halo_f32.py): 1 = the 7-group launch this replaced
+  if (f32_halo_fwd_variant() == 1)
+    return run_halo_f32<32, 32, 8, 0, 2>(x, w, C, Cout, bias, relu, nullptr, 0, Nb, y, Cout, Cout, st);
+  return run_halo_f32<32, 32, 8, 0, 1, 4>(x, w, C, Cout, bias, relu, nullptr, 0, Nb, y, Cout, Cout, st);
 }
 hipError_t f32_halo_dgrad(const float* dy, const float* w, int Nb, int Cout, int Cin, const float* mask, float* dx,
                           hipStream_t st) {

@@ -145,6 +145,7 @@ hipError_t f32_dense_wgrad(const float* x, const float* dy, int B, int Din, int 
 // conv_halo_f32.hip: LDS-halo fp32 conv2 of the reference CNN (fwd / dgrad), routed to by f32_conv_*
 bool f32_halo_fwd_ok(int H, int W, int C, int OH, int OW, int KH, int KW, int ph, int pw, int Cout);
 bool f32_halo_dgrad_ok(int OH, int OW, int Cout, int H, int W, int KH, int KW, int ph, int pw, int Cin);
+void set_f32_halo_fwd_variant(int v);   // 1: the pre-balance 7-group forward (A/B, tests)
 hipError_t f32_halo_fwd(const float* x, const float* w, int Nb, int C, int Cout, const float* bias, int relu, float* y,
                         hipStream_t st);
 hipError_t f32_halo_dgrad(const float* dy, const float* w, int Nb, int Cout, int Cin, const float* mask, float* dx,

@@ -166,13 +166,23 @@ def test_f32_training_cli(dev, K, tmp_path):
     assert json.load(open(out / "val.json"))
 
 
+@pytest.mark.parametrize("fv", [0, 1])
 @pytest.mark.parametrize("Nb,Co,cap", [(1, 64, 0), (37, 64, 0), (700, 32, 0), (37, 64, 3), (50, 32, 4)])
-def test_f32_halo_conv2(dev, K, grid_cap, Nb, Co, cap):
+def test_f32_halo_conv2(dev, K, grid_cap, Nb, Co, cap, fv):
     """conv_halo_f32.hip (reference conv2 geometry: 14x14, 5x5 SAME, 32 -> Co channels;
     dgrad of 64 dY channels with the input-ReLU mask) against PyTorch fp32, over
     persistent grids with several images per workgroup (cap > 0: `cap` blocks, >= 12
-    images each)."""
+    images each).  fv: forward launch (0: (row, fragment) units balanced over the SIMDs,
+    1: the 7 two-row groups it replaced)."""
     grid_cap(cap)
+    K.set_f32_halo_fwd_variant(fv)
+    try:
+        _halo_conv2_case(dev, K, Nb, Co)
+    finally:
+        K.set_f32_halo_fwd_variant(0)
+
+
+def _halo_conv2_case(dev, K, Nb, Co):
     torch.manual_seed(Nb)
     x = torch.randn(Nb, 14, 14, 32, device=dev)
     w = torch.randn(5, 5, 32, Co, device=dev) * 0.05

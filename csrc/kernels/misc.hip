@@ -839,9 +839,18 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void finalize_k(int64_t* step, floa
   } else if (l2 && l2r) {
     for (int w = wv - 1; w < nw && w < FIN_MAXW; w += FIN_WAVES - 1) {
       const int b0 = l2r[3 * w + 1], b1 = l2r[3 * w + 2];
-      // 4 independent chains per lane (loads in flight), combined in a fixed order
+      // 4 independent chains per lane, combined in a fixed order; 16 loads in flight per
+      // round (the reference CNN's local3 has thousands of partials: 4 per round left this
+      // wave's round trips most of finalize_k's ~11 us)
       float s4[4] = {0.f, 0.f, 0.f, 0.f};
       int b = b0 + t;
+      for (; b + 64 * 15 < b1; b += 64 * 16) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = l2[l2base + b + 64 * u];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s4[u & 3] += v[u];
+      }
       for (; b + 192 < b1; b += 256) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) s4[u] += l2[l2base + b + 64 * u];

@@ -7,7 +7,7 @@
 # STEP  one of
 #   tests[:EXPR]        pytest -m gpu (optionally -k EXPR), 900 s limit
 #   smoke               __graft_entry__.smoke()
-#   bench[:NAME]        python bench.py ARGS (NAME.json; ARGS from $BENCH_ARGS_<NAME> or none)
+#   bench[:NAME]        python bench.py ARGS (NAME.json; ARGS from $ARGS_<NAME> or none)
 #   prof[:NAME]         rocprofv3 kernel trace of a bench config -> NAME/kernels.md
 #   pmc[:NAME]          PMC passes (bench/pmc.sh) of a bench config -> NAME/pmc.md
 #   py:SCRIPT           python bench/SCRIPT.py (args from $ARGS_SCRIPT) -> SCRIPT.txt, 300 s limit

@@ -338,7 +338,7 @@ void lrn_pool_bwd(Tensor x, Tensor dP, Tensor arg, Tensor dx, int64_t Nb, int64_
 
 int64_t softmax_ce(Tensor logits, int64_t ldl, optional<Tensor> labels, int64_t B, int64_t NC, double scale,
                    optional<Tensor> dlogits, int64_t ldd, optional<Tensor> stats, optional<Tensor> probs,
-                   optional<Tensor> work, bool defer_stats) {
+                   optional<Tensor> work, bool defer_stats, optional<Tensor> dbias) {
   TORCH_CHECK(ldl >= NC, "ldl < NC");
   check(logits, at::kFloat, B * ldl, "logits");   // whole padded rows (vector loads)
   const int32_t* lab = nullptr;
@@ -369,9 +369,17 @@ int64_t softmax_ce(Tensor logits, int64_t ldl, optional<Tensor> labels, int64_t 
     check(*work, at::kFloat, 4 * 1024 + 1, "work");
     wk = P<float>(*work);
   }
+  float* db = nullptr;
+  if (dbias.has_value() && dbias->defined()) {
+    TORCH_CHECK(dl != nullptr, "dbias needs dlogits");
+    const int nblk = mnistx::softmax_ce_dbias_blocks((int)B, (int)ldl);
+    TORCH_CHECK(nblk > 0, "dbias: only the row kernel (ldl 16 / 32) writes bias partials");
+    check(*dbias, at::kFloat, (int64_t)nblk * ldl, "dbias");
+    db = P<float>(*dbias);
+  }
   int deferred = 0;
   hip_ok(mnistx::softmax_ce(P<const float>(logits), (int)ldl, lab, (int)B, (int)NC, (float)scale, dl, (int)ldd, st, pr,
-                            wk, cur_stream(), defer_stats ? &deferred : nullptr),
+                            wk, cur_stream(), defer_stats ? &deferred : nullptr, db),
          "softmax_ce");
   return deferred;   // blocks whose CE partials the caller's finalize_step must combine
 }
@@ -387,7 +395,7 @@ bool mlp_head_supported(int64_t d0, int64_t ld1, int64_t ld2, int64_t ld3, int64
 void mlp_head(Tensor x, Tensor w3t, Tensor b3, int64_t n1, Tensor w4t, Tensor b4, int64_t n2, Tensor w5t, Tensor b5,
               int64_t nc, Tensor labels, int64_t nb, double scale, Tensor h3, Tensor h4, Tensor logits,
               optional<Tensor> dl, optional<Tensor> dh4, optional<Tensor> dh3, optional<Tensor> dx, Tensor stats,
-              optional<Tensor> work, bool defer_stats) {
+              optional<Tensor> work, bool defer_stats, optional<Tensor> dbias) {
   TORCH_CHECK(mnistx::mlp_head_supported(400, 120, 88, 16, (int)n1, (int)n2, (int)nc, (int)std::max<int64_t>(nb, 1)),
               "mlp_head: unsupported geometry");
   check(x, at::kBFloat16, nb * 400, "x");
@@ -420,10 +428,16 @@ void mlp_head(Tensor x, Tensor w3t, Tensor b3, int64_t n1, Tensor w4t, Tensor b4
     pdh3 = BFm(*dh3);
     pdx = BFm(*dx);
   }
+  float* db = nullptr;
+  if (dbias.has_value() && dbias->defined()) {
+    TORCH_CHECK(pdl != nullptr, "mlp_head: dbias needs dl");
+    check(*dbias, at::kFloat, (int64_t)mnistx::mlp_head_blocks((int)nb) * 16, "dbias");
+    db = P<float>(*dbias);
+  }
   hip_ok(mnistx::mlp_head(BF(x), BF(w3t), P<const float>(b3), (int)n1, BF(w4t), P<const float>(b4), (int)n2, BF(w5t),
                           P<const float>(b5), (int)nc, P<const int32_t>(labels), (int)nb, (float)scale, BFm(h3),
                           BFm(h4), P<float>(logits), pdl, pdh4, pdh3, pdx, P<float>(stats), has_work ? P<float>(*work) : nullptr,
-                          cur_stream(), (defer_stats && has_work) ? 1 : 0),
+                          cur_stream(), (defer_stats && has_work) ? 1 : 0, db),
          "mlp_head");
 }
 
@@ -1172,7 +1186,9 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("lrn_pool_bwd", &lrn_pool_bwd);
   m.def("softmax_ce", &softmax_ce, py::arg("logits"), py::arg("ldl"), py::arg("labels"), py::arg("B"), py::arg("NC"),
         py::arg("scale"), py::arg("dlogits"), py::arg("ldd"), py::arg("stats"), py::arg("probs"),
-        py::arg("work") = py::none(), py::arg("defer_stats") = false);
+        py::arg("work") = py::none(), py::arg("defer_stats") = false, py::arg("dbias") = py::none());
+  m.def("softmax_ce_dbias_blocks",
+        [](int64_t B, int64_t ldl) { return (int64_t)mnistx::softmax_ce_dbias_blocks((int)B, (int)ldl); });
   m.def("splitk_reduce", &splitk_reduce);
   m.def("splitk_reduce_multi", &splitk_reduce_multi);
   m.def("mlp_head_supported", &mlp_head_supported);
@@ -1180,7 +1196,7 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("b4"), py::arg("n2"), py::arg("w5t"), py::arg("b5"), py::arg("nc"), py::arg("labels"), py::arg("nb"),
         py::arg("scale"), py::arg("h3"), py::arg("h4"), py::arg("logits"), py::arg("dl") = py::none(),
         py::arg("dh4") = py::none(), py::arg("dh3") = py::none(), py::arg("dx") = py::none(), py::arg("stats"),
-        py::arg("work"), py::arg("defer_stats") = false);
+        py::arg("work"), py::arg("defer_stats") = false, py::arg("dbias") = py::none());
   m.def("fused_optimizer", &fused_optimizer, py::arg("params"), py::arg("grads"), py::arg("mom"), py::arg("ema"),
         py::arg("bf"), py::arg("segs"), py::arg("step"), py::arg("lr0"), py::arg("decay_rate"),
         py::arg("decay_steps"), py::arg("momentum"), py::arg("nesterov"), py::arg("use_momentum"),

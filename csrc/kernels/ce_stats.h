@@ -79,3 +79,25 @@ DEV void ce_block_stats(float loss, float corr, float bad, float* __restrict__ s
     *(unsigned*)(work + 4 * CE_MAXB) = 0u;
   }
 }
+
+// Deterministic per-block column sums of fp32 values (the last layer's bias gradient =
+// sum over rows of dlogits, kept in fp32 as the reference's tf.float32 graph does:
+// mnist_input.py:203-205 / 224-226): v[c] of every thread -> wave (fixed xor tree) ->
+// waves in order -> out[c].  Every thread of the block must call this.
+template <int NW, int LD>
+DEV void block_colsum(const float (&v)[LD], float* __restrict__ out) {
+  __shared__ float red[NW][LD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < LD; ++c) {
+    const float s = warp_sum(v[c]);
+    if (lane == 0) red[wave][c] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < LD) {
+    float s = red[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) s += red[w][threadIdx.x];
+    out[threadIdx.x] = s;
+  }
+}

@@ -618,23 +618,8 @@ __global__ __launch_bounds__(256) void lrn_pool_f32_bwd_k(const float* __restric
       f32x4 g;
 #pragma unroll
       for (int j = 0; j < 4; ++j) g[j] = ((a >> (8 * j)) & 0xffu) == (uint32_t)d ? gp[j] : 0.f;
-      const f32x4 s = win4(v * v, threadIdx.x % G, G, r);
-      f32x4 nb, tv;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float p0, p1;
-        pow_neg2(fmaf(alpha, s[j], bias), beta, p0, p1);
-        nb[j] = p0;
-        tv[j] = g[j] * v[j] * p1;
-      }
-      const f32x4 u = win4(tv, threadIdx.x % G, G, r);
-      f32x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float dd = g[j] * nb[j] - 2.f * alpha * beta * v[j] * u[j];
-        if (relu_mask && !(v[j] > 0.f)) dd = 0.f;
-        o[j] = dd;
-      }
+      // the shared LRN backward (no FMA contraction): bitwise the unfused LRNF + PoolF pair
+      const f32x4 o = lrn_f32_bwd4(v, g, threadIdx.x % G, G, r, bias, alpha, beta, relu_mask);
       if (ok) *(f32x4*)(dx + off) = o;
     }
   }

@@ -226,9 +226,12 @@ hipError_t lrn_pool_bwd(const bf16_t* x, const bf16_t* dP, const uint8_t* arg, i
 // defer_blocks (optional out): with it, the row kernel writes per-block partials only and
 // reports its block count there (0 when the fallback kernel ran: plain atomics); the
 // caller's finalize_step combines them (ce_stats.h defer)
+// dbias (optional, with dlogits): per-block fp32 column sums of dlogits [blocks][ldl]
+// (blocks = softmax_ce_dbias_blocks; only the row kernel, ldl 16 / 32, writes them)
 hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B, int NC, float scale,
                       bf16_t* dlogits, int ldd, float* stats, float* probs, float* work, hipStream_t st,
-                      int* defer_blocks = nullptr);
+                      int* defer_blocks = nullptr, float* dbias = nullptr);
+int softmax_ce_dbias_blocks(int B, int ldl);
 // Fused LeNet-5 dense head (mlp_head.hip): fc3/fc4/fc5 + softmax-CE (+ with dl:
 // the data-gradient chain dlogits -> dh4 -> dh3 -> dx).  Writes h3, h4, logits
 // always; dl, dh4, dh3, dx when dl != nullptr.  Same work-buffer contract as softmax_ce.
@@ -237,7 +240,7 @@ bool mlp_head_supported(int d0, int ld1, int ld2, int ld3, int n1, int n2, int n
 hipError_t mlp_head(const bf16_t* x, const bf16_t* w3t, const float* b3, int n1, const bf16_t* w4t, const float* b4,
                     int n2, const bf16_t* w5t, const float* b5, int nc, const int32_t* labels, int nb, float scale,
                     bf16_t* h3, bf16_t* h4, float* logits, bf16_t* dl, bf16_t* dh4, bf16_t* dh3, bf16_t* dx,
-                    float* stats, float* work, hipStream_t st, int defer_stats = 0);
+                    float* stats, float* work, hipStream_t st, int defer_stats = 0, float* dbias = nullptr);
 // blocks of one mlp_head launch (its per-block CE partials when defer_stats is set)
 int mlp_head_blocks(int nb);
 // NOTE: many splits over a small output are pre-summed IN PLACE (the slab is scratch).

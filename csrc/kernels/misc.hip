@@ -487,8 +487,12 @@ __global__ __launch_bounds__(256) void softmax_ce_rows_k(const float* __restrict
                                                          const int32_t* __restrict__ labels, int B, int NC,
                                                          float scale, bf16_t* __restrict__ dl,
                                                          float* __restrict__ stats, float* __restrict__ probs,
-                                                         float* __restrict__ work, int defer_stats) {
+                                                         float* __restrict__ work, int defer_stats,
+                                                         float* __restrict__ dbias) {
   float loss = 0.f, corr = 0.f, bad = 0.f;
+  float cs[LD];   // fp32 column sums of dlogits (dbias: the last layer's bias gradient partial)
+#pragma unroll
+  for (int c = 0; c < LD; ++c) cs[c] = 0.f;
   for (int row = blockIdx.x * 256 + threadIdx.x; row < B; row += gridDim.x * 256) {
     float l[LD];
 #pragma unroll
@@ -527,9 +531,11 @@ __global__ __launch_bounds__(256) void softmax_ce_rows_k(const float* __restrict
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
           const int c0 = 8 * v + 2 * h;
-          const float g0 = (e[c0] * inv - (c0 == lab ? 1.f : 0.f)) * scale;
-          const float g1 = (e[c0 + 1] * inv - (c0 + 1 == lab ? 1.f : 0.f)) * scale;
-          o[h] = pack2(c0 < NC ? g0 : 0.f, c0 + 1 < NC ? g1 : 0.f);
+          const float g0 = c0 < NC ? (e[c0] * inv - (c0 == lab ? 1.f : 0.f)) * scale : 0.f;
+          const float g1 = c0 + 1 < NC ? (e[c0 + 1] * inv - (c0 + 1 == lab ? 1.f : 0.f)) * scale : 0.f;
+          o[h] = pack2(g0, g1);
+          cs[c0] += g0;
+          cs[c0 + 1] += g1;
         }
         *(u32x4*)(dl + (int64_t)row * LD + 8 * v) = o;
       }
@@ -539,6 +545,7 @@ __global__ __launch_bounds__(256) void softmax_ce_rows_k(const float* __restrict
       for (int c = 0; c < LD; ++c)
         if (c < NC) probs[(int64_t)row * NC + c] = e[c] * inv;
   }
+  if (dl && dbias) block_colsum<4, LD>(cs, dbias + (int64_t)blockIdx.x * LD);
   if (stats) ce_block_stats<4>(loss, corr, bad, stats, work, defer_stats != 0);
 }
 
@@ -1019,9 +1026,13 @@ hipError_t lrn_bwd(const bf16_t* x, const bf16_t* dy, int P, int C, int r, float
   return hipErrorInvalidValue;
 }
 
+int softmax_ce_dbias_blocks(int B, int ldl) {
+  return (ldl == 16 || ldl == 32) && B > 0 ? (int)std::min<int64_t>(CE_MAXB, ((int64_t)B + 255) / 256) : 0;
+}
+
 hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B, int NC, float scale,
                       bf16_t* dlogits, int ldd, float* stats, float* probs, float* work, hipStream_t st,
-                      int* defer_blocks) {
+                      int* defer_blocks, float* dbias) {
   const int nb = (int)std::min<int64_t>(CE_MAXB, ((int64_t)B + 255) / 256);
   if (defer_blocks) *defer_blocks = 0;
   const bool rows_ok = (ldl == 16 || ldl == 32) && NC <= ldl && (!dlogits || ldd == ldl) &&
@@ -1031,12 +1042,13 @@ hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B
     if (defer) *defer_blocks = nb;
     if (ldl == 16)
       hipLaunchKernelGGL(softmax_ce_rows_k<16>, dim3(nb), dim3(256), 0, st, logits, labels, B, NC, scale, dlogits,
-                         stats, probs, work, defer);
+                         stats, probs, work, defer, dbias);
     else
       hipLaunchKernelGGL(softmax_ce_rows_k<32>, dim3(nb), dim3(256), 0, st, logits, labels, B, NC, scale, dlogits,
-                         stats, probs, work, defer);
+                         stats, probs, work, defer, dbias);
     return hipGetLastError();
   }
+  if (dbias) return hipErrorInvalidValue;   // the row kernel's block partials only
   hipLaunchKernelGGL(softmax_ce_k, dim3((B + TPB - 1) / TPB), dim3(TPB), 0, st, logits, ldl, labels, B, NC, scale,
                      dlogits, ldd, stats, probs);
   return hipGetLastError();

@@ -178,7 +178,8 @@ __global__ __launch_bounds__(64 * NW) void mlp_head_k(const bf16_t* __restrict__
                                                   float* __restrict__ logits, bf16_t* __restrict__ dl,
                                                   bf16_t* __restrict__ dh4, bf16_t* __restrict__ dh3,
                                                   bf16_t* __restrict__ dx, float* __restrict__ stats,
-                                                  float* __restrict__ work, int defer_stats) {
+                                                  float* __restrict__ work, int defer_stats,
+                                                  float* __restrict__ dbias) {
   __shared__ __attribute__((aligned(16))) bf16_t i3[R3 * S3];
   __shared__ __attribute__((aligned(16))) bf16_t i4[R4 * S4];
   __shared__ __attribute__((aligned(16))) bf16_t i5[R5 * S5];
@@ -234,6 +235,7 @@ __global__ __launch_bounds__(64 * NW) void mlp_head_k(const bf16_t* __restrict__
   __syncthreads();
 
   float loss = 0.f, corr = 0.f, bad = 0.f;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // fp32 dlogits column sums (dbias)
 #pragma unroll
   for (int ti = 0; ti < TPW; ++ti) {
   const int m0 = tile_m0(ti);
@@ -351,6 +353,7 @@ __global__ __launch_bounds__(64 * NW) void mlp_head_k(const bf16_t* __restrict__
         for (int k = 0; k < 2; ++k) {
           const int i = 2 * w + k, cls = (i & 3) + 8 * (i >> 2) + 4 * h;
           g2[k] = cls < nc ? (e[i] * inv - (cls == lab ? 1.f : 0.f)) * scale : 0.f;
+          cs[i] += valid ? g2[k] : 0.f;
         }
         dlp[w] = pack2(g2[0], g2[1]);
       }
@@ -421,6 +424,27 @@ __global__ __launch_bounds__(64 * NW) void mlp_head_k(const bf16_t* __restrict__
   }
   lab = lab_next;
   }
+  if (GRADS && dbias) {
+    // the softmax_linear bias gradient in fp32 (the reference's tf.float32,
+    // mnist_input.py:203-205): this block's column sums, lanes of a half in a fixed xor
+    // tree, then the waves in order
+    __shared__ float dbs[NW][16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) cs[i] += __shfl_xor(cs[i], o, 64);
+    }
+    if (r == 0)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dbs[wave][(i & 3) + 8 * (i >> 2) + 4 * h] = cs[i];
+    __syncthreads();
+    if (tid < 16) {
+      float v = dbs[0][tid];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) v += dbs[w][tid];
+      dbias[(int64_t)blockIdx.x * 16 + tid] = v;
+    }
+  }
   if (stats) ce_block_stats<NW>(loss, corr, bad, stats, work, defer_stats != 0);
 }
 
@@ -436,15 +460,15 @@ bool mlp_head_supported(int d0, int ld1, int ld2, int ld3, int n1, int n2, int n
 hipError_t mlp_head(const bf16_t* x, const bf16_t* w3t, const float* b3, int n1, const bf16_t* w4t, const float* b4,
                     int n2, const bf16_t* w5t, const float* b5, int nc, const int32_t* labels, int nb, float scale,
                     bf16_t* h3, bf16_t* h4, float* logits, bf16_t* dl, bf16_t* dh4, bf16_t* dh3, bf16_t* dx,
-                    float* stats, float* work, hipStream_t st, int defer_stats) {
+                    float* stats, float* work, hipStream_t st, int defer_stats, float* dbias) {
   if (nb <= 0) return hipSuccess;
   const dim3 grid((nb + ROWS - 1) / ROWS);   // ROWS rows per block
   if (dl)
     hipLaunchKernelGGL(mlp_head_k<true>, grid, dim3(NTH), 0, st, x, w3t, b3, n1, w4t, b4, n2, w5t, b5, nc, labels, nb,
-                       scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work, defer_stats);
+                       scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work, defer_stats, dbias);
   else
     hipLaunchKernelGGL(mlp_head_k<false>, grid, dim3(NTH), 0, st, x, w3t, b3, n1, w4t, b4, n2, w5t, b5, nc, labels, nb,
-                       scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work, defer_stats);
+                       scale, h3, h4, logits, dl, dh4, dh3, dx, stats, work, defer_stats, nullptr);
   return hipGetLastError();
 }
 

@@ -90,6 +90,7 @@ tasks restarting at once, or a worker dying (the supervisor restarts the whole j
 from __future__ import annotations
 
 import os
+import re
 import signal
 import sys
 import time
@@ -148,8 +149,12 @@ def is_peer_loss(e: BaseException) -> bool:
         if t is not None and isinstance(e, t):
             return True
     msg = str(e).lower()
-    return any(k in msg for k in ("gloo", "connection", "connect", "timed out", "timeout", "reset by peer",
-                                  "broken pipe", "socket", "closed", "eof"))
+    if re.search(r"\bhip|cuda", msg):
+        return False             # e.g. hipErrorLaunchTimeOut: a compute failure, re-raised at once
+    # only gloo's own transport errors (plain RuntimeError in some builds): the word gloo
+    # together with a connection / timeout symptom
+    return "gloo" in msg and any(k in msg for k in ("connection", "connect", "timed out", "timeout", "reset by peer",
+                                                    "broken pipe", "socket", "closed", "eof"))
 
 
 class PushIntegrityError(RuntimeError):
@@ -741,10 +746,9 @@ class PSClient:
 
     def done(self) -> None:
         """DONE to every PS, through the same recovery as an exchange: a PS that dies
-        while the workers shut down is relaunched and still hears every DONE."""
-        if self.cluster is not None and self.cluster.store is not None:
-            from .cluster import DONE_KEY
-            self.cluster.store.set(f"{DONE_KEY}/rank{dist.get_rank()}", "1")
+        while the workers shut down is relaunched and still hears every DONE.  The
+        store's done key (which makes a relaunched PS give up in-place recovery) is set
+        only once every PS has been told: until then this worker can still rejoin."""
         told: set = set()
         while True:
             try:
@@ -755,6 +759,9 @@ class PSClient:
                     c[0] = DONE
                     dist.send(c, j, group=self.group, tag=TAG_CTRL)
                     told.add(j)
+                if self.cluster is not None and self.cluster.store is not None:
+                    from .cluster import DONE_KEY
+                    self.cluster.store.set(f"{DONE_KEY}/rank{dist.get_rank()}", "1")
                 return
             except RuntimeError as e:
                 if not is_peer_loss(e):

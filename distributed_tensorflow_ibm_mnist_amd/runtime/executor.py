@@ -331,11 +331,23 @@ class DenseLayer(_Layer):
                           Fk.pick_splits(self.M_wg, self.Np, nb, dense=True))
         self.reduce_wgrad(S, slab, red)
 
+    # (per-block fp32 dlogits column sums [blocks, Np], blocks): set by the softmax-CE /
+    # fused-head launch of the step; the last layer's bias gradient is their sum instead of
+    # the bias row of the bf16-dlogits GEMM (the reference computes it in tf.float32,
+    # mnist_input.py:203-205,224-226)
+    ce_bias: Optional[Tuple[torch.Tensor, int]] = None
+
     def reduce_wgrad(self, S: int, slab: torch.Tensor, red: Optional[list] = None) -> None:
         """Queue (or run) the split-K reduce of an S-split weight-gradient slab."""
         s = self.spec
+        bgrad = self.fp.grad_view(self.bname)
+        cb = self.ce_bias
         _reduce(red, slab, (S, self.M_wg, self.Np, 1, self.Dp, s.din, s.dout, self.Dp),
-                self.fp.grad_view(self.wname), self.fp.grad_view(self.bname))
+                self.fp.grad_view(self.wname), bgrad if cb is None else bgrad[:0])
+        if cb is not None:
+            # bias only (G = 0): sum of the CE kernel's block partials, rows = blocks
+            _reduce(red, cb[0], (cb[1], 1, self.Np, 0, 1, 0, s.dout, 0), bgrad[:0], bgrad)
+            self.ce_bias = None
 
     def bwd_data(self, nb: int, dy: torch.Tensor, dx: Optional[torch.Tensor]) -> None:
         if dx is not None:
@@ -443,6 +455,8 @@ class HipNet:
         self.logits = self.layers[-1].out
         self.n_classes = spec.num_classes
         self.dlogits = _bf16(batch, self.logits.shape[1], device=dev)
+        # per-block fp32 column sums of dlogits (the last layer's bias gradient, DenseLayer.ce_bias)
+        self.ce_dbias = torch.zeros(1024 * 32, dtype=torch.float32, device=dev)
         # overlap_backward: every weight gradient (+ its split-K reduce) runs on a side
         # stream, concurrently with the data-gradient chain on the main stream (one
         # input-gradient buffer and one slab region per layer, so the streams never share
@@ -571,7 +585,10 @@ class HipNet:
                            self.labels, nb, scale, l3.out, l4.out, l5.out,
                            dl=self.dlogits if grads else None, dh4=self.dbuf[i + 2] if grads else None,
                            dh3=self.dbuf[i + 1] if grads else None, dx=self.dbuf[i] if grads else None,
-                           stats=stats, work=self.ce_work, defer_stats=defer)
+                           stats=stats, work=self.ce_work, defer_stats=defer,
+                           dbias=self.ce_dbias if grads else None)
+        if grads:
+            l5.ce_bias = (self.ce_dbias, kernels().mlp_head_blocks(nb))
         if defer:
             self._ce_defer_blocks = kernels().mlp_head_blocks(nb)
 
@@ -668,10 +685,14 @@ class HipNet:
             self._head_pending, self._head_grads = None, True
             return
         # training statistics deferred to this step's finalize_k, as for the fused head
+        ld = self.logits.shape[1]
+        nblk = kernels().softmax_ce_dbias_blocks(nb, ld)
         self._ce_defer_blocks = kernels().softmax_ce(
-            self.logits, self.logits.shape[1], self.labels, nb, self.n_classes,
-            (1.0 / nb) if scale is None else scale, self.dlogits, self.logits.shape[1], self.stats,
-            None, self.ce_work, defer_stats=self.ce_work is not None)
+            self.logits, ld, self.labels, nb, self.n_classes,
+            (1.0 / nb) if scale is None else scale, self.dlogits, ld, self.stats,
+            None, self.ce_work, defer_stats=self.ce_work is not None,
+            dbias=self.ce_dbias if nblk > 0 else None)
+        self.layers[-1].ce_bias = (self.ce_dbias, nblk) if nblk > 0 else None
 
     def backward(self, nb: Optional[int] = None) -> None:
         """Data-gradient chain on the current stream; each layer's weight gradient

@@ -164,6 +164,13 @@ class CheckpointSaverHook(SessionRunHook):
             self._save(session)
 
     def _save(self, session) -> None:
+        # The NaN guard reads the device flag only every N steps (NanTensorHook), so a save
+        # can fall between a NaN step and its detection: read the flag synchronously here
+        # (one sync per checkpoint) and never write poisoned parameters -- a restart would
+        # restore them and fail again.
+        st = getattr(session, "stats", None)
+        if st is not None and float(st[2]) != 0.0:
+            raise NanLossDuringTrainingError()
         session.save_checkpoint()
         self._last_step = session.global_step
         self._last_time = time.time()

@@ -454,3 +454,15 @@ def test_ps_supervisor_never_restarts_a_fatal_ps(tmp_path):
     assert any("(fatal); not restarting" in m for m in msgs), msgs
     assert not any("restarting it in place" in m or "attempt 1" in m for m in msgs), msgs
     assert "PushIntegrityError" in open(os.path.join(logs, "attempt0_ps0.log")).read()
+
+
+def test_is_peer_loss_classification():
+    """Only lost-peer control-plane errors enter PS recovery; a HIP / CUDA failure that
+    happens to mention a timeout is re-raised at once (it is not a lost peer)."""
+    from distributed_tensorflow_ibm_mnist_amd.parallel.ps import PushIntegrityError, is_peer_loss
+    assert is_peer_loss(RuntimeError("[../third_party/gloo/gloo/transport/tcp/pair.cc:534] Connection closed by peer"))
+    assert is_peer_loss(RuntimeError("Gloo: Timed out waiting 60000ms for recv operation to complete"))
+    assert not is_peer_loss(RuntimeError("HIP error: hipErrorLaunchTimeOut: the launch timed out"))
+    assert not is_peer_loss(RuntimeError("CUDA error: unspecified launch failure (connection to gloo lost?)"))
+    assert not is_peer_loss(RuntimeError("socket timeout"))          # no gloo: not ours to recover
+    assert not is_peer_loss(PushIntegrityError("gloo connection closed"))

@@ -104,11 +104,23 @@ def test_f32_pool_lrn(dev, K):
 def test_f32_step_matches_oracle(dev, K, model, cin):
     """The whole fp32 step (fwd + CE + explicit bwd + fused update) vs the fp32
     oracle at rtol 1e-4 -- no bf16 noise floor in this mode."""
+    _f32_step_vs_oracle(dev, model, cin, 96)
+
+
+@pytest.mark.parametrize("cin", [1, 3])
+def test_f32_step_matches_oracle_bench_batch(dev, K, cin):
+    """The fp32 benchmark's own batch (reference CNN, B = 16384, the reference's
+    tf.float32: mnist_input.py:86,107), 1- and 3-channel input, at the same 1e-4: every
+    persistent kernel loops over many images per block and the split-K weight gradients
+    sum 16384 images in a different order than the oracle (fp32 reassociation only)."""
+    _f32_step_vs_oracle(dev, "reference_cnn", cin, 16384)
+
+
+def _f32_step_vs_oracle(dev, model, cin, B):
     from distributed_tensorflow_ibm_mnist_amd.runtime.executor_f32 import HipNetF32
     torch.manual_seed(0)
     spec = get_model(model, cin)
     init = torch_ref.init_params(spec, seed=1)
-    B = 96
     net = HipNetF32(spec, B, dev, init, OptConfig(lr0=0.05, decay_steps=0, use_momentum=False, ema_max=0.9999))
     x = torch.rand(B, 28, 28, cin, device=dev) - 0.5
     y = torch.randint(0, 10, (B,), device=dev, dtype=torch.int32)

@@ -91,6 +91,20 @@ def test_nan_guard_fault_injection(tmp_path, every):
     assert lc is None or lc.endswith("model.ckpt-0")
 
 
+def test_no_checkpoint_inside_nan_window(tmp_path):
+    """A checkpoint due between a NaN step and the asynchronous NaN check (every 40 steps
+    here, saves every 2) must not be written: the saver reads the device flag itself."""
+    r = run_main(["--model=mlp", "--in_channels=1", "--batch_size=16", "--max_steps=30", "--test_interval=100",
+                  f"--train_dir={tmp_path}", "--nan_check_steps=40", "--save_checkpoint_steps=2"],
+                 env={"MNIST_FI_NAN_AT_STEP": "5"})
+    assert r.returncode != 0
+    assert "NaN loss during training" in (r.stderr + r.stdout)
+    from distributed_tensorflow_ibm_mnist_amd.ckpt.saver import Saver, latest_checkpoint
+    lc = latest_checkpoint(str(tmp_path))
+    assert lc is not None and int(lc.rsplit("-", 1)[1]) <= 5, lc
+    assert np.isfinite(Saver.restore(lc)["hidden/weights"]).all()
+
+
 def test_crash_and_resume_from_last_checkpoint(tmp_path):
     d = str(tmp_path)
     r = run_main(["--model=mlp", "--in_channels=1", "--batch_size=16", "--max_steps=40", "--test_interval=100",

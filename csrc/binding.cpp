@@ -1154,6 +1154,19 @@ PYBIND11_MODULE(_kernels, m) {
   // test hook: cap every persistent kernel's grid (0 = off) so small-batch oracle tests run
   // the multi-iteration (several tiles per block) paths the benchmark batches run
   m.def("set_grid_cap", [](int64_t n) { mnistx::set_grid_cap((int)n); });
+  m.def("set_reserve_cus", [](int64_t n) { mnistx::set_reserve_cus((int)n); });
+  m.def("reserve_cus", []() { return (int64_t)mnistx::reserve_cus(); });
+  m.def("clock_mark", [](Tensor out, int64_t slot) {
+    TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kLong && out.is_contiguous() && slot >= 0 &&
+                    slot < out.numel(), "clock_mark: int64 GPU buffer with the slot in range");
+    hip_ok(mnistx::clock_mark((uint64_t*)out.data_ptr<int64_t>(), (int)slot, cur_stream()), "clock_mark");
+  });
+  m.def("coresidency_probe", [](Tensor out, int64_t blocks, int64_t threads, int64_t lds_bytes, int64_t spin_ticks) {
+    TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kLong && out.is_contiguous() && out.numel() >= 2 * blocks,
+                "coresidency_probe: int64 GPU buffer of 2 * blocks stamps");
+    hip_ok(mnistx::coresidency_probe((uint64_t*)out.data_ptr<int64_t>(), (int)blocks, (int)threads, (int)lds_bytes,
+                                     (int)spin_ticks, cur_stream()), "coresidency_probe");
+  });
   m.def("grid_cap", []() { return (int64_t)mnistx::grid_cap(); });
   m.doc() = "MI355X (gfx950) HIP kernels for the MNIST trainer";
   m.def("dense_fwd", &dense_fwd);

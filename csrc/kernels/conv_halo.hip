@@ -426,36 +426,37 @@ __global__ __launch_bounds__(64 * NW) void conv5_halo_wgrad_k(const bf16_t* __re
 }
 
 template <int CIN, int COUT, int NW>
-int halo_wgrad_resident() {
-  static int per = -1;
+int halo_wgrad_resident(int* per_cu = nullptr) {
+  static int per = -1, pc = 1;
   if (per < 0) {
-    int dev = 0, cus = 0, pc = 0;
+    int dev = 0, cus = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, conv5_halo_wgrad_k<CIN, COUT, NW>, 64 * NW, 0) ==
             hipSuccess &&
         hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && pc > 0)
       per = pc * cus;
     else
-      per = 256;
+      per = 256, pc = 1;
   }
+  if (per_cu) *per_cu = pc;
   return per;
 }
 
 template <int CIN, int CW, int NW, int MODE, int FR, int IMGS, bool LRNX = false, bool ROWS = false>
 int halo_grid(int B) {
-  static int per = -1;
+  static int per = -1, pc = 1;
   if (per < 0) {
-    int dev = 0, cus = 0, pc = 0;
+    int dev = 0, cus = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, conv5_halo_k<CIN, CW, NW, MODE, FR, IMGS, LRNX, ROWS>, 64 * NW, 0) ==
             hipSuccess &&
         hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && pc > 0)
       per = pc * cus;
     else
-      per = 256;
+      per = 256, pc = 1;
   }
-  const int groups = (B + IMGS - 1) / IMGS;
-  return cap_grid(groups < per ? groups : per);
+  const int groups = (B + IMGS - 1) / IMGS, res = reserve_cut(per, pc);
+  return cap_grid(groups < res ? groups : res);
 }
 
 template <int CIN, int CW, int NW, int MODE, int FR, int IMGS = 1, bool LRNX = false, bool ROWS = false>
@@ -563,7 +564,8 @@ bool conv5_halo_wgrad_ok(int H, int W, int C, int OH, int OW, int KH, int KW, in
          C == 32 && Cout == 64;
 }
 int conv5_halo_wgrad_grid(int Nb) {
-  const int r = halo_wgrad_resident<32, 64, 8>();
+  int pc = 1;
+  const int r = reserve_cut(halo_wgrad_resident<32, 64, 8>(&pc), pc);
   return Nb < r ? (Nb < 1 ? 1 : Nb) : r;
 }
 hipError_t conv5_halo_wgrad(const bf16_t* x, const bf16_t* dy, int Nb, int grid, float* slab, hipStream_t st,

@@ -19,6 +19,21 @@ inline int cap_grid(int g) {
   const int c = grid_cap();
   return (c > 0 && g > c) ? c : g;
 }
+// CUs kept free of the persistent (one-resident-wave) kernels so that a collective launched
+// on another stream can start while they run (binding set_reserve_cus; parallel/dp.py sets
+// it when a gradient bucket's all-reduce is issued before such a kernel and world > 1;
+// profiles/r5/dp_coresidency/).  A resident grid of per_cu * cus blocks becomes
+// per_cu * (cus - reserve).  0 = every CU (the default and the one-GPU setting).
+int reserve_cus();
+void set_reserve_cus(int n);
+inline int reserve_cut(int resident, int per_cu) {
+  const int r = reserve_cus() * (per_cu > 0 ? per_cu : 1);
+  return (r > 0 && resident - r >= 1) ? resident - r : resident;
+}
+
+// ---- probe.hip (tests / measurements only): wall-clock marks and an RCCL-footprint probe
+hipError_t clock_mark(uint64_t* out, int slot, hipStream_t st);
+hipError_t coresidency_probe(uint64_t* out, int blocks, int threads, int lds_bytes, int spin_ticks, hipStream_t st);
 
 enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_SLAB = 2 };
 

@@ -451,7 +451,8 @@ int fwd_grid(int ntiles) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lenet_band_fwd_k<P1OUT>, NTH, 0) != hipSuccess) return -1;
     per_cu = nb > 0 ? nb : 1;
   }
-  return cap_grid(ntiles < per_cu * cus ? ntiles : per_cu * cus);
+  const int res = reserve_cut(per_cu * cus, per_cu);
+  return cap_grid(ntiles < res ? ntiles : res);
 }
 
 
@@ -582,7 +583,8 @@ int refc1_band_grid(int ntiles) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, refc1_band_fwd_k, RNTH, 0) != hipSuccess) return -1;
     per_cu = nb > 0 ? nb : 1;
   }
-  return cap_grid(ntiles < per_cu * cus ? ntiles : per_cu * cus);
+  const int res = reserve_cut(per_cu * cus, per_cu);
+  return cap_grid(ntiles < res ? ntiles : res);
 }
 
 }  // namespace

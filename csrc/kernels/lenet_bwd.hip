@@ -525,10 +525,10 @@ constexpr BwdKernel kBwd[8] = {lenet_bwd_k<false, false, false>, lenet_bwd_k<fal
 
 }  // namespace
 
-int lenet_bwd_grid() {
-  static int n = 0;
+int lenet_bwd_grid(int* per_cu = nullptr) {
+  static int n = 0, per = 0;
   if (n == 0) {
-    int dev = 0, cus = 0, per = 0;
+    int dev = 0, cus = 0;
     for (BwdKernel k : kBwd)
       if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) != hipSuccess)
         return -1;
@@ -538,6 +538,7 @@ int lenet_bwd_grid() {
       return -1;
     n = per * cus;
   }
+  if (per_cu) *per_cu = per;
   return n;
 }
 
@@ -559,10 +560,13 @@ hipError_t lenet_bwd(const XSrc& x, const bf16_t* p1, const uint8_t* arg1, const
   return hipLaunchKernel((const void*)k, dim3(grid), dim3(NT), args, LDS_BYTES, st);
 }
 
-// the grid the executor sizes the slabs for: one block per CU (capped by the tile count)
+// one block per CU (capped by the tile count), less the reserved CUs; the executor sizes the
+// slabs with it at construction and launches min(that, this) per step
 int lenet_bwd_blocks(int B) {
-  const int res = lenet_bwd_grid();
-  if (res <= 0) return -1;
+  int per = 1;
+  const int full = lenet_bwd_grid(&per);
+  if (full <= 0) return -1;
+  const int res = reserve_cut(full, per);
   const int ntiles = (B + T - 1) / T;
   return cap_grid(ntiles < res ? ntiles : res);
 }

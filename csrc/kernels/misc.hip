@@ -920,6 +920,9 @@ __global__ void cast_pad_k(const float* __restrict__ src, bf16_t* __restrict__ d
 static int g_grid_cap = 0;
 int grid_cap() { return g_grid_cap; }
 void set_grid_cap(int n) { g_grid_cap = n > 0 ? n : 0; }
+static int g_reserve_cus = 0;
+int reserve_cus() { return g_reserve_cus; }
+void set_reserve_cus(int n) { g_reserve_cus = n > 0 ? n : 0; }
 
 hipError_t perm_positions(int64_t* out, int64_t start, int n, int64_t N, uint32_t seed, int h, hipStream_t st,
                           const int32_t* lab_src, int32_t* lab_out) {

@@ -298,10 +298,10 @@ int g_skip = 0;
 
 void refc1_set_skip(int s) { g_skip = s; }
 
-int refc1_wgrad_grid() {
-  static int n = 0;
+int refc1_wgrad_grid(int* per_cu = nullptr) {
+  static int n = 0, per = 0;
   if (n == 0) {
-    int dev = 0, cus = 0, per = 0;
+    int dev = 0, cus = 0;
     for (Kern k : kRefc1)
       if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) != hipSuccess)
         return -1;
@@ -311,12 +311,15 @@ int refc1_wgrad_grid() {
       return -1;
     n = per * cus;
   }
+  if (per_cu) *per_cu = per;
   return n;
 }
 
 int refc1_wgrad_blocks(int B) {
-  const int res = refc1_wgrad_grid();
-  if (res <= 0) return -1;
+  int per = 1;
+  const int full = refc1_wgrad_grid(&per);
+  if (full <= 0) return -1;
+  const int res = reserve_cut(full, per);
   const int ntiles = (B + T - 1) / T;
   return cap_grid(ntiles < res ? ntiles : res);
 }

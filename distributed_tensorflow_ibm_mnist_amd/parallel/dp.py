@@ -13,24 +13,37 @@ Design for MI355X:
   finished bucket overlaps the backward of the layers below it.  For the
   reference CNN the 12.85 MB ``local3/weights`` gradient (92.7 % of the bytes)
   is ready after local3's wgrad and overlaps the whole conv backward;
-* every bucket except the last overlaps the backward still to run, so the cap is
-  small (bench/main default 0.125 MB): LeNet-5's 236 KB fc bucket is reduced
-  while conv2/conv1 backward (~80 % of backward time) runs, leaving a 10 KB
-  latency-bound conv bucket at the end; the reference CNN gets [softmax+local4]
-  0.8 MB, [local3] 12.85 MB (ring per-link bound on xGMI: ~2·7/8·S / 153 GB/s
-  ≈ 150 µs), [conv2], [conv1];
-* where the local3 all-reduce runs, reference CNN at the BASELINE batch
-  (B=16384/GPU, ``profiles/r3/dp_overlap/refcnn_b16384_step_timeline.txt``,
-  rocprofv3 kernel trace of a 2.47 ms step): the bucket is ready at 1.16 ms
-  (after the local3 wgrad GEMM + split-K reduce); 1.2 ms of backward follows.
-  The first 650 µs of it leave room for the RCCL kernel on every CU -- local3
-  dgrad is a 1600-workgroup GEMM (2 per CU, retiring in waves), lrn_pool_bwd
-  uses no LDS, conv2 wgrad is one 69 KB-LDS workgroup per CU -- and only then
-  does the conv2 dgrad halo kernel take 148 KB of each CU's 160 KB LDS for
-  315 µs.  A ~150 µs ring all-reduce therefore fits before the one kernel that
-  could lock it out, so no compute grid is capped.  Not yet measured: the ring
-  kernel's actual CU share on a multi-GPU node (a one-rank RCCL group issues no
-  kernel, so the one-GPU trace pins when the bucket is ready, not the contention);
+* whether an all-reduce issued mid-backward actually overlaps is a question of CU
+  residency, measured on one MI355X with an RCCL-footprint probe kernel launched on a
+  second stream while each persistent compute kernel runs (``bench/dp_coresidency.py``,
+  ``profiles/r5/dp_coresidency/``; first-block start as a fraction of the kernel):
+
+  ====================================  ===========  ===========  ==============
+  kernel (one resident wave)            probe 0 KB   16-32 KB     16-32 KB, R=8
+  ====================================  ===========  ===========  ==============
+  ``lenet_bwd_k`` (LeNet, 157 KB LDS)   0.14         0.94 (waits) 0.12
+  ``lenet_band_fwd_k``                  0.76 (waits) 0.81 (waits) 0.18
+  ``conv5_halo_k`` dgrad (ref conv2)    0.07         0.94 (waits) 0.06
+  ``conv5_halo_wgrad_k`` (ref conv2)    0.07         0.08         0.08
+  ``refc1_wgrad_k`` (ref conv1+norm1)   0.14         0.14         0.13
+  ====================================  ===========  ===========  ==============
+
+  so a collective that needs LDS cannot start beside the LeNet fused backward or the
+  reference CNN's conv2 dgrad, and starts at once when the persistent grids leave
+  ``R`` CUs free (``kernels.set_reserve_cus``: one per XCD);
+* bucket plan (``plan_buckets``): buckets close once they reach the cap (bench / CLI
+  default 0.125 MB) but never right before a CU-locking kernel (``HipNet.bucket_lockout``):
+  there the all-reduce could only start after it, so it would just add one more
+  latency-bound collective.  LeNet-5 (fused head + fused conv backward) therefore has ONE
+  246 KB bucket at the end of backward -- its gradient is latency-bound on xGMI either
+  way, and one collective is one latency -- and needs no reserve.  The reference CNN gets
+  [softmax+local4] 0.8 MB, [local3] 12.85 MB (ring per-link bound: ~2·7/8·S / 153 GB/s
+  ≈ 150 µs, issued after the local3 weight gradient with 1.2 ms of backward still to run)
+  and [conv2+conv1] at the end;
+* with world > 1 and more than one bucket, ``DataParallel`` reserves ``RESERVE_CUS`` = 8
+  CUs from the persistent kernels for the whole step so the early buckets' all-reduce
+  kernels are never locked out (cost per kernel: interleaved A/B in
+  ``profiles/r5/dp_coresidency/``); one GPU and one-bucket plans reserve nothing;
 * split-K weight-gradient reduces of a bucket's layers are flushed as ONE
   multi-tensor launch just before its all-reduce (``HipNet.hook_layers``);
 * ``work.wait()`` only makes the compute stream wait (no host block); the
@@ -58,9 +71,16 @@ class Bucket:
         return (self.end - self.start) * 4
 
 
-def plan_buckets(net, cap_bytes: int) -> List[Bucket]:
+def plan_buckets(net, cap_bytes: int, lockout: Optional[set] = None) -> List[Bucket]:
+    """Contiguous buckets in backward order, closed once they reach ``cap_bytes`` --
+    except at a layer in ``lockout`` (default ``net.bucket_lockout``): the backward
+    kernel right after that layer's grad-ready hook occupies every CU (a persistent,
+    LDS-filling kernel), so an all-reduce issued there could not start before it ends
+    and would only add one more latency-bound collective; the bucket grows on instead."""
     fp = net.fp
     spec = net.spec
+    if lockout is None:
+        lockout = set(getattr(net, "bucket_lockout", ()) or ())
     order = [i for i, L in enumerate(spec.layers) if isinstance(L, (Conv, Dense))]
     rng: Dict[int, tuple] = {}
     for i in order:
@@ -77,17 +97,25 @@ def plan_buckets(net, cap_bytes: int) -> List[Bucket]:
             assert e == cur.start, "parameter layout must be contiguous in layer order"
             cur.start = s
             cur.layers.append(i)
-        if cur.nbytes >= cap_bytes or k == len(order) - 1:
+        if (cur.nbytes >= cap_bytes and i not in lockout) or k == len(order) - 1:
             buckets.append(cur)
             cur = None
     return buckets
 
 
 class DataParallel:
+    # CUs the persistent compute kernels leave free while an early bucket's all-reduce may
+    # be in flight (one per XCD; kernels.set_reserve_cus)
+    RESERVE_CUS = 8
+
     def __init__(self, net, group=None, bucket_cap_mb: float = 1.0, overlap: bool = True,
-                 world: Optional[int] = None, force_collectives: bool = False):
+                 world: Optional[int] = None, force_collectives: bool = False,
+                 reserve_cus: Optional[int] = None):
         """``force_collectives``: issue the bucket all-reduces even with one rank (a
-        one-GPU rehearsal of the RCCL path, e.g. hipGraph capture of the DP step)."""
+        one-GPU rehearsal of the RCCL path, e.g. hipGraph capture of the DP step).
+        ``reserve_cus``: CUs kept free of the persistent kernels (None = auto:
+        RESERVE_CUS when world > 1 and some bucket is all-reduced before the backward
+        ends, else 0)."""
         self.net = net
         self.group = group
         if world is None:
@@ -96,6 +124,13 @@ class DataParallel:
         self.active = world > 1 or force_collectives
         self.buckets = plan_buckets(net, int(bucket_cap_mb * (1 << 20)))
         self.trigger = {b.layers[-1]: b for b in self.buckets}
+        if reserve_cus is None:
+            reserve_cus = self.RESERVE_CUS if (world > 1 and overlap and len(self.buckets) > 1) else 0
+        self.reserve_cus = int(reserve_cus)
+        dev = getattr(getattr(net, "fp", None), "params", None)
+        if dev is not None and dev.device.type == "cuda":
+            from ..ops._ext import kernels
+            kernels().set_reserve_cus(self.reserve_cus)
         self.pending: list = []
         self.overlap = overlap
         # comm_enabled = False skips the all-reduces (replicas drift apart): only for
@@ -201,7 +236,8 @@ class DataParallel:
         return {"cross_entropy": v[0], "accuracy": v[1], "total_loss": v[2]}
 
     def describe(self) -> str:
-        lines = [f"data parallel: world={self.world}, {len(self.buckets)} gradient bucket(s)"]
+        lines = [f"data parallel: world={self.world}, {len(self.buckets)} gradient bucket(s), "
+                 f"{self.reserve_cus} CU(s) reserved for collectives"]
         for k, b in enumerate(self.buckets):
             names = [self.net.spec.layers[i].name for i in b.layers]
             lines.append(f"  bucket {k}: {b.nbytes / 1e6:.3f} MB [{', '.join(names)}] -> RCCL all-reduce "

@@ -544,8 +544,26 @@ class HipNet:
         self.bwd_u8: Optional[torch.Tensor] = None    # uint8 twin of a bound bf16 dataset (bind_u8_input)
         if self.fused_bwd:
             res = kernels().lenet_bwd_blocks(batch)
+            self.lb_grid = res          # the slabs' partial count: per-step grids never exceed it
             self.lb_slab1 = torch.zeros(res * 32 * 8, dtype=torch.float32, device=dev)
             self.lb_slab2 = torch.zeros(res * 208 * 16, dtype=torch.float32, device=dev)
+
+    @property
+    def bucket_lockout(self) -> set:
+        """Spec indices of the layers after whose grad-ready hook the next backward kernel is a
+        persistent one-resident-wave kernel that takes every CU (measured: a collective-sized
+        probe on another stream does not start until it retires, bench/dp_coresidency.py,
+        profiles/r5/dp_coresidency/).  parallel/dp.plan_buckets never closes a bucket there.
+          * fused head + fused LeNet conv backward: the head already produced every data
+            gradient, so fc3's hook is followed directly by lenet_bwd_k;
+          * an interior conv layer: its data gradient (conv5_halo dgrad / convpool_dgrad)."""
+        out = set()
+        if self.head is not None and self.fused_bwd:
+            out.add(self.layers[self.head].idx)
+        for lay in self.layers[1:]:
+            if isinstance(lay, (ConvLayer, ConvPoolLayer)):
+                out.add(lay.idx)
+        return out
 
     def _find_c2d_c1w(self) -> bool:
         if self.device.type != "cuda" or len(self.layers) < 2:
@@ -666,7 +684,7 @@ class HipNet:
         fp = self.fp
         src = l0._src()
         K = kernels()
-        grid = K.lenet_bwd_blocks(nb)
+        grid = min(self.lb_grid, K.lenet_bwd_blocks(nb))   # less any CUs reserved for collectives
         x = src.get("u8", l0._xin())
         if self.bwd_u8 is not None and l0.use_u8 and "idx" in src:
             x = self.bwd_u8        # the uint8 copy of the bound bf16 dataset: half the bytes

@@ -126,6 +126,44 @@ def test_bucket_plan_default_cap():
         ["softmax_linear", "local4"], ["local3"], ["conv2"], ["conv1"]]
 
 
+def test_bucket_plan_lockout():
+    """A bucket is never closed where the next backward kernel takes every CU (HipNet.bucket_lockout):
+    LeNet-5 with the fused head + conv backward becomes ONE end-of-backward bucket, the reference
+    CNN keeps its early local3 bucket but folds conv2 into the final one."""
+    from distributed_tensorflow_ibm_mnist_amd.models import get_model, torch_ref
+    from distributed_tensorflow_ibm_mnist_amd.parallel.dp import plan_buckets
+    from distributed_tensorflow_ibm_mnist_amd.runtime.params import OptConfig
+    from distributed_tensorflow_ibm_mnist_amd.runtime.torchnet import TorchNet
+    cap = int(0.125 * (1 << 20))
+    spec = get_model("lenet5", 1)
+    net = TorchNet(spec, 2, "cpu", torch_ref.init_params(spec), OptConfig())
+    idx = {L.name: i for i, L in enumerate(spec.layers)}
+    b = plan_buckets(net, cap, lockout={idx["fc3"], idx["conv2"]})
+    assert len(b) == 1 and b[0].start == 0 and b[0].end == net.fp.total
+    net.bucket_lockout = {idx["fc3"], idx["conv2"]}       # what HipNet reports for this model
+    assert len(plan_buckets(net, cap)) == 1
+    spec = get_model("reference_cnn", 1)
+    net = TorchNet(spec, 2, "cpu", torch_ref.init_params(spec), OptConfig())
+    idx = {L.name: i for i, L in enumerate(spec.layers)}
+    b = plan_buckets(net, cap, lockout={idx["conv2"]})
+    assert [[spec.layers[i].name for i in bk.layers] for bk in b] == [
+        ["softmax_linear", "local4"], ["local3"], ["conv2", "conv1"]]
+
+
+def test_dp_reserve_policy():
+    """CUs are reserved for collectives only with several ranks AND an early bucket."""
+    from distributed_tensorflow_ibm_mnist_amd.models import get_model, torch_ref
+    from distributed_tensorflow_ibm_mnist_amd.parallel.dp import DataParallel
+    from distributed_tensorflow_ibm_mnist_amd.runtime.params import OptConfig
+    from distributed_tensorflow_ibm_mnist_amd.runtime.torchnet import TorchNet
+    spec = get_model("reference_cnn", 1)
+    net = TorchNet(spec, 2, "cpu", torch_ref.init_params(spec), OptConfig())
+    assert DataParallel(net, bucket_cap_mb=0.125, world=1).reserve_cus == 0
+    assert DataParallel(net, bucket_cap_mb=0.125, world=2).reserve_cus == DataParallel.RESERVE_CUS
+    assert DataParallel(net, bucket_cap_mb=64, world=2).reserve_cus == 0       # one bucket: nothing overlaps
+    assert DataParallel(net, bucket_cap_mb=0.125, world=2, reserve_cus=3).reserve_cus == 3
+
+
 def _spawn_main(args, log):
     env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONUNBUFFERED="1")
     return subprocess.Popen([sys.executable, os.path.join(ROOT, "main.py")] + args, cwd=ROOT, env=env,

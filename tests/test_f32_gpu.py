@@ -110,13 +110,17 @@ def test_f32_step_matches_oracle(dev, K, model, cin):
 @pytest.mark.parametrize("cin", [1, 3])
 def test_f32_step_matches_oracle_bench_batch(dev, K, cin):
     """The fp32 benchmark's own batch (reference CNN, B = 16384, the reference's
-    tf.float32: mnist_input.py:86,107), 1- and 3-channel input, at the same 1e-4: every
-    persistent kernel loops over many images per block and the split-K weight gradients
-    sum 16384 images in a different order than the oracle (fp32 reassociation only)."""
-    _f32_step_vs_oracle(dev, "reference_cnn", cin, 16384)
+    tf.float32: mnist_input.py:86,107), 1- and 3-channel input.  Every persistent kernel
+    loops over many images per block and the split-K weight gradients sum 16384 images in
+    another order than the oracle, so the bound is the larger of 1e-4 and 3x the oracle's
+    OWN fp32 reassociation floor: the same fp32 oracle run on the batch in reverse order
+    (identical math, other summation order).  At B = 16384 with random labels the
+    gradients at init cancel heavily over the batch (conv1/weights: a ~1e-3 floor measured
+    on MI355X, profiles/r5/start/), which 1e-4 at B = 96 does not see."""
+    _f32_step_vs_oracle(dev, "reference_cnn", cin, 16384, floor_check=True)
 
 
-def _f32_step_vs_oracle(dev, model, cin, B):
+def _f32_step_vs_oracle(dev, model, cin, B, floor_check=False):
     from distributed_tensorflow_ibm_mnist_amd.runtime.executor_f32 import HipNetF32
     torch.manual_seed(0)
     spec = get_model(model, cin)
@@ -134,9 +138,20 @@ def _f32_step_vs_oracle(dev, model, cin, B):
     assert rel_err(logits, ref_logits) < 1e-5
     ce = F.cross_entropy(ref_logits, y.long())
     ce.backward()
+    floor = {}
+    if floor_check:
+        q = {k: v.to(dev).float().requires_grad_(True) for k, v in init.items()}
+        rev = torch.arange(B - 1, -1, -1, device=dev)
+        ref_rev, _ = torch_ref.forward(spec, q, x[rev])
+        F.cross_entropy(ref_rev, y.long()[rev]).backward()
+        floor = {n: rel_err(q[n].grad, p[n].grad) for n in init}
+        del q, ref_rev
     for name in init:
         e = rel_err(net.fp.grad_view(name), p[name].grad)
-        assert e < 1e-4, f"{model} {name}: rel err {e:.3e}"
+        tol = max(1e-4, 3 * floor.get(name, 0.0))
+        print(f"{model} cin={cin} B={B} {name}: rel err {e:.3e} (oracle reassociation floor "
+              f"{floor.get(name, float('nan')):.3e}, bound {tol:.1e})")
+        assert e < tol, f"{model} {name}: rel err {e:.3e} >= {tol:.1e}"
     before = {n: net.fp.param_view(n).clone() for n in init}
     grads = {n: net.fp.grad_view(n).clone() for n in init}
     net.update()

@@ -24,8 +24,13 @@ DEV bf16_t f2bf(float f) {
 // uint8 pixel -> x/255 - 0.5 (mnist_input.py:37-39); fmaf so every kernel rounds identically
 DEV float u8_norm(uint32_t b) { return fmaf((float)b, 1.f / 255.f, -0.5f); }
 
+// Two floats -> a packed bf16 pair in ONE v_cvt_pk_bf16_f32 (RNE, bitwise the two f2bf
+// conversions).  Packing two scalar conversions instead costs 4 VALU: hipcc converts each
+// value alone (v_cvt_pk_bf16_f32 v, x, 0) and merges with a shift and an SDWA or.
 DEV uint32_t pack2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  typedef __bf16 pk_bf16x2 __attribute__((ext_vector_type(2)));
+  typedef float pk_f32x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(pk_f32x2{lo, hi}, pk_bf16x2));
 }
 
 // 8 bf16 in a 16-byte vector: element j lives in word j/2, half j%2.

@@ -6,10 +6,6 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
-# the PyTorch oracles' MIOpen convolutions: take the first applicable solution instead of
-# benchmarking every one on each new shape (the B = 16384 fp32 oracle spent ~90 s in that
-# search); the algorithm does not change what an oracle computes beyond fp32 rounding
-os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
 
 
 def pytest_configure(config):

@@ -112,12 +112,12 @@ def test_f32_step_matches_oracle_bench_batch(dev, K, cin):
     """The fp32 benchmark's own batch (reference CNN, B = 16384, the reference's
     tf.float32: mnist_input.py:86,107), 1- and 3-channel input.  Every persistent kernel
     loops over many images per block and the split-K weight gradients sum 16384 images in
-    another order than the oracle, and every max-pool routes its window's gradient to an
-    argmax that fp32 rounding can flip at near-ties.  The bound is the larger of 1e-4 and 3x
-    the oracle's OWN fp32 floor: the same fp32 oracle (a) on the batch in reverse order and
-    (b) on the input moved by ~1 ulp.  At B = 16384 with random labels the gradients at
-    init cancel heavily over the batch, so a few flipped windows show (conv1/weights 1.2e-3
-    against a 4e-5 reassociation-only floor, profiles/r5/), which 1e-4 at B = 96 does not."""
+    another order than the oracle, and every max-pool / ReLU decision that fp32 rounding
+    flips at a near-tie moves a gradient contribution.  So both fp32 steps -- ours and
+    PyTorch's -- are compared with the exact (float64) gradients, and ours must be within
+    3x PyTorch's own error (or 1e-4).  At B = 16384 with random labels the gradients at init
+    cancel heavily over the batch and a few flipped decisions show: PyTorch's fp32 is
+    ~1e-3 from float64 on conv1/weights (profiles/r5/fp32/), which 1e-4 at B = 96 hides."""
     _f32_step_vs_oracle(dev, "reference_cnn", cin, 16384, floor_check=True)
 
 
@@ -141,27 +141,22 @@ def _f32_step_vs_oracle(dev, model, cin, B, floor_check=False):
     ce.backward()
     floor = {}
     if floor_check:
-        # (a) reassociation: the same oracle on the batch in reverse order
-        q = {k: v.to(dev).float().requires_grad_(True) for k, v in init.items()}
-        rev = torch.arange(B - 1, -1, -1, device=dev)
-        ref_rev, _ = torch_ref.forward(spec, q, x[rev])
-        F.cross_entropy(ref_rev, y.long()[rev]).backward()
-        floor = {n: rel_err(q[n].grad, p[n].grad) for n in init}
-        # (b) fp32 rounding of the forward: the oracle on the input moved by ~1 ulp.  The
-        # max-pools route each window's gradient to its argmax, and a 1-ulp change of a
-        # near-tie flips the winner: a discrete effect no summation order shows
-        q = {k: v.to(dev).float().requires_grad_(True) for k, v in init.items()}
-        g = torch.Generator(device=dev).manual_seed(5)
-        xp = x * (1.0 + 2.0 ** -23 * torch.randn(x.shape, device=dev, generator=g))
-        ref_p, _ = torch_ref.forward(spec, q, xp)
-        F.cross_entropy(ref_p, y.long()).backward()
-        floor = {n: max(floor[n], rel_err(q[n].grad, p[n].grad)) for n in init}
-        del q, ref_rev, ref_p
+        # the exact gradients (float64 oracle) and how far PyTorch's OWN fp32 step is from
+        # them: every max-pool / ReLU decision that fp32 rounding flips at a near-tie moves a
+        # gradient contribution, a discrete effect no tolerance on rounding noise covers
+        q = {k: v.to(dev).double().requires_grad_(True) for k, v in init.items()}
+        ref64, _ = torch_ref.forward(spec, q, x.double())
+        F.cross_entropy(ref64, y.long()).backward()
+        exact = {n: q[n].grad for n in init}
+        floor = {n: rel_err(p[n].grad, exact[n]) for n in init}
+        del q, ref64
+    else:
+        exact = {n: p[n].grad for n in init}
     bad = []
     for name in init:
-        e = rel_err(net.fp.grad_view(name), p[name].grad)
+        e = rel_err(net.fp.grad_view(name), exact[name])
         tol = max(1e-4, 3 * floor.get(name, 0.0))
-        print(f"{model} cin={cin} B={B} {name}: rel err {e:.3e} (oracle fp32 floor "
+        print(f"{model} cin={cin} B={B} {name}: rel err {e:.3e} (PyTorch fp32 vs float64: "
               f"{floor.get(name, float('nan')):.3e}, bound {tol:.1e})")
         if not e < tol:
             bad.append(f"{name}: rel err {e:.3e} >= {tol:.1e}")

@@ -67,6 +67,14 @@ DEV void pow_beta(float sc, float beta, float& pw, float& pw1) {
   }
 }
 
+// The contractable spots of the LRN math are written as explicit fmaf: every kernel that
+// inlines these helpers (lrn_*_k, lrn_pool_*_k, the staging folds) then rounds identically,
+// whatever hipcc's fp-contract would fuse in each context (the fused-vs-two-step bitwise tests)
+DEV float lrn_scale(float s, float bias, float alpha) { return fmaf(alpha, s, bias); }
+DEV float lrn_out(float v, float s, float bias, float alpha, float beta) {
+  return v * powp(lrn_scale(s, bias, alpha), -beta);
+}
+
 DEV void unpack8(const u32x4& u, float (&v)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = u4_get(u, j);
@@ -85,8 +93,8 @@ DEV u32x4 lrn_fwd8(const u32x4& xv, int c8, float bias, float alpha, float beta)
   u32x4 o;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const float a = v[2 * j] * powp(bias + alpha * s[2 * j], -beta);
-    const float b = v[2 * j + 1] * powp(bias + alpha * s[2 * j + 1], -beta);
+    const float a = lrn_out(v[2 * j], s[2 * j], bias, alpha, beta);
+    const float b = lrn_out(v[2 * j + 1], s[2 * j + 1], bias, alpha, beta);
     o[j] = pack2(a, b);
   }
   return o;
@@ -96,22 +104,22 @@ DEV u32x4 lrn_fwd8(const u32x4& xv, int c8, float bias, float alpha, float beta)
 // dx[c] = g[c] s[c]^-b - 2ab x[c] sum_{|c'-c|<=R} g[c'] x[c'] s[c']^(-b-1), s = bias +
 // alpha * window sum of x^2; relu_mask zeroes dx where x <= 0.  Rounded to bf16.
 template <int G, int R, bool B075 = false>
-DEV u32x4 lrn_bwd8(const u32x4& xv, const u32x4& gv, int c8, float bias, float alpha, float beta, int relu_mask) {
-  float v[8], g[8], w[8], s[8], u[8];
-  unpack8(xv, v);
-  unpack8(gv, g);
+DEV u32x4 lrn_bwd8_vals(const float (&v)[8], const float (&g)[8], int c8, float bias, float alpha, float beta,
+                        int relu_mask) {
+  float w[8], s[8], u[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) w[j] = v[j] * v[j];
   lane_window_sums<G, R>(w, c8, s);             // s = window sum of x^2
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float sc = bias + alpha * s[j];
+    const float sc = lrn_scale(s[j], bias, alpha);
     float pw, pw1;                                  // sc^-beta, sc^-(beta+1)
     pow_beta<B075>(sc, beta, pw, pw1);
     s[j] = pw;
     w[j] = g[j] * v[j] * pw1;
   }
   lane_window_sums<G, R>(w, c8, u);
+  const float k = 2.f * alpha * beta;
   u32x4 o;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -119,13 +127,20 @@ DEV u32x4 lrn_bwd8(const u32x4& xv, const u32x4& gv, int c8, float bias, float a
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int c = 2 * j + h;
-      float d = g[c] * s[c] - 2.f * alpha * beta * v[c] * u[c];
+      float d = fmaf(g[c], s[c], -((k * v[c]) * u[c]));
       if (relu_mask && !(v[c] > 0.f)) d = 0.f;
       r2[h] = d;
     }
     o[j] = pack2(r2[0], r2[1]);
   }
   return o;
+}
+template <int G, int R, bool B075 = false>
+DEV u32x4 lrn_bwd8(const u32x4& xv, const u32x4& gv, int c8, float bias, float alpha, float beta, int relu_mask) {
+  float v[8], g[8];
+  unpack8(xv, v);
+  unpack8(gv, g);
+  return lrn_bwd8_vals<G, R, B075>(v, g, c8, bias, alpha, beta, relu_mask);
 }
 
 }  // namespace

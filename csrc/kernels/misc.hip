@@ -345,7 +345,7 @@ __global__ __launch_bounds__(TPB) void lrn_pool_fwd_k(const bf16_t* __restrict__
         lane_window_sums<G, R>(sq, c8, s);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float f = bf2f(f2bf(v[j] * powp(bias + alpha * s[j], -beta)));
+          const float f = bf2f(f2bf(lrn_out(v[j], s[j], bias, alpha, beta)));
           if (f > best[j]) { best[j] = f; bi[j] = d; }
         }
       }
@@ -395,38 +395,14 @@ __global__ __launch_bounds__(TPB) void lrn_pool_bwd_k(const bf16_t* __restrict__
     for (int d = 0; d < 4; ++d) {
       const int ih = 2 * oh + (d >> 1), iw = 2 * ow + (d & 1);
       const int64_t xoff = ((n * H + ih) * W + iw) * C + c8 * 8;
-      const u32x4 xv = xq[d];
-      float v[8], g[8], w[8], s[8], u[8];
-      unpack8(xv, v);
+      float v[8], g[8];
+      unpack8(xq[d], v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const uint32_t aj = ((j < 4 ? av[0] : av[1]) >> (8 * (j & 3))) & 0xffu;
         g[j] = aj == (uint32_t)d ? pg[j] : 0.f;          // max-unpool
-        w[j] = v[j] * v[j];
       }
-      lane_window_sums<G, R>(w, c8, s);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float sc = bias + alpha * s[j];
-        float pw, pw1;                                // sc^-beta, sc^-(beta+1) (lrn_math.h)
-        pow_beta<B075>(sc, beta, pw, pw1);
-        s[j] = pw;
-        w[j] = g[j] * v[j] * pw1;
-      }
-      lane_window_sums<G, R>(w, c8, u);
-      u32x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float r2[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int c = 2 * j + h;
-          float dd = g[c] * s[c] - 2.f * alpha * beta * v[c] * u[c];
-          if (relu_mask && !(v[c] > 0.f)) dd = 0.f;
-          r2[h] = dd;
-        }
-        o[j] = pack2(r2[0], r2[1]);
-      }
+      const u32x4 o = lrn_bwd8_vals<G, R, B075>(v, g, c8, bias, alpha, beta, relu_mask);
       if (ok) *(u32x4*)(dx + xoff) = o;
     }
   }

@@ -36,7 +36,7 @@ def main():
     A1 = torch.empty(B, 14, 14, 4, dtype=torch.uint8, device=dev)
     P2 = torch.empty(B, 5, 5, 16, dtype=torch.bfloat16, device=dev)
     A2 = torch.empty(B, 5, 5, 16, dtype=torch.uint8, device=dev)
-    K.lenet_band_fwd(ds, w1, b1, 6, w2, b2, B, P2, A2, p1=P1, arg1=A1, idx=idx)
+    K.lenet_band_fwd(ds, w1, b1, 6, w2, b2, B, P2, A2, p1=P1, idx=idx)
     dP2 = (torch.randn(B, 400, device=dev) * 1e-3).to(torch.bfloat16)
     grid = K.lenet_bwd_blocks(B)
     s1 = torch.zeros(grid * 32 * 8, device=dev)
@@ -58,8 +58,8 @@ def main():
             best = min(best, e0.elapsed_time(e1) / iters * 1e3)
         return best
 
-    timeit(lambda: K.lenet_bwd(ds, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx), iters=200, reps=1)  # clocks up
-    fused = timeit(lambda: K.lenet_bwd(ds, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx))
+    timeit(lambda: K.lenet_bwd(ds, P1, dP2, A2, w2, B, s1, s2, grid, idx=idx), iters=200, reps=1)  # clocks up
+    fused = timeit(lambda: K.lenet_bwd(ds, P1, dP2, A2, w2, B, s1, s2, grid, idx=idx))
     # cold caches: a 1 GiB write between launches evicts the inputs from L2 / MALL (the in-step
     # situation is in between: the band forward wrote pool1 / codes shortly before)
     junk = torch.empty(256 * 1024 * 1024, dtype=torch.float32, device=dev)
@@ -68,7 +68,7 @@ def main():
         junk.fill_(1.0)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        K.lenet_bwd(ds, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx)
+        K.lenet_bwd(ds, P1, dP2, A2, w2, B, s1, s2, grid, idx=idx)
         e1.record()
         torch.cuda.synchronize()
         cold.append(e0.elapsed_time(e1) * 1e3)
@@ -82,29 +82,29 @@ def main():
             pre()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            K.lenet_bwd(ds, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx)
+            K.lenet_bwd(ds, P1, dP2, A2, w2, B, s1, s2, grid, idx=idx)
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1) * 1e3)
         return round(sorted(ts[2:])[len(ts[2:]) // 2], 1)
-    band_call = lambda: K.lenet_band_fwd(ds, w1, b1, 6, w2, b2, B, P2, A2, p1=P1, arg1=A1, idx=idx)
+    band_call = lambda: K.lenet_band_fwd(ds, w1, b1, 6, w2, b2, B, P2, A2, p1=P1, idx=idx)
     traffic = junk[: 38 * 1024 * 1024]
     after_band = seq_time(band_call)
     after_band_traffic = seq_time(lambda: (band_call(), traffic.fill_(2.0)))
     after_traffic = seq_time(lambda: traffic.fill_(3.0))
     del junk, traffic
     # the band forward (conv1 + pool1 + conv2 + pool2, pool1 / codes copied out) on the same box
-    band = timeit(lambda: K.lenet_band_fwd(ds, w1, b1, 6, w2, b2, B, P2, A2, p1=P1, arg1=A1, idx=idx))
+    band = timeit(lambda: K.lenet_band_fwd(ds, w1, b1, 6, w2, b2, B, P2, A2, p1=P1, idx=idx))
     # the input read as uint8 (half the bytes of the bf16 copy; normalised while staging)
     ds_u8 = torch.randint(0, 256, (n, 784), device=dev, dtype=torch.uint8)
-    fused_u8 = timeit(lambda: K.lenet_bwd(ds_u8, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx))
+    fused_u8 = timeit(lambda: K.lenet_bwd(ds_u8, P1, dP2, A2, w2, B, s1, s2, grid, idx=idx))
     # fixed vs per-tile cost: the same kernel over the first Bs images (grid stays 256 blocks
     # while Bs / 8 >= 256), 1 .. B/2048 tiles per block
     scaling = {}
     for Bs in (2048, 4096, 8192, 16384, 32768, B):
         if Bs <= B:
             gs = K.lenet_bwd_blocks(Bs)
-            scaling[Bs] = round(timeit(lambda: K.lenet_bwd(ds, P1, A1, dP2, A2, w2, Bs, s1, s2, gs, idx=idx)), 1)
+            scaling[Bs] = round(timeit(lambda: K.lenet_bwd(ds, P1, dP2, A2, w2, Bs, s1, s2, gs, idx=idx)), 1)
     # the split path: conv2 dgrad -> dP1 in HBM, conv2 / conv1 weight gradients
     dP1 = torch.empty(B, 14, 14, 8, dtype=torch.bfloat16, device=dev)
     g2 = K.convpool_wgrad_grid(8, 16, 5, 0, 14, 14)
@@ -120,11 +120,11 @@ def main():
     pr_buf = torch.zeros(8, dtype=torch.int64, device=dev)
     for sk in [int(v) for v in os.environ.get("SKIPS", "0,1,2,4,8,16,7,15").split(",")]:
         os.environ["MNISTX_BWD_SKIP"] = str(sk)
-        skip_us[sk] = round(timeit(lambda: K.lenet_bwd(ds, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx,
+        skip_us[sk] = round(timeit(lambda: K.lenet_bwd(ds, P1, dP2, A2, w2, B, s1, s2, grid, idx=idx,
                                                        prof=pr_buf)), 1)
     os.environ.pop("MNISTX_BWD_SKIP", None)
     prof = torch.zeros(8, dtype=torch.int64, device=dev)
-    K.lenet_bwd(ds, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx, prof=prof)
+    K.lenet_bwd(ds, P1, dP2, A2, w2, B, s1, s2, grid, idx=idx, prof=prof)
     torch.cuda.synchronize()
     pr = prof.tolist()
     tot = max(1, sum(pr))

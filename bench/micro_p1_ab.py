@@ -51,11 +51,11 @@ def main():
     def bwd(skip):
         def f():
             os.environ["MNISTX_BWD_SKIP"] = str(skip)
-            K.lenet_bwd(ds, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx, prof=pr)
+            K.lenet_bwd(ds, P1, dP2, A2, w2, B, s1, s2, grid, idx=idx, prof=pr)
         return f
 
     cases = {
-        "band_fwd_p1": lambda: K.lenet_band_fwd(ds, w1, b1, 6, w2, b2, B, P2, A2, p1=P1, arg1=A1, idx=idx),
+        "band_fwd_p1": lambda: K.lenet_band_fwd(ds, w1, b1, 6, w2, b2, B, P2, A2, p1=P1, idx=idx),
         "band_fwd_no_p1": lambda: K.lenet_band_fwd(ds, w1, b1, 6, w2, b2, B, P2, A2, idx=idx),
         "bwd_prof": bwd(0),
         "bwd_prof_skip_p1_loads": bwd(32),

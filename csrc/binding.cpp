@@ -787,12 +787,14 @@ void lenet_band_fwd(Tensor x, Tensor w1, Tensor b1, int64_t b1n, Tensor w2, Tens
   check(arg2, at::kByte, B * 400, "arg2");
   mnistx::bf16_t* pp1 = nullptr;
   uint8_t* pa1 = nullptr;
-  if (p1.has_value() && p1->defined()) {
-    TORCH_CHECK(arg1.has_value() && arg1->defined(), "p1 needs arg1");
+  if (p1.has_value() && p1->defined()) {   // with arg1: the convpool layouts; without: combined records
     check(*p1, at::kBFloat16, B * 14 * 14 * 8, "p1");
-    check(*arg1, at::kByte, B * 14 * 14 * 4, "arg1");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(p1->data_ptr()) % 16 == 0, "p1 must be 16-byte aligned");
     pp1 = BFm(*p1);
-    pa1 = P<uint8_t>(*arg1);
+    if (arg1.has_value() && arg1->defined()) {
+      check(*arg1, at::kByte, B * 14 * 14 * 4, "arg1");
+      pa1 = P<uint8_t>(*arg1);
+    }
   }
   unsigned long long* pr = nullptr;
   if (prof.has_value() && prof->defined()) {   // experiments: int64[4] clock sums
@@ -805,10 +807,11 @@ void lenet_band_fwd(Tensor x, Tensor w1, Tensor b1, int64_t b1n, Tensor w2, Tens
 }
 
 // LeNet-5 conv-stack backward as one kernel (lenet_bwd.hip): conv2 dgrad + both weight
-// gradients; x as for lenet_band_fwd (the forward's input), p1 / arg1 / arg2 from it, dp2 =
-// dL/d pool2 [B, 400].  slab1 [grid, 32, 8], slab2 [grid, 208, 16] (split-K partials).
-void lenet_bwd(Tensor x, Tensor p1, Tensor arg1, Tensor dp2, Tensor arg2, Tensor w2, int64_t B, Tensor slab1,
-               Tensor slab2, int64_t grid, optional<Tensor> idx, optional<Tensor> prof) {
+// gradients; x as for lenet_band_fwd (the forward's input), p1c (the combined pool1 records:
+// lenet_band_fwd with p1 and no arg1) / arg2 from it, dp2 = dL/d pool2 [B, 400].
+// slab1 [grid, 32, 8], slab2 [grid, 208, 16] (split-K partials).
+void lenet_bwd(Tensor x, Tensor p1, Tensor dp2, Tensor arg2, Tensor w2, int64_t B, Tensor slab1, Tensor slab2,
+               int64_t grid, optional<Tensor> idx, optional<Tensor> prof) {
   mnistx::XSrc src{nullptr, nullptr, nullptr, 0};
   if (x.scalar_type() == at::kByte) {
     check(x, at::kByte, 784, "x");
@@ -830,14 +833,12 @@ void lenet_bwd(Tensor x, Tensor p1, Tensor arg1, Tensor dp2, Tensor arg2, Tensor
   }
   TORCH_CHECK(B >= 1 && B * 196 * 16 < (int64_t)INT32_MAX, "B");
   check(p1, at::kBFloat16, B * 196 * 8, "p1");
-  check(arg1, at::kByte, B * 196 * 4, "arg1");
   check(dp2, at::kBFloat16, B * 400, "dp2");
   check(arg2, at::kByte, B * 400, "arg2");
   check(w2, at::kBFloat16, 5 * 5 * 8 * 16, "w2");
   for (const Tensor* t : {&p1, &dp2, &w2})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "p1 / dp2 / w2 must be 16-byte aligned");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(arg1.data_ptr()) % 4 == 0 && reinterpret_cast<uintptr_t>(arg2.data_ptr()) % 8 == 0,
-              "arg1 / arg2 alignment");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(arg2.data_ptr()) % 8 == 0, "arg2 alignment");
   const int res = mnistx::lenet_bwd_blocks((int)B);
   TORCH_CHECK(res > 0, "lenet_bwd: occupancy query failed");
   TORCH_CHECK(grid >= 1 && grid <= res, "lenet_bwd: grid must be in [1, ", res, "] (one block per CU, <= tiles)");
@@ -848,8 +849,8 @@ void lenet_bwd(Tensor x, Tensor p1, Tensor arg1, Tensor dp2, Tensor arg2, Tensor
     check(*prof, at::kLong, 8, "prof");
     pr = P<unsigned long long>(*prof);
   }
-  hip_ok(mnistx::lenet_bwd(src, BF(p1), P<const uint8_t>(arg1), BF(dp2), P<const uint8_t>(arg2), BF(w2), (int)B,
-                           P<float>(slab1), P<float>(slab2), (int)grid, cur_stream(), pr),
+  hip_ok(mnistx::lenet_bwd(src, BF(p1), BF(dp2), P<const uint8_t>(arg2), BF(w2), (int)B, P<float>(slab1),
+                           P<float>(slab2), (int)grid, cur_stream(), pr),
          "lenet_bwd");
 }
 
@@ -1248,7 +1249,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("lenet_band_fwd", &lenet_band_fwd, py::arg("x"), py::arg("w1"), py::arg("b1"), py::arg("b1n"),
         py::arg("w2"), py::arg("b2"), py::arg("B"), py::arg("p2"), py::arg("arg2"), py::arg("p1") = py::none(),
         py::arg("arg1") = py::none(), py::arg("idx") = py::none(), py::arg("prof") = py::none());
-  m.def("lenet_bwd", &lenet_bwd, py::arg("x"), py::arg("p1"), py::arg("arg1"), py::arg("dp2"), py::arg("arg2"),
+  m.def("lenet_bwd", &lenet_bwd, py::arg("x"), py::arg("p1"), py::arg("dp2"), py::arg("arg2"),
         py::arg("w2"), py::arg("B"), py::arg("slab1"), py::arg("slab2"), py::arg("grid"), py::arg("idx") = py::none(),
         py::arg("prof") = py::none());
   m.def("lenet_bwd_blocks", [](int64_t B) {

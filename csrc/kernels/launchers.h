@@ -126,10 +126,11 @@ hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const b
 // ---- lenet_bwd.hip: LeNet-5 conv-stack backward (conv2 dgrad + both weight gradients) as ONE
 // persistent kernel; slab1 [grid][32][8] (rows tap 0..24, bias 25), slab2 [grid][208][16]
 // (rows tap * 8 + ci, bias 200) -- the split-K partials splitk_reduce combines
+// p1c: the band forward's combined pool1 records [B][196] x 16 bytes (channels 0-5 bf16 + the
+// window's argmax code word; lenet_band_fwd with p1 and no arg1)
 int lenet_bwd_blocks(int B);         // the grid for a batch (one block per CU, <= tiles); <= 0: error
-hipError_t lenet_bwd(const XSrc& x, const bf16_t* p1, const uint8_t* arg1, const bf16_t* dp2, const uint8_t* arg2,
-                     const bf16_t* w2, int B, float* slab1, float* slab2, int grid, hipStream_t st,
-                     unsigned long long* prof = nullptr);
+hipError_t lenet_bwd(const XSrc& x, const bf16_t* p1c, const bf16_t* dp2, const uint8_t* arg2, const bf16_t* w2,
+                     int B, float* slab1, float* slab2, int grid, hipStream_t st, unsigned long long* prof = nullptr);
 
 // ---- refc1_wgrad.hip: reference-CNN conv1 weight gradient with the norm1 (LRN, radius 4, beta
 // 0.75) backward folded in: dn = dL/d norm1, p1 = pool1 (the LRN input), arg = pool1 codes (one
@@ -142,7 +143,8 @@ hipError_t refc1_wgrad(const XSrc& x, const bf16_t* dn, const bf16_t* p1, const 
 // ---- lenet_band.hip: LeNet-5 conv1+pool1+conv2+pool2 forward on banded MFMA tiles
 // (one persistent kernel; bf16 images only).  x.x = [n][784] images (x.idx: per-sample
 // rows, else sample b = row b).  p1/arg1 (convpool cfg-0 layouts) are written only when
-// p1 != nullptr; p2/arg2 use the convpool cfg-1 layouts.
+// p1 != nullptr; p1 without arg1 = the combined records lenet_bwd reads; p2/arg2 use the
+// convpool cfg-1 layouts.
 bool refc1_band_enabled();
 hipError_t refc1_band_fwd(const XSrc& x, const bf16_t* w, const float* b, int bn, int B, bf16_t* pooled,
                           uint8_t* arg, hipStream_t st);

@@ -104,7 +104,7 @@ struct BandFwd {
   const float* b2;        // [16]
   int B;
   bf16_t* p1;             // [B][14][14][8] pool1 (null: not written)
-  uint8_t* arg1;          // [B][196][4] packed codes (with p1)
+  uint8_t* arg1;          // [B][196][4] packed codes (with p1; null: p1 holds the combined records)
   bf16_t* p2;             // [B][5][5][16]
   uint8_t* arg2;          // [B][25][16]
   unsigned long long* prof;   // optional (experiments): per-role busy / barrier-wait clock sums
@@ -164,7 +164,12 @@ struct XFill {
 // Warp-specialised pipeline over the block's tiles k = 0..nk-1 (tile blockIdx + k * grid):
 // iteration k: conv1 waves turn input[k%2] into pool1[k%2] (and load tile k+1's input),
 // conv2 waves turn pool1[(k-1)%2] into pool2 -- one barrier per iteration, nk+1 iterations.
-template <bool P1OUT>
+// P1OUT: 0 = pool1 stays in LDS (eval / inference); 1 = pool1 [B][196][8] (channels 6-7 zero)
+// + codes [B][196][4], the convpool layouts; 2 = one 16-byte record per pool1 window,
+// channels 0-5 + the window's code word in the channel 6-7 slot -- the LDS record itself,
+// copied out with one store, and what lenet_bwd_k reads (20 -> 16 bytes per window: 51 MB
+// less written and read per step at B = 65536)
+template <int P1OUT>
 __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_X + LDS_P];
   bf16_t* xs = lds;
@@ -271,7 +276,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
           uint32_t cw = kc;
 #pragma unroll
           for (int i = 0; i < 3; ++i) {
-            if constexpr (P1OUT) {
+            if constexpr (P1OUT != 0) {
               const float v = vmax(vmax3(__uint_as_float(__float_as_uint(acc[i]) & ~3u), embed(acc[4 + i], 1u),
                                          embed(acc[8 + i], 2u)), embed(acc[12 + i], 3u));
               o[i] = vmax(__uint_as_float(__float_as_uint(v) & ~3u) + bias1[i], 0.f);
@@ -283,7 +288,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
           }
           const uint32_t w0 = pk2(o[0], o[1]);
           uint32_t w1;
-          if constexpr (P1OUT) {
+          if constexpr (P1OUT != 0) {
             const uint32_t X = h ? __float_as_uint(o[2]) : cw;
             const auto sw = __builtin_amdgcn_permlane32_swap(X, X, false, false);
             w1 = h ? (cw | sw[0]) : pk2(o[2], __uint_as_float(sw[1]));
@@ -351,7 +356,22 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
       const int t0 = tile0(k - 1), gi = t0 + img;
       const bool iv = gi < a.B;
       const bf16_t* pb = p1s + ((k - 1) & 1) * PBUF;
-      if constexpr (P1OUT) {          // pool1 + argmax codes to HBM for the backward kernels
+      if constexpr (P1OUT == 2) {     // combined pool1 / code records for lenet_bwd_k
+        if (cp_r < 196) {
+          const int nimg = min(BT, a.B - t0);
+          const auto rp1 = buf_rsrc(a.p1 + (int64_t)t0 * P1E, (uint32_t)nimg * (P1E * 2));
+          const bf16_t* src = pb + cp_lds;
+#pragma unroll
+          for (int i0 = 0; i0 < BT; i0 += 4) {
+            u32x4 cv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cv[i] = *(const u32x4*)(src + (i0 + i) * PIS);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              __builtin_amdgcn_raw_buffer_store_b128(cv[i], rp1, (uint32_t)cp_r * 16u, (i0 + i) * (P1E * 2), 0);
+          }
+        }
+      } else if constexpr (P1OUT == 1) {   // pool1 + argmax codes to HBM (convpool layouts)
         // copy thread ct owns pooled pixel ct (< 196) of every image of the tile: one LDS
         // offset per thread, image strides as instruction / scalar offsets (no per-element
         // index arithmetic).  ct is rotated so the wave with 4 conv2 units copies least.
@@ -438,7 +458,7 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
   }
 }
 
-template <bool P1OUT>
+template <int P1OUT>
 int fwd_grid(int ntiles) {
   static int per_cu = -1, cus = 0;
   if (per_cu < 0) {
@@ -622,8 +642,9 @@ hipError_t lenet_band_fwd(const XSrc& x, const bf16_t* w1, const float* b1, int 
     hipLaunchKernelGGL(ker, dim3(grid), dim3(NTH), 0, st, a);
     return hipSuccess;
   };
-  const hipError_t e = p1 ? go(lenet_band_fwd_k<true>, fwd_grid<true>(ntiles))
-                          : go(lenet_band_fwd_k<false>, fwd_grid<false>(ntiles));
+  const hipError_t e = !p1    ? go(lenet_band_fwd_k<0>, fwd_grid<0>(ntiles))
+                      : arg1 ? go(lenet_band_fwd_k<1>, fwd_grid<1>(ntiles))
+                             : go(lenet_band_fwd_k<2>, fwd_grid<2>(ntiles));
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }

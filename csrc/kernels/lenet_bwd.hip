@@ -88,8 +88,8 @@ struct BwdArgs {
   const uint8_t* u8;      // input images [n][784] uint8, normalised while staging (or null)
   const int64_t* idx;     // per-sample row of x / u8 (null: sample b is row b)
   int n;
-  const bf16_t* p1;       // pool1 [B][196][8] (channels 6, 7 zero)
-  const uint8_t* arg1;    // pool1 argmax codes [B][196] x 4 bytes: byte k = code(k) | code(k + 4) << 4
+  const bf16_t* p1;       // pool1 records [B][196] x 16 bytes: channels 0-5 bf16, then the window's
+                          // argmax code word (byte k = code(k) | code(k + 4) << 4) -- lenet_band.hip
   const bf16_t* dp2;      // dL/d pool2 [B][400] (NHWC 5x5x16)
   const uint8_t* arg2;    // pool2 argmax codes [B][400]
   const bf16_t* w2;       // conv2 weights [5][5][8][16]
@@ -116,11 +116,11 @@ static_assert(NW == 2 * T && 2 * 128 >= NWIN1 && 128 <= NWIN1, "staging: one wav
 template <bool U8, bool IDX>
 struct Stage {
   u32x2 x[NCH];           // input: 4 pixels per chunk (uint8: x[i][0])
-  uint32_t a1[NCH];       // pool1 argmax word per chunk
   u32x2 rowv;             // IDX: the batch-index entry of this wave's image, one tile ahead
   u32x4 dp;               // dL/dpool2: 8 channels of one pooled pixel (threads < 400)
   u32x2 c2;               // their argmax codes
-  u32x4 p1[NCH];          // pool1: one window (8 channels) per chunk
+  u32x4 p1[NCH];          // pool1 record: one window (channels 0-5 + its code word) per chunk; the
+                          // codes are read by store_xc at the NEXT loop top, after store_dy
 
   DEV static int img_of(int wave) { return wave >> 1; }
   DEV void load_row(const BwdArgs& a, int t0, int wave) {
@@ -142,18 +142,17 @@ struct Stage {
     constexpr uint32_t esz = U8 ? 1u : 2u;
     const void* xb = U8 ? (const void*)(a.u8 + (int64_t)row * 784) : (const void*)(a.x + (int64_t)row * 784);
     const auto rx = buf_rsrc(xb, ok ? 784u * esz : 0u);
-    const auto ra1 = buf_rsrc(a.arg1 + (int64_t)(ok ? t0 + img : 0) * NWIN1 * 4, ok ? NWIN1 * 4u : 0u);
     const int r = ln + 64 * (wave & 1);
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const uint32_t q = (uint32_t)(r + 128 * i);
       const uint32_t oob = q < NWIN1 ? 0u : BUF_OOB;
-      a1[i] = a.skip & 32 ? 0u : buf_b32(ra1, 4u * q + oob);   // (skip: prof experiments only)
       if constexpr (U8) x[i] = u32x2{buf_b32(rx, 4u * q + oob), 0u};
       else x[i] = buf_b64(rx, 8u * q + oob);
     }
   }
-  // input quads + argmax codes (read by the conv1 weight gradient)
+  // input quads + argmax codes (read by the conv1 weight gradient; the codes ride in the pool1
+  // records of this tile, still in p1 until load_dy fetches the next tile's)
   DEV void store_xc(uint8_t* lds, int wave, int ln) const {
     const int img = img_of(wave), r = ln + 64 * (wave & 1);
 #pragma unroll
@@ -169,7 +168,8 @@ struct Stage {
           hi = pack2(u8_norm((b >> 16) & 0xff), u8_norm(b >> 24));
         }
         *(u32x2*)(lds + X_OFF + img * X_IMG + (y + 2) * X_RS + (4 * k + 4) * 2) = u32x2{lo, hi};
-        const uint32_t l4 = a1[i] & 0x0f0f0f0fu, h4 = (a1[i] >> 4) & 0x0f0f0f0fu;   // codes c 0..3 / 4..7
+        const uint32_t a1 = p1[i][3];
+        const uint32_t l4 = a1 & 0x0f0f0f0fu, h4 = (a1 >> 4) & 0x0f0f0f0fu;   // codes c 0..3 / 4..7
         uint8_t* cd = lds + CD_OFF + img * D_IMG + yp * D_RS + xp * 16;   // 8-byte aligned rows
         *(u32x2*)cd = u32x2{bytes01(l4), bytes23(l4)};
         *(u32x2*)(cd + 8) = u32x2{bytes01(h4), bytes23(h4)};
@@ -205,7 +205,7 @@ struct Stage {
       const int q = r + 128 * i;
       if (i == 0 || q < NWIN1) {
         const int yp = (q * 147) >> 11, xp = q - 14 * yp;
-        const u32x4 v = {p1[i][0], p1[i][1], p1[i][2], p1[i][3] | 0x3f80u};
+        const u32x4 v = {p1[i][0], p1[i][1], p1[i][2], 0x3f80u};   // channel 6 = 1.0, 7 = 0
         *(u32x4*)(lds + P1_OFF + img * P1_IMG + yp * P1_RS + xp * 16) = v;
       }
     }
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
 #pragma unroll
   for (int t = 0; t < 3; ++t) acc1[t][0] = acc1[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   float db1[4] = {0.f, 0.f, 0.f, 0.f};
-  const auto rarg1 = buf_rsrc(a.arg1, (uint32_t)a.B * (NWIN1 * 4u));
+  const auto rcode = buf_rsrc(a.p1, (uint32_t)a.B * (NWIN1 * 16u));   // code words of the pool1 records
   const int du = dg_unit[wave];
   const int ks0 = c2_ks0[wave], ks1 = c2_ks1[wave];
   const int cs0 = c1_ks0[wave >> 1], cs1 = c1_ks1[wave >> 1];
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int w1 = orow * 14 + 2 * (u0 + u) + (g >> 1);
-        aw[u] = buf_b32(rarg1, t0 + img < a.B && u0 + u < 7 ? 4u * ((uint32_t)(t0 + img) * NWIN1 + w1) : BUF_OOB);
+        aw[u] = buf_b32(rcode, t0 + img < a.B && u0 + u < 7 ? 16u * ((uint32_t)(t0 + img) * NWIN1 + w1) + 12u : BUF_OOB);
       }
       // the next tile's input after this unit's code loads (vmcnt is in order)
       if (!(PROF && (a.skip & 8))) st.load_xc(a, tile0(k + 1), wave, ln);
@@ -542,14 +542,13 @@ int lenet_bwd_grid(int* per_cu = nullptr) {
   return n;
 }
 
-hipError_t lenet_bwd(const XSrc& x, const bf16_t* p1, const uint8_t* arg1, const bf16_t* dp2, const uint8_t* arg2,
-                     const bf16_t* w2, int B, float* slab1, float* slab2, int grid, hipStream_t st,
-                     unsigned long long* prof) {
+hipError_t lenet_bwd(const XSrc& x, const bf16_t* p1, const bf16_t* dp2, const uint8_t* arg2, const bf16_t* w2,
+                     int B, float* slab1, float* slab2, int grid, hipStream_t st, unsigned long long* prof) {
   if (B <= 0) return hipSuccess;
   if ((!x.x && !x.u8) || grid <= 0) return hipErrorInvalidValue;
   const int res = lenet_bwd_grid();
   if (res <= 0) return hipErrorInvalidValue;
-  BwdArgs a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, p1, arg1, dp2, arg2, w2, B, slab1, slab2, prof, 0};
+  BwdArgs a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, p1, dp2, arg2, w2, B, slab1, slab2, prof, 0};
   if (prof) {   // experiments only: skip bits 1 dgrad, 2 conv2 wgrad, 4 conv1 wgrad, 8 staging, 16 loop
                 // barriers, 32 pool1 / code loads
     const char* e = getenv("MNISTX_BWD_SKIP");

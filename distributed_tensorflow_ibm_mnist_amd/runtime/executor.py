@@ -672,9 +672,11 @@ class HipNet:
         l0, l1 = self.layers[0], self.layers[1]
         fp = self.fp
         src = l0._src()   # {} (x0) | {"idx"} (bf16 dataset = _xin()) | {"u8", "idx"} (uint8 dataset)
+        # for the fused backward: ONE 16-byte record per pool1 window (channels 0-5 + the code
+        # word, lenet_band.hip P1OUT 2) in l0.out; the unfused backward reads the convpool layouts
         kernels().lenet_band_fwd(src.get("u8", l0._xin()), fp.bf16_view(l0.wname), fp.param_view(l0.bname), l0.spec.cout,
                                  fp.bf16_view(l1.wname), fp.param_view(l1.bname), nb, l1.out, l1.arg,
-                                 p1=l0.out, arg1=l0.arg, idx=src.get("idx"))
+                                 p1=l0.out, arg1=None if self.fused_bwd else l0.arg, idx=src.get("idx"))
 
     def _fused_conv_backward(self, nb: int, dp2: torch.Tensor, pending: list) -> None:
         """LeNet-5 conv1+conv2 backward in one launch (lenet_bwd.hip) reading the band
@@ -688,7 +690,7 @@ class HipNet:
         x = src.get("u8", l0._xin())
         if self.bwd_u8 is not None and l0.use_u8 and "idx" in src:
             x = self.bwd_u8        # the uint8 copy of the bound bf16 dataset: half the bytes
-        K.lenet_bwd(x, l0.out, l0.arg, dp2, l1.arg, fp.bf16_view(l1.wname), nb,
+        K.lenet_bwd(x, l0.out, dp2, l1.arg, fp.bf16_view(l1.wname), nb,
                     self.lb_slab1, self.lb_slab2, grid, idx=src.get("idx"))
         _reduce(pending, self.lb_slab2, (grid, 208, 16, 25, 8, l1.spec.cin, l1.spec.cout, 200),
                 fp.grad_view(l1.wname), fp.grad_view(l1.bname))

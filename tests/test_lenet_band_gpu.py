@@ -36,6 +36,16 @@ def _unpack1(arg1):   # byte k = code(c = k) | code(c = k + 4) << 4
     return torch.cat([arg1 & 15, arg1 >> 4], dim=-1)
 
 
+def _combined(P1, A1):
+    """The fused backward's pool1 records (lenet_band.hip P1OUT 2): per window channels 0-5
+    of P1, then the window's 4-byte code word from A1 in the channel 6-7 slot."""
+    B = P1.shape[0]
+    c = P1.contiguous().clone()
+    cb = c.view(torch.uint8).view(B * 196, 16)
+    cb[:, 12:] = A1.contiguous().view(B * 196, 4)
+    return c
+
+
 def _band(K, x, w1, b1, w2, b2, B, idx=None, p1=True):
     dev = x.device
     P1 = torch.full((B, 14, 14, 8), 7.0, dtype=torch.bfloat16, device=dev)
@@ -126,3 +136,20 @@ def test_hipnet_band_step_matches_convpool(dev, K, monkeypatch):
     for a, b in zip(l_a, l_b):
         assert abs(a - b) < 2e-2 * max(1.0, abs(b)), (l_a, l_b)
     assert (p_a - p_b).abs().max().item() < 5e-3
+
+
+@pytest.mark.parametrize("B,cap", [(1, 0), (100, 0), (1000, 0), (333, 3)])
+def test_band_fwd_combined_records(dev, K, grid_cap, B, cap):
+    """p1 without arg1: one 16-byte record per pool1 window (what lenet_bwd reads) ==
+    the convpool-layout outputs recombined, bitwise; pool2 outputs unchanged."""
+    grid_cap(cap)
+    torch.manual_seed(B)
+    w1, b1, w2, b2 = _weights(dev)
+    x = (torch.rand(B, 28, 28, 1, device=dev) - 0.5).to(torch.bfloat16)
+    P1, A1, P2, A2 = _band(K, x, w1, b1, w2, b2, B)
+    R = torch.full((B, 14, 14, 8), 7.0, dtype=torch.bfloat16, device=dev)
+    Q2 = torch.empty_like(P2)
+    C2 = torch.empty_like(A2)
+    K.lenet_band_fwd(x, w1, b1, 6, w2, b2, B, Q2, C2, p1=R)
+    assert torch.equal(R.view(torch.uint8), _combined(P1, A1).view(torch.uint8))
+    assert torch.equal(Q2, P2) and torch.equal(C2, A2)

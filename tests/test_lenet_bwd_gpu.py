@@ -9,7 +9,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from test_lenet_band_gpu import _band, _weights
+from test_lenet_band_gpu import _band, _combined, _weights
 
 pytestmark = pytest.mark.gpu
 
@@ -47,7 +47,7 @@ def _fused(K, x, P1, A1, A2, dP2, w2, B, idx=None, xsrc=None):
     grid = K.lenet_bwd_blocks(B)
     s1 = torch.full((grid * 32 * 8,), float("nan"), device=x.device)
     s2 = torch.full((grid * 208 * 16,), float("nan"), device=x.device)
-    K.lenet_bwd(x if xsrc is None else xsrc, P1, A1, dP2, A2, w2, B, s1, s2, grid, idx=idx)
+    K.lenet_bwd(x if xsrc is None else xsrc, _combined(P1, A1), dP2, A2, w2, B, s1, s2, grid, idx=idx)
     dW1 = torch.empty(5, 5, 1, 6, device=x.device)
     db1 = torch.empty(6, device=x.device)
     dW2 = torch.empty(5, 5, 6, 16, device=x.device)

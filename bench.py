@@ -70,7 +70,10 @@ def parse():
     ap.add_argument("--mode", default="dp", choices=["dp", "ps"],
                     help="dp = synchronous data parallel (headline); ps = asynchronous parameter server: "
                          "rank 0 is the PS, ranks 1..N-1 are workers (BASELINE config '1 PS + 7 workers')")
-    ap.add_argument("--ps_transport", default="ipc", choices=["ipc", "host"],
+    ap.add_argument("--ps_no_compute", type=int, default=0,
+                    help="PS mode: workers push the same gradient back to back without computing a step -- "
+                         "the PS data plane's own capacity (ms per applied update), e.g. 7 workers on one GPU")
+    ap.add_argument("--ps_transport", default="ipc", choices=["shm", "ipc", "host"],
                     help="PS data plane: ipc = xGMI peer copies into PS-owned buffers; host = gloo, host-staged")
     ap.add_argument("--eager_steps", type=int, default=-1,
                     help="N=1 with a hipGraph: also time this many EAGER steps after the timed region "
@@ -170,8 +173,11 @@ def run_ps(args) -> int:
     if world < 2:
         print("[bench] --mode ps needs >= 2 ranks (torchrun --nproc-per-node N)", file=sys.stderr)
         return 2
-    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
-    torch.cuda.set_device(dev)
+    if rank == 0 and args.ps_transport == "shm":
+        dev = torch.device("cpu")             # the shm PS is a CPU task: it never opens the GPU
+    else:
+        dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+        torch.cuda.set_device(dev)
     dist.init_process_group("gloo")          # control plane; data moves on the PS transport
     spec = get_model(args.model, args.in_channels)
     init = init_params(spec, seed=args.seed)
@@ -197,7 +203,8 @@ def run_ps(args) -> int:
             "data": "synthetic 28x28x1 (on-device generated MNIST-like glyphs), random-init weights",
             "config": {"model": MODEL_LABEL[args.model], "per_worker_batch": args.batch,
                        "parallelism": f"ps1+w{nw}", "ps_transport": args.ps_transport,
-                       "gpus_visible": torch.cuda.device_count(), "optimizer": args.optimizer},
+                       "gpus_visible": torch.cuda.device_count(), "optimizer": args.optimizer,
+                       "ps_device": ps.device.type},
             "applied_per_worker": res["per_worker"], "global_step": res["global_step"],
             # PS host time per served message, by phase (whole run incl. warmup): idle = waiting
             # for a worker, apply = optimizer launch, reply = stage + sync + control answer
@@ -230,17 +237,20 @@ def run_ps(args) -> int:
 
         graph = None
         evs = []       # device time of the worker's own step (input + fwd/bwd), shared GPU included
+        if args.ps_no_compute:            # one real step: the gradient every push then re-sends
+            compute()
         while not client.stop:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-            loader.next()
-            if args.graph == 0:
-                compute()
-            elif graph is None:
-                from distributed_tensorflow_ibm_mnist_amd.runtime.graph import StepGraph
-                graph = StepGraph(compute, warmup=1)     # the warm-up computes this step
-            else:
-                graph.replay()
+            if not args.ps_no_compute:
+                loader.next()
+                if args.graph == 0:
+                    compute()
+                elif graph is None:
+                    from distributed_tensorflow_ibm_mnist_amd.runtime.graph import StepGraph
+                    graph = StepGraph(compute, warmup=1)     # the warm-up computes this step
+                else:
+                    graph.replay()
             ev[1].record()
             if (graph is not None or args.graph == 0) and len(evs) < 4096:
                 evs.append(ev)

@@ -1155,6 +1155,12 @@ PYBIND11_MODULE(_kernels, m) {
   // test hook: cap every persistent kernel's grid (0 = off) so small-batch oracle tests run
   // the multi-iteration (several tiles per block) paths the benchmark batches run
   m.def("set_grid_cap", [](int64_t n) { mnistx::set_grid_cap((int)n); });
+  // pin / unpin host memory the caller mapped itself (the PS shm data plane's slots, so the
+  // worker's gradient / parameter copies are DMA, not staged through a bounce buffer)
+  m.def("host_register", [](uintptr_t addr, int64_t nbytes) {
+    return hipHostRegister((void*)addr, (size_t)nbytes, hipHostRegisterDefault) == hipSuccess;
+  });
+  m.def("host_unregister", [](uintptr_t addr) { return hipHostUnregister((void*)addr) == hipSuccess; });
   m.def("set_reserve_cus", [](int64_t n) { mnistx::set_reserve_cus((int)n); });
   m.def("reserve_cus", []() { return (int64_t)mnistx::reserve_cus(); });
   m.def("clock_mark", [](Tensor out, int64_t slot) {

@@ -3,6 +3,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "ps_shm.h"
 #include "runtime_core.h"
 
 namespace py = pybind11;
@@ -33,6 +34,51 @@ std::vector<std::pair<py::bytes, py::bytes>> parse_table(const std::string& file
   return out;
 }
 
+// parallel/ps.py ShmTransport: one ps_serve call (GIL released).  Pointers are raw
+// addresses (the segment mapping, and the contiguous CPU tensors / numpy arrays the PS owns).
+py::tuple ps_shm_serve(uintptr_t base, std::vector<int64_t> lay, uintptr_t params, uintptr_t mom, uintptr_t ema,
+                       uintptr_t wd, std::vector<double> opt, std::vector<int64_t> st, uintptr_t per_worker,
+                       uintptr_t last_seq, uintptr_t arrivals, int64_t arrivals_cap, uintptr_t mark_steps,
+                       uintptr_t mark_times, int nmarks, uintptr_t phase, double idle_timeout) {
+  if (lay.size() != 7 || opt.size() != 7 || st.size() != 7) throw std::invalid_argument("ps_shm_serve: bad tuple");
+  PsLayout L{lay[0], lay[1], lay[2], lay[3], lay[4], lay[5], lay[6]};
+  PsOpt o{opt[0], opt[1], (int64_t)opt[2], opt[3], (int)opt[4], (int)opt[5], opt[6]};
+  PsState S{};
+  S.gstep = st[0];
+  S.max_steps = st[1];
+  S.applied = st[2];
+  S.rejected = st[3];
+  S.kill_step = st[4];
+  S.narr = st[5];
+  S.last = (int)st[6];
+  S.per_worker = (int64_t*)per_worker;
+  S.last_seq = (int64_t*)last_seq;
+  S.arrivals = (int32_t*)arrivals;
+  S.arrivals_cap = arrivals_cap;
+  S.mark_steps = (const int64_t*)mark_steps;
+  S.mark_times = (double*)mark_times;
+  S.nmarks = nmarks;
+  double* ph = (double*)phase;
+  for (int i = 0; i < 3; ++i) S.phase[i] = ph[i];
+  S.idle_timeout = idle_timeout;
+  int who = -1, rc;
+  {
+    py::gil_scoped_release nogil;
+    rc = ps_serve((uint8_t*)base, L, (float*)params, (float*)mom, (float*)ema, (const float*)wd, o, S, &who);
+  }
+  for (int i = 0; i < 3; ++i) ph[i] = S.phase[i];
+  return py::make_tuple(rc, who, S.gstep, S.applied, S.rejected, S.narr, S.last);
+}
+
+// the same update alone (tests: bitwise runtime/torchnet.torch_update)
+void ps_apply_once(uintptr_t params, uintptr_t grads, uintptr_t mom, uintptr_t ema, uintptr_t wd, int64_t n,
+                   std::vector<double> opt, int64_t step) {
+  if (opt.size() != 7) throw std::invalid_argument("ps_apply_once: bad opt tuple");
+  PsOpt o{opt[0], opt[1], (int64_t)opt[2], opt[3], (int)opt[4], (int)opt[5], opt[6]};
+  py::gil_scoped_release nogil;
+  ps_apply((float*)params, (const float*)grads, (float*)mom, (float*)ema, (const float*)wd, n, o, step);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_host, m) {
@@ -54,6 +100,8 @@ PYBIND11_MODULE(_host, m) {
   m.def("sstable_build", [](const std::vector<std::pair<std::string, std::string>>& e) {
     return py::bytes(sstable_build(e));
   });
+  m.def("ps_shm_serve", &ps_shm_serve);
+  m.def("ps_apply_once", &ps_apply_once);
   m.def("sstable_parse", [](py::bytes b, bool verify) { return parse_table(std::string(b), verify); },
         py::arg("data"), py::arg("verify") = true);
 }

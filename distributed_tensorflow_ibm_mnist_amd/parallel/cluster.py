@@ -44,7 +44,7 @@ class Cluster:
     master: str = ""
     device: Optional[torch.device] = None
     backend: str = ""
-    transport: str = ""             # PS-mode data plane (ipc | host)
+    transport: str = ""             # PS-mode data plane (shm | ipc | host)
     store: Optional[object] = None  # PS mode: the chief-hosted TCPStore (survives PS restarts)
     gen: int = 0                    # PS mode: session generation of the current control group
     timeout: Optional[datetime.timedelta] = None
@@ -161,14 +161,17 @@ def setup_distribute(job_name: str = "", ps_hosts: str = "", worker_hosts: str =
             cl.backend = dp_backend
         if cl.mode == "ps":
             # PS mode: the process group is the gloo control plane; gradients and
-            # parameters move on the PS data plane (parallel/ps.py): xGMI peer copies
-            # ("ipc", default on GPU) or gloo messages staged through host ("host").
+            # parameters move on the PS data plane (parallel/ps.py): a CPU PS serving a
+            # shared-memory segment natively ("shm", one host), xGMI peer copies into a GPU
+            # PS ("ipc", default on GPU) or gloo messages staged through host ("host").
             cl.backend = "gloo"
-            t = {"": "", "gloo": "host", "host": "host", "ipc": "ipc"}.get(ps_backend)
+            t = {"": "", "gloo": "host", "host": "host", "ipc": "ipc", "shm": "shm"}.get(ps_backend)
             if t is None:
-                raise ValueError(f"--ps_backend={ps_backend!r}: expected ipc | host (gloo)")
+                raise ValueError(f"--ps_backend={ps_backend!r}: expected shm | ipc | host (gloo)")
             from .ps import default_transport
             cl.transport = t or default_transport(cl.device)
+            if cl.transport == "shm" and cl.job_name == "ps":
+                cl.device = torch.device("cpu")    # the shm PS is a CPU task: it never opens a GPU
         if cl.device.type == "cuda":
             torch.cuda.set_device(cl.device)
         cl.timeout = to

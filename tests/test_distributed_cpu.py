@@ -170,8 +170,10 @@ def _spawn_main(args, log):
                             stdout=open(log, "w"), stderr=subprocess.STDOUT)
 
 
-@pytest.mark.parametrize("num_ps,num_workers", [(1, 2), (2, 1)])
-def test_ps_mode_cli(tmp_path, num_ps, num_workers):
+@pytest.mark.parametrize("num_ps,num_workers,backend", [(1, 2, ""), (2, 1, ""), (1, 2, "shm"), (2, 2, "shm")])
+def test_ps_mode_cli(tmp_path, num_ps, num_workers, backend):
+    """backend shm: CPU parameter servers serving the gradient pushes natively from shared
+    memory (parallel/ps.py ShmTransport, csrc/host/ps_shm.h)."""
     base = free_port()
     ps_hosts = ",".join(f"localhost:{base + i}" for i in range(num_ps))
     wk_hosts = ",".join(f"localhost:{base + 100 + i}" for i in range(num_workers))
@@ -179,7 +181,7 @@ def test_ps_mode_cli(tmp_path, num_ps, num_workers):
     common = ["--impl=torch", "--cpu", "--model=mlp", "--in_channels=1", "--batch_size=32", "--max_steps=40",
               "--test_interval=20", "--log_step_count_steps=0", "--train_data=synthetic://1500",
               "--test_data=synthetic://300?seed=1", f"--train_dir={d}", f"--ps_hosts={ps_hosts}",
-              f"--worker_hosts={wk_hosts}", "--optimizer=momentum"]
+              f"--worker_hosts={wk_hosts}", "--optimizer=momentum"] + ([f"--ps_backend={backend}"] if backend else [])
     procs = []
     for j in range(num_ps):
         procs.append(("ps", j, _spawn_main(common + ["--job_name=ps", f"--task_id={j}"], tmp_path / f"ps{j}.log")))
@@ -199,6 +201,7 @@ def test_ps_mode_cli(tmp_path, num_ps, num_workers):
         assert p.returncode == 0, logs[f"{k}{i}"][-3000:]
     assert "applied 40 update(s)" in logs["ps0"]                   # exactly max_steps pushes applied
     assert "global_step 40" in logs["ps0"]
+    assert f"transport {backend or 'host'}" in logs["ps0"]
     assert "result: global_step=40" in logs["w0"]
     from distributed_tensorflow_ibm_mnist_amd.ckpt.bundle import read_index
     from distributed_tensorflow_ibm_mnist_amd.ckpt.saver import Saver, latest_checkpoint
@@ -329,6 +332,42 @@ def test_ps_async_arrival_order_slow_worker(tmp_path):
     assert "transport host" in logs["ps0"]
 
 
+@pytest.mark.parametrize("nesterov,ema", [(True, 0.9999), (False, -1.0)])
+def test_ps_native_apply_bitwise_torch_update(nesterov, ema):
+    """The shm PS's native update (csrc/host/ps_shm.h) is bitwise the reference-semantics
+    update (runtime/torchnet.torch_update): momentum / Nesterov, staircase LR decay, weight
+    decay and the EMA -- both single-threaded (LeNet) and threaded (reference CNN) shards."""
+    from distributed_tensorflow_ibm_mnist_amd import _host
+    from distributed_tensorflow_ibm_mnist_amd.models import get_model, torch_ref
+    from distributed_tensorflow_ibm_mnist_amd.runtime.params import FlatParams, OptConfig
+    from distributed_tensorflow_ibm_mnist_amd.runtime.torchnet import torch_update
+    from distributed_tensorflow_ibm_mnist_amd.train.trainer import param_specs
+    cfg = OptConfig(lr0=0.05, decay_rate=0.5, decay_steps=2, momentum=0.9, use_momentum=True, nesterov=nesterov,
+                    ema_max=ema)
+    opt = [cfg.lr0, cfg.decay_rate, float(cfg.decay_steps), cfg.momentum, float(cfg.nesterov),
+           float(cfg.use_momentum), cfg.ema_max]
+    for model in ("lenet5", "reference_cnn"):
+        spec = get_model(model, 1)
+        init = torch_ref.init_params(spec, seed=0)
+        a = FlatParams.build(param_specs(spec), init, "cpu", pads={})
+        b = FlatParams.build(param_specs(spec), init, "cpu", pads={})
+        wd = torch.zeros_like(a.params)
+        for e in a.entries:
+            if e.wd:
+                wd[e.off:e.off + e.n] = e.wd
+        g = torch.Generator().manual_seed(1)
+        for step in range(4):
+            gr = torch.randn(a.total, generator=g) * 0.01
+            a.grads.copy_(gr)
+            a.step.fill_(step)
+            torch_update(a, cfg, 1.0)
+            _host.ps_apply_once(b.params.data_ptr(), gr.data_ptr(), b.mom.data_ptr(), b.ema.data_ptr(),
+                                wd.data_ptr(), b.total, opt, step)
+        assert torch.equal(a.params, b.params) and torch.equal(a.mom, b.mom), model
+        if ema >= 0:
+            assert torch.equal(a.ema, b.ema), model
+
+
 def test_ps_push_stamp_helpers():
     """A push slot = the slice padded to an even length + an int64 stamp in its last 8 bytes."""
     from distributed_tensorflow_ibm_mnist_amd.parallel.ps import slot_len, stamp_view
@@ -340,10 +379,11 @@ def test_ps_push_stamp_helpers():
         assert int(stamp_view(slot)) == 123456789012 and slot[:n].abs().sum() == 0   # stamp never overlaps data
 
 
-def test_ps_corrupt_push_is_rejected_and_names_worker(tmp_path):
-    """Push integrity (host transport): worker 1's 5th push carries a wrong sequence
-    stamp (MNIST_FI_CORRUPT_PUSH=1:5); the PS rejects it BEFORE applying it and exits
-    non-zero naming that worker; the workers do not hang."""
+@pytest.mark.parametrize("backend", ["", "shm"])
+def test_ps_corrupt_push_is_rejected_and_names_worker(tmp_path, backend):
+    """Push integrity (host transport, and the shm data plane's native check): worker 1's
+    5th push carries a wrong sequence stamp (MNIST_FI_CORRUPT_PUSH=1:5); the PS rejects it
+    BEFORE applying it and exits non-zero naming that worker; the workers do not hang."""
     base = free_port()
     ps_hosts = f"localhost:{base}"
     wk_hosts = ",".join(f"localhost:{base + 100 + i}" for i in range(2))
@@ -352,7 +392,7 @@ def test_ps_corrupt_push_is_rejected_and_names_worker(tmp_path):
               "--test_interval=1000", "--log_step_count_steps=0", "--train_data=synthetic://600",
               "--test_data=synthetic://100?seed=1", f"--train_dir={d}", f"--ps_hosts={ps_hosts}",
               f"--worker_hosts={wk_hosts}", "--save_checkpoint_secs=0", "--eval_examples=100",
-              "--collective_timeout=60"]
+              "--collective_timeout=60"] + ([f"--ps_backend={backend}"] if backend else [])
     os.environ["MNIST_FI_CORRUPT_PUSH"] = "1:5"
     try:
         procs = [("ps0", _spawn_main(common + ["--job_name=ps", "--task_id=0"], tmp_path / "ps0.log"))]
@@ -371,9 +411,13 @@ def test_ps_corrupt_push_is_rejected_and_names_worker(tmp_path):
             pytest.fail(f"{name} hung:\n" + open(tmp_path / f"{name}.log").read()[-3000:])
     logs = {n: open(tmp_path / f"{n}.log").read() for n, _ in procs}
     assert procs[0][1].returncode != 0, logs["ps0"][-2000:]
-    assert "PushIntegrityError" in logs["ps0"] and "push from worker 1 carries stamp 1005" in logs["ps0"], \
-        logs["ps0"][-2000:]
-    assert "announced 5" in logs["ps0"]
+    if backend == "shm":
+        assert "PushIntegrityError" in logs["ps0"] and "push from worker 1 failed its sequence-stamp check" \
+            in logs["ps0"], logs["ps0"][-2000:]
+    else:
+        assert "PushIntegrityError" in logs["ps0"] and "push from worker 1 carries stamp 1005" in logs["ps0"], \
+            logs["ps0"][-2000:]
+        assert "announced 5" in logs["ps0"]
     for n, p in procs[1:]:
         assert p.returncode is not None            # no hang: the workers fail once the PS is gone
 
@@ -401,11 +445,11 @@ def test_ps_worker_weight_loss_terms():
     assert int(net.fp.step.item()) == 0
 
 
-def _sup_flags(d):
+def _sup_flags(d, backend=""):
     return ["--impl=torch", "--cpu", "--model=mlp", "--in_channels=1", "--batch_size=32", "--max_steps=40",
             "--test_interval=100", "--log_step_count_steps=0", "--train_data=synthetic://1500",
             "--test_data=synthetic://300?seed=1", f"--train_dir={d}", "--save_checkpoint_steps=5",
-            "--collective_timeout=60"]
+            "--collective_timeout=60"] + ([f"--ps_backend={backend}"] if backend else [])
 
 
 def test_ps_supervisor_restarts_after_ps_death(tmp_path):
@@ -433,8 +477,8 @@ def test_ps_supervisor_restarts_after_ps_death(tmp_path):
     assert latest_checkpoint(d).endswith("model.ckpt-40")
 
 
-@pytest.mark.parametrize("num_ps,kill_rank", [(1, 0), (2, 1)])
-def test_ps_session_recovery_in_place(tmp_path, num_ps, kill_rank):
+@pytest.mark.parametrize("num_ps,kill_rank,backend", [(1, 0, ""), (2, 1, ""), (1, 0, "shm"), (2, 1, "shm")])
+def test_ps_session_recovery_in_place(tmp_path, num_ps, kill_rank, backend):
     """In-place session recovery (MonitoredTrainingSession's, main.py:140-146): a PS is
     SIGKILLed at step 17; the supervisor relaunches ONLY that PS, which restores its
     shard from the last checkpoint and opens session generation 1; both workers (same
@@ -447,8 +491,8 @@ def test_ps_session_recovery_in_place(tmp_path, num_ps, kill_rank):
     msgs = []
     os.environ["MNIST_FI_KILL_RANK_AT_STEP"] = f"{kill_rank}:17"
     try:
-        rc = supervise(_sup_flags(d), num_ps=num_ps, num_workers=2, max_restarts=2, log_dir=logs, timeout_s=400,
-                       log=msgs.append)
+        rc = supervise(_sup_flags(d, backend), num_ps=num_ps, num_workers=2, max_restarts=2, log_dir=logs,
+                       timeout_s=400, log=msgs.append)
     finally:
         os.environ.pop("MNIST_FI_KILL_RANK_AT_STEP", None)
     read = lambda n: open(os.path.join(logs, n)).read()

@@ -63,7 +63,7 @@ def _launch(tmp_path, transport, num_ps=1, num_workers=2, max_steps=60):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("transport", ["ipc", "host"])
+@pytest.mark.parametrize("transport", ["ipc", "host", "shm"])
 def test_ps_mode_hip_workers_one_gpu(tmp_path, dev, transport):
     d, logs = _launch(tmp_path, transport)
     assert f"transport {transport}" in logs["ps0"]
@@ -113,10 +113,13 @@ def test_ps_transports_bitwise_equal_one_worker(dev):
 
 
 @pytest.mark.timeout(300)
-def test_bench_ps_mode_json(dev):
+@pytest.mark.parametrize("transport", ["ipc", "shm"])
+def test_bench_ps_mode_json(dev, transport):
+    """transport shm: the PS is a CPU task serving a shared-memory segment natively (it never
+    opens the GPU); the workers DMA to / from pinned slots."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.join(ROOT, "bench.py"),
-           "--mode", "ps", "--batch", "4096", "--steps", "10", "--warmup", "2"]
+           "--mode", "ps", "--batch", "4096", "--steps", "10", "--warmup", "2", "--ps_transport", transport]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240,
                        env=dict(os.environ, OMP_NUM_THREADS="2"))
     out = r.stdout + r.stderr
@@ -129,7 +132,8 @@ def test_bench_ps_mode_json(dev):
     # serve-loop phase split (host us per applied update)
     assert set(d["ps_us_per_msg"]) == {"idle", "apply", "reply"} and d["ps_us_per_msg"]["apply"] > 0
     # data plane per GRAD message, per worker: push / pull us and GB/s
-    assert len(d["ps_comm"]) == 2 and d["transport_used"] == "ipc"
+    assert len(d["ps_comm"]) == 2 and d["transport_used"] == transport
+    assert d["config"]["ps_device"] == ("cpu" if transport == "shm" else "cuda")
     for c in d["ps_comm"]:
         assert c["msgs"] >= 1 and c["push_us"] > 0 and c["push_GBps"] > 0 and c["pull_us"] > 0
         assert c["bytes_per_push"] >= c["bytes_per_pull"] > 0          # the push carries the 8-byte stamp

@@ -23,10 +23,14 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+MODEL, CIN = "lenet5", 1
+
+
 def run_cli(batch, steps, every):
+    cfg = "reference_cnn_synth.yaml" if MODEL == "reference_cnn" else "lenet5_synth.yaml"
     with tempfile.TemporaryDirectory() as d:
         cmd = [sys.executable, "-u", os.path.join(ROOT, "main.py"), f"--train_dir={d}",
-               f"--config={os.path.join(ROOT, 'configs', 'lenet5_synth.yaml')}", "--model=lenet5", "--in_channels=1",
+               f"--config={os.path.join(ROOT, 'configs', cfg)}", f"--model={MODEL}", f"--in_channels={CIN}",
                f"--batch_size={batch}", f"--max_steps={steps}", f"--test_interval={steps + 1}",
                f"--log_step_count_steps={every}"]
         out = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
@@ -44,7 +48,8 @@ def run_cli(batch, steps, every):
 
 def run_bench(batch):
     steps = "2000" if batch <= 1024 else "50"
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--batch", str(batch), "--steps", steps, "--warmup", "10"]
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--batch", str(batch), "--steps", steps, "--warmup", "10",
+           "--model", MODEL, "--in_channels", str(CIN)]
     if batch <= 1024:
         cmd += ["--graph", "1"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
@@ -58,9 +63,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps128", type=int, default=4000)
     ap.add_argument("--steps64k", type=int, default=400)
+    ap.add_argument("--model", default="lenet5")
+    ap.add_argument("--in_channels", type=int, default=1)
+    ap.add_argument("--big_batch", type=int, default=65536, help="the second batch (0 = only 128)")
     args = ap.parse_args()
+    global MODEL, CIN
+    MODEL, CIN = args.model, args.in_channels
     res = {}
-    for batch, steps, every in ((128, args.steps128, 500), (65536, args.steps64k, 50)):
+    runs = [(128, args.steps128, 500)] + ([(args.big_batch, args.steps64k, 50)] if args.big_batch else [])
+    for batch, steps, every in runs:
         cli = run_cli(batch, steps, every)
         b = run_bench(batch)
         cli["bench_ms_per_step"] = b["ms_per_step"]

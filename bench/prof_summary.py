@@ -1,6 +1,11 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 ``--kernel-trace --stats`` CSV directory: per-kernel
-time per training step, sorted.  Usage: prof_summary.py <dir> <steps> [out.md]"""
+time per training step, sorted.  Usage: prof_summary.py <dir> <steps> [out.md] [skip]
+
+``steps`` = every step the traced command ran (warmup included); the first ``skip`` step
+windows (warmup: clock ramp, first touches) are left out of the table, and the table ends
+with the traced wall span per kept step (first kept step's first kernel start to the last
+kernel's end), which is what the kernel sum is reconciled against."""
 import csv
 import glob
 import os
@@ -21,7 +26,7 @@ def short(name: str) -> str:
     return base + tmpl
 
 
-def step_windows(d: str, steps: int):
+def step_windows(d: str, steps: int, skip: int = 0):
     """Per-kernel (calls, total ns) inside the training steps, from the kernel trace:
     the step boundaries are the launches of the earliest kernel that runs exactly once per
     step; everything before the first boundary (dataset upload, buffer fills, clock
@@ -40,25 +45,32 @@ def step_windows(d: str, steps: int):
     if not once:
         return None
     k0 = min(once, key=lambda n: first[n])
-    t0 = first[k0]
+    bounds = [int(r["Start_Timestamp"]) for r in rows if r["Kernel_Name"] == k0]
+    t0 = bounds[min(skip, len(bounds) - 1)]
     agg: dict = {}
     setup_ns = 0
+    end = t0
     for r in rows:
         dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         if int(r["Start_Timestamp"]) < t0:
             setup_ns += dur
             continue
+        end = max(end, int(r["End_Timestamp"]))
         c, t = agg.get(r["Kernel_Name"], (0, 0))
         agg[r["Kernel_Name"]] = (c + 1, t + dur)
-    return agg, setup_ns
+    step_wall_ns = (end - t0) / max(1, steps - skip)
+    return agg, setup_ns, step_wall_ns
 
 
 def main():
     d, steps = sys.argv[1], int(sys.argv[2])
-    win = step_windows(d, steps)
+    skip = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+    win = step_windows(d, steps, skip)
+    wall_ns = None
     if win is not None:
-        agg, setup_ns = win
+        agg, setup_ns, wall_ns = win
         rows = [{"Name": n, "Calls": str(c), "TotalDurationNs": str(t), "AverageNs": str(t / c)} for n, (c, t) in agg.items()]
+        steps -= skip
     else:
         f = glob.glob(os.path.join(d, "*kernel_stats.csv"))[0]
         rows, setup_ns = list(csv.DictReader(open(f))), 0
@@ -71,6 +83,9 @@ def main():
         lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | "
                      f"{t/1e3/steps:.1f} | {100*t/tot:.1f}% |")
     lines.append(f"| **total GPU time / step** | | | **{tot/1e3/steps:.1f}** | |")
+    if wall_ns:
+        lines.append(f"| _traced wall span / step ({steps} steps after {skip} warmup; kernel sum / span "
+                     f"{tot / steps / wall_ns:.3f})_ | | | _{wall_ns/1e3:.1f}_ | |")
     if setup_ns:
         lines.append(f"| _setup before the first step (dataset upload, fills, prewarm): not in the total_ | | | "
                      f"_{setup_ns/1e3:.1f} us in all_ | |")

@@ -857,11 +857,14 @@ void lenet_bwd(Tensor x, Tensor p1, Tensor dp2, Tensor arg2, Tensor w2, int64_t 
 // Reference-CNN conv1 weight gradient with the norm1 backward folded in (refc1_wgrad.hip).
 // x / u8 / idx as for convpool_wgrad (cfg RefC1g); dn = dL/d norm1, p1 = pool1, arg = pool1 codes.
 void refc1_wgrad(Tensor x, Tensor dn, Tensor p1, Tensor arg, Tensor slab, int64_t grid, int64_t B, double lrn_bias,
-                 double lrn_alpha, double lrn_beta, optional<Tensor> u8, optional<Tensor> idx) {
-  const int cfg = mnistx::convpool_config(1, 32, 5, 2, 28, 28);
+                 double lrn_alpha, double lrn_beta, optional<Tensor> u8, optional<Tensor> idx, int64_t cin) {
+  TORCH_CHECK(cin == 1 || cin == 3, "refc1_wgrad: 1 or 3 input channels");
+  const int cfg = mnistx::convpool_config((int)cin, 32, 5, 2, 28, 28);
   TORCH_CHECK(cfg >= 0, "refc1_wgrad: no RefC1 geometry");
-  TORCH_CHECK(B >= 1 && B * 784 * 2 < (int64_t)INT32_MAX, "B: the batch (and its index) must stay < 2 GB");
-  const auto src = cp_src(x, u8, idx, cfg, B, 784);
+  TORCH_CHECK(B >= 1 && B * 784 * cin * 2 < (int64_t)INT32_MAX, "B: the batch (and its index) must stay < 2 GB");
+  TORCH_CHECK(cin == 1 || (!(u8.has_value() && u8->defined()) && !(idx.has_value() && idx->defined())),
+              "refc1_wgrad: 3 channels read the bf16 batch only");
+  const auto src = cp_src(x, u8, idx, cfg, B, 784 * cin);
   if (src.x) TORCH_CHECK(reinterpret_cast<uintptr_t>(src.x) % 8 == 0, "x must be 8-byte aligned");
   const int64_t np = B * 196 * 32;
   check(dn, at::kBFloat16, np, "dn");
@@ -874,9 +877,9 @@ void refc1_wgrad(Tensor x, Tensor dn, Tensor p1, Tensor arg, Tensor slab, int64_
   const int res = mnistx::refc1_wgrad_blocks((int)B);
   TORCH_CHECK(res > 0, "refc1_wgrad: occupancy query failed");
   TORCH_CHECK(grid >= 1 && grid <= res, "refc1_wgrad: grid must be in [1, ", res, "] (one block per CU, <= tiles)");
-  check(slab, at::kFloat, grid * 48 * 32, "slab");
+  check(slab, at::kFloat, grid * (cin == 1 ? 48 : 80) * 32, "slab");
   hip_ok(mnistx::refc1_wgrad(src, BF(dn), BF(p1), P<const uint8_t>(arg), (int)B, (float)lrn_bias, (float)lrn_alpha,
-                             (float)lrn_beta, P<float>(slab), (int)grid, cur_stream()),
+                             (float)lrn_beta, P<float>(slab), (int)grid, cur_stream(), (int)cin),
          "refc1_wgrad");
 }
 
@@ -1265,7 +1268,7 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.def("refc1_wgrad", &refc1_wgrad, py::arg("x"), py::arg("dn"), py::arg("p1"), py::arg("arg"), py::arg("slab"),
         py::arg("grid"), py::arg("B"), py::arg("lrn_bias"), py::arg("lrn_alpha"), py::arg("lrn_beta"),
-        py::arg("u8") = py::none(), py::arg("idx") = py::none());
+        py::arg("u8") = py::none(), py::arg("idx") = py::none(), py::arg("cin") = 1);
   m.def("refc1_set_skip", [](int64_t s) { mnistx::refc1_set_skip((int)s); });
   m.def("refc1_wgrad_blocks", [](int64_t B) {
     const int n = mnistx::refc1_wgrad_blocks((int)B);

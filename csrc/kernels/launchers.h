@@ -137,8 +137,9 @@ hipError_t lenet_bwd(const XSrc& x, const bf16_t* p1c, const bf16_t* dp2, const 
 // byte per channel), all [B][196][32].  slab [grid][48][32] in convpool_wgrad's RefC1g layout.
 int refc1_wgrad_blocks(int B);       // the grid for a batch (one block per CU, <= tiles); <= 0: error
 void refc1_set_skip(int s);          // experiments (bench/micro_refc1.py): parts of the kernel left out
+// cin 3: the bf16 NHWC batch only (x.x, no index); slab [grid][80][32] (convpool's Geo<3, 32> layout)
 hipError_t refc1_wgrad(const XSrc& x, const bf16_t* dn, const bf16_t* p1, const uint8_t* arg, int B, float bias,
-                       float alpha, float beta, float* slab, int grid, hipStream_t st);
+                       float alpha, float beta, float* slab, int grid, hipStream_t st, int cin = 1);
 
 // ---- lenet_band.hip: LeNet-5 conv1+pool1+conv2+pool2 forward on banded MFMA tiles
 // (one persistent kernel; bf16 images only).  x.x = [n][784] images (x.idx: per-sample

@@ -195,10 +195,14 @@ class ConvPoolLayer(_Layer):
     lrn_fold: Optional[tuple] = None
 
     def _refc1(self, ls) -> bool:
-        """The reference CNN's conv1 (28x28x1 -> 32, SAME) under norm1 (radius 4, beta 0.75):
-        refc1_wgrad replaces the folded convpool_wgrad (MNISTX_REFC1_WGRAD=0 keeps the latter)."""
-        return (self.C == 1 and self.Cp == 32 and self.spec.cout == 32 and self.pad == 2 and self.H == self.W == 28
-                and ls.depth_radius == 4 and float(ls.beta) == 0.75 and os.environ.get("MNISTX_REFC1_WGRAD", "1") != "0")
+        """The reference CNN's conv1 (28x28x1 or x3 -> 32, SAME) under norm1 (radius 4, beta
+        0.75): refc1_wgrad replaces the folded convpool_wgrad (MNISTX_REFC1_WGRAD=0 keeps the
+        latter).  3 channels (the reference's DLI records): the bf16 batch input only."""
+        if self.C == 3 and self._src():
+            return False
+        return (self.C in (1, 3) and self.Cp == 32 and self.spec.cout == 32 and self.pad == 2
+                and self.H == self.W == 28 and ls.depth_radius == 4 and float(ls.beta) == 0.75
+                and os.environ.get("MNISTX_REFC1_WGRAD", "1") != "0")
 
     def bwd_weight(self, nb: int, dy: torch.Tensor, slab: torch.Tensor, red: Optional[list] = None) -> None:
         K = kernels()
@@ -207,7 +211,7 @@ class ConvPoolLayer(_Layer):
             ls, dn = self.lrn_fold
             grid = min(self.grid, K.refc1_wgrad_blocks(nb))
             K.refc1_wgrad(self._xin(), dn, self.out, self.arg, slab, grid, nb, ls.bias, ls.alpha, ls.beta,
-                          **self._src())
+                          **self._src(), cin=self.C)
         elif self.lrn_fold is not None:
             ls, dn = self.lrn_fold
             grid = min(self.grid, max(1, (nb + 3) // 4))

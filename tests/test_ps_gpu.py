@@ -72,9 +72,11 @@ def test_ps_mode_hip_workers_one_gpu(tmp_path, dev, transport):
     assert int(m.group(1)) == 60 and int(m.group(2)) + int(m.group(3)) == 60
     assert min(int(m.group(2)), int(m.group(3))) > 0            # both workers contributed
     assert "result: global_step=60" in logs["worker0"]
-    # training made progress: the chief's held-out evaluations (Logger hook) improve
+    # training made progress: the chief's held-out evaluation (Logger hook) at the end.  Async:
+    # a fast worker can push the first 30+ updates before the chief's first step returns (graph
+    # capture), so the chief may see only the final crossing of test_interval
     accs = [float(a) for a in re.findall(r"test accuracy ([0-9.]+)", logs["worker0"])]
-    assert len(accs) >= 2 and accs[-1] > 0.3, accs
+    assert len(accs) >= 1 and accs[-1] > 0.3, accs
     from distributed_tensorflow_ibm_mnist_amd.ckpt.saver import Saver, latest_checkpoint
     p = latest_checkpoint(d)
     assert p.endswith("model.ckpt-60")

@@ -26,46 +26,49 @@ def _lrn_bwd_oracle(p, g, r=4):
     return x.grad
 
 
-def _setup(dev, K, B, seed):
+def _setup(dev, K, B, seed, cin=1):
     torch.manual_seed(seed)
-    x = (torch.rand(B, 28, 28, 1, device=dev) - 0.5).to(torch.bfloat16)
-    w = (torch.randn(5, 5, 1, 32, device=dev) * 0.2).to(torch.bfloat16)
+    x = (torch.rand(B, 28, 28, cin, device=dev) - 0.5).to(torch.bfloat16)
+    w = (torch.randn(5, 5, cin, 32, device=dev) * 0.2).to(torch.bfloat16)
     b = torch.randn(32, device=dev) * 0.05
     P1 = torch.empty(B, 14, 14, 32, dtype=torch.bfloat16, device=dev)
     A1 = torch.empty(B, 14, 14, 32, dtype=torch.uint8, device=dev)
-    K.convpool_fwd(x, w, b, 32, P1, A1, B, 1, 32, 5, 2, 28, 28)
+    K.convpool_fwd(x, w, b, 32, P1, A1, B, cin, 32, 5, 2, 28, 28)
     dn = (torch.randn(B, 14, 14, 32, device=dev) * 0.1).to(torch.bfloat16)
     return x, P1, A1, dn
 
 
-def _reduce(K, slab, grid, dev):
-    G, Ip, I, brow = K.convpool_reduce_args(1, 32, 5, 2, 28, 28, 1)
-    dw = torch.empty(5, 5, 1, 32, device=dev)
+def _reduce(K, slab, grid, dev, cin=1):
+    G, Ip, I, brow = K.convpool_reduce_args(cin, 32, 5, 2, 28, 28, cin)
+    dw = torch.empty(5, 5, cin, 32, device=dev)
     db = torch.empty(32, device=dev)
-    K.splitk_reduce(slab, grid, K.convpool_rows(1, 32, 5, 2, 28, 28), 32, G, Ip, I, 32, brow, dw, db, 1.0)
+    K.splitk_reduce(slab, grid, K.convpool_rows(cin, 32, 5, 2, 28, 28), 32, G, Ip, I, 32, brow, dw, db, 1.0)
     return dw, db
 
 
-def _refc1(K, x, P1, A1, dn, B, **src):
+def _refc1(K, x, P1, A1, dn, B, cin=1, **src):
     grid = K.refc1_wgrad_blocks(B)
-    slab = torch.full((grid * 48 * 32,), float("nan"), device=P1.device)
-    K.refc1_wgrad(x, dn, P1, A1, slab, grid, B, LRN["bias"], LRN["alpha"], LRN["beta"], **src)
-    return (*_reduce(K, slab, grid, P1.device), grid)
+    slab = torch.full((grid * (48 if cin == 1 else 80) * 32,), float("nan"), device=P1.device)
+    K.refc1_wgrad(x, dn, P1, A1, slab, grid, B, LRN["bias"], LRN["alpha"], LRN["beta"], **src, cin=cin)
+    return (*_reduce(K, slab, grid, P1.device, cin), grid)
 
 
-@pytest.mark.parametrize("B,cap", [(1, 0), (5, 0), (100, 0), (1000, 0), (333, 3), (77, 2), (4096, 7)])
-def test_refc1_wgrad_matches_oracle(dev, K, grid_cap, B, cap):
+@pytest.mark.parametrize("B,cap,cin", [(1, 0, 1), (5, 0, 1), (100, 0, 1), (1000, 0, 1), (333, 3, 1), (77, 2, 1),
+                                       (4096, 7, 1), (1, 0, 3), (100, 0, 3), (1000, 0, 3), (333, 3, 3),
+                                       (4096, 7, 3)])
+def test_refc1_wgrad_matches_oracle(dev, K, grid_cap, B, cap, cin):
     """cap > 0: few persistent blocks over many 4-image tiles (next tile prefetched, partial
-    last tile, accumulators carried) -- the benchmark path."""
+    last tile, accumulators carried) -- the benchmark path.  cin 3: the reference's
+    3-channel records (input planes de-interleaved while staging, the GEMM per plane)."""
     grid_cap(cap)
-    x, P1, A1, dn = _setup(dev, K, B, seed=B + cap)
-    dw, db, grid = _refc1(K, x, P1, A1, dn, B)
+    x, P1, A1, dn = _setup(dev, K, B, seed=B + cap, cin=cin)
+    dw, db, grid = _refc1(K, x, P1, A1, dn, B, cin=cin)
     if cap:
         assert grid == min(cap, (B + 3) // 4)
     dP1 = _lrn_bwd_oracle(P1, dn)
     dY = _unpool(dP1.to(torch.bfloat16), A1.long())                 # the kernel stages bf16 dP1
     g = dY.permute(0, 3, 1, 2)
-    want_w = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (32, 1, 5, 5), g, padding=2)
+    want_w = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (32, cin, 5, 5), g, padding=2)
     want_w = want_w.permute(2, 3, 1, 0)
     want_b = g.sum((0, 2, 3))
     assert torch.isfinite(dw).all() and torch.isfinite(db).all()

@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--mode", default="dp", choices=["dp", "ps"],
                     help="dp = synchronous data parallel (headline); ps = asynchronous parameter server: "
                          "rank 0 is the PS, ranks 1..N-1 are workers (BASELINE config '1 PS + 7 workers')")
+    ap.add_argument("--bwd_u8", type=int, default=1,
+                    help="--input bf16: the fused LeNet conv backward reads the uint8 twin of the dataset (half "
+                         "the bytes, normalised in the kernel) instead of the bf16 copy")
     ap.add_argument("--ps_no_compute", type=int, default=0,
                     help="PS mode: workers push the same gradient back to back without computing a step -- "
                          "the PS data plane's own capacity (ms per applied update), e.g. 7 workers on one GPU")
@@ -319,7 +322,7 @@ def main() -> int:
     mode = "u8" if args.fused_input else args.input
     fused_in = (args.impl == "hip" and mode != "prep" and getattr(net, "can_gather_input", lambda: True)()
                 and net.bind_u8_input(ds.images if mode == "u8" else ds.bf16_images(),
-                                       bwd_images=None if mode == "u8" else ds.images))
+                                       bwd_images=None if (mode == "u8" or not args.bwd_u8) else ds.images))
     loader = DeviceLoader(ds, net.x0, net.labels, rank=rank, world=world, seed=args.seed,
                           idx_out=net.idx_buf if fused_in else None)
 

@@ -118,10 +118,11 @@ int64_t dense_wgrad(Tensor x, Tensor dy, Tensor slab, int64_t Din, int64_t Dout,
   const int64_t M = Din + (with_bias ? 1 : 0);
   const int64_t S = eff_splits(B, splits);
   auto ep = make_slab(slab, S, M, Dout);
+  int used = (int)S;
   hip_ok(mnistx::dense_wgrad(BF(x), BF(dy), (int)Din, (int)Dout, (int)B, (int)ldx, (int)lddy, with_bias ? 1 : 0,
-                             (int)S, ep, cur_stream(), (int)tile),
+                             (int)S, ep, cur_stream(), (int)tile, &used),
          "dense_wgrad");
-  return S;
+  return used;   // the reduce sums exactly the partials written
 }
 
 // Split count the conv weight gradient prefers (slab sizing): the halo kernel's
@@ -1164,6 +1165,8 @@ PYBIND11_MODULE(_kernels, m) {
     return hipHostRegister((void*)addr, (size_t)nbytes, hipHostRegisterDefault) == hipSuccess;
   });
   m.def("host_unregister", [](uintptr_t addr) { return hipHostUnregister((void*)addr) == hipSuccess; });
+  m.def("set_gemm256", &mnistx::set_gemm256, "route the GEMMs that fill the GPU to gemm256.hip (A/B switch)");
+  m.def("gemm256_enabled", &mnistx::gemm256_enabled);
   m.def("set_reserve_cus", [](int64_t n) { mnistx::set_reserve_cus((int)n); });
   m.def("reserve_cus", []() { return (int64_t)mnistx::reserve_cus(); });
   m.def("clock_mark", [](Tensor out, int64_t slot) {

@@ -750,6 +750,7 @@ void gemm_tile(int M, int N, int wgrad, int* bm, int* bn) {
 
 hipError_t dense_fwd(const bf16_t* x, const bf16_t* w, int M, int N, int K, int ldx, int ldw,
                      const GemmEpi& ep, hipStream_t st) {
+  if (gemm256_ok(M, N, K, ep)) return gemm256_fwd(x, w, M, N, K, ldx, ldw, ep, st);
   MatLoader a{x, M, K, ldx, -1};
   MatLoader b{w, K, N, ldw, -1};
   return launch_pick<MatLoaderV, MatLoaderV, true, false>(a, b, ep, M, N, K, 1, st);
@@ -758,14 +759,32 @@ hipError_t dense_fwd(const bf16_t* x, const bf16_t* w, int M, int N, int K, int 
 hipError_t dense_dgrad(const bf16_t* dy, const bf16_t* w, int M, int N, int K, int lddy, int ldw,
                        const GemmEpi& ep, hipStream_t st) {
   // dX[M, N=Din] = dY[M, K=Dout] . W[Din, Dout]^T  ; B(k, n) = W[n][k]  (K-contiguous rows n)
+  if (gemm256_ok(M, N, K, ep)) return gemm256_dgrad(dy, w, M, N, K, lddy, ldw, ep, st);
   MatLoader a{dy, M, K, lddy, -1};
   MatLoader b{w, N, K, ldw, -1};
   return launch_pick<MatLoaderV, MatLoaderV, true, true>(a, b, ep, M, N, K, 1, st);
 }
 
 hipError_t dense_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int B, int ldx, int lddy,
-                       int with_bias, int splits, const GemmEpi& ep, hipStream_t st, int tile) {
+                       int with_bias, int splits, const GemmEpi& ep, hipStream_t st, int tile, int* used) {
   // slab[Din(+1), Dout] = X^T dY ; A(m=din, k=b) = X[b][din] ; B(k=b, n) = dY[b][n]
+  if (used) *used = splits;
+  if (tile < 0 && used) {
+    // the GEMMs that fill the GPU on 256 x 256 tiles: gemm256's own split count (one round
+    // of blocks), when the caller's slab holds that many partials
+    static int cus = 0;
+    if (cus == 0) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = -1;
+    }
+    const int s2 = cus > 0 ? gemm256_wgrad_splits(Din, Dout, B, with_bias, cus) : 0;
+    if (s2 > 0 && s2 <= splits) {
+      *used = s2;
+      return gemm256_wgrad(x, dy, Din, Dout, B, ldx, lddy, with_bias, s2, ep, st);
+    }
+  }
   MatLoader a{x, B, Din, ldx, with_bias ? Din : -1};
   MatLoader b{dy, B, Dout, lddy, -1};
   const int M = Din + (with_bias ? 1 : 0);

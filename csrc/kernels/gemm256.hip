@@ -1,0 +1,336 @@
+// Large dense GEMMs on 256 x 256 tiles with LDS-DMA staging, gfx950.
+//
+// The reference CNN's local3 layer (/root/reference/mnist_input.py:175-184: 16384 x 3136
+// -> 1024 at the BASELINE batch) is the one GEMM of the framework big enough to be bound by
+// the MFMA engine itself; the register-staged 256 x 128 x 32 tiles of gemm.hip run it at
+// ~0.75-0.9 PFLOP/s (MFMA busy ~33 %, profiles/r4/gemm_kc/).  This kernel is built the way
+// the CDNA4 playbook's large-GEMM recipe reads (cdna_hip_programming.md §5):
+//  * one 256 x 256 output tile per workgroup, 8 waves (2 along M x 4 along N), each wave
+//    128 x 64 = 8 x 4 v_mfma_f32_16x16x32_bf16 accumulators;
+//  * K steps of 64, staged global -> LDS by buffer_load_dwordx4 ... lds (no VGPR round trip,
+//    no ds_write pass; an out-of-range 16-byte chunk reads zeros through the descriptor's
+//    num_records, so tails need no branches), two LDS buffers (2 x 64 KB): the DMA of step
+//    t + 1 runs under the MFMAs of step t, one vmcnt(0) + barrier per step;
+//  * the LDS images are lane-linear (the DMA writes base + 16 lane), so the bank swizzle
+//    is applied to the per-lane GLOBAL source chunk and undone on the read (rule 21):
+//      K-contiguous operand  [256 rows][64 k]  (128 B rows): chunk c of row r at c ^ ((r >> 1) & 7)
+//                                              -> every ds_read_b128 lane group conflict-free
+//      MN-contiguous operand [64 k][256 cols]  (512 B rows): chunk c of row r at c ^ f(r),
+//                            f(r) = 2 (r & 1) + 4 ((r >> 1) & 1) + 8 ((r >> 3) & 1)
+//                                              -> every ds_read_b64_tr_b16 half-wave conflict-free
+//    (both searched exhaustively over XOR-of-row-bit swizzles with the gfx950 lane-group
+//    tables, bench/lds_gemm256.py);
+//  * fragments in natural k order (lane l: k = 8 (l >> 4) + j), read by one ds_read_b128
+//    (K-contiguous) or two ds_read_b64_tr_b16 (MN-contiguous) per fragment;
+//  * XCD-aware tile order (the column tiles of one row panel share an L2);
+//  * the epilogue of gemm.hip: bias / ReLU / ReLU-backward mask, bf16 or fp32 out, 16-byte
+//    stores staged through LDS per wave.
+// Operand orientations: forward (x K-contiguous, W [K][N] MN-contiguous) and data gradient
+// (dY and W both K-contiguous).  The weight gradient stays on gemm.hip's split-K engine.
+#include <cstdlib>
+
+#include "common.h"
+#include "launchers.h"
+
+namespace mnistx {
+namespace {
+
+constexpr int BM = 256, BN = 256, BKT = 64, NTH = 512;
+constexpr int WM = 2, WN = 4, TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+constexpr int IMG = BM * BKT * 2;          // bytes of one operand image (A and B alike: 32 KB)
+constexpr int BUF = 2 * IMG;               // one stage: A image then B image
+constexpr int LDS_BYTES = 2 * BUF;         // 128 KB: one workgroup per CU
+static_assert(BM == BN, "one image size for both operands");
+
+DEV int kc_swz(int r) { return (r >> 1) & 7; }
+DEV int mn_swz(int r) { return ((r & 1) << 1) | (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 3); }
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// One operand: KC = K-contiguous rows [R][K] (ld >= K), else MN-contiguous [K][R] (ld >= R).
+struct Opnd {
+  const bf16_t* p;
+  int ld, R, K;
+  uint32_t nbytes;
+};
+
+// One LDS-DMA instruction (16 bytes per lane to lds_dst + 16 lane) issued from inline asm:
+// through the builtin, hipcc sees an LDS write it cannot tell apart from the next step's
+// ds_reads and waits vmcnt(0) in front of them, which serialises the DMA of step t + 1 with
+// the MFMAs of step t.  Hidden in asm it is not counted by hipcc at all: the kernel drains
+// it with its own vmcnt(0) before the barrier that publishes the image.  M0 (the DMA's LDS
+// base) is compiler-reserved, so it is saved and restored inside the statement; s_nop 4
+// covers a descriptor fresh from readfirstlane (cdna_hip_programming.md §5.7).
+DEV void dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(lds_dst), "s"(rs)
+      : "memory");
+}
+
+// Stage the 64-deep K slab k0 (rows past kend: zeros) of rows / cols r0 .. r0 + 255 into the
+// image at byte offset img: 32 DMA instructions of 1 KB (8 KC rows or 2 MN rows each), 4 per wave.
+template <bool KC>
+DEV void stage(uint32_t lds_base, int img, const Opnd& o, int r0, int k0, int kend, int wave, int lane) {
+  const auto rs = buf_rsrc(o.p, o.nbytes);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = wave + 8 * u;                                 // DMA instruction of the image
+    uint32_t off;
+    if constexpr (KC) {
+      const int row = 8 * i + (lane >> 3), ch = (lane & 7) ^ kc_swz(row);
+      const int r = r0 + row, k = k0 + 8 * ch;
+      off = (r < o.R && k < kend) ? (uint32_t)(r * o.ld + k) * 2u : BUF_OOB;
+    } else {
+      const int row = 2 * i + (lane >> 5), ch = (lane & 31) ^ mn_swz(row);
+      const int k = k0 + row, c = r0 + 8 * ch;
+      off = (k < kend && c < o.R) ? (uint32_t)(k * o.ld + c) * 2u : BUF_OOB;
+    }
+    dma16(rs, off, (uint32_t)__builtin_amdgcn_readfirstlane(lds_base + img + 1024 * i));
+  }
+}
+
+// Fragment of rows / cols c0 .. c0 + 15 for k-half kh (k = 32 kh + 8 (lane >> 4) + j)
+template <bool KC>
+DEV bf16x8 frag(const uint8_t* lds, int img, int c0, int kh, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  if constexpr (KC) {
+    const int r = c0 + i, ch = (4 * kh + g) ^ kc_swz(r);
+    return __builtin_bit_cast(bf16x8, *(const u32x4*)(lds + img + r * 128 + 16 * ch));
+  } else {
+    const int q = (lane >> 2) & 3, p = lane & 3;
+    const int r = 32 * kh + 8 * g + q;                          // k rows r (j 0-3) and r + 4 (j 4-7)
+    const int cb = 2 * (c0 + 4 * p);                            // byte in the row before the swizzle
+    const int lo = r * 512 + 16 * ((cb >> 4) ^ mn_swz(r)) + (cb & 15);
+    const int hi = (r + 4) * 512 + 16 * ((cb >> 4) ^ mn_swz(r + 4)) + (cb & 15);
+    const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + img + lo));
+    const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + img + hi));
+    return join(a, b);
+  }
+}
+
+template <bool AKC, bool BKC, bool WG>
+__global__ __launch_bounds__(NTH, 1) void gemm256_k(const Opnd a, const Opnd b, const GemmEpi ep, int M, int N,
+                                                    int K, int tiles_n, int tiles_mn, int kchunk, int ones) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  // split-K (weight gradients): consecutive logical ids are the tiles of one split, which
+  // read the same K rows of both operands -- remapped onto one XCD's L2 (gemm.hip gemm_kernel)
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = WG ? lin / tiles_mn : 0, t = lin - split * tiles_mn;
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+  const int nk = (kend - kbeg + BKT - 1) / BKT;
+  // weight gradients: the A image column `ones` (Din, the bias row of the output) reads zeros
+  // from the DMA (past the operand); the lanes that staged its chunk write 1.0 over it
+  const bool has_ones = WG && ones >= m0 && ones < m0 + BM;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_void*)lds;
+  stage<AKC>(lds_base, 0, a, m0, kbeg, kend, wave, lane);
+  stage<BKC>(lds_base, IMG, b, n0, kbeg, kend, wave, lane);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = (kt & 1) * BUF;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (WG) {
+      if (has_ones) {   // this wave's own DMA chunks of the ones column (its vmcnt(0) above ordered them)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = wave + 8 * u, row = 2 * i + (lane >> 5), ch = (lane & 31) ^ mn_swz(row);
+          if (m0 + 8 * ch == ones && kbeg + kt * BKT + row < kend)
+            *(bf16_t*)(lds + cur + 1024 * i + 16 * lane) = (bf16_t)0x3f80;   // the lane's DMA slot
+        }
+      }
+    }
+    __syncthreads();   // step kt's images landed (every wave's DMA drained); step kt - 1's reads done
+    if (kt + 1 < nk) {
+      const int nxt = BUF - cur;
+      stage<AKC>(lds_base, nxt, a, m0, kbeg + (kt + 1) * BKT, kend, wave, lane);
+      stage<BKC>(lds_base, nxt + IMG, b, n0, kbeg + (kt + 1) * BKT, kend, wave, lane);
+    }
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = frag<BKC>(lds, cur + IMG, wn * TN + 16 * j, kh, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = frag<AKC>(lds, cur, wm * TM + 16 * i, kh, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();   // operand images dead: the epilogue reuses the LDS
+
+  // ---- epilogue (gemm.hip's vector path): a wave stages one 16-row fragment row of its
+  // 128 x 64 block, then every lane owns 8 consecutive columns of a row (2 vectors per lane)
+  const int g = lane >> 4, li = lane & 15;
+  constexpr int EP_LD = TN + 4, VI = 16 * (TN / 8) / 64;
+  float* eb = (float*)lds + wave * 16 * EP_LD;
+  float bv[VI][8];
+#pragma unroll
+  for (int k = 0; k < VI; ++k) {
+    const int v = lane + 64 * k, n = n0 + wn * TN + (v % (TN / 8)) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bv[k][e] = (ep.bias && n + e < ep.bias_n) ? ep.bias[n + e] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) eb[(4 * g + r) * EP_LD + j * 16 + li] = acc[i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int k = 0; k < VI; ++k) {
+      const int v = lane + 64 * k, rr = v / (TN / 8), cv = v % (TN / 8);
+      const int m = m0 + wm * TM + 16 * i + rr, n = n0 + wn * TN + 8 * cv;
+      if (m < M && n < N) {
+        const f32x4 lo = *(const f32x4*)(eb + rr * EP_LD + 8 * cv), hi = *(const f32x4*)(eb + rr * EP_LD + 8 * cv + 4);
+        if constexpr (WG) {   // split-K partial: this split's fp32 slab
+          float* o = (float*)ep.out + (int64_t)split * ep.slab_stride + (int64_t)m * ep.ldc + n;
+          *(f32x4*)o = lo;
+          *(f32x4*)(o + 4) = hi;
+          continue;
+        }
+        float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] += bv[k][e];
+        if (ep.relu)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] = fmaxf(x[e], 0.f);
+        if (ep.mask) {
+          const u32x4 mk = *(const u32x4*)(ep.mask + (int64_t)m * ep.ldm + n);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (!(u4_get(mk, e) > 0.f)) x[e] = 0.f;
+        }
+        if (ep.mode == EPI_F32) {
+          float* o = (float*)ep.out + (int64_t)m * ep.ldc + n;
+          *(f32x4*)o = f32x4{x[0], x[1], x[2], x[3]};
+          *(f32x4*)(o + 4) = f32x4{x[4], x[5], x[6], x[7]};
+        } else {
+          *(u32x4*)((bf16_t*)ep.out + (int64_t)m * ep.ldc + n) =
+              u32x4{pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(x[4], x[5]), pack2(x[6], x[7])};
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+template <bool AKC, bool BKC, bool WG>
+hipError_t launch256(const Opnd& a, const Opnd& b, const GemmEpi& ep, int M, int N, int K, int splits, int ones,
+                     hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)gemm256_k<AKC, BKC, WG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            LDS_BYTES) != hipSuccess)
+      return hipErrorInvalidValue;
+    attr = true;
+  }
+  const int tn = (N + BN - 1) / BN, tm = (M + BM - 1) / BM;
+  int kchunk = K;
+  if (WG) {   // the caller's split count (its slab is sized for it), chunks a multiple of the step
+    kchunk = ((K + splits - 1) / splits + BKT - 1) / BKT * BKT;
+    if ((K + kchunk - 1) / kchunk != splits) return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL((gemm256_k<AKC, BKC, WG>), dim3(tm * tn * (WG ? splits : 1)), dim3(NTH), LDS_BYTES, st, a, b, ep,
+                     M, N, K, tn, tm * tn, kchunk, ones);
+  return hipGetLastError();
+}
+
+bool sizes_ok(int64_t rows, int ld, int K, int R) {
+  return (ld & 7) == 0 && (K & 7) == 0 && (R & 7) == 0 && rows * ld * 2 < ((int64_t)1 << 31);
+}
+
+}  // namespace
+
+// Routing switch (A/B): MNISTX_GEMM256=0 starts with every dense GEMM on gemm.hip;
+// set_gemm256 flips it at run time (tests and benches compare both paths in one process).
+static int g_gemm256 = -1;
+bool gemm256_enabled() {
+  if (g_gemm256 < 0) {
+    const char* e = getenv("MNISTX_GEMM256");
+    g_gemm256 = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_gemm256 != 0;
+}
+void set_gemm256(bool on) { g_gemm256 = on ? 1 : 0; }
+
+// The 256 x 256 path takes a GEMM when it fills the GPU at least once (>= 256 tiles of a
+// mostly-full 256 x 256), the epilogue is a plain bf16 / fp32 store and every vector is whole.
+bool gemm256_ok(int M, int N, int K, const GemmEpi& ep) {
+  if (!gemm256_enabled() || ep.mode == EPI_SLAB || K < 2 * BKT) return false;
+  const int64_t tiles = (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const double fill = (double)M * N / ((double)tiles * BM * BN);
+  return tiles >= 256 && fill >= 0.9 && (N & 7) == 0 && (ep.ldc & 7) == 0 && ((uintptr_t)ep.out & 15) == 0 &&
+         (ep.mask == nullptr || ((ep.ldm & 7) == 0 && ((uintptr_t)ep.mask & 15) == 0));
+}
+
+// y[M, N] = x[M, K] . W[K, N]   (x K-contiguous, W MN-contiguous)
+hipError_t gemm256_fwd(const bf16_t* x, const bf16_t* w, int M, int N, int K, int ldx, int ldw, const GemmEpi& ep,
+                       hipStream_t st) {
+  if (!sizes_ok(M, ldx, K, 8) || !sizes_ok(K, ldw, 8, N)) return hipErrorInvalidValue;
+  const Opnd a{x, ldx, M, K, (uint32_t)((int64_t)M * ldx * 2)};
+  const Opnd b{w, ldw, N, K, (uint32_t)((int64_t)K * ldw * 2)};
+  return launch256<true, false, false>(a, b, ep, M, N, K, 1, -1, st);
+}
+
+// dX[M, N] = dY[M, K] . W[N, K]^T   (both K-contiguous)
+hipError_t gemm256_dgrad(const bf16_t* dy, const bf16_t* w, int M, int N, int K, int lddy, int ldw, const GemmEpi& ep,
+                         hipStream_t st) {
+  if (!sizes_ok(M, lddy, K, 8) || !sizes_ok(N, ldw, K, 8)) return hipErrorInvalidValue;
+  const Opnd a{dy, lddy, M, K, (uint32_t)((int64_t)M * lddy * 2)};
+  const Opnd b{w, ldw, N, K, (uint32_t)((int64_t)N * ldw * 2)};
+  return launch256<true, true, false>(a, b, ep, M, N, K, 1, -1, st);
+}
+
+// Weight gradient slab[split][Din (+1)][Dout] = X^T dY over the split's K rows (X [B][Din],
+// dY [B][Dout]: both MN-contiguous); with_bias: row Din sums dY (the ones column of X^T).
+// The split count is the caller's (gemm256_wgrad_splits chose it).
+hipError_t gemm256_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int B, int ldx, int lddy,
+                         int with_bias, int splits, const GemmEpi& ep, hipStream_t st) {
+  if (!sizes_ok(B, ldx, 8, Din) || !sizes_ok(B, lddy, 8, Dout) || ep.mode != EPI_SLAB || (ep.ldc & 7) != 0 ||
+      ((uintptr_t)ep.out & 15) != 0 || (ep.slab_stride & 3) != 0)
+    return hipErrorInvalidValue;
+  const Opnd a{x, ldx, Din, B, (uint32_t)((int64_t)B * ldx * 2)};
+  const Opnd b{dy, lddy, Dout, B, (uint32_t)((int64_t)B * lddy * 2)};
+  return launch256<false, false, true>(a, b, ep, Din + (with_bias ? 1 : 0), Dout, B, splits, with_bias ? Din : -1, st);
+}
+
+// Split count of a gemm256 weight gradient: the most splits whose blocks still fit in one
+// round of the CUs (a 257th block would run as a second round), chunks >= 8 steps; 0 when
+// the shape does not belong on this path (too few tiles, partial vectors).
+int gemm256_wgrad_splits(int Din, int Dout, int B, int with_bias, int cus) {
+  if (!gemm256_enabled() || (Din & 7) || (Dout & 7) || B < 16 * BKT) return 0;
+  const int M = Din + (with_bias ? 1 : 0);
+  const int tiles = ((M + BM - 1) / BM) * ((Dout + BN - 1) / BN);
+  const double fill = (double)M * Dout / ((double)tiles * BM * BN);
+  if (tiles < 32 || tiles > cus || fill < 0.9) return 0;
+  int s = cus / tiles;
+  while (s > 1 && B / s < 8 * BKT) --s;
+  // the effective count of the chunking launch256 uses
+  const int kchunk = ((B + s - 1) / s + BKT - 1) / BKT * BKT;
+  return (B + kchunk - 1) / kchunk;
+}
+
+}  // namespace mnistx

@@ -56,6 +56,19 @@ struct LrnParams {
   int on;
 };
 
+// ---- gemm256.hip: 256 x 256 LDS-DMA tiles for the GEMMs that fill the GPU (dense_fwd /
+// dense_dgrad route to it when gemm256_ok)
+bool gemm256_enabled();              // MNISTX_GEMM256 != 0, or set_gemm256
+void set_gemm256(bool on);
+bool gemm256_ok(int M, int N, int K, const GemmEpi& ep);
+hipError_t gemm256_fwd(const bf16_t* x, const bf16_t* w, int M, int N, int K, int ldx, int ldw, const GemmEpi& ep,
+                       hipStream_t st);
+hipError_t gemm256_dgrad(const bf16_t* dy, const bf16_t* w, int M, int N, int K, int lddy, int ldw, const GemmEpi& ep,
+                         hipStream_t st);
+int gemm256_wgrad_splits(int Din, int Dout, int B, int with_bias, int cus);   // 0: not this path
+hipError_t gemm256_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int B, int ldx, int lddy,
+                         int with_bias, int splits, const GemmEpi& ep, hipStream_t st);
+
 // ---- gemm.hip
 // tile (BM, BN) launch_any picks for an M x N output (wgrad: both operands MN-contiguous)
 void gemm_tile(int M, int N, int wgrad, int* bm, int* bn);
@@ -63,8 +76,11 @@ hipError_t dense_fwd(const bf16_t* x, const bf16_t* w, int M, int N, int K, int 
                      const GemmEpi& ep, hipStream_t st);
 hipError_t dense_dgrad(const bf16_t* dy, const bf16_t* w, int M, int N, int K, int lddy, int ldw,
                        const GemmEpi& ep, hipStream_t st);
+// used (optional): the split count actually written -- the 256 x 256 path (tile < 0, used set)
+// may write fewer partials than `splits` (the slab's capacity); the reduce must use *used
 hipError_t dense_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int B, int ldx, int lddy,
-                       int with_bias, int splits, const GemmEpi& ep, hipStream_t st, int tile = -1);
+                       int with_bias, int splits, const GemmEpi& ep, hipStream_t st, int tile = -1,
+                       int* used = nullptr);
 // np (<= 4) dense weight gradients in one launch (64x64 tiles; splits[] in: requested, out: effective)
 hipError_t dense_wgrad_group(int np, const bf16_t* const* x, const bf16_t* const* dy, const int* Din, const int* Dout,
                              int B, const int* ldx, const int* lddy, int* splits, const GemmEpi* ep, hipStream_t st);

@@ -19,3 +19,10 @@ def test_gemm_kc_swap_conflict_free():
     assert m.store(48, True, False) == 1 and m.store(48, True, True) == 1
     assert all(m.read(48, True, r0) == 1 for r0 in (0, 16, 32, 48))
     assert m.store(48, False, False) == 2
+
+
+def test_gemm256_swizzles_conflict_free():
+    import lds_gemm256 as m
+    # gemm256.hip LDS-DMA images: linear would be 4-way (KC b128) / 8-way (MN tr_b16)
+    assert m.kc_worst(lambda r: 0) == 4 and m.mn_worst(lambda r: 0) == 8
+    assert m.kc_worst(m.kc_swz) == 1 and m.mn_worst(m.mn_swz) == 1

@@ -50,11 +50,19 @@ def main():
             K.dense_wgrad(x, dy, slab, din, dout, B, din, dout, True, S)
         return f
 
-    cases = {"wgrad_gemm256": wgrad(True), "wgrad_gemm_hip": wgrad(False),
-             "wgrad_torch_matmul": lambda: torch.matmul(x.t(), dy),
-             "fwd_gemm256": fwd(True), "fwd_gemm_hip": fwd(False),
+    def dbg(f, bits):   # gemm256 experiment bits: 1 = no in-loop DMA (timing only), 2 = BK 64 ring
+        def g():
+            K.set_gemm256_debug(bits)
+            f()
+            K.set_gemm256_debug(0)
+        return g
+
+    cases = {"fwd_gemm256_no_dma": dbg(fwd(True), 1),
+             "wgrad_gemm256": wgrad(True), "wgrad_gemm256_bk64": dbg(wgrad(True), 2),
+             "wgrad_gemm_hip": wgrad(False), "wgrad_torch_matmul": lambda: torch.matmul(x.t(), dy),
+             "fwd_gemm256": fwd(True), "fwd_gemm256_bk64": dbg(fwd(True), 2), "fwd_gemm_hip": fwd(False),
              "fwd_torch_matmul": lambda: torch.matmul(x, w, out=y),
-             "dgrad_gemm256": dgrad(True), "dgrad_gemm_hip": dgrad(False),
+             "dgrad_gemm256": dgrad(True), "dgrad_gemm256_bk64": dbg(dgrad(True), 2), "dgrad_gemm_hip": dgrad(False),
              "dgrad_torch_matmul": lambda: torch.matmul(dy, w.t(), out=dx)}
     res = {k: [] for k in cases}
     for _ in range(2):

@@ -35,14 +35,31 @@
 namespace mnistx {
 namespace {
 
-constexpr int BM = 256, BN = 256, BKT = 64, NTH = 512;
+constexpr int BM = 256, BN = 256, NTH = 512;
 constexpr int WM = 2, WN = 4, TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
-constexpr int IMG = BM * BKT * 2;          // bytes of one operand image (A and B alike: 32 KB)
-constexpr int BUF = 2 * IMG;               // one stage: A image then B image
-constexpr int LDS_BYTES = 2 * BUF;         // 128 KB: one workgroup per CU
+constexpr int LDS_BYTES = 128 * 1024;      // every stage ring: one workgroup per CU
 static_assert(BM == BN, "one image size for both operands");
 
-DEV int kc_swz(int r) { return (r >> 1) & 7; }
+// K-step geometry.  BK = 64: two 64 KB stages (DMA of step t + 1 under the MFMAs of step t,
+// vmcnt(0) each step).  BK = 32: four 32 KB stages, three steps of DMA in flight, each step
+// waits only for its own stage (counted vmcnt), so an HBM miss has ~3 steps of MFMAs to land.
+template <int BK>
+struct Geo {
+  static constexpr int IMG = BM * BK * 2;            // bytes of one operand image
+  static constexpr int BUF = 2 * IMG;                // one stage: A image then B image
+  static constexpr int STAGES = LDS_BYTES / BUF;
+  static constexpr int NI = IMG / 1024 / 8;          // 1 KB DMA instructions per wave per image
+  static constexpr int DPS = 2 * NI;                 // ... per stage (A + B)
+  static constexpr int KC_RB = 2 * BK;               // K-contiguous image row bytes
+  static constexpr int KC_RPI = 1024 / KC_RB;        // K-contiguous rows per DMA instruction
+  static_assert(STAGES * BUF == LDS_BYTES && (BK == 32 || BK == 64), "");
+};
+
+// Bank swizzles (16-byte chunk XOR per row), bench/lds_gemm256.py:
+//   K-contiguous, 128-byte rows (BK 64): c ^ ((r >> 1) & 7); 64-byte rows (BK 32): c ^ (2 ((r >> 3) & 1))
+//   MN-contiguous, 512-byte rows: c ^ f(r)
+template <int BK>
+DEV int kc_swz(int r) { return BK == 64 ? (r >> 1) & 7 : ((r >> 3) & 1) << 1; }
 DEV int mn_swz(int r) { return ((r & 1) << 1) | (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 3); }
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -57,8 +74,8 @@ struct Opnd {
 // One LDS-DMA instruction (16 bytes per lane to lds_dst + 16 lane) issued from inline asm:
 // through the builtin, hipcc sees an LDS write it cannot tell apart from the next step's
 // ds_reads and waits vmcnt(0) in front of them, which serialises the DMA of step t + 1 with
-// the MFMAs of step t.  Hidden in asm it is not counted by hipcc at all: the kernel drains
-// it with its own vmcnt(0) before the barrier that publishes the image.  M0 (the DMA's LDS
+// the MFMAs of step t.  Hidden in asm it is not counted by hipcc at all: the kernel waits
+// for it with its own vmcnt before the barrier that publishes the image.  M0 (the DMA's LDS
 // base) is compiler-reserved, so it is saved and restored inside the statement; s_nop 4
 // covers a descriptor fresh from readfirstlane (cdna_hip_programming.md §5.7).
 DEV void dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t lds_dst) {
@@ -74,18 +91,30 @@ DEV void dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t lds_dst) {
       : "v"(voff), "s"(lds_dst), "s"(rs)
       : "memory");
 }
+// wait until at most N of this wave's DMA instructions are outstanding
+template <int N>
+DEV void wait_dma() {
+  static_assert(N == 0 || N == 4 || N == 8 || N == 16, "");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+}
 
-// Stage the 64-deep K slab k0 (rows past kend: zeros) of rows / cols r0 .. r0 + 255 into the
-// image at byte offset img: 32 DMA instructions of 1 KB (8 KC rows or 2 MN rows each), 4 per wave.
-template <bool KC>
+// Stage the BK-deep K slab k0 (rows past kend: zeros) of rows / cols r0 .. r0 + 255 into the
+// image at byte offset img: IMG / 1 KB DMA instructions (KC_RPI K-contiguous rows or 2 MN rows
+// each), NI per wave.
+template <int BK, bool KC>
 DEV void stage(uint32_t lds_base, int img, const Opnd& o, int r0, int k0, int kend, int wave, int lane) {
+  using G = Geo<BK>;
   const auto rs = buf_rsrc(o.p, o.nbytes);
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < G::NI; ++u) {
     const int i = wave + 8 * u;                                 // DMA instruction of the image
     uint32_t off;
     if constexpr (KC) {
-      const int row = 8 * i + (lane >> 3), ch = (lane & 7) ^ kc_swz(row);
+      constexpr int CPR = BK / 8;                               // 16-byte chunks per row
+      const int row = G::KC_RPI * i + lane / CPR, ch = (lane % CPR) ^ kc_swz<BK>(row);
       const int r = r0 + row, k = k0 + 8 * ch;
       off = (r < o.R && k < kend) ? (uint32_t)(r * o.ld + k) * 2u : BUF_OOB;
     } else {
@@ -98,12 +127,12 @@ DEV void stage(uint32_t lds_base, int img, const Opnd& o, int r0, int k0, int ke
 }
 
 // Fragment of rows / cols c0 .. c0 + 15 for k-half kh (k = 32 kh + 8 (lane >> 4) + j)
-template <bool KC>
+template <int BK, bool KC>
 DEV bf16x8 frag(const uint8_t* lds, int img, int c0, int kh, int lane) {
   const int i = lane & 15, g = lane >> 4;
   if constexpr (KC) {
-    const int r = c0 + i, ch = (4 * kh + g) ^ kc_swz(r);
-    return __builtin_bit_cast(bf16x8, *(const u32x4*)(lds + img + r * 128 + 16 * ch));
+    const int r = c0 + i, ch = (4 * kh + g) ^ kc_swz<BK>(r);
+    return __builtin_bit_cast(bf16x8, *(const u32x4*)(lds + img + r * Geo<BK>::KC_RB + 16 * ch));
   } else {
     const int q = (lane >> 2) & 3, p = lane & 3;
     const int r = 32 * kh + 8 * g + q;                          // k rows r (j 0-3) and r + 4 (j 4-7)
@@ -116,9 +145,12 @@ DEV bf16x8 frag(const uint8_t* lds, int img, int c0, int kh, int lane) {
   }
 }
 
-template <bool AKC, bool BKC, bool WG>
+template <bool AKC, bool BKC, bool WG, int BK>
 __global__ __launch_bounds__(NTH, 1) void gemm256_k(const Opnd a, const Opnd b, const GemmEpi ep, int M, int N,
-                                                    int K, int tiles_n, int tiles_mn, int kchunk, int ones) {
+                                                    int K, int tiles_n, int tiles_mn, int kchunk, int ones,
+                                                    int dbg) {
+  using G = Geo<BK>;
+  constexpr int S = G::STAGES;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
@@ -128,7 +160,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm256_k(const Opnd a, const Opnd b, 
   const int split = WG ? lin / tiles_mn : 0, t = lin - split * tiles_mn;
   const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
   const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
-  const int nk = (kend - kbeg + BKT - 1) / BKT;
+  const int nk = (kend - kbeg + BK - 1) / BK;
   // weight gradients: the A image column `ones` (Din, the bias row of the output) reads zeros
   // from the DMA (past the operand); the lanes that staged its chunk write 1.0 over it
   const bool has_ones = WG && ones >= m0 && ones < m0 + BM;
@@ -140,34 +172,44 @@ __global__ __launch_bounds__(NTH, 1) void gemm256_k(const Opnd a, const Opnd b, 
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_void*)lds;
-  stage<AKC>(lds_base, 0, a, m0, kbeg, kend, wave, lane);
-  stage<BKC>(lds_base, IMG, b, n0, kbeg, kend, wave, lane);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = (kt & 1) * BUF;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (WG) {
-      if (has_ones) {   // this wave's own DMA chunks of the ones column (its vmcnt(0) above ordered them)
+  auto issue = [&](int kt) {   // stage of step kt into ring slot kt % S
+    const int buf = (kt % S) * G::BUF;
+    stage<BK, AKC>(lds_base, buf, a, m0, kbeg + kt * BK, kend, wave, lane);
+    stage<BK, BKC>(lds_base, buf + G::IMG, b, n0, kbeg + kt * BK, kend, wave, lane);
+  };
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+  for (int p = 0; p < S - 1; ++p)
+    if (p < nk) issue(p);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = (kt % S) * G::BUF;
+    // this wave's DMA of step kt done: the stages issued after it may stay in flight
+    const int ahead = min(S - 2, nk - 1 - kt);
+    if constexpr (S == 4) {
+      if (ahead >= 2) wait_dma<2 * G::DPS>();
+      else if (ahead == 1) wait_dma<G::DPS>();
+      else wait_dma<0>();
+    } else {
+      wait_dma<0>();
+    }
+    if constexpr (WG) {
+      if (has_ones) {   // this wave's own DMA chunks of the ones column (its wait above ordered them)
+#pragma unroll
+        for (int u = 0; u < G::NI; ++u) {
           const int i = wave + 8 * u, row = 2 * i + (lane >> 5), ch = (lane & 31) ^ mn_swz(row);
-          if (m0 + 8 * ch == ones && kbeg + kt * BKT + row < kend)
+          if (m0 + 8 * ch == ones && kbeg + kt * BK + row < kend)
             *(bf16_t*)(lds + cur + 1024 * i + 16 * lane) = (bf16_t)0x3f80;   // the lane's DMA slot
         }
       }
     }
-    __syncthreads();   // step kt's images landed (every wave's DMA drained); step kt - 1's reads done
-    if (kt + 1 < nk) {
-      const int nxt = BUF - cur;
-      stage<AKC>(lds_base, nxt, a, m0, kbeg + (kt + 1) * BKT, kend, wave, lane);
-      stage<BKC>(lds_base, nxt + IMG, b, n0, kbeg + (kt + 1) * BKT, kend, wave, lane);
-    }
+    __syncthreads();   // step kt's images landed (every wave's DMA); step kt - 1's reads done
+    if (kt + S - 1 < nk && !(dbg & 1)) issue(kt + S - 1);   // into the slot step kt - 1 read
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
+    for (int kh = 0; kh < BK / 32; ++kh) {
       bf16x8 af[FM], bfr[FN];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = frag<BKC>(lds, cur + IMG, wn * TN + 16 * j, kh, lane);
+      for (int j = 0; j < FN; ++j) bfr[j] = frag<BK, BKC>(lds, cur + G::IMG, wn * TN + 16 * j, kh, lane);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = frag<AKC>(lds, cur, wm * TM + 16 * i, kh, lane);
+      for (int i = 0; i < FM; ++i) af[i] = frag<BK, AKC>(lds, cur, wm * TM + 16 * i, kh, lane);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -237,25 +279,40 @@ __global__ __launch_bounds__(NTH, 1) void gemm256_k(const Opnd a, const Opnd b, 
   }
 }
 
-template <bool AKC, bool BKC, bool WG>
-hipError_t launch256(const Opnd& a, const Opnd& b, const GemmEpi& ep, int M, int N, int K, int splits, int ones,
+// experiments only (set_gemm256_debug): bit 0 skips the in-loop staging (timing, wrong
+// results); bit 1 runs the 2-stage BK = 64 ring instead of the 4-stage BK = 32 one (also
+// MNISTX_GEMM256_BK=64 at load, for whole-step A/Bs)
+int g_gemm256_dbg = [] {
+  const char* e = getenv("MNISTX_GEMM256_BK");
+  return (e && e[0] == '6') ? 2 : 0;
+}();
+
+template <bool AKC, bool BKC, bool WG, int BK>
+hipError_t launch_bk(const Opnd& a, const Opnd& b, const GemmEpi& ep, int M, int N, int K, int splits, int ones,
                      hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)gemm256_k<AKC, BKC, WG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)gemm256_k<AKC, BKC, WG, BK>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             LDS_BYTES) != hipSuccess)
       return hipErrorInvalidValue;
     attr = true;
   }
   const int tn = (N + BN - 1) / BN, tm = (M + BM - 1) / BM;
   int kchunk = K;
-  if (WG) {   // the caller's split count (its slab is sized for it), chunks a multiple of the step
-    kchunk = ((K + splits - 1) / splits + BKT - 1) / BKT * BKT;
+  if (WG) {   // the caller's split count (its slab is sized for it), chunks a multiple of 64
+    kchunk = ((K + splits - 1) / splits + 63) / 64 * 64;
     if ((K + kchunk - 1) / kchunk != splits) return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL((gemm256_k<AKC, BKC, WG>), dim3(tm * tn * (WG ? splits : 1)), dim3(NTH), LDS_BYTES, st, a, b, ep,
-                     M, N, K, tn, tm * tn, kchunk, ones);
+  hipLaunchKernelGGL((gemm256_k<AKC, BKC, WG, BK>), dim3(tm * tn * (WG ? splits : 1)), dim3(NTH), LDS_BYTES, st, a,
+                     b, ep, M, N, K, tn, tm * tn, kchunk, ones, g_gemm256_dbg);
   return hipGetLastError();
+}
+
+template <bool AKC, bool BKC, bool WG>
+hipError_t launch256(const Opnd& a, const Opnd& b, const GemmEpi& ep, int M, int N, int K, int splits, int ones,
+                     hipStream_t st) {
+  if (g_gemm256_dbg & 2) return launch_bk<AKC, BKC, WG, 64>(a, b, ep, M, N, K, splits, ones, st);
+  return launch_bk<AKC, BKC, WG, 32>(a, b, ep, M, N, K, splits, ones, st);
 }
 
 bool sizes_ok(int64_t rows, int ld, int K, int R) {
@@ -275,11 +332,12 @@ bool gemm256_enabled() {
   return g_gemm256 != 0;
 }
 void set_gemm256(bool on) { g_gemm256 = on ? 1 : 0; }
+void set_gemm256_debug(int bits) { g_gemm256_dbg = bits; }
 
 // The 256 x 256 path takes a GEMM when it fills the GPU at least once (>= 256 tiles of a
 // mostly-full 256 x 256), the epilogue is a plain bf16 / fp32 store and every vector is whole.
 bool gemm256_ok(int M, int N, int K, const GemmEpi& ep) {
-  if (!gemm256_enabled() || ep.mode == EPI_SLAB || K < 2 * BKT) return false;
+  if (!gemm256_enabled() || ep.mode == EPI_SLAB || K < 512) return false;   // >= 8 K steps of 64
   const int64_t tiles = (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const double fill = (double)M * N / ((double)tiles * BM * BN);
   return tiles >= 256 && fill >= 0.9 && (N & 7) == 0 && (ep.ldc & 7) == 0 && ((uintptr_t)ep.out & 15) == 0 &&
@@ -321,15 +379,15 @@ hipError_t gemm256_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, i
 // round of the CUs (a 257th block would run as a second round), chunks >= 8 steps; 0 when
 // the shape does not belong on this path (too few tiles, partial vectors).
 int gemm256_wgrad_splits(int Din, int Dout, int B, int with_bias, int cus) {
-  if (!gemm256_enabled() || (Din & 7) || (Dout & 7) || B < 16 * BKT) return 0;
+  if (!gemm256_enabled() || (Din & 7) || (Dout & 7) || B < 1024) return 0;
   const int M = Din + (with_bias ? 1 : 0);
   const int tiles = ((M + BM - 1) / BM) * ((Dout + BN - 1) / BN);
   const double fill = (double)M * Dout / ((double)tiles * BM * BN);
   if (tiles < 32 || tiles > cus || fill < 0.9) return 0;
   int s = cus / tiles;
-  while (s > 1 && B / s < 8 * BKT) --s;
-  // the effective count of the chunking launch256 uses
-  const int kchunk = ((B + s - 1) / s + BKT - 1) / BKT * BKT;
+  while (s > 1 && B / s < 512) --s;
+  // the effective count of the chunking launch_bk uses
+  const int kchunk = ((B + s - 1) / s + 63) / 64 * 64;
   return (B + kchunk - 1) / kchunk;
 }
 

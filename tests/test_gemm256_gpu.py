@@ -19,6 +19,14 @@ def _rel(a, b):
     return float((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-12))
 
 
+@pytest.fixture(params=[0, 2], ids=["bk32_4stage", "bk64_2stage"])
+def ring(request, K):
+    """gemm256's K-step ring: the default 4 x 32-deep stages, or 2 x 64 (set_gemm256_debug bit 1)."""
+    K.set_gemm256_debug(request.param)
+    yield request.param
+    K.set_gemm256_debug(0)
+
+
 def _both(K, f):
     """f() run on the gemm256 route and on gemm.hip; returns (new, old)."""
     K.set_gemm256(True)
@@ -34,9 +42,9 @@ def _both(K, f):
 
 # (M, N, K): the reference CNN's local3 at B = 16384; a tail in every dimension (M, N not
 # multiples of 256, K not a multiple of the 64-deep step); the smallest grid routed (256 tiles)
-@pytest.mark.parametrize("M,N,Kd", [(16384, 1024, 3136), (8104, 2040, 200), (4096, 4096, 128)])
+@pytest.mark.parametrize("M,N,Kd", [(16384, 1024, 3136), (8104, 2040, 520), (4096, 4096, 512)])
 @pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
-def test_gemm256_fwd_bias_relu(K, M, N, Kd, out_dtype):
+def test_gemm256_fwd_bias_relu(K, ring, M, N, Kd, out_dtype):
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(M + N + Kd)
     x = (torch.randn(M, Kd, device=dev, generator=g)).to(torch.bfloat16)
@@ -57,9 +65,9 @@ def test_gemm256_fwd_bias_relu(K, M, N, Kd, out_dtype):
         assert _rel(new, old) < 1e-5
 
 
-@pytest.mark.parametrize("M,N,Kd", [(16384, 3136, 1024), (8104, 2040, 200)])
+@pytest.mark.parametrize("M,N,Kd", [(16384, 3136, 1024), (8104, 2040, 520)])
 @pytest.mark.parametrize("with_mask", [False, True])
-def test_gemm256_dgrad(K, M, N, Kd, with_mask):
+def test_gemm256_dgrad(K, ring, M, N, Kd, with_mask):
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(7 * M + N)
     dy = torch.randn(M, Kd, device=dev, generator=g).to(torch.bfloat16)
@@ -84,7 +92,7 @@ def test_gemm256_route_is_on_by_default(K):
 
 
 @pytest.mark.parametrize("B,Din,Dout", [(16384, 3136, 1024), (5000, 3000, 1000)])
-def test_gemm256_wgrad_bias_row(K, B, Din, Dout):
+def test_gemm256_wgrad_bias_row(K, ring, B, Din, Dout):
     """Split-K weight gradient with the bias row (the ones column of X^T patched into the LDS
     image): the partials the call reports having written sum to X^T dY and dY's column sums."""
     dev = torch.device("cuda", 0)

@@ -64,6 +64,26 @@ def main():
              "fwd_torch_matmul": lambda: torch.matmul(x, w, out=y),
              "dgrad_gemm256": dgrad(True), "dgrad_gemm256_bk64": dbg(dgrad(True), 2), "dgrad_gemm_hip": dgrad(False),
              "dgrad_torch_matmul": lambda: torch.matmul(dy, w.t(), out=dx)}
+    # fp32 (--precision fp32): the same local3 GEMMs on gemm256.hip's fp32 kernel vs f32.hip
+    xf, wf, dyf = x.float(), w.float(), dy.float()
+    yf = torch.empty(B, dout, device=dev)
+    dxf = torch.empty(B, din, device=dev)
+    Sf = 8
+    slabf = torch.empty(Sf * (din + 1) * dout, device=dev)
+
+    def f32(on, which):
+        def f():
+            K.set_gemm256(on)
+            if which == "fwd":
+                K.f32_dense_fwd(xf, wf, yf, B, dout, din, dout, b, True)
+            elif which == "dgrad":
+                K.f32_dense_dgrad(dyf, wf, dxf, B, din, dout, None)
+            else:
+                K.f32_dense_wgrad(xf, dyf, slabf, B, din, dout, Sf if on else 3)
+        return f
+    for which in ("fwd", "dgrad", "wgrad"):
+        cases[f"f32_{which}_gemm256"] = f32(True, which)
+        cases[f"f32_{which}_f32_hip"] = f32(False, which)
     res = {k: [] for k in cases}
     for _ in range(2):
         for f in cases.values():

@@ -911,14 +911,17 @@ void f32_dense_dgrad(Tensor dy, Tensor w, Tensor dx, int64_t M, int64_t Din, int
          "f32_dense_dgrad");
 }
 
-void f32_dense_wgrad(Tensor x, Tensor dy, Tensor slab, int64_t B, int64_t Din, int64_t Dout, int64_t splits) {
+// returns the split count written (the reduce must sum exactly those partials)
+int64_t f32_dense_wgrad(Tensor x, Tensor dy, Tensor slab, int64_t B, int64_t Din, int64_t Dout, int64_t splits) {
   check(x, at::kFloat, B * Din, "x");
   check(dy, at::kFloat, B * Dout, "dy");
   TORCH_CHECK(splits >= 1 && splits <= 65535, "splits");
   check(slab, at::kFloat, splits * (Din + 1) * Dout, "slab");
+  int used = (int)splits;
   hip_ok(mnistx::f32_dense_wgrad(P<const float>(x), P<const float>(dy), (int)B, (int)Din, (int)Dout, (int)splits,
-                                 P<float>(slab), cur_stream()),
+                                 P<float>(slab), cur_stream(), &used),
          "f32_dense_wgrad");
+  return used;
 }
 
 void f32_conv_fwd(Tensor x, Tensor w, Tensor y, int64_t Nb, int64_t H, int64_t W, int64_t C, int64_t OH, int64_t OW,
@@ -1136,6 +1139,9 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("f32_dense_fwd", &f32_dense_fwd);
   m.def("f32_dense_dgrad", &f32_dense_dgrad);
   m.def("f32_dense_wgrad", &f32_dense_wgrad);
+  m.def("f32_wgrad_splits_cap", [](int64_t din, int64_t dout, int64_t b) {
+    return (int64_t)mnistx::f32_wgrad_splits_cap((int)din, (int)dout, (int)b);
+  }, "slab partials the fp32 256 x 256 weight-gradient path writes for this shape (0: not that path)");
   m.def("f32_conv_fwd", &f32_conv_fwd);
   m.def("f32_conv_dgrad", &f32_conv_dgrad);
   m.def("f32_conv_wgrad", &f32_conv_wgrad);
@@ -1167,6 +1173,7 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("host_unregister", [](uintptr_t addr) { return hipHostUnregister((void*)addr) == hipSuccess; });
   m.def("set_gemm256", &mnistx::set_gemm256, "route the GEMMs that fill the GPU to gemm256.hip (A/B switch)");
   m.def("gemm256_enabled", &mnistx::gemm256_enabled);
+  m.def("set_gemm256_debug", [](int64_t b) { mnistx::set_gemm256_debug((int)b); });
   m.def("set_reserve_cus", [](int64_t n) { mnistx::set_reserve_cus((int)n); });
   m.def("reserve_cus", []() { return (int64_t)mnistx::reserve_cus(); });
   m.def("clock_mark", [](Tensor out, int64_t slot) {

@@ -633,8 +633,14 @@ int ew_grid(int64_t n) {
 }  // namespace
 
 // ---------------------------------------------------------------- host launchers
+// The local3-sized GEMMs (>= one round of 256 x 256 tiles) run on gemm256.hip's fp32 LDS-DMA
+// kernel; everything smaller stays on gemm_f32_k.
+static bool al16p(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 hipError_t f32_dense_fwd(const float* x, const float* w, int M, int N, int K, const float* bias, int bias_n, int relu,
                          float* y, int ldy, hipStream_t st) {
+  if (gemm256f_ok(M, N, K) && (ldy & 3) == 0 && al16p(x) && al16p(w) && al16p(y))
+    return gemm256f_fwd(x, w, M, N, K, bias, bias_n, relu, y, ldy, st);
   return launch_f32(StridedF<true>{x, M, K, K, -1}, StridedF<false>{w, N, K, N, -1}, M, N, K, 1,
                     store_epi(y, ldy, bias, bias_n, relu, nullptr, 0), st);
 }
@@ -642,13 +648,38 @@ hipError_t f32_dense_fwd(const float* x, const float* w, int M, int N, int K, co
 hipError_t f32_dense_dgrad(const float* dy, const float* w, int M, int Din, int Dout, const float* mask, float* dx,
                            hipStream_t st) {
   // dx[m][i] = sum_o dy[m][o] W[i][o]
+  if (gemm256f_ok(M, Din, Dout) && al16p(dy) && al16p(w) && al16p(dx) && al16p(mask))
+    return gemm256f_dgrad(dy, w, M, Din, Dout, mask, dx, st);
   return launch_f32(StridedF<true>{dy, M, Dout, Dout, -1}, StridedF<true>{w, Din, Dout, Dout, -1}, M, Din, Dout, 1,
                     store_epi(dx, Din, nullptr, 0, 0, mask, Din), st);
 }
 
+static int num_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = -1;
+  }
+  return cus;
+}
+
+int f32_wgrad_splits_cap(int Din, int Dout, int B) {
+  const int cus = num_cus();
+  return cus > 0 ? gemm256f_wgrad_splits(Din, Dout, B, cus) : 0;
+}
+
 hipError_t f32_dense_wgrad(const float* x, const float* dy, int B, int Din, int Dout, int splits, float* slab,
-                           hipStream_t st) {
+                           hipStream_t st, int* used) {
   // slab[z][Din + 1][Dout]: rows < Din = x^T dy, row Din = column sums of dy (bias)
+  if (used) {
+    *used = splits;
+    const int s2 = f32_wgrad_splits_cap(Din, Dout, B);
+    if (s2 > 0 && s2 <= splits && al16p(x) && al16p(dy) && al16p(slab)) {
+      *used = s2;
+      return gemm256f_wgrad(x, dy, B, Din, Dout, s2, slab, st);
+    }
+  }
   return launch_f32(StridedF<false>{x, Din, B, Din, Din}, StridedF<false>{dy, Dout, B, Dout, -1}, Din + 1, Dout, B,
                     splits, slab_epi(slab, (int64_t)(Din + 1) * Dout), st);
 }

@@ -319,6 +319,232 @@ bool sizes_ok(int64_t rows, int ld, int K, int R) {
   return (ld & 7) == 0 && (K & 7) == 0 && (R & 7) == 0 && rows * ld * 2 < ((int64_t)1 << 31);
 }
 
+// ---------------------------------------------------------------- fp32 (--precision fp32)
+// The same tile, DMA ring and epilogue on v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32
+// sums: the reference trains in tf.float32, mnist_input.py:86,107).  16-deep K stages, four
+// of them (4 x 32 KB), three in flight.  The 4 k-slots of an MFMA are k = 4 g + s for lane
+// group g and MFMA s of the stage's 4 slices, so a lane's 4 k of one fragment row are one
+// 16-byte chunk: a K-contiguous operand gives them in ONE ds_read_b128, an MN-contiguous one
+// in 4 ds_read_b32 (rows 4 g .. 4 g + 3 at the lane's column).
+constexpr int BKF = 16;
+constexpr int IMGF = BM * BKF * 4;          // 16 KB per operand image
+constexpr int BUFF = 2 * IMGF;
+constexpr int SF = LDS_BYTES / BUFF;        // 4 stages
+constexpr int NIF = IMGF / 1024 / 8;        // 1 KB DMA instructions per wave per image (2)
+constexpr int DPSF = 2 * NIF;               // ... per stage (4)
+static_assert(SF == 4 && DPSF == 4, "fp32 ring: 4 stages of 4 DMA instructions per wave");
+// swizzles (bench/lds_gemm256.py): 64-byte K-contiguous rows read by ds_read_b128 (the
+// bf16 32-deep geometry); 1 KB MN rows read by ds_read_b32: rows 4 apart in one half-wave
+// are moved to the other 64-byte half of the bank line
+DEV int kcs_f(int r) { return ((r >> 3) & 1) << 1; }
+DEV int mns_f(int r) { return ((r >> 2) & 1) << 2; }
+
+struct OpndF {
+  const float* p;
+  int ld, R, K;
+  uint32_t nbytes;
+};
+struct EpiF32 {
+  float* out;            // output, or the split-K slab base (WG)
+  int ldc;
+  const float* bias;     // + bias[n] (n < bias_n)
+  int bias_n, relu;
+  const float* mask;     // keep v where mask[m * ldm + n] > 0 (ReLU backward)
+  int ldm;
+  int64_t slab_stride;
+};
+
+template <bool KC>
+DEV void stage_f(uint32_t lds_base, int img, const OpndF& o, int r0, int k0, int kend, int wave, int lane) {
+  const auto rs = buf_rsrc(o.p, o.nbytes);
+#pragma unroll
+  for (int u = 0; u < NIF; ++u) {
+    const int i = wave + 8 * u;
+    uint32_t off;
+    if constexpr (KC) {   // 16 rows of 64 bytes per instruction
+      const int row = 16 * i + (lane >> 2), ch = (lane & 3) ^ kcs_f(row);
+      const int r = r0 + row, k = k0 + 4 * ch;
+      off = (r < o.R && k < kend) ? (uint32_t)(r * o.ld + k) * 4u : BUF_OOB;
+    } else {              // one 1 KB row (256 columns) per instruction
+      const int row = i, ch = lane ^ mns_f(row);
+      const int k = k0 + row, c = r0 + 4 * ch;
+      off = (k < kend && c < o.R) ? (uint32_t)(k * o.ld + c) * 4u : BUF_OOB;
+    }
+    dma16(rs, off, (uint32_t)__builtin_amdgcn_readfirstlane(lds_base + img + 1024 * i));
+  }
+}
+
+// the 4 k (= 4 g .. 4 g + 3) of row / column c0 + (lane & 15) for the stage's 4 MFMAs
+template <bool KC>
+DEV f32x4 frag_f(const uint8_t* lds, int img, int c0, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  if constexpr (KC) {
+    const int r = c0 + i;
+    return *(const f32x4*)(lds + img + r * 64 + 16 * (g ^ kcs_f(r)));
+  } else {
+    const int c = c0 + i;
+    f32x4 v;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int k = 4 * g + s;
+      v[s] = *(const float*)(lds + img + k * 1024 + 16 * ((c >> 2) ^ mns_f(k)) + 4 * (c & 3));
+    }
+    return v;
+  }
+}
+
+template <bool AKC, bool BKC, bool WG>
+__global__ __launch_bounds__(NTH, 1) void gemm256f_k(const OpndF a, const OpndF b, const EpiF32 ep, int M, int N,
+                                                     int K, int tiles_n, int tiles_mn, int kchunk, int ones) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = WG ? lin / tiles_mn : 0, t = lin - split * tiles_mn;
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+  const int nk = (kend - kbeg + BKF - 1) / BKF;
+  const bool has_ones = WG && ones >= m0 && ones < m0 + BM;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_void*)lds;
+  auto issue = [&](int kt) {
+    const int buf = (kt % SF) * BUFF;
+    stage_f<AKC>(lds_base, buf, a, m0, kbeg + kt * BKF, kend, wave, lane);
+    stage_f<BKC>(lds_base, buf + IMGF, b, n0, kbeg + kt * BKF, kend, wave, lane);
+  };
+#pragma unroll
+  for (int p = 0; p < SF - 1; ++p)
+    if (p < nk) issue(p);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = (kt % SF) * BUFF;
+    const int ahead = min(SF - 2, nk - 1 - kt);
+    if (ahead >= 2) wait_dma<2 * DPSF>();
+    else if (ahead == 1) wait_dma<DPSF>();
+    else wait_dma<0>();
+    if constexpr (WG) {
+      if (has_ones) {   // this wave's own DMA chunks of the ones column
+#pragma unroll
+        for (int u = 0; u < NIF; ++u) {
+          const int i = wave + 8 * u, ch = lane ^ mns_f(i);
+          if (m0 + 4 * ch == ones && kbeg + kt * BKF + i < kend) *(float*)(lds + cur + 1024 * i + 16 * lane) = 1.f;
+        }
+      }
+    }
+    __syncthreads();
+    if (kt + SF - 1 < nk) issue(kt + SF - 1);
+    f32x4 fa[FM], fb[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) fb[j] = frag_f<BKC>(lds, cur + IMGF, wn * TN + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) fa[i] = frag_f<AKC>(lds, cur, wm * TM + 16 * i, lane);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+  }
+  __syncthreads();
+
+  // epilogue: the bf16 kernel's (8 consecutive columns of one row per lane and vector)
+  const int g = lane >> 4, li = lane & 15;
+  constexpr int EP_LD = TN + 4, VI = 16 * (TN / 8) / 64;
+  float* eb = (float*)lds + wave * 16 * EP_LD;
+  float bv[VI][8];
+#pragma unroll
+  for (int k = 0; k < VI; ++k) {
+    const int v = lane + 64 * k, n = n0 + wn * TN + (v % (TN / 8)) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bv[k][e] = (!WG && ep.bias && n + e < ep.bias_n) ? ep.bias[n + e] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) eb[(4 * g + r) * EP_LD + j * 16 + li] = acc[i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int k = 0; k < VI; ++k) {
+      const int v = lane + 64 * k, rr = v / (TN / 8), cv = v % (TN / 8);
+      const int m = m0 + wm * TM + 16 * i + rr, n = n0 + wn * TN + 8 * cv;
+      if (m < M && n < N) {
+        f32x4 lo = *(const f32x4*)(eb + rr * EP_LD + 8 * cv), hi = *(const f32x4*)(eb + rr * EP_LD + 8 * cv + 4);
+        float* o;
+        if constexpr (WG) {
+          o = ep.out + (int64_t)split * ep.slab_stride + (int64_t)m * ep.ldc + n;
+        } else {
+          o = ep.out + (int64_t)m * ep.ldc + n;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            lo[e] += bv[k][e];
+            hi[e] += bv[k][e + 4];
+          }
+          if (ep.relu) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              lo[e] = fmaxf(lo[e], 0.f);
+              hi[e] = fmaxf(hi[e], 0.f);
+            }
+          }
+          if (ep.mask) {
+            const f32x4 ml = *(const f32x4*)(ep.mask + (int64_t)m * ep.ldm + n);
+            const f32x4 mh = *(const f32x4*)(ep.mask + (int64_t)m * ep.ldm + n + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              if (!(ml[e] > 0.f)) lo[e] = 0.f;
+              if (!(mh[e] > 0.f)) hi[e] = 0.f;
+            }
+          }
+        }
+        *(f32x4*)o = lo;
+        *(f32x4*)(o + 4) = hi;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+template <bool AKC, bool BKC, bool WG>
+hipError_t launch_f(const OpndF& a, const OpndF& b, const EpiF32& ep, int M, int N, int K, int splits, int ones,
+                    hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)gemm256f_k<AKC, BKC, WG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            LDS_BYTES) != hipSuccess)
+      return hipErrorInvalidValue;
+    attr = true;
+  }
+  const int tn = (N + BN - 1) / BN, tm = (M + BM - 1) / BM;
+  int kchunk = K;
+  if (WG) {
+    kchunk = ((K + splits - 1) / splits + 63) / 64 * 64;
+    if ((K + kchunk - 1) / kchunk != splits) return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL((gemm256f_k<AKC, BKC, WG>), dim3(tm * tn * (WG ? splits : 1)), dim3(NTH), LDS_BYTES, st, a, b,
+                     ep, M, N, K, tn, tm * tn, kchunk, ones);
+  return hipGetLastError();
+}
+
+bool sizes_ok_f(int64_t rows, int ld, int K, int R) {
+  return (ld & 3) == 0 && (K & 3) == 0 && (R & 3) == 0 && rows * ld * 4 < ((int64_t)1 << 31);
+}
+
+bool fill_ok(int M, int N, int min_tiles) {
+  const int64_t tiles = (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  return tiles >= min_tiles && (double)M * N / ((double)tiles * BM * BN) >= 0.9;
+}
+
 }  // namespace
 
 // Routing switch (A/B): MNISTX_GEMM256=0 starts with every dense GEMM on gemm.hip;
@@ -389,6 +615,68 @@ int gemm256_wgrad_splits(int Din, int Dout, int B, int with_bias, int cus) {
   // the effective count of the chunking launch_bk uses
   const int kchunk = ((B + s - 1) / s + 63) / 64 * 64;
   return (B + kchunk - 1) / kchunk;
+}
+
+// ---- fp32: the f32.hip launchers route here (same conditions as the bf16 path; N % 8 for
+// the 8-column epilogue vectors, 16-byte aligned operands)
+// fp32 only: also require the last round of tiles to be >= 90 % full -- the fp32 data
+// gradient of local3 (832 tiles = 3.25 rounds of 256 CUs) ran 993 us here vs 925 on
+// f32.hip's 128 x 128 tiles (bench/micro_gemm256.py), its forward 761 vs 893 (1 round)
+bool gemm256f_ok(int M, int N, int K) {
+  if (!gemm256_enabled() || K < 256 || (N & 7) || !fill_ok(M, N, 256)) return false;
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = -1;
+  }
+  if (cus <= 0) return false;
+  const int64_t tiles = (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const int64_t rounds = (tiles + cus - 1) / cus;
+  return (double)tiles / (double)(rounds * cus) >= 0.9;
+}
+
+// y[M, N] = x[M, K] . W[K, N] (+ bias, ReLU)
+hipError_t gemm256f_fwd(const float* x, const float* w, int M, int N, int K, const float* bias, int bias_n, int relu,
+                        float* y, int ldy, hipStream_t st) {
+  if (!sizes_ok_f(M, K, K, 4) || !sizes_ok_f(K, N, 4, N) || (ldy & 3) || ((uintptr_t)y & 15)) return hipErrorInvalidValue;
+  const OpndF a{x, K, M, K, (uint32_t)((int64_t)M * K * 4)};
+  const OpndF b{w, N, N, K, (uint32_t)((int64_t)K * N * 4)};
+  return launch_f<true, false, false>(a, b, EpiF32{y, ldy, bias, bias_n, relu, nullptr, 0, 0}, M, N, K, 1, -1, st);
+}
+
+// dx[M, Din] = dy[M, Dout] . W[Din, Dout]^T (x mask > 0)
+hipError_t gemm256f_dgrad(const float* dy, const float* w, int M, int Din, int Dout, const float* mask, float* dx,
+                          hipStream_t st) {
+  if (!sizes_ok_f(M, Dout, Dout, 4) || !sizes_ok_f(Din, Dout, Dout, 4) || (Din & 7) || ((uintptr_t)dx & 15) ||
+      ((uintptr_t)mask & 15))
+    return hipErrorInvalidValue;
+  const OpndF a{dy, Dout, M, Dout, (uint32_t)((int64_t)M * Dout * 4)};
+  const OpndF b{w, Dout, Din, Dout, (uint32_t)((int64_t)Din * Dout * 4)};
+  return launch_f<true, true, false>(a, b, EpiF32{dx, Din, nullptr, 0, 0, mask, Din, 0}, M, Din, Dout, 1, -1, st);
+}
+
+int gemm256f_wgrad_splits(int Din, int Dout, int B, int cus) {
+  if (!gemm256_enabled() || (Din & 3) || (Dout & 7) || B < 1024) return 0;
+  const int M = Din + 1;
+  const int tiles = ((M + BM - 1) / BM) * ((Dout + BN - 1) / BN);
+  if (tiles < 32 || tiles > cus || !fill_ok(M, Dout, 32)) return 0;
+  int s = cus / tiles;
+  while (s > 1 && B / s < 512) --s;
+  const int kchunk = ((B + s - 1) / s + 63) / 64 * 64;
+  return (B + kchunk - 1) / kchunk;
+}
+
+// slab[split][Din + 1][Dout]: rows < Din = x^T dy over the split's rows, row Din = sums of dy
+hipError_t gemm256f_wgrad(const float* x, const float* dy, int B, int Din, int Dout, int splits, float* slab,
+                          hipStream_t st) {
+  if (!sizes_ok_f(B, Din, 4, Din) || !sizes_ok_f(B, Dout, 4, Dout) || ((uintptr_t)slab & 15)) return hipErrorInvalidValue;
+  const OpndF a{x, Din, Din, B, (uint32_t)((int64_t)B * Din * 4)};
+  const OpndF b{dy, Dout, Dout, B, (uint32_t)((int64_t)B * Dout * 4)};
+  const int64_t stride = (int64_t)(Din + 1) * Dout;
+  if (stride & 3) return hipErrorInvalidValue;
+  return launch_f<false, false, true>(a, b, EpiF32{slab, Dout, nullptr, 0, 0, nullptr, 0, stride}, Din + 1, Dout, B,
+                                      splits, Din, st);
 }
 
 }  // namespace mnistx

@@ -60,12 +60,22 @@ struct LrnParams {
 // dense_dgrad route to it when gemm256_ok)
 bool gemm256_enabled();              // MNISTX_GEMM256 != 0, or set_gemm256
 void set_gemm256(bool on);
+void set_gemm256_debug(int bits);     // experiments: bit 0 = skip the in-loop DMA (wrong results)
 bool gemm256_ok(int M, int N, int K, const GemmEpi& ep);
 hipError_t gemm256_fwd(const bf16_t* x, const bf16_t* w, int M, int N, int K, int ldx, int ldw, const GemmEpi& ep,
                        hipStream_t st);
 hipError_t gemm256_dgrad(const bf16_t* dy, const bf16_t* w, int M, int N, int K, int lddy, int ldw, const GemmEpi& ep,
                          hipStream_t st);
 int gemm256_wgrad_splits(int Din, int Dout, int B, int with_bias, int cus);   // 0: not this path
+// fp32 twins (f32_dense_* route here when gemm256f_ok / gemm256f_wgrad_splits > 0)
+bool gemm256f_ok(int M, int N, int K);
+hipError_t gemm256f_fwd(const float* x, const float* w, int M, int N, int K, const float* bias, int bias_n, int relu,
+                        float* y, int ldy, hipStream_t st);
+hipError_t gemm256f_dgrad(const float* dy, const float* w, int M, int Din, int Dout, const float* mask, float* dx,
+                          hipStream_t st);
+int gemm256f_wgrad_splits(int Din, int Dout, int B, int cus);
+hipError_t gemm256f_wgrad(const float* x, const float* dy, int B, int Din, int Dout, int splits, float* slab,
+                          hipStream_t st);
 hipError_t gemm256_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int B, int ldx, int lddy,
                          int with_bias, int splits, const GemmEpi& ep, hipStream_t st);
 
@@ -174,8 +184,10 @@ hipError_t f32_dense_fwd(const float* x, const float* w, int M, int N, int K, co
                          float* y, int ldy, hipStream_t st);
 hipError_t f32_dense_dgrad(const float* dy, const float* w, int M, int Din, int Dout, const float* mask, float* dx,
                            hipStream_t st);
+// used (optional): the split count written (the 256 x 256 path may write fewer than `splits`)
 hipError_t f32_dense_wgrad(const float* x, const float* dy, int B, int Din, int Dout, int splits, float* slab,
-                           hipStream_t st);
+                           hipStream_t st, int* used = nullptr);
+int f32_wgrad_splits_cap(int Din, int Dout, int B);   // slabs the 256 x 256 path may write (0: none)
 // conv_halo_f32.hip: LDS-halo fp32 conv2 of the reference CNN (fwd / dgrad), routed to by f32_conv_*
 bool f32_halo_fwd_ok(int H, int W, int C, int OH, int OW, int KH, int KW, int ph, int pw, int Cout);
 bool f32_halo_dgrad_ok(int OH, int OW, int Cout, int H, int W, int KH, int KW, int ph, int pw, int Cin);

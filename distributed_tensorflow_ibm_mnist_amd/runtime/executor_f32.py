@@ -247,7 +247,8 @@ class DenseF(_L):
         assert self.x.shape[1] == spec.din, f"{spec.name}: flatten {self.x.shape[1]} != din {spec.din}"
         self.out = _f32(B, spec.dout, device=dev)
         self.wname, self.bname = f"{spec.name}/weights", f"{spec.name}/biases"
-        self.splits = wgrad_splits(spec.din + 1, spec.dout, B)
+        # slab capacity: the 64x64-tile split, or the 256x256 path's own (one round of blocks)
+        self.splits = max(wgrad_splits(spec.din + 1, spec.dout, B), kernels().f32_wgrad_splits_cap(spec.din, spec.dout, B))
         self.slab = _f32(self.splits * (spec.din + 1) * spec.dout, device=dev)
 
     def fwd(self, nb: int) -> None:
@@ -257,8 +258,8 @@ class DenseF(_L):
 
     def bwd_weight(self, nb: int, dy: torch.Tensor) -> None:
         s, K = self.spec, kernels()
-        S = min(self.splits, wgrad_splits(s.din + 1, s.dout, nb))
-        K.f32_dense_wgrad(self.x, dy.view(-1, s.dout), self.slab, nb, s.din, s.dout, S)
+        S = min(self.splits, max(wgrad_splits(s.din + 1, s.dout, nb), K.f32_wgrad_splits_cap(s.din, s.dout, nb)))
+        S = K.f32_dense_wgrad(self.x, dy.view(-1, s.dout), self.slab, nb, s.din, s.dout, S)   # partials written
         K.splitk_reduce(self.slab, S, s.din + 1, s.dout, 1, s.din, s.din, s.dout, s.din,
                         self.fp.grad_view(self.wname), self.fp.grad_view(self.bname), 1.0)
 

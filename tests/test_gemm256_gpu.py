@@ -120,3 +120,53 @@ def test_gemm256_wgrad_bias_row(K, ring, B, Din, Dout):
     assert _rel(new, ref) < 1e-4, _rel(new, ref)
     assert _rel(new[Din], ref[Din]) < 1e-4, _rel(new[Din], ref[Din])   # bias row
     assert _rel(old, ref) < 1e-4
+
+
+def _rel64(a, ref):
+    return float((a.double() - ref).norm() / ref.norm().clamp_min(1e-30))
+
+
+# fp32 (--precision fp32): the same tiles on v_mfma_f32_16x16x4_f32, against float64 (the
+# fp32 route also needs its last round of tiles >= 90 % full: the forwards of the first two
+# shapes and the dgrad of the third (4096 x 4096 out) are routed; local3's dgrad (3.25
+# rounds) stays on f32.hip -- either way the result must match)
+@pytest.mark.parametrize("M,N,Kd", [(16384, 1024, 3136), (8104, 2040, 520), (4096, 512, 4096)])
+def test_gemm256_f32_fwd_dgrad(K, M, N, Kd):
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(3 * M + Kd)
+    x = torch.randn(M, Kd, device=dev, generator=g)
+    w = torch.randn(Kd, N, device=dev, generator=g) / Kd ** 0.5
+    b = torch.randn(N, device=dev, generator=g) * 0.1
+    y = torch.full((M, N), float("nan"), device=dev)
+    K.set_gemm256(True)
+    K.f32_dense_fwd(x, w, y, M, N, Kd, N, b, True)
+    ref = torch.relu(x.double() @ w.double() + b.double())
+    assert not torch.isnan(y).any()
+    assert _rel64(y, ref) < 1e-5, _rel64(y, ref)   # fp32 sums over K (f32.hip tests: 1e-5)
+    # dgrad: dx[M, Kd] = dy[M, N] . w[Kd, N]^T, masked (w here plays W[Din = Kd][Dout = N])
+    dy = torch.randn(M, N, device=dev, generator=g)
+    mask = torch.randn(M, Kd, device=dev, generator=g)
+    dx = torch.full((M, Kd), float("nan"), device=dev)
+    K.f32_dense_dgrad(dy, w, dx, M, Kd, N, mask)
+    refd = (dy.double() @ w.double().t()) * (mask > 0)
+    assert not torch.isnan(dx).any()
+    assert _rel64(dx, refd) < 1e-5, _rel64(dx, refd)
+
+
+@pytest.mark.parametrize("B,Din,Dout", [(16384, 3136, 1024), (5000, 3000, 1000)])
+def test_gemm256_f32_wgrad_bias_row(K, B, Din, Dout):
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(B + Dout)
+    x = torch.randn(B, Din, device=dev, generator=g)
+    dy = torch.randn(B, Dout, device=dev, generator=g)
+    cap = 8
+    assert 1 <= K.f32_wgrad_splits_cap(Din, Dout, B) < cap
+    slab = torch.full((cap * (Din + 1) * Dout,), float("nan"), device=dev)
+    S = K.f32_dense_wgrad(x, dy, slab, B, Din, Dout, cap)
+    torch.cuda.synchronize()
+    assert S == K.f32_wgrad_splits_cap(Din, Dout, B)
+    tot = slab.view(cap, Din + 1, Dout)[:S].sum(0)
+    assert not torch.isnan(tot).any()
+    # fp32 sums over K = B rows (1.1e-6 measured at B = 16384; f32.hip's tests use 1e-5)
+    assert _rel64(tot[:Din], x.double().t() @ dy.double()) < 1e-5
+    assert _rel64(tot[Din], dy.double().sum(0)) < 1e-5

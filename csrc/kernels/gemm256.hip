@@ -71,6 +71,36 @@ struct Opnd {
   uint32_t nbytes;
 };
 
+// Block -> (tile, K split) schedule.  Data / forward GEMMs: one block per tile.  Weight
+// gradients (split-K): the full-height row tiles take S splits and a partial last row tile
+// (local3: rows 3072-3136 of 3137) its own S_p, so the grid fills the CUs once without the
+// thin tiles holding full-size K chunks (local3: 48 x 5 + 4 x 4 = 256 blocks instead of
+// 52 x 4 = 208); the last split of a partial tile zero-fills slabs S_p .. S - 1 of its rows,
+// which the S-slab reduce then sums harmlessly.
+struct Sched {
+  int tiles_n;          // column tiles
+  int tm_full;          // row tiles scheduled with S splits (all of them when not split)
+  int S, kchunk;        // their splits and K chunk (1, K when not split)
+  int np, S_p, kchunk_p;   // blocks / splits / K chunk of the partial last row tile (np = 0: none)
+};
+DEV void decode(const Sched& sc, int lin, int& m0, int& n0, int& split, int& kchunk, bool& zero_rest) {
+  if (lin < sc.np) {
+    split = lin / sc.tiles_n;
+    m0 = sc.tm_full * BM;
+    n0 = (lin - split * sc.tiles_n) * BN;
+    kchunk = sc.kchunk_p;
+    zero_rest = split == sc.S_p - 1;
+  } else {
+    const int l = lin - sc.np, per = sc.tm_full * sc.tiles_n;
+    split = l / per;
+    const int t = l - split * per;
+    m0 = (t / sc.tiles_n) * BM;
+    n0 = (t % sc.tiles_n) * BN;
+    kchunk = sc.kchunk;
+    zero_rest = false;
+  }
+}
+
 // One LDS-DMA instruction (16 bytes per lane to lds_dst + 16 lane) issued from inline asm:
 // through the builtin, hipcc sees an LDS write it cannot tell apart from the next step's
 // ds_reads and waits vmcnt(0) in front of them, which serialises the DMA of step t + 1 with
@@ -147,8 +177,7 @@ DEV bf16x8 frag(const uint8_t* lds, int img, int c0, int kh, int lane) {
 
 template <bool AKC, bool BKC, bool WG, int BK>
 __global__ __launch_bounds__(NTH, 1) void gemm256_k(const Opnd a, const Opnd b, const GemmEpi ep, int M, int N,
-                                                    int K, int tiles_n, int tiles_mn, int kchunk, int ones,
-                                                    int dbg) {
+                                                    int K, const Sched sc, int ones, int dbg) {
   using G = Geo<BK>;
   constexpr int S = G::STAGES;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -156,9 +185,9 @@ __global__ __launch_bounds__(NTH, 1) void gemm256_k(const Opnd a, const Opnd b, 
   const int wm = wave / WN, wn = wave % WN;
   // split-K (weight gradients): consecutive logical ids are the tiles of one split, which
   // read the same K rows of both operands -- remapped onto one XCD's L2 (gemm.hip gemm_kernel)
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = WG ? lin / tiles_mn : 0, t = lin - split * tiles_mn;
-  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  int m0, n0, split, kchunk;
+  bool zero_rest;
+  decode(sc, xcd_remap(blockIdx.x, gridDim.x), m0, n0, split, kchunk, zero_rest);
   const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
   const int nk = (kend - kbeg + BK - 1) / BK;
   // weight gradients: the A image column `ones` (Din, the bias row of the output) reads zeros
@@ -245,10 +274,16 @@ __global__ __launch_bounds__(NTH, 1) void gemm256_k(const Opnd a, const Opnd b, 
       const int m = m0 + wm * TM + 16 * i + rr, n = n0 + wn * TN + 8 * cv;
       if (m < M && n < N) {
         const f32x4 lo = *(const f32x4*)(eb + rr * EP_LD + 8 * cv), hi = *(const f32x4*)(eb + rr * EP_LD + 8 * cv + 4);
-        if constexpr (WG) {   // split-K partial: this split's fp32 slab
+        if constexpr (WG) {   // split-K partial: this split's fp32 slab (+ zeros in the slabs it skips)
           float* o = (float*)ep.out + (int64_t)split * ep.slab_stride + (int64_t)m * ep.ldc + n;
           *(f32x4*)o = lo;
           *(f32x4*)(o + 4) = hi;
+          if (zero_rest)
+            for (int z = split + 1; z < sc.S; ++z) {
+              float* oz = o + (int64_t)(z - split) * ep.slab_stride;
+              *(f32x4*)oz = f32x4{0.f, 0.f, 0.f, 0.f};
+              *(f32x4*)(oz + 4) = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
           continue;
         }
         float x[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -287,6 +322,42 @@ int g_gemm256_dbg = [] {
   return (e && e[0] == '6') ? 2 : 0;
 }();
 
+// the CU count (cached)
+int num_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = -1;
+  }
+  return cus;
+}
+
+// Schedule of an M x N x K launch; WG: `splits` for the full-height row tiles (the caller's
+// slab count), the partial last row tile gets what fills the remaining CUs (<= splits).
+// Returns the grid size, 0 if `splits` is not an exact chunking of K.
+int make_sched(Sched& sc, int M, int N, int K, bool wg, int splits) {
+  const int tn = (N + BN - 1) / BN, tm = (M + BM - 1) / BM;
+  if (!wg) {
+    sc = Sched{tn, tm, 1, K, 0, 0, 0};
+    return tm * tn;
+  }
+  const int kchunk = ((K + splits - 1) / splits + 63) / 64 * 64;
+  if ((K + kchunk - 1) / kchunk != splits) return 0;
+  const int tm_full = M / BM;
+  sc = Sched{tn, tm_full, splits, kchunk, 0, 0, 0};
+  if (tm_full < tm) {
+    const int cus = num_cus();
+    int sp = cus > 0 ? (cus - tm_full * tn * splits) / tn : 1;
+    sp = sp < 1 ? 1 : (sp > splits ? splits : sp);
+    const int kcp = ((K + sp - 1) / sp + 63) / 64 * 64;
+    sc.S_p = (K + kcp - 1) / kcp;
+    sc.kchunk_p = kcp;
+    sc.np = tn * sc.S_p;
+  }
+  return sc.np + tm_full * tn * splits;
+}
+
 template <bool AKC, bool BKC, bool WG, int BK>
 hipError_t launch_bk(const Opnd& a, const Opnd& b, const GemmEpi& ep, int M, int N, int K, int splits, int ones,
                      hipStream_t st) {
@@ -297,14 +368,11 @@ hipError_t launch_bk(const Opnd& a, const Opnd& b, const GemmEpi& ep, int M, int
       return hipErrorInvalidValue;
     attr = true;
   }
-  const int tn = (N + BN - 1) / BN, tm = (M + BM - 1) / BM;
-  int kchunk = K;
-  if (WG) {   // the caller's split count (its slab is sized for it), chunks a multiple of 64
-    kchunk = ((K + splits - 1) / splits + 63) / 64 * 64;
-    if ((K + kchunk - 1) / kchunk != splits) return hipErrorInvalidValue;
-  }
-  hipLaunchKernelGGL((gemm256_k<AKC, BKC, WG, BK>), dim3(tm * tn * (WG ? splits : 1)), dim3(NTH), LDS_BYTES, st, a,
-                     b, ep, M, N, K, tn, tm * tn, kchunk, ones, g_gemm256_dbg);
+  Sched sc;
+  const int grid = make_sched(sc, M, N, K, WG, splits);   // WG: the caller's split count (its slab)
+  if (grid <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gemm256_k<AKC, BKC, WG, BK>), dim3(grid), dim3(NTH), LDS_BYTES, st, a, b, ep, M, N, K, sc, ones,
+                     g_gemm256_dbg);
   return hipGetLastError();
 }
 
@@ -395,13 +463,13 @@ DEV f32x4 frag_f(const uint8_t* lds, int img, int c0, int lane) {
 
 template <bool AKC, bool BKC, bool WG>
 __global__ __launch_bounds__(NTH, 1) void gemm256f_k(const OpndF a, const OpndF b, const EpiF32 ep, int M, int N,
-                                                     int K, int tiles_n, int tiles_mn, int kchunk, int ones) {
+                                                     int K, const Sched sc, int ones) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = WG ? lin / tiles_mn : 0, t = lin - split * tiles_mn;
-  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  int m0, n0, split, kchunk;
+  bool zero_rest;
+  decode(sc, xcd_remap(blockIdx.x, gridDim.x), m0, n0, split, kchunk, zero_rest);
   const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
   const int nk = (kend - kbeg + BKF - 1) / BKF;
   const bool has_ones = WG && ones >= m0 && ones < m0 + BM;
@@ -481,6 +549,12 @@ __global__ __launch_bounds__(NTH, 1) void gemm256f_k(const OpndF a, const OpndF 
         float* o;
         if constexpr (WG) {
           o = ep.out + (int64_t)split * ep.slab_stride + (int64_t)m * ep.ldc + n;
+          if (zero_rest)
+            for (int z = split + 1; z < sc.S; ++z) {
+              float* oz = o + (int64_t)(z - split) * ep.slab_stride;
+              *(f32x4*)oz = f32x4{0.f, 0.f, 0.f, 0.f};
+              *(f32x4*)(oz + 4) = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
         } else {
           o = ep.out + (int64_t)m * ep.ldc + n;
 #pragma unroll
@@ -525,14 +599,10 @@ hipError_t launch_f(const OpndF& a, const OpndF& b, const EpiF32& ep, int M, int
       return hipErrorInvalidValue;
     attr = true;
   }
-  const int tn = (N + BN - 1) / BN, tm = (M + BM - 1) / BM;
-  int kchunk = K;
-  if (WG) {
-    kchunk = ((K + splits - 1) / splits + 63) / 64 * 64;
-    if ((K + kchunk - 1) / kchunk != splits) return hipErrorInvalidValue;
-  }
-  hipLaunchKernelGGL((gemm256f_k<AKC, BKC, WG>), dim3(tm * tn * (WG ? splits : 1)), dim3(NTH), LDS_BYTES, st, a, b,
-                     ep, M, N, K, tn, tm * tn, kchunk, ones);
+  Sched sc;
+  const int grid = make_sched(sc, M, N, K, WG, splits);
+  if (grid <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gemm256f_k<AKC, BKC, WG>), dim3(grid), dim3(NTH), LDS_BYTES, st, a, b, ep, M, N, K, sc, ones);
   return hipGetLastError();
 }
 
@@ -610,7 +680,9 @@ int gemm256_wgrad_splits(int Din, int Dout, int B, int with_bias, int cus) {
   const int tiles = ((M + BM - 1) / BM) * ((Dout + BN - 1) / BN);
   const double fill = (double)M * Dout / ((double)tiles * BM * BN);
   if (tiles < 32 || tiles > cus || fill < 0.9) return 0;
-  int s = cus / tiles;
+  // splits of the full-height tiles (make_sched gives a partial last row tile the rest)
+  const int full = (M / BM) * ((Dout + BN - 1) / BN);
+  int s = cus / (full > 0 ? full : tiles);
   while (s > 1 && B / s < 512) --s;
   // the effective count of the chunking launch_bk uses
   const int kchunk = ((B + s - 1) / s + 63) / 64 * 64;
@@ -624,12 +696,7 @@ int gemm256_wgrad_splits(int Din, int Dout, int B, int with_bias, int cus) {
 // f32.hip's 128 x 128 tiles (bench/micro_gemm256.py), its forward 761 vs 893 (1 round)
 bool gemm256f_ok(int M, int N, int K) {
   if (!gemm256_enabled() || K < 256 || (N & 7) || !fill_ok(M, N, 256)) return false;
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = -1;
-  }
+  const int cus = num_cus();
   if (cus <= 0) return false;
   const int64_t tiles = (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const int64_t rounds = (tiles + cus - 1) / cus;
@@ -661,7 +728,8 @@ int gemm256f_wgrad_splits(int Din, int Dout, int B, int cus) {
   const int M = Din + 1;
   const int tiles = ((M + BM - 1) / BM) * ((Dout + BN - 1) / BN);
   if (tiles < 32 || tiles > cus || !fill_ok(M, Dout, 32)) return 0;
-  int s = cus / tiles;
+  const int full = (M / BM) * ((Dout + BN - 1) / BN);
+  int s = cus / (full > 0 ? full : tiles);
   while (s > 1 && B / s < 512) --s;
   const int kchunk = ((B + s - 1) / s + 63) / 64 * 64;
   return (B + kchunk - 1) / kchunk;

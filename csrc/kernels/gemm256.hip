@@ -124,10 +124,11 @@ DEV void dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t lds_dst) {
 // wait until at most N of this wave's DMA instructions are outstanding
 template <int N>
 DEV void wait_dma() {
-  static_assert(N == 0 || N == 4 || N == 8 || N == 16, "");
+  static_assert(N == 0 || N == 4 || N == 8 || N == 12 || N == 16, "");
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
 }
 
@@ -175,11 +176,11 @@ DEV bf16x8 frag(const uint8_t* lds, int img, int c0, int kh, int lane) {
   }
 }
 
-template <bool AKC, bool BKC, bool WG, int BK>
+template <bool AKC, bool BKC, bool WG, int BK, int S>
 __global__ __launch_bounds__(NTH, 1) void gemm256_k(const Opnd a, const Opnd b, const GemmEpi ep, int M, int N,
                                                     int K, const Sched sc, int ones, int dbg) {
   using G = Geo<BK>;
-  constexpr int S = G::STAGES;
+  static_assert(S >= 2 && S * G::BUF <= 160 * 1024, "stage ring fits the LDS");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
@@ -213,7 +214,12 @@ __global__ __launch_bounds__(NTH, 1) void gemm256_k(const Opnd a, const Opnd b, 
     const int cur = (kt % S) * G::BUF;
     // this wave's DMA of step kt done: the stages issued after it may stay in flight
     const int ahead = min(S - 2, nk - 1 - kt);
-    if constexpr (S == 4) {
+    if constexpr (S >= 5) {
+      if (ahead >= 3) wait_dma<3 * G::DPS>();
+      else if (ahead == 2) wait_dma<2 * G::DPS>();
+      else if (ahead == 1) wait_dma<G::DPS>();
+      else wait_dma<0>();
+    } else if constexpr (S == 4) {
       if (ahead >= 2) wait_dma<2 * G::DPS>();
       else if (ahead == 1) wait_dma<G::DPS>();
       else wait_dma<0>();
@@ -315,11 +321,15 @@ __global__ __launch_bounds__(NTH, 1) void gemm256_k(const Opnd a, const Opnd b, 
 }
 
 // experiments only (set_gemm256_debug): bit 0 skips the in-loop staging (timing, wrong
-// results); bit 1 runs the 2-stage BK = 64 ring instead of the 4-stage BK = 32 one (also
-// MNISTX_GEMM256_BK=64 at load, for whole-step A/Bs)
+// results); bit 1 runs the 2-stage BK = 64 ring instead of the 4-stage BK = 32 one, bit 2 a
+// 5-stage BK = 32 ring (160 KB), bit 3 the BK = 64 ring for the data gradient only (also
+// MNISTX_GEMM256_BK=64 / MNISTX_GEMM256_STAGES=5 / MNISTX_GEMM256_DGRAD_BK=64 at load,
+// for whole-step A/Bs)
 int g_gemm256_dbg = [] {
   const char* e = getenv("MNISTX_GEMM256_BK");
-  return (e && e[0] == '6') ? 2 : 0;
+  const char* s5 = getenv("MNISTX_GEMM256_STAGES");
+  const char* dg = getenv("MNISTX_GEMM256_DGRAD_BK");
+  return ((e && e[0] == '6') ? 2 : 0) | ((s5 && s5[0] == '5') ? 4 : 0) | ((dg && dg[0] == '6') ? 8 : 0);
 }();
 
 // the CU count (cached)
@@ -358,20 +368,21 @@ int make_sched(Sched& sc, int M, int N, int K, bool wg, int splits) {
   return sc.np + tm_full * tn * splits;
 }
 
-template <bool AKC, bool BKC, bool WG, int BK>
+template <bool AKC, bool BKC, bool WG, int BK, int S>
 hipError_t launch_bk(const Opnd& a, const Opnd& b, const GemmEpi& ep, int M, int N, int K, int splits, int ones,
                      hipStream_t st) {
+  constexpr int bytes = S * Geo<BK>::BUF;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)gemm256_k<AKC, BKC, WG, BK>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            LDS_BYTES) != hipSuccess)
+    if (hipFuncSetAttribute((const void*)gemm256_k<AKC, BKC, WG, BK, S>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            bytes) != hipSuccess)
       return hipErrorInvalidValue;
     attr = true;
   }
   Sched sc;
   const int grid = make_sched(sc, M, N, K, WG, splits);   // WG: the caller's split count (its slab)
   if (grid <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm256_k<AKC, BKC, WG, BK>), dim3(grid), dim3(NTH), LDS_BYTES, st, a, b, ep, M, N, K, sc, ones,
+  hipLaunchKernelGGL((gemm256_k<AKC, BKC, WG, BK, S>), dim3(grid), dim3(NTH), bytes, st, a, b, ep, M, N, K, sc, ones,
                      g_gemm256_dbg);
   return hipGetLastError();
 }
@@ -379,8 +390,10 @@ hipError_t launch_bk(const Opnd& a, const Opnd& b, const GemmEpi& ep, int M, int
 template <bool AKC, bool BKC, bool WG>
 hipError_t launch256(const Opnd& a, const Opnd& b, const GemmEpi& ep, int M, int N, int K, int splits, int ones,
                      hipStream_t st) {
-  if (g_gemm256_dbg & 2) return launch_bk<AKC, BKC, WG, 64>(a, b, ep, M, N, K, splits, ones, st);
-  return launch_bk<AKC, BKC, WG, 32>(a, b, ep, M, N, K, splits, ones, st);
+  if ((g_gemm256_dbg & 2) || ((g_gemm256_dbg & 8) && AKC && BKC))
+    return launch_bk<AKC, BKC, WG, 64, 2>(a, b, ep, M, N, K, splits, ones, st);
+  if (g_gemm256_dbg & 4) return launch_bk<AKC, BKC, WG, 32, 5>(a, b, ep, M, N, K, splits, ones, st);
+  return launch_bk<AKC, BKC, WG, 32, 4>(a, b, ep, M, N, K, splits, ones, st);
 }
 
 bool sizes_ok(int64_t rows, int ld, int K, int R) {

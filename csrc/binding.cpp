@@ -91,22 +91,25 @@ int64_t eff_splits(int64_t K, int64_t splits) {
 }
 
 void dense_fwd(Tensor x, Tensor w, Tensor out, int64_t M, int64_t N, int64_t K, int64_t ldx, int64_t ldw,
-               int64_t ldc, optional<Tensor> bias, int64_t bias_n, bool relu, optional<Tensor> mask, int64_t ldm) {
+               int64_t ldc, optional<Tensor> bias, int64_t bias_n, bool relu, optional<Tensor> mask, int64_t ldm,
+               int64_t tile) {
   check(x, at::kBFloat16, span(M, ldx, K), "x");
   check(w, at::kBFloat16, span(K, ldw, N), "w");
   TORCH_CHECK(ldx >= K && ldw >= N, "bad leading dims");
   auto ep = make_epi(out, M, N, ldc, bias, bias_n, relu, mask, ldm);
-  hip_ok(mnistx::dense_fwd(BF(x), BF(w), (int)M, (int)N, (int)K, (int)ldx, (int)ldw, ep, cur_stream()), "dense_fwd");
+  hip_ok(mnistx::dense_fwd(BF(x), BF(w), (int)M, (int)N, (int)K, (int)ldx, (int)ldw, ep, cur_stream(), (int)tile),
+         "dense_fwd");
 }
 
 void dense_dgrad(Tensor dy, Tensor w, Tensor out, int64_t M, int64_t N, int64_t K, int64_t lddy, int64_t ldw,
-                 int64_t ldc, optional<Tensor> mask, int64_t ldm) {
+                 int64_t ldc, optional<Tensor> mask, int64_t ldm, int64_t tile) {
   // out[M, N=Din] = dy[M, K=Dout] . W[Din, Dout]^T
   check(dy, at::kBFloat16, span(M, lddy, K), "dy");
   check(w, at::kBFloat16, span(N, ldw, K), "w");
   TORCH_CHECK(lddy >= K && ldw >= K, "bad leading dims");
   auto ep = make_epi(out, M, N, ldc, c10::nullopt, 0, false, mask, ldm);
-  hip_ok(mnistx::dense_dgrad(BF(dy), BF(w), (int)M, (int)N, (int)K, (int)lddy, (int)ldw, ep, cur_stream()),
+  hip_ok(mnistx::dense_dgrad(BF(dy), BF(w), (int)M, (int)N, (int)K, (int)lddy, (int)ldw, ep, cur_stream(),
+                             (int)tile),
          "dense_dgrad");
 }
 
@@ -1189,8 +1192,14 @@ PYBIND11_MODULE(_kernels, m) {
   });
   m.def("grid_cap", []() { return (int64_t)mnistx::grid_cap(); });
   m.doc() = "MI355X (gfx950) HIP kernels for the MNIST trainer";
-  m.def("dense_fwd", &dense_fwd);
-  m.def("dense_dgrad", &dense_dgrad);
+  m.def("dense_fwd", &dense_fwd, py::arg("x"), py::arg("w"), py::arg("out"), py::arg("M"), py::arg("N"), py::arg("K"),
+        py::arg("ldx"), py::arg("ldw"), py::arg("ldc"), py::arg("bias"), py::arg("bias_n"), py::arg("relu"),
+        py::arg("mask"), py::arg("ldm"), py::arg("tile") = -1);
+  m.def("dense_dgrad", &dense_dgrad, py::arg("dy"), py::arg("w"), py::arg("out"), py::arg("M"), py::arg("N"),
+        py::arg("K"), py::arg("lddy"), py::arg("ldw"), py::arg("ldc"), py::arg("mask"), py::arg("ldm"),
+        py::arg("tile") = -1);
+  m.def("set_tile192", [](int64_t on) { mnistx::set_tile192((int)on); },
+        "A/B switch of gemm.hip's 192-column tiles (MNISTX_TILE192)");
   m.def("dense_wgrad", &dense_wgrad, py::arg("x"), py::arg("dy"), py::arg("slab"), py::arg("Din"), py::arg("Dout"),
         py::arg("B"), py::arg("ldx"), py::arg("lddy"), py::arg("with_bias"), py::arg("splits"), py::arg("tile") = -1);
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("out"), py::arg("Nb"), py::arg("H"), py::arg("W"),

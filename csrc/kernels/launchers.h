@@ -82,10 +82,12 @@ hipError_t gemm256_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, i
 // ---- gemm.hip
 // tile (BM, BN) launch_any picks for an M x N output (wgrad: both operands MN-contiguous)
 void gemm_tile(int M, int N, int wgrad, int* bm, int* bn);
+// tile >= 0: that launch_any tile code (benches / tests), skipping the gemm256 route
 hipError_t dense_fwd(const bf16_t* x, const bf16_t* w, int M, int N, int K, int ldx, int ldw,
-                     const GemmEpi& ep, hipStream_t st);
+                     const GemmEpi& ep, hipStream_t st, int tile = -1);
 hipError_t dense_dgrad(const bf16_t* dy, const bf16_t* w, int M, int N, int K, int lddy, int ldw,
-                       const GemmEpi& ep, hipStream_t st);
+                       const GemmEpi& ep, hipStream_t st, int tile = -1);
+void set_tile192(int on);   // A/B switch of the 192-column tiles (MNISTX_TILE192)
 // used (optional): the split count actually written -- the 256 x 256 path (tile < 0, used set)
 // may write fewer partials than `splits` (the slab's capacity); the reduce must use *used
 hipError_t dense_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int B, int ldx, int lddy,

@@ -91,7 +91,8 @@ def test_dense_wgrad(dev, K, B, Din, Dout, splits):
 @pytest.mark.parametrize("M,N,Kd,tile", [(262144, 16, 88, (256, 16)), (262144, 32, 40, (256, 32)),
                                          (131072, 64, 64, (128, 64)), (131072, 128, 64, (128, 128)),
                                          (65536, 128, 400, (64, 128)), (4000, 64, 72, (64, 64)),
-                                         (9000, 24, 48, (64, 32)), (1000, 10, 40, (64, 16))])
+                                         (9000, 24, 48, (64, 32)), (1000, 10, 40, (64, 16)),
+                                         (65536, 192, 72, (64, 192)), (2000, 184, 40, (32, 192))])
 def test_gemm_tile_codes(dev, K, M, N, Kd, tile):
     assert tuple(K.gemm_tile(M, N, False)) == tile
     torch.manual_seed(5)

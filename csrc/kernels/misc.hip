@@ -672,7 +672,7 @@ __global__ __launch_bounds__(256) void splitk_partial4_k(RedTable tab) {
 // L2 norm needed for the weight-decay loss is reduced in the workgroup and added
 // with a single atomic per workgroup.
 constexpr int MAXSEG = 16;
-constexpr int OPT_EPT = 2;                       // elements per thread (more, shorter blocks: latency)
+constexpr int OPT_EPT = 2;                       // elements per thread: one consecutive pair (fused_opt_k)
 constexpr int OPT_CHUNK = TPB * OPT_EPT;         // elements per workgroup
 struct SegTable {
   OptSeg s[MAXSEG];
@@ -703,48 +703,102 @@ __global__ __launch_bounds__(TPB) void fused_opt_k(float* __restrict__ params, c
   const int64_t lo = (int64_t)(blockIdx.x - tab.blk0[si]) * OPT_CHUNK;
   const int64_t ij = (int64_t)sg.I * sg.J;
   float sq = 0.f;
-  // every element's loads issued before any use (one memory round trip per thread, not
-  // one per element); out-of-range slots load element 0 and are never stored
+  // each thread owns a PAIR of consecutive elements (8-byte loads / stores of params, grads,
+  // momentum and EMA; one 4-byte bf16 store when the pair stays in one row of the padded
+  // copy), all loads issued before any use; the pair falls back to two scalar accesses in a
+  // segment at an odd offset.  Out-of-range elements load element 0 and are never stored.
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  const int64_t li0 = lo + 2 * (int64_t)threadIdx.x;
+  const bool vec = (sg.off & 1) == 0 && li0 + 1 < sg.n;
   float pv[OPT_EPT], gv[OPT_EPT], mv[OPT_EPT], ev[OPT_EPT];
+  if (vec) {
+    const int64_t e = sg.off + li0;
+    const f32x2_t p2 = *(const f32x2_t*)(params + e), g2 = *(const f32x2_t*)(grads + e);
+    const f32x2_t m2 = op.use_momentum ? *(const f32x2_t*)(mom + e) : f32x2_t{0.f, 0.f};
+    const f32x2_t e2 = op.ema_max >= 0.f ? *(const f32x2_t*)(ema + e) : f32x2_t{0.f, 0.f};
 #pragma unroll
-  for (int u = 0; u < OPT_EPT; ++u) {
-    const int64_t li = lo + u * TPB + threadIdx.x;
-    const int64_t e = sg.off + (li < sg.n ? li : 0);
-    pv[u] = params[e];
-    gv[u] = grads[e];
-    mv[u] = op.use_momentum ? mom[e] : 0.f;
-    ev[u] = op.ema_max >= 0.f ? ema[e] : 0.f;
+    for (int u = 0; u < OPT_EPT; ++u) {
+      pv[u] = p2[u];
+      gv[u] = g2[u];
+      mv[u] = m2[u];
+      ev[u] = e2[u];
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < OPT_EPT; ++u) {
+      const int64_t li = li0 + u;
+      const int64_t e = sg.off + (li < sg.n ? li : 0);
+      pv[u] = params[e];
+      gv[u] = grads[e];
+      mv[u] = op.use_momentum ? mom[e] : 0.f;
+      ev[u] = op.ema_max >= 0.f ? ema[e] : 0.f;
+    }
   }
+  float po[OPT_EPT], mo[OPT_EPT], eo[OPT_EPT];
 #pragma unroll
   for (int u = 0; u < OPT_EPT; ++u) {
-    const int64_t li = lo + u * TPB + threadIdx.x;
-    if (li >= sg.n) continue;
-    const int64_t e = sg.off + li;
     float p = pv[u];
-    sq += p * p;
+    if (li0 + u < sg.n) sq += p * p;
     const float g = gv[u] * op.grad_scale + sg.wd * p;
     float upd = g;
+    mo[u] = 0.f;
     if (op.use_momentum) {
       const float v = mv[u] * op.momentum + g;
-      mom[e] = v;
+      mo[u] = v;
       upd = op.nesterov ? g + op.momentum * v : v;
     }
     p -= lr * upd;
-    params[e] = p;
-    if (op.ema_max >= 0.f) {
-      const float s = ev[u];
-      ema[e] = s - (1.f - ema_d) * (s - p);
+    po[u] = p;
+    eo[u] = op.ema_max >= 0.f ? ev[u] - (1.f - ema_d) * (ev[u] - p) : 0.f;
+  }
+  if (vec) {
+    const int64_t e = sg.off + li0;
+    *(f32x2_t*)(params + e) = f32x2_t{po[0], po[1]};
+    if (op.use_momentum) *(f32x2_t*)(mom + e) = f32x2_t{mo[0], mo[1]};
+    if (op.ema_max >= 0.f) *(f32x2_t*)(ema + e) = f32x2_t{eo[0], eo[1]};
+  } else {
+#pragma unroll
+    for (int u = 0; u < OPT_EPT; ++u) {
+      if (li0 + u >= sg.n) continue;
+      const int64_t e = sg.off + li0 + u;
+      params[e] = po[u];
+      if (op.use_momentum) mom[e] = mo[u];
+      if (op.ema_max >= 0.f) ema[e] = eo[u];
     }
-    if (sg.bf_off >= 0) {
-      // 32-bit magic-number divisions (segments < 2^31 elements): the 64-bit divides
-      // here were most of this kernel's time on the 3.2M-element local3 weights
-      const int l32 = (int)li;
+  }
+  if (sg.bf_off >= 0) {
+    // 32-bit magic-number divisions (segments < 2^31 elements): the 64-bit divides here
+    // were most of this kernel's time on the 3.2M-element local3 weights
+    int64_t bi[OPT_EPT];
+    int jj0 = 0, ii0 = 0;
+#pragma unroll
+    for (int u = 0; u < OPT_EPT; ++u) {
+      const int l32 = (int)(li0 + u);
       const int gg = tab.fij[si].div(l32);
       const int rem = l32 - gg * (int)ij;
       const int ii = tab.fj[si].div(rem), jj = rem - ii * sg.J;
-      const bf16_t pb = f2bf(p);
-      bf[sg.bf_off + ((int64_t)gg * sg.Ip + ii) * sg.Jp + jj] = pb;
-      if (sg.bft_off >= 0) bf[sg.bft_off + (int64_t)jj * sg.It + ii] = pb;  // W^T copy (fused dense head)
+      bi[u] = sg.bf_off + ((int64_t)gg * sg.Ip + ii) * sg.Jp + jj;
+      if (u == 0) {
+        jj0 = jj;
+        ii0 = ii;
+      }
+    }
+    const bf16_t b0 = f2bf(po[0]), b1 = f2bf(po[1]);
+    if (vec && bi[1] == bi[0] + 1 && (bi[0] & 1) == 0) {
+      *(uint32_t*)(bf + bi[0]) = (uint32_t)b0 | ((uint32_t)b1 << 16);
+    } else {
+      if (li0 < sg.n) bf[bi[0]] = b0;
+      if (li0 + 1 < sg.n) bf[bi[1]] = b1;
+    }
+    if (sg.bft_off >= 0) {   // W^T copy (fused dense head): scattered 2-byte stores
+      if (li0 < sg.n) bf[sg.bft_off + (int64_t)jj0 * sg.It + ii0] = b0;
+      if (li0 + 1 < sg.n) {
+        const int l32 = (int)(li0 + 1);
+        const int gg = tab.fij[si].div(l32);
+        const int rem = l32 - gg * (int)ij;
+        const int ii = tab.fj[si].div(rem), jj = rem - ii * sg.J;
+        bf[sg.bft_off + (int64_t)jj * sg.It + ii] = b1;
+      }
     }
   }
   if (l2 && sg.track_l2) {

@@ -654,18 +654,8 @@ hipError_t f32_dense_dgrad(const float* dy, const float* w, int M, int Din, int 
                     store_epi(dx, Din, nullptr, 0, 0, mask, Din), st);
 }
 
-static int num_cus() {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = -1;
-  }
-  return cus;
-}
-
 int f32_wgrad_splits_cap(int Din, int Dout, int B) {
-  const int cus = num_cus();
+  const int cus = gemm256_cus();
   return cus > 0 ? gemm256f_wgrad_splits(Din, Dout, B, cus) : 0;
 }
 

@@ -791,13 +791,7 @@ hipError_t dense_wgrad(const bf16_t* x, const bf16_t* dy, int Din, int Dout, int
   if (tile < 0 && used) {
     // the GEMMs that fill the GPU on 256 x 256 tiles: gemm256's own split count (one round
     // of blocks), when the caller's slab holds that many partials
-    static int cus = 0;
-    if (cus == 0) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus = -1;
-    }
+    const int cus = gemm256_cus();
     const int s2 = cus > 0 ? gemm256_wgrad_splits(Din, Dout, B, with_bias, cus) : 0;
     if (s2 > 0 && s2 <= splits) {
       *used = s2;

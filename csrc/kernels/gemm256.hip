@@ -332,7 +332,9 @@ int g_gemm256_dbg = [] {
   return ((e && e[0] == '6') ? 2 : 0) | ((s5 && s5[0] == '5') ? 4 : 0) | ((dg && dg[0] == '6') ? 8 : 0);
 }();
 
-// the CU count (cached)
+// the CUs a launch can count on: all of them less the ones reserved for a collective running
+// beside it (set_reserve_cus, data-parallel runs with world > 1).  A one-round grid of 256
+// blocks on 248 free CUs would run as TWO rounds.
 int num_cus() {
   static int cus = 0;
   if (cus == 0) {
@@ -340,7 +342,15 @@ int num_cus() {
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = -1;
   }
-  return cus;
+  if (cus <= 0) return cus;
+  const int r = reserve_cus();
+  return (r > 0 && cus - r >= 1) ? cus - r : cus;
+}
+
+// fraction of the last round of `tiles` one-per-CU blocks that is busy
+double round_fill(int64_t tiles, int cus) {
+  const int64_t rounds = (tiles + cus - 1) / cus;
+  return (double)tiles / (double)(rounds * cus);
 }
 
 // Schedule of an M x N x K launch; WG: `splits` for the full-height row tiles (the caller's
@@ -630,6 +640,8 @@ bool fill_ok(int M, int N, int min_tiles) {
 
 }  // namespace
 
+int gemm256_cus() { return num_cus(); }
+
 // Routing switch (A/B): MNISTX_GEMM256=0 starts with every dense GEMM on gemm.hip;
 // set_gemm256 flips it at run time (tests and benches compare both paths in one process).
 static int g_gemm256 = -1;
@@ -649,7 +661,11 @@ bool gemm256_ok(int M, int N, int K, const GemmEpi& ep) {
   if (!gemm256_enabled() || ep.mode == EPI_SLAB || K < 512) return false;   // >= 8 K steps of 64
   const int64_t tiles = (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const double fill = (double)M * N / ((double)tiles * BM * BN);
-  return tiles >= 256 && fill >= 0.9 && (N & 7) == 0 && (ep.ldc & 7) == 0 && ((uintptr_t)ep.out & 15) == 0 &&
+  const int cus = num_cus();
+  // the last round >= 80 % busy (local3 dgrad: 832 tiles = 3.25 rounds of 256 measured faster
+  // than gemm.hip; local3 forward, 256 tiles, would be 2 rounds on 248 free CUs)
+  return tiles >= 256 && fill >= 0.9 && cus > 0 && round_fill(tiles, cus) >= 0.8 && (N & 7) == 0 &&
+         (ep.ldc & 7) == 0 && ((uintptr_t)ep.out & 15) == 0 &&
          (ep.mask == nullptr || ((ep.ldm & 7) == 0 && ((uintptr_t)ep.mask & 15) == 0));
 }
 
@@ -711,9 +727,7 @@ bool gemm256f_ok(int M, int N, int K) {
   if (!gemm256_enabled() || K < 256 || (N & 7) || !fill_ok(M, N, 256)) return false;
   const int cus = num_cus();
   if (cus <= 0) return false;
-  const int64_t tiles = (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  const int64_t rounds = (tiles + cus - 1) / cus;
-  return (double)tiles / (double)(rounds * cus) >= 0.9;
+  return round_fill((int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN), cus) >= 0.9;
 }
 
 // y[M, N] = x[M, K] . W[K, N] (+ bias, ReLU)

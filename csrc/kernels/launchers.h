@@ -66,6 +66,7 @@ hipError_t gemm256_fwd(const bf16_t* x, const bf16_t* w, int M, int N, int K, in
                        hipStream_t st);
 hipError_t gemm256_dgrad(const bf16_t* dy, const bf16_t* w, int M, int N, int K, int lddy, int ldw, const GemmEpi& ep,
                          hipStream_t st);
+int gemm256_cus();   // CUs a gemm256 grid can count on (all less reserve_cus())
 int gemm256_wgrad_splits(int Din, int Dout, int B, int with_bias, int cus);   // 0: not this path
 // fp32 twins (f32_dense_* route here when gemm256f_ok / gemm256f_wgrad_splits > 0)
 bool gemm256f_ok(int M, int N, int K);

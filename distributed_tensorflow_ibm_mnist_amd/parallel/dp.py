@@ -43,7 +43,10 @@ Design for MI355X:
 * with world > 1 and more than one bucket, ``DataParallel`` reserves ``RESERVE_CUS`` = 8
   CUs from the persistent kernels for the whole step so the early buckets' all-reduce
   kernels are never locked out (cost per kernel: interleaved A/B in
-  ``profiles/r5/dp_coresidency/``); one GPU and one-bucket plans reserve nothing;
+  ``profiles/r5/dp_coresidency/``); one GPU and one-bucket plans reserve nothing.  The
+  one-block-per-tile GEMMs size themselves for the CUs left too (``gemm256.hip``
+  ``num_cus``): local3's forward (256 tiles = one round of 256 CUs, two of 248) goes back
+  to gemm.hip's finer tiles, and the split-K weight gradient recounts its splits;
 * split-K weight-gradient reduces of a bucket's layers are flushed as ONE
   multi-tensor launch just before its all-reduce (``HipNet.hook_layers``);
 * ``work.wait()`` only makes the compute stream wait (no host block); the

@@ -170,3 +170,29 @@ def test_gemm256_f32_wgrad_bias_row(K, B, Din, Dout):
     # fp32 sums over K = B rows (1.1e-6 measured at B = 16384; f32.hip's tests use 1e-5)
     assert _rel64(tot[:Din], x.double().t() @ dy.double()) < 1e-5
     assert _rel64(tot[Din], dy.double().sum(0)) < 1e-5
+
+
+def test_gemm256_respects_reserved_cus(K):
+    """With CUs reserved for a collective (data-parallel, world > 1), gemm256 sizes its split
+    counts for the CUs left (local3's weight gradient: 248 // 48 full tiles = 5 splits) and
+    routes no one-round grid that would spill into a second round; results unchanged."""
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(11)
+    B, Din, Dout = 16384, 3136, 1024
+    x = torch.randn(B, Din, device=dev, generator=g).to(torch.bfloat16)
+    dy = torch.randn(B, Dout, device=dev, generator=g).to(torch.bfloat16)
+    w = (torch.randn(Din, Dout, device=dev, generator=g) / Din ** 0.5).to(torch.bfloat16)
+    slab = torch.full((8 * (Din + 1) * Dout,), float("nan"), device=dev)
+    y = torch.empty(B, Dout, device=dev, dtype=torch.bfloat16)
+    K.set_reserve_cus(8)
+    try:
+        S = K.dense_wgrad(x, dy, slab, Din, Dout, B, Din, Dout, True, 8)
+        K.dense_fwd(x, w, y, B, Dout, Din, Din, Dout, Dout, None, 0, False, None, 0)
+        torch.cuda.synchronize()
+    finally:
+        K.set_reserve_cus(0)
+    assert S == 5
+    tot = slab.view(8, Din + 1, Dout)[:S].sum(0)
+    ref = torch.cat([x.float().t() @ dy.float(), dy.float().sum(0, keepdim=True)], 0)
+    assert _rel(tot, ref) < 1e-4
+    assert _rel(y, x.float() @ w.float()) < 1e-2

@@ -59,8 +59,8 @@ def main():
 
     cases = {"fwd_gemm256_no_dma": dbg(fwd(True), 1),
              "wgrad_gemm256": wgrad(True), "wgrad_gemm256_bk64": dbg(wgrad(True), 2),
-             "wgrad_gemm256_s5": dbg(wgrad(True), 4), "fwd_gemm256_s5": dbg(fwd(True), 4),
-             "dgrad_gemm256_s5": dbg(dgrad(True), 4),
+             "wgrad_gemm256_rp": dbg(wgrad(True), 16), "fwd_gemm256_rp": dbg(fwd(True), 16),
+             "dgrad_gemm256_rp": dbg(dgrad(True), 16),
              "wgrad_gemm_hip": wgrad(False), "wgrad_torch_matmul": lambda: torch.matmul(x.t(), dy),
              "fwd_gemm256": fwd(True), "fwd_gemm256_bk64": dbg(fwd(True), 2), "fwd_gemm_hip": fwd(False),
              "fwd_torch_matmul": lambda: torch.matmul(x, w, out=y),

@@ -176,7 +176,7 @@ DEV bf16x8 frag(const uint8_t* lds, int img, int c0, int kh, int lane) {
   }
 }
 
-template <bool AKC, bool BKC, bool WG, int BK, int S>
+template <bool AKC, bool BKC, bool WG, int BK, int S, bool RP = false>
 __global__ __launch_bounds__(NTH, 1) void gemm256_k(const Opnd a, const Opnd b, const GemmEpi ep, int M, int N,
                                                     int K, const Sched sc, int ones, int dbg) {
   using G = Geo<BK>;
@@ -207,9 +207,82 @@ __global__ __launch_bounds__(NTH, 1) void gemm256_k(const Opnd a, const Opnd b, 
     stage<BK, AKC>(lds_base, buf, a, m0, kbeg + kt * BK, kend, wave, lane);
     stage<BK, BKC>(lds_base, buf + G::IMG, b, n0, kbeg + kt * BK, kend, wave, lane);
   };
+  auto patch_ones = [&](int kt) {   // this wave's own DMA chunks of the ones column of stage kt
+    if constexpr (WG) {
+      if (has_ones) {
+        const int buf = (kt % S) * G::BUF;
+#pragma unroll
+        for (int u = 0; u < G::NI; ++u) {
+          const int i = wave + 8 * u, row = 2 * i + (lane >> 5), ch = (lane & 31) ^ mn_swz(row);
+          if (m0 + 8 * ch == ones && kbeg + kt * BK + row < kend)
+            *(bf16_t*)(lds + buf + 1024 * i + 16 * lane) = (bf16_t)0x3f80;   // the lane's DMA slot
+        }
+      }
+    }
+  };
 #pragma unroll
   for (int p = 0; p < S - 1; ++p)
     if (p < nk) issue(p);
+  if constexpr (RP) {
+    // Register-prefetch schedule (one 32-deep k-half per step): the fragments of step kt + 1
+    // are read from LDS while the MFMAs of step kt run, so no step starts on a ds_read
+    // latency.  At the top of step kt each wave waits for ITS DMA of stage kt + 1 (stage
+    // kt + 2 may stay in flight), patches, and the barrier makes every wave's stage kt + 1
+    // visible; the DMA of stage kt + 3 then refills the slot of stage kt - 1, whose
+    // fragments were read during step kt - 2 and consumed before this barrier.
+    static_assert(S == 4 && BK == 32, "register prefetch: the 4 x 32-deep ring");
+    // prefetched per step: the B fragments and the first PH A fragments (2 x 24 VGPRs next to
+    // the 128 accumulators; a full second fragment set spilled); the other A fragments are
+    // read at the step's start, behind the PH x FN MFMAs that need none of them
+    constexpr int PH = 2;
+    bf16x8 pa0[PH], pb0[FN], pa1[PH], pb1[FN];
+    auto rd = [&](int kt, bf16x8 (&pa)[PH], bf16x8 (&pb)[FN]) {
+      const int buf = (kt % S) * G::BUF;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) pb[j] = frag<BK, BKC>(lds, buf + G::IMG, wn * TN + 16 * j, 0, lane);
+#pragma unroll
+      for (int i = 0; i < PH; ++i) pa[i] = frag<BK, AKC>(lds, buf, wm * TM + 16 * i, 0, lane);
+    };
+    auto mm = [&](int kt, const bf16x8 (&pa)[PH], const bf16x8 (&pb)[FN]) {
+      const int buf = (kt % S) * G::BUF;
+      bf16x8 fa[FM];
+#pragma unroll
+      for (int i = PH; i < FM; ++i) fa[i] = frag<BK, AKC>(lds, buf, wm * TM + 16 * i, 0, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(i < PH ? pa[i < PH ? i : 0] : fa[i], pb[j], acc[i][j], 0, 0, 0);
+    };
+    // stages 0 and 1 landed (stage 2 may stay in flight), visible to every wave
+    if (nk > 2) wait_dma<G::DPS>();
+    else wait_dma<0>();
+    patch_ones(0);
+    if (nk > 1) patch_ones(1);
+    __syncthreads();
+    rd(0, pa0, pb0);
+    // step kt: the barrier makes stage kt + 1 visible; the rest of step kt's A fragments
+    // (its slot visible since step kt - 1's barrier) are read inside mm, after the prefetch
+    auto step = [&](int kt, bf16x8 (&pa)[PH], bf16x8 (&pb)[FN], bf16x8 (&na)[PH], bf16x8 (&nb)[FN]) {
+      if (kt + 1 < nk) {
+        if (kt >= 1) {   // stage kt + 1 (issued two steps ago); kt + 2 may stay in flight
+          if (kt + 2 < nk) wait_dma<G::DPS>();
+          else wait_dma<0>();
+          patch_ones(kt + 1);
+        }
+        __syncthreads();
+        if (kt + 3 < nk && !(dbg & 1)) issue(kt + 3);
+        rd(kt + 1, na, nb);
+      }
+      mm(kt, pa, pb);
+    };
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+      step(kt, pa0, pb0, pa1, pb1);
+      step(kt + 1, pa1, pb1, pa0, pb0);
+    }
+    if (kt < nk) step(kt, pa0, pb0, pa1, pb1);
+  } else
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = (kt % S) * G::BUF;
     // this wave's DMA of step kt done: the stages issued after it may stay in flight
@@ -226,16 +299,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm256_k(const Opnd a, const Opnd b, 
     } else {
       wait_dma<0>();
     }
-    if constexpr (WG) {
-      if (has_ones) {   // this wave's own DMA chunks of the ones column (its wait above ordered them)
-#pragma unroll
-        for (int u = 0; u < G::NI; ++u) {
-          const int i = wave + 8 * u, row = 2 * i + (lane >> 5), ch = (lane & 31) ^ mn_swz(row);
-          if (m0 + 8 * ch == ones && kbeg + kt * BK + row < kend)
-            *(bf16_t*)(lds + cur + 1024 * i + 16 * lane) = (bf16_t)0x3f80;   // the lane's DMA slot
-        }
-      }
-    }
+    patch_ones(kt);    // (its wait above ordered this wave's DMA)
     __syncthreads();   // step kt's images landed (every wave's DMA); step kt - 1's reads done
     if (kt + S - 1 < nk && !(dbg & 1)) issue(kt + S - 1);   // into the slot step kt - 1 read
 #pragma unroll
@@ -322,14 +386,17 @@ __global__ __launch_bounds__(NTH, 1) void gemm256_k(const Opnd a, const Opnd b, 
 
 // experiments only (set_gemm256_debug): bit 0 skips the in-loop staging (timing, wrong
 // results); bit 1 runs the 2-stage BK = 64 ring instead of the 4-stage BK = 32 one, bit 2 a
-// 5-stage BK = 32 ring (160 KB), bit 3 the BK = 64 ring for the data gradient only (also
-// MNISTX_GEMM256_BK=64 / MNISTX_GEMM256_STAGES=5 / MNISTX_GEMM256_DGRAD_BK=64 at load,
+// 5-stage BK = 32 ring (160 KB), bit 3 the BK = 64 ring for the data gradient only, bit 4 the
+// register-prefetch schedule (also MNISTX_GEMM256_BK=64 / MNISTX_GEMM256_STAGES=5 /
+// MNISTX_GEMM256_DGRAD_BK=64 / MNISTX_GEMM256_RP=1 at load,
 // for whole-step A/Bs)
 int g_gemm256_dbg = [] {
   const char* e = getenv("MNISTX_GEMM256_BK");
   const char* s5 = getenv("MNISTX_GEMM256_STAGES");
   const char* dg = getenv("MNISTX_GEMM256_DGRAD_BK");
-  return ((e && e[0] == '6') ? 2 : 0) | ((s5 && s5[0] == '5') ? 4 : 0) | ((dg && dg[0] == '6') ? 8 : 0);
+  const char* rp = getenv("MNISTX_GEMM256_RP");
+  return ((e && e[0] == '6') ? 2 : 0) | ((s5 && s5[0] == '5') ? 4 : 0) | ((dg && dg[0] == '6') ? 8 : 0) |
+         ((rp && rp[0] == '1') ? 16 : 0);
 }();
 
 // the CUs a launch can count on: all of them less the ones reserved for a collective running
@@ -378,13 +445,13 @@ int make_sched(Sched& sc, int M, int N, int K, bool wg, int splits) {
   return sc.np + tm_full * tn * splits;
 }
 
-template <bool AKC, bool BKC, bool WG, int BK, int S>
+template <bool AKC, bool BKC, bool WG, int BK, int S, bool RP = false>
 hipError_t launch_bk(const Opnd& a, const Opnd& b, const GemmEpi& ep, int M, int N, int K, int splits, int ones,
                      hipStream_t st) {
   constexpr int bytes = S * Geo<BK>::BUF;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)gemm256_k<AKC, BKC, WG, BK, S>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)gemm256_k<AKC, BKC, WG, BK, S, RP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             bytes) != hipSuccess)
       return hipErrorInvalidValue;
     attr = true;
@@ -392,7 +459,7 @@ hipError_t launch_bk(const Opnd& a, const Opnd& b, const GemmEpi& ep, int M, int
   Sched sc;
   const int grid = make_sched(sc, M, N, K, WG, splits);   // WG: the caller's split count (its slab)
   if (grid <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm256_k<AKC, BKC, WG, BK, S>), dim3(grid), dim3(NTH), bytes, st, a, b, ep, M, N, K, sc, ones,
+  hipLaunchKernelGGL((gemm256_k<AKC, BKC, WG, BK, S, RP>), dim3(grid), dim3(NTH), bytes, st, a, b, ep, M, N, K, sc, ones,
                      g_gemm256_dbg);
   return hipGetLastError();
 }
@@ -403,6 +470,7 @@ hipError_t launch256(const Opnd& a, const Opnd& b, const GemmEpi& ep, int M, int
   if ((g_gemm256_dbg & 2) || ((g_gemm256_dbg & 8) && AKC && BKC))
     return launch_bk<AKC, BKC, WG, 64, 2>(a, b, ep, M, N, K, splits, ones, st);
   if (g_gemm256_dbg & 4) return launch_bk<AKC, BKC, WG, 32, 5>(a, b, ep, M, N, K, splits, ones, st);
+  if (g_gemm256_dbg & 16) return launch_bk<AKC, BKC, WG, 32, 4, true>(a, b, ep, M, N, K, splits, ones, st);
   return launch_bk<AKC, BKC, WG, 32, 4>(a, b, ep, M, N, K, splits, ones, st);
 }
 

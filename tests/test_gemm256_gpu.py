@@ -19,7 +19,7 @@ def _rel(a, b):
     return float((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-12))
 
 
-@pytest.fixture(params=[0, 2, 4], ids=["bk32_4stage", "bk64_2stage", "bk32_5stage"])
+@pytest.fixture(params=[0, 2, 4, 16], ids=["bk32_4stage", "bk64_2stage", "bk32_5stage", "bk32_4stage_rp"])
 def ring(request, K):
     """gemm256's K-step ring: the default 4 x 32-deep stages, or 2 x 64 (set_gemm256_debug bit 1)."""
     K.set_gemm256_debug(request.param)

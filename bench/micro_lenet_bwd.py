@@ -123,16 +123,28 @@ def main():
         skip_us[sk] = round(timeit(lambda: K.lenet_bwd(ds, P1, dP2, A2, w2, B, s1, s2, grid, idx=idx,
                                                        prof=pr_buf)), 1)
     os.environ.pop("MNISTX_BWD_SKIP", None)
-    prof = torch.zeros(8, dtype=torch.int64, device=dev)
+    os.environ["MNISTX_BWD_PROF_WAVES"] = "1"      # [8 phases] + [16 waves][8 phases]
+    prof = torch.zeros(8 + 16 * 8, dtype=torch.int64, device=dev)
     K.lenet_bwd(ds, P1, dP2, A2, w2, B, s1, s2, grid, idx=idx, prof=prof)
     torch.cuda.synchronize()
-    pr = prof.tolist()
+    os.environ.pop("MNISTX_BWD_PROF_WAVES", None)
+    allp = prof.tolist()
+    pr = allp[:8]
+    # per wave: phase-1 work (staging, dgrad, conv2 wgrad) and phase-2 work (next-tile issue,
+    # conv1 wgrad + dY2 store) as shares of the wave's total, and the waits
+    per_wave = []
+    for w in range(16):
+        v = allp[8 + 8 * w: 16 + 8 * w]
+        t = max(1, sum(v))
+        per_wave.append({"p1": round((v[0] + v[1] + v[2]) / t, 3), "bar1": round(v[3] / t, 3),
+                         "p2": round((v[4] + v[5]) / t, 3), "bar2": round(v[6] / t, 3)})
     tot = max(1, sum(pr))
     print(json.dumps({"B": B, "grid": grid, "fused_us": round(fused, 1), "fused_cold_us": round(fused_cold, 1), "after_band_us": after_band,
                       "after_band_150MB_us": after_band_traffic, "after_150MB_us": after_traffic, "band_fwd_us": round(band, 1), "fused_u8_us": round(fused_u8, 1), "fused_us_by_batch": scaling, "prof_us_by_skip": skip_us,
                       "split_us": {"c2_dgrad": round(dgr, 1), "c2_wgrad": round(w2g, 1), "c1_wgrad": round(w1g, 1),
                                    "sum": round(dgr + w2g + w1g, 1)},
-                      "phase_share": {k: round(v / tot, 3) for k, v in zip(PHASES, pr)}}), flush=True)
+                      "phase_share": {k: round(v / tot, 3) for k, v in zip(PHASES, pr)},
+                      "per_wave": per_wave}), flush=True)
 
 
 if __name__ == "__main__":

@@ -850,7 +850,8 @@ void lenet_bwd(Tensor x, Tensor p1, Tensor dp2, Tensor arg2, Tensor w2, int64_t 
   check(slab2, at::kFloat, grid * 208 * 16, "slab2");
   unsigned long long* pr = nullptr;
   if (prof.has_value() && prof->defined()) {
-    check(*prof, at::kLong, 8, "prof");
+    const char* pw = getenv("MNISTX_BWD_PROF_WAVES");
+    check(*prof, at::kLong, (pw && pw[0] == '1') ? 8 + 16 * 8 : 8, "prof");
     pr = P<unsigned long long>(*prof);
   }
   hip_ok(mnistx::lenet_bwd(src, BF(p1), BF(dp2), P<const uint8_t>(arg2), BF(w2), (int)B, P<float>(slab1),

@@ -98,6 +98,7 @@ struct BwdArgs {
   float* slab2;           // [grid][208][16]: rows tap * 8 + ci, 200 = bias
   unsigned long long* prof;   // optional (experiments): per-phase clock sums [NPROF] over all waves
   int skip;               // experiments (prof launches only): work to skip, for time attribution
+  int prof_waves;         // experiments: also per-wave sums prof[NPROF + wave * NPROF + phase]
 };
 // phase clocks (s_memtime): 0 store input / codes, 1 dgrad (+ next-tile input loads), 2 conv2
 // wgrad, 3 barrier 1, 4 next-tile dY2 / pool1 loads issue, 5 conv1 wgrad + dY2 / pool1 store,
@@ -513,6 +514,7 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
       for (int w = 0; w < NW; ++w) v += ep[w * NPROF + tid];
       atomicAdd(a.prof + tid, v);
     }
+    if (a.prof_waves && tid < NW * NPROF) atomicAdd(a.prof + NPROF + tid, ep[tid]);   // [wave][phase]
   }
 }
 
@@ -548,11 +550,14 @@ hipError_t lenet_bwd(const XSrc& x, const bf16_t* p1, const bf16_t* dp2, const u
   if ((!x.x && !x.u8) || grid <= 0) return hipErrorInvalidValue;
   const int res = lenet_bwd_grid();
   if (res <= 0) return hipErrorInvalidValue;
-  BwdArgs a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, p1, dp2, arg2, w2, B, slab1, slab2, prof, 0};
+  BwdArgs a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, p1, dp2, arg2, w2, B, slab1, slab2, prof, 0, 0};
   if (prof) {   // experiments only: skip bits 1 dgrad, 2 conv2 wgrad, 4 conv1 wgrad, 8 staging, 16 loop
-                // barriers, 32 pool1 / code loads
+                // barriers, 32 pool1 / code loads; MNISTX_BWD_PROF_WAVES=1: per-wave sums too
+                // (the prof buffer then holds NPROF + NW * NPROF entries)
     const char* e = getenv("MNISTX_BWD_SKIP");
     a.skip = e ? atoi(e) : 0;
+    const char* pw = getenv("MNISTX_BWD_PROF_WAVES");
+    a.prof_waves = (pw && pw[0] == '1') ? 1 : 0;
   }
   const BwdKernel k = kBwd[(prof ? 4 : 0) + (x.u8 ? 2 : 0) + (x.idx ? 1 : 0)];
   void* args[] = {&a};

@@ -44,6 +44,7 @@
 // the next tile's dY2 / pool1].  The accumulators are split (a wave holds at
 // most 4 conv2 tiles and one conv1 set: 40 registers) so the kernel fits 128 VGPRs.
 #include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 #include "launchers.h"
@@ -99,6 +100,10 @@ struct BwdArgs {
   unsigned long long* prof;   // optional (experiments): per-phase clock sums [NPROF] over all waves
   int skip;               // experiments (prof launches only): work to skip, for time attribution
   int prof_waves;         // experiments: also per-wave sums prof[NPROF + wave * NPROF + phase]
+  // the static work split (defaults below; MNISTX_BWD_SPLIT overrides it for experiments):
+  // dgrad unit per wave, conv2 weight-gradient k-step range per wave (within its tile group),
+  // conv1 weight-gradient k-step range per rank (wave >> 1)
+  int8_t du[16], k20[16], k21[16], k10[8], k11[8];
 };
 // phase clocks (s_memtime): 0 store input / codes, 1 dgrad (+ next-tile input loads), 2 conv2
 // wgrad, 3 barrier 1, 4 next-tile dY2 / pool1 loads issue, 5 conv1 wgrad + dY2 / pool1 store,
@@ -277,18 +282,24 @@ DEV void c2w_steps(const uint8_t* lds, int ks0, int ks1, int ln, f32x4 (&acc2)[C
   }
 }
 
-// ---- static work split.  Waves w, w + 4, w + 8, w + 12 share a SIMD; per SIMD the phase-1
-// MFMA counts are 199 / 199 / 198 / 199 (dgrad units: kernel-row counts 2, 4, 5, 5, 5, 4, 2
-// x 9 or 6 MFMAs; conv2 k-steps: 4 / 3 / 3 / 3 MFMAs in tile groups 0 / 1 / 2 / 3).
+// ---- static work split.  Waves w, w + 4, w + 8, w + 12 share a SIMD (dgrad units: kernel-row
+// counts 2, 4, 5, 5, 5, 4, 2 x 9 or 6 MFMAs; conv2 k-steps: 4 / 3 / 3 / 3 MFMAs in tile
+// groups 0 / 1 / 2 / 3).
 // dgrad unit of each wave (row pair * 2 + half, -1: none) and its conv2 k-step range
 // (group wave >> 2; the group's 30 steps split end to end).
-__constant__ int dg_unit[NW] = {2, 10, 0, -1, 6, 5, 3, 8, 7, 11, -1, 1, 12, 13, 9, 4};
-__constant__ int c2_ks0[NW] = {0, 1, 8, 23, 0, 8, 16, 23, 0, 7, 15, 22, 0, 7, 14, 22};
-__constant__ int c2_ks1[NW] = {1, 8, 23, 30, 8, 16, 23, 30, 7, 15, 22, 30, 7, 14, 22, 30};
+// Per-wave clocks (bench/micro_lenet_bwd.py, profiles/r5/lenet/bwd_per_wave/) showed the
+// youngest waves of each SIMD reaching barrier 1 last whatever their MFMA count; the split
+// below moves the two heaviest dgrad units off waves 14 / 15 onto waves 3 / 10, evens tile
+// group 0's k-steps and gives the conv1 ranks 3,3,4,4,4,4,3,3 steps: 201.8 -> 196.1 us
+// (bench/bwd_split_search.py, three interleaved rounds; round-4 split: 2,10,0,-1,... / 0,1,8,23
+// / ranks 4,4,4,4,3,3,3,3).
+constexpr int8_t DG_UNIT[NW] = {2, 10, 0, 4, 6, 5, 3, 8, 7, 11, 9, 1, 12, 13, -1, -1};
+constexpr int8_t C2_KS0[NW] = {0, 6, 13, 23, 0, 8, 16, 23, 0, 7, 15, 22, 0, 7, 14, 22};
+constexpr int8_t C2_KS1[NW] = {6, 13, 23, 30, 8, 16, 23, 30, 7, 15, 22, 30, 7, 14, 22, 30};
 // conv1 k-steps (s: window row s / 2, windows 4 (s % 2) .. + 3 of the set) of parity set
-// w & 1: rank w >> 1 runs 4, 4, 4, 4, 3, 3, 3, 3 steps (14 per SIMD)
-__constant__ int c1_ks0[8] = {0, 4, 8, 12, 16, 19, 22, 25};
-__constant__ int c1_ks1[8] = {4, 8, 12, 16, 19, 22, 25, 28};
+// w & 1: rank w >> 1 runs 3, 3, 4, 4, 4, 4, 3, 3 steps
+constexpr int8_t C1_KS0[8] = {0, 3, 6, 10, 14, 18, 22, 25};
+constexpr int8_t C1_KS1[8] = {3, 6, 10, 14, 18, 22, 25, 28};
 
 template <bool PROF, bool U8, bool IDX>
 __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
@@ -325,9 +336,9 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
   for (int t = 0; t < 3; ++t) acc1[t][0] = acc1[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   float db1[4] = {0.f, 0.f, 0.f, 0.f};
   const auto rcode = buf_rsrc(a.p1, (uint32_t)a.B * (NWIN1 * 16u));   // code words of the pool1 records
-  const int du = dg_unit[wave];
-  const int ks0 = c2_ks0[wave], ks1 = c2_ks1[wave];
-  const int cs0 = c1_ks0[wave >> 1], cs1 = c1_ks1[wave >> 1];
+  const int du = a.du[wave];
+  const int ks0 = a.k20[wave], ks1 = a.k21[wave];
+  const int cs0 = a.k10[wave >> 1], cs1 = a.k11[wave >> 1];
 
   uint64_t pc_acc[NPROF] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tclk = __builtin_amdgcn_s_memtime();
@@ -518,6 +529,70 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
   }
 }
 
+// The work split a launch uses: the defaults, or MNISTX_BWD_SPLIT = 64 comma-separated ints
+// (du[16], k20[16], k21[16], k10[8], k11[8]) for balancing experiments
+// (bench/micro_lenet_bwd_quick.py); an override is validated (every dgrad unit exactly once,
+// each tile group's and the conv1 k-step ranges partitioning their steps) and refused if not.
+struct BwdSplit {
+  int8_t du[16], k20[16], k21[16], k10[8], k11[8];
+  bool ok;
+};
+BwdSplit bwd_split() {
+  BwdSplit s{};
+  memcpy(s.du, DG_UNIT, 16);
+  memcpy(s.k20, C2_KS0, 16);
+  memcpy(s.k21, C2_KS1, 16);
+  memcpy(s.k10, C1_KS0, 8);
+  memcpy(s.k11, C1_KS1, 8);
+  s.ok = true;
+  const char* e = getenv("MNISTX_BWD_SPLIT");
+  if (!e || !*e) return s;
+  int v[64], n = 0;
+  for (const char* p = e; *p && n < 64;) {
+    char* end = nullptr;
+    const long x = strtol(p, &end, 10);
+    if (end == p) break;
+    v[n++] = (int)x;
+    p = *end == ',' ? end + 1 : end;
+  }
+  if (n != 64) return BwdSplit{{}, {}, {}, {}, {}, false};
+  int seen[14] = {};
+  for (int w = 0; w < 16; ++w) {
+    if (v[w] < -1 || v[w] > 13) return BwdSplit{{}, {}, {}, {}, {}, false};
+    if (v[w] >= 0) ++seen[v[w]];
+  }
+  for (int u = 0; u < 14; ++u)
+    if (seen[u] != 1) return BwdSplit{{}, {}, {}, {}, {}, false};
+  for (int G = 0; G < 4; ++G) {   // each group's ranges: a partition of [0, 30) in some wave order
+    int cover[30] = {};
+    for (int t = 0; t < 4; ++t) {
+      const int w = 4 * G + t, k0 = v[16 + w], k1 = v[32 + w];
+      if (k0 < 0 || k1 < k0 || k1 > 30) return BwdSplit{{}, {}, {}, {}, {}, false};
+      for (int k = k0; k < k1; ++k) ++cover[k];
+    }
+    for (int k = 0; k < 30; ++k)
+      if (cover[k] != 1) return BwdSplit{{}, {}, {}, {}, {}, false};
+  }
+  int cover1[28] = {};
+  for (int r = 0; r < 8; ++r) {
+    const int k0 = v[48 + r], k1 = v[56 + r];
+    if (k0 < 0 || k1 < k0 || k1 > 28) return BwdSplit{{}, {}, {}, {}, {}, false};
+    for (int k = k0; k < k1; ++k) ++cover1[k];
+  }
+  for (int k = 0; k < 28; ++k)
+    if (cover1[k] != 1) return BwdSplit{{}, {}, {}, {}, {}, false};
+  for (int i = 0; i < 16; ++i) {
+    s.du[i] = (int8_t)v[i];
+    s.k20[i] = (int8_t)v[16 + i];
+    s.k21[i] = (int8_t)v[32 + i];
+  }
+  for (int i = 0; i < 8; ++i) {
+    s.k10[i] = (int8_t)v[48 + i];
+    s.k11[i] = (int8_t)v[56 + i];
+  }
+  return s;
+}
+
 using BwdKernel = void (*)(BwdArgs);
 // [prof][u8][idx]
 constexpr BwdKernel kBwd[8] = {lenet_bwd_k<false, false, false>, lenet_bwd_k<false, false, true>,
@@ -550,7 +625,15 @@ hipError_t lenet_bwd(const XSrc& x, const bf16_t* p1, const bf16_t* dp2, const u
   if ((!x.x && !x.u8) || grid <= 0) return hipErrorInvalidValue;
   const int res = lenet_bwd_grid();
   if (res <= 0) return hipErrorInvalidValue;
-  BwdArgs a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, p1, dp2, arg2, w2, B, slab1, slab2, prof, 0, 0};
+  BwdArgs a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, p1, dp2, arg2, w2, B, slab1, slab2, prof, 0, 0,
+            {}, {}, {}, {}, {}};
+  static const BwdSplit sp = bwd_split();
+  if (!sp.ok) return hipErrorInvalidValue;
+  memcpy(a.du, sp.du, 16);
+  memcpy(a.k20, sp.k20, 16);
+  memcpy(a.k21, sp.k21, 16);
+  memcpy(a.k10, sp.k10, 8);
+  memcpy(a.k11, sp.k11, 8);
   if (prof) {   // experiments only: skip bits 1 dgrad, 2 conv2 wgrad, 4 conv1 wgrad, 8 staging, 16 loop
                 // barriers, 32 pool1 / code loads; MNISTX_BWD_PROF_WAVES=1: per-wave sums too
                 // (the prof buffer then holds NPROF + NW * NPROF entries)

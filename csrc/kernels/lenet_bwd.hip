@@ -288,18 +288,19 @@ DEV void c2w_steps(const uint8_t* lds, int ks0, int ks1, int ln, f32x4 (&acc2)[C
 // dgrad unit of each wave (row pair * 2 + half, -1: none) and its conv2 k-step range
 // (group wave >> 2; the group's 30 steps split end to end).
 // Per-wave clocks (bench/micro_lenet_bwd.py, profiles/r5/lenet/bwd_per_wave/) showed the
-// youngest waves of each SIMD reaching barrier 1 last whatever their MFMA count; the split
-// below moves the two heaviest dgrad units off waves 14 / 15 onto waves 3 / 10, evens tile
-// group 0's k-steps and gives the conv1 ranks 3,3,4,4,4,4,3,3 steps: 201.8 -> 196.1 us
-// (bench/bwd_split_search.py, three interleaved rounds; round-4 split: 2,10,0,-1,... / 0,1,8,23
-// / ranks 4,4,4,4,3,3,3,3).
-constexpr int8_t DG_UNIT[NW] = {2, 10, 0, 4, 6, 5, 3, 8, 7, 11, 9, 1, 12, 13, -1, -1};
+// youngest waves of each SIMD (s, s+4, s+8, s+12) reaching the barriers last whatever their MFMA
+// count; the split below moves dgrad units off waves 14 / 15 and the heavier ones (rows 2-4: 5
+// taps) onto the oldest waves, evens tile group 0's k-steps and gives the conv1 ranks
+// 4,4,4,4,4,4,2,2 steps: 201.8 -> 196.1 us (search round 3), -> 194.5 vs 196.9 us (rounds 4-5,
+// eight interleaved rounds; bench/bwd_split_search.py, profiles/r5/lenet/bwd_split/; round-4
+// split: 2,10,0,-1,... / 0,1,8,23 / ranks 4,4,4,4,3,3,3,3).
+constexpr int8_t DG_UNIT[NW] = {7, 5, 9, 4, 6, 10, 3, 8, 2, 11, 0, 1, 12, 13, -1, -1};
 constexpr int8_t C2_KS0[NW] = {0, 6, 13, 23, 0, 8, 16, 23, 0, 7, 15, 22, 0, 7, 14, 22};
 constexpr int8_t C2_KS1[NW] = {6, 13, 23, 30, 8, 16, 23, 30, 7, 15, 22, 30, 7, 14, 22, 30};
 // conv1 k-steps (s: window row s / 2, windows 4 (s % 2) .. + 3 of the set) of parity set
-// w & 1: rank w >> 1 runs 3, 3, 4, 4, 4, 4, 3, 3 steps
-constexpr int8_t C1_KS0[8] = {0, 3, 6, 10, 14, 18, 22, 25};
-constexpr int8_t C1_KS1[8] = {3, 6, 10, 14, 18, 22, 25, 28};
+// w & 1: rank w >> 1 runs 4, 4, 4, 4, 4, 4, 2, 2 steps
+constexpr int8_t C1_KS0[8] = {0, 4, 8, 12, 16, 20, 24, 26};
+constexpr int8_t C1_KS1[8] = {4, 8, 12, 16, 20, 24, 26, 28};
 
 template <bool PROF, bool U8, bool IDX>
 __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {

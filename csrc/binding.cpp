@@ -490,10 +490,15 @@ void splitk_reduce_multi(std::vector<Tensor> slabs, std::vector<Tensor> wdsts, s
 
 // segs: int64 tensor [nseg, 14] on CPU:
 //   off, n, G, I, J, Ip, Jp, bf_off, wd_bits(float32 as int), track_l2, bft_off, Jt, It, 0
+mnistx::FinArgs prep_fin(Tensor step, Tensor stats, optional<Tensor> l2, optional<Tensor> wds, int64_t nw,
+                         optional<Tensor> loss_ema, int64_t n_ema, int64_t batch, bool increment,
+                         optional<Tensor> l2_ranges, optional<Tensor> ce_work, int64_t ce_nblk);
+
 void fused_optimizer(Tensor params, Tensor grads, Tensor mom, Tensor ema, Tensor bf, Tensor segs, Tensor step,
                      double lr0, double decay_rate, int64_t decay_steps, double momentum, bool nesterov,
                      bool use_momentum, double grad_scale, double ema_max, optional<Tensor> l2,
-                     optional<Tensor> guard, int64_t guard_want, optional<Tensor> guard_err, int64_t guard_id) {
+                     optional<Tensor> guard, int64_t guard_want, optional<Tensor> guard_err, int64_t guard_id,
+                     optional<py::tuple> fin) {
   const int64_t total = params.numel();
   check(params, at::kFloat, total, "params");
   check(grads, at::kFloat, total, "grads");
@@ -564,47 +569,66 @@ void fused_optimizer(Tensor params, Tensor grads, Tensor mom, Tensor ema, Tensor
     op.guard_err = P<int>(*guard_err);
     op.guard_id = (int)guard_id;
   }
+  // fin: finalize_step's arguments after `step` (the same step tensor), run in this launch
+  mnistx::FinArgs fa{};
+  const bool has_fin = fin.has_value() && !fin->is_none();
+  if (has_fin) {
+    const py::tuple& t = *fin;
+    TORCH_CHECK(t.size() == 11, "fin: (stats, l2, wds, nw, loss_ema, n_ema, batch, increment, l2_ranges, ce_work, ce_nblk)");
+    auto ot = [&](int i) { return t[i].is_none() ? optional<Tensor>() : optional<Tensor>(t[i].cast<Tensor>()); };
+    fa = prep_fin(step, t[0].cast<Tensor>(), ot(1), ot(2), t[3].cast<int64_t>(), ot(4), t[5].cast<int64_t>(),
+                  t[6].cast<int64_t>(), t[7].cast<bool>(), ot(8), ot(9), t[10].cast<int64_t>());
+  }
   hip_ok(mnistx::fused_optimizer(P<float>(params), P<const float>(grads), use_momentum ? P<float>(mom) : nullptr,
                                  ema_max >= 0 ? P<float>(ema) : nullptr, BFm(bf), sv.data(), nseg, total,
-                                 P<const int64_t>(step), op, l2p, l2n, cur_stream()),
+                                 P<const int64_t>(step), op, l2p, l2n, cur_stream(), has_fin ? &fa : nullptr),
          "fused_optimizer");
+}
+
+mnistx::FinArgs prep_fin(Tensor step, Tensor stats, optional<Tensor> l2, optional<Tensor> wds, int64_t nw,
+                         optional<Tensor> loss_ema, int64_t n_ema, int64_t batch, bool increment,
+                         optional<Tensor> l2_ranges, optional<Tensor> ce_work, int64_t ce_nblk) {
+  check(step, at::kLong, 1, "step");
+  check(stats, at::kFloat, 8, "stats");
+  TORCH_CHECK(nw <= 64, "finalize: at most 64 weight-decay entries");
+  mnistx::FinArgs f{};
+  f.step = P<int64_t>(step);
+  f.stats = P<float>(stats);
+  if (nw > 0) {
+    TORCH_CHECK(l2.has_value() && wds.has_value(), "l2/wds needed when nw > 0");
+    check(*l2, at::kFloat, nw, "l2");
+    check(*wds, at::kFloat, nw, "wds");
+    f.l2 = P<float>(*l2);
+    f.wds = P<const float>(*wds);
+  }
+  f.nw = (int)nw;
+  if (loss_ema.has_value() && loss_ema->defined()) {
+    check(*loss_ema, at::kFloat, 3 * n_ema, "loss_ema");
+    f.loss_ema = P<float>(*loss_ema);
+    f.n_ema = (int)n_ema;
+  }
+  if (nw > 0 && l2_ranges.has_value() && l2_ranges->defined()) {
+    check(*l2_ranges, at::kInt, 3 * nw, "l2_ranges");
+    f.l2r = P<const int>(*l2_ranges);
+    // partials follow the nw per-weight slots (binding fused_optimizer: l2n = max track index)
+  }
+  f.l2base = (int)nw;
+  if (ce_nblk > 0) {
+    TORCH_CHECK(ce_work.has_value() && ce_work->defined() && ce_nblk <= 1024, "ce_work needed for ce_nblk > 0");
+    check(*ce_work, at::kFloat, 4 * 1024 + 1, "ce_work");
+    f.ce_work = P<const float>(*ce_work);
+    f.ce_nblk = (int)ce_nblk;
+  }
+  f.batch = (int)batch;
+  f.increment = increment ? 1 : 0;
+  return f;
 }
 
 void finalize_step(Tensor step, Tensor stats, optional<Tensor> l2, optional<Tensor> wds, int64_t nw,
                    optional<Tensor> loss_ema, int64_t n_ema, int64_t batch, bool increment,
                    optional<Tensor> l2_ranges, optional<Tensor> ce_work, int64_t ce_nblk) {
-  check(step, at::kLong, 1, "step");
-  check(stats, at::kFloat, 8, "stats");
-  const float* l2p = nullptr;
-  const float* wp = nullptr;
-  if (nw > 0) {
-    TORCH_CHECK(l2.has_value() && wds.has_value(), "l2/wds needed when nw > 0");
-    check(*l2, at::kFloat, nw, "l2");
-    check(*wds, at::kFloat, nw, "wds");
-    l2p = P<const float>(*l2);
-    wp = P<const float>(*wds);
-  }
-  float* le = nullptr;
-  if (loss_ema.has_value() && loss_ema->defined()) {
-    check(*loss_ema, at::kFloat, 3 * n_ema, "loss_ema");
-    le = P<float>(*loss_ema);
-  }
-  const int* rp = nullptr;
-  if (nw > 0 && l2_ranges.has_value() && l2_ranges->defined()) {
-    check(*l2_ranges, at::kInt, 3 * nw, "l2_ranges");
-    rp = P<const int>(*l2_ranges);
-    // partials follow the nw per-weight slots (binding fused_optimizer: l2n = max track index)
-  }
-  const float* cw = nullptr;
-  if (ce_nblk > 0) {
-    TORCH_CHECK(ce_work.has_value() && ce_work->defined() && ce_nblk <= 1024, "ce_work needed for ce_nblk > 0");
-    check(*ce_work, at::kFloat, 4 * 1024 + 1, "ce_work");
-    cw = P<const float>(*ce_work);
-  }
-  hip_ok(mnistx::finalize_step(P<int64_t>(step), P<float>(stats), l2p, rp, (int)nw, wp, (int)nw, le,
-                               le ? (int)n_ema : 0, (int)batch, increment ? 1 : 0, cur_stream(), cw,
-                               (int)ce_nblk),
-         "finalize_step");
+  const auto f = prep_fin(step, stats, l2, wds, nw, loss_ema, n_ema, batch, increment, l2_ranges, ce_work, ce_nblk);
+  hip_ok(mnistx::finalize_step(f, cur_stream()), "finalize_step");
 }
 
 void cast_f32_bf16_padded(Tensor src, Tensor dst, int64_t G, int64_t I, int64_t J, int64_t Ip, int64_t Jp) {
@@ -1201,6 +1225,9 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("tile") = -1);
   m.def("set_tile192", [](int64_t on) { mnistx::set_tile192((int)on); },
         "A/B switch of gemm.hip's 192-column tiles (MNISTX_TILE192)");
+  m.def("set_reduce_fused", [](int64_t on) { mnistx::set_reduce_fused((int)on); },
+        "A/B switch of the one-launch split-K reduce (MNISTX_REDUCE_FUSED)");
+  m.def("reduce_fused_enabled", []() { return mnistx::reduce_fused_enabled() != 0; });
   m.def("dense_wgrad", &dense_wgrad, py::arg("x"), py::arg("dy"), py::arg("slab"), py::arg("Din"), py::arg("Dout"),
         py::arg("B"), py::arg("ldx"), py::arg("lddy"), py::arg("with_bias"), py::arg("splits"), py::arg("tile") = -1);
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("out"), py::arg("Nb"), py::arg("H"), py::arg("W"),
@@ -1244,7 +1271,11 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("bf"), py::arg("segs"), py::arg("step"), py::arg("lr0"), py::arg("decay_rate"),
         py::arg("decay_steps"), py::arg("momentum"), py::arg("nesterov"), py::arg("use_momentum"),
         py::arg("grad_scale"), py::arg("ema_max"), py::arg("l2") = py::none(), py::arg("guard") = py::none(),
-        py::arg("guard_want") = 0, py::arg("guard_err") = py::none(), py::arg("guard_id") = 0);
+        py::arg("guard_want") = 0, py::arg("guard_err") = py::none(), py::arg("guard_id") = 0,
+        py::arg("fin") = py::none());
+  m.def("set_opt_fin_fused", [](int64_t on) { mnistx::set_opt_fin_fused((int)on); },
+        "A/B switch of the optimizer launch running the step's finalize (MNISTX_OPT_FIN_FUSED)");
+  m.def("opt_fin_fused_enabled", []() { return mnistx::opt_fin_fused_enabled() != 0; });
   m.def("fused_optimizer_blocks", [](Tensor segs) {
     TORCH_CHECK(!segs.is_cuda() && segs.scalar_type() == at::kLong && segs.dim() == 2, "segs: CPU int64 [n,14]");
     auto a = segs.accessor<int64_t, 2>();

@@ -305,6 +305,9 @@ struct RedSpec {
   float scale;
 };
 hipError_t splitk_reduce_multi(const RedSpec* specs, int n, hipStream_t st);
+// one launch for the partial and reduce passes (default; MNISTX_REDUCE_FUSED=0: two launches)
+void set_reduce_fused(int on);
+int reduce_fused_enabled();
 
 struct OptSeg {          // one trainable tensor inside the flat buffers
   int64_t off;           // offset in the flat fp32 buffers
@@ -336,15 +339,34 @@ struct OptParams {
 
 // l2 (optional): [l2n per-tensor sums | fused_optimizer_blocks() per-block partials]
 int fused_optimizer_blocks(const OptSeg* segs, int nseg);
+// finalize_step's arguments (finalize_k, or the last block of fused_opt_k: ticket != nullptr)
+struct FinArgs {
+  int64_t* step;
+  float* stats;
+  float* l2;
+  const int* l2r;
+  int l2base;
+  const float* wds;
+  int nw;
+  float* loss_ema;
+  int n_ema, batch, increment;
+  const float* ce_work;
+  int ce_nblk;
+  int* ticket;
+};
+// fin (optional): the step's finalize_step, run by the optimizer launch's last block when the
+// grid is small (<= 1024 blocks: one ticket address per launch) and no PS guard is set, else
+// launched right after it (MNISTX_OPT_FIN_FUSED=0: always separate)
 hipError_t fused_optimizer(float* params, const float* grads, float* mom, float* ema, bf16_t* bf, const OptSeg* segs,
-                           int nseg, int64_t total, const int64_t* step, OptParams op, float* l2, int l2n, hipStream_t st);
+                           int nseg, int64_t total, const int64_t* step, OptParams op, float* l2, int l2n, hipStream_t st,
+                           const FinArgs* fin = nullptr);
+void set_opt_fin_fused(int on);
+int opt_fin_fused_enabled();
 // l2r (optional, device int32 [nw][3] = {weight index, first block, end block}): sum the
 // fused optimizer's per-block partials at l2[l2base + block] for each weight
 // ce_work / ce_nblk: per-block CE partials of a deferred-stats mlp_head launch, added to
 // stats[0..2] in block order before anything reads them
-hipError_t finalize_step(int64_t* step, float* stats, const float* l2, const int* l2r, int l2base, const float* wds,
-                         int nw, float* loss_ema, int n_ema, int batch, int increment, hipStream_t st,
-                         const float* ce_work = nullptr, int ce_nblk = 0);
+hipError_t finalize_step(const FinArgs& f, hipStream_t st);
 hipError_t cast_f32_bf16_padded(const float* src, bf16_t* dst, int G, int I, int J, int Ip, int Jp,
                                 hipStream_t st);
 

@@ -11,6 +11,7 @@
 #include "launchers.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace mnistx {
 namespace {
@@ -574,6 +575,7 @@ struct RedDesc {
   int64_t nq;        // M * N / 4 quads per split
   int S, M, N, G, Ipad, I, J, bias_row;
   int qb, sb;        // reduce blocks; partial-pass split blocks (0 = no partial pass)
+  int tick0;         // first ticket of this descriptor's quad blocks (fused launch, partial pass)
   float scale;
 };
 struct RedTable {
@@ -589,34 +591,9 @@ DEV int red_find(const int* blk0, int n, int b) {
   return k;
 }
 
-__global__ __launch_bounds__(256) void splitk_reduce4_k(RedTable tab) {
-  __shared__ f32x4 part[4][64];
-  const int k = red_find(tab.rblk0, tab.n, blockIdx.x);
-  const RedDesc& D = tab.d[k];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// the reduced quad qd (4 consecutive slab columns of one row) -> weight / bias destination
+DEV void red_emit(const RedDesc& D, int64_t qd, const f32x4 t) {
   const int NQ = D.N >> 2;
-  const int64_t nq = D.nq;
-  const int64_t qd = (int64_t)(blockIdx.x - tab.rblk0[k]) * 64 + lane;
-  const int S = D.sb ? D.sb : D.S;
-  const int64_t zs = (int64_t)(D.sb ? RED_CHUNK : 1) * nq;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  if (qd < nq) {
-    const f32x4* p = (const f32x4*)D.slab + qd;
-    int z = wave;
-    for (; z + 12 < S; z += 16) {
-      const f32x4 a = p[z * zs], b = p[(z + 4) * zs];
-      const f32x4 c = p[(z + 8) * zs], d = p[(z + 12) * zs];
-      acc += a;
-      acc += b;
-      acc += c;
-      acc += d;
-    }
-    for (; z < S; z += 4) acc += p[z * zs];
-  }
-  part[wave][lane] = acc;
-  __syncthreads();
-  if (wave != 0 || qd >= nq) return;
-  const f32x4 t = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
   const int row = (int)(qd / NQ), j0 = (int)(qd - (int64_t)row * NQ) * 4;
   if (row == D.bias_row) {
     if (D.bdst)
@@ -633,19 +610,70 @@ __global__ __launch_bounds__(256) void splitk_reduce4_k(RedTable tab) {
     if (j0 + jj < D.J) d[j0 + jj] = t[jj] * D.scale;
 }
 
+// block b of the reduce pass: 64 quads, the 4 waves take every 4th split
+DEV void red_reduce_block(const RedTable& tab, int b, f32x4 (*part)[64]) {
+  const int k = red_find(tab.rblk0, tab.n, b);
+  const RedDesc& D = tab.d[k];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t nq = D.nq;
+  const int64_t qd = (int64_t)(b - tab.rblk0[k]) * 64 + lane;
+  const int S = D.sb ? D.sb : D.S;
+  const int64_t zs = (int64_t)(D.sb ? RED_CHUNK : 1) * nq;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (qd < nq) {
+    const f32x4* p = (const f32x4*)D.slab + qd;
+    int z = wave;
+    for (; z + 12 < S; z += 16) {
+      const f32x4 a = p[z * zs], b2 = p[(z + 4) * zs];
+      const f32x4 c = p[(z + 8) * zs], d = p[(z + 12) * zs];
+      acc += a;
+      acc += b2;
+      acc += c;
+      acc += d;
+    }
+    for (; z < S; z += 4) acc += p[z * zs];
+  }
+  part[wave][lane] = acc;
+  __syncthreads();
+  if (wave != 0 || qd >= nq) return;
+  red_emit(D, qd, ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]);
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce4_k(RedTable tab) {
+  __shared__ f32x4 part[4][64];
+  red_reduce_block(tab, blockIdx.x, part);
+}
+
 // First pass for many splits over a small output: block (q, s) of a descriptor
 // sums splits [64 s, 64 s + 64) of its 64 quads and stores the sum IN PLACE in
 // split 64 s (only this block reads or writes that range), so the reduce pass
-// has S/64 splits.
-__global__ __launch_bounds__(256) void splitk_partial4_k(RedTable tab) {
-  __shared__ f32x4 part[4][64];
-  const int k = red_find(tab.pblk0, tab.n, blockIdx.x);
+// has S/64 splits.  Returns the quad block's descriptor and quad index (for the ticket).
+// agent-scope relaxed store / load: written through to / read from the coherence point (no
+// L2-wide write-back or invalidate: the fences those need cost ~18 us in the LeNet-5 step and
+// ~190 us in the reference CNN's when every block of a launch ran one)
+DEV void st_coh(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DEV float ld_coh(const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// a ticket taken after this wave's coherent stores have completed (vmcnt counts stores too)
+DEV int take_ticket(int* t) {
+  __builtin_amdgcn_s_waitcnt(0);
+  return __hip_atomic_fetch_add(t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// First pass for many splits over a small output: block (q, s) of a descriptor
+// sums splits [64 s, 64 s + 64) of its 64 quads and stores the sum IN PLACE in
+// split 64 s (only this block reads or writes that range), so the reduce pass
+// has S/64 splits.  COH: the store goes to the coherence point (fused launch).
+template <bool COH>
+DEV const RedDesc& red_partial_block(const RedTable& tab, int b, f32x4 (*part)[64], int& qblk, int64_t& qd_out) {
+  const int k = red_find(tab.pblk0, tab.n, b);
   const RedDesc& D = tab.d[k];
-  const int local = blockIdx.x - tab.pblk0[k];
-  const int qblk = local % D.qb, sblk = local / D.qb;
+  const int local = b - tab.pblk0[k];
+  qblk = local % D.qb;
+  const int sblk = local / D.qb;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t nq = D.nq;
   const int64_t qd = (int64_t)qblk * 64 + lane;
+  qd_out = qd;
   const int z0 = sblk * RED_CHUNK, z1 = min(D.S, z0 + RED_CHUNK);
   f32x4* p = (f32x4*)D.slab + qd;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -663,7 +691,56 @@ __global__ __launch_bounds__(256) void splitk_partial4_k(RedTable tab) {
   }
   part[wave][lane] = acc;
   __syncthreads();
-  if (wave == 0 && qd < nq) p[(int64_t)z0 * nq] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+  if (wave == 0 && qd < nq) {
+    const f32x4 t = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+    if constexpr (COH) {
+      float* d = (float*)(p + (int64_t)z0 * nq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) st_coh(d + j, t[j]);
+    } else {
+      p[(int64_t)z0 * nq] = t;
+    }
+  }
+  return D;
+}
+
+__global__ __launch_bounds__(256) void splitk_partial4_k(RedTable tab) {
+  __shared__ f32x4 part[4][64];
+  int qblk;
+  int64_t qd;
+  red_partial_block<false>(tab, blockIdx.x, part, qblk, qd);
+}
+
+// ONE launch for both passes (the partial pass's blocks first, then the reduce blocks of the
+// descriptors without one): wave 0 of the block that stores the last of a quad block's sb
+// partials (coherent stores, then a ticket) sums them in split order (coherent loads) and
+// emits.  The winner resets its ticket to 0.
+__global__ __launch_bounds__(256) void splitk_fused4_k(RedTable tab, int* __restrict__ tickets) {
+  __shared__ f32x4 part[4][64];
+  const int pb = tab.pblk0[MAXRED];
+  if ((int)blockIdx.x >= pb) {
+    red_reduce_block(tab, (int)blockIdx.x - pb, part);
+    return;
+  }
+  int qblk;
+  int64_t qd;
+  const RedDesc& D = red_partial_block<true>(tab, blockIdx.x, part, qblk, qd);
+  if (threadIdx.x >= 64) return;   // wave 0 stored the partials
+  int* tk = tickets + D.tick0 + qblk;
+  int last = 0;
+  if (threadIdx.x == 0) last = take_ticket(tk) == D.sb - 1;
+  last = __shfl(last, 0, 64);
+  if (!last) return;
+  if (threadIdx.x == 0) *tk = 0;
+  if (qd >= D.nq) return;
+  const float* p = (const float*)((const f32x4*)D.slab + qd);
+  const int64_t zs = (int64_t)RED_CHUNK * D.nq * 4;
+  f32x4 acc = {ld_coh(p), ld_coh(p + 1), ld_coh(p + 2), ld_coh(p + 3)};
+  for (int z = 1; z < D.sb; ++z) {
+    const float* q = p + z * zs;
+    acc += f32x4{ld_coh(q), ld_coh(q + 1), ld_coh(q + 2), ld_coh(q + 3)};
+  }
+  red_emit(D, qd, acc);
 }
 
 // ------------------------------------------------------------------ K9 fused optimizer
@@ -672,6 +749,9 @@ __global__ __launch_bounds__(256) void splitk_partial4_k(RedTable tab) {
 // L2 norm needed for the weight-decay loss is reduced in the workgroup and added
 // with a single atomic per workgroup.
 constexpr int MAXSEG = 16;
+constexpr int FIN_WAVES = 4, FIN_MAXW = 64;
+template <bool COH>
+DEV void finalize_body(const FinArgs& f, float* wsum);
 constexpr int OPT_EPT = 2;                       // elements per thread: one consecutive pair (fused_opt_k)
 constexpr int OPT_CHUNK = TPB * OPT_EPT;         // elements per workgroup
 struct SegTable {
@@ -686,8 +766,10 @@ __global__ __launch_bounds__(TPB) void fused_opt_k(float* __restrict__ params, c
                                                    float* __restrict__ mom, float* __restrict__ ema,
                                                    bf16_t* __restrict__ bf, SegTable tab,
                                                    const int64_t* __restrict__ step_p, OptParams op,
-                                                   float* __restrict__ l2) {
+                                                   float* __restrict__ l2, FinArgs fin) {
   __shared__ float red[TPB / 64];
+  __shared__ float wsum[FIN_MAXW];
+  __shared__ int last;
   if (op.guard && *op.guard != op.guard_want) {   // a stale / torn PS push: never applied
     if (blockIdx.x == 0 && threadIdx.x == 0) *op.guard_err = op.guard_id;
     return;
@@ -811,25 +893,44 @@ __global__ __launch_bounds__(TPB) void fused_opt_k(float* __restrict__ params, c
     if (threadIdx.x == 0) {
       float t = 0.f;
       for (int w = 0; w < TPB / 64; ++w) t += red[w];
-      l2[tab.l2n + blockIdx.x] = t;
+      if (fin.ticket) st_coh(l2 + tab.l2n + blockIdx.x, t);
+      else l2[tab.l2n + blockIdx.x] = t;
     }
   }
+  if (!fin.ticket) return;
+  // the step's finalize in this launch: the last block to take a ticket (thread 0, after its
+  // coherent partial store) runs it, reading the partials coherently; every block has read
+  // *step_p by now
+  if (threadIdx.x == 0) last = take_ticket(fin.ticket) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) *fin.ticket = 0;
+  finalize_body<true>(fin, wsum);
 }
 
 // stats: [0] ce_sum acc [1] correct acc [2] nan flag [3] -
 //        [4] ce_mean [5] accuracy [6] total_loss [7] steps done (float)
 // loss_ema: n_ema x {biased, local_step, avg}  (TF zero-debiased EMA, decay 0.9:
 //           mnist_input.py:288-290); order = weight losses..., cross_entropy, total_loss
-constexpr int FIN_WAVES = 4, FIN_MAXW = 64;
-__global__ __launch_bounds__(64 * FIN_WAVES) void finalize_k(int64_t* step, float* stats, float* l2, const int* __restrict__ l2r, int l2base,
-                           const float* wds, int nw, float* loss_ema, int n_ema, int batch, int increment,
-                           const float* __restrict__ ce_work, int ce_nblk) {
+static_assert(64 * FIN_WAVES == TPB, "finalize_body also runs as the last block of fused_opt_k");
+// the body of finalize_k, run by one TPB-thread block: by finalize_k, or by the last block of
+// fused_opt_k (FinArgs::ticket set), which then replaces the separate launch
+template <bool COH>   // COH: the optimizer's l2 partials of this launch, read coherently
+DEV void finalize_body(const FinArgs& f, float* wsum) {
+  int64_t* step = f.step;
+  float* stats = f.stats;
+  float* l2 = f.l2;
+  const int* l2r = f.l2r;
+  const int l2base = f.l2base, nw = f.nw, n_ema = f.n_ema, batch = f.batch, increment = f.increment;
+  const float* wds = f.wds;
+  float* loss_ema = f.loss_ema;
+  const float* ce_work = f.ce_work;
+  const int ce_nblk = f.ce_nblk;
   // wave 0 lane i owns loss entry i (weight losses..., cross_entropy, total_loss), so the
   // EMA read-modify-writes run in parallel instead of as one dependent chain.  The per-
   // weight sum(w^2) partials are summed by all FIN_WAVES waves (weight w by wave w %
   // FIN_WAVES, the same per-weight order as one wave): their load latencies overlap
   // instead of queueing behind each other (LeNet: 5 weights, ~11 -> ~5 us).
-  __shared__ float wsum[FIN_MAXW];
   const int t = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // wave 0: the CE partials and every per-lane input of the EMA update, loaded up front;
   // waves 1..FIN_WAVES-1: the per-weight sum(w^2) partials -- the two phases' memory
@@ -884,15 +985,15 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void finalize_k(int64_t* step, floa
       for (; b + 64 * 15 < b1; b += 64 * 16) {
         float v[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = l2[l2base + b + 64 * u];
+        for (int u = 0; u < 16; ++u) v[u] = COH ? ld_coh(l2 + l2base + b + 64 * u) : l2[l2base + b + 64 * u];
 #pragma unroll
         for (int u = 0; u < 16; ++u) s4[u & 3] += v[u];
       }
       for (; b + 192 < b1; b += 256) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) s4[u] += l2[l2base + b + 64 * u];
+        for (int u = 0; u < 4; ++u) s4[u] += COH ? ld_coh(l2 + l2base + b + 64 * u) : l2[l2base + b + 64 * u];
       }
-      for (; b < b1; b += 64) s4[0] += l2[l2base + b];
+      for (; b < b1; b += 64) s4[0] += COH ? ld_coh(l2 + l2base + b) : l2[l2base + b];
       float sum = (s4[0] + s4[1]) + (s4[2] + s4[3]);
       sum = warp_sum(sum);
       if (t == 0) wsum[w] = sum;
@@ -929,6 +1030,11 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void finalize_k(int64_t* step, floa
   stats[0] = 0.f;
   stats[1] = 0.f;
   if (increment) *step += 1;
+}
+
+__global__ __launch_bounds__(64 * FIN_WAVES) void finalize_k(FinArgs f) {
+  __shared__ float wsum[FIN_MAXW];
+  finalize_body<false>(f, wsum);
 }
 
 __global__ void cast_pad_k(const float* __restrict__ src, bf16_t* __restrict__ dst, int G, int I, int J, int Ip,
@@ -1087,6 +1193,37 @@ hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B
   return hipGetLastError();
 }
 
+// Tickets of the fused reduce (one int per partial-pass quad block of a launch: at most
+// MAXRED * 512) and of the optimizer's finalize (slot MAXRED * 512), zeroed once per device and left zeroed by every launch.  nullptr (the two-launch
+// path) when disabled (MNISTX_REDUCE_FUSED=0) or when the first use falls inside a stream
+// capture (no allocation there).  Launches on one device must not overlap in time: the
+// executors issue them on their compute stream.
+static int g_reduce_fused = -1;
+void set_reduce_fused(int on) { g_reduce_fused = on; }
+int reduce_fused_enabled() {
+  if (g_reduce_fused < 0) {
+    const char* e = getenv("MNISTX_REDUCE_FUSED");
+    g_reduce_fused = (e && *e) ? atoi(e) != 0 : 1;
+  }
+  return g_reduce_fused;
+}
+static int* red_tickets(hipStream_t st, bool any_use = false) {
+  if (!any_use && !reduce_fused_enabled()) return nullptr;
+  static int* tick[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!tick[dev]) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    int* p = nullptr;
+    const size_t bytes = (MAXRED * 512 + 64) * sizeof(int);   // + the optimizer's finalize ticket
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
+    tick[dev] = p;
+  }
+  return tick[dev];
+}
+
 hipError_t splitk_reduce_multi(const RedSpec* specs, int n, hipStream_t st) {
   if (n < 1) return hipSuccess;
   // one-split slabs (small batches: K below pick_splits' min_k) take the same multi-tensor
@@ -1103,10 +1240,12 @@ hipError_t splitk_reduce_multi(const RedSpec* specs, int n, hipStream_t st) {
     }
     return hipGetLastError();
   }
+  int* tickets = red_tickets(st);
   for (int i0 = 0; i0 < n; i0 += MAXRED) {
     RedTable tab;
     tab.n = std::min(MAXRED, n - i0);
-    int pb = 0, rb = 0;
+    int pb = 0, rb = 0, tk = 0;
+    const bool fused = tickets != nullptr;
     for (int i = 0; i < tab.n; ++i) {
       const RedSpec& r = specs[i0 + i];
       RedDesc& D = tab.d[i];
@@ -1125,14 +1264,20 @@ hipError_t splitk_reduce_multi(const RedSpec* specs, int n, hipStream_t st) {
       D.scale = r.scale;
       D.qb = (int)((D.nq + 63) / 64);
       D.sb = (D.S > RED_CHUNK && D.qb < 512) ? (D.S + RED_CHUNK - 1) / RED_CHUNK : 0;
+      D.tick0 = tk;
       tab.pblk0[i] = pb;
       tab.rblk0[i] = rb;
       pb += D.sb ? D.qb * D.sb : 0;
-      rb += D.qb;
+      tk += D.sb ? D.qb : 0;
+      rb += (fused && D.sb) ? 0 : D.qb;   // fused: the partial pass finishes its own quads
     }
     for (int i = tab.n; i <= MAXRED; ++i) {
       tab.pblk0[i] = pb;
       tab.rblk0[i] = rb;
+    }
+    if (fused) {
+      if (pb + rb > 0) hipLaunchKernelGGL(splitk_fused4_k, dim3(pb + rb), dim3(256), 0, st, tab, tickets);
+      continue;
     }
     if (pb > 0) hipLaunchKernelGGL(splitk_partial4_k, dim3(pb), dim3(256), 0, st, tab);
     hipLaunchKernelGGL(splitk_reduce4_k, dim3(rb), dim3(256), 0, st, tab);
@@ -1152,10 +1297,29 @@ int fused_optimizer_blocks(const OptSeg* segs, int nseg) {
   return nb;
 }
 
+static int g_opt_fin_fused = -1;
+void set_opt_fin_fused(int on) { g_opt_fin_fused = on; }
+int opt_fin_fused_enabled() {
+  if (g_opt_fin_fused < 0) {
+    const char* e = getenv("MNISTX_OPT_FIN_FUSED");
+    g_opt_fin_fused = (e && *e) ? atoi(e) != 0 : 1;
+  }
+  return g_opt_fin_fused;
+}
+
+hipError_t finalize_step(const FinArgs& f, hipStream_t st) {
+  if (f.nw > FIN_MAXW) return hipErrorInvalidValue;
+  FinArgs a = f;
+  a.ticket = nullptr;
+  hipLaunchKernelGGL(finalize_k, dim3(1), dim3(64 * FIN_WAVES), 0, st, a);
+  return hipGetLastError();
+}
+
 hipError_t fused_optimizer(float* params, const float* grads, float* mom, float* ema, bf16_t* bf, const OptSeg* segs,
                            int nseg, int64_t total, const int64_t* step, OptParams op, float* l2, int l2n,
-                           hipStream_t st) {
+                           hipStream_t st, const FinArgs* fin) {
   if (nseg > MAXSEG || nseg < 1) return hipErrorInvalidValue;
+  if (fin && fin->nw > FIN_MAXW) return hipErrorInvalidValue;
   SegTable tab;
   int nb = 0;
   for (int i = 0; i < nseg; ++i) {
@@ -1170,16 +1334,15 @@ hipError_t fused_optimizer(float* params, const float* grads, float* mom, float*
   tab.n = nseg;
   tab.l2n = l2n;
   (void)total;
-  hipLaunchKernelGGL(fused_opt_k, dim3(nb), dim3(TPB), 0, st, params, grads, mom, ema, bf, tab, step, op, l2);
-  return hipGetLastError();
-}
-
-hipError_t finalize_step(int64_t* step, float* stats, const float* l2, const int* l2r, int l2base, const float* wds,
-                         int nw, float* loss_ema, int n_ema, int batch, int increment, hipStream_t st,
-                         const float* ce_work, int ce_nblk) {
-  if (nw > FIN_MAXW) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(finalize_k, dim3(1), dim3(64 * FIN_WAVES), 0, st, step, stats, (float*)l2, l2r, l2base, wds, nw, loss_ema,
-                     n_ema, batch, increment, ce_work, ce_nblk);
+  FinArgs fa{};
+  int* tickets = nullptr;
+  if (fin && !op.guard && nb <= 1024 && opt_fin_fused_enabled()) tickets = red_tickets(st, true);
+  if (tickets) {
+    fa = *fin;
+    fa.ticket = tickets + MAXRED * 512;   // the optimizer's slot after the reduce's
+  }
+  hipLaunchKernelGGL(fused_opt_k, dim3(nb), dim3(TPB), 0, st, params, grads, mom, ema, bf, tab, step, op, l2, fa);
+  if (fin && !tickets) return finalize_step(*fin, st);
   return hipGetLastError();
 }
 

@@ -799,17 +799,21 @@ class HipNet:
         pending.clear()
 
     def update(self, grad_scale: float = 1.0, increment: bool = True, batch_for_stats: Optional[int] = None) -> None:
-        self.fp.apply(self.opt, grad_scale)
-        self.finalize(batch_for_stats or self.B, increment)
+        # the step's finalize rides on the optimizer launch (its last block runs it: one launch
+        # fewer per step, misc.hip fused_opt_k; the launcher falls back to two launches)
+        self.fp.apply(self.opt, grad_scale, fin=self._fin_args(batch_for_stats or self.B, increment))
 
-    def finalize(self, batch: int, increment: bool = True) -> None:
+    def _fin_args(self, batch: int, increment: bool) -> tuple:
+        """finalize_step's arguments after `step` (consumes the deferred CE block count)."""
         fp = self.fp
         nw = len(fp.wd_entries)
         nblk = getattr(self, "_ce_defer_blocks", 0)   # HipNetF32 borrows this method
         self._ce_defer_blocks = 0
-        kernels().finalize_step(fp.step, self.stats, fp.l2 if nw else None, fp.wds if nw else None, nw,
-                                self.loss_ema, len(self.loss_names), batch, increment,
-                                fp.l2_ranges if nw else None, self.ce_work if nblk else None, nblk)
+        return (self.stats, fp.l2 if nw else None, fp.wds if nw else None, nw, self.loss_ema, len(self.loss_names),
+                batch, increment, fp.l2_ranges if nw else None, self.ce_work if nblk else None, nblk)
+
+    def finalize(self, batch: int, increment: bool = True) -> None:
+        kernels().finalize_step(self.fp.step, *self._fin_args(batch, increment))
 
     def train_step(self, grad_scale: float = 1.0) -> None:
         self.forward(defer_head=True)

@@ -352,6 +352,7 @@ class HipNetF32:
     # shared with the bf16 plan: K9 update + finalisation, stats readback
     update = HipNet.update
     finalize = HipNet.finalize
+    _fin_args = HipNet._fin_args
     read_stats = HipNet.read_stats
 
     def can_gather_input(self) -> bool:

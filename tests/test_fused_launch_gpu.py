@@ -1,0 +1,59 @@
+"""Launch fusions of the step's tail (misc.hip):
+
+* the optimizer launch runs the step's finalize in its last block (agent-scope ticket),
+  instead of a separate finalize_k launch -- the same code on the same partials, so the step
+  counter, the stats, the loss EMAs and the parameters are BITWISE those of the two-launch path;
+* the split-K reduce's partial pass finishes its own quads by ticket (one launch instead of
+  two) -- the same sums up to the fp32 order of > 4 partials.
+
+Several steps, so the tickets' self-reset is exercised too.
+"""
+import pytest
+import torch
+
+from distributed_tensorflow_ibm_mnist_amd.models import get_model, torch_ref
+from distributed_tensorflow_ibm_mnist_amd.runtime.params import OptConfig
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(dev, K, model, B, fin_fused, red_fused, steps=3):
+    from distributed_tensorflow_ibm_mnist_amd.runtime.executor import HipNet
+    K.set_opt_fin_fused(int(fin_fused))
+    K.set_reduce_fused(int(red_fused))
+    try:
+        spec = get_model(model, 1)
+        net = HipNet(spec, B, dev, torch_ref.init_params(spec, seed=5),
+                     OptConfig(lr0=0.05, momentum=0.9, use_momentum=True, ema_max=0.999))
+        g = torch.Generator(device=dev).manual_seed(5)
+        for _ in range(steps):
+            net.x0.copy_((torch.rand(B, 28, 28, 1, device=dev, generator=g) - 0.5).to(torch.bfloat16))
+            net.labels.copy_(torch.randint(0, 10, (B,), device=dev, generator=g, dtype=torch.int32))
+            net.train_step()
+        torch.cuda.synchronize()
+        return {"params": net.fp.params.clone(), "stats": net.stats.clone(), "ema": net.loss_ema.clone(),
+                "step": int(net.fp.step.item()), "grads": net.fp.grads.clone()}
+    finally:
+        K.set_opt_fin_fused(1)
+        K.set_reduce_fused(1)
+
+
+@pytest.mark.parametrize("model,B", [("lenet5", 4096), ("reference_cnn", 512)])
+def test_optimizer_runs_finalize_bitwise(dev, K, model, B):
+    a = _run(dev, K, model, B, fin_fused=False, red_fused=True)
+    b = _run(dev, K, model, B, fin_fused=True, red_fused=True)
+    assert a["step"] == b["step"] == 3
+    for k in ("params", "stats", "ema"):
+        assert torch.equal(a[k], b[k]), k
+    assert K.opt_fin_fused_enabled() and K.reduce_fused_enabled()
+
+
+@pytest.mark.parametrize("model,B", [("lenet5", 4096), ("reference_cnn", 512)])
+def test_one_launch_reduce_matches_two(dev, K, model, B):
+    a = _run(dev, K, model, B, fin_fused=True, red_fused=False)
+    b = _run(dev, K, model, B, fin_fused=True, red_fused=True)
+    assert a["step"] == b["step"] == 3
+    err = ((a["params"].double() - b["params"].double()).norm() / a["params"].double().norm()).item()
+    assert err < 1e-6, err
+    gerr = ((a["grads"].double() - b["grads"].double()).norm() / a["grads"].double().norm()).item()
+    assert gerr < 1e-5, gerr

@@ -430,6 +430,45 @@ def test_splitk_reduce_multi_matches_single(dev, K):
     assert torch.allclose(b.double(), ref[br, :J], rtol=1e-5, atol=1e-4)
 
 
+def test_splitk_reduce_fused_matches_two_launch(dev, K):
+    """The one-launch reduce (partial blocks finish their quads by ticket) == the partial +
+    reduce launches: bitwise where the partial pass leaves <= 4 partials (the same summation
+    order), to fp32 rounding otherwise; repeated launches (tickets reset) give the same bits."""
+    torch.manual_seed(1)
+    cases = [  # (splits, M, N, G, Ipad, I, J, bias_row)
+        (256, 208, 16, 25, 8, 6, 16, 200),    # LeNet-5 conv2 slab: sb = 4
+        (256, 32, 8, 25, 1, 1, 8, 25),        # LeNet-5 conv1 slab: one quad block
+        (1024, 208, 16, 25, 8, 6, 16, 200),   # sb = 16
+        (48, 401, 120, 1, 400, 400, 120, 400),   # no partial pass, same launch
+        (300, 48, 8, 5, 8, 5, 6, 40),
+    ]
+    base = [torch.randn(S * M * N, device=dev) for (S, M, N, *_r) in cases]
+    geo = torch.tensor(cases, dtype=torch.int64)
+
+    def run(fused):
+        K.set_reduce_fused(int(fused))
+        ws = [torch.empty(G * I * J, device=dev) for (S, M, N, G, Ip, I, J, br) in cases]
+        bs = [torch.empty(J, device=dev) for (S, M, N, G, Ip, I, J, br) in cases]
+        K.splitk_reduce_multi([b.clone() for b in base], ws, bs, geo, [0.5] * len(cases))
+        torch.cuda.synchronize()
+        return ws, bs
+
+    try:
+        w0, b0 = run(False)
+        w1, b1 = run(True)
+        w2, b2 = run(True)
+    finally:
+        K.set_reduce_fused(1)
+    assert K.reduce_fused_enabled()
+    for i, c in enumerate(cases):
+        assert torch.equal(w1[i], w2[i]) and torch.equal(b1[i], b2[i])
+        if c[0] <= 256:
+            assert torch.equal(w0[i], w1[i]) and torch.equal(b0[i], b1[i]), i
+        else:
+            assert torch.allclose(w0[i], w1[i], rtol=1e-5, atol=1e-5)
+            assert torch.allclose(b0[i], b1[i], rtol=1e-5, atol=1e-5)
+
+
 # odd (non multiple-of-8) dense shapes take the general scalar-tail loaders
 @pytest.mark.parametrize("M,Din,Dout", [(77, 37, 13), (300, 101, 9), (5, 9, 3)])
 def test_dense_general_loaders(dev, K, M, Din, Dout):

@@ -12,6 +12,9 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
+#include <tuple>
+#include <vector>
 
 namespace mnistx {
 namespace {
@@ -1194,10 +1197,11 @@ hipError_t softmax_ce(const float* logits, int ldl, const int32_t* labels, int B
 }
 
 // Tickets of the fused reduce (one int per partial-pass quad block of a launch: at most
-// MAXRED * 512) and of the optimizer's finalize (slot MAXRED * 512), zeroed once per device and left zeroed by every launch.  nullptr (the two-launch
-// path) when disabled (MNISTX_REDUCE_FUSED=0) or when the first use falls inside a stream
-// capture (no allocation there).  Launches on one device must not overlap in time: the
-// executors issue them on their compute stream.
+// MAXRED * 512) and of the optimizer's finalize (slot MAXRED * 512): one zeroed buffer per
+// (device, stream), left zeroed by every launch, so launches on different streams (the
+// executor's overlapped side-stream reduces) never share a ticket, and launches on one
+// stream are ordered.  nullptr (the two-launch path) when disabled (MNISTX_REDUCE_FUSED=0)
+// or while the stream is being captured (graphs keep the two launches).
 static int g_reduce_fused = -1;
 void set_reduce_fused(int on) { g_reduce_fused = on; }
 int reduce_fused_enabled() {
@@ -1209,19 +1213,21 @@ int reduce_fused_enabled() {
 }
 static int* red_tickets(hipStream_t st, bool any_use = false) {
   if (!any_use && !reduce_fused_enabled()) return nullptr;
-  static int* tick[64] = {};
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (!tick[dev]) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    int* p = nullptr;
-    const size_t bytes = (MAXRED * 512 + 64) * sizeof(int);   // + the optimizer's finalize ticket
-    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
-    tick[dev] = p;
-  }
-  return tick[dev];
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  static std::mutex mu;
+  static std::vector<std::tuple<int, hipStream_t, int*>> bufs;
+  std::lock_guard<std::mutex> lk(mu);
+  for (const auto& b : bufs)
+    if (std::get<0>(b) == dev && std::get<1>(b) == st) return std::get<2>(b);
+  int* p = nullptr;
+  const size_t bytes = (MAXRED * 512 + 64) * sizeof(int);   // + the optimizer's finalize ticket
+  if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+  if (hipMemset(p, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
+  bufs.emplace_back(dev, st, p);
+  return p;
 }
 
 hipError_t splitk_reduce_multi(const RedSpec* specs, int n, hipStream_t st) {

@@ -57,3 +57,27 @@ def test_one_launch_reduce_matches_two(dev, K, model, B):
     assert err < 1e-6, err
     gerr = ((a["grads"].double() - b["grads"].double()).norm() / a["grads"].double().norm()).item()
     assert gerr < 1e-5, gerr
+
+
+def test_fused_reduce_on_two_streams_at_once(dev, K):
+    """Tickets are per stream: one-launch reduces queued on two streams without any
+    synchronisation between them (the executor's overlapped side-stream reduces) still sum
+    every quad block exactly once."""
+    torch.manual_seed(3)
+    case = (256, 208, 16, 25, 8, 6, 16, 200)   # LeNet-5 conv2 slab: 13 quad blocks x 4 partials
+    S, M, N, G, Ip, I, J, br = case
+    geo = torch.tensor([case], dtype=torch.int64)
+    n = 12
+    slabs = [torch.randn(S * M * N, device=dev) for _ in range(n)]
+    refs = [(s.double().view(S, M, N).sum(0) * 0.5) for s in slabs]
+    outs = [(torch.empty(G * I * J, device=dev), torch.empty(J, device=dev)) for _ in range(n)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    for i in range(n):
+        with torch.cuda.stream(streams[i % 2]):
+            K.splitk_reduce_multi([slabs[i]], [outs[i][0]], [outs[i][1]], geo, [0.5])
+    torch.cuda.synchronize()
+    for i in range(n):
+        wr = refs[i][:G * Ip].view(G, Ip, N)[:, :I, :J].reshape(-1)
+        assert torch.allclose(outs[i][0].double(), wr, rtol=1e-5, atol=1e-4), i
+        assert torch.allclose(outs[i][1].double(), refs[i][br, :J], rtol=1e-5, atol=1e-4), i

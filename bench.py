@@ -73,6 +73,9 @@ def parse():
     ap.add_argument("--bwd_u8", type=int, default=1,
                     help="--input bf16: the fused LeNet conv backward reads the uint8 twin of the dataset (half "
                          "the bytes, normalised in the kernel) instead of the bf16 copy")
+    ap.add_argument("--input_lookahead", type=int, default=1,
+                    help="--input u8/bf16, eager: the next batch's shuffle rows + labels are computed by extra "
+                         "blocks of the optimizer launch (DeviceLoader.lookahead_job) instead of a launch of their own")
     ap.add_argument("--ps_no_compute", type=int, default=0,
                     help="PS mode: workers push the same gradient back to back without computing a step -- "
                          "the PS data plane's own capacity (ms per applied update), e.g. 7 workers on one GPU")
@@ -339,6 +342,8 @@ def main() -> int:
     if use_graph:
         from distributed_tensorflow_ibm_mnist_amd.runtime.graph import StepGraph
         graph = StepGraph(step_body)
+    elif fused_in and args.input_lookahead:
+        net.next_input_job = loader.lookahead_job   # a captured launch would replay one fixed batch
 
     def step():
         loader.next()
@@ -455,6 +460,7 @@ def main() -> int:
                 "optimizer": args.optimizer,
                 "input": mode if fused_in else "prep",
                 "lenet_bwd": ("fused" if getattr(net, "fused_bwd", False) else "split") if args.model == "lenet5" else None,
+                "input_lookahead": getattr(net, "next_input_job", None) is not None,
             },
             "tflops_per_s": round(tot * value / 1e12, 2),
             "final_train_loss": round(stats["cross_entropy"], 5),

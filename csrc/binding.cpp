@@ -498,7 +498,7 @@ void fused_optimizer(Tensor params, Tensor grads, Tensor mom, Tensor ema, Tensor
                      double lr0, double decay_rate, int64_t decay_steps, double momentum, bool nesterov,
                      bool use_momentum, double grad_scale, double ema_max, optional<Tensor> l2,
                      optional<Tensor> guard, int64_t guard_want, optional<Tensor> guard_err, int64_t guard_id,
-                     optional<py::tuple> fin) {
+                     optional<py::tuple> fin, optional<py::tuple> perm) {
   const int64_t total = params.numel();
   check(params, at::kFloat, total, "params");
   check(grads, at::kFloat, total, "grads");
@@ -579,9 +579,35 @@ void fused_optimizer(Tensor params, Tensor grads, Tensor mom, Tensor ema, Tensor
     fa = prep_fin(step, t[0].cast<Tensor>(), ot(1), ot(2), t[3].cast<int64_t>(), ot(4), t[5].cast<int64_t>(),
                   t[6].cast<int64_t>(), t[7].cast<bool>(), ot(8), ot(9), t[10].cast<int64_t>());
   }
+  // perm: (out, lab_src, lab_out, start, N, seed, h) -- perm_positions of the next batch, run by
+  // extra blocks of this launch
+  mnistx::PermJob pj{};
+  const bool has_perm = perm.has_value() && !perm->is_none();
+  if (has_perm) {
+    const py::tuple& t = *perm;
+    TORCH_CHECK(t.size() == 7, "perm: (out, lab_src, lab_out, start, N, seed, h)");
+    Tensor out = t[0].cast<Tensor>(), ls = t[1].cast<Tensor>(), lo = t[2].cast<Tensor>();
+    const int64_t start = t[3].cast<int64_t>(), N = t[4].cast<int64_t>(), seed = t[5].cast<int64_t>(),
+                  h = t[6].cast<int64_t>();
+    TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kLong && out.is_contiguous() &&
+                    out.device() == params.device(), "perm: out");
+    TORCH_CHECK(N > 0 && h >= 1 && h <= 31 && (1ll << (2 * h)) >= N, "perm: bad domain");
+    TORCH_CHECK(out.numel() < (1ll << 31), "perm: too many rows");
+    check(ls, at::kInt, N, "perm lab_src");
+    check(lo, at::kInt, out.numel(), "perm lab_out");
+    pj.out = out.data_ptr<int64_t>();
+    pj.lab_src = P<const int32_t>(ls);
+    pj.lab_out = P<int32_t>(lo);
+    pj.start = start;
+    pj.N = N;
+    pj.seed = (uint32_t)seed;
+    pj.h = (int)h;
+    pj.n = (int)out.numel();
+  }
   hip_ok(mnistx::fused_optimizer(P<float>(params), P<const float>(grads), use_momentum ? P<float>(mom) : nullptr,
                                  ema_max >= 0 ? P<float>(ema) : nullptr, BFm(bf), sv.data(), nseg, total,
-                                 P<const int64_t>(step), op, l2p, l2n, cur_stream(), has_fin ? &fa : nullptr),
+                                 P<const int64_t>(step), op, l2p, l2n, cur_stream(), has_fin ? &fa : nullptr,
+                                 has_perm ? &pj : nullptr),
          "fused_optimizer");
 }
 
@@ -1272,7 +1298,7 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("decay_steps"), py::arg("momentum"), py::arg("nesterov"), py::arg("use_momentum"),
         py::arg("grad_scale"), py::arg("ema_max"), py::arg("l2") = py::none(), py::arg("guard") = py::none(),
         py::arg("guard_want") = 0, py::arg("guard_err") = py::none(), py::arg("guard_id") = 0,
-        py::arg("fin") = py::none());
+        py::arg("fin") = py::none(), py::arg("perm") = py::none());
   m.def("set_opt_fin_fused", [](int64_t on) { mnistx::set_opt_fin_fused((int)on); },
         "A/B switch of the optimizer launch running the step's finalize (MNISTX_OPT_FIN_FUSED)");
   m.def("opt_fin_fused_enabled", []() { return mnistx::opt_fin_fused_enabled() != 0; });

@@ -357,9 +357,21 @@ struct FinArgs {
 // fin (optional): the step's finalize_step, run by the optimizer launch's last block when the
 // grid is small (<= 1024 blocks: one ticket address per launch) and no PS guard is set, else
 // launched right after it (MNISTX_OPT_FIN_FUSED=0: always separate)
+// the next batch's epoch-shuffle rows + labels (perm_positions), computed by extra blocks of the
+// optimizer launch instead of a launch of their own at the next step's start (blk0: set by
+// the launcher)
+struct PermJob {
+  int64_t* out;
+  const int32_t* lab_src;
+  int32_t* lab_out;
+  int64_t start, N;
+  uint32_t seed;
+  int h, n, blk0;
+};
+// perm (optional): run that job in the same launch
 hipError_t fused_optimizer(float* params, const float* grads, float* mom, float* ema, bf16_t* bf, const OptSeg* segs,
                            int nseg, int64_t total, const int64_t* step, OptParams op, float* l2, int l2n, hipStream_t st,
-                           const FinArgs* fin = nullptr);
+                           const FinArgs* fin = nullptr, const PermJob* perm = nullptr);
 void set_opt_fin_fused(int on);
 int opt_fin_fused_enabled();
 // l2r (optional, device int32 [nw][3] = {weight index, first block, end block}): sum the

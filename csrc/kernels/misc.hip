@@ -54,9 +54,8 @@ DEV uint64_t feistel4(uint64_t x, const uint32_t* key, int h) {
 }
 // lab_src / lab_out (optional): the labels of the chosen rows gathered in the same
 // launch (the resident-dataset input modes need only the index and the labels).
-__global__ void perm_positions_k(int64_t* __restrict__ out, int64_t start, int n, int64_t N, uint32_t seed, int h,
-                                 const int32_t* __restrict__ lab_src, int32_t* __restrict__ lab_out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+DEV void perm_one(int i, int64_t* __restrict__ out, int64_t start, int n, int64_t N, uint32_t seed, int h,
+                  const int32_t* __restrict__ lab_src, int32_t* __restrict__ lab_out) {
   if (i >= n) return;
   const int64_t p = start + i;
   const int64_t e = p / N;
@@ -68,6 +67,10 @@ __global__ void perm_positions_k(int64_t* __restrict__ out, int64_t start, int n
   do { x = feistel4(x, key, h); } while (x >= (uint64_t)N);
   out[i] = (int64_t)x;
   if (lab_out) lab_out[i] = lab_src[x];
+}
+__global__ void perm_positions_k(int64_t* __restrict__ out, int64_t start, int n, int64_t N, uint32_t seed, int h,
+                                 const int32_t* __restrict__ lab_src, int32_t* __restrict__ lab_out) {
+  perm_one(blockIdx.x * blockDim.x + threadIdx.x, out, start, n, N, seed, h, lab_src, lab_out);
 }
 
 // ------------------------------------------------------------------ K10 input prep
@@ -769,10 +772,16 @@ __global__ __launch_bounds__(TPB) void fused_opt_k(float* __restrict__ params, c
                                                    float* __restrict__ mom, float* __restrict__ ema,
                                                    bf16_t* __restrict__ bf, SegTable tab,
                                                    const int64_t* __restrict__ step_p, OptParams op,
-                                                   float* __restrict__ l2, FinArgs fin) {
+                                                   float* __restrict__ l2, FinArgs fin, PermJob pj) {
   __shared__ float red[TPB / 64];
   __shared__ float wsum[FIN_MAXW];
   __shared__ int last;
+  const int nopt = pj.n > 0 ? pj.blk0 : (int)gridDim.x;   // optimizer blocks; the rest: the perm job
+  if ((int)blockIdx.x >= nopt) {
+    perm_one(((int)blockIdx.x - nopt) * TPB + threadIdx.x, pj.out, pj.start, pj.n, pj.N, pj.seed, pj.h, pj.lab_src,
+             pj.lab_out);
+    return;
+  }
   if (op.guard && *op.guard != op.guard_want) {   // a stale / torn PS push: never applied
     if (blockIdx.x == 0 && threadIdx.x == 0) *op.guard_err = op.guard_id;
     return;
@@ -904,7 +913,7 @@ __global__ __launch_bounds__(TPB) void fused_opt_k(float* __restrict__ params, c
   // the step's finalize in this launch: the last block to take a ticket (thread 0, after its
   // coherent partial store) runs it, reading the partials coherently; every block has read
   // *step_p by now
-  if (threadIdx.x == 0) last = take_ticket(fin.ticket) == (int)gridDim.x - 1;
+  if (threadIdx.x == 0) last = take_ticket(fin.ticket) == nopt - 1;
   __syncthreads();
   if (!last) return;
   if (threadIdx.x == 0) *fin.ticket = 0;
@@ -1323,7 +1332,7 @@ hipError_t finalize_step(const FinArgs& f, hipStream_t st) {
 
 hipError_t fused_optimizer(float* params, const float* grads, float* mom, float* ema, bf16_t* bf, const OptSeg* segs,
                            int nseg, int64_t total, const int64_t* step, OptParams op, float* l2, int l2n,
-                           hipStream_t st, const FinArgs* fin) {
+                           hipStream_t st, const FinArgs* fin, const PermJob* perm) {
   if (nseg > MAXSEG || nseg < 1) return hipErrorInvalidValue;
   if (fin && fin->nw > FIN_MAXW) return hipErrorInvalidValue;
   SegTable tab;
@@ -1347,7 +1356,15 @@ hipError_t fused_optimizer(float* params, const float* grads, float* mom, float*
     fa = *fin;
     fa.ticket = tickets + MAXRED * 512;   // the optimizer's slot after the reduce's
   }
-  hipLaunchKernelGGL(fused_opt_k, dim3(nb), dim3(TPB), 0, st, params, grads, mom, ema, bf, tab, step, op, l2, fa);
+  PermJob pj{};
+  int npb = 0;
+  if (perm && perm->n > 0) {
+    pj = *perm;
+    pj.blk0 = nb;
+    npb = (pj.n + TPB - 1) / TPB;
+  }
+  hipLaunchKernelGGL(fused_opt_k, dim3(nb + npb), dim3(TPB), 0, st, params, grads, mom, ema, bf, tab, step, op, l2, fa,
+                     pj);
   if (fin && !tickets) return finalize_step(*fin, st);
   return hipGetLastError();
 }

@@ -149,6 +149,7 @@ class DeviceLoader:
         self.seed = (seed if shard else seed + 7919 * rank) & M32
         self.idx = torch.empty(self.B, dtype=torch.int64, device=ds.device)
         self.pos = 0          # stream position of the next global batch
+        self._ahead = None    # position whose rows + labels an optimizer launch already wrote
 
     @property
     def epoch(self) -> int:
@@ -158,9 +159,28 @@ class DeviceLoader:
         """Position the stream at global step ``step`` (resume from a checkpoint)."""
         self.pos = int(step) * self.global_batch
 
+    def lookahead_job(self) -> Optional[tuple]:
+        """The NEXT local batch's ``perm_positions`` job -- (rows out, dataset labels, labels out,
+        start, N, seed, h) -- for the current step's optimizer launch to run in extra blocks
+        (``HipNet.next_input_job``, misc.hip ``PermJob``); the next ``next()`` then launches
+        nothing.  Only for the resident-dataset shuffle (``idx_out``) with full batches, and
+        only where nothing else writes the index / label buffers between the optimizer and
+        the next ``next()`` (bench.py; not the CLI loop, which evaluates into them)."""
+        if not (self.shuffle and self.idx_out is not None and self.idx_out.is_cuda and self.ds.device.type == "cuda"):
+            return None
+        N = len(self.ds)
+        start = self.pos + (self.rank * self.B if self.shard else 0)
+        self._ahead = self.pos
+        return (self.idx_out[:self.B], self.ds.labels, self.out_labels[:self.B], int(start), int(N), int(self.seed),
+                _half_bits(N))
+
     def next(self, nb: Optional[int] = None) -> int:
         """Gather the next local batch into the output buffers; returns its size."""
         nb = self.B if nb is None else nb
+        ahead, self._ahead = self._ahead, None
+        if ahead is not None and ahead == self.pos and nb == self.B:
+            self.pos += self.global_batch   # the previous optimizer launch wrote this batch
+            return nb
         start = self.pos + (self.rank * self.B if self.shard else 0)
         N = len(self.ds)
         if (self.shuffle and self.idx_out is None and self.ds.device.type == "cuda" and self.ds.hw == 784

@@ -801,7 +801,10 @@ class HipNet:
     def update(self, grad_scale: float = 1.0, increment: bool = True, batch_for_stats: Optional[int] = None) -> None:
         # the step's finalize rides on the optimizer launch (its last block runs it: one launch
         # fewer per step, misc.hip fused_opt_k; the launcher falls back to two launches)
-        self.fp.apply(self.opt, grad_scale, fin=self._fin_args(batch_for_stats or self.B, increment))
+        # and, when a loader offers it (next_input_job: DeviceLoader.lookahead_job), the next
+        # batch's shuffle rows + labels run in extra blocks of the same launch
+        job = self.next_input_job() if getattr(self, "next_input_job", None) is not None else None
+        self.fp.apply(self.opt, grad_scale, fin=self._fin_args(batch_for_stats or self.B, increment), perm=job)
 
     def _fin_args(self, batch: int, increment: bool) -> tuple:
         """finalize_step's arguments after `step` (consumes the deferred CE block count)."""

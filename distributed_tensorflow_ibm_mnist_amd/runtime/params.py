@@ -226,11 +226,13 @@ class FlatParams:
         return {e.name: self.param_view(e.name).detach().cpu().clone() for e in self.entries}
 
     # -- K9 -------------------------------------------------------------------
-    def apply(self, cfg: OptConfig, grad_scale: float = 1.0, track_l2: bool = True, fin: Optional[tuple] = None) -> None:
+    def apply(self, cfg: OptConfig, grad_scale: float = 1.0, track_l2: bool = True, fin: Optional[tuple] = None,
+              perm: Optional[tuple] = None) -> None:
         """``fin``: finalize_step's arguments after ``step`` -- the step's finalize then runs
-        in the same launch (HipNet.update)."""
+        in the same launch (HipNet.update); ``perm``: the next batch's perm_positions job
+        (DeviceLoader.lookahead_job), run by extra blocks of the launch."""
         from ..ops._ext import kernels
         kernels().fused_optimizer(self.params, self.grads, self.mom, self.ema, self.bf16, self.segs, self.step,
                                   cfg.lr0, cfg.decay_rate, cfg.decay_steps, cfg.momentum, cfg.nesterov,
                                   cfg.use_momentum, grad_scale, cfg.ema_max,
-                                  self.l2 if (track_l2 and self.wd_entries) else None, fin=fin)
+                                  self.l2 if (track_l2 and self.wd_entries) else None, fin=fin, perm=perm)

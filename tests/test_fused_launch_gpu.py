@@ -81,3 +81,38 @@ def test_fused_reduce_on_two_streams_at_once(dev, K):
         wr = refs[i][:G * Ip].view(G, Ip, N)[:, :I, :J].reshape(-1)
         assert torch.allclose(outs[i][0].double(), wr, rtol=1e-5, atol=1e-4), i
         assert torch.allclose(outs[i][1].double(), refs[i][br, :J], rtol=1e-5, atol=1e-4), i
+
+
+@pytest.mark.parametrize("model", ["lenet5", "reference_cnn"])
+def test_optimizer_launch_writes_next_batch_rows(dev, K, model):
+    """DeviceLoader.lookahead_job: the optimizer launch of step k writes step k+1's shuffle
+    rows + labels (extra blocks), the next ``next()`` launches nothing, and the rows are those
+    of perm_positions at the right stream position, across epoch boundaries; the training is
+    bitwise the same as with a perm launch per step."""
+    from distributed_tensorflow_ibm_mnist_amd.data.device_loader import (DeviceDataset, DeviceLoader, _half_bits,
+                                                                          perm_positions)
+    from distributed_tensorflow_ibm_mnist_amd.data.synthetic import make_synthetic
+    from distributed_tensorflow_ibm_mnist_amd.runtime.executor import HipNet
+    B, N, steps = 256, 1000, 6   # epoch boundaries inside steps 3 and 7
+    imgs, labs = make_synthetic(N, seed=2, channels=1, device=dev)
+    ds = DeviceDataset(imgs, labs, dev, hw=784, channels=1)
+    runs = []
+    for ahead in (False, True):
+        spec = get_model(model, 1)
+        net = HipNet(spec, B, dev, torch_ref.init_params(spec, seed=9), OptConfig(lr0=0.05, momentum=0.9,
+                                                                                   use_momentum=True))
+        assert net.bind_u8_input(ds.images)
+        loader = DeviceLoader(ds, net.x0, net.labels, seed=4, idx_out=net.idx_buf)
+        if ahead:
+            net.next_input_job = loader.lookahead_job
+        for k in range(steps):
+            loader.next()
+            want = perm_positions(k * B, B, N, 4, device=dev)
+            assert torch.equal(net.idx_buf[:B], want), (ahead, k)
+            assert torch.equal(net.labels[:B], ds.labels[want]), (ahead, k)
+            net.train_step()
+        torch.cuda.synchronize()
+        assert loader.pos == steps * B
+        runs.append(net.fp.params.clone())
+    assert torch.equal(runs[0], runs[1])
+    assert _half_bits(N) == 5

@@ -172,6 +172,21 @@ def test_feistel_epoch_permutation_and_sharding():
     l2.next(); l1b.next()
     assert torch.equal(l2.out_labels, l1b.out_labels)
 
+    # lookahead bookkeeping (the rows themselves are written on the GPU by the optimizer
+    # launch, tests/test_fused_launch_gpu.py): no job off the resident-GPU mode; a recorded
+    # position makes exactly the matching next() skip its gather, any other falls through
+    assert l0.lookahead_job() is None
+    la = loader(0, 1)
+    la.next()
+    la._ahead = la.pos                       # what lookahead_job records
+    before = la.out_labels.clone()
+    la.out_labels.fill_(-1)
+    assert la.next() == 8 and la.pos == 16 and la._ahead is None
+    assert int(la.out_labels.min()) == -1    # skipped: the optimizer launch wrote this batch
+    la._ahead = 0                            # stale (e.g. after seek): gather as usual
+    la.next()
+    assert la.pos == 24 and int(la.out_labels.min()) >= 0 and not torch.equal(la.out_labels, before)
+
 
 def test_meta_graph_def_structure(tmp_path):
     """model.ckpt-N.meta is a MetaGraphDef of the checkpoint's variable graph: one VariableV2

@@ -650,10 +650,6 @@ __global__ __launch_bounds__(256) void splitk_reduce4_k(RedTable tab) {
   red_reduce_block(tab, blockIdx.x, part);
 }
 
-// First pass for many splits over a small output: block (q, s) of a descriptor
-// sums splits [64 s, 64 s + 64) of its 64 quads and stores the sum IN PLACE in
-// split 64 s (only this block reads or writes that range), so the reduce pass
-// has S/64 splits.  Returns the quad block's descriptor and quad index (for the ticket).
 // agent-scope relaxed store / load: written through to / read from the coherence point (no
 // L2-wide write-back or invalidate: the fences those need cost ~18 us in the LeNet-5 step and
 // ~190 us in the reference CNN's when every block of a launch ran one)

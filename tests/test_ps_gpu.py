@@ -149,7 +149,9 @@ def test_ps_ipc_corrupt_push_aborts_naming_worker(dev):
     silently)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.join(ROOT, "bench.py"),
-           "--mode", "ps", "--ps_transport", "ipc", "--batch", "256", "--steps", "20", "--warmup", "2"]
+           "--mode", "ps", "--ps_transport", "ipc", "--batch", "256", "--steps", "150", "--warmup", "2"]
+    # 150 steps: the workers race for a shared update budget, and one run where worker 0's
+    # cold first step took 122 ms left it a single push of 44 (its 4th never came)
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240,
                        env=dict(os.environ, OMP_NUM_THREADS="2", MNIST_FI_CORRUPT_PUSH="0:4"))
     out = r.stdout + r.stderr

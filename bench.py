@@ -83,8 +83,10 @@ def parse():
     ap.add_argument("--ps_no_compute", type=int, default=0,
                     help="PS mode: workers push the same gradient back to back without computing a step -- "
                          "the PS data plane's own capacity (ms per applied update), e.g. 7 workers on one GPU")
-    ap.add_argument("--ps_transport", default="ipc", choices=["shm", "ipc", "host"],
-                    help="PS data plane: ipc = xGMI peer copies into PS-owned buffers; host = gloo, host-staged")
+    ap.add_argument("--ps_transport", default="", choices=["", "shm", "ipc", "host"],
+                    help="PS data plane: '' = the CLI's default (parallel/ps.default_transport: shm up to 1 M "
+                         "parameters per shard, ipc above); shm = CPU PS on pinned shared memory; ipc = xGMI peer "
+                         "copies into a GPU PS; host = gloo, host-staged")
     ap.add_argument("--eager_steps", type=int, default=-1,
                     help="N=1 with a hipGraph: also time this many EAGER steps after the timed region "
                          "(ms_per_step_eager, comparable with N>1 runs); -1 = --steps")
@@ -210,6 +212,11 @@ def run_ps(args) -> int:
     if world < 2:
         print("[bench] --mode ps needs >= 2 ranks (torchrun --nproc-per-node N)", file=sys.stderr)
         return 2
+    from distributed_tensorflow_ibm_mnist_amd.parallel.ps import default_transport, max_shard_params
+    from distributed_tensorflow_ibm_mnist_amd.train.trainer import param_specs as _pspecs
+    # the same resolution as the CLI (main.py --ps_backend ''), on every rank
+    args.ps_transport = args.ps_transport or default_transport(
+        torch.device("cuda"), max_shard_params(_pspecs(get_model(args.model, args.in_channels)), 1))
     if rank == 0 and args.ps_transport == "shm":
         dev = torch.device("cpu")             # the shm PS is a CPU task: it never opens the GPU
     else:

@@ -3,10 +3,12 @@
 gradient back to back (no compute), so the PS's service time per applied update is what is
 measured -- the bound of the BASELINE "1 PS + 7 workers" config once every worker owns a
 GPU (on a one-GPU box the workers' step graphs time-slice the GPU and hide it,
-profiles/r5/ps/).  Transports: shm (CPU PS, native loop on a shared-memory segment) and
-host (gloo messages, the portable fallback).
+profiles/r5/ps/).  Transports: shm (CPU PS, native loop on a shared-memory segment),
+host (gloo messages, the portable fallback) and ipc (GPU PS: every rank on cuda:0 of a
+one-GPU box, peer copies degenerate to device copies -- the PS's own service time, not
+xGMI bandwidth).  '' = the CLI default for the model (parallel/ps.default_transport).
 
-    python bench/ps_capacity.py [--model lenet5] [--workers 3,7] [--updates 3000]
+    python bench/ps_capacity.py [--model lenet5] [--workers 3,7] [--updates 3000] [--transports shm,host]
 """
 from __future__ import annotations
 
@@ -39,12 +41,16 @@ def _rank(rank, world, port, model, transport, updates, q):
     from distributed_tensorflow_ibm_mnist_amd.parallel.ps import ParameterServer, PSClient
     from distributed_tensorflow_ibm_mnist_amd.runtime.params import OptConfig
     from distributed_tensorflow_ibm_mnist_amd.train.trainer import param_specs
+    from distributed_tensorflow_ibm_mnist_amd.parallel.ps import default_transport, max_shard_params
     spec = get_model(model, 1)
     init = torch_ref.init_params(spec, seed=0)
     opt = OptConfig(lr0=0.01, momentum=0.9, use_momentum=True, ema_max=0.9999)
     nw = world - 1
+    if not transport:
+        transport = default_transport(torch.device("cuda"), max_shard_params(param_specs(spec), 1))
+    dev = "cuda:0" if transport == "ipc" else "cpu"
     if rank == 0:
-        ps = ParameterServer(0, 1, nw, param_specs(spec), init, opt, "cpu", updates, log=lambda *a: None,
+        ps = ParameterServer(0, 1, nw, param_specs(spec), init, opt, dev, updates, log=lambda *a: None,
                              transport=transport)
         m0 = updates // 10
         ps.marks = {m0: 0.0, updates: 0.0}
@@ -57,7 +63,7 @@ def _rank(rank, world, port, model, transport, updates, q):
                "per_worker": res["per_worker"]})
     else:
         from distributed_tensorflow_ibm_mnist_amd.runtime.torchnet import TorchNet
-        net = TorchNet(spec, 2, "cpu", init, opt)
+        net = TorchNet(spec, 2, dev, init, opt)
         net.fp.grads.normal_(0, 1e-3)
         client = PSClient(net, 1, nw, rank - 1, transport=transport)
         client.hello()

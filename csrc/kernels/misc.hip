@@ -655,10 +655,31 @@ __global__ __launch_bounds__(256) void splitk_reduce4_k(RedTable tab) {
 // ~190 us in the reference CNN's when every block of a launch ran one)
 DEV void st_coh(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 DEV float ld_coh(const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-// a ticket taken after this wave's coherent stores have completed (vmcnt counts stores too)
+// The last-block ticket ("fence-free" hand-off; splitk_fused4_k, fused_opt_k):
+//   every block: st_coh its partials -> take_ticket -> the block whose ticket is the last one
+//   reads every block's partials with ld_coh and combines them.
+// Memory-model argument.  In the HIP / C++ model the relaxed stores and the relaxed fetch_add
+// carry no happens-before, so the language alone does not order them; the protocol rests on the
+// gfx950 lowering of agent-scope relaxed atomics, which is the hand-off the microarchitecture
+// guide (MI355X_MICROARCH.md, "Valid forms", first table row) measures as correct without an
+// acquire: (1) st_coh is `global_store_* sc1` -- written through past the XCD's L2 to the
+// coherence point; (2) `s_waitcnt vmcnt(0)` before the ticket: every such store of the issuing
+// wave has completed (vmcnt counts stores) before the atomic is issued, and the storing wave is
+// the ticket-taking wave (thread 0's wave after a __syncthreads in fused_opt_k; wave 0, which
+// did all the stores, in splitk_fused4_k); (3) the winner's ld_coh is `global_load_* sc1`,
+// served from the coherence point, never from a stale L1 / L2 line; (4) the winner's loads are
+// control-dependent on the ticket's returned value.  The compiler must not move (1) below the
+// ticket or (3) above it: the s_waitcnt builtin is not a compiler barrier, so both sides get a
+// signal fence (compiler-only: no instruction).  tests/test_isa_ticket.py disassembles the
+// built code object and fails if any of sc1 stores, sc1 loads or the vmcnt(0) before the ticket
+// atomic goes missing (a compiler or flag change); release/acquire fences instead cost +20 us
+// (LeNet-5) / +180 us (reference CNN) per step (profiles/r5/launch_fusion/README.md).
 DEV int take_ticket(int* t) {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
   __builtin_amdgcn_s_waitcnt(0);
-  return __hip_atomic_fetch_add(t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int v = __hip_atomic_fetch_add(t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  return v;
 }
 
 // First pass for many splits over a small output: block (q, s) of a descriptor

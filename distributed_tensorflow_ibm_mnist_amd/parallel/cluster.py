@@ -132,7 +132,7 @@ def current_gen(cl: "Cluster") -> int:
 
 def setup_distribute(job_name: str = "", ps_hosts: str = "", worker_hosts: str = "", task_id: int = 0,
                      want_gpu: bool = True, timeout_s: float = 600.0, log=print,
-                     ps_backend: str = "", dp_backend: str = "") -> Cluster:
+                     ps_backend: str = "", dp_backend: str = "", ps_shard_params: int = 0) -> Cluster:
     ps, workers = _split(ps_hosts), _split(worker_hosts)
     env_world = int(os.environ.get("WORLD_SIZE", "1"))
     to = datetime.timedelta(seconds=timeout_s)
@@ -162,14 +162,15 @@ def setup_distribute(job_name: str = "", ps_hosts: str = "", worker_hosts: str =
         if cl.mode == "ps":
             # PS mode: the process group is the gloo control plane; gradients and
             # parameters move on the PS data plane (parallel/ps.py): a CPU PS serving a
-            # shared-memory segment natively ("shm", one host), xGMI peer copies into a GPU
-            # PS ("ipc", default on GPU) or gloo messages staged through host ("host").
+            # shared-memory segment natively ("shm", one host; default on GPU for shards up
+            # to 1 M parameters), xGMI peer copies into a GPU PS ("ipc", default on GPU for
+            # larger shards: ps.default_transport) or gloo messages staged through host ("host").
             cl.backend = "gloo"
             t = {"": "", "gloo": "host", "host": "host", "ipc": "ipc", "shm": "shm"}.get(ps_backend)
             if t is None:
                 raise ValueError(f"--ps_backend={ps_backend!r}: expected shm | ipc | host (gloo)")
             from .ps import default_transport
-            cl.transport = t or default_transport(cl.device)
+            cl.transport = t or default_transport(cl.device, ps_shard_params)
             if cl.transport == "shm" and cl.job_name == "ps":
                 cl.device = torch.device("cpu")    # the shm PS is a CPU task: it never opens a GPU
         if cl.device.type == "cuda":

@@ -140,12 +140,36 @@ def shard_ranges(fp: FlatParams, num_ps: int) -> List[Tuple[int, int, List[str]]
     return out
 
 
-def default_transport(device: torch.device) -> str:
-    """GPU workers: ``shm`` -- a CPU parameter server serving pinned shared memory natively
-    (23 us of PS time per update on MI355X hosts vs 61 us for the GPU PS of ``ipc``, and
-    the PS never time-slices a worker's GPU: profiles/r5/ps/); setup_transport falls back
-    to ``host`` when the ranks span hosts.  CPU runs: ``host`` (gloo)."""
-    return "shm" if torch.device(device).type == "cuda" else "host"
+# The shm data plane's CPU parameter server streams every byte of its shard through host
+# memory per update (params, grads, momentum, EMA, weight decay: 32 bytes per parameter):
+# 23 us for LeNet-5's 61.7 K parameters, but 2.4 ms of apply + 2.2 ms of reply copy for the
+# reference CNN's 3.46 M (bench/ps_capacity.py).  Above this many parameters per
+# shard the GPU parameter server of ``ipc`` (HBM-speed apply, xGMI peer copies) serves instead.
+SHM_MAX_SHARD_PARAMS = 1 << 20
+
+
+def max_shard_params(specs_or_fp, num_ps: int) -> int:
+    """Parameters of the largest PS shard (shard_ranges' split) -- the same number on every
+    rank, computed from the model's parameter specs or a FlatParams."""
+    fp = specs_or_fp if isinstance(specs_or_fp, FlatParams) else FlatParams.build(specs_or_fp, {}, "cpu")
+    size = {e.name: e.n for e in fp.entries}
+    return max(sum(size[n] for n in names) for _, _, names in shard_ranges(fp, num_ps))
+
+
+def default_transport(device: torch.device, shard_params: int = 0) -> str:
+    """The PS data plane when none is asked for; every rank resolves the same one.
+
+    GPU ranks: ``shm`` -- a CPU parameter server serving pinned shared memory natively (23 us
+    of PS time per update at LeNet-5 size vs 61 us for the GPU PS of ``ipc``, and the PS
+    never time-slices a worker's GPU: profiles/r5/ps/) -- for shards up to
+    SHM_MAX_SHARD_PARAMS (``MNISTX_PS_SHM_MAX_PARAMS``); larger shards (the reference CNN)
+    ``ipc``, whose apply runs at HBM speed (profiles/r6/ps/).  setup_transport falls back to
+    ``host`` when the ranks span hosts or a GPU lacks peer access.  CPU runs: ``host`` (gloo).
+    ``shard_params`` 0 = unknown (treated as small)."""
+    if torch.device(device).type != "cuda":
+        return "host"
+    limit = int(os.environ.get("MNISTX_PS_SHM_MAX_PARAMS", str(SHM_MAX_SHARD_PARAMS)))
+    return "shm" if shard_params <= limit else "ipc"
 
 
 def _sync(t: torch.Tensor) -> None:
@@ -167,7 +191,9 @@ def is_peer_loss(e: BaseException) -> bool:
         if t is not None and isinstance(e, t):
             return True
     msg = str(e).lower()
-    if re.search(r"\bhip|cuda", msg):
+    # explicit HIP / CUDA error forms only (a device string such as "cuda:0" inside a gloo
+    # transport error is not a compute error)
+    if re.search(r"\bhip ?error|\bcuda ?error|\bhip runtime error|device-side assert|\bhipgraph\w*error", msg):
         return False             # e.g. hipErrorLaunchTimeOut: a compute failure, re-raised at once
     # only gloo's own transport errors (plain RuntimeError in some builds): the word gloo
     # together with a connection / timeout symptom
@@ -396,10 +422,20 @@ class ShmSegment:
         fd = os.open(path, flags, 0o600)
         try:
             if create:
-                os.ftruncate(fd, lay.total)
+                # reserve every page now: a /dev/shm smaller than the segment then
+                # fails here with ENOSPC -- setup_transport falls back to the host transport --
+                # instead of a SIGBUS when some process first touches a page past the limit
+                try:
+                    os.posix_fallocate(fd, 0, lay.total)
+                except OSError:
+                    os.close(fd)
+                    fd = -1
+                    os.unlink(path)
+                    raise
             self.mm = mmap.mmap(fd, lay.total, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
         finally:
-            os.close(fd)
+            if fd >= 0:
+                os.close(fd)
         import ctypes
         self._cbuf = ctypes.c_char.from_buffer(self.mm)
         self.addr = ctypes.addressof(self._cbuf)
@@ -422,10 +458,17 @@ class ShmSegment:
     def ps_pid(self) -> int:
         return int(self.hdr[3])
 
-    def pin(self) -> bool:
-        """hipHostRegister the mapping (a GPU worker's copies become DMA)."""
+    def pin(self, worker: Optional[int] = None) -> bool:
+        """hipHostRegister the mapping (a GPU worker's copies become DMA): only the
+        worker's own block when ``worker`` is given (registering faults every page in, so
+        pinning the whole segment from every worker would touch every other worker's
+        block), else the whole segment."""
         from ..ops._ext import kernels
-        self.pinned = bool(kernels().host_register(self.addr, self.lay.total))
+        if worker is None:
+            self._pin_at, n = self.addr, self.lay.total
+        else:
+            self._pin_at, n = self.addr + self.lay.HDR + worker * self.lay.wblock, self.lay.wblock
+        self.pinned = bool(kernels().host_register(self._pin_at, n))
         return self.pinned
 
     def close(self) -> None:
@@ -433,7 +476,7 @@ class ShmSegment:
             return
         if self.pinned:
             from ..ops._ext import kernels
-            kernels().host_unregister(self.addr)
+            kernels().host_unregister(self._pin_at)
             self.pinned = False
         self.hdr = self.ctrl = self.push = self.reply = self.state = None
         self._cbuf = None
@@ -484,13 +527,20 @@ class ShmTransport:
         """Collective over the control group: PS j creates its segment, every worker maps
         it, then the names are unlinked."""
         import uuid
+        self.fallback = ""
         for j in range(self.k):
             obj = [None]
             if is_me and ps.j == j:
                 lay = ShmLayout(ps.fp.total, self.W)
                 gen = ps.cluster.gen if ps.cluster is not None else 0
                 path = f"/dev/shm/mnistx_ps{j}_{os.getpid()}_{gen}_{uuid.uuid4().hex[:8]}"
-                self.seg = ShmSegment(path, lay, create=True, gen=gen)
+                try:
+                    self.seg = ShmSegment(path, lay, create=True, gen=gen)
+                except OSError as e:      # e.g. ENOSPC: /dev/shm smaller than the segment
+                    obj = [{"fallback": f"PS {j}: {lay.total / 2**20:.0f} MiB segment: {e}"}]
+                    dist.broadcast_object_list(obj, src=j, group=self.g)
+                    self.fallback = obj[0]["fallback"]
+                    continue
                 self.wd = torch.zeros(ps.fp.total, dtype=torch.float32)
                 for e in ps.fp.entries:
                     if e.wd:
@@ -502,11 +552,15 @@ class ShmTransport:
                 self.cursor = self.W - 1
                 obj = [{"path": path, "n": ps.fp.total}]
             dist.broadcast_object_list(obj, src=j, group=self.g)
-            if ps is None:
+            if "fallback" in obj[0]:
+                self.fallback = self.fallback or obj[0]["fallback"]
+            elif ps is None:
                 self.segs[j] = ShmSegment(obj[0]["path"], ShmLayout(obj[0]["n"], self.W), create=False)
         dist.barrier(group=self.g)
         if self.seg is not None:
             os.unlink(self.seg.path)
+        if self.fallback:                 # every rank saw the same broadcasts: all fall back together
+            self.close()
 
     def ps_take_grads(self, ps, r: int, expect: int) -> torch.Tensor:
         raise RuntimeError("shm transport: gradients never travel on the control plane")
@@ -571,7 +625,7 @@ class ShmTransport:
 
     def pin(self) -> None:
         for s in self.segs.values():
-            s.pin()
+            s.pin(self.wi)
 
     def worker_before_ctrl(self, j: int, kind: int, grads: Optional[torch.Tensor]) -> None:
         # a control word follows on gloo: the PS's native loop must hand over to Python
@@ -644,6 +698,13 @@ def setup_transport(name: str, group, num_ps: int, num_workers: int, ps=None, de
             name = "host"
     tx = make_transport(name, group, num_ps, num_workers)
     tx.ps_setup(ps, ps is not None)
+    if getattr(tx, "fallback", ""):
+        if os.environ.get("MNISTX_PS_STRICT", "0") == "1":
+            raise RuntimeError(f"PS shm transport unavailable: {tx.fallback}")
+        log(f"[ps] shm data plane unavailable ({tx.fallback}): using the host transport")
+        name = "host"
+        tx = make_transport(name, group, num_ps, num_workers)
+        tx.ps_setup(ps, ps is not None)
     if name == "shm" and ps is None and device is not None and torch.device(device).type == "cuda":
         tx.pin()
     return tx
@@ -656,6 +717,7 @@ class ParameterServer:
                  log=print, transport: str = "", group=None, cluster=None):
         self.j, self.k, self.W = ps_index, num_ps, num_workers
         self.device = torch.device(device)
+        transport = transport or default_transport(self.device, max_shard_params(specs, num_ps))
         if transport == "shm":
             self.device = torch.device("cpu")      # the shm PS is a CPU task: the GPUs are the workers'
         self.max_steps = max_steps
@@ -691,7 +753,7 @@ class ParameterServer:
         self.rejected = 0
         self.per_worker = [0] * num_workers
         self.arrivals: List[int] = []            # worker index of every applied push, in order
-        self.tx = setup_transport(transport or default_transport(self.device), group, num_ps, num_workers, ps=self,
+        self.tx = setup_transport(transport, group, num_ps, num_workers, ps=self,
                                   device=self.device, log=log)
         # global-step values at which serve() records a wall-clock mark (bench.py --mode ps)
         self.marks: Dict[int, float] = {}
@@ -734,7 +796,7 @@ class ParameterServer:
             torch.cuda.synchronize(self.device)
         rejoin(self.cluster, gen)
         old_tx = self.tx
-        self.tx = setup_transport(self.transport_name or default_transport(self.device), self.group, self.k,
+        self.tx = setup_transport(self.transport_name, self.group, self.k,
                                   self.W, ps=self, device=self.device, log=self.log)
         if hasattr(old_tx, "close"):
             old_tx.close()
@@ -852,6 +914,11 @@ class PSClient:
         self.log = log
         self.transport_name = transport
         self.recoveries = 0
+        # shm data plane: longest wait for a reply word before the PS counts as lost
+        # (MNISTX_PS_REPLY_TIMEOUT; default the cluster's collective timeout, else 600 s)
+        to = getattr(cluster, "timeout", None) if cluster is not None else None
+        self.reply_timeout_s = float(os.environ.get(
+            "MNISTX_PS_REPLY_TIMEOUT", to.total_seconds() if hasattr(to, "total_seconds") else 600.0))
         self.ranges = shard_ranges(net.fp, num_ps)
         self.global_step = 0
         self.stop = False
@@ -874,7 +941,8 @@ class PSClient:
             if dev.type == "cuda":
                 torch.cuda.synchronize(dev)     # no copy of ours still reads the old mapping
             old.close()
-        self.tx = setup_transport(self.transport_name or default_transport(dev), self.group, self.k, self.W,
+        self.tx = setup_transport(self.transport_name or default_transport(dev, max_shard_params(self.net.fp, self.k)),
+                                  self.group, self.k, self.W,
                                   device=dev)
         self.tx.worker_open(self.wi, self.ranges)
         # one stamped push slot per PS shard: the slice + its int64 sequence stamp, sent as ONE message
@@ -1051,7 +1119,14 @@ class PSClient:
                 if spins & 0x3ff == 0:
                     if not _pid_alive(seg.ps_pid):
                         raise PeerLostError(f"parameter server {j} (pid {seg.ps_pid}) is gone")
-                    time.sleep(0)
+                    # a PS that is alive but stuck (e.g. blocked in a control recv from a
+                    # worker that died between its pending flag and its message): bounded by
+                    # the reply deadline, then recovered like a lost peer
+                    if time.perf_counter() - tw > self.reply_timeout_s:
+                        raise PeerLostError(f"parameter server {j} (pid {seg.ps_pid}) sent no reply within "
+                                            f"{self.reply_timeout_s:.0f} s")
+                    # back off once the reply is clearly not imminent (a PS apply is < 10 ms)
+                    time.sleep(0 if spins < (1 << 16) else 50e-6)
             wait += time.perf_counter() - tw
             if evs is not None and j == 0:
                 evs[0].record()

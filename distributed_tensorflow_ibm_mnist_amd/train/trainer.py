@@ -85,9 +85,15 @@ def train(FLAGS, log=print) -> Dict[str, float]:
     want_gpu = impl == "hip" or (impl == "torch" and torch.cuda.is_available() and not FLAGS.cpu)
     if impl == "hip" and not torch.cuda.is_available():
         raise RuntimeError("--impl=hip needs an MI355X (HIP device); use --impl=torch for the CPU path")
+    # the PS data plane's default depends on the largest PS shard (parallel/ps.default_transport)
+    n_ps = len([h for h in (FLAGS.ps_hosts or "").split(",") if h.strip()])
+    shard_params = 0
+    if n_ps and FLAGS.worker_hosts and not FLAGS.ps_backend:
+        from ..parallel.ps import max_shard_params
+        shard_params = max_shard_params(param_specs(models.get_model(FLAGS.model, FLAGS.in_channels)), n_ps)
     cl = setup_distribute(FLAGS.job_name, FLAGS.ps_hosts, FLAGS.worker_hosts, FLAGS.task_id, want_gpu=want_gpu,
                           timeout_s=FLAGS.collective_timeout, log=log, ps_backend=FLAGS.ps_backend,
-                          dp_backend=FLAGS.dp_backend)
+                          dp_backend=FLAGS.dp_backend, ps_shard_params=shard_params)
     try:
         return _train(FLAGS, cl, max_steps, test_interval, batch_size, impl, log)
     finally:

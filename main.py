@@ -72,7 +72,8 @@ flags.DEFINE_integer("max_to_keep", 5, "checkpoints to keep")
 flags.DEFINE_integer("nan_check_steps", -1, "NaN guard: read the device NaN flag every N steps, asynchronously "
                      "(a NaN at step k raises by step k + N); -1 = --log_step_count_steps (100 when that is 0)")
 flags.DEFINE_integer("eval_examples", 10000, "examples per test-summary evaluation (0: whole split)")
-flags.DEFINE_string("ps_backend", "", "PS-mode data plane: '' (ipc on GPU, host on CPU) | shm (CPU parameter server "
+flags.DEFINE_string("ps_backend", "", "PS-mode data plane: '' (GPU: shm for PS shards up to 1 M parameters, e.g. "
+                    "LeNet-5, ipc above, e.g. the reference CNN; CPU: host) | shm (CPU parameter server "
                     "serving a shared-memory segment natively; one host) | ipc (xGMI peer copies into a GPU PS) | "
                     "host / gloo (staged through host memory)")
 flags.DEFINE_string("dp_backend", "", "DP transport override: '' (RCCL on GPU, gloo on CPU) | gloo (host-staged; "

@@ -548,3 +548,41 @@ def test_is_peer_loss_classification():
     assert not is_peer_loss(RuntimeError("CUDA error: unspecified launch failure (connection to gloo lost?)"))
     assert not is_peer_loss(RuntimeError("socket timeout"))          # no gloo: not ours to recover
     assert not is_peer_loss(PushIntegrityError("gloo connection closed"))
+    # a device string inside a gloo transport error is not a compute error
+    assert is_peer_loss(RuntimeError("Gloo connection closed by peer while sending tensor on cuda:0"))
+    assert not is_peer_loss(RuntimeError("hipErrorIllegalAddress: gloo connection reset"))
+
+
+def test_default_ps_transport_by_shard_size():
+    """GPU ranks: shm (CPU PS) for small shards, ipc (GPU PS) above 1 M parameters per shard;
+    the same answer from the model's specs (PS side) and from a worker's FlatParams."""
+    import torch
+    from distributed_tensorflow_ibm_mnist_amd.models import get_model
+    from distributed_tensorflow_ibm_mnist_amd.parallel.ps import default_transport, max_shard_params
+    from distributed_tensorflow_ibm_mnist_amd.runtime.params import FlatParams
+    from distributed_tensorflow_ibm_mnist_amd.train.trainer import param_specs
+    gpu = torch.device("cuda", 0)
+    lenet = param_specs(get_model("lenet5", 1))
+    ref = param_specs(get_model("reference_cnn", 3))
+    assert max_shard_params(lenet, 1) == 61706
+    assert max_shard_params(ref, 1) == 3464714
+    assert max_shard_params(ref, 2) == max_shard_params(FlatParams.build(ref, {}, "cpu", pads={}), 2)
+    assert default_transport(gpu, max_shard_params(lenet, 1)) == "shm"
+    assert default_transport(gpu, max_shard_params(ref, 1)) == "ipc"
+    assert default_transport(torch.device("cpu"), max_shard_params(ref, 1)) == "host"
+
+
+def test_shm_segment_enospc_is_a_clean_error(monkeypatch, tmp_path):
+    """The shm segment reserves its pages at creation (posix_fallocate): a /dev/shm too small
+    for it is an OSError there -- setup_transport's fallback -- not a SIGBUS at first touch;
+    the half-made file is removed."""
+    import errno
+    from distributed_tensorflow_ibm_mnist_amd.parallel import ps as psm
+
+    def full(fd, off, n):
+        raise OSError(errno.ENOSPC, "No space left on device")
+    monkeypatch.setattr(psm.os, "posix_fallocate", full)
+    path = str(tmp_path / "seg")
+    with pytest.raises(OSError):
+        psm.ShmSegment(path, psm.ShmLayout(1000, 2), create=True)
+    assert not os.path.exists(path)

@@ -30,12 +30,12 @@ def free_port() -> int:
     return p
 
 
-def _launch(tmp_path, transport, num_ps=1, num_workers=2, max_steps=60):
+def _launch(tmp_path, transport, num_ps=1, num_workers=2, max_steps=60, model="lenet5", in_channels=1, batch=256):
     base = free_port()
     ps_hosts = ",".join(f"localhost:{base + i}" for i in range(num_ps))
     wk_hosts = ",".join(f"localhost:{base + 100 + i}" for i in range(num_workers))
     d = str(tmp_path / f"train_{transport}_{num_ps}")
-    common = ["--model=lenet5", "--in_channels=1", "--batch_size=256", f"--max_steps={max_steps}",
+    common = [f"--model={model}", f"--in_channels={in_channels}", f"--batch_size={batch}", f"--max_steps={max_steps}",
               "--test_interval=30", "--log_step_count_steps=0", "--train_data=synthetic://8000",
               "--test_data=synthetic://512?seed=1", "--eval_examples=512", f"--train_dir={d}",
               f"--ps_hosts={ps_hosts}", f"--worker_hosts={wk_hosts}", f"--ps_backend={transport}",
@@ -82,6 +82,23 @@ def test_ps_mode_hip_workers_one_gpu(tmp_path, dev, transport):
     assert p.endswith("model.ckpt-60")
     t = Saver.restore(p)
     assert int(t["global_step"]) == 60 and "fc3/weights/Momentum" in t
+
+
+@pytest.mark.timeout(300)
+def test_ps_mode_reference_cnn_default_transport(tmp_path, dev):
+    """The reference's own model and configuration (3.46 M parameters, 3 input channels,
+    batch 128: /root/reference/main.py:80-82, mnist_input.py:13-15,261-264) through the
+    DEFAULT data plane, which for a shard this size is the GPU PS of ipc
+    (parallel/ps.default_transport): every update applied, both workers contributing."""
+    d, logs = _launch(tmp_path, "", max_steps=40, model="reference_cnn", in_channels=3, batch=128)
+    assert "transport ipc" in logs["ps0"], logs["ps0"][-2000:]
+    m = re.search(r"applied (\d+) update\(s\), per worker \[(\d+), (\d+)\]", logs["ps0"])
+    assert m, logs["ps0"][-2000:]
+    assert int(m.group(1)) == 40 and min(int(m.group(2)), int(m.group(3))) > 0
+    assert "result: global_step=40" in logs["worker0"]
+    from distributed_tensorflow_ibm_mnist_amd.ckpt.saver import Saver, latest_checkpoint
+    t = Saver.restore(latest_checkpoint(d))
+    assert int(t["global_step"]) == 40 and t["local3/weights"].shape == (3136, 1024)
 
 
 @pytest.mark.timeout(300)

@@ -7,7 +7,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run_one(p1: bool, B: int, iters: int = 50):
+def run_one(p1: int, B: int, iters: int = 50):
+    """p1: 0 = pool1 stays in LDS, 1 = pool1 + codes (convpool layouts), 2 = the combined
+    16-byte records the training step writes (lenet_bwd_k reads them)."""
     import torch
     from distributed_tensorflow_ibm_mnist_amd.ops._ext import kernels
     K = kernels()
@@ -24,7 +26,7 @@ def run_one(p1: bool, B: int, iters: int = 50):
     A1 = torch.empty(B, 14, 14, 4, dtype=torch.uint8, device=dev)
     P2 = torch.empty(B, 5, 5, 16, dtype=torch.bfloat16, device=dev)
     A2 = torch.empty(B, 5, 5, 16, dtype=torch.uint8, device=dev)
-    kw = dict(p1=P1, arg1=A1) if p1 else {}
+    kw = dict(p1=P1, arg1=A1) if p1 == 1 else dict(p1=P1) if p1 == 2 else {}
     f = lambda: K.lenet_band_fwd(ds, w1, b1, 6, w2, b2, B, P2, A2, idx=idx, **kw)
     for _ in range(10):
         f()
@@ -48,7 +50,7 @@ def run_one(p1: bool, B: int, iters: int = 50):
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "one":
-        print(json.dumps({"us": run_one(sys.argv[2] == "1", int(sys.argv[3]))}))
+        print(json.dumps({"us": run_one(int(sys.argv[2]), int(sys.argv[3]))}))
         sys.exit(0)
     B = int(os.environ.get("B", "65536"))
     for p1 in (1, 0):

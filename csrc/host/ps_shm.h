@@ -19,7 +19,8 @@
 // (HELLO / STATE / DONE / RESET) still travel on the gloo group: a worker raises its
 // pending flag first, and the loop returns to Python to receive it.
 //
-// Segment layout (bytes; mirrored by parallel/ps.py ShmLayout): a 256-byte header, then
+// Segment layout (bytes; mirrored by parallel/ps.py ShmLayout): a 4096-byte header page (so every
+// worker block starts on a page: a worker pins -- hipHostRegister -- only its own block), then
 // one block per worker at wblock stride: control words int64[16] at ctrl_off, the push
 // slot (slot_floats floats, the last 8 bytes = the stamp) at push_off, the reply
 // parameters at reply_off.
@@ -35,6 +36,7 @@
 
 namespace mnistx_host {
 
+constexpr int64_t kPsHdr = 4096;   // header page (ShmLayout.HDR)
 enum PsCtrl { C_PUSH_SEQ = 0, C_PENDING = 1, C_REPLY_SEQ = 2, C_REPLY_GSTEP = 3, C_REPLY_STOP = 4, C_REPLY_APPLIED = 5 };
 enum PsServeRc { PS_CTRL = 0, PS_BAD_STAMP = 1, PS_KILL = 2, PS_IDLE_TIMEOUT = 3 };
 
@@ -158,7 +160,7 @@ inline void ps_apply(float* __restrict__ p, const float* __restrict__ g, float* 
 }
 
 inline volatile int64_t* ps_ctrl(uint8_t* base, const PsLayout& L, int64_t w) {
-  return (volatile int64_t*)(base + 256 + w * L.wblock + L.ctrl_off);
+  return (volatile int64_t*)(base + kPsHdr + w * L.wblock + L.ctrl_off);
 }
 
 // Serve pushes until a worker raises its control flag (PS_CTRL), a push carries a stamp
@@ -209,7 +211,7 @@ inline int ps_serve(uint8_t* base, const PsLayout& L, float* params, float* mom,
     const int w = found;
     S.last = w;
     S.last_seq[w] = seq;
-    uint8_t* blk = base + 256 + (int64_t)w * L.wblock;
+    uint8_t* blk = base + kPsHdr + (int64_t)w * L.wblock;
     const float* g = (const float*)(blk + L.push_off);
     int64_t stamp;
     memcpy(&stamp, (const uint8_t*)g + L.slot_floats * 4 - 8, 8);

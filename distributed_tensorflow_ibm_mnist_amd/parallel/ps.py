@@ -391,10 +391,10 @@ def _align(v: int, a: int) -> int:
 
 
 class ShmLayout:
-    """Byte layout of one PS shard's segment (mirrored by csrc/host/ps_shm.h): a 256-byte
-    header (int64: magic, n, W, PS pid, generation), then per worker: control words
+    """Byte layout of one PS shard's segment (mirrored by csrc/host/ps_shm.h): a 4096-byte
+    header page (int64: magic, n, W, PS pid, generation), then per worker (page-aligned blocks): control words
     int64[16], the stamped push slot, the reply parameters, the optimizer-state reply."""
-    HDR, MAGIC = 256, 0x6D6E69737870735F
+    HDR, MAGIC = 4096, 0x6D6E69737870735F     # a header PAGE: every worker block is page-aligned
 
     def __init__(self, n: int, W: int):
         self.n, self.W = n, W
@@ -622,6 +622,8 @@ class ShmTransport:
     # -- worker side
     def worker_open(self, w_index: int, ranges) -> None:
         self.wi = w_index
+        if getattr(self, "want_pin", False):
+            self.pin()
 
     def pin(self) -> None:
         for s in self.segs.values():
@@ -706,7 +708,7 @@ def setup_transport(name: str, group, num_ps: int, num_workers: int, ps=None, de
         tx = make_transport(name, group, num_ps, num_workers)
         tx.ps_setup(ps, ps is not None)
     if name == "shm" and ps is None and device is not None and torch.device(device).type == "cuda":
-        tx.pin()
+        tx.want_pin = True        # pinned at worker_open, once the worker's block is known
     return tx
 
 

@@ -586,3 +586,20 @@ def test_shm_segment_enospc_is_a_clean_error(monkeypatch, tmp_path):
     with pytest.raises(OSError):
         psm.ShmSegment(path, psm.ShmLayout(1000, 2), create=True)
     assert not os.path.exists(path)
+
+
+def test_shm_worker_pins_only_its_own_page_aligned_block(monkeypatch, tmp_path):
+    """A GPU worker of the shm data plane registers (hipHostRegister) only its own block, once
+    its worker index is known (worker_open), and that block starts on a page boundary."""
+    from distributed_tensorflow_ibm_mnist_amd.parallel import ps as psm
+    lay = psm.ShmLayout(1000, 3)
+    assert lay.HDR % 4096 == 0 and lay.wblock % 4096 == 0
+    seg = psm.ShmSegment(str(tmp_path / "seg"), lay, create=True)
+    calls = []
+    monkeypatch.setattr(psm.ShmSegment, "pin", lambda self, worker=None: calls.append(worker) or True)
+    tx = psm.ShmTransport(None, 1, 3)
+    tx.segs = {0: seg}
+    tx.want_pin = True
+    tx.worker_open(2, None)
+    assert calls == [2]
+    seg.close()

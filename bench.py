@@ -266,8 +266,8 @@ def run_ps(args) -> int:
     else:
         from distributed_tensorflow_ibm_mnist_amd.runtime.executor import HipNet
         net = HipNet(spec, args.batch, dev, init, opt)
-        imgs, labs = make_synthetic(args.dataset_size, seed=args.seed, channels=1, device=dev)
-        loader = DeviceLoader(DeviceDataset(imgs, labs, dev, hw=784, channels=1), net.x0, net.labels,
+        imgs, labs = make_synthetic(args.dataset_size, seed=args.seed, channels=args.in_channels, device=dev)
+        loader = DeviceLoader(DeviceDataset(imgs, labs, dev, hw=784, channels=args.in_channels), net.x0, net.labels,
                               rank=0, world=1, seed=args.seed + 7919 * rank, shard=False)
         client = PSClient(net, 1, nw, rank - 1, transport=args.ps_transport)
         client.hello()
@@ -356,8 +356,10 @@ def main() -> int:
     dp = DataParallel(net, bucket_cap_mb=args.bucket_mb, force_collectives=bool(args.force_collectives))
     dp.broadcast_state()
 
-    imgs, labs = make_synthetic(args.dataset_size, seed=args.seed, channels=1, device=dev)
-    ds = DeviceDataset(imgs, labs, dev, hw=784, channels=1)
+    # --in_channels 3: 3-channel records (the glyphs replicated to RGB, as the reference's DLI
+    # import stored MNIST: /root/reference/mnist_input.py:13-15), gathered by the first conv
+    imgs, labs = make_synthetic(args.dataset_size, seed=args.seed, channels=args.in_channels, device=dev)
+    ds = DeviceDataset(imgs, labs, dev, hw=784, channels=args.in_channels)
     # --input u8 / bf16: the first fused conv gathers the resident dataset through the
     # batch index (K10 fused into its staging); prep: one gather+normalise kernel per step
     mode = "u8" if args.fused_input else args.input
@@ -488,7 +490,7 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.precision if args.impl == "hip" else "bf16",
-            "data": "synthetic 28x28x1 (on-device generated MNIST-like glyphs), random-init weights",
+            "data": f"synthetic 28x28x{args.in_channels} (on-device generated MNIST-like glyphs), random-init weights",
             "config": {
                 "model": MODEL_LABEL[args.model],
                 "global_batch": global_batch,

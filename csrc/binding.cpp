@@ -711,7 +711,7 @@ mnistx::XSrc cp_src(const Tensor& x, const optional<Tensor>& u8, const optional<
                     int64_t hwc) {
   mnistx::XSrc src{nullptr, nullptr, nullptr, 0};
   if (u8.has_value() && u8->defined()) {
-    TORCH_CHECK(mnistx::convpool_u8_input(cfg), "convpool: uint8 input only for 1-channel first layers");
+    TORCH_CHECK(mnistx::convpool_u8_input(cfg), "convpool: uint8 input only for first layers (Cin 1, or 3 at 28x28)");
     TORCH_CHECK(idx.has_value() && idx->defined(), "convpool: uint8 input needs idx");
     check(*u8, at::kByte, hwc, "u8");
     TORCH_CHECK(u8->numel() % hwc == 0 && u8->numel() < (int64_t)INT32_MAX,
@@ -723,7 +723,7 @@ mnistx::XSrc cp_src(const Tensor& x, const optional<Tensor>& u8, const optional<
     src.n = (int)(u8->numel() / hwc);       // the kernel clamps every index into [0, n)
   } else if (idx.has_value() && idx->defined()) {
     // x is the resident bf16 dataset [n, H*W*C] (normalised once), gathered through idx
-    TORCH_CHECK(mnistx::convpool_u8_input(cfg), "convpool: dataset input only for 1-channel first layers");
+    TORCH_CHECK(mnistx::convpool_u8_input(cfg), "convpool: dataset input only for first layers (Cin 1, or 3 at 28x28)");
     check(x, at::kBFloat16, hwc, "x (dataset)");
     TORCH_CHECK(x.numel() % hwc == 0 && x.numel() * 2 < (int64_t)INT32_MAX,
                 "x (dataset): [n, H*W*C] bf16 images, < 2 GB (one buffer resource)");
@@ -917,8 +917,8 @@ void refc1_wgrad(Tensor x, Tensor dn, Tensor p1, Tensor arg, Tensor slab, int64_
   const int cfg = mnistx::convpool_config((int)cin, 32, 5, 2, 28, 28);
   TORCH_CHECK(cfg >= 0, "refc1_wgrad: no RefC1 geometry");
   TORCH_CHECK(B >= 1 && B * 784 * cin * 2 < (int64_t)INT32_MAX, "B: the batch (and its index) must stay < 2 GB");
-  TORCH_CHECK(cin == 1 || (!(u8.has_value() && u8->defined()) && !(idx.has_value() && idx->defined())),
-              "refc1_wgrad: 3 channels read the bf16 batch only");
+  TORCH_CHECK(cin == 1 || !(u8.has_value() && u8->defined()),
+              "refc1_wgrad: 3 channels read bf16 (the batch, or the dataset through idx) only");
   const auto src = cp_src(x, u8, idx, cfg, B, 784 * cin);
   if (src.x) TORCH_CHECK(reinterpret_cast<uintptr_t>(src.x) % 8 == 0, "x must be 8-byte aligned");
   const int64_t np = B * 196 * 32;

@@ -213,7 +213,9 @@ struct XStage {
   static constexpr int NV = IMGS * G::H * G::ROWV;
   static constexpr int VPI = G::H * G::ROWV;   // vectors per image
   static constexpr int NWV = NTH / 64;
-  static constexpr bool U8 = G::CIN == 1;      // dataset gathers only for 1-channel first layers
+  // dataset gathers (first layers only): 1-channel images, and the reference CNN's
+  // 3-channel 28x28 records (mnist_input.py:13-15: NHWC rows, the layout of the batch x0)
+  static constexpr bool U8 = G::CIN == 1 || (G::CIN == 3 && G::H == 28 && G::W == 28);
   // First-layer geometries: whole waves load one image (WPI waves per image), so the
   // image -- and, for dataset gathers, its row -- is wave-uniform: one index load per
   // wave per group and no per-vector row select (the select + 64-bit clamp cost
@@ -1762,7 +1764,9 @@ int convpool_arg_bytes(int cfg) {
   }
 }
 
-int convpool_u8_input(int cfg) { return (cfg == 0 || cfg == 2) ? 1 : 0; }  // Cin == 1 first layers
+// first layers that gather a resident dataset: Cin == 1 (LeNet / reference conv1) and the
+// reference conv1 on 3-channel records
+int convpool_u8_input(int cfg) { return (cfg == 0 || cfg == 2 || cfg == 3) ? 1 : 0; }
 
 hipError_t convpool_dgrad(int cfg, const bf16_t* dP, const uint8_t* arg, const bf16_t* w, int B, bf16_t* dx,
                           int grid_cap, hipStream_t st) {

@@ -132,8 +132,14 @@ struct Stage {
       off = ((uint32_t)(ok ? t0 + img : 0) * 196u + (uint32_t)q) * 4u * esz;
     }
     const auto rx = buf_rsrc(base, 0x7fffffffu);
-    if constexpr (CIN == 3) {   // bf16 NHWC batch only (the executor's x0): 24 bytes per quad
-      off = ok ? ((uint32_t)(t0 + img) * 196u + (uint32_t)q) * 24u : BUF_OOB;
+    if constexpr (CIN == 3) {   // bf16 NHWC: the batch (x0) or, IDX, the dataset rows; 24 bytes per quad
+      if constexpr (IDX) {
+        const uint32_t lo = rowv[0], hi = rowv[1];
+        const int row = (hi != 0u || (int)lo < 0) ? 0 : ((int)lo >= g.n ? g.n - 1 : (int)lo);
+        off = ok ? ((uint32_t)row * 196u + (uint32_t)q) * 24u : BUF_OOB;
+      } else {
+        off = ok ? ((uint32_t)(t0 + img) * 196u + (uint32_t)q) * 24u : BUF_OOB;
+      }
 #pragma unroll
       for (int c = 0; c < 3; ++c) x[c] = buf_b64(rx, off + 8u * c);
       return;
@@ -340,7 +346,8 @@ __global__ __launch_bounds__(NT, 1) void refc1_wgrad_k(const Args g) {
 using Kern = void (*)(Args);
 constexpr Kern kRefc1[4] = {refc1_wgrad_k<false, false>, refc1_wgrad_k<false, true>, refc1_wgrad_k<true, false>,
                             refc1_wgrad_k<true, true>};
-constexpr Kern kRefc1x3 = refc1_wgrad_k<false, false, 3>;   // bf16 NHWC batch (x0) only
+// 3 channels: bf16 NHWC, the batch (x0) or the resident dataset through the batch index
+constexpr Kern kRefc1x3[2] = {refc1_wgrad_k<false, false, 3>, refc1_wgrad_k<false, true, 3>};
 
 int g_skip = 0;
 
@@ -356,11 +363,12 @@ int refc1_wgrad_grid(int* per_cu = nullptr) {
       if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, Lay<1>::LDS_BYTES) !=
           hipSuccess)
         return -1;
-    if (hipFuncSetAttribute((const void*)kRefc1x3, hipFuncAttributeMaxDynamicSharedMemorySize, Lay<3>::LDS_BYTES) !=
+    for (Kern k : kRefc1x3)
+      if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, Lay<3>::LDS_BYTES) !=
         hipSuccess)
       return -1;
     // both channel counts hold one block per CU (LDS); the grid is the same
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kRefc1x3, NT, Lay<3>::LDS_BYTES) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kRefc1x3[0], NT, Lay<3>::LDS_BYTES) != hipSuccess ||
         hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per <= 0)
       return -1;
@@ -384,9 +392,9 @@ hipError_t refc1_wgrad(const XSrc& x, const bf16_t* dn, const bf16_t* p1, const 
   if (B <= 0) return hipSuccess;
   if ((!x.x && !x.u8) || grid <= 0 || refc1_wgrad_grid() <= 0) return hipErrorInvalidValue;
   if (beta != 0.75f) return hipErrorInvalidValue;   // the lrn_bwd8 fast path (the reference's beta)
-  if (cin != 1 && !(cin == 3 && x.x && !x.idx)) return hipErrorInvalidValue;
+  if (cin != 1 && !(cin == 3 && x.x && !x.u8)) return hipErrorInvalidValue;
   Args a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, dn, p1, arg, B, bias, alpha, beta, slab, g_skip};
-  const Kern k = cin == 3 ? kRefc1x3 : kRefc1[(x.u8 ? 2 : 0) + (x.idx ? 1 : 0)];
+  const Kern k = cin == 3 ? kRefc1x3[x.idx ? 1 : 0] : kRefc1[(x.u8 ? 2 : 0) + (x.idx ? 1 : 0)];
   void* args[] = {&a};
   return hipLaunchKernel((const void*)k, dim3(grid), dim3(NT), args, cin == 3 ? Lay<3>::LDS_BYTES : Lay<1>::LDS_BYTES,
                          st);

@@ -1246,6 +1246,24 @@ class PSWorkerReplica:
         sw = os.environ.get("MNIST_FI_SLOW_WORKER", "")
         self._sleep = float(sw.split(":")[1]) if ":" in sw and int(sw.split(":")[0]) == worker_index else 0.0
         self.client.hello()
+        self._cluster, self._nw = cluster, num_workers
+        self._started = False
+
+    def _start_barrier(self) -> None:
+        """MNISTX_PS_START_BARRIER=1: before its FIRST push (its first step computed, graphs
+        captured) every worker waits on the cluster store until all have got there -- for runs
+        that must see every worker contribute (tests); async PS semantics are unchanged after
+        the start.  Without it a worker whose start-up is slower (the chief's graph capture and
+        initial checkpoint) can find a short job already finished, as TF's workers can."""
+        self._started = True
+        cl = self._cluster
+        if os.environ.get("MNISTX_PS_START_BARRIER", "0") != "1" or cl is None or cl.store is None:
+            return
+        key = f"mnistx/started/gen{cl.gen}"
+        cl.store.add(key, 1)
+        t_end = time.time() + 300
+        while int(cl.store.add(key, 0)) < self._nw and time.time() < t_end:
+            time.sleep(0.005)
 
     @property
     def global_step(self) -> int:
@@ -1277,6 +1295,8 @@ class PSWorkerReplica:
             self._compute()
         if self._sleep:
             time.sleep(self._sleep)
+        if not self._started:
+            self._start_barrier()
         self.client.push_pull()
 
     @property

@@ -197,8 +197,9 @@ class ConvPoolLayer(_Layer):
     def _refc1(self, ls) -> bool:
         """The reference CNN's conv1 (28x28x1 or x3 -> 32, SAME) under norm1 (radius 4, beta
         0.75): refc1_wgrad replaces the folded convpool_wgrad (MNISTX_REFC1_WGRAD=0 keeps the
-        latter).  3 channels (the reference's DLI records): the bf16 batch input only."""
-        if self.C == 3 and self._src():
+        latter).  3 channels (the reference's DLI records): bf16 input only (the batch, or the
+        resident dataset through the batch index)."""
+        if self.C == 3 and "u8" in self._src():
             return False
         return (self.C in (1, 3) and self.Cp == 32 and self.spec.cout == 32 and self.pad == 2
                 and self.H == self.W == 28 and ls.depth_radius == 4 and float(ls.beta) == 0.75
@@ -618,7 +619,7 @@ class HipNet:
         """Whether ``bind_u8_input`` would accept a resident dataset (checked BEFORE the
         caller builds a normalised bf16 copy of it)."""
         first = self.layers[0]
-        return (isinstance(first, ConvPoolLayer) and self.spec.in_channels == 1
+        return (isinstance(first, ConvPoolLayer) and self.spec.in_channels in (1, 3)
                 and bool(kernels().convpool_u8_input(*first._geo())))
 
     def bind_u8_input(self, images: torch.Tensor, bwd_images: Optional[torch.Tensor] = None) -> bool:
@@ -636,9 +637,12 @@ class HipNet:
         in-kernel normalisation is bitwise the bf16 copy's, tests/test_lenet_bwd_gpu.py)."""
         first = self.layers[0]
         H, W = self.spec.input_hw
-        if not (isinstance(first, ConvPoolLayer) and self.spec.in_channels == 1
-                and images.dtype in (torch.uint8, torch.bfloat16) and images.dim() == 2
-                and images.shape[1] == H * W and images.device == self.device
+        C = self.spec.in_channels
+        # 3 channels (the reference CNN on its 3-channel records): the bf16 dataset only -- the
+        # conv1 weight gradient (refc1_wgrad) gathers bf16 NHWC rows
+        if not (isinstance(first, ConvPoolLayer) and C in (1, 3)
+                and images.dtype in ((torch.uint8, torch.bfloat16) if C == 1 else (torch.bfloat16,))
+                and images.dim() == 2 and images.shape[1] == H * W * C and images.device == self.device
                 and kernels().convpool_u8_input(*first._geo())):
             return False
         self.idx_buf = torch.zeros(self.B, dtype=torch.int64, device=self.device)
@@ -733,6 +737,9 @@ class HipNet:
         # fused head: its three weight gradients run as ONE grouped split-K launch
         self._group_S = None
         if self.group_head_wgrad and self._head_grads and self.defer_reduce and not self.overlap:
+            # before the fused conv backward: launched after it instead (the conv backward then
+            # reads the band forward's pool1 records with ~110 MB less traffic in between) the
+            # step measured 11 us SLOWER same-box (profiles/r6/order/)
             hl = self.layers[self.head:]
             dys = [self.dbuf[self.head + 1], self.dbuf[self.head + 2], self.dlogits]
             self._group_S = kernels().dense_wgrad_group(

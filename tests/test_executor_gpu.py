@@ -162,7 +162,7 @@ def test_graph_replay_matches_eager(dev, K):
 
 
 @pytest.mark.parametrize("mode", ["u8", "bf16", "bf16_u8bwd"])
-@pytest.mark.parametrize("model", ["lenet5", "reference_cnn"])
+@pytest.mark.parametrize("model", ["lenet5", "reference_cnn", "reference_cnn3"])
 def test_u8_input_path_bitwise_equal(dev, K, model, mode):
     """First fused conv gathering the resident dataset through the batch index (fused
     K10) -- uint8 normalised in the kernels, or bf16 normalised once (bf16_u8bwd: with
@@ -171,11 +171,16 @@ def test_u8_input_path_bitwise_equal(dev, K, model, mode):
     Feistel index+label launch must equal the prep's."""
     from distributed_tensorflow_ibm_mnist_amd.data.synthetic import make_synthetic
     from distributed_tensorflow_ibm_mnist_amd.data.device_loader import DeviceDataset, DeviceLoader
-    spec = get_model(model, 1)
+    # reference_cnn3: the reference's own 3-channel records (mnist_input.py:13-15), gathered by
+    # conv1's forward (convpool) and weight gradient (refc1_wgrad) from the bf16 dataset
+    cin = 3 if model == "reference_cnn3" else 1
+    if cin == 3 and mode != "bf16":
+        pytest.skip("3-channel records: the bf16 dataset only")
+    spec = get_model(model.rstrip("3"), cin)
     init = torch_ref.init_params(spec, seed=3)
     opt = OptConfig(lr0=0.05, use_momentum=True, momentum=0.9, ema_max=0.9999)
-    imgs, labs = make_synthetic(3000, seed=4, device=dev)
-    ds = DeviceDataset(imgs, labs, dev)
+    imgs, labs = make_synthetic(3000, seed=4, device=dev, channels=cin)
+    ds = DeviceDataset(imgs, labs, dev, channels=cin)
     a = HipNet(spec, 200, dev, init, opt)
     b = HipNet(spec, 200, dev, init, opt)
     assert b.bind_u8_input(ds.images if mode == "u8" else ds.bf16_images(),
@@ -308,3 +313,4 @@ def test_refcnn_lrn1_backward_fold(dev, K, cin, monkeypatch):
             assert rel_err(fold[n], ref[n]) < 1e-5, n
         else:
             assert torch.equal(fold[n], ref[n]), n
+

@@ -40,7 +40,8 @@ def _launch(tmp_path, transport, num_ps=1, num_workers=2, max_steps=60, model="l
               "--test_data=synthetic://512?seed=1", "--eval_examples=512", f"--train_dir={d}",
               f"--ps_hosts={ps_hosts}", f"--worker_hosts={wk_hosts}", f"--ps_backend={transport}",
               "--optimizer=momentum", "--base_lr=0.02"]
-    env = dict(os.environ, PYTHONUNBUFFERED="1", OMP_NUM_THREADS="2")
+    # every worker starts pushing only once all have said HELLO (the per-worker counts below)
+    env = dict(os.environ, PYTHONUNBUFFERED="1", OMP_NUM_THREADS="2", MNISTX_PS_START_BARRIER="1")
     procs = []
     for job, n in (("ps", num_ps), ("worker", num_workers)):
         for i in range(n):

@@ -741,13 +741,24 @@ mnistx::XSrc cp_src(const Tensor& x, const optional<Tensor>& u8, const optional<
 
 void convpool_fwd(Tensor x, Tensor w, Tensor bias, int64_t bias_n, Tensor pooled, Tensor arg, int64_t B, int64_t cin,
                   int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t wd, optional<Tensor> u8,
-                  optional<Tensor> idx) {
+                  optional<Tensor> idx, optional<Tensor> lrn_out, double lrn_bias, double lrn_alpha,
+                  double lrn_beta, int64_t lrn_r) {
   auto g = cp_geo(cin, cout, ks, pad, h, wd);
   const auto src = cp_src(x, u8, idx, g.cfg, B, h * wd * cin);
   check(w, at::kBFloat16, ks * ks * cin * cout, "w");
   check(bias, at::kFloat, bias_n, "bias");
   check(pooled, at::kBFloat16, B * g.PH * g.PW * cout, "pooled");
   check(arg, at::kByte, B * g.PH * g.PW * mnistx::convpool_arg_bytes(g.cfg), "arg");
+  if (lrn_out.has_value() && lrn_out->defined()) {
+    // the following LRN (radius 4) written by the same launch (refc1n_fwd_k): reference conv1 only
+    TORCH_CHECK(g.cfg == 2 && lrn_r == 4 && mnistx::refc1_fwd_lrn_ok(),
+                "convpool_fwd: lrn_out only for the reference conv1 (1 -> 32, SAME) with norm1 radius 4");
+    check(*lrn_out, at::kBFloat16, B * g.PH * g.PW * cout, "lrn_out");
+    hip_ok(mnistx::refc1_band_fwd(src, BF(w), P<const float>(bias), (int)bias_n, (int)B, BFm(pooled), P<uint8_t>(arg),
+                                  cur_stream(), BFm(*lrn_out), (float)lrn_bias, (float)lrn_alpha, (float)lrn_beta),
+           "convpool_fwd (+ norm1)");
+    return;
+  }
   hip_ok(mnistx::convpool_fwd(g.cfg, src, BF(w), P<const float>(bias), (int)bias_n, (int)B, BFm(pooled),
                               P<uint8_t>(arg), cur_stream()),
          "convpool_fwd");
@@ -1320,7 +1331,12 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("convpool_reduce_args", &convpool_reduce_args);
   m.def("convpool_fwd", &convpool_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("bias_n"),
         py::arg("pooled"), py::arg("arg"), py::arg("B"), py::arg("cin"), py::arg("cout"), py::arg("ks"),
-        py::arg("pad"), py::arg("h"), py::arg("w_"), py::arg("u8") = py::none(), py::arg("idx") = py::none());
+        py::arg("pad"), py::arg("h"), py::arg("w_"), py::arg("u8") = py::none(), py::arg("idx") = py::none(),
+        py::arg("lrn_out") = py::none(), py::arg("lrn_bias") = 0.0, py::arg("lrn_alpha") = 0.0,
+        py::arg("lrn_beta") = 0.0, py::arg("lrn_r") = 0);
+  m.def("convpool_fwd_lrn_ok", [](int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t w) {
+    return cp_geo(cin, cout, ks, pad, h, w).cfg == 2 && mnistx::refc1_fwd_lrn_ok();
+  });
   m.def("convpool_wgrad", &convpool_wgrad, py::arg("x"), py::arg("dP"), py::arg("arg"), py::arg("slab"),
         py::arg("grid"), py::arg("B"), py::arg("cin"), py::arg("cout"), py::arg("ks"), py::arg("pad"), py::arg("h"),
         py::arg("w_"), py::arg("u8") = py::none(), py::arg("idx") = py::none(), py::arg("lrn_p") = py::none(),
@@ -1347,6 +1363,7 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("grid"), py::arg("B"), py::arg("lrn_bias"), py::arg("lrn_alpha"), py::arg("lrn_beta"),
         py::arg("u8") = py::none(), py::arg("idx") = py::none(), py::arg("cin") = 1);
   m.def("refc1_set_skip", [](int64_t s) { mnistx::refc1_set_skip((int)s); });
+  m.def("refc1_set_fwd_variant", [](int64_t v) { mnistx::refc1_set_fwd_variant((int)v); });
   m.def("refc1_wgrad_blocks", [](int64_t B) {
     const int n = mnistx::refc1_wgrad_blocks((int)B);
     TORCH_CHECK(n > 0, "refc1_wgrad_blocks: occupancy query failed");

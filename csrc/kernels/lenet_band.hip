@@ -38,6 +38,7 @@
 // uses the same ops).
 #include "common.h"
 #include "launchers.h"
+#include "lrn_math.h"
 
 #include <cstdlib>
 
@@ -591,6 +592,189 @@ __global__ __launch_bounds__(RNTH) void refc1_band_fwd_k(const BandFwd a) {
   }
 }
 
+// ---------------------------------------------------------------------------- + norm1 in the epilogue
+// The same conv1 + pool1 with ALL 32 channels of a unit in one wave (4 channel groups x 3
+// k-steps = 12 MFMAs per unit, units w + 4 j), so the pooled pixel's 32 channels sit in the lane
+// pair (l, l + 32): lane half h holds channels 8 q + 4 h + i of groups q = 0..3.  Two
+// v_permlane32_swap per 4-channel block pair -- swap(P[k], P[k + 2]) -- turn that into
+// channels 16 h .. 16 h + 15 per lane (the swap IS the transpose: no selects), so a lane
+// stores 32 contiguous bytes of pool1, 16 of codes and 32 of norm1, and the norm1 LRN
+// (mnist_input.py:152-153, radius 4) of its two 8-channel vectors needs no other data: the
+// 4-channel neighbours are blocks the lane already holds.  The LRN arithmetic replays
+// lrn_fwd8 (same squares of the bf16 pool1 values, same running window sum, same
+// lrn_out), so norm1 is bitwise lrn_fwd_k's; pool1 and the codes are bitwise
+// refc1_band_fwd_k's (same pooling expressions).  Replaces refc1_band_fwd_k + lrn_fwd_k:
+// norm1 is computed from registers instead of a second 205 MB pool1 pass at B = 16384.
+struct RefC1Lrn {
+  bf16_t* norm;           // [B][196][32] norm1 (null: not written)
+  float bias, alpha, beta;
+};
+
+template <bool LRN>
+__global__ __launch_bounds__(RNTH, 2) void refc1n_fwd_k(const BandFwd a, const RefC1Lrn l) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[R_LDS];
+  bf16_t* xs = lds;
+  bf16_t* ws = lds + LDS_X;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 31, h = lane >> 5, img = (col >> 1) & 7, half = col >> 4, xq = col & 1;
+  const int ntiles = (a.B + BT - 1) / BT;
+  const int nk = ntiles > (int)blockIdx.x ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  auto tile0 = [&](int k) { return ((int)blockIdx.x + k * (int)gridDim.x) * BT; };
+  for (int e = tid; e < RW_E / 8; e += RNTH) *(u32x4*)(ws + 8 * e) = *(const u32x4*)(a.w1 + 8 * e);
+  if (tid == 0) *(u32x4*)(ws + RW_E) = u32x4{0u, 0u, 0u, 0u};
+  for (int e = tid; e < LDS_X / 8; e += RNTH) *(u32x4*)(xs + 8 * e) = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  bf16x8 af[4][3];
+  {
+    const int g = col >> 3, ypr = g >> 1, xpr = g & 1, c8 = col & 7;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int dy = 2 * p + h - ypr, dx = j - xpr, c = 8 * q + c8;
+          const bool ok = dy >= 0 && dy <= 4 && dx >= 0 && dx <= 4;
+          af[q][p][j] = __builtin_bit_cast(__bf16, ws[ok ? (dy * 5 + dx) * 32 + c : RW_E]);
+        }
+  }
+  float bias[4][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = 8 * q + 4 * h + i;
+      bias[q][i] = c < a.b1n ? a.b1[c] : 0.f;
+    }
+  const auto rx = a.u8 ? buf_rsrc(a.u8, (uint32_t)a.n * XIMG) : buf_rsrc(a.x, (uint32_t)a.n * (XIMG * 2));
+  const int xlane = img * XIS + h * XPL + (7 * half - 1) * XRW + 2 * xq;
+  const bool top = half == 0, bot = half == 1;
+  XFill xf;
+  xf.init(tid);
+  xf.load(rx, a, nk > 0 ? tile0(0) : -1, tid);
+  xf.store_pre(xs, tid, a.u8 != nullptr);
+  const int nu = (U1 - wave + 3) / 4;          // units wave + 4 j: 13, 12, 12, 12
+  for (int k = 0; k < nk; ++k) {
+    __syncthreads();                           // input[k % 2] landed; input[(k + 1) % 2] free
+    const bf16_t* xb = xs + (k & 1) * XBUF + xlane;
+    const int t0 = tile0(k), gi = t0 + img;
+    xf.load(rx, a, k + 1 < nk ? tile0(k + 1) : -1, tid);
+    struct Frags { bf16x8 b[3]; };
+    auto fetch = [&](int j) {
+      const int f = min(wave + 4 * j, U1 - 1), yp0 = f / 7, u = f - 7 * yp0;
+      const bf16_t* base = xb + yp0 * XRW + 4 * u;
+      Frags fr;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const bf16_t* rp = base + p * XRW;
+        if (p == 0 && yp0 == 0) rp = top ? xs + XZERO : rp;
+        if (p == 2 && yp0 == 6) rp = bot ? xs + XZERO : rp;
+        const uint32_t* qq = (const uint32_t*)rp;
+        fr.b[p] = as_frag(u32x4{qq[0], qq[1], qq[2], qq[3]});
+      }
+      return fr;
+    };
+    Frags fa = fetch(0);
+#pragma unroll 1
+    for (int j = 0; j < nu; ++j) {
+      const Frags fb = fetch(j + 1 < nu ? j + 1 : j);
+      uint32_t P[4][2], CW[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f32x16 acc = {};
+#pragma unroll
+        for (int p = 0; p < 3; ++p) acc = mfma32(af[q][p], fa.b[p], acc);
+        // pool / bias / ReLU / code: refc1_band_fwd_k's expressions (bitwise the same pool1)
+        float o[4];
+        uint32_t cw = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v = vmax(vmax3(__uint_as_float(__float_as_uint(acc[i]) & ~3u), embed(acc[4 + i], 1u),
+                                     embed(acc[8 + i], 2u)), embed(acc[12 + i], 3u));
+          o[i] = vmax(__uint_as_float(__float_as_uint(v) & ~3u) + bias[q][i], 0.f);
+          cw |= (o[i] > 0.f ? (__float_as_uint(v) & 3u) : ARG_OFF) << (8 * i);
+        }
+        P[q][0] = pk2(o[0], o[1]);
+        P[q][1] = pk2(o[2], o[3]);
+        CW[q] = cw;
+      }
+      fa = fb;
+      // lane half h: 4-channel blocks Bk = channels 16 h + 4 k .. + 3 (swap(P[k], P[k + 2]): lanes
+      // of h = 0 keep P[k] in the first result and receive the partner's P[k] in the second;
+      // lanes of h = 1 receive the partner's P[k + 2] in the first and keep P[k + 2] in the second)
+      uint32_t Bk[4][2], Ck[4];
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(P[k2][w], P[k2 + 2][w], false, false);
+          Bk[2 * k2][w] = sw[0];
+          Bk[2 * k2 + 1][w] = sw[1];
+        }
+        const auto sc = __builtin_amdgcn_permlane32_swap(CW[k2], CW[k2 + 2], false, false);
+        Ck[2 * k2] = sc[0];
+        Ck[2 * k2 + 1] = sc[1];
+      }
+      const int f = wave + 4 * j, yp0 = f / 7, u = f - 7 * yp0;
+      const bool st = gi < a.B;
+      const int64_t e = ((int64_t)(st ? gi : 0) * 196 + (yp0 + 7 * half) * 14 + 2 * u + xq) * 32 + 16 * h;
+      if (st) {
+        *(u32x4*)(a.p1 + e) = u32x4{Bk[0][0], Bk[0][1], Bk[1][0], Bk[1][1]};
+        *(u32x4*)(a.p1 + e + 8) = u32x4{Bk[2][0], Bk[2][1], Bk[3][0], Bk[3][1]};
+        *(u32x4*)(a.arg1 + e) = u32x4{Ck[0], Ck[1], Ck[2], Ck[3]};
+      }
+      if constexpr (LRN) {
+        // vector 0 = B0 B1 (left: channels 16 h - 4.. = own P[1] of h = 1, zeros for h = 0;
+        // right: B2); vector 1 = B2 B3 (left B1; right: own P[2] of h = 0, zeros for h = 1)
+        uint32_t lw[2], rw[2];
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+          lw[w] = h ? P[1][w] : 0u;
+          rw[w] = h ? 0u : P[2][w];
+        }
+        auto val = [](const uint32_t (&b)[2], int i) {
+          const uint32_t w = b[i >> 1];
+          return (i & 1) ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(w << 16);
+        };
+        uint32_t nv[2][4];
+#pragma unroll
+        for (int vec = 0; vec < 2; ++vec) {
+          const uint32_t(&L)[2] = vec ? Bk[1] : lw;
+          const uint32_t(&M0)[2] = vec ? Bk[2] : Bk[0];
+          const uint32_t(&M1)[2] = vec ? Bk[3] : Bk[1];
+          const uint32_t(&R)[2] = vec ? rw : Bk[2];
+          float v[8], e16[16];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[i] = val(M0, i);
+            v[4 + i] = val(M1, i);
+            const float lv = val(L, i), rv = val(R, i);
+            e16[i] = lv * lv;
+            e16[12 + i] = rv * rv;
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) e16[4 + i] = v[i] * v[i];
+          // materialised squares: no fma contraction into the window sum (lrn_fwd_k rounds
+          // each square on its own)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(e16[i]));
+          float s[8];
+          window_sums_e<4>(e16, s);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            nv[vec][i] = pack2(lrn_out(v[2 * i], s[2 * i], l.bias, l.alpha, l.beta),
+                               lrn_out(v[2 * i + 1], s[2 * i + 1], l.bias, l.alpha, l.beta));
+        }
+        if (st) {
+          *(u32x4*)(l.norm + e) = u32x4{nv[0][0], nv[0][1], nv[0][2], nv[0][3]};
+          *(u32x4*)(l.norm + e + 8) = u32x4{nv[1][0], nv[1][1], nv[1][2], nv[1][3]};
+        }
+      }
+    }
+    if (k + 1 < nk) xf.store_pre(xs + ((k + 1) & 1) * XBUF, tid, a.u8 != nullptr);
+  }
+}
+
 int refc1_band_grid(int ntiles) {
   static int per_cu = -1, cus = 0;
   if (per_cu < 0) {
@@ -615,13 +799,47 @@ bool refc1_band_enabled() {
   return on != 0;
 }
 
+// MNISTX_REFC1_FWD: 2 (default) = refc1n_fwd_k (all 32 channels per wave; norm1 in the epilogue
+// when asked for), 1 = the round-5 refc1_band_fwd_k (two waves per unit; no norm1)
+static int g_refc1_fwd = [] { const char* e = getenv("MNISTX_REFC1_FWD"); return (e && e[0] == '1') ? 1 : 2; }();
+static int refc1_fwd_variant() { return g_refc1_fwd; }
+void refc1_set_fwd_variant(int v) { g_refc1_fwd = v == 1 ? 1 : 2; }   // tests: A/B in one process
+bool refc1_fwd_lrn_ok() { return refc1_band_enabled() && refc1_fwd_variant() == 2; }
+
+static int refc1n_grid(int ntiles) {
+  static int per_cu = -1, cus = 0;
+  if (per_cu < 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return -1;
+    cus = prop.multiProcessorCount;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, refc1n_fwd_k<true>, RNTH, 0) != hipSuccess) return -1;
+    per_cu = nb > 0 ? nb : 1;
+  }
+  const int res = reserve_cut(per_cu * cus, per_cu);
+  return cap_grid(ntiles < res ? ntiles : res);
+}
+
 hipError_t refc1_band_fwd(const XSrc& x, const bf16_t* w, const float* b, int bn, int B, bf16_t* pooled,
-                          uint8_t* arg, hipStream_t st) {
+                          uint8_t* arg, hipStream_t st, bf16_t* norm, float lrn_bias, float lrn_alpha,
+                          float lrn_beta) {
   if (B <= 0) return hipSuccess;
   if (!x.x && !x.u8) return hipErrorInvalidValue;
   BandFwd a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, w, b, bn, nullptr, nullptr, B, pooled, arg,
             nullptr, nullptr, nullptr, 0};
-  const int grid = refc1_band_grid((B + BT - 1) / BT);
+  const int ntiles = (B + BT - 1) / BT;
+  if (refc1_fwd_variant() == 2) {
+    const RefC1Lrn l{norm, lrn_bias, lrn_alpha, lrn_beta};
+    const int grid = refc1n_grid(ntiles);
+    if (grid <= 0) return hipErrorInvalidValue;
+    if (norm) hipLaunchKernelGGL(refc1n_fwd_k<true>, dim3(grid), dim3(RNTH), 0, st, a, l);
+    else hipLaunchKernelGGL(refc1n_fwd_k<false>, dim3(grid), dim3(RNTH), 0, st, a, l);
+    return hipGetLastError();
+  }
+  if (norm) return hipErrorInvalidValue;   // the round-5 kernel writes no norm1
+  const int grid = refc1_band_grid(ntiles);
   if (grid <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(refc1_band_fwd_k, dim3(grid), dim3(RNTH), 0, st, a);
   return hipGetLastError();

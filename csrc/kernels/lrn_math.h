@@ -17,6 +17,23 @@ DEV float dpp_from_right(float v) {  // lane i <- lane i+1 within its 16-lane ro
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x101, 0xf, 0xf, true));
 }
 
+// running window sums of an 8-channel vector: e = R left neighbours, the 8 values, R right
+// neighbours (zeros past the pixel's channels).  One full sum, then +entering -leaving (the
+// inputs are non-negative squares or same-scale products, so the running form loses nothing
+// at bf16 output).  Every LRN kernel sums through this, in this order.
+template <int R>
+DEV void window_sums_e(const float (&e)[8 + 2 * R], float (&s)[8]) {
+  float a = 0.f;
+#pragma unroll
+  for (int d = 0; d <= 2 * R; ++d) a += e[d];
+  s[0] = a;
+#pragma unroll
+  for (int j = 1; j < 8; ++j) {
+    a += e[j + 2 * R] - e[j - 1];
+    s[j] = a;
+  }
+}
+
 // window sums over channels of the 8 values of this lane, with the R neighbours on
 // either side taken from the adjacent lanes of the same pixel (G lanes per pixel)
 template <int G, int R>
@@ -35,17 +52,7 @@ DEV void lane_window_sums(const float (&v)[8], int c8, float (&s)[8]) {
     e[k] = c8 == 0 ? 0.f : l;
     e[R + 8 + k] = c8 == G - 1 ? 0.f : r;
   }
-  // sliding window: one full sum, then +entering -leaving (inputs are non-negative
-  // squares or same-scale products, so the running form loses nothing at bf16 output)
-  float a = 0.f;
-#pragma unroll
-  for (int d = 0; d <= 2 * R; ++d) a += e[d];
-  s[0] = a;
-#pragma unroll
-  for (int j = 1; j < 8; ++j) {
-    a += e[j + 2 * R] - e[j - 1];
-    s[j] = a;
-  }
+  window_sums_e<R>(e, s);
 }
 
 // x^p for x > 0 as exp2(p log2 x): two transcendental ops, no ln/log2e rescaling

@@ -184,9 +184,17 @@ class ConvPoolLayer(_Layer):
             return self.u8[0]
         return self.x
 
+    # (LRN spec, LRN output): the following LRN is written by this layer's forward launch
+    # (reference CNN conv1 -> norm1, lenet_band.hip refc1n_fwd_k; HipNet.fold_lrn_fwd1)
+    lrn_out: Optional[tuple] = None
+
     def fwd(self, nb: int) -> None:
+        lrn = {}
+        if self.lrn_out is not None:
+            ls, out = self.lrn_out
+            lrn = dict(lrn_out=out, lrn_bias=ls.bias, lrn_alpha=ls.alpha, lrn_beta=ls.beta, lrn_r=ls.depth_radius)
         kernels().convpool_fwd(self._xin(), self.fp.bf16_view(self.wname), self.fp.param_view(self.bname),
-                               self.spec.cout, self.out, self.arg, nb, *self._geo(), **self._src())
+                               self.spec.cout, self.out, self.arg, nb, *self._geo(), **self._src(), **lrn)
 
     skip_dgrad = False
 
@@ -524,6 +532,19 @@ class HipNet:
                     a.lrn_fold = (b.spec, self.dbuf[k + 2])   # dL/d(LRN output) = the LRN's incoming gradient
                     b.skip_bwd = True
                     self.fold_lrn = True
+        # reference CNN: norm1's forward written by conv1's forward launch from its pooled
+        # registers (refc1n_fwd_k: no lrn_fwd_k pass over pool1); MNISTX_FOLD_LRN_FWD1=0 keeps
+        # the separate LRN launch
+        self.fold_lrn_fwd1 = False
+        if dev.type == "cuda" and not fold_lrn_fwd and os.environ.get("MNISTX_FOLD_LRN_FWD1", "1") != "0":
+            for k in range(len(self.layers) - 1):
+                a, b = self.layers[k], self.layers[k + 1]
+                if (k == 0 and isinstance(a, ConvPoolLayer) and isinstance(b, LRNLayer) and b.x is a.out
+                        and b.spec.depth_radius == 4 and b.C == 32
+                        and kernels().convpool_fwd_lrn_ok(*a._geo())):
+                    a.lrn_out = (b.spec, b.out)
+                    b.skip_fwd = True
+                    self.fold_lrn_fwd1 = True
         # reference CNN: norm1's forward in conv2's input staging (LDS-halo fwd and weight-
         # gradient kernels read pool1 and normalise it; norm1 never written).  Opt-in
         # (fold_lrn_fwd=True): the LRN math in both staging loops costs more than the 67 us

@@ -751,11 +751,14 @@ void convpool_fwd(Tensor x, Tensor w, Tensor bias, int64_t bias_n, Tensor pooled
   check(arg, at::kByte, B * g.PH * g.PW * mnistx::convpool_arg_bytes(g.cfg), "arg");
   if (lrn_out.has_value() && lrn_out->defined()) {
     // the following LRN (radius 4) written by the same launch (refc1n_fwd_k): reference conv1 only
-    TORCH_CHECK(g.cfg == 2 && lrn_r == 4 && mnistx::refc1_fwd_lrn_ok(),
-                "convpool_fwd: lrn_out only for the reference conv1 (1 -> 32, SAME) with norm1 radius 4");
+    TORCH_CHECK(lrn_r == 4 && ((g.cfg == 2 && mnistx::refc1_fwd_lrn_ok()) ||
+                               (g.cfg == 3 && mnistx::refc1_fwd3_ok() && !src.u8)),
+                "convpool_fwd: lrn_out only for the reference conv1 (1 or 3 -> 32, SAME; 3 channels: bf16 input) "
+                "with norm1 radius 4");
     check(*lrn_out, at::kBFloat16, B * g.PH * g.PW * cout, "lrn_out");
     hip_ok(mnistx::refc1_band_fwd(src, BF(w), P<const float>(bias), (int)bias_n, (int)B, BFm(pooled), P<uint8_t>(arg),
-                                  cur_stream(), BFm(*lrn_out), (float)lrn_bias, (float)lrn_alpha, (float)lrn_beta),
+                                  cur_stream(), BFm(*lrn_out), (float)lrn_bias, (float)lrn_alpha, (float)lrn_beta,
+                                  g.cfg == 3 ? 3 : 1),
            "convpool_fwd (+ norm1)");
     return;
   }
@@ -1334,9 +1337,11 @@ PYBIND11_MODULE(_kernels, m) {
         py::arg("pad"), py::arg("h"), py::arg("w_"), py::arg("u8") = py::none(), py::arg("idx") = py::none(),
         py::arg("lrn_out") = py::none(), py::arg("lrn_bias") = 0.0, py::arg("lrn_alpha") = 0.0,
         py::arg("lrn_beta") = 0.0, py::arg("lrn_r") = 0);
-  m.def("convpool_fwd_lrn_ok", [](int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t w) {
-    return cp_geo(cin, cout, ks, pad, h, w).cfg == 2 && mnistx::refc1_fwd_lrn_ok();
-  });
+  // u8: the forward reads a uint8 dataset (3 channels: the fold needs bf16 input)
+  m.def("convpool_fwd_lrn_ok", [](int64_t cin, int64_t cout, int64_t ks, int64_t pad, int64_t h, int64_t w, bool u8) {
+    const int cfg = cp_geo(cin, cout, ks, pad, h, w).cfg;
+    return (cfg == 2 && mnistx::refc1_fwd_lrn_ok()) || (cfg == 3 && !u8 && mnistx::refc1_fwd3_ok());
+  }, py::arg("cin"), py::arg("cout"), py::arg("ks"), py::arg("pad"), py::arg("h"), py::arg("w"), py::arg("u8") = false);
   m.def("convpool_wgrad", &convpool_wgrad, py::arg("x"), py::arg("dP"), py::arg("arg"), py::arg("slab"),
         py::arg("grid"), py::arg("B"), py::arg("cin"), py::arg("cout"), py::arg("ks"), py::arg("pad"), py::arg("h"),
         py::arg("w_"), py::arg("u8") = py::none(), py::arg("idx") = py::none(), py::arg("lrn_p") = py::none(),

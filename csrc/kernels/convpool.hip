@@ -1698,7 +1698,9 @@ hipError_t convpool_fwd(int cfg, const XSrc& x, const bf16_t* w, const float* bi
     case 2:
       if (refc1_band_enabled()) return refc1_band_fwd(x, w, bias, bias_n, B, pooled, arg, st);
       return run_fwd<RefC1g, 2>(x, w, bias, bias_n, B, pooled, arg, st);
-    case 3: return run_fwd<RefC1c, 4>(x, w, bias, bias_n, B, pooled, arg, st);
+    case 3:
+      if (refc1_fwd3_ok() && !x.u8) return refc1_band_fwd(x, w, bias, bias_n, B, pooled, arg, st, nullptr, 0.f, 0.f, 0.f, 3);
+      return run_fwd<RefC1c, 4>(x, w, bias, bias_n, B, pooled, arg, st);
   }
   return hipErrorInvalidValue;
 }

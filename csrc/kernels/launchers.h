@@ -180,9 +180,12 @@ bool refc1_band_enabled();
 // the same launch (refc1n_fwd_k) when refc1_fwd_lrn_ok()
 bool refc1_fwd_lrn_ok();
 void refc1_set_fwd_variant(int v);   // 1: the round-5 refc1_band_fwd_k, 2: refc1n_fwd_k (default)
+// cin 3 (refc1n3_fwd_k, when refc1_fwd3_ok()): bf16 input only (x.x: the NHWC batch or the bf16
+// dataset [n][2352] through x.idx)
+bool refc1_fwd3_ok();
 hipError_t refc1_band_fwd(const XSrc& x, const bf16_t* w, const float* b, int bn, int B, bf16_t* pooled,
                           uint8_t* arg, hipStream_t st, bf16_t* norm = nullptr, float lrn_bias = 0.f,
-                          float lrn_alpha = 0.f, float lrn_beta = 0.f);
+                          float lrn_alpha = 0.f, float lrn_beta = 0.f, int cin = 1);
 hipError_t lenet_band_fwd(const XSrc& x, const bf16_t* w1, const float* b1, int b1n, const bf16_t* w2,
                           const float* b2, int B, bf16_t* p1, uint8_t* arg1, bf16_t* p2, uint8_t* arg2,
                           hipStream_t st, unsigned long long* prof = nullptr);

@@ -610,6 +610,99 @@ struct RefC1Lrn {
   float bias, alpha, beta;
 };
 
+// pool / bias / ReLU / code of channel group q (the accumulator of one unit): refc1_band_fwd_k's
+// expressions, so pool1 and the codes are bitwise that kernel's
+DEV void refc1_pool_q(const f32x16& acc, const float (&bias)[4], uint32_t (&P)[2], uint32_t& CW) {
+  float o[4];
+  uint32_t cw = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float v = vmax(vmax3(__uint_as_float(__float_as_uint(acc[i]) & ~3u), embed(acc[4 + i], 1u),
+                               embed(acc[8 + i], 2u)), embed(acc[12 + i], 3u));
+    o[i] = vmax(__uint_as_float(__float_as_uint(v) & ~3u) + bias[i], 0.f);
+    cw |= (o[i] > 0.f ? (__float_as_uint(v) & 3u) : ARG_OFF) << (8 * i);
+  }
+  P[0] = pk2(o[0], o[1]);
+  P[1] = pk2(o[2], o[3]);
+  CW = cw;
+}
+
+// A unit's pooled pixel: lane half h holds channels 8 q + 4 h + i (P[q], CW[q]).  Transposes to
+// channels 16 h .. 16 h + 15 per lane, stores pool1 / codes at element e (if st) and, with LRN,
+// norm1 from the lane's own blocks (see refc1n_fwd_k).
+template <bool LRN>
+DEV void refc1_unit_out(const uint32_t (&P)[4][2], const uint32_t (&CW)[4], int h, int64_t e, bool st,
+                        const BandFwd& a, const RefC1Lrn& l) {
+  // lane half h: 4-channel blocks Bk = channels 16 h + 4 k .. + 3 (swap(P[k], P[k + 2]): lanes
+  // of h = 0 keep P[k] in the first result and receive the partner's P[k] in the second;
+  // lanes of h = 1 receive the partner's P[k + 2] in the first and keep P[k + 2] in the second)
+  uint32_t Bk[4][2], Ck[4];
+#pragma unroll
+  for (int k2 = 0; k2 < 2; ++k2) {
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      const auto sw = __builtin_amdgcn_permlane32_swap(P[k2][w], P[k2 + 2][w], false, false);
+      Bk[2 * k2][w] = sw[0];
+      Bk[2 * k2 + 1][w] = sw[1];
+    }
+    const auto sc = __builtin_amdgcn_permlane32_swap(CW[k2], CW[k2 + 2], false, false);
+    Ck[2 * k2] = sc[0];
+    Ck[2 * k2 + 1] = sc[1];
+  }
+  if (st) {
+    *(u32x4*)(a.p1 + e) = u32x4{Bk[0][0], Bk[0][1], Bk[1][0], Bk[1][1]};
+    *(u32x4*)(a.p1 + e + 8) = u32x4{Bk[2][0], Bk[2][1], Bk[3][0], Bk[3][1]};
+    *(u32x4*)(a.arg1 + e) = u32x4{Ck[0], Ck[1], Ck[2], Ck[3]};
+  }
+  if constexpr (LRN) {
+    // vector 0 = B0 B1 (left: channels 16 h - 4.. = own P[1] of h = 1, zeros for h = 0;
+    // right: B2); vector 1 = B2 B3 (left B1; right: own P[2] of h = 0, zeros for h = 1)
+    uint32_t lw[2], rw[2];
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      lw[w] = h ? P[1][w] : 0u;
+      rw[w] = h ? 0u : P[2][w];
+    }
+    auto val = [](const uint32_t (&b)[2], int i) {
+      const uint32_t w = b[i >> 1];
+      return (i & 1) ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(w << 16);
+    };
+    uint32_t nv[2][4];
+#pragma unroll
+    for (int vec = 0; vec < 2; ++vec) {
+      const uint32_t(&L)[2] = vec ? Bk[1] : lw;
+      const uint32_t(&M0)[2] = vec ? Bk[2] : Bk[0];
+      const uint32_t(&M1)[2] = vec ? Bk[3] : Bk[1];
+      const uint32_t(&R)[2] = vec ? rw : Bk[2];
+      float v[8], e16[16];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = val(M0, i);
+        v[4 + i] = val(M1, i);
+        const float lv = val(L, i), rv = val(R, i);
+        e16[i] = lv * lv;
+        e16[12 + i] = rv * rv;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) e16[4 + i] = v[i] * v[i];
+      // materialised squares: no fma contraction into the window sum (lrn_fwd_k rounds
+      // each square on its own)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(e16[i]));
+      float s[8];
+      window_sums_e<4>(e16, s);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        nv[vec][i] = pack2(lrn_out(v[2 * i], s[2 * i], l.bias, l.alpha, l.beta),
+                           lrn_out(v[2 * i + 1], s[2 * i + 1], l.bias, l.alpha, l.beta));
+    }
+    if (st) {
+      *(u32x4*)(l.norm + e) = u32x4{nv[0][0], nv[0][1], nv[0][2], nv[0][3]};
+      *(u32x4*)(l.norm + e + 8) = u32x4{nv[1][0], nv[1][1], nv[1][2], nv[1][3]};
+    }
+  }
+}
+
 template <bool LRN>
 __global__ __launch_bounds__(RNTH, 2) void refc1n_fwd_k(const BandFwd a, const RefC1Lrn l) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[R_LDS];
@@ -684,94 +777,171 @@ __global__ __launch_bounds__(RNTH, 2) void refc1n_fwd_k(const BandFwd a, const R
         f32x16 acc = {};
 #pragma unroll
         for (int p = 0; p < 3; ++p) acc = mfma32(af[q][p], fa.b[p], acc);
-        // pool / bias / ReLU / code: refc1_band_fwd_k's expressions (bitwise the same pool1)
-        float o[4];
-        uint32_t cw = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float v = vmax(vmax3(__uint_as_float(__float_as_uint(acc[i]) & ~3u), embed(acc[4 + i], 1u),
-                                     embed(acc[8 + i], 2u)), embed(acc[12 + i], 3u));
-          o[i] = vmax(__uint_as_float(__float_as_uint(v) & ~3u) + bias[q][i], 0.f);
-          cw |= (o[i] > 0.f ? (__float_as_uint(v) & 3u) : ARG_OFF) << (8 * i);
-        }
-        P[q][0] = pk2(o[0], o[1]);
-        P[q][1] = pk2(o[2], o[3]);
-        CW[q] = cw;
+        refc1_pool_q(acc, bias[q], P[q], CW[q]);
       }
       fa = fb;
-      // lane half h: 4-channel blocks Bk = channels 16 h + 4 k .. + 3 (swap(P[k], P[k + 2]): lanes
-      // of h = 0 keep P[k] in the first result and receive the partner's P[k] in the second;
-      // lanes of h = 1 receive the partner's P[k + 2] in the first and keep P[k + 2] in the second)
-      uint32_t Bk[4][2], Ck[4];
-#pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2) {
-#pragma unroll
-        for (int w = 0; w < 2; ++w) {
-          const auto sw = __builtin_amdgcn_permlane32_swap(P[k2][w], P[k2 + 2][w], false, false);
-          Bk[2 * k2][w] = sw[0];
-          Bk[2 * k2 + 1][w] = sw[1];
-        }
-        const auto sc = __builtin_amdgcn_permlane32_swap(CW[k2], CW[k2 + 2], false, false);
-        Ck[2 * k2] = sc[0];
-        Ck[2 * k2 + 1] = sc[1];
-      }
       const int f = wave + 4 * j, yp0 = f / 7, u = f - 7 * yp0;
       const bool st = gi < a.B;
       const int64_t e = ((int64_t)(st ? gi : 0) * 196 + (yp0 + 7 * half) * 14 + 2 * u + xq) * 32 + 16 * h;
-      if (st) {
-        *(u32x4*)(a.p1 + e) = u32x4{Bk[0][0], Bk[0][1], Bk[1][0], Bk[1][1]};
-        *(u32x4*)(a.p1 + e + 8) = u32x4{Bk[2][0], Bk[2][1], Bk[3][0], Bk[3][1]};
-        *(u32x4*)(a.arg1 + e) = u32x4{Ck[0], Ck[1], Ck[2], Ck[3]};
-      }
-      if constexpr (LRN) {
-        // vector 0 = B0 B1 (left: channels 16 h - 4.. = own P[1] of h = 1, zeros for h = 0;
-        // right: B2); vector 1 = B2 B3 (left B1; right: own P[2] of h = 0, zeros for h = 1)
-        uint32_t lw[2], rw[2];
-#pragma unroll
-        for (int w = 0; w < 2; ++w) {
-          lw[w] = h ? P[1][w] : 0u;
-          rw[w] = h ? 0u : P[2][w];
-        }
-        auto val = [](const uint32_t (&b)[2], int i) {
-          const uint32_t w = b[i >> 1];
-          return (i & 1) ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(w << 16);
-        };
-        uint32_t nv[2][4];
-#pragma unroll
-        for (int vec = 0; vec < 2; ++vec) {
-          const uint32_t(&L)[2] = vec ? Bk[1] : lw;
-          const uint32_t(&M0)[2] = vec ? Bk[2] : Bk[0];
-          const uint32_t(&M1)[2] = vec ? Bk[3] : Bk[1];
-          const uint32_t(&R)[2] = vec ? rw : Bk[2];
-          float v[8], e16[16];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            v[i] = val(M0, i);
-            v[4 + i] = val(M1, i);
-            const float lv = val(L, i), rv = val(R, i);
-            e16[i] = lv * lv;
-            e16[12 + i] = rv * rv;
-          }
-#pragma unroll
-          for (int i = 0; i < 8; ++i) e16[4 + i] = v[i] * v[i];
-          // materialised squares: no fma contraction into the window sum (lrn_fwd_k rounds
-          // each square on its own)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(e16[i]));
-          float s[8];
-          window_sums_e<4>(e16, s);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            nv[vec][i] = pack2(lrn_out(v[2 * i], s[2 * i], l.bias, l.alpha, l.beta),
-                               lrn_out(v[2 * i + 1], s[2 * i + 1], l.bias, l.alpha, l.beta));
-        }
-        if (st) {
-          *(u32x4*)(l.norm + e) = u32x4{nv[0][0], nv[0][1], nv[0][2], nv[0][3]};
-          *(u32x4*)(l.norm + e + 8) = u32x4{nv[1][0], nv[1][1], nv[1][2], nv[1][3]};
-        }
-      }
+      refc1_unit_out<LRN>(P, CW, h, e, st, a, l);
     }
     if (k + 1 < nk) xf.store_pre(xs + ((k + 1) & 1) * XBUF, tid, a.u8 != nullptr);
+  }
+}
+
+// ---------------------------------------------------------------------------- 3 input channels
+// The reference's own records are 28x28x3 (mnist_input.py:13-15,134): the same banded GEMM per
+// input plane, accumulated -- a unit is 4 groups x 3 k-steps x 3 planes = 36 MFMAs.  The 36 A
+// fragments (144 VGPRs) live in an LDS table read lane-linearly (one conflict-free ds_read_b128
+// each, 1 per MFMA: under the LDS array's 2-per-gap rate), the input is staged de-interleaved
+// (one 12-byte load = 2 pixels x 3 channels -> one dword per plane), and the epilogue is
+// refc1n_fwd_k's (pool1, codes, norm1).  512 threads, units w + 8 j; the double-buffered 3-plane
+// input ring (86 KB) + table (36 KB) make it one block per CU.  bf16 input only (the batch, or
+// the bf16 dataset through the batch index, as refc1_wgrad reads it).
+constexpr int R3TH = 512, R3NW = 8;
+constexpr int PLN = XIS;                        // one input plane of an image ([2][14][32] + pad)
+constexpr int XIS3 = 3 * PLN, XBUF3 = BT * XIS3;
+constexpr int XZERO3 = 2 * XBUF3;               // zero row (out-of-image input rows)
+constexpr int AT_OFF = XZERO3 + XRW;            // A-fragment table [36][64 lanes] x 8 bf16
+constexpr int R3_LDS = AT_OFF + 36 * 64 * 8;
+static_assert(R3_LDS * 2 <= 163840, "one workgroup per CU");
+static_assert(XBUF3 >= 5 * 5 * 3 * 32 + 8, "the weights are staged in input buffer 1");
+constexpr int FC3 = 7;                          // 12-byte chunks per thread: 64 threads x 7 >= 392 per image
+
+template <bool LRN>
+__global__ __launch_bounds__(R3TH, 1) void refc1n3_fwd_k(const BandFwd a, const RefC1Lrn l) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds3[];
+  bf16_t* xs = lds3;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 31, h = lane >> 5, img = (col >> 1) & 7, half = col >> 4, xq = col & 1;
+  const int ntiles = (a.B + BT - 1) / BT;
+  const int nk = ntiles > (int)blockIdx.x ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  auto tile0 = [&](int k) { return ((int)blockIdx.x + k * (int)gridDim.x) * BT; };
+  constexpr int W3E = 5 * 5 * 3 * 32;
+  {
+    bf16_t* ws = xs + XBUF3;                     // weights [5][5][3][32] + one zero slot, in buffer 1
+    for (int e = tid; e < W3E / 8; e += R3TH) *(u32x4*)(ws + 8 * e) = *(const u32x4*)(a.w1 + 8 * e);
+    if (tid == 0) *(u32x4*)(ws + W3E) = u32x4{0u, 0u, 0u, 0u};
+    for (int e = tid; e < (XBUF3 + 0) / 8; e += R3TH) *(u32x4*)(xs + 8 * e) = u32x4{0u, 0u, 0u, 0u};
+    if (tid < XRW / 8) *(u32x4*)(xs + XZERO3 + 8 * tid) = u32x4{0u, 0u, 0u, 0u};
+    __syncthreads();
+    // A table: fragment fi = (q * 3 + p) * 3 + c, lane ln: W[dy][dx][c][8 q + c8] as in refc1n_fwd_k
+    for (int e = tid; e < 36 * 64; e += R3TH) {
+      const int fi = e >> 6, ln = e & 63, q = fi / 9, p = (fi / 3) % 3, c = fi % 3;
+      const int cl = ln & 31, hh = ln >> 5, g = cl >> 3, ypr = g >> 1, xpr = g & 1, c8 = cl & 7;
+      uint32_t wv[4];
+#pragma unroll
+      for (int j2 = 0; j2 < 4; ++j2) {
+        uint32_t pr = 0;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int j = 2 * j2 + t, dy = 2 * p + hh - ypr, dx = j - xpr;
+          const bool ok = dy >= 0 && dy <= 4 && dx >= 0 && dx <= 4;
+          pr |= (uint32_t)ws[ok ? ((dy * 5 + dx) * 3 + c) * 32 + 8 * q + c8 : W3E] << (16 * t);
+        }
+        wv[j2] = pr;
+      }
+      *(u32x4*)(xs + AT_OFF + 8 * e) = u32x4{wv[0], wv[1], wv[2], wv[3]};
+    }
+    __syncthreads();
+    for (int e = tid; e < XBUF3 / 8; e += R3TH) *(u32x4*)(xs + XBUF3 + 8 * e) = u32x4{0u, 0u, 0u, 0u};
+  }
+  float bias[4][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = 8 * q + 4 * h + i;
+      bias[q][i] = c < a.b1n ? a.b1[c] : 0.f;
+    }
+  // input staging: thread t -> image t >> 6, pixel pairs r = (t & 63) + 64 i (< 392) of its row
+  constexpr uint32_t IMGB = 784 * 3 * 2;
+  const auto rx = buf_rsrc(a.x, (uint32_t)a.n * IMGB);
+  int soff[FC3];
+#pragma unroll
+  for (int i = 0; i < FC3; ++i) {
+    const int r = (tid & 63) + 64 * i, y = r / 14, x2 = 2 * (r - 14 * y);
+    soff[i] = (tid >> 6) * XIS3 + 2 + (y & 1) * XPL + (y >> 1) * XRW + x2;
+  }
+  u32x4 xv[FC3];
+  auto xload = [&](int t0) {
+    const int gi2 = t0 + (tid >> 6);
+    uint32_t base = BUF_OOB;
+    if (t0 >= 0 && gi2 < a.B) {
+      int64_t row = a.idx ? a.idx[gi2] : (int64_t)gi2;
+      row = row < 0 ? 0 : (row >= a.n ? a.n - 1 : row);
+      base = (uint32_t)row * IMGB;
+    }
+#pragma unroll
+    for (int i = 0; i < FC3; ++i) {
+      const int r = (tid & 63) + 64 * i;
+      const auto v3 = __builtin_amdgcn_raw_buffer_load_b96(rx, r < 392 ? base + 12u * r : BUF_OOB, 0, 0);
+      xv[i] = u32x4{v3[0], v3[1], v3[2], 0u};
+    }
+  };
+  auto xstore = [&](bf16_t* xb) {
+#pragma unroll
+    for (int i = 0; i < FC3; ++i) {
+      if ((tid & 63) + 64 * i < 392) {
+        // (p0c0 p0c1) (p0c2 p1c0) (p1c1 p1c2) -> plane c = (p0c, p1c)
+        const uint32_t d0 = xv[i][0], d1 = xv[i][1], d2 = xv[i][2];
+        uint32_t* o = (uint32_t*)(xb + soff[i]);
+        o[0] = (d0 & 0xffffu) | (d1 & 0xffff0000u);
+        o[PLN / 2] = (d0 >> 16) | (d2 << 16);
+        o[PLN] = (d1 & 0xffffu) | (d2 & 0xffff0000u);
+      }
+    }
+  };
+  xload(nk > 0 ? tile0(0) : -1);
+  xstore(xs);
+  const int xlane = img * XIS3 + h * XPL + (7 * half - 1) * XRW + 2 * xq;
+  const bool top = half == 0, bot = half == 1;
+  const bf16_t* at = xs + AT_OFF + 8 * lane;
+  const int nu = (U1 - wave + R3NW - 1) / R3NW;   // units wave + 8 j: 7, 6, ..., 6
+  for (int k = 0; k < nk; ++k) {
+    __syncthreads();                              // input[k % 2] landed; input[(k + 1) % 2] free
+    const bf16_t* xb = xs + (k & 1) * XBUF3 + xlane;
+    const int t0 = tile0(k), gi = t0 + img;
+    xload(k + 1 < nk ? tile0(k + 1) : -1);
+    struct Frags { bf16x8 b[3][3]; };
+    auto fetch = [&](int j) {
+      const int f = min(wave + R3NW * j, U1 - 1), yp0 = f / 7, u = f - 7 * yp0;
+      const bf16_t* base = xb + yp0 * XRW + 4 * u;
+      Frags fr;
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const bf16_t* rp = base + p * XRW + c * PLN;
+          if (p == 0 && yp0 == 0) rp = top ? xs + XZERO3 : rp;
+          if (p == 2 && yp0 == 6) rp = bot ? xs + XZERO3 : rp;
+          const uint32_t* qq = (const uint32_t*)rp;
+          fr.b[p][c] = as_frag(u32x4{qq[0], qq[1], qq[2], qq[3]});
+        }
+      return fr;
+    };
+    Frags fa = fetch(0);
+#pragma unroll 1
+    for (int j = 0; j < nu; ++j) {
+      const Frags fb = fetch(j + 1 < nu ? j + 1 : j);
+      uint32_t P[4][2], CW[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f32x16 acc = {};
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+            acc = mfma32(*(const bf16x8*)(at + ((q * 3 + p) * 3 + c) * 512), fa.b[p][c], acc);
+        refc1_pool_q(acc, bias[q], P[q], CW[q]);
+      }
+      fa = fb;
+      const int f = wave + R3NW * j, yp0 = f / 7, u = f - 7 * yp0;
+      const bool st = gi < a.B;
+      const int64_t e = ((int64_t)(st ? gi : 0) * 196 + (yp0 + 7 * half) * 14 + 2 * u + xq) * 32 + 16 * h;
+      refc1_unit_out<LRN>(P, CW, h, e, st, a, l);
+    }
+    if (k + 1 < nk) xstore(xs + ((k + 1) & 1) * XBUF3);
   }
 }
 
@@ -822,14 +992,46 @@ static int refc1n_grid(int ntiles) {
   return cap_grid(ntiles < res ? ntiles : res);
 }
 
+static int refc1n3_grid(int ntiles) {
+  static int per_cu = -1, cus = 0;
+  if (per_cu < 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return -1;
+    cus = prop.multiProcessorCount;
+    for (auto k : {refc1n3_fwd_k<true>, refc1n3_fwd_k<false>})
+      if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, R3_LDS * 2) != hipSuccess)
+        return -1;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, refc1n3_fwd_k<true>, R3TH, R3_LDS * 2) != hipSuccess)
+      return -1;
+    per_cu = nb > 0 ? nb : 1;
+  }
+  const int res = reserve_cut(per_cu * cus, per_cu);
+  return cap_grid(ntiles < res ? ntiles : res);
+}
+
+bool refc1_fwd3_ok() { return refc1_band_enabled() && refc1_fwd_variant() == 2; }
+
 hipError_t refc1_band_fwd(const XSrc& x, const bf16_t* w, const float* b, int bn, int B, bf16_t* pooled,
                           uint8_t* arg, hipStream_t st, bf16_t* norm, float lrn_bias, float lrn_alpha,
-                          float lrn_beta) {
+                          float lrn_beta, int cin) {
   if (B <= 0) return hipSuccess;
   if (!x.x && !x.u8) return hipErrorInvalidValue;
   BandFwd a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, w, b, bn, nullptr, nullptr, B, pooled, arg,
             nullptr, nullptr, nullptr, 0};
   const int ntiles = (B + BT - 1) / BT;
+  if (cin == 3) {   // refc1n3_fwd_k: bf16 input only
+    if (x.u8 || !x.x || refc1_fwd_variant() != 2) return hipErrorInvalidValue;
+    const RefC1Lrn l{norm, lrn_bias, lrn_alpha, lrn_beta};
+    const int grid = refc1n3_grid(ntiles);
+    if (grid <= 0) return hipErrorInvalidValue;
+    if (norm) hipLaunchKernelGGL(refc1n3_fwd_k<true>, dim3(grid), dim3(R3TH), R3_LDS * 2, st, a, l);
+    else hipLaunchKernelGGL(refc1n3_fwd_k<false>, dim3(grid), dim3(R3TH), R3_LDS * 2, st, a, l);
+    return hipGetLastError();
+  }
+  if (cin != 1) return hipErrorInvalidValue;
   if (refc1_fwd_variant() == 2) {
     const RefC1Lrn l{norm, lrn_bias, lrn_alpha, lrn_beta};
     const int grid = refc1n_grid(ntiles);

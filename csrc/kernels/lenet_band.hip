@@ -924,15 +924,23 @@ __global__ __launch_bounds__(R3TH, 1) void refc1n3_fwd_k(const BandFwd a, const 
 #pragma unroll 1
     for (int j = 0; j < nu; ++j) {
       const Frags fb = fetch(j + 1 < nu ? j + 1 : j);
+      // A fragments of group q + 1 are read while group q's 9 MFMAs run (read one by one in
+      // front of each dependent MFMA, every MFMA waited a full LDS latency)
       uint32_t P[4][2], CW[4];
+      bf16x8 Ar[2][9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) Ar[0][i] = *(const bf16x8*)(at + i * 512);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        if (q + 1 < 4) {
+#pragma unroll
+          for (int i = 0; i < 9; ++i) Ar[(q + 1) & 1][i] = *(const bf16x8*)(at + ((q + 1) * 9 + i) * 512);
+        }
         f32x16 acc = {};
 #pragma unroll
         for (int p = 0; p < 3; ++p)
 #pragma unroll
-          for (int c = 0; c < 3; ++c)
-            acc = mfma32(*(const bf16x8*)(at + ((q * 3 + p) * 3 + c) * 512), fa.b[p][c], acc);
+          for (int c = 0; c < 3; ++c) acc = mfma32(Ar[q & 1][p * 3 + c], fa.b[p][c], acc);
         refc1_pool_q(acc, bias[q], P[q], CW[q]);
       }
       fa = fb;

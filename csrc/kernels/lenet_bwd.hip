@@ -336,7 +336,6 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
 #pragma unroll
   for (int t = 0; t < 3; ++t) acc1[t][0] = acc1[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
   float db1[4] = {0.f, 0.f, 0.f, 0.f};
-  const auto rcode = buf_rsrc(a.p1, (uint32_t)a.B * (NWIN1 * 16u));   // code words of the pool1 records
   const int du = a.du[wave];
   const int ks0 = a.k20[wave], ks1 = a.k21[wave];
   const int cs0 = a.k10[wave >> 1], cs1 = a.k11[wave >> 1];
@@ -369,14 +368,16 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
       const int img = i16 >> 1, rr = i16 & 1, orow = 2 * pr + rr;
       const int dylo = max(0, 2 * pr - 9), dyhi = min(4, 2 * pr + 1);
       const int u0 = 4 * hx;
-      // argmax words of this lane's windows (conv1 bias gradient: active windows only)
-      uint32_t aw[4];
+      // this lane's windows' pool1 values (channels 4 (g & 1) .. + 3), from the LDS tile: the
+      // conv1 bias gradient sums dP1 over the ACTIVE windows, and a window is active exactly
+      // when its pooled ReLU output is > 0 (code != 4).  (Read from the records' code words in
+      // HBM right in front of this unit, that latency was exposed whenever the records had
+      // left the Infinity Cache.)  Padded channels 6 / 7 have dP1 = 0 (zero conv2 weights).
+      u32x2 pv[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int w1 = orow * 14 + 2 * (u0 + u) + (g >> 1);
-        aw[u] = buf_b32(rcode, t0 + img < a.B && u0 + u < 7 ? 16u * ((uint32_t)(t0 + img) * NWIN1 + w1) + 12u : BUF_OOB);
-      }
-      // the next tile's input after this unit's code loads (vmcnt is in order)
+      for (int u = 0; u < 4; ++u)
+        pv[u] = *(const u32x2*)(lds + P1_OFF + img * P1_IMG + orow * P1_RS + (2 * min(u0 + u, 6) + (g >> 1)) * 16 +
+                                8 * (g & 1));
       if (!(PROF && (a.skip & 8))) st.load_xc(a, tile0(k + 1), wave, ln);
       f32x4 acc[4];
 #pragma unroll
@@ -387,15 +388,16 @@ __global__ __launch_bounds__(NT, 1) void lenet_bwd_k(const BwdArgs a) {
       else dgrad_unit<0>(lds, bB, bZ, orow, ln, dylo, dyhi, acc);
       // dP1 (bf16) for the conv1 weight gradient; the conv1 bias gradient from the fp32
       // sums of the active windows (code != 4, i.e. bit 2 of the nibble clear)
-      const int sh = 4 * (g & 1);
       const int wB = DP1_OFF + img * D_IMG + orow * D_RS + (2 * u0 + (g >> 1)) * 16 + 8 * (g & 1);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (u0 + u < 7) {
           *(u32x2*)(lds + wB + 32 * u) = u32x2{pack2(acc[u][0], acc[u][1]), pack2(acc[u][2], acc[u][3])};
-          const uint32_t act = (~aw[u] >> (sh + 2)) & 0x01010101u;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) db1[i] = fmaf(acc[u][i], (float)((act >> (8 * i)) & 0xffu), db1[i]);
+          for (int i = 0; i < 4; ++i) {
+            const int16_t pvi = (int16_t)((pv[u][i >> 1] >> (16 * (i & 1))) & 0xffffu);   // bf16 > 0
+            db1[i] = fmaf(acc[u][i], pvi > 0 ? 1.f : 0.f, db1[i]);
+          }
         }
       }
     } else if (!(PROF && (a.skip & 8))) {

@@ -358,18 +358,26 @@ __global__ __launch_bounds__(NTH, 4) void lenet_band_fwd_k(const BandFwd a) {
       const bool iv = gi < a.B;
       const bf16_t* pb = p1s + ((k - 1) & 1) * PBUF;
       if constexpr (P1OUT == 2) {     // combined pool1 / code records for lenet_bwd_k
-        if (cp_r < 196) {
+        // all 196 records by wave 7 (4 rounds of 64 lanes): it runs one of the 7 conv2 units
+        // where waves 4-6 run two, so the copy no longer lands on two of the busiest waves
+        if (w2v == 3) {
           const int nimg = min(BT, a.B - t0);
           const auto rp1 = buf_rsrc(a.p1 + (int64_t)t0 * P1E, (uint32_t)nimg * (P1E * 2));
-          const bf16_t* src = pb + cp_lds;
+#pragma unroll 1
+          for (int rr = 0; rr < 4; ++rr) {
+            const int r = lane + 64 * rr;
+            if (r < 196) {
+              const bf16_t* src = pb + ((r / 14) & 1) * PPL + ((r / 14) >> 1) * PRW + (r % 14) * 8;
 #pragma unroll
-          for (int i0 = 0; i0 < BT; i0 += 4) {
-            u32x4 cv[4];
+              for (int i0 = 0; i0 < BT; i0 += 4) {
+                u32x4 cv[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) cv[i] = *(const u32x4*)(src + (i0 + i) * PIS);
+                for (int i = 0; i < 4; ++i) cv[i] = *(const u32x4*)(src + (i0 + i) * PIS);
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-              __builtin_amdgcn_raw_buffer_store_b128(cv[i], rp1, (uint32_t)cp_r * 16u, (i0 + i) * (P1E * 2), 0);
+                for (int i = 0; i < 4; ++i)
+                  __builtin_amdgcn_raw_buffer_store_b128(cv[i], rp1, (uint32_t)r * 16u, (i0 + i) * (P1E * 2), 0);
+              }
+            }
           }
         }
       } else if constexpr (P1OUT == 1) {   // pool1 + argmax codes to HBM (convpool layouts)

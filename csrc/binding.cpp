@@ -396,6 +396,45 @@ bool mlp_head_supported(int64_t d0, int64_t ld1, int64_t ld2, int64_t ld3, int64
 // Fused LeNet-5 dense head.  x [>=nb, 400] bf16; w3t [128,416], w4t [96,128], w5t [16,96]
 // zero-padded transposed bf16 weights (FlatParams.bf16t_view); outputs h3 [nb,120], h4 [nb,88] bf16, logits [nb,16] fp32;
 // with dl: dl [nb,16], dh4 [nb,88], dh3 [nb,120], dx [nb,400] bf16.
+bool ce_tail_supported(int64_t d0, int64_t nc, int64_t B) { return mnistx::ce_tail_supported((int)d0, (int)nc, (int)B); }
+
+// the reference CNN's softmax_linear + softmax CE (+ data gradient masked by x > 0): mlp_head.hip ce_tail_k
+void ce_tail(Tensor x, Tensor w5t, Tensor b5, int64_t nc, Tensor labels, int64_t nb, double scale, Tensor logits,
+             optional<Tensor> dl, optional<Tensor> dx, Tensor stats, optional<Tensor> work, bool defer_stats,
+             optional<Tensor> dbias) {
+  TORCH_CHECK(mnistx::ce_tail_supported(192, (int)nc, (int)std::max<int64_t>(nb, 1)), "ce_tail: unsupported geometry");
+  check(x, at::kBFloat16, nb * 192, "x");
+  check(w5t, at::kBFloat16, 16 * 192, "w5t");
+  check(b5, at::kFloat, nc, "b5");
+  check(labels, at::kInt, nb, "labels");
+  check(logits, at::kFloat, nb * 16, "logits");
+  check(stats, at::kFloat, 8, "stats");
+  for (const Tensor* t : {&x, &w5t, &logits})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "ce_tail: operands must be 16-byte aligned");
+  const bool has_work = work.has_value() && work->defined();
+  if (has_work) check(*work, at::kFloat, 4 * 1024 + 1, "work");
+  mnistx::bf16_t *pdl = nullptr, *pdx = nullptr;
+  if (dl.has_value() && dl->defined()) {
+    TORCH_CHECK(dx.has_value() && dx->defined(), "ce_tail: dl needs dx");
+    check(*dl, at::kBFloat16, nb * 16, "dl");
+    check(*dx, at::kBFloat16, nb * 192, "dx");
+    for (const Tensor* t : {&*dl, &*dx})
+      TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "ce_tail: gradients must be 16-byte aligned");
+    pdl = BFm(*dl);
+    pdx = BFm(*dx);
+  }
+  float* db = nullptr;
+  if (dbias.has_value() && dbias->defined()) {
+    TORCH_CHECK(pdl != nullptr, "ce_tail: dbias needs dl");
+    check(*dbias, at::kFloat, (int64_t)mnistx::ce_tail_blocks((int)nb) * 16, "dbias");
+    db = P<float>(*dbias);
+  }
+  hip_ok(mnistx::ce_tail(BF(x), BF(w5t), P<const float>(b5), (int)nc, P<const int32_t>(labels), (int)nb, (float)scale,
+                         P<float>(logits), pdl, pdx, P<float>(stats), has_work ? P<float>(*work) : nullptr, cur_stream(),
+                         defer_stats ? 1 : 0, db),
+         "ce_tail");
+}
+
 void mlp_head(Tensor x, Tensor w3t, Tensor b3, int64_t n1, Tensor w4t, Tensor b4, int64_t n2, Tensor w5t, Tensor b5,
               int64_t nc, Tensor labels, int64_t nb, double scale, Tensor h3, Tensor h4, Tensor logits,
               optional<Tensor> dl, optional<Tensor> dh4, optional<Tensor> dh3, optional<Tensor> dx, Tensor stats,
@@ -1302,6 +1341,11 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("splitk_reduce", &splitk_reduce);
   m.def("splitk_reduce_multi", &splitk_reduce_multi);
   m.def("mlp_head_supported", &mlp_head_supported);
+  m.def("ce_tail_supported", &ce_tail_supported);
+  m.def("ce_tail_blocks", [](int64_t nb) { return (int64_t)mnistx::ce_tail_blocks((int)nb); });
+  m.def("ce_tail", &ce_tail, py::arg("x"), py::arg("w5t"), py::arg("b5"), py::arg("nc"), py::arg("labels"),
+        py::arg("nb"), py::arg("scale"), py::arg("logits"), py::arg("dl") = py::none(), py::arg("dx") = py::none(),
+        py::arg("stats"), py::arg("work") = py::none(), py::arg("defer_stats") = false, py::arg("dbias") = py::none());
   m.def("mlp_head", &mlp_head, py::arg("x"), py::arg("w3t"), py::arg("b3"), py::arg("n1"), py::arg("w4t"),
         py::arg("b4"), py::arg("n2"), py::arg("w5t"), py::arg("b5"), py::arg("nc"), py::arg("labels"), py::arg("nb"),
         py::arg("scale"), py::arg("h3"), py::arg("h4"), py::arg("logits"), py::arg("dl") = py::none(),

@@ -300,6 +300,14 @@ hipError_t mlp_head(const bf16_t* x, const bf16_t* w3t, const float* b3, int n1,
                     float* stats, float* work, hipStream_t st, int defer_stats = 0, float* dbias = nullptr);
 // blocks of one mlp_head launch (its per-block CE partials when defer_stats is set)
 int mlp_head_blocks(int nb);
+// the reference CNN's softmax_linear (192 -> nc <= 16) + softmax CE + its data gradient (masked by
+// x > 0) in one launch; w5t = W^T [16][192] (the optimizer's transposed copy); dbias: fp32 per-block
+// column sums [ce_tail_blocks][16]
+bool ce_tail_supported(int d0, int nc, int B);
+int ce_tail_blocks(int nb);
+hipError_t ce_tail(const bf16_t* x, const bf16_t* w5t, const float* b5, int nc, const int32_t* labels, int nb,
+                   float scale, float* logits, bf16_t* dl, bf16_t* dx, float* stats, float* work, hipStream_t st,
+                   int defer_stats, float* dbias);
 // NOTE: many splits over a small output are pre-summed IN PLACE (the slab is scratch).
 hipError_t splitk_reduce(float* slab, int splits, int M, int N, int G, int Ipad, int I, int J,
                          int bias_row, float* wdst, float* bdst, float scale, hipStream_t st);

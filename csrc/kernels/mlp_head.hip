@@ -448,7 +448,177 @@ __global__ __launch_bounds__(64 * NW) void mlp_head_k(const bf16_t* __restrict__
   if (stats) ce_block_stats<NW>(loss, corr, bad, stats, work, defer_stats != 0);
 }
 
+// ---------------------------------------------------------------------------- softmax tail
+// The reference CNN's last layer (softmax_linear 192 -> 10, mnist_input.py:200-205) with the
+// softmax cross-entropy and its data gradient as ONE kernel -- the fc5 / CE / fc5-dgrad part of
+// mlp_head_k on a 192-wide input: logits^T = W5^T . h4^T (v_mfma_f32_32x32x16_bf16, batch rows
+// as the lanes), CE statistics and dlogits in registers, then dh4^T = W5 . dlogits^T masked by
+// h4 > 0 (local4's ReLU: the layered path's dgrad mask).  Replaces three launches (the fc5 GEMM,
+// softmax_ce_rows_k, the fc5 data-gradient GEMM).  The input's k-slots are loaded in the order
+// of the dgrad accumulator (lane half h: features 16 s + 4 h .. + 3 and 16 s + 8 + 4 h .. + 3 of
+// chunk s; the W5^T image stores its columns with bits 2 and 3 swapped to match, as mlp_head's
+// fc4 / fc5 images), so the ReLU mask of every dgrad register is already in the lane.
+constexpr int TD0 = 192, TK = TD0 / 16, TU = TD0 / 32, TNW = 4, TROWS = 32 * TNW;
+DEV int toff(int r, int col) { return r * TD0 + ((((col >> 3) ^ ((r >> 2) & 3)) << 3) | (col & 7)); }
+
+template <bool GRADS>
+__global__ __launch_bounds__(64 * TNW) void ce_tail_k(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W5t,
+                                                     const float* __restrict__ b5, int nc,
+                                                     const int32_t* __restrict__ labels, int nb, float scale,
+                                                     float* __restrict__ logits, bf16_t* __restrict__ dl,
+                                                     bf16_t* __restrict__ dx, float* __restrict__ stats,
+                                                     float* __restrict__ work, int defer_stats,
+                                                     float* __restrict__ dbias) {
+  __shared__ __attribute__((aligned(16))) bf16_t i5[16 * TD0];
+  __shared__ __attribute__((aligned(16))) float bias5[LD3];
+  __shared__ __attribute__((aligned(16))) bf16_t stage[TNW * STG];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int m0 = ((int)blockIdx.x * TNW + wave) * 32, m = m0 + r;
+  const bool valid = m < nb, active = m0 < nb;
+  bf16_t* stg = stage + wave * STG;
+  // W5^T [16][192] -> the swizzled, bit-2/3-permuted image (two 8-byte halves per chunk)
+  for (int b = tid; b < 16 * TD0 / 8; b += 64 * TNW) {
+    const int rr = b / (TD0 / 8), c = (b % (TD0 / 8)) * 8;
+    const u32x4 o = *(const u32x4*)(W5t + (int64_t)b * 8);
+    *(u32x2*)(i5 + toff(rr, p23(c))) = u32x2{o[0], o[1]};
+    *(u32x2*)(i5 + toff(rr, p23(c + 4))) = u32x2{o[2], o[3]};
+  }
+  if (tid < LD3) bias5[tid] = tid < nc ? b5[tid] : 0.f;
+  // the wave's 32 x 192 input tile in the permuted k-slot order (rows past nb: row nb - 1)
+  u32x4 xr[TK];
+  int lab = -1;
+  if (active) {
+    const int mc = min(m, nb - 1);
+    const bf16_t* xrow = X + (int64_t)mc * TD0 + 4 * h;
+#pragma unroll
+    for (int c = 0; c < TK; ++c) {
+      const u32x2 a = *(const u32x2*)(xrow + 16 * c), b = *(const u32x2*)(xrow + 16 * c + 8);
+      xr[c] = u32x4{a[0], a[1], b[0], b[1]};
+    }
+    lab = labels[mc];
+  }
+  __syncthreads();
+  float loss = 0.f, corr = 0.f, bad = 0.f;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (active) {
+    f32x16 a3 = f32x16{};
+#pragma unroll
+    for (int s = 0; s < TK; ++s) {
+      bf16x8 wa = *(const bf16x8*)(i5 + toff(r & 15, 16 * s + 8 * h));
+      if (r >= 16) wa = bf16x8{};
+      a3 = mfma32(wa, __builtin_bit_cast(bf16x8, xr[s]), a3);
+    }
+    // softmax cross-entropy: mlp_head_k's (registers 0..7 hold classes (i&3) + 8(i>>2) + 4h)
+    float lg[8];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const f32x4 bb = *(const f32x4*)(bias5 + 8 * q + 4 * h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) lg[4 * q + e] = a3[4 * q + e] + bb[e];
+      if (valid) *(f32x4*)(logits + (int64_t)m * LD3 + 8 * q + 4 * h) = f32x4{lg[4 * q], lg[4 * q + 1], lg[4 * q + 2], lg[4 * q + 3]};
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if ((i & 3) + 8 * (i >> 2) + 4 * h < nc) mx = fmaxf(mx, lg[i]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float e[8], se = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      e[i] = ((i & 3) + 8 * (i >> 2) + 4 * h < nc) ? __expf(lg[i] - mx) : 0.f;
+      se += e[i];
+    }
+    se += __shfl_xor(se, 32, 64);
+    if (!valid) lab = -1;
+    float ll = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ll = ((i & 3) + 8 * (i >> 2) + 4 * h == lab) ? lg[i] : ll;
+    ll += __shfl_xor(ll, 32, 64);
+    if (valid && h == 0) {
+      const float lo = -(ll - mx - __logf(se));
+      loss += lo;
+      corr += (ll >= mx) ? 1.f : 0.f;
+      bad = isfinite(lo) ? bad : 1.f;
+    }
+    if constexpr (GRADS) {
+      const float inv = 1.f / se;
+      uint32_t dlp[4];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        float g2[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int i = 2 * w + k, cls = (i & 3) + 8 * (i >> 2) + 4 * h;
+          g2[k] = cls < nc ? (e[i] * inv - (cls == lab ? 1.f : 0.f)) * scale : 0.f;
+          cs[i] += valid ? g2[k] : 0.f;
+        }
+        dlp[w] = pack2(g2[0], g2[1]);
+      }
+      if (valid)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) *(u32x2*)(dl + (int64_t)m * LD3 + 8 * q + 4 * h) = u32x2{dlp[2 * q], dlp[2 * q + 1]};
+      // dh4^T[192 x 32] = W5 . dlogits^T, masked by h4 > 0: register k of tile u = feature
+      // 32 u + 8 (k >> 2) + 4 h + (k & 3) = chunk 2 u + (k >> 3), word 2 ((k >> 2) & 1) + ((k & 3) >> 1)
+      const int q4 = (lane >> 2) & 3, c16 = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+      const bf16x8 db = as_frag(dlp[0], dlp[1], dlp[2], dlp[3]);
+#pragma unroll
+      for (int u = 0; u < TU; ++u) {
+        const int col = p23(32 * u + c16);
+        const s16x4 lo = lds_tr4(i5 + toff(4 * h + q4, col));
+        const s16x4 hi = lds_tr4(i5 + toff(8 + 4 * h + q4, col));
+        const f32x16 acc = mfma32(join(lo, hi), db, f32x16{});
+        uint32_t pk[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+          const uint32_t xw = xr[2 * u + (w >> 2)][w & 3];   // features of registers 2w, 2w + 1
+          const float v0 = pos_lo(xw) ? acc[2 * w] : 0.f;
+          const float v1 = pos_hi(xw) ? acc[2 * w + 1] : 0.f;
+          pk[w] = pack2(v0, v1);
+        }
+        store_tile(stg, pk, dx, TD0, m0, nb, 32 * u, TD0 - 32 * u, lane);
+      }
+    }
+  }
+  if (GRADS && dbias) {
+    __shared__ float dbs[TNW][16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) cs[i] += __shfl_xor(cs[i], o, 64);
+    }
+    if (r == 0)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dbs[wave][(i & 3) + 8 * (i >> 2) + 4 * h] = cs[i];
+    __syncthreads();
+    if (tid < 16) {
+      float v = dbs[0][tid];
+#pragma unroll
+      for (int w = 1; w < TNW; ++w) v += dbs[w][tid];
+      dbias[(int64_t)blockIdx.x * 16 + tid] = v;
+    }
+  }
+  if (stats) ce_block_stats<TNW>(loss, corr, bad, stats, work, defer_stats != 0);
+}
+
 }  // namespace
+
+int ce_tail_blocks(int nb) { return (nb + TROWS - 1) / TROWS; }
+bool ce_tail_supported(int d0, int nc, int B) { return d0 == TD0 && nc > 0 && nc <= LD3 && B > 0 && ce_tail_blocks(B) <= CE_MAXB; }
+
+hipError_t ce_tail(const bf16_t* x, const bf16_t* w5t, const float* b5, int nc, const int32_t* labels, int nb,
+                   float scale, float* logits, bf16_t* dl, bf16_t* dx, float* stats, float* work, hipStream_t st,
+                   int defer_stats, float* dbias) {
+  if (nb <= 0) return hipSuccess;
+  const dim3 grid(ce_tail_blocks(nb));
+  if (dl)
+    hipLaunchKernelGGL(ce_tail_k<true>, grid, dim3(64 * TNW), 0, st, x, w5t, b5, nc, labels, nb, scale, logits, dl, dx,
+                       stats, work, defer_stats, dbias);
+  else
+    hipLaunchKernelGGL(ce_tail_k<false>, grid, dim3(64 * TNW), 0, st, x, w5t, b5, nc, labels, nb, scale, logits,
+                       nullptr, nullptr, stats, work, defer_stats, nullptr);
+  return hipGetLastError();
+}
 
 int mlp_head_blocks(int nb) { return (nb + ROWS - 1) / ROWS; }
 

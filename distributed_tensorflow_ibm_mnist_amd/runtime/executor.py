@@ -514,10 +514,17 @@ class HipNet:
         self.idx_buf: Optional[torch.Tensor] = None
         # fused dense head (mlp_head.hip): index of its first layer, or None
         self.head: Optional[int] = self._find_head() if (fuse_head and dev.type == "cuda") else None
+        # "mlp" (LeNet-5's three-layer head) or "tail" (the reference CNN's softmax_linear +
+        # softmax-CE + its masked data gradient as one launch, mlp_head.hip ce_tail_k;
+        # MNISTX_CE_TAIL=0 keeps the GEMM + softmax_ce + dgrad launches)
+        self.head_kind = "mlp" if self.head is not None else None
+        if self.head is None and fuse_head and dev.type == "cuda" and os.environ.get("MNISTX_CE_TAIL", "1") != "0":
+            self.head = self._find_tail()
+            self.head_kind = "tail" if self.head is not None else None
         self._head_pending: Optional[int] = None   # nb of a deferred head (forward(defer_head=True))
         # the head's fc3/fc4/fc5 weight gradients as one grouped launch (gemm.hip
         # dense_wgrad_group)
-        self.group_head_wgrad = (self.head is not None
+        self.group_head_wgrad = (self.head_kind == "mlp"
                                  and all(l.Dp % 8 == 0 and l.Np % 8 == 0 for l in self.layers[self.head:]))
         self._group_S: Optional[list] = None
         self._head_grads = False                   # loss_and_grad already produced the head's dgrads
@@ -616,11 +623,38 @@ class HipNet:
         self.fp.enable_transposed({l3.wname: (128, 416), l4.wname: (96, 128), l5.wname: (16, 96)})
         return i
 
+    def _find_tail(self) -> Optional[int]:
+        """The reference CNN's softmax_linear (192 -> 10, no ReLU, on local4's ReLU output,
+        mnist_input.py:195-203) + softmax-CE (+ dL/d local4, masked by local4 > 0) as ONE
+        kernel (mlp_head.hip ce_tail_k)."""
+        if len(self.layers) < 2:
+            return None
+        i = len(self.layers) - 1
+        l5 = self.layers[i]
+        if not (isinstance(l5, DenseLayer) and (l5.Dp, l5.Np) == (192, 16) and l5.in_relu and not l5.spec.relu
+                and l5.spec.din == 192):
+            return None
+        if not kernels().ce_tail_supported(192, l5.spec.dout, self.B):
+            return None
+        self.fp.enable_transposed({l5.wname: (16, 192)})
+        return i
+
     def _run_head(self, nb: int, scale: float, grads: bool, stats: torch.Tensor) -> None:
         i = self.head
         # training statistics: the per-block CE partials are combined by this step's
         # finalize_k (no agent-scope fence / ticket inside the head; ce_stats.h)
         defer = grads and stats is self.stats and self.ce_work is not None
+        if self.head_kind == "tail":
+            l5 = self.layers[i]
+            K = kernels()
+            K.ce_tail(l5.x, self.fp.bf16t_view(l5.wname), self.fp.param_view(l5.bname), l5.spec.dout, self.labels,
+                      nb, scale, l5.out, dl=self.dlogits if grads else None, dx=self.dbuf[i] if grads else None,
+                      stats=stats, work=self.ce_work, defer_stats=defer, dbias=self.ce_dbias if grads else None)
+            if grads:
+                l5.ce_bias = (self.ce_dbias, K.ce_tail_blocks(nb))
+            if defer:
+                self._ce_defer_blocks = K.ce_tail_blocks(nb)
+            return
         l3, l4, l5 = self.layers[i:]
         fp = self.fp
         kernels().mlp_head(l3.x, fp.bf16t_view(l3.wname), fp.param_view(l3.bname), l3.spec.dout,

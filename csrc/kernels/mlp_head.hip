@@ -458,10 +458,10 @@ __global__ __launch_bounds__(64 * NW) void mlp_head_k(const bf16_t* __restrict__
 // of the dgrad accumulator (lane half h: features 16 s + 4 h .. + 3 and 16 s + 8 + 4 h .. + 3 of
 // chunk s; the W5^T image stores its columns with bits 2 and 3 swapped to match, as mlp_head's
 // fc4 / fc5 images), so the ReLU mask of every dgrad register is already in the lane.
-constexpr int TD0 = 192, TK = TD0 / 16, TU = TD0 / 32, TNW = 4, TROWS = 32 * TNW;
+constexpr int TD0 = 192, TK = TD0 / 16, TU = TD0 / 32;
 DEV int toff(int r, int col) { return r * TD0 + ((((col >> 3) ^ ((r >> 2) & 3)) << 3) | (col & 7)); }
 
-template <bool GRADS>
+template <int TNW, bool GRADS>
 __global__ __launch_bounds__(64 * TNW) void ce_tail_k(const bf16_t* __restrict__ X, const bf16_t* __restrict__ W5t,
                                                      const float* __restrict__ b5, int nc,
                                                      const int32_t* __restrict__ labels, int nb, float scale,
@@ -603,7 +603,20 @@ __global__ __launch_bounds__(64 * TNW) void ce_tail_k(const bf16_t* __restrict__
 
 }  // namespace
 
-int ce_tail_blocks(int nb) { return (nb + TROWS - 1) / TROWS; }
+// waves per block (32 rows each): 2, or more when the block count would exceed the CE partial
+// slots; MNISTX_CE_TAIL_NW overrides (1, 2 or 4).  At B = 16384 2 waves (256 blocks) measured
+// 9.9 us, 1 wave 11.6 us, 4 waves 10.9 us (profiles/r6/cetail/README.md)
+int ce_tail_nw(int nb) {
+  static const int forced = [] {
+    const char* e = getenv("MNISTX_CE_TAIL_NW");
+    const int v = e ? atoi(e) : 0;
+    return (v == 1 || v == 2 || v == 4) ? v : 0;
+  }();
+  int nw = forced ? forced : 2;
+  while (nw < 4 && (nb + 32 * nw - 1) / (32 * nw) > CE_MAXB) nw *= 2;
+  return nw;
+}
+int ce_tail_blocks(int nb) { const int r = 32 * ce_tail_nw(nb); return (nb + r - 1) / r; }
 bool ce_tail_supported(int d0, int nc, int B) { return d0 == TD0 && nc > 0 && nc <= LD3 && B > 0 && ce_tail_blocks(B) <= CE_MAXB; }
 
 hipError_t ce_tail(const bf16_t* x, const bf16_t* w5t, const float* b5, int nc, const int32_t* labels, int nb,
@@ -611,12 +624,20 @@ hipError_t ce_tail(const bf16_t* x, const bf16_t* w5t, const float* b5, int nc, 
                    int defer_stats, float* dbias) {
   if (nb <= 0) return hipSuccess;
   const dim3 grid(ce_tail_blocks(nb));
-  if (dl)
-    hipLaunchKernelGGL(ce_tail_k<true>, grid, dim3(64 * TNW), 0, st, x, w5t, b5, nc, labels, nb, scale, logits, dl, dx,
-                       stats, work, defer_stats, dbias);
-  else
-    hipLaunchKernelGGL(ce_tail_k<false>, grid, dim3(64 * TNW), 0, st, x, w5t, b5, nc, labels, nb, scale, logits,
-                       nullptr, nullptr, stats, work, defer_stats, nullptr);
+  const int nw = ce_tail_nw(nb);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(64 * nw), 0, st, x, w5t, b5, nc, labels, nb, scale, logits, dl, dx, stats,
+                       work, defer_stats, dl ? dbias : nullptr);
+  };
+  if (dl) {
+    if (nw == 1) go(ce_tail_k<1, true>);
+    else if (nw == 2) go(ce_tail_k<2, true>);
+    else go(ce_tail_k<4, true>);
+  } else {
+    if (nw == 1) go(ce_tail_k<1, false>);
+    else if (nw == 2) go(ce_tail_k<2, false>);
+    else go(ce_tail_k<4, false>);
+  }
   return hipGetLastError();
 }
 

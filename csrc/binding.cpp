@@ -318,13 +318,13 @@ bool lrn_pool_supported(int64_t H, int64_t W, int64_t C, int64_t r) {
 }
 
 void lrn_pool_fwd(Tensor x, Tensor y, Tensor arg, int64_t Nb, int64_t H, int64_t W, int64_t C, int64_t r,
-                  double bias, double alpha, double beta) {
+                  double bias, double alpha, double beta, bool nonneg) {
   TORCH_CHECK(mnistx::lrn_pool_supported((int)H, (int)W, (int)C, (int)r), "lrn_pool: unsupported geometry");
   check(x, at::kBFloat16, Nb * H * W * C, "x");
   check(y, at::kBFloat16, Nb * (H / 2) * (W / 2) * C, "y");
   check(arg, at::kByte, Nb * (H / 2) * (W / 2) * C, "arg");
   hip_ok(mnistx::lrn_pool_fwd(BF(x), (int)Nb, (int)H, (int)W, (int)C, (int)r, (float)bias, (float)alpha,
-                              (float)beta, BFm(y), P<uint8_t>(arg), cur_stream()),
+                              (float)beta, BFm(y), P<uint8_t>(arg), cur_stream(), nonneg ? 1 : 0),
          "lrn_pool_fwd");
 }
 
@@ -1331,7 +1331,10 @@ PYBIND11_MODULE(_kernels, m) {
   m.def("lrn_fwd", &lrn_fwd);
   m.def("lrn_bwd", &lrn_bwd);
   m.def("lrn_pool_supported", &lrn_pool_supported);
-  m.def("lrn_pool_fwd", &lrn_pool_fwd);
+  m.def("lrn_pool_fwd", &lrn_pool_fwd, py::arg("x"), py::arg("y"), py::arg("arg"), py::arg("Nb"), py::arg("H"),
+        py::arg("W"), py::arg("C"), py::arg("r"), py::arg("bias"), py::arg("alpha"), py::arg("beta"),
+        py::arg("nonneg") = false);
+  m.def("lrn_set_packed", [](bool on) { mnistx::lrn_set_packed(on ? 1 : 0); });
   m.def("lrn_pool_bwd", &lrn_pool_bwd);
   m.def("softmax_ce", &softmax_ce, py::arg("logits"), py::arg("ldl"), py::arg("labels"), py::arg("B"), py::arg("NC"),
         py::arg("scale"), py::arg("dlogits"), py::arg("ldd"), py::arg("stats"), py::arg("probs"),

@@ -275,7 +275,9 @@ hipError_t lrn_bwd(const bf16_t* x, const bf16_t* dy, int P, int C, int r, float
 // and its backward from the pooled gradient
 bool lrn_pool_supported(int H, int W, int C, int r);
 hipError_t lrn_pool_fwd(const bf16_t* x, int Nb, int H, int W, int C, int r, float bias, float alpha, float beta,
-                        bf16_t* y, uint8_t* arg, hipStream_t st);
+                        bf16_t* y, uint8_t* arg, hipStream_t st, int nonneg = 0);
+// nonneg: the input is >= 0 (post-ReLU), which the packed 14 x 14 x 64 forward needs
+void lrn_set_packed(int on);
 hipError_t lrn_pool_bwd(const bf16_t* x, const bf16_t* dP, const uint8_t* arg, int Nb, int H, int W, int C, int r,
                         float bias, float alpha, float beta, int relu_mask, bf16_t* dx, hipStream_t st);
 // work (optional): >= 4*1024+1 floats, zero-initialised once; makes the loss /

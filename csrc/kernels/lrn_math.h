@@ -21,9 +21,12 @@ DEV float dpp_from_right(float v) {  // lane i <- lane i+1 within its 16-lane ro
 // neighbours (zeros past the pixel's channels).  One full sum, then +entering -leaving (the
 // inputs are non-negative squares or same-scale products, so the running form loses nothing
 // at bf16 output).  Every LRN kernel sums through this, in this order.
-template <int R>
-DEV void window_sums_e(const float (&e)[8 + 2 * R], float (&s)[8]) {
-  float a = 0.f;
+template <int R, class T>
+DEV void window_sums_e(const T (&e)[8 + 2 * R], T (&s)[8]) {
+  // never fused with the multiplies that produced e (squares, products): every caller then
+  // sums the same rounded values, whatever it inlines (bitwise equality across kernels)
+#pragma clang fp contract(off)
+  T a = T{};
 #pragma unroll
   for (int d = 0; d <= 2 * R; ++d) a += e[d];
   s[0] = a;
@@ -148,6 +151,67 @@ DEV u32x4 lrn_bwd8(const u32x4& xv, const u32x4& gv, int c8, float bias, float a
   unpack8(xv, v);
   unpack8(gv, g);
   return lrn_bwd8_vals<G, R, B075>(v, g, c8, bias, alpha, beta, relu_mask);
+}
+
+// ---- packed forms: two independent vectors per lane (two pool windows, or two pixels of
+// one), so the element-wise work issues as v_pk_{mul,add,fma}_f32.  Each half runs the
+// scalar helpers' IEEE operations in the same order: bitwise the scalar forms above.
+typedef float f2 __attribute__((ext_vector_type(2)));
+DEV f2 f2s(float a) { return f2{a, a}; }
+DEV f2 f2fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+template <int G, int R>
+DEV void lane_window_sums2(const f2 (&v)[8], int c8, f2 (&s)[8]) {
+  static_assert(R <= 8 && 16 % G == 0 && G > 1, "neighbours must come from the adjacent lane of one DPP row");
+  f2 e[8 + 2 * R];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) e[R + j] = v[j];
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const f2 l = f2{dpp_from_left(v[8 - R + k].x), dpp_from_left(v[8 - R + k].y)};
+    const f2 r = f2{dpp_from_right(v[k].x), dpp_from_right(v[k].y)};
+    e[k] = c8 == 0 ? f2{} : l;
+    e[R + 8 + k] = c8 == G - 1 ? f2{} : r;
+  }
+  window_sums_e<R>(e, s);
+}
+
+// lrn_out on two values
+DEV f2 lrn_out2(f2 v, f2 s, float bias, float alpha, float beta) {
+  const f2 sc = f2fma(f2s(alpha), s, f2s(bias));
+  const f2 p = f2s(-beta) * f2{__builtin_amdgcn_logf(sc.x), __builtin_amdgcn_logf(sc.y)};
+  return v * f2{__builtin_amdgcn_exp2f(p.x), __builtin_amdgcn_exp2f(p.y)};
+}
+
+// lrn_bwd8_vals<G, R, true> (beta = 0.75) on two vectors
+template <int G, int R>
+DEV void lrn_bwd2_b075(const f2 (&v)[8], const f2 (&g)[8], int c8, float bias, float alpha, float beta, int relu_mask,
+                       f2 (&o)[8]) {
+  f2 w[8], s[8], u[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) w[j] = v[j] * v[j];
+  lane_window_sums2<G, R>(w, c8, s);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const f2 sc = f2fma(f2s(alpha), s[j], f2s(bias));
+    const f2 r = f2{__builtin_amdgcn_rsqf(sc.x), __builtin_amdgcn_rsqf(sc.y)};
+    const f2 q = f2{__builtin_amdgcn_sqrtf(r.x), __builtin_amdgcn_sqrtf(r.y)};
+    const f2 pw = r * q;
+    const f2 pw1 = pw * (r * r);
+    s[j] = pw;
+    w[j] = g[j] * v[j] * pw1;
+  }
+  lane_window_sums2<G, R>(w, c8, u);
+  const f2 k = f2s(2.f * alpha * beta);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    f2 d = f2fma(g[j], s[j], -((k * v[j]) * u[j]));
+    if (relu_mask) {
+      d.x = v[j].x > 0.f ? d.x : 0.f;
+      d.y = v[j].y > 0.f ? d.y : 0.f;
+    }
+    o[j] = d;
+  }
 }
 
 }  // namespace

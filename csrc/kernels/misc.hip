@@ -415,6 +415,115 @@ __global__ __launch_bounds__(TPB) void lrn_pool_bwd_k(const bf16_t* __restrict__
   }
 }
 
+// The reference CNN's norm2 -> pool2 (64 channels, 14 x 14, radius 4, post-ReLU input) on
+// packed fp32.  lrn_pool_fwd_k / lrn_pool_bwd_k spend most of their issue slots on VALU work
+// (profiles/r6/lrnpk/): 32-bit index math with the geometry as constants (no 64-bit divides),
+// the element-wise LRN math of two vectors per lane as v_pk ops, and -- forward, input >= 0 --
+// the 4-way max + first-argmax as an integer max of keys (bf16 bits << 16 | 3 - d: larger value,
+// then earlier pixel, wins), instead of a compare and two selects per pixel.  Bitwise
+// lrn_pool_fwd_k / lrn_pool_bwd_k (tests/test_kernels_gpu.py test_lrn_pool_packed).
+constexpr int LP14_C = 64, LP14_G = 8, LP14_HW = 14, LP14_OW = 7, LP14_NWIN = 49;
+template <int R>
+__global__ __launch_bounds__(TPB) void lrn_pool14_fwd_k(const bf16_t* __restrict__ x, int Nb, float bias, float alpha,
+                                                        float beta, bf16_t* __restrict__ y, uint8_t* __restrict__ arg) {
+  constexpr int C = LP14_C, G = LP14_G, HW = LP14_HW;
+  const unsigned total = (unsigned)Nb * LP14_NWIN * G;
+  const int c8 = threadIdx.x % G;
+  const unsigned step = gridDim.x * TPB;
+  for (unsigned base = blockIdx.x * TPB; base < total; base += 2 * step) {
+    u32x4 xq[2][4];
+    unsigned wk[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const unsigned t = base + k * step + threadIdx.x;
+      const unsigned win = t < total ? t / G : 0u;
+      wk[k] = win;
+      const unsigned n = win / LP14_NWIN, rem = win - n * LP14_NWIN, oh = rem / LP14_OW, ow = rem - oh * LP14_OW;
+      const bf16_t* p = x + ((int64_t)((n * HW + 2 * oh) * HW + 2 * ow)) * C + c8 * 8;
+      xq[k][0] = *(const u32x4*)p;
+      xq[k][1] = *(const u32x4*)(p + C);
+      xq[k][2] = *(const u32x4*)(p + HW * C);
+      xq[k][3] = *(const u32x4*)(p + HW * C + C);
+    }
+    int best[2][8];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      f2 v[8], sq[8], s[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[j] = f2{u4_get(xq[0][d], j), u4_get(xq[1][d], j)};
+        sq[j] = v[j] * v[j];
+      }
+      lane_window_sums2<G, R>(sq, c8, s);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const f2 yv = lrn_out2(v[j], s[j], bias, alpha, beta);
+        const uint32_t pk = pack2(yv.x, yv.y);   // window 0's bf16 low, window 1's high
+        const int k0 = (int)((pk << 16) | (uint32_t)(3 - d)), k1 = (int)((pk & 0xffff0000u) | (uint32_t)(3 - d));
+        best[0][j] = d == 0 ? k0 : max(best[0][j], k0);
+        best[1][j] = d == 0 ? k1 : max(best[1][j], k1);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const unsigned t = base + k * step + threadIdx.x;
+      if (t < total) {
+        u32x4 o;
+        uint32_t cw[2] = {0u, 0u};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          o[j] = ((uint32_t)best[k][2 * j] >> 16) | ((uint32_t)best[k][2 * j + 1] & 0xffff0000u);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cw[j >> 2] |= (((uint32_t)best[k][j] & 3u) ^ 3u) << (8 * (j & 3));
+        const int64_t off = (int64_t)wk[k] * C + c8 * 8;
+        *(u32x4*)(y + off) = o;
+        *(u32x2*)(arg + off) = u32x2{cw[0], cw[1]};
+      }
+    }
+  }
+}
+
+template <int R>
+__global__ __launch_bounds__(TPB) void lrn_pool14_bwd_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dP,
+                                                        const uint8_t* __restrict__ arg, int Nb, float bias, float alpha,
+                                                        float beta, int relu_mask, bf16_t* __restrict__ dx) {
+  constexpr int C = LP14_C, G = LP14_G, HW = LP14_HW;
+  const unsigned total = (unsigned)Nb * LP14_NWIN * G;
+  const int c8 = threadIdx.x % G;
+  for (unsigned base = blockIdx.x * TPB; base < total; base += gridDim.x * TPB) {
+    const unsigned t = base + threadIdx.x;
+    const bool ok = t < total;
+    const unsigned win = ok ? t / G : 0u;
+    const unsigned n = win / LP14_NWIN, rem = win - n * LP14_NWIN, oh = rem / LP14_OW, ow = rem - oh * LP14_OW;
+    const int64_t poff = (int64_t)win * C + c8 * 8;
+    const u32x4 pv = *(const u32x4*)(dP + poff);
+    const u32x2 av = *(const u32x2*)(arg + poff);
+    const int64_t x0 = ((int64_t)((n * HW + 2 * oh) * HW + 2 * ow)) * C + c8 * 8;
+    u32x4 xq[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) xq[d] = *(const u32x4*)(x + x0 + ((d >> 1) * HW + (d & 1)) * C);
+    float pg[8];
+    unpack8(pv, pg);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {   // pixels 2h, 2h + 1 (one row of the window) as the two halves
+      f2 v[8], g[8], o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t aj = ((j < 4 ? av[0] : av[1]) >> (8 * (j & 3))) & 0xffu;
+        v[j] = f2{u4_get(xq[2 * h], j), u4_get(xq[2 * h + 1], j)};
+        g[j] = f2{aj == (uint32_t)(2 * h) ? pg[j] : 0.f, aj == (uint32_t)(2 * h + 1) ? pg[j] : 0.f};
+      }
+      lrn_bwd2_b075<G, R>(v, g, c8, bias, alpha, beta, relu_mask, o);
+      if (ok) {
+        *(u32x4*)(dx + x0 + (h * HW) * C) =
+            u32x4{pack2(o[0].x, o[1].x), pack2(o[2].x, o[3].x), pack2(o[4].x, o[5].x), pack2(o[6].x, o[7].x)};
+        *(u32x4*)(dx + x0 + (h * HW + 1) * C) =
+            u32x4{pack2(o[0].y, o[1].y), pack2(o[2].y, o[3].y), pack2(o[4].y, o[5].y), pack2(o[6].y, o[7].y)};
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ K8 softmax cross-entropy
 // stats[0] += sum(-log p[label]) ; stats[1] += #(logit[label] == max) ; stats[2] = 1 if non-finite.
 __global__ void softmax_ce_k(const float* __restrict__ logits, int ldl, const int32_t* __restrict__ labels, int B,
@@ -1156,9 +1265,22 @@ hipError_t lrn_fwd(const bf16_t* x, int P, int C, int r, float bias, float alpha
 bool lrn_pool_supported(int H, int W, int C, int r) {
   return H % 2 == 0 && W % 2 == 0 && (C == 32 || C == 64) && r == 4;
 }
+// the packed 14 x 14 x 64 kernels (MNISTX_LRN_PK=0: the generic ones)
+static int g_lrn_pk = [] { const char* e = getenv("MNISTX_LRN_PK"); return (e && e[0] == '0') ? 0 : 1; }();
+void lrn_set_packed(int on) { g_lrn_pk = on; }
+static bool lrn_pk14(int H, int W, int C, int r, int Nb) {
+  return g_lrn_pk && H == LP14_HW && W == LP14_HW && C == LP14_C && r == 4 && (int64_t)Nb * LP14_NWIN * LP14_G < (1ll << 31);
+}
+
 hipError_t lrn_pool_fwd(const bf16_t* x, int Nb, int H, int W, int C, int r, float bias, float alpha, float beta,
-                        bf16_t* y, uint8_t* arg, hipStream_t st) {
+                        bf16_t* y, uint8_t* arg, hipStream_t st, int nonneg) {
   if (!lrn_pool_supported(H, W, C, r)) return hipErrorInvalidValue;
+  if (nonneg && lrn_pk14(H, W, C, r, Nb)) {
+    if (Nb <= 0) return hipSuccess;
+    dim3 grid(nblocks(((int64_t)Nb * LP14_NWIN * LP14_G + 1) / 2, TPB, 16384));
+    hipLaunchKernelGGL((lrn_pool14_fwd_k<4>), grid, dim3(TPB), 0, st, x, Nb, bias, alpha, beta, y, arg);
+    return hipGetLastError();
+  }
   dim3 grid(nblocks(((int64_t)Nb * (H / 2) * (W / 2) * (C / 8) + LRNP_U - 1) / LRNP_U, TPB, 16384));
   if (C == 64) hipLaunchKernelGGL((lrn_pool_fwd_k<64, 4>), grid, dim3(TPB), 0, st, x, Nb, H, W, bias, alpha, beta, y, arg);
   else hipLaunchKernelGGL((lrn_pool_fwd_k<32, 4>), grid, dim3(TPB), 0, st, x, Nb, H, W, bias, alpha, beta, y, arg);
@@ -1168,6 +1290,11 @@ hipError_t lrn_pool_bwd(const bf16_t* x, const bf16_t* dP, const uint8_t* arg, i
                         float bias, float alpha, float beta, int relu_mask, bf16_t* dx, hipStream_t st) {
   if (!lrn_pool_supported(H, W, C, r)) return hipErrorInvalidValue;
   dim3 grid(nblocks((int64_t)Nb * (H / 2) * (W / 2) * (C / 8), TPB, 16384));
+  if (beta == 0.75f && lrn_pk14(H, W, C, r, Nb)) {
+    if (Nb <= 0) return hipSuccess;
+    hipLaunchKernelGGL((lrn_pool14_bwd_k<4>), grid, dim3(TPB), 0, st, x, dP, arg, Nb, bias, alpha, beta, relu_mask, dx);
+    return hipGetLastError();
+  }
 #define LRN_PB(CC, BB) \
   hipLaunchKernelGGL((lrn_pool_bwd_k<CC, 4, BB>), grid, dim3(TPB), 0, st, x, dP, arg, Nb, H, W, bias, alpha, beta, relu_mask, dx)
   const bool b075 = beta == 0.75f;   // the reference's beta (lrn_math.h pow_beta)

@@ -306,7 +306,7 @@ class LRNPoolLayer(_Layer):
     def fwd(self, nb: int) -> None:
         s = self.spec
         kernels().lrn_pool_fwd(self.x, self.out, self.arg, nb, self.H, self.W, self.C, s.depth_radius, s.bias,
-                               s.alpha, s.beta)
+                               s.alpha, s.beta, nonneg=self.in_relu)   # post-ReLU input: the packed kernel
 
     def bwd_data(self, nb: int, dy, dx) -> None:
         if dx is not None:

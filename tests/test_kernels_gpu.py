@@ -545,7 +545,7 @@ def test_lrn_pool_matches_two_step(dev, K, N, H, W, C, relu):
     y = torch.empty(N, OH, OW, C, dtype=torch.bfloat16, device=dev)
     arg = torch.empty(N, OH, OW, C, dtype=torch.uint8, device=dev)
     assert K.lrn_pool_supported(H, W, C, r)
-    K.lrn_pool_fwd(x, y, arg, N, H, W, C, r, bias, alpha, beta)
+    K.lrn_pool_fwd(x, y, arg, N, H, W, C, r, bias, alpha, beta, nonneg=relu)
     l = torch.empty_like(x)
     K.lrn_fwd(x, l, N * H * W, C, r, bias, alpha, beta)
     y2 = torch.empty_like(y)
@@ -560,6 +560,36 @@ def test_lrn_pool_matches_two_step(dev, K, N, H, W, C, relu):
     dx2 = torch.empty_like(x)
     K.lrn_bwd(x, dl, dx2, N * H * W, C, r, bias, alpha, beta, relu)
     assert torch.equal(dx, dx2)
+
+
+@pytest.mark.parametrize("N", [1, 77, 40000])
+def test_lrn_pool_packed(dev, K, N):
+    """The packed 14x14x64 norm2 -> pool2 kernels (misc.hip lrn_pool14_fwd_k / _bwd_k: v_pk math,
+    integer-key argmax on the post-ReLU input) == the generic lrn_pool kernels, bitwise: pooled
+    values, argmax codes (ties included: bf16-rounded inputs repeat) and the input gradient.
+    N = 40000 runs two grid-stride iterations at the 16384-block cap."""
+    torch.manual_seed(N)
+    r, bias, alpha, beta = 4, 1.0, 0.001 / 9.0, 0.75
+    x = (torch.randn(N, 14, 14, 64, device=dev) * 2).relu().to(torch.bfloat16)
+    x[:, ::3, ::2, 5] = x[:, ::3, ::2, 7]      # repeated values: ties inside pool windows
+    x[0, :2, :2, :] = 0                        # an all-zero window
+    dP = (torch.randn(N, 7, 7, 64, device=dev)).to(torch.bfloat16)
+    outs = []
+    for packed in (False, True):
+        K.lrn_set_packed(packed)
+        try:
+            y = torch.full((N, 7, 7, 64), 3.0, dtype=torch.bfloat16, device=dev)
+            arg = torch.full((N, 7, 7, 64), 9, dtype=torch.uint8, device=dev)
+            K.lrn_pool_fwd(x, y, arg, N, 14, 14, 64, r, bias, alpha, beta, nonneg=True)
+            dx = torch.full_like(x, 5.0)
+            K.lrn_pool_bwd(x, dP, arg, dx, N, 14, 14, 64, r, bias, alpha, beta, True)
+            torch.cuda.synchronize()
+            outs.append((y, arg, dx))
+        finally:
+            K.lrn_set_packed(True)
+    for a, b, name in zip(outs[0], outs[1], ("pooled", "argmax", "dx")):
+        assert torch.equal(a, b), name
+    assert int(outs[1][1].max()) <= 3
 
 
 @pytest.mark.parametrize("src", ["bf16_idx", "u8_idx"])

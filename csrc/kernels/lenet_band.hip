@@ -675,34 +675,27 @@ DEV void refc1_unit_out(const uint32_t (&P)[4][2], const uint32_t (&CW)[4], int 
       const uint32_t w = b[i >> 1];
       return (i & 1) ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(w << 16);
     };
+    // the two vectors as the halves of packed (v_pk) values: bitwise the scalar lrn_out path
+    f2 v[8], e16[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[i] = f2{val(Bk[0], i), val(Bk[2], i)};
+      v[4 + i] = f2{val(Bk[1], i), val(Bk[3], i)};
+      const f2 lv = f2{val(lw, i), val(Bk[1], i)}, rv = f2{val(Bk[2], i), val(rw, i)};
+      e16[i] = lv * lv;
+      e16[12 + i] = rv * rv;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e16[4 + i] = v[i] * v[i];
+    f2 s[8];
+    window_sums_e<4>(e16, s);   // (never contracted with the squares: lrn_math.h)
     uint32_t nv[2][4];
 #pragma unroll
-    for (int vec = 0; vec < 2; ++vec) {
-      const uint32_t(&L)[2] = vec ? Bk[1] : lw;
-      const uint32_t(&M0)[2] = vec ? Bk[2] : Bk[0];
-      const uint32_t(&M1)[2] = vec ? Bk[3] : Bk[1];
-      const uint32_t(&R)[2] = vec ? rw : Bk[2];
-      float v[8], e16[16];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        v[i] = val(M0, i);
-        v[4 + i] = val(M1, i);
-        const float lv = val(L, i), rv = val(R, i);
-        e16[i] = lv * lv;
-        e16[12 + i] = rv * rv;
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) e16[4 + i] = v[i] * v[i];
-      // materialised squares: no fma contraction into the window sum (lrn_fwd_k rounds
-      // each square on its own)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(e16[i]));
-      float s[8];
-      window_sums_e<4>(e16, s);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        nv[vec][i] = pack2(lrn_out(v[2 * i], s[2 * i], l.bias, l.alpha, l.beta),
-                           lrn_out(v[2 * i + 1], s[2 * i + 1], l.bias, l.alpha, l.beta));
+    for (int i = 0; i < 4; ++i) {
+      const f2 y0 = lrn_out2(v[2 * i], s[2 * i], l.bias, l.alpha, l.beta);
+      const f2 y1 = lrn_out2(v[2 * i + 1], s[2 * i + 1], l.bias, l.alpha, l.beta);
+      nv[0][i] = pack2(y0.x, y1.x);
+      nv[1][i] = pack2(y0.y, y1.y);
     }
     if (st) {
       *(u32x4*)(l.norm + e) = u32x4{nv[0][0], nv[0][1], nv[0][2], nv[0][3]};

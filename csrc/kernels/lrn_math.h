@@ -214,5 +214,23 @@ DEV void lrn_bwd2_b075(const f2 (&v)[8], const f2 (&g)[8], int c8, float bias, f
   }
 }
 
+// lrn_bwd8<G, R, true> of two independent 8-channel vectors (same lane layout) at once
+template <int G, int R>
+DEV void lrn_bwd8x2_b075(const u32x4& x0, const u32x4& g0, const u32x4& x1, const u32x4& g1, int c8, float bias,
+                         float alpha, float beta, int relu_mask, u32x4& o0, u32x4& o1) {
+  f2 v[8], g[8], o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    v[j] = f2{u4_get(x0, j), u4_get(x1, j)};
+    g[j] = f2{u4_get(g0, j), u4_get(g1, j)};
+  }
+  lrn_bwd2_b075<G, R>(v, g, c8, bias, alpha, beta, relu_mask, o);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o0[j] = pack2(o[2 * j].x, o[2 * j + 1].x);
+    o1[j] = pack2(o[2 * j].y, o[2 * j + 1].y);
+  }
+}
+
 }  // namespace
 }  // namespace mnistx

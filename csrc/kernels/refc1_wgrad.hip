@@ -202,18 +202,43 @@ struct Stage {
     store_x(buf, t);
     load_x(g, t_next, t);
     const Rsrc r = rsrc(g, t_next);
+    // rounds in pairs: the LRN backward of rounds u and u + 1 as one packed (v_pk) computation
+    // (bitwise lrn_bwd8; the last round's lanes past the partial round compute on whatever
+    // their registers hold and store nothing -- whole DPP rows either way)
+    // (CIN 3: one round at a time -- the pairs' registers spilled beside the 3 input planes)
+    static_assert(PER % 2 == 0, "round pairs");
+    if constexpr (CIN == 3) {
 #pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      if (u < PER - 1 || t < NTASK - (PER - 1) * NPT) {   // whole DPP rows (lrn_bwd8's exchanges)
-        const u32x4 d = (g.skip & 2) ? y[u] : lrn_bwd8<4, 4, true>(p[u], y[u], t & 3, g.bias, g.alpha, g.beta, 0);
-        const uint32_t a0 = a[u][0], a1 = a[u][1];
-        if (off[u] >= 0) {
-          *(u32x4*)(buf + L::DP1_OFF + off[u]) = d;
-          *(u32x4*)(buf + L::CD_OFF + off[u]) = u32x4{bytes01(a0), bytes23(a0), bytes01(a1), bytes23(a1)};
+      for (int u = 0; u < PER; ++u) {
+        if (u < PER - 1 || t < NTASK - (PER - 1) * NPT) {   // whole DPP rows (lrn_bwd8's exchanges)
+          const u32x4 d = (g.skip & 2) ? y[u] : lrn_bwd8<4, 4, true>(p[u], y[u], t & 3, g.bias, g.alpha, g.beta, 0);
+          const uint32_t a0 = a[u][0], a1 = a[u][1];
+          if (off[u] >= 0) {
+            *(u32x4*)(buf + L::DP1_OFF + off[u]) = d;
+            *(u32x4*)(buf + L::CD_OFF + off[u]) = u32x4{bytes01(a0), bytes23(a0), bytes01(a1), bytes23(a1)};
+          }
         }
+        load_u(r, u, t);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      load_u(r, u, t);
-      __builtin_amdgcn_sched_barrier(0);
+      return;
+    }
+#pragma unroll
+    for (int u = 0; u < PER; u += 2) {
+      u32x4 d0 = y[u], d1 = y[u + 1];
+      if (!(g.skip & 2))
+        lrn_bwd8x2_b075<4, 4>(p[u], y[u], p[u + 1], y[u + 1], t & 3, g.bias, g.alpha, g.beta, 0, d0, d1);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int uu = u + h;
+        const uint32_t a0 = a[uu][0], a1 = a[uu][1];
+        if ((uu < PER - 1 || t < NTASK - (PER - 1) * NPT) && off[uu] >= 0) {
+          *(u32x4*)(buf + L::DP1_OFF + off[uu]) = h ? d1 : d0;
+          *(u32x4*)(buf + L::CD_OFF + off[uu]) = u32x4{bytes01(a0), bytes23(a0), bytes01(a1), bytes23(a1)};
+        }
+        load_u(r, uu, t);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
   }
 };

@@ -637,8 +637,10 @@ DEV void refc1_pool_q(const f32x16& acc, const float (&bias)[4], uint32_t (&P)[2
 
 // A unit's pooled pixel: lane half h holds channels 8 q + 4 h + i (P[q], CW[q]).  Transposes to
 // channels 16 h .. 16 h + 15 per lane, stores pool1 / codes at element e (if st) and, with LRN,
-// norm1 from the lane's own blocks (see refc1n_fwd_k).
-template <bool LRN>
+// norm1 from the lane's own blocks (see refc1n_fwd_k).  PK: the two LRN vectors as packed
+// (v_pk) halves -- refc1n_fwd_k; refc1n3_fwd_k keeps the scalar form (at 198 VGPRs with its
+// A ring, the packed one spilled: 164 -> 207 us, profiles/r6/refc1pk/)
+template <bool LRN, bool PK = true>
 DEV void refc1_unit_out(const uint32_t (&P)[4][2], const uint32_t (&CW)[4], int h, int64_t e, bool st,
                         const BandFwd& a, const RefC1Lrn& l) {
   // lane half h: 4-channel blocks Bk = channels 16 h + 4 k .. + 3 (swap(P[k], P[k + 2]): lanes
@@ -675,27 +677,57 @@ DEV void refc1_unit_out(const uint32_t (&P)[4][2], const uint32_t (&CW)[4], int 
       const uint32_t w = b[i >> 1];
       return (i & 1) ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(w << 16);
     };
-    // the two vectors as the halves of packed (v_pk) values: bitwise the scalar lrn_out path
-    f2 v[8], e16[16];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      v[i] = f2{val(Bk[0], i), val(Bk[2], i)};
-      v[4 + i] = f2{val(Bk[1], i), val(Bk[3], i)};
-      const f2 lv = f2{val(lw, i), val(Bk[1], i)}, rv = f2{val(Bk[2], i), val(rw, i)};
-      e16[i] = lv * lv;
-      e16[12 + i] = rv * rv;
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) e16[4 + i] = v[i] * v[i];
-    f2 s[8];
-    window_sums_e<4>(e16, s);   // (never contracted with the squares: lrn_math.h)
     uint32_t nv[2][4];
+    if constexpr (PK) {
+      // the two vectors as the halves of packed (v_pk) values: bitwise the scalar lrn_out path
+      f2 v[8], e16[16];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const f2 y0 = lrn_out2(v[2 * i], s[2 * i], l.bias, l.alpha, l.beta);
-      const f2 y1 = lrn_out2(v[2 * i + 1], s[2 * i + 1], l.bias, l.alpha, l.beta);
-      nv[0][i] = pack2(y0.x, y1.x);
-      nv[1][i] = pack2(y0.y, y1.y);
+      for (int i = 0; i < 4; ++i) {
+        v[i] = f2{val(Bk[0], i), val(Bk[2], i)};
+        v[4 + i] = f2{val(Bk[1], i), val(Bk[3], i)};
+        const f2 lv = f2{val(lw, i), val(Bk[1], i)}, rv = f2{val(Bk[2], i), val(rw, i)};
+        e16[i] = lv * lv;
+        e16[12 + i] = rv * rv;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) e16[4 + i] = v[i] * v[i];
+      f2 s[8];
+      window_sums_e<4>(e16, s);   // (never contracted with the squares: lrn_math.h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f2 y0 = lrn_out2(v[2 * i], s[2 * i], l.bias, l.alpha, l.beta);
+        const f2 y1 = lrn_out2(v[2 * i + 1], s[2 * i + 1], l.bias, l.alpha, l.beta);
+        nv[0][i] = pack2(y0.x, y1.x);
+        nv[1][i] = pack2(y0.y, y1.y);
+      }
+    } else {
+#pragma unroll
+      for (int vec = 0; vec < 2; ++vec) {
+        const uint32_t(&L)[2] = vec ? Bk[1] : lw;
+        const uint32_t(&M0)[2] = vec ? Bk[2] : Bk[0];
+        const uint32_t(&M1)[2] = vec ? Bk[3] : Bk[1];
+        const uint32_t(&R)[2] = vec ? rw : Bk[2];
+        float v[8], e16[16];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = val(M0, i);
+          v[4 + i] = val(M1, i);
+          const float lv = val(L, i), rv = val(R, i);
+          e16[i] = lv * lv;
+          e16[12 + i] = rv * rv;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e16[4 + i] = v[i] * v[i];
+        // materialised squares (the round-6 form: this scheduling keeps refc1n3 at 198 VGPRs)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(e16[i]));
+        float s[8];
+        window_sums_e<4>(e16, s);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          nv[vec][i] = pack2(lrn_out(v[2 * i], s[2 * i], l.bias, l.alpha, l.beta),
+                             lrn_out(v[2 * i + 1], s[2 * i + 1], l.bias, l.alpha, l.beta));
+      }
     }
     if (st) {
       *(u32x4*)(l.norm + e) = u32x4{nv[0][0], nv[0][1], nv[0][2], nv[0][3]};
@@ -948,7 +980,7 @@ __global__ __launch_bounds__(R3TH, 1) void refc1n3_fwd_k(const BandFwd a, const 
       const int f = wave + R3NW * j, yp0 = f / 7, u = f - 7 * yp0;
       const bool st = gi < a.B;
       const int64_t e = ((int64_t)(st ? gi : 0) * 196 + (yp0 + 7 * half) * 14 + 2 * u + xq) * 32 + 16 * h;
-      refc1_unit_out<LRN>(P, CW, h, e, st, a, l);
+      refc1_unit_out<LRN, false>(P, CW, h, e, st, a, l);
     }
     if (k + 1 < nk) xstore(xs + ((k + 1) & 1) * XBUF3);
   }

@@ -42,6 +42,8 @@
 #include "lrn_math.h"
 #include "wgrad_tr.h"
 
+#include <cstdlib>
+
 namespace mnistx {
 namespace {
 
@@ -82,7 +84,7 @@ struct Args {
 };
 
 // producer registers of one tile: LRN task vectors (dL/d norm1, pool1, codes) and the input
-template <bool U8, bool IDX, int CIN>
+template <bool U8, bool IDX, int CIN, bool PK3 = false>
 struct Stage {
   using L = Lay<CIN>;
   u32x4 y[PER], p[PER];
@@ -205,9 +207,9 @@ struct Stage {
     // rounds in pairs: the LRN backward of rounds u and u + 1 as one packed (v_pk) computation
     // (bitwise lrn_bwd8; the last round's lanes past the partial round compute on whatever
     // their registers hold and store nothing -- whole DPP rows either way)
-    // (CIN 3: one round at a time -- the pairs' registers spilled beside the 3 input planes)
+    // (CIN 3 without PK3: one round at a time -- the pairs spill 20 bytes beside the 3 input planes)
     static_assert(PER % 2 == 0, "round pairs");
-    if constexpr (CIN == 3) {
+    if constexpr (CIN == 3 && !PK3) {
 #pragma unroll
       for (int u = 0; u < PER; ++u) {
         if (u < PER - 1 || t < NTASK - (PER - 1) * NPT) {   // whole DPP rows (lrn_bwd8's exchanges)
@@ -283,7 +285,7 @@ DEV void gemm_tile(const uint8_t* buf, int w, f32x4 (&acc)[CIN][3][2], f32x4 (&a
   }
 }
 
-template <bool U8, bool IDX, int CIN = 1>
+template <bool U8, bool IDX, int CIN = 1, bool PK3 = false>
 __global__ __launch_bounds__(NT, 1) void refc1_wgrad_k(const Args g) {
   using L = Lay<CIN>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -302,10 +304,10 @@ __global__ __launch_bounds__(NT, 1) void refc1_wgrad_k(const Args g) {
 
   if (wave < NPW) {
     // ======================================================== producers: LRN backward staging
-    Stage<U8, IDX, CIN> st;
+    Stage<U8, IDX, CIN, PK3> st;
     int off[PER];
 #pragma unroll
-    for (int u = 0; u < PER; ++u) off[u] = Stage<U8, IDX, CIN>::task_off(tid, u);
+    for (int u = 0; u < PER; ++u) off[u] = Stage<U8, IDX, CIN, PK3>::task_off(tid, u);
     st.load_row(g, tile0(0), tid);
     st.load(g, tile0(0), tid);
     st.load_row(g, tile0(1), tid);
@@ -371,8 +373,12 @@ __global__ __launch_bounds__(NT, 1) void refc1_wgrad_k(const Args g) {
 using Kern = void (*)(Args);
 constexpr Kern kRefc1[4] = {refc1_wgrad_k<false, false>, refc1_wgrad_k<false, true>, refc1_wgrad_k<true, false>,
                             refc1_wgrad_k<true, true>};
-// 3 channels: bf16 NHWC, the batch (x0) or the resident dataset through the batch index
-constexpr Kern kRefc1x3[2] = {refc1_wgrad_k<false, false, 3>, refc1_wgrad_k<false, true, 3>};
+// 3 channels: bf16 NHWC, the batch (x0) or the resident dataset through the batch index;
+// [packed LRN pairs][idx].  The pairs spill 20 bytes at the 128-VGPR cap and still win: 190.4 vs
+// 197.4 us at B = 16384 (profiles/r6/refc1pk/wg3/; MNISTX_REFC1_PK3=0: one round at a time)
+constexpr Kern kRefc1x3[2][2] = {{refc1_wgrad_k<false, false, 3>, refc1_wgrad_k<false, true, 3>},
+                                 {refc1_wgrad_k<false, false, 3, true>, refc1_wgrad_k<false, true, 3, true>}};
+static int g_pk3 = [] { const char* e = getenv("MNISTX_REFC1_PK3"); return (e && e[0] == '0') ? 0 : 1; }();
 
 int g_skip = 0;
 
@@ -388,12 +394,13 @@ int refc1_wgrad_grid(int* per_cu = nullptr) {
       if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, Lay<1>::LDS_BYTES) !=
           hipSuccess)
         return -1;
-    for (Kern k : kRefc1x3)
-      if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, Lay<3>::LDS_BYTES) !=
-        hipSuccess)
-      return -1;
+    for (const auto& ks : kRefc1x3)
+      for (Kern k : ks)
+        if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, Lay<3>::LDS_BYTES) !=
+            hipSuccess)
+          return -1;
     // both channel counts hold one block per CU (LDS); the grid is the same
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kRefc1x3[0], NT, Lay<3>::LDS_BYTES) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kRefc1x3[0][0], NT, Lay<3>::LDS_BYTES) != hipSuccess ||
         hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per <= 0)
       return -1;
@@ -419,7 +426,7 @@ hipError_t refc1_wgrad(const XSrc& x, const bf16_t* dn, const bf16_t* p1, const 
   if (beta != 0.75f) return hipErrorInvalidValue;   // the lrn_bwd8 fast path (the reference's beta)
   if (cin != 1 && !(cin == 3 && x.x && !x.u8)) return hipErrorInvalidValue;
   Args a{x.u8 ? nullptr : x.x, x.u8, x.idx, x.idx ? x.n : B, dn, p1, arg, B, bias, alpha, beta, slab, g_skip};
-  const Kern k = cin == 3 ? kRefc1x3[x.idx ? 1 : 0] : kRefc1[(x.u8 ? 2 : 0) + (x.idx ? 1 : 0)];
+  const Kern k = cin == 3 ? kRefc1x3[g_pk3][x.idx ? 1 : 0] : kRefc1[(x.u8 ? 2 : 0) + (x.idx ? 1 : 0)];
   void* args[] = {&a};
   return hipLaunchKernel((const void*)k, dim3(grid), dim3(NT), args, cin == 3 ? Lay<3>::LDS_BYTES : Lay<1>::LDS_BYTES,
                          st);

@@ -35,10 +35,12 @@ TARGET_BLOCKS = 2048
 # Round 3, with the head weight gradients grouped on 64x128 tiles: 256 (~1 per CU)
 # beat 512 in 5 of 5 same-box pairs, LeNet-5 0.5255 vs 0.5291 ms/step on average
 # (128: 0.5293, 384: 0.5260, 768: 0.5342, 1024: 0.5402; profiles/r3/lenet/wgrad_blocks/).
-# Round 6 (head weight gradients in one grouped launch, 3 problems): 192 -- kernel tables on one
-# box: gemm_wg_group 34.2 -> 31.8 us, split-K reduce 8.4 -> 7.8 us; step pairs on very noisy
-# boxes 7 of 11 for 192 (profiles/r6/lenet_wgb/)
-TARGET_BLOCKS_FEW_TILES = int(os.environ.get("MNISTX_WGRAD_BLOCKS", "192"))
+TARGET_BLOCKS_FEW_TILES = int(os.environ.get("MNISTX_WGRAD_BLOCKS", "256"))
+# Round 6, the grouped head weight gradients (LeNet fc3 / fc4 / fc5 in one launch): 192 --
+# kernel tables on one box: gemm_wg_group 34.2 -> 31.8 us, split-K reduce 8.4 -> 7.8 us; step
+# pairs on very noisy boxes 7 of 11 for 192.  The standalone few-tile ones (reference local4)
+# stay at 256: 1.8388 vs 1.8406 ms at 192, 3 pairs (profiles/r6/lenet_wgb/)
+TARGET_BLOCKS_GROUPED = int(os.environ.get("MNISTX_WGRAD_BLOCKS_GROUPED", "192"))
 # 128x128-tile dense weight gradients (reference local3): ~2 splits (bench/micro_wgrad.py
 # ref: S=2 155.9 us, S=3 165.0, S=8 154.4, S=16 197.1 -- the fewest splits that fill
 # the GPU keep the slab smallest; round 3, whole reference-CNN step: 256 / 400 / 600 / 800
@@ -90,7 +92,8 @@ def pick_splits(M: int, N: int, K: int, target: Optional[int] = None, min_k: int
         if dense and (bm, bn) == (128, 128):
             target = TARGET_BLOCKS_BIG_TILES
         else:
-            target = TARGET_BLOCKS_FEW_TILES if (dense and tiles < 64) else TARGET_BLOCKS
+            target = (TARGET_BLOCKS_GROUPED if grouped else TARGET_BLOCKS_FEW_TILES) if (dense and tiles < 64) \
+                else TARGET_BLOCKS
     s = max(1, math.ceil(target / tiles))
     s = min(s, max(1, K // min_k), max(1, SLAB_CAP // max(1, M * N)))
     return eff_splits(K, s)
